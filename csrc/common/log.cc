@@ -1,0 +1,122 @@
+// Logger implementation: threshold, sink, optional per-role log file.
+#include "uda/log.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <mutex>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include "uda/compare.h"
+#include "uda/error.h"
+
+namespace uda {
+
+namespace {
+std::atomic<int> g_threshold{kInfo};
+std::mutex g_mu;
+LogSink g_sink = nullptr;
+void* g_sink_ctx = nullptr;
+FILE* g_file = nullptr;
+
+const char* sev_name(int s) {
+  static const char* names[] = {"NONE", "FATAL", "ERROR", "WARN", "INFO", "DEBUG", "TRACE"};
+  return (s >= 0 && s <= 6) ? names[s] : "?";
+}
+}  // namespace
+
+void log_set_threshold(int s) { g_threshold.store(s < 0 ? 0 : (s > kTrace ? kTrace : s)); }
+int log_threshold() { return g_threshold.load(std::memory_order_relaxed); }
+
+void log_set_sink(LogSink sink, void* ctx) {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_sink = sink;
+  g_sink_ctx = ctx;
+}
+
+bool log_open_file(const std::string& dir, const std::string& role) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_file) fclose(g_file);
+  std::string path = (dir.empty() ? std::string(".") : dir) + "/uda" + role + ".log";
+  g_file = fopen(path.c_str(), "a");
+  return g_file != nullptr;
+}
+
+void log_close_file() {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_file) fclose(g_file);
+  g_file = nullptr;
+}
+
+void log_write(int sev, const char* file, int line, const char* func, const char* fmt, ...) {
+  char body[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(body, sizeof(body), fmt, ap);
+  va_end(ap);
+  const char* base = strrchr(file, '/');
+  base = base ? base + 1 : file;
+  char msg[2400];
+  snprintf(msg, sizeof(msg), "%s:%d %s() %s", base, line, func, body);
+
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_file) {
+    struct timeval tv;
+    gettimeofday(&tv, nullptr);
+    struct tm tmv;
+    localtime_r(&tv.tv_sec, &tmv);
+    char ts[64];
+    strftime(ts, sizeof(ts), "%Y-%m-%d %H:%M:%S", &tmv);
+    fprintf(g_file, "%s.%03d %-5s [tid %d] %s\n", ts, (int)(tv.tv_usec / 1000), sev_name(sev),
+            (int)gettid(), msg);
+    fflush(g_file);
+    return;
+  }
+  if (g_sink) {
+    g_sink(g_sink_ctx, msg, sev);
+    return;
+  }
+  fprintf(stderr, "[uda %s] %s\n", sev_name(sev), msg);
+}
+
+bool FailureLatch::report(const std::string& why) {
+  count_.fetch_add(1);
+  bool expected = false;
+  if (!failed_.compare_exchange_strong(expected, true)) return false;
+  reason_ = why;
+  UDA_LOG(kError, "failure reported: %s", why.c_str());
+  if (hook_) hook_(why);
+  return true;
+}
+
+KeyKind key_kind_from_class(const char* n) {
+  static const char* text[] = {"org.apache.hadoop.io.Text", nullptr};
+  static const char* raw[] = {"org.apache.hadoop.io.BooleanWritable", "org.apache.hadoop.io.ByteWritable",
+                              "org.apache.hadoop.io.ShortWritable", "org.apache.hadoop.io.IntWritable",
+                              "org.apache.hadoop.io.LongWritable", nullptr};
+  static const char* bytes[] = {"org.apache.hadoop.io.BytesWritable",
+                                "org.apache.hadoop.hbase.io.ImmutableBytesWritable", nullptr};
+  auto in = [n](const char** arr) {
+    for (; *arr; ++arr)
+      if (strcmp(n, *arr) == 0) return true;
+    return false;
+  };
+  if (!n) return KeyKind::kUnsupported;
+  if (in(text)) return KeyKind::kText;
+  if (in(raw)) return KeyKind::kRaw;
+  if (in(bytes)) return KeyKind::kBytes;
+  return KeyKind::kUnsupported;
+}
+
+const char* key_kind_name(KeyKind k) {
+  switch (k) {
+    case KeyKind::kText: return "text";
+    case KeyKind::kRaw: return "raw";
+    case KeyKind::kBytes: return "bytes";
+    default: return "unsupported";
+  }
+}
+
+}  // namespace uda

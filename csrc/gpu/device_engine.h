@@ -1,0 +1,270 @@
+// Device-side shuffle + merge engine: the MI355X data path behind the Merger/MOFSupplier roles.
+//
+// Reference roles replaced:
+//   * MOFSupplier DataEngine (src/MOFServer/IndexInfo.cc:141-376) reading MOF chunks from disk with
+//     libaio and RDMA-writing them to reducers  ->  map-output partitions resident in HBM
+//     (`PartitionStore`), shipped by an RCCL all-to-all over xGMI in key-range rounds.
+//   * NetMerger MergeManager online merge (src/Merger/MergeManager.cc:47-193) with a CPU heap
+//     k-way merge  ->  `DeviceMerger` (F2 keys, F3 merge-path tree, F4 gather) per round.
+//   * merge_do_merging_phase -> dataFromUda (src/Merger/MergeManager.cc:155-182): merged records are
+//     streamed D2H into a pinned-host ring on a copy stream and handed to the host sink in
+//     <= kv_buf_size buffers of whole records, the last one ending with the IFile EOF marker.
+//
+// Pipeline per step (one process per GPU, W ranks):
+//   comm stream    : [a2a round q+1] .......
+//   compute stream : [extract+merge+gather round q] ....
+//   copy stream    : [D2H pieces of round q-1] ..........  -> deliver thread -> sink
+// Round q of reducer d holds the keys in [bound(d,q), bound(d,q+1)); bounds come from a key sample
+// taken when the job is planned (the TeraSort range-partition sampler's role).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels.h"
+
+typedef struct ncclComm* ncclComm_t;
+
+namespace uda {
+namespace gpu {
+
+void hip_check(hipError_t e, const char* what, const char* file, int line);
+#define HIP_CHECK(x) ::uda::gpu::hip_check((x), #x, __FILE__, __LINE__)
+
+// Owning device allocation.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t bytes) { alloc(bytes); }
+  ~DeviceBuffer();
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  DeviceBuffer(DeviceBuffer&& o) noexcept : ptr_(o.ptr_), size_(o.size_) {
+    o.ptr_ = nullptr;
+    o.size_ = 0;
+  }
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+    if (this != &o) {
+      reset();
+      ptr_ = o.ptr_;
+      size_ = o.size_;
+      o.ptr_ = nullptr;
+      o.size_ = 0;
+    }
+    return *this;
+  }
+  void alloc(size_t bytes);
+  void reset();
+  template <typename T = uint8_t>
+  T* as() const {
+    return reinterpret_cast<T*>(ptr_);
+  }
+  size_t size() const { return size_; }
+
+ private:
+  void* ptr_ = nullptr;
+  size_t size_ = 0;
+};
+
+// Owning pinned host allocation (hipHostMalloc).
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  ~PinnedBuffer();
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  PinnedBuffer(PinnedBuffer&& o) noexcept : ptr_(o.ptr_), size_(o.size_) {
+    o.ptr_ = nullptr;
+    o.size_ = 0;
+  }
+  void alloc(size_t bytes);
+  template <typename T = uint8_t>
+  T* as() const {
+    return reinterpret_cast<T*>(ptr_);
+  }
+  size_t size() const { return size_; }
+
+ private:
+  void* ptr_ = nullptr;
+  size_t size_ = 0;
+};
+
+// Merges K sorted FIXED10 runs on one stream. Enqueue-only: never synchronizes the host except
+// when a plan slot is reused before its previous upload finished.
+class DeviceMerger {
+ public:
+  DeviceMerger(int64_t max_records, int max_runs);
+  ~DeviceMerger();
+  // Merge `runs` (device-resident) into `out` (n*104 bytes). Returns the record count.
+  int64_t merge_fixed(const std::vector<RunDesc>& runs, uint8_t* out, hipStream_t s);
+  // Number of merge-tree passes used by the last call.
+  int last_passes() const { return last_passes_; }
+  bool bad_layout();  // synchronizes; true if any record was not TeraSort-shaped
+  int64_t max_records() const { return max_records_; }
+
+ private:
+  struct Slot {
+    PinnedBuffer host;
+    DeviceBuffer dev;
+    hipEvent_t uploaded = nullptr;
+    bool used = false;
+  };
+  int64_t max_records_;
+  int max_runs_;
+  DeviceBuffer elems_a_, elems_b_, splits_;
+  DeviceBuffer flag_;
+  std::vector<Slot> slots_;
+  int next_slot_ = 0;
+  int last_passes_ = 0;
+  size_t slot_bytes_ = 0;
+};
+
+// Delivery sink: called from the deliver thread with whole-record buffers (<= kv_buf_size).
+// Return nonzero to abort the step.
+using SinkFn = std::function<int(const uint8_t* buf, int64_t len)>;
+
+struct ShuffleConfig {
+  int device = 0;
+  int rank = 0;
+  int world = 1;
+  int maps_per_rank = 32;
+  int64_t records_per_map = 1 << 20;
+  int rounds = 8;
+  uint64_t seed = 0x5eed;
+  int64_t kv_buf_bytes = 1 << 20;        // delivery buffer size (J2CQueue kv_buf_size)
+  int64_t d2h_piece_bytes = 64ll << 20;  // D2H granule (rounded down to whole buffers)
+  int pinned_slots = 6;
+  int d2h_streams = 1;                   // split each piece over this many copy streams
+  bool deliver_host = true;              // false: stop after the device merge (ablation)
+  bool validate = false;                 // device-side order + checksum check per round
+};
+
+struct StepStats {
+  double wall_ms = 0;          // host wall time of the whole step
+  double split_ms = 0;         // round split + counts exchange (host wall)
+  double comm_ms = 0;          // sum of per-round all-to-all time (device events)
+  double merge_ms = 0;         // sum of per-round merge time (device events)
+  double d2h_ms = 0;           // copy-stream busy time (device events, summed over pieces)
+  int64_t bytes_in = 0;        // partition bytes delivered to this reducer (records only)
+  int64_t records = 0;
+  int64_t bytes_sent = 0;      // bytes this rank sent to peers (excl. self)
+  int64_t buffers = 0;         // sink invocations
+  int merge_passes = 0;
+  int64_t order_errors = -1;   // validate only
+  uint64_t checksum = 0;       // validate only: sum of record hashes seen by the device
+  bool bad_layout = false;
+};
+
+class ShuffleJob {
+ public:
+  explicit ShuffleJob(const ShuffleConfig& cfg);
+  ~ShuffleJob();
+
+  const ShuffleConfig& config() const { return cfg_; }
+  // RCCL bootstrap; `uid` is the ncclUniqueId produced by rank 0 (nccl_unique_id()).
+  void init_comm(const std::string& uid);
+  // Map phase stand-in: generate maps_per_rank TeraSort MOFs into the HBM partition store.
+  void generate();
+  // Every `every`-th key of every local run, grouped by destination reducer:
+  // result[d] = flat (hi, lo) pairs.
+  std::vector<std::vector<uint64_t>> sample_keys(int64_t every);
+  // bounds: world x (rounds-1) x 2 u64 (hi, lo16<<48), ascending per destination.
+  void set_bounds(const std::vector<uint64_t>& bounds);
+  // Compute exact per-round volumes and allocate the round buffers. Collective when world > 1.
+  void plan();
+  void set_sink(SinkFn sink) { sink_ = std::move(sink); }
+  // One shuffle+merge+deliver pass over the whole dataset. Collective when world > 1.
+  StepStats run_step();
+
+  // Per-destination checksum of locally generated records (sum of record_hash).
+  std::vector<uint64_t> local_dest_checksums() const { return dest_checksum_; }
+  std::vector<int64_t> local_dest_records() const { return dest_records_; }
+  int64_t store_bytes() const { return store_bytes_; }
+  int64_t max_round_records() const { return max_round_records_; }
+  // Index record of (local map m, reducer d): offset, rawLength, partLength within MOF m.
+  std::vector<int64_t> index_record(int m, int d) const;
+  // Copy a MOF partition (records + EOF) to host (tests / provider fallback path).
+  std::vector<uint8_t> read_partition(int m, int d) const;
+
+ private:
+  struct RoundPlan {
+    // send side: per (dest p, local map m): record range [beg, end) in run (m, p)
+    std::vector<int64_t> send_beg, send_end;  // index p*M + m
+    // recv side: per (src s, map j of s): record count
+    std::vector<int64_t> recv_cnt;  // index s*M + j
+    int64_t recv_records = 0;
+  };
+  void compute_round_plans(std::vector<RoundPlan>* plans, double* ms);
+  void deliver_loop();
+  void copy_loop();
+  uint8_t* run_base(int m, int d) const { return store_.as<uint8_t>() + run_off_[m * cfg_.world + d]; }
+
+  ShuffleConfig cfg_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t s_comm_ = nullptr, s_compute_ = nullptr;
+  std::vector<hipStream_t> s_copy_;
+  DeviceBuffer store_;
+  int64_t store_bytes_ = 0;
+  std::vector<int64_t> mof_off_, run_off_, run_nrec_;  // run index m*W + d
+  std::vector<uint64_t> dest_checksum_;
+  std::vector<int64_t> dest_records_;
+  std::vector<uint64_t> bounds_;  // W x (Q-1) x 2
+  DeviceBuffer d_bounds_, d_run_bases_, d_run_nrec_, d_bound_set_, d_split_out_;
+  std::vector<RoundPlan> plans_;
+  int64_t max_round_records_ = 0;
+  std::vector<DeviceBuffer> recv_slots_, out_slots_;
+  std::unique_ptr<DeviceMerger> merger_;
+  DeviceBuffer d_counts_send_, d_counts_recv_;
+  DeviceBuffer d_validate_;  // stats[2] + prev key + last key
+  PinnedBuffer pinned_;
+  int64_t piece_bytes_ = 0;
+  int64_t buf_records_ = 0;
+
+  // host pipeline state
+  struct Piece {
+    int slot;
+    int64_t bytes;
+    bool last;
+    hipEvent_t done;
+  };
+  struct RoundOut {
+    int q;
+    int out_slot;
+    int64_t records;
+    hipEvent_t merged;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<RoundOut> round_q_;
+  std::deque<Piece> piece_q_;
+  std::vector<bool> pinned_free_;
+  std::vector<hipEvent_t> piece_events_;
+  std::vector<hipEvent_t> out_free_ev_;   // recorded on copy stream after a round's D2H
+  std::vector<int> d2h_enqueued_;         // per round: 1 once its D2H is enqueued
+  std::thread copy_thr_, deliver_thr_;
+  bool stop_ = false;
+  bool step_done_ = false;
+  int64_t step_buffers_ = 0;
+  int step_error_ = 0;
+  double step_d2h_ms_ = 0;
+  std::vector<hipEvent_t> piece_start_ev_;
+  std::vector<hipEvent_t> join_ev_;
+  SinkFn sink_;
+  PinnedBuffer eof_buf_;
+};
+
+// ncclUniqueId as bytes (rank 0 creates, others receive it out of band).
+std::string nccl_unique_id();
+int device_count();
+
+}  // namespace gpu
+}  // namespace uda

@@ -1,0 +1,128 @@
+// Host-callable launchers for the gfx950 HIP kernels of the shuffle/merge data path.
+//
+// Every launcher takes raw device pointers and a hipStream_t and never allocates or synchronizes,
+// so a sequence of launches can be enqueued from one host thread (or captured into a hipGraph).
+//
+// Map to the reference's CPU hot loops:
+//   F1 record index        -> index_records_serial / verify_fixed_stride
+//   F2 key normalization   -> extract_keys_fixed / extract_keys_generic (+ __device__ compare)
+//   F3 k-way merge         -> merge_partition + merge_pass (pairwise merge-path tree on keys)
+//   F4 serialize / gather  -> gather_fixed / gather_var + buffer cut points
+//   F6 block decompress    -> snappy_decompress_blocks / lzo1x_decompress_blocks
+// plus TeraGen-shaped synthetic map-output generation and device-side validation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace uda {
+namespace gpu {
+
+// 16-byte merge element. Ordering is lexicographic on (hi, lo).
+//   FIXED10 mode: hi = key bytes 0..7 (big-endian), lo = key bytes 8..9 << 48 | run << 32 | pos.
+//   GENERIC mode: hi = content prefix bytes 0..7, lo = global record ordinal (ties resolved
+//                 with a full-key comparison through the record index; see merge.hip).
+struct alignas(16) Elem {
+  uint64_t hi;
+  uint64_t lo;
+};
+
+// TeraSort record geometry: Text key (VInt 10 + 10 bytes) and Text value (VInt 90 + 90 bytes)
+// inside an IFile record (VInt keyLen=11, VInt valLen=91): 104 bytes, 8-byte aligned.
+constexpr int kTeraKeyBytes = 10;
+constexpr int kTeraValBytes = 90;
+constexpr int kTeraRecordBytes = 104;
+constexpr int kTeraKeyOffset = 3;  // [0x0B][0x5B][0x0A] key...
+
+// Descriptor of a sorted run (one map-output partition slice) living in device memory.
+struct RunDesc {
+  const uint8_t* base;  // first record
+  int64_t nrec;         // records in the run
+  int64_t nbytes;       // bytes (records only, no EOF marker)
+  const int64_t* offsets;  // GENERIC: record start offsets relative to base (nrec+1 entries), or null
+};
+
+// ---------------------------------------------------------------- synthetic data (TeraGen)
+// Fill `nruns` runs; run r has `nrec[r]` records written at `bases[r]` (8-byte aligned) with keys
+// whose first 8 bytes lie in [key_lo[r], key_lo[r] + key_span[r]) in ascending order (stratified
+// with random jitter, so the K runs of one reducer interleave randomly), random 2 trailing key
+// bytes and 90 printable value bytes, followed by the 2-byte EOF marker. Accumulates an
+// order-independent checksum (sum of record_hash) per run into `run_checksum[r]` (zero it first).
+void launch_teragen(uint8_t* const* bases, const int64_t* nrec, const uint64_t* key_lo,
+                    const uint64_t* key_span, const uint64_t* seeds, int nruns, int64_t max_nrec,
+                    unsigned long long* run_checksum, hipStream_t s);
+
+// ---------------------------------------------------------------- round splitting
+// For each (run r, boundary b): out[r*(nb+2) + 1 + b] = lower_bound of boundary key (hi, lo16)
+// inside run r (FIXED10 layout); out[r*(nb+2)] = 0 and out[r*(nb+2)+nb+1] = nrec[r].
+void launch_split_fixed(uint8_t* const* bases, const int64_t* nrec, const Elem* bounds,
+                        const int* run_bound_set, int nruns, int nb, int64_t* out, hipStream_t s);
+
+// Sample every `every`-th key of each FIXED10 run (starting at every/2): run r writes its samples
+// at out[sample_off[r] ...] as Elem{hi, lo16 << 48}.
+void launch_sample_fixed(uint8_t* const* bases, const int64_t* nrec, int nruns, int64_t every,
+                         const int64_t* sample_off, int64_t total, Elem* out, hipStream_t s);
+
+// ---------------------------------------------------------------- key extraction (F2)
+// Build Elem keys for all records of `nruns` FIXED10 runs; run r's elements start at
+// elem_off[r]. Sets *bad_layout to 1 if any record header is not the TeraSort layout.
+void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nruns, int64_t total,
+                          Elem* out, int* bad_layout, hipStream_t s);
+
+// ---------------------------------------------------------------- merge tree (F3)
+constexpr int kMergeTile = 2048;  // output elements per workgroup (256 threads x 8)
+// One merge pass over S sorted segments (segment k = [seg_off[k], seg_off[k+1])): segments
+// (2p, 2p+1) merge into pair p (an odd last segment is copied through). Pair p produces tiles
+// [tile_prefix[p], tile_prefix[p+1]) of kMergeTile outputs each (last tile of a pair may be short).
+struct PassDesc {
+  const int64_t* seg_off;      // S+1 entries
+  const int64_t* tile_prefix;  // P+1 entries, P = ceil(S/2)
+  int nseg;
+  int npairs;
+  int ntiles;
+};
+// splits[t] = merge-path split (elements taken from A) at the first output of tile t.
+void launch_merge_partition(const Elem* in, PassDesc pd, int64_t* splits, hipStream_t s);
+void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits, hipStream_t s);
+
+// ---------------------------------------------------------------- gather / serialize (F4)
+// out[i*104 .. +104) = record of elem[i] (FIXED10: run/pos encoded in elem.lo).
+void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases, uint8_t* out,
+                         hipStream_t s);
+
+// ---------------------------------------------------------------- validation
+// Checks key order of `n` FIXED10 records at `recs` (and against *prev_key if has_prev) and
+// accumulates an order-independent checksum. Results: stats[0] += out-of-order count,
+// stats[1] += checksum. Writes the last key to *last_key.
+void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key, int has_prev,
+                           Elem* last_key, unsigned long long* stats, hipStream_t s);
+
+// Hash used for order-independent checksums (sum of per-record hashes), host + device.
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+// record_hash over the serialized record bytes, consumed as little-endian 8-byte words (the last
+// one zero padded). Same value on host and device for any alignment.
+__host__ __device__ inline uint64_t record_hash(const uint8_t* p, int64_t len) {
+  uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)len;
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w = 0;
+    for (int b = 7; b >= 0; --b) w = (w << 8) | p[i + b];
+    h = mix64(h ^ w);
+  }
+  if (i < len) {
+    uint64_t w = 0;
+    for (int64_t b = len - 1; b >= i; --b) w = (w << 8) | p[b];
+    h = mix64(h ^ w);
+  }
+  return h;
+}
+
+}  // namespace gpu
+}  // namespace uda

@@ -1,0 +1,106 @@
+"""TeraSort shuffle+merge on MI355X — the flagship workload.
+
+Reference pipeline: every reducer fetches its partition of every map output
+file (MOF) over RDMA, merges the sorted segments with a heap, and streams the merged records to
+the Java reducer through `dataFromUda` in 1 MiB buffers.
+
+Here (one process per GPU, W GPUs):
+  * each GPU holds `maps_per_rank` TeraSort MOFs in HBM (the MOFSupplier's store),
+  * reducer d = GPU d; its partition is shipped in key-range rounds by an RCCL all-to-all,
+  * each round is merged on the GPU (F2 keys -> F3 merge tree -> F4 gather),
+  * merged records go D2H into a pinned ring and are handed to the host sink as whole-record
+    buffers of <= 1 MiB, the last one carrying the IFile EOF marker.
+Data is synthetic and TeraGen-shaped (10-byte keys, 90-byte values, 104-byte IFile records).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+
+import numpy as np
+
+from .._native import native
+from ..parallel.dist import DistContext
+from ..parallel.plan import round_bounds
+
+RECORD_BYTES = 104  # IFile record: VInt(11) VInt(91) Text(10) Text(90)
+TERAGEN_ROW_BYTES = 100
+
+
+@dataclasses.dataclass
+class TeraSortConfig:
+    rows_per_gpu: int = 1_250_000_000   # 1e10 rows (1 TB TeraGen) over 8 GPUs
+    maps_per_rank: int = 32
+    rounds: int = 16
+    seed: int = 0x5EED
+    kv_buf_bytes: int = 1 << 20         # J2CQueue kv_buf_size (UdaPlugin.java:168)
+    d2h_piece_bytes: int = 64 << 20
+    pinned_slots: int = 6
+    d2h_streams: int = 1
+    deliver_host: bool = True
+    validate: bool = False
+    sample_every: int = 4096
+
+
+class TeraSortShuffle:
+    def __init__(self, ctx: DistContext, cfg: TeraSortConfig, device: int | None = None):
+        self.ctx = ctx
+        self.cfg = cfg
+        self.device = ctx.local_rank if device is None else device
+        n = native()
+        records_per_map = max(1, cfg.rows_per_gpu // cfg.maps_per_rank)
+        self.records_per_map = records_per_map
+        self.job = n.ShuffleJob(dict(
+            device=self.device, rank=ctx.rank, world=ctx.world,
+            maps_per_rank=cfg.maps_per_rank, records_per_map=records_per_map,
+            rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
+            d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
+            d2h_streams=cfg.d2h_streams, deliver_host=cfg.deliver_host, validate=cfg.validate))
+        self.sink = n.CountingSink()
+        self.expected_checksum = None
+        self.expected_records = None
+        self.setup_s = {}
+
+    def setup(self) -> None:
+        n = native()
+        t0 = time.perf_counter()
+        if self.ctx.world > 1:
+            uid = n.nccl_unique_id() if self.ctx.rank == 0 else None
+            uid = self.ctx.broadcast_bytes(uid)
+            self.job.init_comm(uid)
+        t1 = time.perf_counter()
+        self.job.generate()
+        t2 = time.perf_counter()
+        # sample keys -> per-destination quantile bounds (all ranks agree)
+        local = self.job.sample_keys(self.cfg.sample_every)
+        gathered = self.ctx.all_gather_object([np.asarray(a) for a in local])
+        per_dest = []
+        for d in range(self.ctx.world):
+            parts = [g[d] for g in gathered if g[d].size]
+            per_dest.append(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64))
+        bounds = round_bounds(per_dest, self.cfg.rounds)
+        self.job.set_bounds(np.ascontiguousarray(bounds.reshape(-1)))
+        self.job.plan()
+        t3 = time.perf_counter()
+        # expected per-reducer checksum/records for validation
+        ck = self.ctx.sum_u64(self.job.local_dest_checksums())
+        rec = self.ctx.sum_u64(self.job.local_dest_records())
+        self.expected_checksum = ck[self.ctx.rank]
+        self.expected_records = rec[self.ctx.rank]
+        self.job.set_counting_sink(self.sink)
+        self.setup_s = dict(comm_init=t1 - t0, generate=t2 - t1, plan=t3 - t2)
+
+    def step(self) -> dict:
+        return self.job.run_step()
+
+    def check(self, stats: dict) -> None:
+        """Raise if a validated step lost, duplicated, corrupted or mis-ordered records."""
+        if stats["records"] != self.expected_records:
+            raise AssertionError(f"records {stats['records']} != expected {self.expected_records}")
+        if stats["bad_layout"]:
+            raise AssertionError("non-TeraSort record layout seen by the merge")
+        if self.cfg.validate:
+            if stats["order_errors"] != 0:
+                raise AssertionError(f"{stats['order_errors']} out-of-order records")
+            if stats["checksum"] != self.expected_checksum:
+                raise AssertionError("checksum mismatch")
