@@ -1,0 +1,181 @@
+// C ABI of libuda.so (see uda/uda_bridge.h). Role dispatch mirrors Java_..._startNative
+// (src/UdaBridge.cc:187-263): is_net_merger selects the NetMerger (ReduceTask) or the MOFSupplier.
+#include "uda/uda_bridge.h"
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../consumer/reduce_task.h"
+#include "../provider/supplier.h"
+#include "uda/cmd.h"
+#include "uda/host.h"
+#include "uda/log.h"
+
+#define UDA_VERSION_STRING "uda_amd-0.1.0 (MI355X-native; reference API 3.4.1)"
+
+struct uda_handle {
+  bool is_merger = false;
+  uda::NetlevOptions opt;
+  std::unique_ptr<uda::Host> host;
+  std::unique_ptr<uda::Supplier> supplier;
+  std::unique_ptr<uda::ReduceTask> task;
+  std::string last_error;
+  std::mutex mu;
+};
+
+namespace {
+std::mutex g_log_mu;
+uda_callbacks g_log_cb;  // the most recent handle's log sink (the logger is process-wide)
+bool g_log_cb_set = false;
+
+void log_trampoline(void*, const char* msg, int sev) {
+  uda_callbacks cb;
+  {
+    std::lock_guard<std::mutex> g(g_log_mu);
+    if (!g_log_cb_set) return;
+    cb = g_log_cb;
+  }
+  if (cb.log) cb.log(cb.ctx, msg, sev);
+}
+
+int fail_call(uda_handle* h, const std::string& why) {
+  h->last_error = why;
+  UDA_LOG(uda::kError, "%s", why.c_str());
+  return -1;
+}
+}  // namespace
+
+extern "C" {
+
+const char* uda_version(void) { return UDA_VERSION_STRING; }
+
+void uda_set_log_level(int level) { uda::log_set_threshold(level); }
+
+uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int log_level, int log_to_file,
+                      const uda_callbacks* cb) {
+  auto h = std::make_unique<uda_handle>();
+  h->is_merger = is_net_merger != 0;
+  h->host = std::make_unique<uda::Host>(cb);
+  uda::log_set_threshold(log_level);
+  std::vector<std::string> args;
+  for (int i = 0; i < argc; ++i) args.emplace_back(argv[i] ? argv[i] : "");
+  std::string err;
+  if (!uda::parse_options(args, &h->opt, &err)) {
+    UDA_LOG(uda::kError, "bad options: %s", err.c_str());
+    return nullptr;
+  }
+  if (log_to_file) {
+    uda::log_open_file(h->opt.log_dir, h->is_merger ? "NetMerger" : "MOFSupplier");
+  } else if (cb && cb->log) {
+    std::lock_guard<std::mutex> g(g_log_mu);
+    g_log_cb = *cb;
+    g_log_cb_set = true;
+    uda::log_set_sink(log_trampoline, nullptr);
+  }
+  UDA_LOG(uda::kInfo, "UDA version is %s; role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
+  try {
+    if (h->is_merger) {
+      h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());
+    } else {
+      uda::Supplier::Options so;
+      so.transport = h->host->get_conf("mapred.uda.transport", "loopback");
+      so.loopback_host = h->host->get_conf("mapred.uda.loopback.host", "*");
+      so.io_threads = (int)h->host->conf_i64("mapred.uda.provider.blocked.threads.per.disk", 4);
+      so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);
+      h->supplier = std::make_unique<uda::Supplier>(h->opt, so, h->host.get());
+      h->supplier->start();
+    }
+  } catch (const std::exception& e) {
+    UDA_LOG(uda::kError, "startNative failed: %s", e.what());
+    return nullptr;
+  }
+  return h.release();
+}
+
+int uda_do_command(uda_handle* h, const char* cmd) {
+  if (!h) return -1;
+  std::lock_guard<std::mutex> g(h->mu);
+  uda::HadoopCmd c;
+  if (!uda::parse_cmd(cmd ? cmd : "", &c)) return fail_call(h, "C++ could not parse Hadoop command");
+  try {
+    if (h->is_merger) {
+      if (!h->task) return fail_call(h, "reduce task already closed");
+      h->task->handle(c);
+    } else {
+      // mof_downcall_handler (MOFSupplierMain.cc:37-81): only EXIT matters
+      if (c.header == uda::kExitMsg && h->supplier) {
+        h->supplier->stop();
+        UDA_LOG(uda::kInfo, "MOFSupplier stopped");
+      }
+    }
+  } catch (const std::exception& e) {
+    return fail_call(h, e.what());
+  }
+  return 0;
+}
+
+int uda_reduce_exit(uda_handle* h) {
+  if (!h) return -1;
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    if (h->task) {
+      h->task->exit();
+      UDA_LOG(uda::kInfo, "reduce task closed: %s", h->task->stats_json().c_str());
+    }
+    if (h->supplier) h->supplier->stop();
+  } catch (const std::exception& e) {
+    return fail_call(h, e.what());
+  }
+  return 0;
+}
+
+void uda_destroy(uda_handle* h) {
+  if (!h) return;
+  {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->task) h->task->exit();
+    if (h->supplier) h->supplier->stop();
+    h->task.reset();
+    h->supplier.reset();
+  }
+  delete h;
+}
+
+const char* uda_last_error(uda_handle* h) { return h ? h->last_error.c_str() : ""; }
+
+int uda_provider_register_mof(uda_handle* h, const char* job_id, const char* map_id, const void* data, int64_t len,
+                              const int64_t* index, int32_t num_partitions) {
+  if (!h || !h->supplier) return -1;
+  std::vector<uda::IndexRec> recs((size_t)num_partitions);
+  for (int i = 0; i < num_partitions; ++i) {
+    recs[i].start_offset = index[3 * i];
+    recs[i].raw_length = index[3 * i + 1];
+    recs[i].part_length = index[3 * i + 2];
+    recs[i].path = std::string("mem:") + job_id + "/" + map_id;
+  }
+  h->supplier->register_mof(job_id, map_id, (const uint8_t*)data, len, std::move(recs));
+  return 0;
+}
+
+int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
+  if (!h || !out || outlen <= 0) return -1;
+  std::string s;
+  if (h->task) {
+    s = h->task->stats_json();
+  } else if (h->supplier) {
+    s = "{\"role\":\"mof_supplier\",\"requests\":" + std::to_string(h->supplier->requests()) +
+        ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) + ",\"port\":" +
+        std::to_string(h->supplier->port()) + ",\"io\":\"" + h->supplier->io_backend() + "\"}";
+  } else {
+    s = "{}";
+  }
+  const int32_t n = (int32_t)std::min<size_t>(s.size(), (size_t)outlen - 1);
+  std::memcpy(out, s.data(), (size_t)n);
+  out[n] = 0;
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,494 @@
+#include "reduce_task.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <sstream>
+
+#include "uda/log.h"
+#include "uda/queues.h"
+
+namespace uda {
+
+namespace {
+constexpr int kProgressReportLimit = 20;  // PROGRESS_REPORT_LIMIT (MergeManager.cc:44)
+constexpr int kExtraBuffers = 10;         // EXTRA_RDMA_BUFFERS (reducer.cc:50)
+constexpr int kMinParallelLpqs = 3;       // MIN_PARALLEL_LPQS (MergeManager.h:125)
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Merged-records spill file reader for the RPQ (SuperSegment, StreamRW.cc:813-861).
+struct FileSource {
+  int fd = -1;
+  int64_t off = 0;
+  int64_t read(uint8_t* dst, int64_t cap) {
+    for (;;) {
+      ssize_t r = ::pread(fd, dst, (size_t)cap, off);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) throw UdaError(std::string("spill read failed: ") + strerror(errno));
+      off += r;
+      return r;
+    }
+  }
+};
+}  // namespace
+
+// --------------------------------------------------------------------------------- MofFetcher
+MofFetcher::MofFetcher(ReduceTask* task, FetchParams p, int64_t buf_size, Codec codec)
+    : task_(task), p_(std::move(p)), buf_size_(buf_size), codec_(codec) {
+  bufs_[0].resize((size_t)buf_size_);
+  bufs_[1].resize((size_t)buf_size_);
+  proto_.job_id = p_.job_id;
+  proto_.map_id = p_.map_id;
+  proto_.reduce_id = p_.reduce_id;
+  if (codec_ != Codec::kNone) dec_ = std::make_unique<BlockDecoder>(codec_);
+}
+
+void MofFetcher::start() {
+  std::function<void()> call;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    call = prepare(0);
+  }
+  call();
+}
+
+std::function<void()> MofFetcher::prepare(int b) {
+  FetchRequest req = proto_;
+  req.fetched = requested_;
+  req.buf_len = buf_size_;
+  requested_ += buf_size_;
+  inflight_[b] = true;
+  ready_[b] = false;
+  auto self = shared_from_this();
+  uint8_t* dst = bufs_[b].data();
+  return [self, b, req, dst] {
+    self->task_->transport()->fetch(self->p_.host, req, dst, [self, b](const FetchAck& a) { self->on_done(b, a); });
+  };
+}
+
+void MofFetcher::on_done(int b, const FetchAck& a) {
+  bool first = false;
+  {
+    std::unique_lock<std::mutex> lk(mu_, std::defer_lock);
+    lk.lock();
+    inflight_[b] = false;
+    if (a.status != 0) {
+      error_ = a.error.empty() ? "fetch failed" : a.error;
+    } else {
+      len_[b] = a.sent;
+      ready_[b] = true;
+      part_len_ = a.part_len;
+      proto_.mof_offset = a.mof_offset;
+      proto_.raw_len = a.raw_len;
+      proto_.part_len = a.part_len;
+      proto_.path = a.path;
+    }
+    if (!first_done_) {
+      first_done_ = true;
+      first = true;
+    }
+  }
+  cv_.notify_all();
+  if (first) {
+    {
+      std::lock_guard<std::mutex> g(task_->mu_);
+      task_->fetched_.push_back(shared_from_this());
+    }
+    task_->cv_.notify_all();
+  }
+}
+
+int64_t MofFetcher::pull_raw(uint8_t* dst, int64_t cap) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (part_len_ >= 0 && consumed_ >= part_len_) {
+    lk.unlock();
+    release_pair();
+    return 0;
+  }
+  const int b = cur_;
+  auto t0 = std::chrono::steady_clock::now();
+  cv_.wait(lk, [&] { return ready_[b] || !error_.empty(); });
+  wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  if (!error_.empty()) throw UdaError("fetch of " + p_.map_id + " failed: " + error_);
+  const int64_t n = std::min(len_[b], cap);
+  std::memcpy(dst, bufs_[b].data(), (size_t)n);
+  consumed_ += n;
+  ready_[b] = false;
+  cur_ ^= 1;
+  // keep one request ahead: the buffer just drained and the other one (if idle) get the next
+  // chunks in offset order
+  const int nb = cur_;  // next chunk expected here
+  std::vector<std::function<void()>> calls;
+  if (!inflight_[nb] && !ready_[nb] && requested_ < part_len_) calls.push_back(prepare(nb));
+  if (!inflight_[b] && !ready_[b] && requested_ < part_len_) calls.push_back(prepare(b));
+  const bool ended = consumed_ >= part_len_;
+  lk.unlock();
+  for (auto& c : calls) c();
+  {
+    std::lock_guard<std::mutex> g(task_->st_mu_);
+    task_->st_.bytes_fetched += n;
+  }
+  if (ended) release_pair();
+  return n;
+}
+
+void MofFetcher::release_pair() {
+  if (released_.exchange(true)) return;  // buffers go back to the pool once
+  {
+    std::lock_guard<std::mutex> g(task_->mu_);
+    task_->free_pairs_++;
+  }
+  task_->cv_.notify_all();
+}
+
+int64_t MofFetcher::pull(uint8_t* dst, int64_t cap) {
+  if (!dec_) return pull_raw(dst, cap);
+  std::vector<uint8_t> tmp;
+  for (;;) {
+    size_t r = dec_->read(dst, (size_t)cap);
+    if (r > 0) return (int64_t)r;
+    if (tmp.empty()) tmp.resize((size_t)buf_size_);
+    int64_t n = pull_raw(tmp.data(), (int64_t)tmp.size());
+    if (n == 0) {
+      if (!dec_->idle()) throw UdaError("compressed MOF ended inside a block");
+      return 0;
+    }
+    dec_->feed(tmp.data(), (size_t)n);
+  }
+}
+
+// --------------------------------------------------------------------------------- ReduceTask
+ReduceTask::ReduceTask(const NetlevOptions& net, Host* host) : net_(net), host_(host) {}
+
+ReduceTask::~ReduceTask() { exit(); }
+
+void ReduceTask::handle(const HadoopCmd& cmd) {
+  std::string err;
+  switch (cmd.header) {
+    case kInitMsg: {
+      InitParams p;
+      if (!parse_init_params(cmd, &p, &err)) throw ProtocolError(err);
+      on_init(p);
+      break;
+    }
+    case kFetchMsg: {
+      FetchParams f;
+      if (!parse_fetch_params(cmd, &f, &err)) throw ProtocolError(err);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        fetch_list_.push_back(f);
+      }
+      cv_.notify_all();
+      break;
+    }
+    case kFinalMsg: {
+      std::lock_guard<std::mutex> g(mu_);
+      final_ = true;
+      cv_.notify_all();
+      break;
+    }
+    case kExitMsg:
+      exit();
+      break;
+    default:
+      UDA_LOG(kDebug, "ignoring command %d", (int)cmd.header);
+      break;
+  }
+}
+
+void ReduceTask::on_init(const InitParams& p) {
+  if (inited_) throw ProtocolError("INIT received twice");
+  init_ = p;
+  kind_ = key_kind_from_class(p.key_class.c_str());
+  if (kind_ == KeyKind::kUnsupported)
+    throw ProtocolError("using compare function for unsupported type: " + p.key_class);
+  bool unsup = false;
+  codec_ = codec_from_class(p.codec, &unsup);
+  if (unsup) throw ProtocolError("unsupported compression codec: " + p.codec);
+  const int maps = p.num_maps;
+  // LPQ geometry (reduce_task::init, reducer.cc:260-285)
+  if (p.lpq_size > 0) {
+    num_lpqs_ = maps / p.lpq_size;
+    if (maps % p.lpq_size > 1) num_lpqs_++;
+  } else {
+    num_lpqs_ = (int)std::sqrt((double)maps);
+  }
+  num_parallel_lpqs_ = std::max<int>(kMinParallelLpqs, (int)host_->conf_i64("mapred.rdma.num.parallel.lpqs", 0));
+  const bool hybrid = net_.online == 2 && num_lpqs_ > 1 && maps >= num_lpqs_;
+  const int max_mofs_in_lpq = num_lpqs_ > 0 ? maps / num_lpqs_ + 1 : maps;
+  num_kv_bufs_ = hybrid ? max_mofs_in_lpq * num_parallel_lpqs_ : std::max(1, maps);
+  // buffer sizing (handle_init_msg, reducer.cc:102-120)
+  int64_t max_buf = std::min<int64_t>(p.max_buf_bytes, net_.buf_size > 0 ? net_.buf_size : p.max_buf_bytes);
+  if (max_buf <= 0) max_buf = 1 << 20;
+  if (p.shuffle_mem_bytes > 0 && p.shuffle_mem_bytes < (int64_t)num_kv_bufs_ * max_buf * 2) {
+    max_buf = p.shuffle_mem_bytes / ((int64_t)num_kv_bufs_ * 2);
+    if (max_buf < p.min_buf_bytes) throw UdaError("Not enough memory for rdma buffers");
+    UDA_LOG(kWarn, "using calculated buffer size %ld instead of %ld", (long)max_buf, (long)p.max_buf_bytes);
+  }
+  const int64_t page = sysconf(_SC_PAGESIZE);
+  buffer_size_ = max_buf - max_buf % page;
+  if (buffer_size_ <= 0 || buffer_size_ < p.min_buf_bytes) throw UdaError("RDMA Buffer is too small");
+  free_pairs_ = num_kv_bufs_ + kExtraBuffers;
+  kv_buf_size_ = host_->conf_i64("mapred.uda.kv.buf.size", 1 << 20);
+  backend_ = host_->get_conf("mapred.uda.merge.backend", "cpu");
+  const std::string tr = host_->get_conf("mapred.uda.transport", "loopback");
+  transport_ = (tr == "tcp") ? make_tcp_client(net_.data_port, net_.wqes_per_conn) : make_loopback_client();
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.backend = backend_;
+  }
+  inited_ = true;
+  UDA_LOG(kInfo, "reduce task %s: maps=%d approach=%d lpqs=%d kv_bufs=%d buffer=%ld codec=%s key=%s backend=%s",
+          p.reduce_task_id.c_str(), maps, net_.online, num_lpqs_, num_kv_bufs_, (long)buffer_size_,
+          codec_name(codec_), key_kind_name(kind_), backend_.c_str());
+  merge_thr_ = std::thread([this] { merge_main(); });
+}
+
+void ReduceTask::exit() {
+  stop_ = true;
+  cv_.notify_all();
+  if (merge_thr_.joinable()) merge_thr_.join();
+  if (transport_) transport_->close();
+}
+
+void ReduceTask::merge_main() {
+  auto t0 = std::chrono::steady_clock::now();
+  try {
+    if (backend_ == "gpu")
+      merge_gpu();
+    else if (net_.online == 2)
+      merge_hybrid();
+    else
+      merge_online();
+  } catch (const std::exception& e) {
+    if (!stop_) host_->fail(e.what());
+  }
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.total_ms = ms_since(t0);
+  }
+  finished_ = true;
+}
+
+std::unique_ptr<Segment> ReduceTask::segment_for(std::shared_ptr<MofFetcher> f, int index) {
+  auto seg = std::make_unique<StreamSegment>(
+      [f](uint8_t* dst, int64_t cap) { return f->pull(dst, cap); }, buffer_size_);
+  seg->index = index;
+  return seg;
+}
+
+void ReduceTask::fetch_phase(MergeQueue* q, int n) {
+  std::mt19937_64 rng((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
+  int sent = 0, inserted = 0;
+  std::vector<FetchParams> pending;
+  while (inserted < n) {
+    std::vector<std::shared_ptr<MofFetcher>> to_start, arrived;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] {
+        return stop_ || !fetched_.empty() ||
+               ((!fetch_list_.empty() || !pending.empty()) && free_pairs_ > 0 && sent < n);
+      });
+      if (stop_) throw UdaError("reduce task stopped during fetch");
+      // random fetch order spreads load over providers (list_shuffle_in_vector, UdaUtil.h:56-101)
+      while (!fetch_list_.empty()) {
+        pending.push_back(fetch_list_.front());
+        fetch_list_.pop_front();
+      }
+      std::shuffle(pending.begin(), pending.end(), rng);
+      while (!pending.empty() && free_pairs_ > 0 && sent < n) {
+        to_start.push_back(std::make_shared<MofFetcher>(this, pending.back(), buffer_size_, codec_));
+        pending.pop_back();
+        free_pairs_--;
+        sent++;
+      }
+      while (!fetched_.empty()) {
+        arrived.push_back(fetched_.front());
+        fetched_.pop_front();
+      }
+    }
+    for (auto& f : to_start) f->start();
+    for (auto& f : arrived) {
+      q->insert(segment_for(f, next_index_++));
+      inserted++;
+      total_count_++;
+      progress_count_++;
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.maps_fetched++;
+      }
+      if (progress_count_ == kProgressReportLimit || total_count_ == init_.num_maps) {
+        host_->fetch_over();
+        progress_count_ = 0;
+      }
+    }
+  }
+  // requests not needed by this phase go back to the shared list (hybrid: next LPQ)
+  if (!pending.empty()) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& p : pending) fetch_list_.push_front(p);
+  }
+}
+
+void ReduceTask::merging_phase(MergeQueue* q) {
+  std::vector<uint8_t> buf((size_t)kv_buf_size_);
+  KVWriter w(q);
+  bool done = false;
+  while (!done) {
+    if (stop_) throw UdaError("reduce task stopped during merge");
+    int64_t len = 0;
+    done = w.fill(buf.data(), (int64_t)buf.size(), &len);
+    if (host_->data_from_uda(buf.data(), (int32_t)len) != 0) throw UdaError("dataFromUda callback failed");
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.buffers++;
+    st_.bytes_delivered += len;
+  }
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.records += w.records();
+}
+
+void ReduceTask::merge_online() {
+  auto t0 = std::chrono::steady_clock::now();
+  MergeQueue q(kind_);
+  fetch_phase(&q, init_.num_maps);
+  const double f = ms_since(t0);
+  merging_phase(&q);
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.fetch_ms = f;
+  st_.merge_ms = ms_since(t0) - f;
+}
+
+void ReduceTask::merge_hybrid() {
+  const int maps = init_.num_maps;
+  if (num_lpqs_ <= 1 || maps < num_lpqs_) return merge_online();
+  const int per = maps / num_lpqs_;
+  const int regular = num_lpqs_ - maps % num_lpqs_;
+  std::vector<std::string> dirs = init_.local_dirs;
+  if (dirs.empty()) dirs.push_back("/tmp");
+  std::mt19937 rng((unsigned)std::chrono::steady_clock::now().time_since_epoch().count());
+  int dir_counter = (int)(rng() % dirs.size());
+  ExternalQuotaQueue<std::pair<MergeQueue*, std::string>> pending((size_t)num_parallel_lpqs_);
+  std::exception_ptr fetch_err;
+  auto t0 = std::chrono::steady_clock::now();
+  // LPQ fetcher thread (fetch_lpqs, MergeManager.cc:202-232)
+  std::thread fetcher([&] {
+    try {
+      for (int i = 0; i < num_lpqs_; ++i) {
+        const int n = (i < regular) ? per : per + 1;
+        const std::string& dir = dirs[(size_t)(++dir_counter) % dirs.size()];
+        char name[64];
+        snprintf(name, sizeof(name), ".lpq-%03d", i);
+        std::string path = dir + "/uda." + init_.reduce_task_id + name;
+        pending.wait_and_reserve();
+        auto* q = new MergeQueue(kind_);
+        fetch_phase(q, n);
+        pending.push_reserved({q, path});
+      }
+    } catch (...) {
+      fetch_err = std::current_exception();
+      pending.push_reserved({nullptr, std::string()});
+    }
+  });
+  std::vector<std::string> files;
+  std::vector<uint8_t> buf((size_t)kv_buf_size_);
+  try {
+    for (int i = 0; i < num_lpqs_; ++i) {
+      auto item = pending.wait_and_pop_without_dereserve();
+      if (!item.first) break;
+      std::unique_ptr<MergeQueue> q(item.first);
+      // LPQ merge -> spill file (write_kv_to_file, StreamRW.cc:863-887): records + EOF marker
+      int fd = ::open(item.second.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+      if (fd < 0) throw UdaError("cannot create spill file " + item.second + ": " + strerror(errno));
+      files.push_back(item.second);
+      KVWriter w(q.get());
+      bool done = false;
+      int64_t written = 0;
+      while (!done) {
+        int64_t len = 0;
+        done = w.fill(buf.data(), (int64_t)buf.size(), &len);
+        const int64_t body = done ? len - kEofBytes : len;  // EOF once, at the very end
+        if (body > 0 && ::write(fd, buf.data(), (size_t)body) != body) {
+          ::close(fd);
+          throw UdaError("spill write failed");
+        }
+        written += body;
+      }
+      const uint8_t eof[2] = {0xFF, 0xFF};
+      if (::write(fd, eof, 2) != 2) {
+        ::close(fd);
+        throw UdaError("spill write failed");
+      }
+      ::close(fd);
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.lpqs++;
+        st_.spill_bytes += written + 2;
+      }
+      pending.dereserve();
+    }
+  } catch (...) {
+    stop_ = true;
+    cv_.notify_all();
+    pending.dereserve();
+    fetcher.join();
+    for (auto& f : files) ::unlink(f.c_str());
+    throw;
+  }
+  fetcher.join();
+  if (fetch_err) {
+    for (auto& f : files) ::unlink(f.c_str());
+    std::rethrow_exception(fetch_err);
+  }
+  const double fetch_ms = ms_since(t0);
+  // RPQ over the spilled LPQ outputs (SuperSegment)
+  MergeQueue rpq(kind_);
+  std::vector<std::shared_ptr<FileSource>> srcs;
+  for (size_t i = 0; i < files.size(); ++i) {
+    auto s = std::make_shared<FileSource>();
+    s->fd = ::open(files[i].c_str(), O_RDONLY | O_CLOEXEC);
+    if (s->fd < 0) throw UdaError("cannot reopen spill file " + files[i]);
+    srcs.push_back(s);
+    auto seg = std::make_unique<StreamSegment>([s](uint8_t* d, int64_t c) { return s->read(d, c); },
+                                               std::max<int64_t>(buffer_size_, 1 << 20));
+    seg->index = (int)i;
+    rpq.insert(std::move(seg));
+  }
+  merging_phase(&rpq);
+  for (auto& s : srcs) ::close(s->fd);
+  for (auto& f : files) ::unlink(f.c_str());  // transient, like SuperSegment's dtor
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.fetch_ms = fetch_ms;
+  st_.merge_ms = ms_since(t0) - fetch_ms;
+}
+
+void ReduceTask::merge_gpu() {
+  UDA_LOG(kWarn, "GPU merge backend not available in this build path; using the CPU merge");
+  merge_online();
+}
+
+ReduceStats ReduceTask::stats() const {
+  std::lock_guard<std::mutex> g(st_mu_);
+  return st_;
+}
+
+std::string ReduceTask::stats_json() const {
+  ReduceStats s = stats();
+  std::ostringstream o;
+  o << "{\"role\":\"net_merger\",\"backend\":\"" << s.backend << "\",\"maps_fetched\":" << s.maps_fetched
+    << ",\"bytes_fetched\":" << s.bytes_fetched << ",\"bytes_delivered\":" << s.bytes_delivered
+    << ",\"records\":" << s.records << ",\"buffers\":" << s.buffers << ",\"lpqs\":" << s.lpqs
+    << ",\"spill_bytes\":" << s.spill_bytes << ",\"fetch_ms\":" << s.fetch_ms << ",\"merge_ms\":" << s.merge_ms
+    << ",\"total_ms\":" << s.total_ms << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+  return o.str();
+}
+
+}  // namespace uda

@@ -1,0 +1,146 @@
+// NetMerger reduce task: INIT/FETCH/FINAL/EXIT handling, memory planning, fetch phase, online and
+// hybrid (LPQ/RPQ with local-dir spill) merge, delivery to the host through dataFromUda.
+//
+// Parity:
+//   handle_init_msg / reduce_downcall_handler / calculateMemPool (src/Merger/reducer.cc:56-217, 453-496)
+//   merge_do_fetching_phase / merge_do_merging_phase / merge_online / fetch_lpqs / merge_hybrid
+//   (src/Merger/MergeManager.cc:47-314)
+// Backends: "cpu" (heap k-way merge, the reference algorithm) and "gpu" (whole partitions staged in
+// HBM and merged by the HIP merge tree; csrc/consumer/gpu_merge.cc), chosen with
+// mapred.uda.merge.backend.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "uda/cmd.h"
+#include "uda/codec.h"
+#include "uda/compare.h"
+#include "uda/host.h"
+#include "uda/ifile.h"
+#include "uda/transport.h"
+
+namespace uda {
+
+class MofFetcher;
+
+struct ReduceStats {
+  int64_t maps_fetched = 0;
+  int64_t bytes_fetched = 0;      // partition bytes received (compressed if compressed)
+  int64_t bytes_delivered = 0;    // merged bytes handed to the host
+  int64_t records = 0;
+  int64_t buffers = 0;
+  int64_t lpqs = 0;
+  int64_t spill_bytes = 0;
+  double fetch_ms = 0, merge_ms = 0, total_ms = 0;
+  double wait_ms = 0;             // time the merge waited on the network (total_wait_mem_time)
+  std::string backend;
+};
+
+class ReduceTask {
+ public:
+  ReduceTask(const NetlevOptions& net, Host* host);
+  ~ReduceTask();
+  // Downcall from the host. Throws ProtocolError on a malformed/unsupported command.
+  void handle(const HadoopCmd& cmd);
+  // Close (reduceExitMsg): stop and join the merge thread.
+  void exit();
+  bool finished() const { return finished_.load(); }
+  ReduceStats stats() const;
+  std::string stats_json() const;
+
+  // exposed for the fetchers
+  ClientTransport* transport() { return transport_.get(); }
+
+ private:
+  void on_init(const InitParams& p);
+  void merge_main();
+  void merge_online();
+  void merge_hybrid();
+  void merge_gpu();
+  // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
+  void fetch_phase(MergeQueue* q, int n);
+  void merging_phase(MergeQueue* q);
+  std::unique_ptr<Segment> segment_for(std::shared_ptr<MofFetcher> f, int index);
+
+  NetlevOptions net_;
+  Host* host_;
+  InitParams init_;
+  KeyKind kind_ = KeyKind::kText;
+  Codec codec_ = Codec::kNone;
+  int64_t buffer_size_ = 0;        // per fetch buffer (pair = 2 of these)
+  int64_t kv_buf_size_ = 1 << 20;  // delivery buffer (NETLEV_KV_POOL_EXPO)
+  int num_kv_bufs_ = 0;
+  int num_lpqs_ = 0;
+  int num_parallel_lpqs_ = 3;
+  std::string backend_ = "cpu";
+  std::unique_ptr<ClientTransport> transport_;
+
+  // fetch bookkeeping
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<FetchParams> fetch_list_;
+  std::deque<std::shared_ptr<MofFetcher>> fetched_;  // first chunk arrived
+  int free_pairs_ = 0;
+  int total_count_ = 0;
+  int progress_count_ = 0;
+  bool final_ = false;
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> finished_{false};
+  std::thread merge_thr_;
+  bool inited_ = false;
+  int next_index_ = 0;
+
+  mutable std::mutex st_mu_;
+  ReduceStats st_;
+  friend class MofFetcher;
+};
+
+// Pulls one MOF partition chunk by chunk with one request in flight ahead of the consumer
+// (double buffering, Segment::send_request in the reference); decompresses when a codec is set.
+class MofFetcher : public std::enable_shared_from_this<MofFetcher> {
+ public:
+  MofFetcher(ReduceTask* task, FetchParams p, int64_t buf_size, Codec codec);
+  void start();
+  // ChunkSource: blocks until the next chunk is available; returns bytes (0 at end).
+  int64_t pull(uint8_t* dst, int64_t cap);
+  bool first_arrived() const { return first_done_; }
+  const FetchParams& params() const { return p_; }
+  int64_t part_len() const { return part_len_; }
+  int64_t wait_ns = 0;
+
+ private:
+  // Prepare a fetch into buffer `buf` (mu_ held); the returned call runs after mu_ is released
+  // because a transport may complete inline.
+  std::function<void()> prepare(int buf);
+  void on_done(int buf, const FetchAck& a);
+  int64_t pull_raw(uint8_t* dst, int64_t cap);
+  void release_pair();
+  std::atomic<bool> released_{false};
+  ReduceTask* task_;
+  FetchParams p_;
+  int64_t buf_size_;
+  Codec codec_;
+  std::unique_ptr<BlockDecoder> dec_;
+  std::vector<uint8_t> bufs_[2];
+  int64_t len_[2] = {0, 0};
+  bool ready_[2] = {false, false};
+  bool inflight_[2] = {false, false};
+  int cur_ = 0;
+  int64_t requested_ = 0;   // next offset to request
+  int64_t consumed_ = 0;
+  int64_t part_len_ = -1;
+  FetchRequest proto_;
+  bool first_done_ = false;
+  std::string error_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
+}  // namespace uda

@@ -1,0 +1,225 @@
+#include "supplier.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstring>
+
+#include "uda/log.h"
+
+namespace uda {
+
+Supplier::Supplier(const NetlevOptions& net, const Options& o, Host* host) : net_(net), opt_(o), host_(host) {
+  AsyncIO::Options ao;
+  ao.threads = o.io_threads;
+  aio_ = AsyncIO::create(ao);
+}
+
+Supplier::~Supplier() { stop(); }
+
+void Supplier::start() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = false;
+  }
+  for (int i = 0; i < std::max(1, opt_.workers); ++i) workers_.emplace_back([this] { worker(); });
+  if (opt_.transport == "tcp")
+    server_ = make_tcp_server(net_.data_port, net_.wqes_per_conn);
+  else
+    server_ = make_loopback_server(opt_.loopback_host);
+  server_->start(this);
+  UDA_LOG(kInfo, "MOFSupplier started: transport=%s port=%d io=%s", opt_.transport.c_str(), port(),
+          aio_->backend());
+}
+
+void Supplier::stop() {
+  if (server_) server_->stop();
+  server_.reset();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : workers_) t.join();
+  workers_.clear();
+  if (aio_) aio_->drain();
+  std::lock_guard<std::mutex> g(fd_mu_);
+  for (auto& kv : fds_)
+    if (kv.second.fd >= 0) ::close(kv.second.fd);
+  fds_.clear();
+}
+
+void Supplier::register_mof(const std::string& job, const std::string& map, const uint8_t* data, int64_t len,
+                            std::vector<IndexRec> index) {
+  std::lock_guard<std::mutex> g(idx_mu_);
+  mem_[job + "|" + map] = MemMof{data, len, std::move(index)};
+}
+
+void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(Job{req, dst, std::move(done)});
+  }
+  cv_.notify_one();
+}
+
+void Supplier::worker() {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      j = std::move(q_.front());
+      q_.pop_front();
+    }
+    try {
+      process(j);
+    } catch (const std::exception& e) {
+      FetchAck a;
+      a.status = -9;
+      a.error = e.what();
+      j.done(a);
+    }
+  }
+}
+
+bool Supplier::resolve(const FetchRequest& req, IndexRec* rec, const MemMof** mem) {
+  *mem = nullptr;
+  std::lock_guard<std::mutex> g(idx_mu_);
+  auto m = mem_.find(req.job_id + "|" + req.map_id);
+  if (m != mem_.end()) {
+    if (req.reduce_id < 0 || req.reduce_id >= (int)m->second.index.size()) return false;
+    *rec = m->second.index[req.reduce_id];
+    *mem = &m->second;
+    return true;
+  }
+  const std::string key = req.job_id + "|" + req.map_id + "|" + std::to_string(req.reduce_id);
+  auto c = idx_cache_.find(key);
+  if (c != idx_cache_.end()) {
+    *rec = c->second;
+    return true;
+  }
+  // first touch: ask the host (getPathUda -> IndexRecordBridge)
+  IndexRec r;
+  if (!host_ || !host_->get_path(req.job_id, req.map_id, req.reduce_id, &r)) return false;
+  idx_cache_[key] = r;
+  *rec = r;
+  return true;
+}
+
+int Supplier::acquire_fd(const std::string& path) {
+  std::lock_guard<std::mutex> g(fd_mu_);
+  auto it = fds_.find(path);
+  if (it == fds_.end()) {
+    // evict idle descriptors beyond the bound
+    if ((int)fds_.size() >= opt_.max_open_files) {
+      for (auto e = fds_.begin(); e != fds_.end();) {
+        if (e->second.refs == 0) {
+          ::close(e->second.fd);
+          e = fds_.erase(e);
+        } else {
+          ++e;
+        }
+      }
+    }
+    int flags = O_RDONLY | O_CLOEXEC | (opt_.odirect ? O_DIRECT : 0);
+    int fd = ::open(path.c_str(), flags);
+    if (fd < 0 && opt_.odirect) fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);  // fs without O_DIRECT
+    if (fd < 0) return -1;
+    it = fds_.emplace(path, OpenFile{fd, 0, 0}).first;
+  }
+  it->second.refs++;
+  it->second.last_use = ++fd_clock_;
+  return it->second.fd;
+}
+
+void Supplier::release_fd(const std::string& path) {
+  std::lock_guard<std::mutex> g(fd_mu_);
+  auto it = fds_.find(path);
+  if (it != fds_.end() && it->second.refs > 0) it->second.refs--;
+}
+
+void Supplier::process(Job& j) {
+  requests_++;
+  IndexRec rec;
+  const MemMof* mem = nullptr;
+  FetchAck ack;
+  if (!resolve(j.req, &rec, &mem)) {
+    ack.status = -2;
+    ack.error = "cannot resolve MOF " + j.req.job_id + "/" + j.req.map_id + "/" + std::to_string(j.req.reduce_id);
+    j.done(ack);
+    return;
+  }
+  if ((int)rec.path.size() > kMofPathMax) {  // MOF_PATH_SIZE_TOO_LONG (IndexInfo.cc:265-270)
+    ack.status = -3;
+    ack.error = "MOF path too long";
+    j.done(ack);
+    return;
+  }
+  ack.raw_len = rec.raw_length;
+  ack.part_len = rec.part_length;
+  ack.mof_offset = rec.start_offset;
+  ack.path = rec.path;
+  const int64_t remaining = rec.part_length - j.req.fetched;
+  const int64_t len = std::max<int64_t>(0, std::min<int64_t>(remaining, j.req.buf_len));
+  ack.sent = len;
+  if (len == 0) {
+    j.done(ack);
+    return;
+  }
+  const int64_t off = rec.start_offset + j.req.fetched;
+  if (mem) {
+    if (off + len > mem->len) {
+      ack.status = -4;
+      ack.error = "index beyond registered MOF";
+      j.done(ack);
+      return;
+    }
+    std::memcpy(j.dst, mem->data + off, (size_t)len);
+    bytes_ += len;
+    j.done(ack);
+    return;
+  }
+  const int fd = acquire_fd(rec.path);
+  if (fd < 0) {
+    ack.status = -5;
+    ack.error = "cannot open " + rec.path + ": " + strerror(errno);
+    j.done(ack);
+    return;
+  }
+  const std::string path = rec.path;
+  auto done = std::move(j.done);
+  if (opt_.odirect) {
+    // aligned read into a bounce chunk (aio_read_chunk_data alignment math, IndexInfo.cc:304-335)
+    const int64_t aoff = off - off % kAioAlignment;
+    const int64_t alen = ((off + len - aoff) + kAioAlignment - 1) / kAioAlignment * kAioAlignment;
+    uint8_t* bounce = (uint8_t*)aligned_alloc_io((size_t)alen);
+    uint8_t* dst = j.dst;
+    aio_->read(fd, aoff, alen, bounce, [this, bounce, dst, off, aoff, len, ack, done, path](int64_t r) mutable {
+      if (r < off - aoff + len) {
+        ack.status = -6;
+        ack.error = "short read";
+      } else {
+        std::memcpy(dst, bounce + (off - aoff), (size_t)len);
+        bytes_ += len;
+      }
+      aligned_free_io(bounce);
+      release_fd(path);
+      done(ack);
+    });
+  } else {
+    aio_->read(fd, off, len, j.dst, [this, len, ack, done, path](int64_t r) mutable {
+      if (r != len) {
+        ack.status = -6;
+        ack.error = "short read (" + std::to_string(r) + " of " + std::to_string(len) + ")";
+      } else {
+        bytes_ += len;
+      }
+      release_fd(path);
+      done(ack);
+    });
+  }
+}
+
+}  // namespace uda

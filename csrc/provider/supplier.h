@@ -1,0 +1,96 @@
+// MOFSupplier: serves map-output-file partitions to reducers.
+//
+// Parity:
+//   MOFSupplier_main / mof_downcall_handler   (src/MOFServer/MOFSupplierMain.cc:37-157)
+//   OutputServer request queue                 (src/MOFServer/MOFServlet.cc:99-180)
+//   DataEngine: index resolution via getPathUda on first touch, refcounted fd cache, aligned
+//   O_DIRECT AIO chunk reads, completion -> data + ACK (src/MOFServer/IndexInfo.cc:141-376)
+// MI355X-native differences: partitions can be registered from memory (host or, through the GPU
+// engine, HBM) and the disk path goes through io_uring (uda/aio.h). The data lands directly in the
+// transport's destination buffer (the one-sided RDMA WRITE analogue) instead of a staging chunk.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "uda/aio.h"
+#include "uda/cmd.h"
+#include "uda/host.h"
+#include "uda/transport.h"
+
+namespace uda {
+
+class Supplier : public DataServer {
+ public:
+  struct Options {
+    int workers = 2;             // DataEngine threads
+    int io_threads = 4;          // AsyncIO pool size (blocked.threads.per.disk analogue)
+    bool odirect = false;        // read MOF files with O_DIRECT (4 KiB aligned bounce chunks)
+    int max_open_files = 512;    // fd cache bound (rlimit analogue)
+    std::string transport = "loopback";  // loopback | tcp
+    std::string loopback_host = "*";
+  };
+  Supplier(const NetlevOptions& net, const Options& o, Host* host);
+  ~Supplier() override;
+  void start();
+  void stop();
+
+  // In-memory MOF registration: index[p] = {start_offset, raw_length, part_length}.
+  void register_mof(const std::string& job, const std::string& map, const uint8_t* data, int64_t len,
+                    std::vector<IndexRec> index);
+  void serve(const FetchRequest& req, uint8_t* dst, FetchDone done) override;
+
+  int port() const { return server_ ? server_->port() : -1; }
+  int64_t requests() const { return requests_.load(); }
+  int64_t bytes_served() const { return bytes_.load(); }
+  const char* io_backend() const { return aio_ ? aio_->backend() : "none"; }
+
+ private:
+  struct Job {
+    FetchRequest req;
+    uint8_t* dst;
+    FetchDone done;
+  };
+  struct MemMof {
+    const uint8_t* data;
+    int64_t len;
+    std::vector<IndexRec> index;
+  };
+  struct OpenFile {
+    int fd = -1;
+    int refs = 0;
+    uint64_t last_use = 0;
+  };
+  void worker();
+  void process(Job& j);
+  bool resolve(const FetchRequest& req, IndexRec* rec, const MemMof** mem);
+  int acquire_fd(const std::string& path);
+  void release_fd(const std::string& path);
+
+  NetlevOptions net_;
+  Options opt_;
+  Host* host_;
+  std::unique_ptr<AsyncIO> aio_;
+  std::unique_ptr<ServerTransport> server_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  std::vector<std::thread> workers_;
+  bool stop_ = false;
+  std::mutex idx_mu_;
+  std::map<std::string, MemMof> mem_;                    // key job|map
+  std::unordered_map<std::string, IndexRec> idx_cache_;  // key job|map|reduce
+  std::mutex fd_mu_;
+  std::unordered_map<std::string, OpenFile> fds_;
+  uint64_t fd_clock_ = 0;
+  std::atomic<int64_t> requests_{0}, bytes_{0};
+};
+
+}  // namespace uda

@@ -5,10 +5,17 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cstring>
 
 #include "device_engine.h"
+#include "uda/aio.h"
+#include "uda/codec.h"
+#include "uda/ifile.h"
+#include "uda/uda_bridge.h"
 #include "uda/cmd.h"
 #include "uda/compare.h"
 #include "uda/log.h"
@@ -66,6 +73,115 @@ struct CountingSink {
   std::atomic<int64_t> max_len{0};
 };
 
+// Python host for the C ABI (the "fake JVM"): Python callables stand in for the UdaBridge.java
+// static callbacks. Native threads take the GIL for each callback; bridge entry points release it.
+struct PyBridge {
+  py::object fetch_over, data_from_uda, get_path, get_conf, log, failure;
+  uda_handle* h = nullptr;
+  std::vector<std::shared_ptr<std::string>> keep;
+
+  static PyBridge* self(void* ctx) { return static_cast<PyBridge*>(ctx); }
+  static void t_fetch_over(void* ctx) {
+    py::gil_scoped_acquire g;
+    try {
+      if (!self(ctx)->fetch_over.is_none()) self(ctx)->fetch_over();
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("fetch_over");
+    }
+  }
+  static int t_data(void* ctx, const void* buf, int32_t len) {
+    py::gil_scoped_acquire g;
+    try {
+      if (self(ctx)->data_from_uda.is_none()) return 0;
+      py::object r = self(ctx)->data_from_uda(py::bytes((const char*)buf, (size_t)len));
+      return r.is_none() ? 0 : r.cast<int>();
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("data_from_uda");
+      return -1;
+    }
+  }
+  static int t_get_path(void* ctx, const char* job, const char* map, int32_t reduce, uda_index_record* out) {
+    py::gil_scoped_acquire g;
+    try {
+      if (self(ctx)->get_path.is_none()) return -1;
+      py::object r = self(ctx)->get_path(std::string(job), std::string(map), reduce);
+      if (r.is_none()) return -1;
+      auto t = r.cast<py::tuple>();
+      out->start_offset = t[0].cast<int64_t>();
+      out->raw_length = t[1].cast<int64_t>();
+      out->part_length = t[2].cast<int64_t>();
+      std::string path = t[3].cast<std::string>();
+      std::strncpy(out->path, path.c_str(), UDA_PATH_MAX - 1);
+      return 0;
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("get_path");
+      return -1;
+    }
+  }
+  static int t_get_conf(void* ctx, const char* key, const char* dflt, char* out, int32_t outlen) {
+    py::gil_scoped_acquire g;
+    try {
+      std::string v = dflt ? dflt : "";
+      if (!self(ctx)->get_conf.is_none()) {
+        py::object r = self(ctx)->get_conf(std::string(key), v);
+        if (!r.is_none()) v = r.cast<std::string>();
+      }
+      int32_t n = (int32_t)std::min<size_t>(v.size(), (size_t)outlen - 1);
+      std::memcpy(out, v.data(), (size_t)n);
+      out[n] = 0;
+      return n;
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("get_conf");
+      return -1;
+    }
+  }
+  static void t_log(void* ctx, const char* msg, int32_t sev) {
+    py::gil_scoped_acquire g;
+    try {
+      if (!self(ctx)->log.is_none()) self(ctx)->log(std::string(msg), sev);
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("log");
+    }
+  }
+  static void t_failure(void* ctx, const char* reason) {
+    py::gil_scoped_acquire g;
+    try {
+      if (!self(ctx)->failure.is_none()) self(ctx)->failure(std::string(reason ? reason : ""));
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("failure");
+    }
+  }
+  ~PyBridge() {
+    if (h) {
+      py::gil_scoped_release r;
+      uda_destroy(h);
+    }
+  }
+};
+
+py::bytes cpu_merge_impl(const std::vector<std::string>& runs, const std::string& key_class, int64_t buf,
+                         std::vector<int64_t>* lens) {
+  KeyKind kind = key_kind_from_class(key_class.c_str());
+  if (kind == KeyKind::kUnsupported) throw py::value_error("unsupported key class");
+  MergeQueue q(kind);
+  for (size_t i = 0; i < runs.size(); ++i) {
+    auto seg = std::make_unique<MemorySegment>(reinterpret_cast<const uint8_t*>(runs[i].data()), runs[i].size());
+    seg->index = (int)i;
+    q.insert(std::move(seg));
+  }
+  KVWriter w(&q);
+  std::string out;
+  std::vector<uint8_t> b((size_t)buf);
+  bool done = false;
+  while (!done) {
+    int64_t len = 0;
+    done = w.fill(b.data(), buf, &len);
+    out.append(reinterpret_cast<const char*>(b.data()), (size_t)len);
+    lens->push_back(len);
+  }
+  return py::bytes(out);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_uda_native, m) {
@@ -116,6 +232,167 @@ PYBIND11_MODULE(_uda_native, m) {
     return gpu::record_hash(reinterpret_cast<const uint8_t*>(s.data()), (int64_t)s.size());
   });
   m.def("log_set_threshold", &log_set_threshold);
+
+  m.def("version", &uda_version);
+
+  // ---------------------------------------------------------------- codecs
+  m.def("snappy_compress", [](py::bytes b) {
+    std::string s = b;
+    std::string out(snappy_max_compressed_length(s.size()), '\0');
+    size_t n = snappy_compress((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0]);
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("snappy_decompress", [](py::bytes b, size_t cap) {
+    std::string s = b;
+    std::string out(cap, '\0');
+    size_t n = 0;
+    if (!snappy_decompress((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0], cap, &n))
+      throw py::value_error("corrupt snappy data");
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("lzo1x_compress", [](py::bytes b) {
+    std::string s = b;
+    std::string out(lzo1x_max_compressed_length(s.size()), '\0');
+    size_t n = lzo1x_compress((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0]);
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("lzo1x_decompress", [](py::bytes b, size_t cap) {
+    std::string s = b;
+    std::string out(cap, '\0');
+    size_t n = 0;
+    if (!lzo1x_decompress((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0], cap, &n))
+      throw py::value_error("corrupt lzo1x data");
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("codec_from_class", [](const std::string& c) {
+    bool unsup = false;
+    int v = (int)codec_from_class(c, &unsup);
+    return unsup ? -1 : v;
+  });
+  m.def("block_compress", [](int codec, py::bytes b, size_t block) {
+    std::string s = b;
+    auto v = block_compress((Codec)codec, (const uint8_t*)s.data(), s.size(), block);
+    return py::bytes((const char*)v.data(), v.size());
+  });
+  m.def("block_decompress", [](int codec, py::bytes b, size_t feed_chunk) {
+    std::string s = b;
+    BlockDecoder d((Codec)codec);
+    std::string out;
+    std::vector<uint8_t> tmp(1 << 16);
+    for (size_t off = 0; off < s.size(); off += feed_chunk) {
+      d.feed((const uint8_t*)s.data() + off, std::min(feed_chunk, s.size() - off));
+      for (;;) {
+        size_t n = d.read(tmp.data(), tmp.size());
+        if (!n) break;
+        out.append((const char*)tmp.data(), n);
+      }
+    }
+    if (!d.idle()) throw py::value_error("truncated block stream");
+    return py::bytes(out);
+  });
+
+  // ---------------------------------------------------------------- CPU engine
+  m.def("cpu_merge", [](const std::vector<std::string>& runs, const std::string& key_class, int64_t buf) {
+    std::vector<int64_t> lens;
+    py::bytes out;
+    {
+      out = cpu_merge_impl(runs, key_class, buf, &lens);
+    }
+    return py::make_tuple(out, lens);
+  });
+
+  // ---------------------------------------------------------------- async IO
+  m.def("aio_selftest", [](const std::string& path, int64_t size, const std::string& backend) {
+    // write `size` bytes in 64 KiB pieces then read them back through the same backend
+    if (!backend.empty()) setenv("UDA_AIO_BACKEND", backend.c_str(), 1);
+    auto io = AsyncIO::create(AsyncIO::Options());
+    unsetenv("UDA_AIO_BACKEND");
+    int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0600);
+    if (fd < 0) throw std::runtime_error("open failed");
+    std::vector<uint8_t> src((size_t)size), dst((size_t)size, 0);
+    for (int64_t i = 0; i < size; ++i) src[(size_t)i] = (uint8_t)(i * 131 + (i >> 9));
+    std::atomic<int64_t> bad{0};
+    const int64_t piece = 64 << 10;
+    for (int64_t off = 0; off < size; off += piece) {
+      int64_t len = std::min(piece, size - off);
+      io->write(fd, off, len, src.data() + off, [&bad, len](int64_t r) { if (r != len) bad++; });
+    }
+    io->drain();
+    for (int64_t off = 0; off < size; off += piece) {
+      int64_t len = std::min(piece, size - off);
+      io->read(fd, off, len, dst.data() + off, [&bad, len](int64_t r) { if (r != len) bad++; });
+    }
+    io->drain();
+    ::close(fd);
+    return py::make_tuple(std::string(io->backend()), bad.load() == 0 && src == dst);
+  });
+
+  // ---------------------------------------------------------------- bridge (C ABI)
+  py::class_<PyBridge, std::shared_ptr<PyBridge>>(m, "Bridge")
+      .def(py::init([](bool is_net_merger, const std::vector<std::string>& args, int log_level, py::object fetch_over,
+                       py::object data_from_uda, py::object get_path, py::object get_conf, py::object log,
+                       py::object failure) {
+             auto b = std::make_shared<PyBridge>();
+             b->fetch_over = fetch_over;
+             b->data_from_uda = data_from_uda;
+             b->get_path = get_path;
+             b->get_conf = get_conf;
+             b->log = log;
+             b->failure = failure;
+             uda_callbacks cb;
+             std::memset(&cb, 0, sizeof(cb));
+             cb.ctx = b.get();
+             cb.fetch_over = &PyBridge::t_fetch_over;
+             cb.data_from_uda = &PyBridge::t_data;
+             cb.get_path = &PyBridge::t_get_path;
+             cb.get_conf = &PyBridge::t_get_conf;
+             cb.log = log.is_none() ? nullptr : &PyBridge::t_log;
+             cb.failure = &PyBridge::t_failure;
+             std::vector<const char*> argv;
+             for (auto& a : args) argv.push_back(a.c_str());
+             {
+               py::gil_scoped_release r;
+               b->h = uda_start(is_net_merger ? 1 : 0, (int)argv.size(), argv.data(), log_level, 0, &cb);
+             }
+             if (!b->h) throw std::runtime_error("uda_start failed");
+             return b;
+           }),
+           py::arg("is_net_merger"), py::arg("args"), py::arg("log_level") = 3, py::arg("fetch_over") = py::none(),
+           py::arg("data_from_uda") = py::none(), py::arg("get_path") = py::none(), py::arg("get_conf") = py::none(),
+           py::arg("log") = py::none(), py::arg("failure") = py::none())
+      .def("do_command",
+           [](PyBridge& b, const std::string& cmd) {
+             int r;
+             {
+               py::gil_scoped_release g;
+               r = uda_do_command(b.h, cmd.c_str());
+             }
+             if (r != 0) throw std::runtime_error(std::string("UdaRuntimeException: ") + uda_last_error(b.h));
+           })
+      .def("reduce_exit",
+           [](PyBridge& b) {
+             py::gil_scoped_release g;
+             return uda_reduce_exit(b.h);
+           })
+      .def("register_mof",
+           [](PyBridge& b, const std::string& job, const std::string& map, py::bytes data,
+              const std::vector<int64_t>& index) {
+             // the bridge keeps a reference: the data must outlive the provider
+             auto keep = std::make_shared<std::string>(data);
+             b.keep.push_back(keep);
+             return uda_provider_register_mof(b.h, job.c_str(), map.c_str(), keep->data(), (int64_t)keep->size(),
+                                              index.data(), (int32_t)(index.size() / 3));
+           })
+      .def("stats", [](PyBridge& b) {
+        std::vector<char> buf(4096);
+        uda_stats_json(b.h, buf.data(), (int32_t)buf.size());
+        return std::string(buf.data());
+      });
+  m.def("set_log_level", &uda_set_log_level);
 
   // ---------------------------------------------------------------- GPU engine
   m.def("device_count", &gpu::device_count);

@@ -1,0 +1,371 @@
+// TCP transport: multi-process / multi-host fetch path with the reference's message shapes.
+//
+// Frame = 16-byte netlev header {u8 type, u8 credits, u16 pad, u32 tot_len, u64 src_req}
+// (RDMAComm.h:65-72) + payload. Request payload: the RTS string. Response payload:
+// u32 ack_len | ACK string | partition bytes (the RDMA WRITE + SEND ack pair of
+// RDMAServer.cc:537-631 folded into one frame). Credits: at most `credits` requests in flight per
+// connection (wqes_per_conn); the client connects with up to 5 tries (RECONNECT_TRIES).
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "uda/log.h"
+#include "uda/transport.h"
+
+namespace uda {
+
+namespace {
+constexpr uint8_t kMsgRts = 1;
+constexpr uint8_t kMsgAck = 2;
+constexpr int kReconnectTries = 5;
+
+struct Header {
+  uint8_t type;
+  uint8_t credits;
+  uint16_t pad;
+  uint32_t tot_len;
+  uint64_t src_req;
+};
+static_assert(sizeof(Header) == 16, "netlev header is 16 bytes");
+
+bool read_full(int fd, void* p, size_t n) {
+  uint8_t* b = (uint8_t*)p;
+  while (n) {
+    ssize_t r = ::recv(fd, b, n, 0);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    b += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+bool write_full(int fd, const void* p, size_t n) {
+  const uint8_t* b = (const uint8_t*)p;
+  while (n) {
+    ssize_t r = ::send(fd, b, n, MSG_NOSIGNAL);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    b += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+void tune(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int sz = 4 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+}
+
+// ------------------------------------------------------------------------------------ server
+class TcpServer : public ServerTransport {
+ public:
+  TcpServer(int port, int credits) : port_(port), credits_(credits) {}
+  ~TcpServer() override { stop(); }
+
+  void start(DataServer* s) override {
+    server_ = s;
+    lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (lfd_ < 0) throw std::runtime_error("socket() failed");
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    a.sin_port = htons((uint16_t)port_);
+    if (::bind(lfd_, (sockaddr*)&a, sizeof(a)) != 0)
+      throw std::runtime_error("bind(" + std::to_string(port_) + ") failed: " + strerror(errno));
+    if (::listen(lfd_, 128) != 0) throw std::runtime_error("listen failed");
+    socklen_t len = sizeof(a);
+    getsockname(lfd_, (sockaddr*)&a, &len);
+    port_ = ntohs(a.sin_port);
+    running_ = true;
+    acceptor_ = std::thread([this] { accept_loop(); });
+  }
+
+  void stop() override {
+    if (!running_.exchange(false)) return;
+    ::shutdown(lfd_, SHUT_RDWR);
+    ::close(lfd_);
+    if (acceptor_.joinable()) acceptor_.join();
+    std::vector<std::thread> ts;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& c : conns_) ::shutdown(c->fd, SHUT_RDWR);
+      ts.swap(readers_);
+    }
+    for (auto& t : ts) t.join();
+    std::lock_guard<std::mutex> g(mu_);
+    // wait for in-flight serves to drain before closing sockets
+    for (auto& c : conns_) {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv.wait(lk, [&] { return c->inflight == 0; });
+      ::close(c->fd);
+    }
+    conns_.clear();
+  }
+  int port() const override { return port_; }
+
+ private:
+  struct Conn {
+    int fd;
+    std::mutex mu;  // serializes writes
+    std::condition_variable cv;
+    int inflight = 0;
+  };
+
+  void accept_loop() {
+    while (running_) {
+      int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
+      if (fd < 0) {
+        if (!running_) return;
+        if (errno == EINTR) continue;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        continue;
+      }
+      tune(fd);
+      auto c = std::make_shared<Conn>();
+      c->fd = fd;
+      std::lock_guard<std::mutex> g(mu_);
+      conns_.push_back(c);
+      readers_.emplace_back([this, c] { read_loop(c); });
+    }
+  }
+
+  void read_loop(std::shared_ptr<Conn> c) {
+    std::vector<char> payload;
+    for (;;) {
+      Header h;
+      if (!read_full(c->fd, &h, sizeof(h))) return;
+      if (h.tot_len > (uint32_t)kFetchReqMax * 4) return;  // protocol violation: drop the connection
+      payload.resize(h.tot_len);
+      if (h.tot_len && !read_full(c->fd, payload.data(), h.tot_len)) return;
+      if (h.type != kMsgRts) continue;
+      FetchRequest req;
+      if (!parse_rts(std::string(payload.data(), payload.size()), &req, nullptr, nullptr)) continue;
+      // chunk for the data (the provider's registered chunk, NETLEV_RDMA_MEM_CHUNKS_NUM pool)
+      auto chunk = std::make_shared<std::vector<uint8_t>>((size_t)std::max<int64_t>(0, req.buf_len));
+      {
+        std::unique_lock<std::mutex> lk(c->mu);
+        c->cv.wait(lk, [&] { return c->inflight < credits_; });
+        c->inflight++;
+      }
+      const uint64_t id = h.src_req;
+      server_->serve(req, chunk->data(), [c, chunk, id](const FetchAck& a) {
+        std::string ack = format_ack(a);
+        const uint32_t ack_len = (uint32_t)ack.size();
+        const uint64_t data_len = a.status == 0 ? (uint64_t)a.sent : 0;
+        Header r{kMsgAck, 1, 0, (uint32_t)(4 + ack_len + data_len), id};
+        std::lock_guard<std::mutex> g(c->mu);
+        bool ok = write_full(c->fd, &r, sizeof(r)) && write_full(c->fd, &ack_len, 4) &&
+                  write_full(c->fd, ack.data(), ack_len) && (data_len == 0 || write_full(c->fd, chunk->data(), data_len));
+        if (!ok) ::shutdown(c->fd, SHUT_RDWR);
+        c->inflight--;
+        c->cv.notify_all();
+      });
+    }
+  }
+
+  int port_;
+  int credits_;
+  int lfd_ = -1;
+  std::atomic<bool> running_{false};
+  DataServer* server_ = nullptr;
+  std::thread acceptor_;
+  std::mutex mu_;
+  std::vector<std::shared_ptr<Conn>> conns_;
+  std::vector<std::thread> readers_;
+};
+
+// ------------------------------------------------------------------------------------ client
+class TcpClient : public ClientTransport {
+ public:
+  TcpClient(int port, int credits) : port_(port), credits_(credits > 0 ? credits : 1) {}
+  ~TcpClient() override { close(); }
+
+  void fetch(const std::string& host, const FetchRequest& req, uint8_t* dst, FetchDone done) override {
+    std::shared_ptr<Conn> c;
+    try {
+      c = connect(host);
+    } catch (const std::exception& e) {
+      FetchAck a;
+      a.status = -7;
+      a.error = e.what();
+      done(a);
+      return;
+    }
+    if (fault_should_fail_fetch()) {
+      FetchAck a;
+      a.status = -5;
+      a.error = "injected fetch failure";
+      done(a);
+      return;
+    }
+    const uint64_t id = next_id_++;
+    std::string rts = format_rts(req, (uint64_t)(uintptr_t)dst, id);
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv.wait(lk, [&] { return c->dead || (int)c->pending.size() < credits_; });
+      if (c->dead) {
+        lk.unlock();
+        FetchAck a;
+        a.status = -8;
+        a.error = "connection to " + host + " lost";
+        done(a);
+        return;
+      }
+      c->pending[id] = Pending{dst, req.buf_len, std::move(done)};
+      Header h{kMsgRts, (uint8_t)credits_, 0, (uint32_t)rts.size(), id};
+      if (!write_full(c->fd, &h, sizeof(h)) || !write_full(c->fd, rts.data(), rts.size())) {
+        c->dead = true;
+        ::shutdown(c->fd, SHUT_RDWR);
+      }
+    }
+  }
+
+  void close() override {
+    std::vector<std::shared_ptr<Conn>> cs;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& kv : conns_) cs.push_back(kv.second);
+      conns_.clear();
+    }
+    for (auto& c : cs) {
+      ::shutdown(c->fd, SHUT_RDWR);
+      if (c->reader.joinable()) c->reader.join();
+      ::close(c->fd);
+    }
+  }
+  const char* name() const override { return "tcp"; }
+
+ private:
+  struct Pending {
+    uint8_t* dst;
+    int64_t cap;
+    FetchDone done;
+  };
+  struct Conn {
+    int fd = -1;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<uint64_t, Pending> pending;
+    bool dead = false;
+    std::thread reader;
+  };
+
+  std::shared_ptr<Conn> connect(const std::string& host_spec) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = conns_.find(host_spec);
+    if (it != conns_.end() && !it->second->dead) return it->second;
+    std::string host = host_spec;
+    int port = port_;
+    auto colon = host_spec.rfind(':');
+    if (colon != std::string::npos) {
+      host = host_spec.substr(0, colon);
+      port = std::atoi(host_spec.c_str() + colon + 1);
+    }
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
+      throw std::runtime_error("cannot resolve host " + host);
+    int fd = -1;
+    for (int attempt = 0; attempt < kReconnectTries && fd < 0; ++attempt) {
+      fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      if (::connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
+        ::close(fd);
+        fd = -1;
+        std::this_thread::sleep_for(std::chrono::milliseconds(50 << attempt));
+      }
+    }
+    freeaddrinfo(res);
+    if (fd < 0) throw std::runtime_error("cannot connect to " + host + ":" + std::to_string(port));
+    tune(fd);
+    auto c = std::make_shared<Conn>();
+    c->fd = fd;
+    c->reader = std::thread([c] { reader(c); });
+    conns_[host_spec] = c;
+    return c;
+  }
+
+  static void reader(std::shared_ptr<Conn> c) {
+    std::string ack;
+    for (;;) {
+      Header h;
+      uint32_t ack_len = 0;
+      if (!read_full(c->fd, &h, sizeof(h)) || !read_full(c->fd, &ack_len, 4) || ack_len > (1u << 16)) break;
+      ack.resize(ack_len);
+      if (!read_full(c->fd, &ack[0], ack_len)) break;
+      Pending p;
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        auto it = c->pending.find(h.src_req);
+        if (it == c->pending.end()) break;
+        p = std::move(it->second);
+        c->pending.erase(it);
+      }
+      c->cv.notify_all();
+      FetchAck a;
+      if (!parse_ack(ack, &a)) {
+        a.status = -10;
+        a.error = "bad ack";
+      }
+      const uint64_t data_len = (uint64_t)h.tot_len - 4 - ack_len;
+      if (data_len > (uint64_t)p.cap || (data_len && !read_full(c->fd, p.dst, data_len))) {
+        FetchAck e;
+        e.status = -8;
+        e.error = "bad or truncated response";
+        p.done(e);
+        break;
+      }
+      p.done(a);  // data landed zero-copy in the client buffer
+    }
+    // connection lost: fail everything pending
+    std::map<uint64_t, Pending> left;
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      c->dead = true;
+      left.swap(c->pending);
+    }
+    c->cv.notify_all();
+    for (auto& kv : left) {
+      FetchAck a;
+      a.status = -8;
+      a.error = "connection lost";
+      kv.second.done(a);
+    }
+  }
+
+  int port_;
+  int credits_;
+  std::atomic<uint64_t> next_id_{1};
+  std::mutex mu_;
+  std::unordered_map<std::string, std::shared_ptr<Conn>> conns_;
+};
+}  // namespace
+
+std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits) {
+  return std::make_unique<TcpServer>(port, credits > 0 ? credits : 256);
+}
+std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits) {
+  return std::make_unique<TcpClient>(default_port, credits);
+}
+
+}  // namespace uda

@@ -1,0 +1,166 @@
+"""End-to-end UdaBridge contract over the in-process loopback transport (CPU, no GPU).
+
+Provider (MOFSupplier) and consumer (NetMerger) run in one process, driven through the C ABI the
+way the Java plugins drive JNI. Oracle: a plain Python sort of all map-output records of the
+partition (ties across maps may come out in any map order, as in the reference, so equal-key groups
+are compared as multisets).
+"""
+import collections
+import os
+
+import pytest
+
+from uda_amd.bridge import UdaConsumer, UdaFallback, UdaProvider, run_reduce
+from uda_amd.utils import datagen
+from uda_amd.utils.ifile import EOF_MARKER, decode_stream
+from uda_amd.utils.mof import write_mof
+
+
+def expected(maps, partition, key_class):
+    recs = [kv for m in maps for kv in m[partition]]
+    return sorted(recs, key=datagen.sort_key(key_class))
+
+
+def check_output(got, want, key_class):
+    kf = datagen.sort_key(key_class)
+    assert [kf(kv) for kv in got] == [kf(kv) for kv in want]
+    assert collections.Counter(got) == collections.Counter(want)
+
+
+@pytest.fixture
+def provider(tmp_path):
+    p = UdaProvider()
+    yield p
+    p.close()
+
+
+def publish(provider, tmp_path, job, maps, codec=None, on_disk=True):
+    streams = datagen.streams(maps)
+    ids = []
+    for i, parts in enumerate(streams):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        if on_disk:
+            path, _ = write_mof(str(tmp_path), mid, parts, codec=codec)
+            provider.add_mof_file(job, mid, path)
+        else:
+            from uda_amd.utils.mof import encode_partitions
+            data, index = encode_partitions(parts, codec)
+            provider.add_mof_memory(job, mid, data, index)
+        ids.append(mid)
+    return ids
+
+
+@pytest.mark.parametrize("on_disk", [True, False])
+def test_wordcount_online(provider, tmp_path, on_disk):
+    maps = datagen.wordcount(num_maps=7, reducers=3, words_per_map=3000)
+    ids = publish(provider, tmp_path, "job_1_0001", maps, on_disk=on_disk)
+    for r in range(3):
+        recs, st, c = run_reduce("host-a", "job_1_0001", ids, r, datagen.TEXT)
+        check_output(recs, expected(maps, r, datagen.TEXT), datagen.TEXT)
+        assert st["maps_fetched"] == 7 and st["finished"]
+        assert c.failure is None
+        assert c.fetch_over_calls == 1  # fewer than 20 maps: one report at the end
+
+
+def test_terasort_small_buffers_and_progress(provider, tmp_path):
+    maps = datagen.terasort(num_maps=45, reducers=2, rows_per_map=300)
+    ids = publish(provider, tmp_path, "job_1_0002", maps)
+    # 16 KiB fetch buffers force many chunks per MOF (records straddle chunk boundaries: the join),
+    # 64 KiB delivery buffers force many dataFromUda calls
+    recs, st, c = run_reduce("h", "job_1_0002", ids, 1, datagen.TEXT, max_buf_kb=16, kv_buf_size=64 << 10)
+    check_output(recs, expected(maps, 1, datagen.TEXT), datagen.TEXT)
+    assert c.fetch_over_calls == 3   # every 20 maps + the last one (45 = 20 + 20 + 5)
+    assert c.buffers > 5
+
+
+def test_delivery_framing_matches_reference_packing(provider, tmp_path):
+    # buffers are packed greedily with whole records (J2CQueueReader asserts no record straddles
+    # buffers and no buffer exceeds kv_buf_size); the last buffer ends with the EOF marker
+    maps = datagen.secondary_sort(num_maps=5, reducers=1, rows_per_map=400)
+    ids = publish(provider, tmp_path, "job_1_0003", maps)
+    recs, st, c = run_reduce("h", "job_1_0003", ids, 0, datagen.TEXT, kv_buf_size=8192)
+    want = expected(maps, 0, datagen.TEXT)
+    check_output(recs, want, datagen.TEXT)
+    total = sum(len(datagen.streams([[[kv]]])[0][0]) - 2 for kv in want) + 2
+    assert c.bytes == total
+    # greedy packing leaves less than one record of slack per buffer
+    max_rec = max(len(datagen.streams([[[kv]]])[0][0]) - 2 for kv in want)
+    assert c.buffers <= total // (8192 - max_rec) + 1
+
+
+@pytest.mark.parametrize("codec", ["snappy", "lzo"])
+def test_compressed_map_outputs(provider, tmp_path, codec):
+    maps = datagen.wordcount(num_maps=6, reducers=2, words_per_map=4000, seed=9)
+    ids = publish(provider, tmp_path, "job_1_0004", maps, codec=codec)
+    recs, st, c = run_reduce("h", "job_1_0004", ids, 0, datagen.TEXT, codec=codec, max_buf_kb=16)
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+
+
+def test_hybrid_merge_spills_lpqs(provider, tmp_path):
+    maps = datagen.terasort(num_maps=23, reducers=1, rows_per_map=200, seed=4)
+    ids = publish(provider, tmp_path, "job_1_0005", maps)
+    d1, d2 = tmp_path / "local1", tmp_path / "local2"
+    d1.mkdir()
+    d2.mkdir()
+    recs, st, c = run_reduce("h", "job_1_0005", ids, 0, datagen.TEXT, approach=2, lpq_size=5,
+                             local_dirs=(str(d1), str(d2)))
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+    assert st["lpqs"] == 5          # 23 maps / lpq 5 -> 4 regular + 1 for the remainder (> 1)
+    assert st["spill_bytes"] > 0
+    assert not os.listdir(d1) and not os.listdir(d2)  # LPQ files are transient
+
+
+def test_int_and_bytes_keys(provider, tmp_path):
+    import random
+    rng = random.Random(8)
+    for key_class, mk in [(datagen.INT, lambda: rng.randrange(0, 10**6).to_bytes(4, "big")),
+                          (datagen.BYTES, lambda: (lambda s: len(s).to_bytes(4, "big") + s)(
+                              bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 12)))))]:
+        kf = datagen.sort_key(key_class)
+        maps = [[sorted([(mk(), b"v%d" % i) for i in range(300)], key=kf)] for _ in range(4)]
+        job = "job_k_%d" % len(key_class)
+        ids = publish(provider, tmp_path, job, maps)
+        recs, st, c = run_reduce("h", job, ids, 0, key_class)
+        check_output(recs, expected(maps, 0, key_class), key_class)
+
+
+def test_unsupported_key_class_raises_for_fallback(provider):
+    with pytest.raises(RuntimeError, match="UdaRuntimeException"):
+        UdaConsumer(1, "job_x", "attempt_x_r_0", "org.apache.hadoop.io.DoubleWritable")
+
+
+def test_unknown_mof_triggers_failure_once(provider, tmp_path):
+    c = UdaConsumer(2, "job_missing", "attempt_job_missing_r_000000_0", datagen.TEXT)
+    c.fetch("h", "job_missing", "attempt_nope_m_0", 0)
+    c.fetch("h", "job_missing", "attempt_nope_m_1", 0)
+    with pytest.raises(UdaFallback):
+        c.wait(30)
+    c.close()
+    assert c.failure_calls == 1
+
+
+def test_injected_fetch_fault(provider, tmp_path, monkeypatch):
+    maps = datagen.wordcount(num_maps=4, reducers=1, words_per_map=500)
+    ids = publish(provider, tmp_path, "job_1_0006", maps)
+    monkeypatch.setenv("UDA_FAULT_FETCH", "3")
+    c = UdaConsumer(len(ids), "job_1_0006", "attempt_job_1_0006_r_000000_0", datagen.TEXT, max_buf_kb=16)
+    for m in ids:
+        c.fetch("h", "job_1_0006", m, 0)
+    with pytest.raises(UdaFallback, match="injected"):
+        c.wait(30)
+    c.close()
+    assert c.failure_calls == 1
+
+
+def test_eof_only_partition(provider, tmp_path):
+    ids = publish(provider, tmp_path, "job_1_0007", [[[]], [[]]])
+    recs, st, c = run_reduce("h", "job_1_0007", ids, 0, datagen.TEXT)
+    assert recs == [] and c.bytes == len(EOF_MARKER)
+
+
+def test_cpu_merge_binding_matches_python(native):
+    maps = datagen.secondary_sort(num_maps=9, reducers=1, rows_per_map=200, seed=12)
+    runs = [s[0] for s in datagen.streams(maps)]
+    out, lens = native.cpu_merge(runs, datagen.TEXT, 4096)
+    assert all(n <= 4096 for n in lens) and out.endswith(EOF_MARKER)
+    check_output(decode_stream(out), expected(maps, 0, datagen.TEXT), datagen.TEXT)

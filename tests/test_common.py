@@ -1,0 +1,106 @@
+"""Unit tests for the native common layer: VInt codec, command protocol, options, comparators."""
+import random
+
+import pytest
+
+from uda_amd.utils import ifile
+
+
+VINT_CASES = [0, 1, -1, 127, 128, -112, -113, 255, 256, -256, 65535, 65536, 2**31 - 1, -2**31,
+              2**40, -2**40, 2**63 - 1, -2**63]
+
+
+@pytest.mark.parametrize("v", VINT_CASES)
+def test_vint_matches_hadoop_writable_utils(native, v):
+    enc = native.vint_encode(v)
+    assert enc == ifile.vint_encode(v)
+    assert native.vint_decode(enc) == (v, len(enc))
+    assert native.vint_size(v) == len(enc)
+    first = enc[0] - 256 if enc[0] > 127 else enc[0]
+    assert native.vint_decode_size(first) == len(enc)
+    assert ifile.vint_decode(enc) == (v, len(enc))
+
+
+def test_vint_random_roundtrip(native):
+    rng = random.Random(7)
+    for _ in range(2000):
+        v = rng.randint(-2**63, 2**63 - 1) >> rng.randint(0, 63)
+        assert native.vint_decode(native.vint_encode(v)) == (v, native.vint_size(v))
+
+
+def test_vint_truncated(native):
+    assert native.vint_decode(b"\x8e")[1] == 0  # length byte promises 2 more bytes
+
+
+def form_cmd_java(cmd, params):
+    # UdaCmd.formCmd (UdaPlugin.java:577-586)
+    ret = f"{len(params) + 1}:{cmd}"
+    for p in params:
+        ret += ":" + p
+    return ret
+
+
+@pytest.mark.parametrize("params", [[], ["a"], ["host1", "job_1", "attempt_1_m_000001_0", "3"],
+                                    ["x", "/path/with:colon"]])
+def test_command_format_parity(native, params):
+    assert native.form_cmd(4, params) == form_cmd_java(4, params)
+    count, header, got = native.parse_cmd(form_cmd_java(4, params))
+    assert (count, header) == (len(params) + 1, 4)
+    assert got == params
+
+
+def test_command_edge_cases(native):
+    assert native.parse_cmd("") == (1, 0, [])          # empty == EXIT
+    assert native.parse_cmd("1:0") == (1, 0, [])
+    with pytest.raises(ValueError):
+        native.parse_cmd("garbage")
+    with pytest.raises(ValueError):
+        native.parse_cmd("4:7:a")                        # declares 3 params, carries 1
+
+
+def test_init_command_params_roundtrip(native):
+    params = ["12", "job_201208301702_0002", "attempt_201208301702_0002_r_000002_0", "0",
+              str(1024 * 1024), str(16 * 1024), "org.apache.hadoop.io.Text", "null", str(256 * 1024),
+              str(1 << 30), "2", "/data1/mapred/local", "/data2/mapred/local"]
+    count, header, got = native.parse_cmd(native.form_cmd(7, params))
+    assert header == 7 and got == params
+
+
+def test_options_parser(native):
+    d = native.parse_options(["-w", "128", "-r", "9100", "-a", "2", "-m", "1", "-g", "/tmp/logs", "-s", "1023"])
+    assert d["wqes_per_conn"] == 128 and d["data_port"] == 9100 and d["online"] == 2
+    assert d["log_dir"] == "/tmp/logs"
+    assert d["buf_size"] == 1023 * 1024 - (1023 * 1024) % 4096   # KB -> bytes, 4 KiB aligned
+
+
+TEXT, INT, BYTES = "org.apache.hadoop.io.Text", "org.apache.hadoop.io.IntWritable", "org.apache.hadoop.io.BytesWritable"
+
+
+def test_key_classes(native):
+    assert native.key_kind(TEXT) == 0
+    for c in ("BooleanWritable", "ByteWritable", "ShortWritable", "IntWritable", "LongWritable"):
+        assert native.key_kind("org.apache.hadoop.io." + c) == 1
+    assert native.key_kind(BYTES) == 2
+    assert native.key_kind("org.apache.hadoop.hbase.io.ImmutableBytesWritable") == 2
+    assert native.key_kind("org.apache.hadoop.io.DoubleWritable") == -1
+
+
+def sign(x):
+    return (x > 0) - (x < 0)
+
+
+def test_text_comparator_skips_vint_prefix(native):
+    rng = random.Random(3)
+    for _ in range(500):
+        a = bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 300)))
+        b = a[:rng.randint(0, len(a))] + bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 3)))
+        got = sign(native.key_compare(0, ifile.text(a), ifile.text(b)))
+        assert got == sign((a > b) - (a < b))
+
+
+def test_raw_and_bytes_comparators(native):
+    assert native.key_compare(1, (5).to_bytes(4, "big"), (7).to_bytes(4, "big")) < 0
+    assert native.key_compare(1, b"\x00\x01", b"\x00\x01\x00") < 0  # tie on prefix -> shorter first
+    bw = lambda s: len(s).to_bytes(4, "big") + s  # noqa: E731
+    assert native.key_compare(2, bw(b"abc"), bw(b"abd")) < 0
+    assert native.key_compare(2, bw(b"b"), bw(b"abc")) > 0   # length prefix is skipped, not compared
