@@ -18,12 +18,6 @@ namespace gpu {
 namespace {
 constexpr int kSlots = 2;  // recv/out double buffering across rounds
 
-void nccl_check(ncclResult_t r, const char* what, const char* file, int line) {
-  if (r != ncclSuccess)
-    throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r) + " in " + what +
-                             " at " + file + ":" + std::to_string(line));
-}
-#define NCCL_CHECK(x) nccl_check((x), #x, __FILE__, __LINE__)
 
 double now_ms() {
   return std::chrono::duration<double, std::milli>(
@@ -68,7 +62,8 @@ void PinnedBuffer::alloc(size_t bytes) {
 
 std::string nccl_unique_id() {
   ncclUniqueId id;
-  NCCL_CHECK(ncclGetUniqueId(&id));
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) throw std::runtime_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
@@ -239,7 +234,9 @@ ShuffleJob::~ShuffleJob() {
   for (auto e : piece_start_ev_) (void)hipEventDestroy(e);
   for (auto e : out_free_ev_) (void)hipEventDestroy(e);
   for (auto e : join_ev_) (void)hipEventDestroy(e);
-  if (comm_) ncclCommDestroy(comm_);
+  for (auto& d : desc_slots_)
+    if (d.uploaded) (void)hipEventDestroy(d.uploaded);
+  exchange_.reset();
   for (auto s : s_copy_) (void)hipStreamDestroy(s);
   if (s_comm_) (void)hipStreamDestroy(s_comm_);
   if (s_compute_) (void)hipStreamDestroy(s_compute_);
@@ -247,11 +244,15 @@ ShuffleJob::~ShuffleJob() {
 
 void ShuffleJob::init_comm(const std::string& uid) {
   if (cfg_.world == 1) return;
-  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("init_comm: bad unique id size");
-  ncclUniqueId id;
-  std::memcpy(&id, uid.data(), sizeof(id));
   HIP_CHECK(hipSetDevice(cfg_.device));
-  NCCL_CHECK(ncclCommInitRank(&comm_, cfg_.world, id, cfg_.rank));
+  exchange_ = make_rccl_exchange(cfg_.rank, cfg_.world, uid);
+}
+
+void ShuffleJob::init_local() {
+  if (cfg_.world == 1) return;
+  if (cfg_.local_group.empty()) throw std::runtime_error("init_local: config.local_group is empty");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  exchange_ = make_local_exchange(cfg_.local_group, cfg_.rank, cfg_.world);
 }
 
 void ShuffleJob::generate() {
@@ -412,22 +413,8 @@ void ShuffleJob::compute_round_plans(std::vector<RoundPlan>* plans, double* ms) 
   if (W == 1) {
     recv_counts = send_counts;
   } else {
-    const size_t chunk = (size_t)Q * M;
-    if (d_counts_send_.size() < chunk * W * 8) {
-      d_counts_send_.alloc(chunk * W * 8);
-      d_counts_recv_.alloc(chunk * W * 8);
-    }
-    HIP_CHECK(hipMemcpyAsync(d_counts_send_.as(), send_counts.data(), chunk * W * 8,
-                             hipMemcpyHostToDevice, s_comm_));
-    NCCL_CHECK(ncclGroupStart());
-    for (int p = 0; p < W; ++p) {
-      NCCL_CHECK(ncclSend(d_counts_send_.as<int64_t>() + p * chunk, chunk, ncclInt64, p, comm_, s_comm_));
-      NCCL_CHECK(ncclRecv(d_counts_recv_.as<int64_t>() + p * chunk, chunk, ncclInt64, p, comm_, s_comm_));
-    }
-    NCCL_CHECK(ncclGroupEnd());
-    HIP_CHECK(hipMemcpyAsync(recv_counts.data(), d_counts_recv_.as(), chunk * W * 8,
-                             hipMemcpyDeviceToHost, s_comm_));
-    HIP_CHECK(hipStreamSynchronize(s_comm_));
+    if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
+    exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), (size_t)Q * M, s_comm_);
   }
   for (int q = 0; q < Q; ++q) {
     auto& rp = (*plans)[q];
@@ -458,6 +445,23 @@ void ShuffleJob::plan() {
   if (W > 1) {
     recv_slots_.resize(kSlots);
     for (auto& b : recv_slots_) b.alloc(slot_bytes);
+    max_send_bytes_ = 0;
+    for (const auto& rp : plans_) {
+      int64_t sb = 0;
+      for (int p = 0; p < W; ++p)
+        if (p != cfg_.rank)
+          for (int m = 0; m < M; ++m) sb += (rp.send_end[p * M + m] - rp.send_beg[p * M + m]) * kTeraRecordBytes;
+      max_send_bytes_ = std::max(max_send_bytes_, sb);
+    }
+    pack_slots_.clear();
+    pack_slots_.resize(kSlots);
+    for (auto& b : pack_slots_) b.alloc((size_t)std::max<int64_t>(max_send_bytes_, 16));
+    desc_slots_.resize(4);
+    for (auto& d : desc_slots_) {
+      d.host.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
+      d.dev.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
+      HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
+    }
   }
   d_validate_.alloc(256);
   if (cfg_.deliver_host && pinned_.size() == 0) {
@@ -654,37 +658,54 @@ StepStats ShuffleJob::run_step() {
       }
     } else {
       uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
+      uint8_t* pbuf = pack_slots_[slot].as<uint8_t>();
       if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged[slot], 0));
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
       std::vector<int64_t> roff((size_t)W * M + 1, 0);
       for (int i = 0; i < W * M; ++i) roff[i + 1] = roff[i] + rp.recv_cnt[i] * kTeraRecordBytes;
-      NCCL_CHECK(ncclGroupStart());
+      // pack: per destination, this rank's slices of the round in map order, destinations in
+      // rotating order; the self partition goes straight to its place in the receive slot
+      DescSlot& ds = desc_slots_[next_desc_];
+      next_desc_ = (next_desc_ + 1) % (int)desc_slots_.size();
+      if (ds.used) HIP_CHECK(hipEventSynchronize(ds.uploaded));
+      ds.used = true;
+      CopyDesc* descs = ds.host.as<CopyDesc>();
+      int nd = 0;
+      int64_t max_bytes = 0;
+      std::vector<int64_t> sb(W, 0), sd(W, 0), rb(W, 0), rd(W, 0);
+      int64_t packed = 0;
       for (int k = 1; k < W; ++k) {
-        const int to = (me + k) % W;          // rotating peer order spreads xGMI link load
-        const int from = (me - k + W) % W;
+        const int to = (me + k) % W;
+        sd[to] = packed;
         for (int m = 0; m < M; ++m) {
           const int64_t c = rp.send_end[to * M + m] - rp.send_beg[to * M + m];
-          if (c > 0) {
-            NCCL_CHECK(ncclSend(run_base(m, to) + rp.send_beg[to * M + m] * kTeraRecordBytes,
-                                (size_t)c * kTeraRecordBytes, ncclUint8, to, comm_, s_comm_));
-            bytes_sent += c * kTeraRecordBytes;
-          }
+          if (c <= 0) continue;
+          descs[nd++] = CopyDesc{run_base(m, to) + rp.send_beg[to * M + m] * kTeraRecordBytes, pbuf + packed,
+                                 c * kTeraRecordBytes};
+          max_bytes = std::max(max_bytes, c * kTeraRecordBytes);
+          packed += c * kTeraRecordBytes;
         }
-        for (int j = 0; j < M; ++j) {
-          const int64_t c = rp.recv_cnt[from * M + j];
-          if (c > 0)
-            NCCL_CHECK(ncclRecv(rbuf + roff[from * M + j], (size_t)c * kTeraRecordBytes, ncclUint8,
-                                from, comm_, s_comm_));
-        }
+        sb[to] = packed - sd[to];
       }
-      NCCL_CHECK(ncclGroupEnd());
-      for (int m = 0; m < M; ++m) {  // self partition: device copy
+      for (int m = 0; m < M; ++m) {
         const int64_t c = rp.send_end[me * M + m] - rp.send_beg[me * M + m];
-        if (c > 0)
-          HIP_CHECK(hipMemcpyAsync(rbuf + roff[me * M + m],
-                                   run_base(m, me) + rp.send_beg[me * M + m] * kTeraRecordBytes,
-                                   (size_t)c * kTeraRecordBytes, hipMemcpyDeviceToDevice, s_comm_));
+        if (c <= 0) continue;
+        descs[nd++] = CopyDesc{run_base(m, me) + rp.send_beg[me * M + m] * kTeraRecordBytes, rbuf + roff[me * M + m],
+                               c * kTeraRecordBytes};
+        max_bytes = std::max(max_bytes, c * kTeraRecordBytes);
       }
+      for (int s = 0; s < W; ++s) {
+        if (s == me) continue;
+        rd[s] = roff[s * M];
+        rb[s] = roff[(s + 1) * M] - roff[s * M];
+      }
+      bytes_sent += packed;
+      if (nd > 0) {
+        HIP_CHECK(hipMemcpyAsync(ds.dev.as(), descs, sizeof(CopyDesc) * nd, hipMemcpyHostToDevice, s_comm_));
+        HIP_CHECK(hipEventRecord(ds.uploaded, s_comm_));
+        launch_batched_copy(ds.dev.as<CopyDesc>(), nd, max_bytes, s_comm_);
+      }
+      exchange_->alltoallv(pbuf, sb.data(), sd.data(), rbuf, rb.data(), rd.data(), s_comm_);
       HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
       HIP_CHECK(hipEventRecord(comm_done[slot], s_comm_));
       HIP_CHECK(hipStreamWaitEvent(s_compute_, comm_done[slot], 0));

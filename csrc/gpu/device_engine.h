@@ -30,9 +30,8 @@
 #include <thread>
 #include <vector>
 
+#include "exchange.h"
 #include "kernels.h"
-
-typedef struct ncclComm* ncclComm_t;
 
 namespace uda {
 namespace gpu {
@@ -146,6 +145,7 @@ struct ShuffleConfig {
   int d2h_streams = 1;                   // split each piece over this many copy streams
   bool deliver_host = true;              // false: stop after the device merge (ablation)
   bool validate = false;                 // device-side order + checksum check per round
+  std::string local_group;               // world > 1 without RCCL: ranks are threads of one process
 };
 
 struct StepStats {
@@ -172,6 +172,8 @@ class ShuffleJob {
   const ShuffleConfig& config() const { return cfg_; }
   // RCCL bootstrap; `uid` is the ncclUniqueId produced by rank 0 (nccl_unique_id()).
   void init_comm(const std::string& uid);
+  // Single-process rehearsal: ranks are threads sharing this device (config.local_group).
+  void init_local();
   // Map phase stand-in: generate maps_per_rank TeraSort MOFs into the HBM partition store.
   void generate();
   // Every `every`-th key of every local run, grouped by destination reducer:
@@ -209,7 +211,7 @@ class ShuffleJob {
   uint8_t* run_base(int m, int d) const { return store_.as<uint8_t>() + run_off_[m * cfg_.world + d]; }
 
   ShuffleConfig cfg_;
-  ncclComm_t comm_ = nullptr;
+  std::unique_ptr<Exchange> exchange_;
   hipStream_t s_comm_ = nullptr, s_compute_ = nullptr;
   std::vector<hipStream_t> s_copy_;
   DeviceBuffer store_;
@@ -221,9 +223,18 @@ class ShuffleJob {
   DeviceBuffer d_bounds_, d_run_bases_, d_run_nrec_, d_bound_set_, d_split_out_;
   std::vector<RoundPlan> plans_;
   int64_t max_round_records_ = 0;
-  std::vector<DeviceBuffer> recv_slots_, out_slots_;
+  std::vector<DeviceBuffer> recv_slots_, out_slots_, pack_slots_;
+  int64_t max_send_bytes_ = 0;
+  // copy-descriptor upload ring (pinned host -> device), guarded by events
+  struct DescSlot {
+    PinnedBuffer host;
+    DeviceBuffer dev;
+    hipEvent_t uploaded = nullptr;
+    bool used = false;
+  };
+  std::vector<DescSlot> desc_slots_;
+  int next_desc_ = 0;
   std::unique_ptr<DeviceMerger> merger_;
-  DeviceBuffer d_counts_send_, d_counts_recv_;
   DeviceBuffer d_validate_;  // stats[2] + prev key + last key
   PinnedBuffer pinned_;
   int64_t piece_bytes_ = 0;

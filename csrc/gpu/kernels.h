@@ -90,6 +90,15 @@ void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* sp
 void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases, uint8_t* out,
                          hipStream_t s);
 
+// ---------------------------------------------------------------- batched copy
+struct CopyDesc {
+  const uint8_t* src;
+  uint8_t* dst;
+  int64_t bytes;
+};
+// descs: device array of n descriptors; max_bytes: largest descriptor (sizes the grid).
+void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s);
+
 // ---------------------------------------------------------------- validation
 // Checks key order of `n` FIXED10 records at `recs` (and against *prev_key if has_prev) and
 // accumulates an order-independent checksum. Results: stats[0] += out-of-order count,

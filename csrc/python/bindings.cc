@@ -62,6 +62,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("d2h_streams", c.d2h_streams);
   get("deliver_host", c.deliver_host);
   get("validate", c.validate);
+  get("local_group", c.local_group);
   return c;
 }
 
@@ -413,6 +414,7 @@ PYBIND11_MODULE(_uda_native, m) {
       .def(py::init([](const py::dict& cfg) { return new gpu::ShuffleJob(config_from_dict(cfg)); }))
       .def("init_comm", [](gpu::ShuffleJob& j, py::bytes uid) { j.init_comm(uid); },
            py::call_guard<py::gil_scoped_release>())
+      .def("init_local", &gpu::ShuffleJob::init_local, py::call_guard<py::gil_scoped_release>())
       .def("generate", &gpu::ShuffleJob::generate, py::call_guard<py::gil_scoped_release>())
       .def("sample_keys",
            [](gpu::ShuffleJob& j, int64_t every) {

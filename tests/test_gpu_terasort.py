@@ -64,3 +64,34 @@ def test_merge_tree_many_runs(require_gpu):
     st = j.step()
     j.check(st)
     assert st["merge_passes"] == 9
+
+
+@pytest.mark.parametrize("world,maps,rounds", [(2, 3, 3), (3, 2, 4), (4, 1, 1)])
+def test_multirank_schedule_local_group(require_gpu, world, maps, rounds):
+    """The multi-GPU shuffle schedule (pack -> all-to-all-v rounds -> merge -> deliver) rehearsed
+    with `world` ranks sharing one GPU; every reducer must receive exactly its key range."""
+    from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
+    cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, validate=True,
+                         sample_every=64, kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"t{world}{maps}{rounds}")
+    readers = [J2CQueueReader(max_len=64 << 10) for _ in range(world)]
+    for j, r in zip(jobs, readers):
+        j.set_python_sink(r.feed)
+    for step in range(2):
+        stats = run_collective(jobs, lambda j: j.run_step())
+        for d, st in enumerate(stats):
+            assert st["records"] == rec[d]
+            assert st["order_errors"] == 0
+            assert st["checksum"] == ck[d]
+            if world > 1:
+                assert st["bytes_sent"] > 0
+        if step == 0:
+            for d in range(world):
+                recs = []
+                for j in jobs:  # global map order = (rank, local map)
+                    for m in range(maps):
+                        recs += decode_stream(j.read_partition(m, d))
+                expect = sorted(recs, key=lambda kv: _text_content(kv[0]))
+                assert readers[d].records == expect
+                readers[d] = J2CQueueReader(max_len=64 << 10)
+                jobs[d].set_python_sink(readers[d].feed)

@@ -104,3 +104,56 @@ class TeraSortShuffle:
                 raise AssertionError(f"{stats['order_errors']} out-of-order records")
             if stats["checksum"] != self.expected_checksum:
                 raise AssertionError("checksum mismatch")
+
+
+def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: str = "local"):
+    """Single-process rehearsal of a `world`-rank shuffle: every rank is a ShuffleJob on `device`
+    driven from its own thread, exchanging rounds through device memcpys with the same pack /
+    all-to-all-v schedule as the RCCL path. Returns (jobs, expected_checksums, expected_records)."""
+    import threading
+
+    n = native()
+    records_per_map = max(1, cfg.rows_per_gpu // cfg.maps_per_rank)
+    jobs = [n.ShuffleJob(dict(
+        device=device, rank=r, world=world, maps_per_rank=cfg.maps_per_rank,
+        records_per_map=records_per_map, rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
+        d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots, d2h_streams=cfg.d2h_streams,
+        deliver_host=cfg.deliver_host, validate=cfg.validate, local_group=group)) for r in range(world)]
+    for j in jobs:
+        j.init_local()
+        j.generate()
+    local = [j.sample_keys(cfg.sample_every) for j in jobs]
+    per_dest = []
+    for d in range(world):
+        parts = [np.asarray(s[d]) for s in local if np.asarray(s[d]).size]
+        per_dest.append(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64))
+    bounds = np.ascontiguousarray(round_bounds(per_dest, cfg.rounds).reshape(-1))
+    for j in jobs:
+        j.set_bounds(bounds)
+    run_collective(jobs, lambda j: j.plan())
+    ck = [sum(j.local_dest_checksums()[d] for j in jobs) % (1 << 64) for d in range(world)]
+    rec = [sum(j.local_dest_records()[d] for j in jobs) for d in range(world)]
+    return jobs, ck, rec
+
+
+def run_collective(jobs, fn):
+    """Call fn(job) on every rank concurrently (collective operations need all ranks)."""
+    import threading
+
+    out = [None] * len(jobs)
+    err = []
+
+    def work(i):
+        try:
+            out[i] = fn(jobs[i])
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if err:
+        raise err[0]
+    return out
