@@ -470,11 +470,6 @@ void ReduceTask::merge_hybrid() {
   st_.merge_ms = ms_since(t0) - fetch_ms;
 }
 
-void ReduceTask::merge_gpu() {
-  UDA_LOG(kWarn, "GPU merge backend not available in this build path; using the CPU merge");
-  merge_online();
-}
-
 ReduceStats ReduceTask::stats() const {
   std::lock_guard<std::mutex> g(st_mu_);
   return st_;

@@ -85,6 +85,43 @@ struct PassDesc {
 void launch_merge_partition(const Elem* in, PassDesc pd, int64_t* splits, hipStream_t s);
 void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits, hipStream_t s);
 
+// GENERIC key context: record i of run r starts at bases[r] + offsets[r][i]; kind = uda::KeyKind.
+struct GenericKeyCtx {
+  uint8_t* const* bases;
+  const int64_t* const* offsets;
+  int kind;
+};
+void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits, GenericKeyCtx ctx,
+                                    hipStream_t s);
+void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
+                               GenericKeyCtx ctx, hipStream_t s);
+
+// ---------------------------------------------------------------- GENERIC record path (F1/F2/F4)
+// F1 pass 1: per run, count records and the record bytes before the EOF marker (serial VInt walk;
+// runs are walked in parallel). status[r] != 0 on a corrupt/truncated stream.
+void launch_count_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* counts,
+                          int64_t* rec_bytes, int* status, hipStream_t s);
+// F1 pass 2: offsets[r][0..n_r] = record start offsets (offsets[r][n_r] = record bytes).
+void launch_index_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* const* offsets,
+                          hipStream_t s);
+// F2: normalized elements for all records; elem_off[r] = first element of run r (nruns+1 entries).
+void launch_normalize_generic(GenericKeyCtx ctx, const int64_t* elem_off, int nruns, int64_t total, Elem* out,
+                              hipStream_t s);
+// F4: sizes[i] = size of the record elems[i] refers to.
+void launch_record_sizes(GenericKeyCtx ctx, const Elem* elems, int64_t n, int64_t* sizes, hipStream_t s);
+// Exclusive scan of n int64 (out has n+1 entries, out[n] = total); tmp >= scan_tmp_elems(n).
+int64_t scan_tmp_elems(int64_t n);
+void launch_exclusive_scan(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s);
+// F4: copy record elems[i] to out + out_off[i].
+void launch_gather_var(GenericKeyCtx ctx, const Elem* elems, int64_t n, const int64_t* out_off, uint8_t* out,
+                       hipStream_t s);
+// *out = max(v[0..n)) (zeroed first).
+void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStream_t s);
+// Delivery cut points: cuts[j] = output byte offset of the first record whose offset >= j*chunk
+// (cuts[nbuf] = total bytes), j = 0..nbuf.
+void launch_buffer_cuts(const int64_t* out_off, int64_t n, int64_t chunk, int64_t nbuf, int64_t* cuts,
+                        hipStream_t s);
+
 // ---------------------------------------------------------------- gather / serialize (F4)
 // out[i*104 .. +104) = record of elem[i] (FIXED10: run/pos encoded in elem.lo).
 void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases, uint8_t* out,

@@ -19,6 +19,8 @@
 //    records and streams them as 832 consecutive 8-byte words (13 per record), so every store
 //    instruction writes 512 contiguous bytes and every load reads whole record spans.
 #include "kernels.h"
+#include "uda/compare.h"
+#include "uda/vint.h"
 
 namespace uda {
 namespace gpu {
@@ -28,6 +30,40 @@ namespace {
 __device__ __forceinline__ bool elem_le(const Elem& a, const Elem& b) {
   return a.hi < b.hi || (a.hi == b.hi && a.lo <= b.lo);
 }
+
+// FIXED10: (hi, lo) is the whole key plus the (run, pos) tie-break.
+struct FixedCmp {
+  __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const { return elem_le(a, b); }
+};
+
+// GENERIC: hi = first 8 content bytes, lo = capped content length << 48 | run << 32 | pos.
+// Prefix ties between two keys longer than 8 bytes are settled on the raw key bytes.
+struct GenericCmp {
+  GenericKeyCtx ctx;
+  __device__ const uint8_t* content(const Elem& e, int* len) const {
+    const int run = (int)((e.lo >> 32) & 0xFFFF);
+    const uint64_t pos = e.lo & 0xFFFFFFFFull;
+    const uint8_t* rec = ctx.bases[run] + ctx.offsets[run][pos];
+    int64_t kl = 0, vl = 0;
+    const int a = vint_decode(rec, 9, &kl);
+    const int b = vint_decode(rec + a, 9, &vl);
+    const uint8_t* key = rec + a + b;
+    const int o = key_content_offset((KeyKind)ctx.kind, key, (int)kl);
+    *len = (int)kl - o;
+    return key + o;
+  }
+  __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const {
+    if (a.hi != b.hi) return a.hi < b.hi;
+    if ((a.lo >> 48) > 8 && (b.lo >> 48) > 8) {
+      int la, lb;
+      const uint8_t* pa = content(a, &la);
+      const uint8_t* pb = content(b, &lb);
+      const int c = bytes_compare(pa + 8, la - 8, pb + 8, lb - 8);
+      if (c != 0) return c < 0;
+    }
+    return a.lo <= b.lo;
+  }
+};
 
 __device__ __forceinline__ Elem ld_elem(const Elem* p) {
   const uint4 v = *reinterpret_cast<const uint4*>(p);
@@ -83,13 +119,14 @@ __global__ void __launch_bounds__(256) extract_fixed_kernel(const RunDesc* runs,
 }
 
 // ------------------------------------------------------------------------- F3: merge path
-__device__ __forceinline__ int64_t merge_path_global(const Elem* A, int64_t a_len, const Elem* B,
+template <class Cmp>
+__device__ __forceinline__ int64_t merge_path_global(const Cmp& cmp, const Elem* A, int64_t a_len, const Elem* B,
                                                      int64_t b_len, int64_t diag) {
   int64_t lo = diag > b_len ? diag - b_len : 0;
   int64_t hi = diag < a_len ? diag : a_len;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (elem_le(ld_elem(A + mid), ld_elem(B + (diag - 1 - mid))))
+    if (cmp.le(ld_elem(A + mid), ld_elem(B + (diag - 1 - mid))))
       lo = mid + 1;
     else
       hi = mid;
@@ -123,20 +160,22 @@ __device__ __forceinline__ TileGeo tile_geo(const PassDesc& pd, int t) {
   return g;
 }
 
+template <class Cmp>
 __global__ void __launch_bounds__(256) merge_partition_kernel(const Elem* in, PassDesc pd,
-                                                              int64_t* splits) {
+                                                              int64_t* splits, Cmp cmp) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= pd.ntiles) return;
   const TileGeo g = tile_geo(pd, t);
   const Elem* A = in + g.a0;
-  splits[t] = merge_path_global(A, g.a_len, A + g.a_len, g.b_len, g.d0);
+  splits[t] = merge_path_global(cmp, A, g.a_len, A + g.a_len, g.b_len, g.d0);
 }
 
 constexpr int kThreads = 256;
 constexpr int kItems = kMergeTile / kThreads;  // 8
 
+template <class Cmp>
 __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, Elem* out, PassDesc pd,
-                                                              const int64_t* splits) {
+                                                              const int64_t* splits, Cmp cmp) {
   __shared__ __attribute__((aligned(16))) Elem lds[kMergeTile];
   const int t = blockIdx.x;
   const TileGeo g = tile_geo(pd, t);
@@ -169,7 +208,7 @@ __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, El
     int hi = diag < la ? diag : la;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (elem_le(lds[mid], lds[la + diag - 1 - mid]))
+      if (cmp.le(lds[mid], lds[la + diag - 1 - mid]))
         lo = mid + 1;
       else
         hi = mid;
@@ -180,7 +219,7 @@ __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, El
     Elem eb = (ib < lb) ? lds[la + ib] : Elem{~0ull, ~0ull};
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
-      const bool take_a = (ib >= lb) || (ia < la && elem_le(ea, eb));
+      const bool take_a = (ib >= lb) || (ia < la && cmp.le(ea, eb));
       rh[k] = take_a ? ea.hi : eb.hi;
       rl[k] = take_a ? ea.lo : eb.lo;
       if (take_a) {
@@ -278,15 +317,29 @@ void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nrun
 
 void launch_merge_partition(const Elem* in, PassDesc pd, int64_t* splits, hipStream_t s) {
   if (pd.ntiles <= 0) return;
-  hipLaunchKernelGGL(merge_partition_kernel, dim3((unsigned)((pd.ntiles + 255) / 256)), dim3(256),
-                     0, s, in, pd, splits);
+  hipLaunchKernelGGL(merge_partition_kernel<FixedCmp>, dim3((unsigned)((pd.ntiles + 255) / 256)), dim3(256),
+                     0, s, in, pd, splits, FixedCmp{});
 }
 
 void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
                        hipStream_t s) {
   if (pd.ntiles <= 0) return;
-  hipLaunchKernelGGL(merge_pass_kernel, dim3((unsigned)pd.ntiles), dim3(kThreads), 0, s, in, out,
-                     pd, splits);
+  hipLaunchKernelGGL(merge_pass_kernel<FixedCmp>, dim3((unsigned)pd.ntiles), dim3(kThreads), 0, s, in, out,
+                     pd, splits, FixedCmp{});
+}
+
+void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits, GenericKeyCtx ctx,
+                                    hipStream_t s) {
+  if (pd.ntiles <= 0) return;
+  hipLaunchKernelGGL(merge_partition_kernel<GenericCmp>, dim3((unsigned)((pd.ntiles + 255) / 256)),
+                     dim3(256), 0, s, in, pd, splits, GenericCmp{ctx});
+}
+
+void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
+                               GenericKeyCtx ctx, hipStream_t s) {
+  if (pd.ntiles <= 0) return;
+  hipLaunchKernelGGL(merge_pass_kernel<GenericCmp>, dim3((unsigned)pd.ntiles), dim3(kThreads), 0, s, in,
+                     out, pd, splits, GenericCmp{ctx});
 }
 
 void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases, uint8_t* out,

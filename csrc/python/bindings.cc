@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include "device_engine.h"
+#include "generic_merger.h"
 #include "uda/aio.h"
 #include "uda/codec.h"
 #include "uda/ifile.h"
@@ -397,6 +398,43 @@ PYBIND11_MODULE(_uda_native, m) {
 
   // ---------------------------------------------------------------- GPU engine
   m.def("device_count", &gpu::device_count);
+  m.def("gpu_merge_runs", [](const std::vector<std::string>& runs, const std::string& key_class, int64_t kv_buf,
+                             int device) {
+    KeyKind kind = key_kind_from_class(key_class.c_str());
+    if (kind == KeyKind::kUnsupported) throw py::value_error("unsupported key class");
+    std::string out;
+    std::vector<int64_t> cuts;
+    int64_t records = 0;
+    int passes = 0;
+    {
+      py::gil_scoped_release rel;
+      HIP_CHECK(hipSetDevice(device));
+      int64_t total = 0;
+      for (auto& r : runs) total += (int64_t)r.size();
+      gpu::DeviceBuffer in((size_t)std::max<int64_t>(total, 16)), dout((size_t)std::max<int64_t>(total, 16));
+      hipStream_t s;
+      HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      std::vector<const uint8_t*> ptrs;
+      std::vector<int64_t> bytes;
+      int64_t off = 0;
+      for (auto& r : runs) {
+        if (!r.empty()) HIP_CHECK(hipMemcpyAsync(in.as<uint8_t>() + off, r.data(), r.size(), hipMemcpyHostToDevice, s));
+        ptrs.push_back(in.as<uint8_t>() + off);
+        bytes.push_back((int64_t)r.size());
+        off += (int64_t)r.size();
+      }
+      gpu::GenericMerger gm;
+      auto res = gm.merge(ptrs, bytes, (int)kind, dout.as<uint8_t>(), total, kv_buf, s);
+      out.resize((size_t)res.bytes);
+      if (res.bytes) HIP_CHECK(hipMemcpyAsync(&out[0], dout.as(), (size_t)res.bytes, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      HIP_CHECK(hipStreamDestroy(s));
+      cuts = res.cuts;
+      records = res.records;
+      passes = res.passes;
+    }
+    return py::make_tuple(py::bytes(out), cuts, records, passes);
+  }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
   m.def("nccl_unique_id", []() { return py::bytes(gpu::nccl_unique_id()); });
 
   py::class_<CountingSink, std::shared_ptr<CountingSink>>(m, "CountingSink")
