@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Benchmarks for the BASELINE.json configs other than the flagship (bench.py).
+
+  wordcount_loopback  uda_standalone wordcount on CPU loopback: provider + R NetMergers in one
+                      process through the UdaBridge C ABI (the JNI plumbing path), heap merge.
+  cpu_reference       in-house baseline: the reference algorithm (single-threaded heap k-way merge,
+                      write_kv_to_stream packing) on TeraSort runs on this host's CPU.
+  secondary_sort      variable-length Text keys with long common prefixes + partition skew: GPU generic
+                      merge (F1/F2/F3/F4 kernels) vs the CPU heap merge on the same runs.
+  spill               TeraSort whose map outputs live in pinned host DRAM (the spill tier used when a
+                      job exceeds HBM): rounds are streamed H2D, merged on the GPU, delivered D2H.
+
+Each prints one JSON line per result. Data is synthetic (native generators, csrc/engine/datagen.cc).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import threading
+import time
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def wordcount_loopback(args) -> dict:
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+
+    n = native()
+    maps, reducers = args.maps, args.reducers
+    rows = int(args.gb * 1e9 / maps / 17)  # ~17 B per (word, 1) IFile record
+    t0 = time.perf_counter()
+    runs = n.generate_runs("wordcount", maps, reducers, rows, 7)
+    gen_s = time.perf_counter() - t0
+    prov = UdaProvider()
+    total = 0
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        total += len(data) - 2 * len(parts)
+        prov.add_mof_memory("job_wc", f"attempt_wc_m_{m:06d}_0", data, index)
+    consumers = [UdaConsumer(maps, "job_wc", f"attempt_wc_r_{r:06d}_0", TEXT, keep_records=False)
+                 for r in range(reducers)]
+    t0 = time.perf_counter()
+    for r, c in enumerate(consumers):
+        for m in range(maps):
+            c.fetch("localhost", "job_wc", f"attempt_wc_m_{m:06d}_0", r)
+    for c in consumers:
+        c.wait(3600)
+    wall = time.perf_counter() - t0
+    stats = [c.close() for c in consumers]
+    prov.close()
+    delivered = sum(s["bytes_delivered"] for s in stats) - 2 * reducers
+    assert delivered == total, (delivered, total)
+    return {"config": "uda_standalone wordcount CPU loopback", "gb": round(total / 1e9, 3),
+            "maps": maps, "reducers": reducers, "wall_s": round(wall, 3),
+            "shuffle_merge_gbps": round(total / wall / 1e9, 3), "gen_s": round(gen_s, 1),
+            "records": sum(s["records"] for s in stats), "backend": "cpu heap merge, loopback transport"}
+
+
+def cpu_reference(args) -> dict:
+    from uda_amd import native
+    n = native()
+    rows = int(args.gb * 1e9 / 104 / args.maps)
+    runs = [p[0] for p in n.generate_runs("terasort", args.maps, 1, rows, 3)]
+    nbytes = sum(len(r) - 2 for r in runs)
+    t0 = time.perf_counter()
+    out, lens = n.cpu_merge(runs, "org.apache.hadoop.io.Text", 1 << 20)
+    dt = time.perf_counter() - t0
+    assert len(out) == nbytes + 2
+    return {"config": "reference algorithm: 1-thread heap k-way merge (CPU)", "gb": round(nbytes / 1e9, 3),
+            "runs": args.maps, "merge_s": round(dt, 3), "merge_gbps": round(nbytes / dt / 1e9, 3),
+            "buffers": len(lens)}
+
+
+def secondary_sort(args) -> dict:
+    from uda_amd import native, ops
+    n = native()
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    gen = n.generate_runs("secondary", args.maps, 2, rows, 5)
+    runs = [m[0] for m in gen]  # reducer 0 receives the skewed majority
+    nbytes = sum(len(r) - 2 for r in runs)
+    ops.merge_runs(runs[:2], "org.apache.hadoop.io.Text", "gpu")  # warm up the device
+    res = {}
+    for dev in ("gpu", "cpu"):
+        t0 = time.perf_counter()
+        body, cuts = ops.merge_runs(runs, "org.apache.hadoop.io.Text", dev)
+        dt = time.perf_counter() - t0
+        res[dev] = (dt, body)
+    assert res["gpu"][1] == res["cpu"][1], "GPU and CPU merges differ"
+    return {"config": "secondary sort: variable-length Text keys, long common prefixes, 60% skew to reducer 0",
+            "gb": round(nbytes / 1e9, 3), "runs": args.maps,
+            "gpu_s_incl_h2d_d2h": round(res["gpu"][0], 3), "cpu_heap_s": round(res["cpu"][0], 3),
+            "gpu_gbps": round(nbytes / res["gpu"][0] / 1e9, 3), "cpu_gbps": round(nbytes / res["cpu"][0] / 1e9, 3),
+            "byte_identical": True}
+
+
+def spill(args) -> dict:
+    import torch  # noqa: F401
+    from uda_amd.models.terasort import TeraSortConfig, TeraSortShuffle
+    from uda_amd.parallel.dist import DistContext
+    cfg = TeraSortConfig(rows_per_gpu=int(args.gb * 1e9 / 104), maps_per_rank=args.maps, rounds=args.rounds,
+                         store="host", validate=args.validate)
+    job = TeraSortShuffle(DistContext(), cfg, device=0)
+    job.setup()
+    job.step()
+    t0 = time.perf_counter()
+    st = job.step()
+    dt = time.perf_counter() - t0
+    job.check(st)
+    return {"config": "TeraSort with map outputs in pinned host DRAM (spill tier), 1 GPU",
+            "gb": round(st["bytes_in"] / 1e9, 3), "wall_s": round(dt, 3),
+            "shuffle_merge_gbps": round(st["bytes_in"] / dt / 1e9, 3),
+            "breakdown_ms": {k: round(st[k], 1) for k in ("comm_ms", "merge_ms", "d2h_ms")}}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill"])
+    ap.add_argument("--gb", type=float, default=1.0)
+    ap.add_argument("--maps", type=int, default=16)
+    ap.add_argument("--reducers", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--validate", action="store_true")
+    a = ap.parse_args()
+    fn = globals()[a.config]
+    out = fn(a)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -275,16 +275,33 @@ void ShuffleJob::generate() {
   }
   mof_off_[M] = off;
   store_bytes_ = off;
-  store_.alloc((size_t)store_bytes_);
+  if (host_store()) {
+    hstore_.alloc((size_t)store_bytes_);
+    store_base_ = hstore_.as<uint8_t>();
+    void* dp = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&dp, store_base_, 0));
+    store_dev_base_ = reinterpret_cast<uint8_t*>(dp);
+  } else if (cfg_.store == "hbm") {
+    store_.alloc((size_t)store_bytes_);
+    store_base_ = store_dev_base_ = store_.as<uint8_t>();
+  } else {
+    throw std::runtime_error("unknown store tier " + cfg_.store);
+  }
 
-  std::vector<uint8_t*> bases(nruns);
+  std::vector<uint8_t*> bases(nruns), gen_bases(nruns);
   std::vector<uint64_t> key_lo(nruns), key_span(nruns), seeds(nruns);
   const uint64_t step = (W == 1) ? ~0ull : (~0ull / (uint64_t)W);
-  int64_t max_n = 0;
+  int64_t max_n = 0, max_mof = 0;
+  DeviceBuffer tmp;  // host tier: one MOF at a time is generated in HBM, then copied out
+  if (host_store()) {
+    for (int m = 0; m < M; ++m) max_mof = std::max(max_mof, mof_off_[m + 1] - mof_off_[m]);
+    tmp.alloc((size_t)max_mof);
+  }
   for (int m = 0; m < M; ++m)
     for (int d = 0; d < W; ++d) {
       const int r = m * W + d;
-      bases[r] = store_.as<uint8_t>() + run_off_[r];
+      bases[r] = store_dev_base_ + run_off_[r];
+      gen_bases[r] = host_store() ? tmp.as<uint8_t>() + (run_off_[r] - mof_off_[m]) : bases[r];
       key_lo[r] = step * (uint64_t)d;
       key_span[r] = step;
       const uint64_t gmap = (uint64_t)cfg_.rank * M + m;
@@ -293,16 +310,28 @@ void ShuffleJob::generate() {
     }
   DeviceBuffer d_b(nruns * sizeof(uint8_t*)), d_n(nruns * 8), d_lo(nruns * 8), d_sp(nruns * 8),
       d_sd(nruns * 8), d_ck(nruns * 8);
-  HIP_CHECK(hipMemcpy(d_b.as(), bases.data(), nruns * sizeof(uint8_t*), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(d_b.as(), gen_bases.data(), nruns * sizeof(uint8_t*), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_n.as(), run_nrec_.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_lo.as(), key_lo.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sp.as(), key_span.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sd.as(), seeds.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemset(d_ck.as(), 0, nruns * 8));
-  launch_teragen(d_b.as<uint8_t*>(), d_n.as<int64_t>(), d_lo.as<uint64_t>(), d_sp.as<uint64_t>(),
-                 d_sd.as<uint64_t>(), nruns, max_n, d_ck.as<unsigned long long>(), s_compute_);
-  HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipStreamSynchronize(s_compute_));
+  if (!host_store()) {
+    launch_teragen(d_b.as<uint8_t*>(), d_n.as<int64_t>(), d_lo.as<uint64_t>(), d_sp.as<uint64_t>(),
+                   d_sd.as<uint64_t>(), nruns, max_n, d_ck.as<unsigned long long>(), s_compute_);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(s_compute_));
+  } else {
+    for (int m = 0; m < M; ++m) {
+      launch_teragen(d_b.as<uint8_t*>() + m * W, d_n.as<int64_t>() + m * W, d_lo.as<uint64_t>() + m * W,
+                     d_sp.as<uint64_t>() + m * W, d_sd.as<uint64_t>() + m * W, W, max_n,
+                     d_ck.as<unsigned long long>() + m * W, s_compute_);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpyAsync(store_base_ + mof_off_[m], tmp.as(), (size_t)(mof_off_[m + 1] - mof_off_[m]),
+                               hipMemcpyDeviceToHost, s_compute_));
+    }
+    HIP_CHECK(hipStreamSynchronize(s_compute_));
+  }
   std::vector<uint64_t> ck(nruns);
   HIP_CHECK(hipMemcpy(ck.data(), d_ck.as(), nruns * 8, hipMemcpyDeviceToHost));
   dest_checksum_.assign(W, 0);
@@ -321,7 +350,8 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(d_run_bases_.as(), bases.data(), nruns * sizeof(uint8_t*), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_run_nrec_.as(), run_nrec_.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_bound_set_.as(), bset.data(), nruns * sizeof(int), hipMemcpyHostToDevice));
-  UDA_LOG(kInfo, "rank %d generated %d MOFs, %ld bytes in HBM", cfg_.rank, M, (long)store_bytes_);
+  UDA_LOG(kInfo, "rank %d generated %d MOFs, %ld bytes in %s", cfg_.rank, M, (long)store_bytes_,
+          host_store() ? "pinned host DRAM" : "HBM");
 }
 
 std::vector<int64_t> ShuffleJob::index_record(int m, int d) const {
@@ -335,8 +365,8 @@ std::vector<int64_t> ShuffleJob::index_record(int m, int d) const {
 std::vector<uint8_t> ShuffleJob::read_partition(int m, int d) const {
   auto ir = index_record(m, d);
   std::vector<uint8_t> out((size_t)ir[2]);
-  HIP_CHECK(hipMemcpy(out.data(), store_.as<uint8_t>() + mof_off_[m] + ir[0], out.size(),
-                      hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(out.data(), store_base_ + mof_off_[m] + ir[0], out.size(),
+                      host_store() ? hipMemcpyHostToHost : hipMemcpyDeviceToHost));
   return out;
 }
 
@@ -442,9 +472,17 @@ void ShuffleJob::plan() {
   recv_slots_.clear();
   out_slots_.resize(kSlots);
   for (auto& b : out_slots_) b.alloc(slot_bytes);
-  if (W > 1) {
+  if (W > 1 || host_store()) {
     recv_slots_.resize(kSlots);
     for (auto& b : recv_slots_) b.alloc(slot_bytes);
+    desc_slots_.resize(4);
+    for (auto& d : desc_slots_) {
+      d.host.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
+      d.dev.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
+      HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
+    }
+  }
+  if (W > 1) {
     max_send_bytes_ = 0;
     for (const auto& rp : plans_) {
       int64_t sb = 0;
@@ -456,12 +494,6 @@ void ShuffleJob::plan() {
     pack_slots_.clear();
     pack_slots_.resize(kSlots);
     for (auto& b : pack_slots_) b.alloc((size_t)std::max<int64_t>(max_send_bytes_, 16));
-    desc_slots_.resize(4);
-    for (auto& d : desc_slots_) {
-      d.host.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
-      d.dev.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
-      HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
-    }
   }
   d_validate_.alloc(256);
   if (cfg_.deliver_host && pinned_.size() == 0) {
@@ -645,7 +677,7 @@ StepStats ShuffleJob::run_step() {
     const int slot = q % kSlots;
     const RoundPlan& rp = plans[q];
     std::vector<RunDesc> runs;
-    if (W == 1) {
+    if (W == 1 && !host_store()) {
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_compute_));
       HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_compute_));
       for (int m = 0; m < M; ++m) {
@@ -658,7 +690,7 @@ StepStats ShuffleJob::run_step() {
       }
     } else {
       uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
-      uint8_t* pbuf = pack_slots_[slot].as<uint8_t>();
+      uint8_t* pbuf = W > 1 ? pack_slots_[slot].as<uint8_t>() : nullptr;
       if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged[slot], 0));
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
       std::vector<int64_t> roff((size_t)W * M + 1, 0);
@@ -700,12 +732,22 @@ StepStats ShuffleJob::run_step() {
         rb[s] = roff[(s + 1) * M] - roff[s * M];
       }
       bytes_sent += packed;
-      if (nd > 0) {
+      if (nd > 0 && !host_store()) {
         HIP_CHECK(hipMemcpyAsync(ds.dev.as(), descs, sizeof(CopyDesc) * nd, hipMemcpyHostToDevice, s_comm_));
         HIP_CHECK(hipEventRecord(ds.uploaded, s_comm_));
         launch_batched_copy(ds.dev.as<CopyDesc>(), nd, max_bytes, s_comm_);
+      } else if (nd > 0) {
+        // spill tier: the slices stream H2D over PCIe (SDMA) straight into the pack / receive slots
+        for (int i = 0; i < nd; ++i)
+          HIP_CHECK(hipMemcpyAsync(descs[i].dst, descs[i].src, (size_t)descs[i].bytes, hipMemcpyHostToDevice, s_comm_));
+        HIP_CHECK(hipEventRecord(ds.uploaded, s_comm_));
+        st.bytes_h2d += [&] {
+          int64_t b = 0;
+          for (int i = 0; i < nd; ++i) b += descs[i].bytes;
+          return b;
+        }();
       }
-      exchange_->alltoallv(pbuf, sb.data(), sd.data(), rbuf, rb.data(), rd.data(), s_comm_);
+      if (W > 1) exchange_->alltoallv(pbuf, sb.data(), sd.data(), rbuf, rb.data(), rd.data(), s_comm_);
       HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
       HIP_CHECK(hipEventRecord(comm_done[slot], s_comm_));
       HIP_CHECK(hipStreamWaitEvent(s_compute_, comm_done[slot], 0));

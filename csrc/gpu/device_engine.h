@@ -146,6 +146,7 @@ struct ShuffleConfig {
   bool deliver_host = true;              // false: stop after the device merge (ablation)
   bool validate = false;                 // device-side order + checksum check per round
   std::string local_group;               // world > 1 without RCCL: ranks are threads of one process
+  std::string store = "hbm";             // map-output store: "hbm" or "host" (pinned DRAM spill tier)
 };
 
 struct StepStats {
@@ -157,6 +158,7 @@ struct StepStats {
   int64_t bytes_in = 0;        // partition bytes delivered to this reducer (records only)
   int64_t records = 0;
   int64_t bytes_sent = 0;      // bytes this rank sent to peers (excl. self)
+  int64_t bytes_h2d = 0;       // spill tier: bytes streamed host -> device
   int64_t buffers = 0;         // sink invocations
   int merge_passes = 0;
   int64_t order_errors = -1;   // validate only
@@ -208,13 +210,19 @@ class ShuffleJob {
   void compute_round_plans(std::vector<RoundPlan>* plans, double* ms);
   void deliver_loop();
   void copy_loop();
-  uint8_t* run_base(int m, int d) const { return store_.as<uint8_t>() + run_off_[m * cfg_.world + d]; }
+  // Host-visible address of a run (device address for the HBM store, host address for the host
+  // tier); kernels use the device-mapped addresses in d_run_bases_.
+  uint8_t* run_base(int m, int d) const { return store_base_ + run_off_[m * cfg_.world + d]; }
+  bool host_store() const { return cfg_.store == "host"; }
 
   ShuffleConfig cfg_;
   std::unique_ptr<Exchange> exchange_;
   hipStream_t s_comm_ = nullptr, s_compute_ = nullptr;
   std::vector<hipStream_t> s_copy_;
   DeviceBuffer store_;
+  PinnedBuffer hstore_;
+  uint8_t* store_base_ = nullptr;      // where run_base() points
+  uint8_t* store_dev_base_ = nullptr;  // device-accessible alias for kernels
   int64_t store_bytes_ = 0;
   std::vector<int64_t> mof_off_, run_off_, run_nrec_;  // run index m*W + d
   std::vector<uint64_t> dest_checksum_;

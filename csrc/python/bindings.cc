@@ -15,6 +15,7 @@
 #include "generic_merger.h"
 #include "uda/aio.h"
 #include "uda/codec.h"
+#include "uda/datagen.h"
 #include "uda/ifile.h"
 #include "uda/uda_bridge.h"
 #include "uda/cmd.h"
@@ -37,6 +38,7 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   d["bytes_in"] = s.bytes_in;
   d["records"] = s.records;
   d["bytes_sent"] = s.bytes_sent;
+  d["bytes_h2d"] = s.bytes_h2d;
   d["buffers"] = s.buffers;
   d["merge_passes"] = s.merge_passes;
   d["order_errors"] = s.order_errors;
@@ -64,6 +66,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("deliver_host", c.deliver_host);
   get("validate", c.validate);
   get("local_group", c.local_group);
+  get("store", c.store);
   return c;
 }
 
@@ -297,13 +300,25 @@ PYBIND11_MODULE(_uda_native, m) {
     return py::bytes(out);
   });
 
+  m.def("generate_runs", [](const std::string& kind, int maps, int reducers, int64_t rows, uint64_t seed) {
+    std::vector<std::vector<std::vector<uint8_t>>> r;
+    {
+      py::gil_scoped_release g;
+      r = generate_runs(kind, maps, reducers, rows, seed);
+    }
+    py::list out;
+    for (auto& m : r) {
+      py::list parts;
+      for (auto& p : m) parts.append(py::bytes((const char*)p.data(), p.size()));
+      out.append(parts);
+    }
+    return out;
+  });
+
   // ---------------------------------------------------------------- CPU engine
   m.def("cpu_merge", [](const std::vector<std::string>& runs, const std::string& key_class, int64_t buf) {
     std::vector<int64_t> lens;
-    py::bytes out;
-    {
-      out = cpu_merge_impl(runs, key_class, buf, &lens);
-    }
+    py::bytes out = cpu_merge_impl(runs, key_class, buf, &lens);
     return py::make_tuple(out, lens);
   });
 

@@ -95,3 +95,28 @@ def test_multirank_schedule_local_group(require_gpu, world, maps, rounds):
                 assert readers[d].records == expect
                 readers[d] = J2CQueueReader(max_len=64 << 10)
                 jobs[d].set_python_sink(readers[d].feed)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_host_dram_spill_tier(require_gpu, world):
+    """Map outputs in pinned host DRAM (jobs larger than HBM): rounds stream H2D, then merge."""
+    from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
+    cfg = TeraSortConfig(rows_per_gpu=40000, maps_per_rank=4, rounds=3, validate=True, sample_every=64,
+                         kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10, store="host")
+    if world == 1:
+        j = _job(40000, 4, 3, store="host", kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
+        reader = J2CQueueReader(max_len=64 << 10)
+        j.job.set_python_sink(reader.feed)
+        st = j.step()
+        j.check(st)
+        assert st["bytes_h2d"] == st["bytes_in"]
+        recs = []
+        for m in range(4):
+            recs += decode_stream(j.job.read_partition(m, 0))
+        assert reader.records == sorted(recs, key=lambda kv: _text_content(kv[0]))
+    else:
+        jobs, ck, rec = make_local_group(world, cfg, group="spill2")
+        stats = run_collective(jobs, lambda j: j.run_step())
+        for d, st in enumerate(stats):
+            assert st["records"] == rec[d] and st["order_errors"] == 0 and st["checksum"] == ck[d]
+            assert st["bytes_h2d"] > 0

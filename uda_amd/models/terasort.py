@@ -40,6 +40,7 @@ class TeraSortConfig:
     deliver_host: bool = True
     validate: bool = False
     sample_every: int = 4096
+    store: str = "hbm"                  # "hbm" or "host" (pinned-DRAM spill tier for jobs > HBM)
 
 
 class TeraSortShuffle:
@@ -55,7 +56,8 @@ class TeraSortShuffle:
             maps_per_rank=cfg.maps_per_rank, records_per_map=records_per_map,
             rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
             d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
-            d2h_streams=cfg.d2h_streams, deliver_host=cfg.deliver_host, validate=cfg.validate))
+            d2h_streams=cfg.d2h_streams, deliver_host=cfg.deliver_host, validate=cfg.validate,
+            store=cfg.store))
         self.sink = n.CountingSink()
         self.expected_checksum = None
         self.expected_records = None
@@ -118,7 +120,8 @@ def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: st
         device=device, rank=r, world=world, maps_per_rank=cfg.maps_per_rank,
         records_per_map=records_per_map, rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
         d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots, d2h_streams=cfg.d2h_streams,
-        deliver_host=cfg.deliver_host, validate=cfg.validate, local_group=group)) for r in range(world)]
+        deliver_host=cfg.deliver_host, validate=cfg.validate, local_group=group, store=cfg.store))
+        for r in range(world)]
     for j in jobs:
         j.init_local()
         j.generate()
