@@ -90,11 +90,14 @@ def secondary_sort(args) -> dict:
         body, cuts = ops.merge_runs(runs, "org.apache.hadoop.io.Text", dev)
         dt = time.perf_counter() - t0
         res[dev] = (dt, body)
+        if dev == "gpu":
+            dev_ms = ops.last_stats["merge_ms"]
     assert res["gpu"][1] == res["cpu"][1], "GPU and CPU merges differ"
     return {"config": "secondary sort: variable-length Text keys, long common prefixes, 60% skew to reducer 0",
             "gb": round(nbytes / 1e9, 3), "runs": args.maps,
             "gpu_s_incl_h2d_d2h": round(res["gpu"][0], 3), "cpu_heap_s": round(res["cpu"][0], 3),
             "gpu_gbps": round(nbytes / res["gpu"][0] / 1e9, 3), "cpu_gbps": round(nbytes / res["cpu"][0] / 1e9, 3),
+            "gpu_device_merge_ms": round(dev_ms, 1), "gpu_device_merge_gbps": round(nbytes / dev_ms / 1e6, 2),
             "byte_identical": True}
 
 

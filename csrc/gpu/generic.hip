@@ -19,52 +19,212 @@ namespace gpu {
 
 namespace {
 
-// Walk one run; returns record count and writes record bytes (offset of the EOF marker or end).
-__device__ int64_t walk_run(const uint8_t* p, int64_t n, int64_t* offsets, int64_t* rec_bytes, int* status) {
-  int64_t pos = 0, cnt = 0;
-  *status = 0;
-  while (pos < n) {
-    int64_t kl = 0, vl = 0;
-    const int a = vint_decode(p + pos, (size_t)(n - pos), &kl);
-    if (a == 0) {
-      *status = 1;
-      break;
-    }
-    const int b = vint_decode(p + pos + a, (size_t)(n - pos - a), &vl);
-    if (b == 0) {
-      *status = 1;
-      break;
-    }
-    if (kl == -1 && vl == -1) break;  // EOF marker
-    if (kl < 0 || vl < 0 || pos + a + b + kl + vl > n) {
-      *status = 2;
-      break;
-    }
-    if (offsets) offsets[cnt] = pos;
-    pos += a + b + kl + vl;
-    ++cnt;
+// F1 in two passes.
+//  pass 1 (one wave per run, serial along the run): the run streams through LDS in 4 KiB chunks
+//    (the next chunk is fetched into registers while the current one is walked); lane 0 follows
+//    the record chain decoding the two VInt headers from LDS and leaves a checkpoint per chunk:
+//    the offset of the first record starting in the chunk and the number of records starting in it.
+//  pass 2 (one wave per chunk, all chunks of all runs in parallel): each chunk is staged in LDS
+//    again and re-walked from its checkpoint, writing the record offsets.
+constexpr int kF1Chunk = 4096;
+constexpr int kF1Halo = 32;
+constexpr int kF1Lanes = 64;
+constexpr int kF1Bytes = kF1Chunk / kF1Lanes;  // 64 bytes per lane
+
+__device__ __forceinline__ int lds_vint(const uint8_t* b, int p, int lim, int64_t* v) {
+  if (p >= lim) return 0;
+  const int8_t f = (int8_t)b[p];
+  if (f >= -112) {
+    *v = f;
+    return 1;
   }
-  if (offsets) offsets[cnt] = pos;
-  *rec_bytes = pos;
-  return cnt;
+  const bool neg = f < -120;
+  const int n = neg ? (-120 - f) : (-112 - f);
+  if (p + 1 + n > lim) return 0;
+  int64_t t = 0;
+  for (int i = 0; i < n; ++i) t = (t << 8) | b[p + 1 + i];
+  if (neg) t ^= -1ll;
+  *v = t;
+  return n + 1;
 }
 
-__global__ void count_records_kernel(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* counts,
-                                     int64_t* rec_bytes, int* status) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nruns) return;
-  int st = 0;
-  counts[r] = walk_run(bases[r], nbytes[r], nullptr, rec_bytes + r, &st);
-  status[r] = st;
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
 }
 
-__global__ void index_records_kernel(uint8_t* const* bases, const int64_t* nbytes, int nruns,
-                                     int64_t* const* offsets) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nruns) return;
+// Load bytes [at, at+64) of a run (zero beyond n) into registers.
+__device__ __forceinline__ void f1_fetch64(const uint8_t* p, int64_t n, int64_t at, uint32_t (&w)[16]) {
+  if (at + 64 <= n && (((uintptr_t)(p + at)) & 15) == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + at);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = q[k];
+      w[4 * k] = v.x;
+      w[4 * k + 1] = v.y;
+      w[4 * k + 2] = v.z;
+      w[4 * k + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t i = at + 4 * k + b;
+        x |= (uint32_t)(i < n ? p[i] : 0) << (8 * b);
+      }
+      w[k] = x;
+    }
+  }
+}
+
+__device__ __forceinline__ void f1_stage(uint8_t* buf, int lane, const uint32_t (&w)[16]) {
+  uint32_t* d = reinterpret_cast<uint32_t*>(buf + lane * kF1Bytes);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) d[k] = w[k];
+}
+
+// Decode the record at LDS position i; returns its size, 0 for EOF, -1 for corrupt/truncated.
+// Fast path: both VInt headers are single bytes (lengths < 128, the common case); the two header
+// bytes come from two independent aligned dword reads instead of two dependent byte reads.
+__device__ __forceinline__ int64_t f1_record(const uint8_t* buf, int i, int lim, int64_t remain) {
+  if (i + 2 <= lim) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (i & ~3));
+    const uint64_t two = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    const int sh = (i & 3) * 8;
+    const int8_t b0 = (int8_t)(two >> sh), b1 = (int8_t)(two >> (sh + 8));
+    if (b0 >= 0 && b1 >= 0) {
+      const int64_t sz = 2 + (int64_t)b0 + (int64_t)b1;
+      return sz > remain ? -1 : sz;
+    }
+  }
+  int64_t kl = 0, vl = 0;
+  const int a = lds_vint(buf, i, lim, &kl);
+  const int b = a ? lds_vint(buf, i + a, lim, &vl) : 0;
+  if (a == 0 || b == 0) return -1;
+  if (kl == -1 && vl == -1) return 0;
+  if (kl < 0 || vl < 0) return -1;
+  const int64_t sz = a + b + kl + vl;
+  return sz > remain ? -1 : sz;
+}
+
+template <bool kProf>
+__global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases, const int64_t* nbytes,
+                                                           const int64_t* chunk_base, int64_t* ck_start,
+                                                           int64_t* ck_count, int64_t* counts, int64_t* rec_bytes,
+                                                           int* status, uint64_t* prof) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kF1Chunk + 64];
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  const uint8_t* p = bases[r];
+  const int64_t n = nbytes[r];
+  const int64_t cb = chunk_base[r];
+  uint32_t cur[16], nxt[16];
+  f1_fetch64(p, n, (int64_t)lane * kF1Bytes, cur);
+  int64_t pos = 0, cnt = 0;
   int st = 0;
-  int64_t rb = 0;
-  walk_run(bases[r], nbytes[r], offsets[r], &rb, &st);
+  bool done = false;
+  uint64_t t_stage = 0, t_walk = 0, t0 = 0;
+  int64_t c = 0;
+  for (int64_t c0 = 0; c0 < n && !done; c0 += kF1Chunk, ++c) {
+    if (kProf) t0 = stamp();
+    f1_fetch64(p, n, c0 + kF1Chunk + (int64_t)lane * kF1Bytes, nxt);  // prefetch
+    f1_stage(buf, lane, cur);
+    if (lane == 0) {  // halo: the first bytes of the next chunk
+      uint32_t* h = reinterpret_cast<uint32_t*>(buf + kF1Chunk);
+#pragma unroll
+      for (int k = 0; k < kF1Halo / 4; ++k) h[k] = nxt[k];
+    }
+    __syncthreads();
+    if (kProf) {
+      const uint64_t t1 = stamp();
+      t_stage += t1 - t0;
+      t0 = t1;
+    }
+    if (lane == 0) {
+      const int lim = (int)((n - c0) < (int64_t)(kF1Chunk + kF1Halo) ? (n - c0) : (kF1Chunk + kF1Halo));
+      const int64_t end = c0 + (lim < kF1Chunk ? lim : kF1Chunk);
+      int64_t here = 0;
+      ck_start[cb + c] = pos;  // first record at or after c0 (or the end)
+      while (pos < end) {
+        const int64_t sz = f1_record(buf, (int)(pos - c0), lim, n - pos);
+        if (sz <= 0) {
+          if (sz < 0) st = 1;
+          done = true;
+          break;
+        }
+        pos += sz;
+        ++here;
+      }
+      ck_count[cb + c] = here;
+      cnt += here;
+    }
+    done = __shfl(done ? 1 : 0, 0, 64) != 0;
+    if (kProf) t_walk += stamp() - t0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cur[k] = nxt[k];
+  }
+  if (lane == 0) {
+    // chunks after an early EOF carry no records
+    const int64_t nchunks = (n + kF1Chunk - 1) / kF1Chunk;
+    for (int64_t k = c; k < nchunks; ++k) {
+      ck_start[cb + k] = pos;
+      ck_count[cb + k] = 0;
+    }
+    counts[r] = cnt;
+    rec_bytes[r] = pos;
+    status[r] = st;
+    if (kProf) {
+      prof[2 * r] = t_stage;
+      prof[2 * r + 1] = t_walk;
+    }
+  }
+}
+
+// Pass 2: one wave per chunk; ck_ord[c] = global ordinal of the chunk's first record (exclusive
+// scan of ck_count); chunk_run[c] = its run. Writes offsets[run][ord - run_first] for its records.
+__global__ void __launch_bounds__(kF1Lanes) f1_index_kernel(uint8_t* const* bases, const int64_t* nbytes,
+                                                            const int64_t* chunk_base, const int32_t* chunk_run,
+                                                            const int64_t* ck_start, const int64_t* ck_count,
+                                                            const int64_t* ck_ord, const int64_t* elem_off,
+                                                            const int64_t* rec_bytes, int64_t* const* offsets,
+                                                            int64_t total_chunks) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kF1Chunk + 2 * 64];
+  const int64_t c = blockIdx.x;
+  if (c >= total_chunks) return;
+  const int64_t here = ck_count[c];
+  const int r = chunk_run[c];
+  const int64_t n = nbytes[r];
+  const uint8_t* p = bases[r];
+  const int64_t c0 = (c - chunk_base[r]) * kF1Chunk;
+  const int lane = threadIdx.x;
+  if (here > 0) {
+    uint32_t w[16];
+    f1_fetch64(p, n, c0 + (int64_t)lane * kF1Bytes, w);
+    f1_stage(buf, lane, w);
+    if (lane == 0) {
+      uint32_t h[16];
+      f1_fetch64(p, n, c0 + kF1Chunk, h);
+      uint32_t* d = reinterpret_cast<uint32_t*>(buf + kF1Chunk);
+#pragma unroll
+      for (int k = 0; k < kF1Halo / 4; ++k) d[k] = h[k];
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const int lim = (int)((n - c0) < (int64_t)(kF1Chunk + kF1Halo) ? (n - c0) : (kF1Chunk + kF1Halo));
+      int64_t* out = offsets[r] + (ck_ord[c] - elem_off[r]);
+      int64_t pos = ck_start[c];
+      for (int64_t i = 0; i < here; ++i) {
+        out[i] = pos;
+        pos += f1_record(buf, (int)(pos - c0), lim, n - pos);
+      }
+    }
+  }
+  // the first chunk of a run writes the run's terminating offset (record bytes from pass 1)
+  if (c == chunk_base[r] && lane == 0) offsets[r][elem_off[r + 1] - elem_off[r]] = rec_bytes[r];
 }
 
 __device__ __forceinline__ int find_run(const int64_t* elem_off, int nruns, int64_t g) {
@@ -95,18 +255,19 @@ __global__ void __launch_bounds__(256) normalize_kernel(GenericKeyCtx ctx, const
   Elem e;
   e.hi = load_be_prefix(key + o, cl);
   const uint64_t capped = cl > 0xFFFF ? 0xFFFF : (uint64_t)cl;
-  e.lo = (capped << 48) | ((uint64_t)r << 32) | (uint64_t)pos;
+  e.lo = (capped << 48) | (uint64_t)g;
   out[g] = e;
+  ctx.keyptr[g] = key + o;
+  ctx.keylen[g] = cl;
+  ctx.recptr[g] = rec;
+  ctx.reclen[g] = (int32_t)(ctx.offsets[r][pos + 1] - ctx.offsets[r][pos]);
 }
 
 __global__ void __launch_bounds__(256) record_sizes_kernel(GenericKeyCtx ctx, const Elem* elems, int64_t n,
                                                            int64_t* sizes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Elem e = elems[i];
-  const int r = (int)((e.lo >> 32) & 0xFFFF);
-  const uint64_t pos = e.lo & 0xFFFFFFFFull;
-  sizes[i] = ctx.offsets[r][pos + 1] - ctx.offsets[r][pos];
+  sizes[i] = ctx.reclen[elems[i].lo & 0xFFFFFFFFFFFFull];
 }
 
 // ---- exclusive scan: per-block reduce, scan of block sums (one block), add-back
@@ -198,12 +359,9 @@ __global__ void __launch_bounds__(256) gather_var_kernel(GenericKeyCtx ctx, cons
   unsigned long long src = 0;
   long long len = 0, dst = 0;
   if (lane < valid) {
-    const Elem e = elems[rec0 + lane];
-    const int r = (int)((e.lo >> 32) & 0xFFFF);
-    const uint64_t pos = e.lo & 0xFFFFFFFFull;
-    const int64_t o = ctx.offsets[r][pos];
-    src = (unsigned long long)(ctx.bases[r] + o);
-    len = ctx.offsets[r][pos + 1] - o;
+    const uint64_t g = elems[rec0 + lane].lo & 0xFFFFFFFFFFFFull;
+    src = (unsigned long long)ctx.recptr[g];
+    len = ctx.reclen[g];
     dst = out_off[rec0 + lane];
   }
   for (int r = 0; r < valid; ++r) {
@@ -249,19 +407,28 @@ void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStr
   hipLaunchKernelGGL(max_kernel, dim3((unsigned)blocks), dim3(256), 0, s, v, n, out);
 }
 
-void launch_count_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* counts,
-                          int64_t* rec_bytes, int* status, hipStream_t s) {
+void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
+                    int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
+                    hipStream_t s, uint64_t* prof) {
   if (nruns <= 0) return;
-  hipLaunchKernelGGL(count_records_kernel, dim3((unsigned)((nruns + 63) / 64)), dim3(64), 0, s, bases, nbytes,
-                     nruns, counts, rec_bytes, status);
+  if (prof)
+    hipLaunchKernelGGL(f1_scan_kernel<true>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes, chunk_base,
+                       ck_start, ck_count, counts, rec_bytes, status, prof);
+  else
+    hipLaunchKernelGGL(f1_scan_kernel<false>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes,
+                       chunk_base, ck_start, ck_count, counts, rec_bytes, status, prof);
 }
 
-void launch_index_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* const* offsets,
-                          hipStream_t s) {
-  if (nruns <= 0) return;
-  hipLaunchKernelGGL(index_records_kernel, dim3((unsigned)((nruns + 63) / 64)), dim3(64), 0, s, bases, nbytes,
-                     nruns, offsets);
+void launch_f1_index(uint8_t* const* bases, const int64_t* nbytes, const int64_t* chunk_base,
+                     const int32_t* chunk_run, const int64_t* ck_start, const int64_t* ck_count,
+                     const int64_t* ck_ord, const int64_t* elem_off, const int64_t* rec_bytes,
+                     int64_t* const* offsets, int64_t total_chunks, hipStream_t s) {
+  if (total_chunks <= 0) return;
+  hipLaunchKernelGGL(f1_index_kernel, dim3((unsigned)total_chunks), dim3(kF1Lanes), 0, s, bases, nbytes, chunk_base,
+                     chunk_run, ck_start, ck_count, ck_ord, elem_off, rec_bytes, offsets, total_chunks);
 }
+
+int64_t f1_chunk_bytes() { return kF1Chunk; }
 
 void launch_normalize_generic(GenericKeyCtx ctx, const int64_t* elem_off, int nruns, int64_t total, Elem* out,
                               hipStream_t s) {

@@ -1,6 +1,8 @@
 #include "generic_merger.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace uda {
@@ -16,6 +18,7 @@ void GenericMerger::reserve(int64_t records, int runs) {
   sizes_.alloc((size_t)records * 8);
   out_off_.alloc((size_t)(std::max<int64_t>(records, runs) + 1) * 8);  // also holds elem_off (runs+1)
   scan_tmp_.alloc((size_t)scan_tmp_elems(records) * 8);
+  side_.alloc((size_t)records * 24);  // keyptr(8) recptr(8) keylen(4) reclen(4)
   cap_records_ = records;
   cap_runs_ = std::max(runs, cap_runs_);
 }
@@ -28,7 +31,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     res.cuts = {0};
     return res;
   }
-  if (K > 65536) throw std::runtime_error("GenericMerger: at most 65536 runs");
+  if (K > (1 << 20)) throw std::runtime_error("GenericMerger: too many runs");
   // ---- per-run tables: bases | nbytes | counts | rec_bytes | status | offsets pointers
   const size_t tb = (size_t)K * (8 * 5 + 8) + 256;
   if (tables_.size() < tb) tables_.alloc(tb);
@@ -41,8 +44,41 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   auto* d_status = reinterpret_cast<int*>(t + 40 * K);
   HIP_CHECK(hipMemcpyAsync(d_bases, runs.data(), 8 * K, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(d_nbytes, run_bytes.data(), 8 * K, hipMemcpyHostToDevice, s));
-  // ---- F1 pass 1: count
-  launch_count_records(d_bases, d_nbytes, K, d_counts, d_recb, d_status, s);
+  // ---- F1 pass 1: chain walk per run with 4 KiB checkpoints
+  const int64_t CH = f1_chunk_bytes();
+  std::vector<int64_t> chunk_base(K + 1, 0);
+  for (int k = 0; k < K; ++k) chunk_base[k + 1] = chunk_base[k] + (run_bytes[k] + CH - 1) / CH;
+  const int64_t nchunks = chunk_base[K];
+  std::vector<int32_t> chunk_run((size_t)std::max<int64_t>(nchunks, 1));
+  for (int k = 0; k < K; ++k)
+    for (int64_t c = chunk_base[k]; c < chunk_base[k + 1]; ++c) chunk_run[(size_t)c] = k;
+  const size_t ckb = (size_t)(K + 1) * 8 + (size_t)(std::max<int64_t>(nchunks, 1) + 1) * (8 + 8 + 8 + 4) + 64;
+  if (ck_.size() < ckb) ck_.alloc(ckb);
+  int64_t* d_cbase = ck_.as<int64_t>();
+  int64_t* d_ckstart = d_cbase + (K + 1);
+  int64_t* d_ckcount = d_ckstart + std::max<int64_t>(nchunks, 1);
+  int64_t* d_ckord = d_ckcount + std::max<int64_t>(nchunks, 1);
+  int32_t* d_crun = reinterpret_cast<int32_t*>(d_ckord + std::max<int64_t>(nchunks, 1) + 1);  // scan writes n+1
+  HIP_CHECK(hipMemcpyAsync(d_cbase, chunk_base.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
+  if (nchunks > 0)
+    HIP_CHECK(hipMemcpyAsync(d_crun, chunk_run.data(), 4 * (size_t)nchunks, hipMemcpyHostToDevice, s));
+  static const bool prof_f1 = std::getenv("UDA_F1_PROFILE") != nullptr;
+  DeviceBuffer d_prof;
+  if (prof_f1) d_prof.alloc((size_t)K * 16);
+  launch_f1_scan(d_bases, d_nbytes, K, d_cbase, d_ckstart, d_ckcount, d_counts, d_recb, d_status, s,
+                 prof_f1 ? d_prof.as<uint64_t>() : nullptr);
+  if (prof_f1) {
+    std::vector<uint64_t> pr((size_t)K * 2);
+    HIP_CHECK(hipMemcpyAsync(pr.data(), d_prof.as(), 16 * K, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    uint64_t a = 0, b = 0;
+    for (int k = 0; k < K; ++k) {
+      a += pr[2 * k];
+      b += pr[2 * k + 1];
+    }
+    fprintf(stderr, "[F1 profile] runs=%d mean cycles per run: stage=%.0f walk=%.0f\n", K, (double)a / K,
+            (double)b / K);
+  }
   std::vector<int64_t> counts(K), recb(K);
   std::vector<int> status(K);
   HIP_CHECK(hipMemcpyAsync(counts.data(), d_counts, 8 * K, hipMemcpyDeviceToHost, s));
@@ -53,7 +89,6 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   int64_t bytes = 0;
   for (int k = 0; k < K; ++k) {
     if (status[k] != 0) throw std::runtime_error("GenericMerger: corrupt or truncated IFile run " + std::to_string(k));
-    if (counts[k] > 0xFFFFFFFFll) throw std::runtime_error("GenericMerger: run has more than 2^32 records");
     eoff[k + 1] = eoff[k] + counts[k];
     bytes += recb[k];
   }
@@ -61,23 +96,39 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   if (bytes > out_cap) throw std::runtime_error("GenericMerger: output capacity too small");
   res.records = total;
   res.bytes = bytes;
-  reserve(total, K);
+  reserve(std::max(total, nchunks), K);
   // offsets storage: run k gets counts[k]+1 entries
   const int64_t off_elems = total + K;
   if (offsets_.size() < (size_t)off_elems * 8) offsets_.alloc((size_t)off_elems * 8);
   std::vector<int64_t*> offp(K);
   for (int k = 0; k < K; ++k) offp[k] = offsets_.as<int64_t>() + eoff[k] + k;
   HIP_CHECK(hipMemcpyAsync(d_offp, offp.data(), 8 * K, hipMemcpyHostToDevice, s));
-  // ---- F1 pass 2: offsets
-  launch_index_records(d_bases, d_nbytes, K, d_offp, s);
-  GenericKeyCtx ctx{d_bases, const_cast<const int64_t* const*>(d_offp), kind};
+  // ---- F1 pass 2: every chunk re-walked in parallel from its checkpoint
+  int64_t* d_eoff = out_off_.as<int64_t>();
+  HIP_CHECK(hipMemcpyAsync(d_eoff, eoff.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
+  for (int k = 0; k < K; ++k)  // empty runs have no chunk to write their terminating offset
+    if (run_bytes[k] == 0) HIP_CHECK(hipMemsetAsync(offp[k], 0, 8, s));
+  if (nchunks > 0) {
+    launch_exclusive_scan(d_ckcount, d_ckord, nchunks, scan_tmp_.as<int64_t>(), s);
+    launch_f1_index(d_bases, d_nbytes, d_cbase, d_crun, d_ckstart, d_ckcount, d_ckord, d_eoff, d_recb, d_offp,
+                    nchunks, s);
+  }
+  GenericKeyCtx ctx;
+  ctx.bases = d_bases;
+  ctx.offsets = const_cast<const int64_t* const*>(d_offp);
+  ctx.kind = kind;
+  {
+    const int64_t nrec = std::max<int64_t>(total, 1);
+    ctx.keyptr = reinterpret_cast<const uint8_t**>(side_.as<uint8_t>());
+    ctx.recptr = reinterpret_cast<const uint8_t**>(side_.as<uint8_t>() + 8 * nrec);
+    ctx.keylen = reinterpret_cast<int32_t*>(side_.as<uint8_t>() + 16 * nrec);
+    ctx.reclen = reinterpret_cast<int32_t*>(side_.as<uint8_t>() + 20 * nrec);
+  }
   if (total == 0) {
     res.cuts = {0};
     return res;
   }
-  // ---- F2: normalize (elem_off goes into the out_off scratch, reused below)
-  int64_t* d_eoff = out_off_.as<int64_t>();
-  HIP_CHECK(hipMemcpyAsync(d_eoff, eoff.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
+  // ---- F2: normalize (elem_off lives in the out_off scratch until the size scan reuses it)
   Elem* cur = elems_a_.as<Elem>();
   Elem* nxt = elems_b_.as<Elem>();
   launch_normalize_generic(ctx, d_eoff, K, total, cur, s);

@@ -31,7 +31,7 @@ class GenericMerger {
 
  private:
   void reserve(int64_t records, int runs);
-  DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_;
+  DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_, side_, ck_;
   int64_t cap_records_ = 0;
   int cap_runs_ = 0;
 };

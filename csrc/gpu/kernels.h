@@ -85,11 +85,18 @@ struct PassDesc {
 void launch_merge_partition(const Elem* in, PassDesc pd, int64_t* splits, hipStream_t s);
 void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits, hipStream_t s);
 
-// GENERIC key context: record i of run r starts at bases[r] + offsets[r][i]; kind = uda::KeyKind.
+// GENERIC key context. Record i of run r starts at bases[r] + offsets[r][i]; kind = uda::KeyKind.
+// After F2 every record g (global ordinal, run-major) also has direct side tables so the merge and
+// the gather never re-parse headers: key content pointer/length and record pointer/length.
+// GENERIC Elem: hi = first 8 content bytes (big-endian), lo = min(content_len, 0xFFFF) << 48 | g.
 struct GenericKeyCtx {
   uint8_t* const* bases;
   const int64_t* const* offsets;
   int kind;
+  const uint8_t** keyptr;   // [g] key content
+  int32_t* keylen;          // [g] content length
+  const uint8_t** recptr;   // [g] record start
+  int32_t* reclen;          // [g] record size
 };
 void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits, GenericKeyCtx ctx,
                                     hipStream_t s);
@@ -97,13 +104,20 @@ void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int
                                GenericKeyCtx ctx, hipStream_t s);
 
 // ---------------------------------------------------------------- GENERIC record path (F1/F2/F4)
-// F1 pass 1: per run, count records and the record bytes before the EOF marker (serial VInt walk;
-// runs are walked in parallel). status[r] != 0 on a corrupt/truncated stream.
-void launch_count_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* counts,
-                          int64_t* rec_bytes, int* status, hipStream_t s);
-// F1 pass 2: offsets[r][0..n_r] = record start offsets (offsets[r][n_r] = record bytes).
-void launch_index_records(uint8_t* const* bases, const int64_t* nbytes, int nruns, int64_t* const* offsets,
-                          hipStream_t s);
+// F1 pass 1 (one wave per run): chunk checkpoints ck_start/ck_count for the chunks of run r at
+// [chunk_base[r], chunk_base[r+1]) (chunks of f1_chunk_bytes()), records per run, record bytes
+// before the EOF marker, status != 0 on a corrupt/truncated stream. prof: diagnostic cycle split.
+int64_t f1_chunk_bytes();
+void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
+                    int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
+                    hipStream_t s, uint64_t* prof = nullptr);
+// F1 pass 2 (one wave per chunk): record offsets; ck_ord = exclusive scan of ck_count (global
+// record ordinal of each chunk's first record), elem_off = first ordinal of each run (nruns+1),
+// chunk_run[c] = run of chunk c. offsets[r] has counts[r]+1 entries (last = record bytes).
+void launch_f1_index(uint8_t* const* bases, const int64_t* nbytes, const int64_t* chunk_base,
+                     const int32_t* chunk_run, const int64_t* ck_start, const int64_t* ck_count,
+                     const int64_t* ck_ord, const int64_t* elem_off, const int64_t* rec_bytes,
+                     int64_t* const* offsets, int64_t total_chunks, hipStream_t s);
 // F2: normalized elements for all records; elem_off[r] = first element of run r (nruns+1 entries).
 void launch_normalize_generic(GenericKeyCtx ctx, const int64_t* elem_off, int nruns, int64_t total, Elem* out,
                               hipStream_t s);

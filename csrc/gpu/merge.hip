@@ -36,30 +36,34 @@ struct FixedCmp {
   __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const { return elem_le(a, b); }
 };
 
-// GENERIC: hi = first 8 content bytes, lo = capped content length << 48 | run << 32 | pos.
-// Prefix ties between two keys longer than 8 bytes are settled on the raw key bytes.
+// GENERIC: prefix ties between two keys longer than 8 bytes are settled on the raw key bytes,
+// read through the per-record side tables 8 bytes at a time.
+__device__ __forceinline__ uint64_t load_be8(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  if (n >= 8) {
+    uint64_t w;
+    __builtin_memcpy(&w, p, 8);
+    return __builtin_bswap64(w);
+  }
+  for (int i = 0; i < 8; ++i) v = (v << 8) | (uint64_t)(i < n ? p[i] : 0);
+  return v;
+}
+
 struct GenericCmp {
   GenericKeyCtx ctx;
-  __device__ const uint8_t* content(const Elem& e, int* len) const {
-    const int run = (int)((e.lo >> 32) & 0xFFFF);
-    const uint64_t pos = e.lo & 0xFFFFFFFFull;
-    const uint8_t* rec = ctx.bases[run] + ctx.offsets[run][pos];
-    int64_t kl = 0, vl = 0;
-    const int a = vint_decode(rec, 9, &kl);
-    const int b = vint_decode(rec + a, 9, &vl);
-    const uint8_t* key = rec + a + b;
-    const int o = key_content_offset((KeyKind)ctx.kind, key, (int)kl);
-    *len = (int)kl - o;
-    return key + o;
-  }
   __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const {
     if (a.hi != b.hi) return a.hi < b.hi;
     if ((a.lo >> 48) > 8 && (b.lo >> 48) > 8) {
-      int la, lb;
-      const uint8_t* pa = content(a, &la);
-      const uint8_t* pb = content(b, &lb);
-      const int c = bytes_compare(pa + 8, la - 8, pb + 8, lb - 8);
-      if (c != 0) return c < 0;
+      const uint64_t ga = a.lo & 0xFFFFFFFFFFFFull, gb = b.lo & 0xFFFFFFFFFFFFull;
+      const uint8_t* pa = ctx.keyptr[ga];
+      const uint8_t* pb = ctx.keyptr[gb];
+      const int la = ctx.keylen[ga], lb = ctx.keylen[gb];
+      const int n = la < lb ? la : lb;
+      for (int i = 8; i < n; i += 8) {
+        const uint64_t x = load_be8(pa + i, n - i), y = load_be8(pb + i, n - i);
+        if (x != y) return x < y;
+      }
+      if (la != lb) return la < lb;
     }
     return a.lo <= b.lo;
   }

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstring>
 
 #include "device_engine.h"
@@ -421,6 +422,7 @@ PYBIND11_MODULE(_uda_native, m) {
     std::vector<int64_t> cuts;
     int64_t records = 0;
     int passes = 0;
+    double merge_ms = 0;
     {
       py::gil_scoped_release rel;
       HIP_CHECK(hipSetDevice(device));
@@ -439,7 +441,11 @@ PYBIND11_MODULE(_uda_native, m) {
         off += (int64_t)r.size();
       }
       gpu::GenericMerger gm;
+      HIP_CHECK(hipStreamSynchronize(s));
+      auto t0 = std::chrono::steady_clock::now();
       auto res = gm.merge(ptrs, bytes, (int)kind, dout.as<uint8_t>(), total, kv_buf, s);
+      HIP_CHECK(hipStreamSynchronize(s));
+      merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       out.resize((size_t)res.bytes);
       if (res.bytes) HIP_CHECK(hipMemcpyAsync(&out[0], dout.as(), (size_t)res.bytes, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
@@ -448,7 +454,7 @@ PYBIND11_MODULE(_uda_native, m) {
       records = res.records;
       passes = res.passes;
     }
-    return py::make_tuple(py::bytes(out), cuts, records, passes);
+    return py::make_tuple(py::bytes(out), cuts, records, passes, merge_ms);
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
   m.def("nccl_unique_id", []() { return py::bytes(gpu::nccl_unique_id()); });
 

@@ -11,6 +11,7 @@ from __future__ import annotations
 from .._native import native
 
 EOF_MARKER = b"\xff\xff"
+last_stats: dict = {}  # timing of the most recent merge_runs call (device merge excludes H2D/D2H)
 
 
 def merge_runs(runs: list[bytes], key_class: str, device: str = "gpu", kv_buf: int = 1 << 20,
@@ -19,7 +20,8 @@ def merge_runs(runs: list[bytes], key_class: str, device: str = "gpu", kv_buf: i
     if device == "gpu":
         if n.device_count() <= 0:
             raise RuntimeError("merge_runs(device='gpu'): no HIP device visible")
-        merged, cuts, _records, _passes = n.gpu_merge_runs(list(runs), key_class, kv_buf - 2, gpu_index)
+        merged, cuts, _records, _passes, merge_ms = n.gpu_merge_runs(list(runs), key_class, kv_buf - 2, gpu_index)
+        last_stats.update(device="gpu", records=_records, passes=_passes, merge_ms=merge_ms)
         return merged, cuts
     if device == "cpu":
         out, lens = n.cpu_merge(list(runs), key_class, kv_buf)
