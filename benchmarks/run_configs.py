@@ -7,6 +7,7 @@
                       write_kv_to_stream packing) on TeraSort runs on this host's CPU.
   secondary_sort      variable-length Text keys with long common prefixes + partition skew: GPU generic
                       merge (F1/F2/F3/F4 kernels) vs the CPU heap merge on the same runs.
+  decode              F6 Snappy / LZO1X block decode on the device vs the host decoder.
   spill               TeraSort whose map outputs live in pinned host DRAM (the spill tier used when a
                       job exceeds HBM): rounds are streamed H2D, merged on the GPU, delivered D2H.
 
@@ -101,6 +102,31 @@ def secondary_sort(args) -> dict:
             "byte_identical": True}
 
 
+def decode(args) -> dict:
+    """F6: device block decode of block-compressed IFile runs (secondary-sort data) vs host decode."""
+    from uda_amd import native
+    n = native()
+    codec = {"snappy": 1, "lzo": 2}[args.codec]
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    runs = [m[0] for m in n.generate_runs("secondary", args.maps, 1, rows, 5)]
+    t0 = time.perf_counter()
+    streams = [n.block_compress(codec, r, 256 * 1024) for r in runs]
+    comp_s = time.perf_counter() - t0
+    raw = sum(len(r) for r in runs)
+    comp = sum(len(s) for s in streams)
+    n.gpu_block_decode(args.codec, streams[:1])  # warm up
+    outs, blocks, ms = n.gpu_block_decode(args.codec, streams)
+    assert outs == runs
+    t0 = time.perf_counter()
+    host = n.block_decompress(codec, streams[0], 1 << 20)
+    host_s = (time.perf_counter() - t0) * len(streams)
+    assert host == runs[0]
+    return {"config": f"F6 device {args.codec} block decode, 256 KiB blocks, secondary-sort IFile data",
+            "raw_gb": round(raw / 1e9, 3), "ratio": round(raw / comp, 2), "blocks": blocks,
+            "device_decode_ms": round(ms, 1), "device_gbps_raw": round(raw / ms / 1e6, 1),
+            "host_1thread_gbps_raw": round(raw / host_s / 1e9, 3), "host_compress_s": round(comp_s, 1)}
+
+
 def spill(args) -> dict:
     import torch  # noqa: F401
     from uda_amd.models.terasort import TeraSortConfig, TeraSortShuffle
@@ -122,7 +148,8 @@ def spill(args) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill"])
+    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode"])
+    ap.add_argument("--codec", default="snappy", choices=["snappy", "lzo"])
     ap.add_argument("--gb", type=float, default=1.0)
     ap.add_argument("--maps", type=int, default=16)
     ap.add_argument("--reducers", type=int, default=4)

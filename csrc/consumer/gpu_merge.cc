@@ -12,6 +12,7 @@
 #include <random>
 #include <thread>
 
+#include "../gpu/block_decoder.h"
 #include "../gpu/device_engine.h"
 #include "../gpu/generic_merger.h"
 #include "reduce_task.h"
@@ -25,6 +26,10 @@ void ReduceTask::merge_gpu() {
   const int maps = init_.num_maps;
   const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
   if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
+  // F6: compressed partitions cross PCIe compressed and are decoded in HBM (host decode only when
+  // the framing needs it, see plan_block_streams)
+  const bool device_decode = codec_ != Codec::kNone && host_->conf_i64("mapred.uda.gpu.decompress", 1) != 0;
+  const Codec fetch_codec = device_decode ? Codec::kNone : codec_;
 
   // ---- fetch: start every MOF (bounded by the buffer pool), drain each fully into host memory
   std::vector<std::vector<uint8_t>> parts;
@@ -46,7 +51,7 @@ void ReduceTask::merge_gpu() {
       }
       std::shuffle(pending.begin(), pending.end(), rng);
       while (!pending.empty() && free_pairs_ > 0 && started < maps) {
-        to_start.push_back(std::make_shared<MofFetcher>(this, pending.back(), buffer_size_, codec_));
+        to_start.push_back(std::make_shared<MofFetcher>(this, pending.back(), buffer_size_, fetch_codec));
         pending.pop_back();
         free_pairs_--;
         started++;
@@ -95,27 +100,69 @@ void ReduceTask::merge_gpu() {
   }
   const double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
-  // ---- stage in HBM and merge
-  int64_t total = 0;
-  for (auto& p : parts) total += (int64_t)p.size();
+  // ---- stage in HBM (decoding compressed partitions there) and merge
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) throw UdaError("hipStreamCreate failed");
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() { (void)hipStreamDestroy(s); }
+  } stream_guard{s};
+  gpu::BlockPlan plan;
+  bool decode_on_device = false;
+  if (device_decode) {
+    std::vector<const uint8_t*> ptrs;
+    std::vector<int64_t> lens;
+    for (auto& p : parts) {
+      ptrs.push_back(p.data());
+      lens.push_back((int64_t)p.size());
+    }
+    decode_on_device = gpu::plan_block_streams(codec_, ptrs, lens, &plan);
+    if (!decode_on_device) {
+      UDA_LOG(kInfo, "device decode: framing needs a host decode (multi-chunk %s block); decoding on host",
+              codec_name(codec_));
+      for (auto& p : parts) {
+        BlockDecoder dec(codec_);
+        dec.feed(p.data(), p.size());
+        std::vector<uint8_t> raw, buf(1 << 20);
+        for (size_t n; (n = dec.read(buf.data(), buf.size())) > 0;) raw.insert(raw.end(), buf.begin(), buf.begin() + (long)n);
+        if (!dec.idle()) throw UdaError("truncated compressed partition");
+        p.swap(raw);
+      }
+    }
+  }
+  int64_t total = 0, staged = 0;
+  for (auto& p : parts) staged += (int64_t)p.size();
+  total = decode_on_device ? plan.raw_total : staged;
   gpu::DeviceBuffer in((size_t)std::max<int64_t>(total, 16)), out((size_t)std::max<int64_t>(total, 16));
+  gpu::DeviceBuffer packed(decode_on_device ? (size_t)std::max<int64_t>(staged, 16) : 0);
+  uint8_t* stage = decode_on_device ? packed.as<uint8_t>() : in.as<uint8_t>();
   std::vector<const uint8_t*> runs;
   std::vector<int64_t> bytes;
   int64_t off = 0;
-  hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) throw UdaError("hipStreamCreate failed");
-  for (auto& p : parts) {
-    if (!p.empty()) HIP_CHECK(hipMemcpyAsync(in.as<uint8_t>() + off, p.data(), p.size(), hipMemcpyHostToDevice, s));
-    runs.push_back(in.as<uint8_t>() + off);
-    bytes.push_back((int64_t)p.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    auto& p = parts[i];
+    if (!p.empty()) HIP_CHECK(hipMemcpyAsync(stage + off, p.data(), p.size(), hipMemcpyHostToDevice, s));
+    if (decode_on_device) {
+      runs.push_back(in.as<uint8_t>() + plan.raw_offset[i]);
+      bytes.push_back(plan.raw_offset[i + 1] - plan.raw_offset[i]);
+    } else {
+      runs.push_back(in.as<uint8_t>() + off);
+      bytes.push_back((int64_t)p.size());
+    }
     off += (int64_t)p.size();
+  }
+  if (decode_on_device) {
+    gpu::DeviceBlockDecoder dec;
+    dec.decode(codec_, plan, packed.as<uint8_t>(), in.as<uint8_t>(), s);
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.device_decoded_blocks += (int64_t)plan.descs.size();
   }
   gpu::GenericMerger merger;
   gpu::GenericMergeResult r = merger.merge(runs, bytes, (int)kind_, out.as<uint8_t>(), total, kv_buf_size_ - kEofBytes, s);
   std::vector<uint8_t> host((size_t)r.bytes + kEofBytes);
   if (r.bytes) HIP_CHECK(hipMemcpyAsync(host.data(), out.as(), (size_t)r.bytes, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  (void)hipStreamDestroy(s);
+  parts.clear();
   host[(size_t)r.bytes] = 0xFF;
   host[(size_t)r.bytes + 1] = 0xFF;
 

@@ -40,6 +40,7 @@ struct ReduceStats {
   int64_t spill_bytes = 0;
   double fetch_ms = 0, merge_ms = 0, total_ms = 0;
   double wait_ms = 0;             // time the merge waited on the network (total_wait_mem_time)
+  int64_t device_decoded_blocks = 0;  // compressed blocks decoded in HBM by the F6 kernels
   std::string backend;
 };
 

@@ -1,0 +1,333 @@
+// F6 — block-decompress kernels (Snappy raw format, LZO1X) for Hadoop block-compressed map
+// outputs, decoded in HBM so the compressed bytes are what crosses PCIe / the network.
+//
+// Reference: DecompressorWrapper::doDecompress (src/Merger/DecompressorWrapper.cc:168-197) feeding
+// liblzo2 / libsnappy one block at a time on the merge thread. Here every Hadoop block is decoded
+// by one wave64, all blocks of all runs in one launch:
+//   * the compressed stream of the wave's block is staged through a per-wave LDS window; the tag /
+//     opcode parse is wave-uniform (every lane decodes the same element; the values are scalar),
+//   * literals and back-references are copied by the 64 lanes cooperatively; an overlapping copy
+//     (offset < length) becomes a periodic fill out[op+i] = out[op-off + i % off],
+//   * a back-reference that reads bytes this wave stored since the last store fence first waits
+//     for its stores (workgroup-scope fence: the wave's own stores are visible through the CU's
+//     write-through L1 once they completed).
+// Format parity with the host decoders in csrc/codec/{snappy,lzo}.cc (same bounds checks); a
+// corrupt block sets its status word and the caller raises.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace uda {
+namespace gpu {
+
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kWin = 2048;  // per-wave LDS window of compressed input
+
+struct Wave {
+  const uint8_t* in;
+  uint8_t* out;
+  uint8_t* win;       // LDS window
+  int64_t win_base;   // stream offset of win[0]
+  int64_t win_end;    // stream offset one past the valid window bytes
+  int64_t in_end;     // end of this block's compressed bytes
+  int64_t flushed;    // output offset below which every store of this wave has completed
+  int lane;
+};
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+__device__ __forceinline__ int64_t uni(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Make [ip, ip+need) resident in the LDS window (need <= 64). Returns false past the block end.
+__device__ __forceinline__ bool ensure(Wave& w, int64_t ip, int need) {
+  if (ip + need > w.in_end) return false;
+  if (ip >= w.win_base && ip + need <= w.win_end) return true;
+  wave_sync();
+  const int64_t base = ip & ~(int64_t)15;
+  const int64_t end = min(base + kWin, w.in_end);
+  for (int i = w.lane * 16; i < kWin; i += 64 * 16) {
+    const int64_t p = base + i;
+    if (p + 16 <= end) {
+      // 16-byte aligned vector load when the source alignment allows, bytes otherwise
+      if ((((uintptr_t)(w.in + p)) & 15) == 0) {
+        *reinterpret_cast<uint4*>(w.win + i) = *reinterpret_cast<const uint4*>(w.in + p);
+      } else {
+        for (int k = 0; k < 16; ++k) w.win[i + k] = w.in[p + k];
+      }
+    } else {
+      for (int k = 0; k < 16; ++k) w.win[i + k] = (p + k < end) ? w.in[p + k] : 0;
+    }
+  }
+  wave_sync();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of every lane done before reads
+  wave_sync();
+  w.win_base = base;
+  w.win_end = end;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t byte_at(const Wave& w, int64_t ip) {
+  return (uint32_t)w.win[ip - w.win_base];
+}
+
+__device__ __forceinline__ void copy_literal(Wave& w, int64_t op, int64_t ip, int64_t len) {
+  for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.in[ip + i];
+}
+
+// out[op .. op+len) = out[op-off ...] with LZ77 overlap semantics.
+__device__ __forceinline__ void copy_match(Wave& w, int64_t op, int64_t off, int64_t len) {
+  const int64_t src = op - off;
+  if (src + min(off, len) > w.flushed) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores completed
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    w.flushed = op;
+  }
+  if (off >= len) {
+    for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.out[src + i];
+  } else {
+    for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.out[src + (i % off)];
+  }
+}
+
+__device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int64_t oend, int64_t* produced) {
+  w.in_end = cend;
+  // varint uncompressed length
+  int64_t ulen = 0;
+  int shift = 0;
+  for (;;) {
+    if (shift > 35 || !ensure(w, ip, 1)) return false;
+    const uint32_t b = byte_at(w, ip++);
+    ulen |= (int64_t)(b & 0x7F) << shift;
+    if (!(b & 0x80)) break;
+    shift += 7;
+  }
+  ulen = uni(ulen);
+  if (op + ulen > oend) return false;
+  const int64_t op0 = op, uend = op + ulen;
+  while (ip < cend) {
+    if (!ensure(w, ip, 1)) return false;
+    const uint32_t tag = byte_at(w, ip++);
+    const uint32_t type = tag & 3;
+    if (type == 0) {
+      int64_t len = tag >> 2;
+      if (len >= 60) {
+        const int nb = (int)len - 59;
+        if (!ensure(w, ip, nb)) return false;
+        len = 0;
+        for (int i = 0; i < nb; ++i) len |= (int64_t)byte_at(w, ip + i) << (8 * i);
+        ip += nb;
+      }
+      len += 1;
+      if (ip + len > cend || op + len > uend) return false;
+      copy_literal(w, op, ip, len);
+      ip += len;
+      op += len;
+    } else {
+      int64_t len, off;
+      if (type == 1) {
+        if (!ensure(w, ip, 1)) return false;
+        len = 4 + ((tag >> 2) & 7);
+        off = ((int64_t)(tag >> 5) << 8) | byte_at(w, ip);
+        ip += 1;
+      } else if (type == 2) {
+        if (!ensure(w, ip, 2)) return false;
+        len = 1 + (tag >> 2);
+        off = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+        ip += 2;
+      } else {
+        if (!ensure(w, ip, 4)) return false;
+        len = 1 + (tag >> 2);
+        off = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8) | ((int64_t)byte_at(w, ip + 2) << 16) |
+              ((int64_t)byte_at(w, ip + 3) << 24);
+        ip += 4;
+      }
+      if (off == 0 || off > op - op0 || op + len > uend) return false;
+      copy_match(w, op, off, len);
+      op += len;
+    }
+  }
+  if (op != uend) return false;
+  *produced = ulen;
+  return true;
+}
+
+// LZO1X: the state machine of csrc/codec/lzo.cc, wave-uniform.
+__device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64_t oend, int64_t* produced) {
+  w.in_end = ip_end;
+  const int64_t out0 = op;
+  int64_t t = 0, next = 0, state = 0, m_pos = 0;
+  bool lit_first = false;
+  if (!ensure(w, ip, 1)) return false;
+  if (byte_at(w, ip) > 17) {
+    t = (int64_t)byte_at(w, ip) - 17;
+    ++ip;
+    if (t < 4) {
+      next = t;
+      goto match_next;
+    }
+    lit_first = true;
+  }
+  for (;;) {
+    if (lit_first) {
+      lit_first = false;
+      goto copy_literal_run;
+    }
+    if (!ensure(w, ip, 1)) return false;
+    t = byte_at(w, ip++);
+    if (t < 16) {
+      if (state == 0) {
+        if (t == 0) {
+          for (;;) {
+            if (!ensure(w, ip, 1)) return false;
+            if (byte_at(w, ip) != 0) break;
+            t += 255;
+            ++ip;
+          }
+          t += 15 + byte_at(w, ip++);
+        }
+        t += 3;
+      copy_literal_run:
+        if (ip + t + 3 > ip_end || op + t > oend) return false;
+        copy_literal(w, op, ip, t);
+        op += t;
+        ip += t;
+        state = 4;
+        continue;
+      } else if (state != 4) {  // M1: 2-byte match after 1..3 trailing literals
+        next = t & 3;
+        if (!ensure(w, ip, 1)) return false;
+        m_pos = op - 1 - (t >> 2) - ((int64_t)byte_at(w, ip++) << 2);
+        if (m_pos < out0 || m_pos >= op || op + 2 > oend) return false;
+        copy_match(w, op, op - m_pos, 2);
+        op += 2;
+        goto match_next;
+      } else {  // M1 after a literal run: 3 bytes, offset 2049..3072
+        next = t & 3;
+        if (!ensure(w, ip, 1)) return false;
+        m_pos = op - (1 + 0x0800) - (t >> 2) - ((int64_t)byte_at(w, ip++) << 2);
+        t = 3;
+      }
+    } else if (t >= 64) {  // M2
+      next = t & 3;
+      if (!ensure(w, ip, 1)) return false;
+      m_pos = op - 1 - ((t >> 2) & 7) - ((int64_t)byte_at(w, ip++) << 3);
+      t = (t >> 5) - 1 + 2;
+    } else if (t >= 32) {  // M3
+      t = (t & 31) + 2;
+      if (t == 2) {
+        for (;;) {
+          if (!ensure(w, ip, 1)) return false;
+          if (byte_at(w, ip) != 0) break;
+          t += 255;
+          ++ip;
+        }
+        t += 31 + byte_at(w, ip++);
+      }
+      if (!ensure(w, ip, 2)) return false;
+      next = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+      ip += 2;
+      m_pos = op - 1 - (next >> 2);
+      next &= 3;
+    } else {  // M4 (16..31), or end of stream
+      m_pos = op - ((t & 8) << 11);
+      t = (t & 7) + 2;
+      if (t == 2) {
+        for (;;) {
+          if (!ensure(w, ip, 1)) return false;
+          if (byte_at(w, ip) != 0) break;
+          t += 255;
+          ++ip;
+        }
+        t += 7 + byte_at(w, ip++);
+      }
+      if (!ensure(w, ip, 2)) return false;
+      next = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+      ip += 2;
+      m_pos -= next >> 2;
+      next &= 3;
+      if (m_pos == op) {
+        *produced = op - out0;
+        return t == 3 && ip == ip_end;
+      }
+      m_pos -= 0x4000;
+    }
+    if (m_pos < out0 || m_pos >= op || op + t > oend) return false;
+    copy_match(w, op, op - m_pos, t);
+    op += t;
+  match_next:
+    state = next;
+    t = next;
+    if (ip + t + 3 > ip_end || op + t > oend) return false;
+    copy_literal(w, op, ip, t);
+    op += t;
+    ip += t;
+  }
+}
+
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+template <int kCodec>
+__global__ void __launch_bounds__(64 * kWavesPerBlock)
+    block_decode_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][kWin + 16];
+  const int wid = threadIdx.x >> 6;
+  const int b = blockIdx.x * kWavesPerBlock + wid;
+  if (b >= n) return;
+  const DecodeDesc d = descs[b];
+  Wave w;
+  w.in = in;
+  w.out = out;
+  w.win = lds[wid];
+  w.win_base = 0;
+  w.win_end = 0;
+  w.flushed = d.dst;
+  w.lane = threadIdx.x & 63;
+  int64_t ip = d.src, op = d.dst;
+  const int64_t oend = d.dst + d.raw;
+  bool ok = true;
+  // one block = one or more [u32 BE compressed_len][chunk] records until its raw bytes are produced
+  while (ok && op < oend) {
+    if (ip + 4 > d.src_end) {
+      ok = false;
+      break;
+    }
+    const int64_t clen = (int64_t)be32(in + ip);
+    ip += 4;
+    if (ip + clen > d.src_end) {
+      ok = false;
+      break;
+    }
+    int64_t produced = 0;
+    w.win_base = w.win_end = 0;
+    ok = (kCodec == 1) ? snappy_chunk(w, ip, ip + clen, op, oend, &produced)
+                       : lzo_chunk(w, ip, ip + clen, op, oend, &produced);
+    ip += clen;
+    op += produced;
+  }
+  if (ok && (op != oend || ip != d.src_end)) ok = false;
+  if (!ok && w.lane == 0) atomicOr(status, 1);
+}
+
+}  // namespace
+
+void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (codec == 1)
+    block_decode_kernel<1><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status);
+  else
+    block_decode_kernel<2><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status);
+}
+
+}  // namespace gpu
+}  // namespace uda

@@ -150,6 +150,19 @@ struct CopyDesc {
 // descs: device array of n descriptors; max_bytes: largest descriptor (sizes the grid).
 void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s);
 
+// ---------------------------------------------------------------- block decode (F6)
+// One Hadoop compressed block: chunks [u32 BE clen][clen bytes]... in [src, src_end) of the
+// compressed buffer decode to exactly `raw` bytes at dst of the output buffer.
+struct DecodeDesc {
+  int64_t src;
+  int64_t src_end;
+  int64_t dst;
+  int64_t raw;
+};
+// codec: 1 = Snappy, 2 = LZO1X (uda::Codec values). *status |= 1 if any block is corrupt.
+void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
+                         hipStream_t s);
+
 // ---------------------------------------------------------------- validation
 // Checks key order of `n` FIXED10 records at `recs` (and against *prev_key if has_prev) and
 // accumulates an order-independent checksum. Results: stats[0] += out-of-order count,

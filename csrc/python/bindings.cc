@@ -12,11 +12,13 @@
 #include <chrono>
 #include <cstring>
 
+#include "block_decoder.h"
 #include "device_engine.h"
 #include "generic_merger.h"
 #include "uda/aio.h"
 #include "uda/codec.h"
 #include "uda/datagen.h"
+#include "uda/error.h"
 #include "uda/ifile.h"
 #include "uda/uda_bridge.h"
 #include "uda/cmd.h"
@@ -456,6 +458,53 @@ PYBIND11_MODULE(_uda_native, m) {
     }
     return py::make_tuple(py::bytes(out), cuts, records, passes, merge_ms);
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
+  // F6: decode Hadoop block-compressed streams on the device; returns (raw streams, blocks, decode_ms)
+  m.def("gpu_block_decode", [](const std::string& codec_cls, const std::vector<std::string>& streams, int device) {
+    bool unsup = false;
+    Codec c = codec_from_class(codec_cls, &unsup);
+    if (c == Codec::kNone) c = codec_cls == "snappy" ? Codec::kSnappy : codec_cls == "lzo" ? Codec::kLzo : Codec::kNone;
+    if (c == Codec::kNone) throw py::value_error("unknown codec " + codec_cls);
+    std::vector<std::string> outs;
+    int64_t blocks = 0;
+    double ms = 0;
+    {
+      py::gil_scoped_release rel;
+      HIP_CHECK(hipSetDevice(device));
+      std::vector<const uint8_t*> ptrs;
+      std::vector<int64_t> lens;
+      int64_t staged = 0;
+      for (auto& st : streams) {
+        ptrs.push_back(reinterpret_cast<const uint8_t*>(st.data()));
+        lens.push_back((int64_t)st.size());
+        staged += (int64_t)st.size();
+      }
+      gpu::BlockPlan plan;
+      if (!gpu::plan_block_streams(c, ptrs, lens, &plan)) throw UdaError("block framing not resolvable on device");
+      gpu::DeviceBuffer din((size_t)std::max<int64_t>(staged, 16)), dout((size_t)std::max<int64_t>(plan.raw_total, 16));
+      hipStream_t s;
+      HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      int64_t off = 0;
+      for (auto& st : streams) {
+        if (!st.empty()) HIP_CHECK(hipMemcpyAsync(din.as<uint8_t>() + off, st.data(), st.size(), hipMemcpyHostToDevice, s));
+        off += (int64_t)st.size();
+      }
+      HIP_CHECK(hipStreamSynchronize(s));
+      gpu::DeviceBlockDecoder dec;
+      auto t0 = std::chrono::steady_clock::now();
+      dec.decode(c, plan, din.as<uint8_t>(), dout.as<uint8_t>(), s);
+      ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      std::string all((size_t)plan.raw_total, '\0');
+      if (plan.raw_total) HIP_CHECK(hipMemcpyAsync(&all[0], dout.as(), all.size(), hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      HIP_CHECK(hipStreamDestroy(s));
+      for (size_t i = 0; i < streams.size(); ++i)
+        outs.push_back(all.substr((size_t)plan.raw_offset[i], (size_t)(plan.raw_offset[i + 1] - plan.raw_offset[i])));
+      blocks = (int64_t)plan.descs.size();
+    }
+    py::list l;
+    for (auto& o : outs) l.append(py::bytes(o));
+    return py::make_tuple(l, blocks, ms);
+  }, py::arg("codec"), py::arg("streams"), py::arg("device") = 0);
   m.def("nccl_unique_id", []() { return py::bytes(gpu::nccl_unique_id()); });
 
   py::class_<CountingSink, std::shared_ptr<CountingSink>>(m, "CountingSink")
