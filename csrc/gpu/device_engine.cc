@@ -556,14 +556,19 @@ void ShuffleJob::copy_loop() {
       // split the piece over the copy streams on whole-record boundaries
       const int64_t recs = len / kTeraRecordBytes;
       int64_t done = 0;
+      // every copy stream starts the piece after the start event (stream 0); stream 0 then joins the
+      // others, so piece_events_[k*NS] marks the whole piece and start->end is a same-stream interval
       for (int i = 0; i < NS; ++i) {
         const int64_t part = (i == NS - 1) ? (recs - done) : recs / NS;
+        if (i > 0) HIP_CHECK(hipStreamWaitEvent(s_copy_[i], piece_start_ev_[k], 0));
         if (part > 0)
           HIP_CHECK(hipMemcpyAsync(dst + done * kTeraRecordBytes, src + off + done * kTeraRecordBytes,
                                    part * kTeraRecordBytes, hipMemcpyDeviceToHost, s_copy_[i]));
-        HIP_CHECK(hipEventRecord(piece_events_[(size_t)k * NS + i], s_copy_[i]));
+        if (i > 0) HIP_CHECK(hipEventRecord(piece_events_[(size_t)k * NS + i], s_copy_[i]));
         done += part;
       }
+      for (int i = 1; i < NS; ++i) HIP_CHECK(hipStreamWaitEvent(s_copy_[0], piece_events_[(size_t)k * NS + i], 0));
+      HIP_CHECK(hipEventRecord(piece_events_[(size_t)k * NS], s_copy_[0]));
       off += len;
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -599,10 +604,9 @@ void ShuffleJob::deliver_loop() {
       p = piece_q_.front();
       piece_q_.pop_front();
     }
-    for (int i = 0; i < NS; ++i) HIP_CHECK(hipEventSynchronize(piece_events_[(size_t)p.slot * NS + i]));
+    HIP_CHECK(hipEventSynchronize(piece_events_[(size_t)p.slot * NS]));  // joins every copy stream
     float ms = 0;
-    if (p.bytes > 0 && hipEventElapsedTime(&ms, piece_start_ev_[p.slot],
-                                           piece_events_[(size_t)p.slot * NS + NS - 1]) == hipSuccess)
+    if (p.bytes > 0 && hipEventElapsedTime(&ms, piece_start_ev_[p.slot], piece_events_[(size_t)p.slot * NS]) == hipSuccess)
       step_d2h_ms_ += ms;
     const uint8_t* base = pinned_.as<uint8_t>() + (int64_t)p.slot * piece_bytes_;
     int err = 0;

@@ -114,9 +114,9 @@ template <bool kProf>
 __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                            const int64_t* chunk_base, int64_t* ck_start,
                                                            int64_t* ck_count, int64_t* counts, int64_t* rec_bytes,
-                                                           int* status, uint64_t* prof) {
+                                                           int* status, uint64_t* prof, const int* run_ids) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kF1Chunk + 64];
-  const int r = blockIdx.x;
+  const int r = run_ids ? run_ids[blockIdx.x] : (int)blockIdx.x;
   const int lane = threadIdx.x;
   const uint8_t* p = bases[r];
   const int64_t n = nbytes[r];
@@ -181,6 +181,212 @@ __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases
       prof[2 * r] = t_stage;
       prof[2 * r + 1] = t_walk;
     }
+  }
+}
+
+// ---- F1 pass 1, parallel form (chunk transfer functions).
+// The record chain of a run is a composition of per-chunk functions: entering chunk c at offset e
+// (the first record start at or after the chunk's first byte, e < kF1Entries when records are at
+// most kF1Entries bytes), the chain leaves the chunk at a known offset after a known number of
+// records. (1) f1_fn: one wave per chunk tabulates that function for all kF1Entries entries (4
+// chains per lane walked in lockstep over the LDS-staged chunk). (2) f1_super: one wave per
+// superchunk of kF1Super chunks composes the chunk functions for every entry. (3) f1_top: one lane
+// per run composes superchunks from offset 0 (the only serial step: run_bytes / 256 KiB hops).
+// (4) f1_expand: one lane per superchunk replays its true entry through its chunks, emitting the
+// same per-chunk checkpoints as the serial scan. A run whose true chain needs an entry beyond the
+// table (a record longer than kF1Entries bytes straddles a chunk) is reported with status 2 and
+// re-indexed by the serial scan.
+constexpr int kF1Entries = 256;
+constexpr int kF1Super = 64;
+constexpr int kF1FnWaves = 4;
+constexpr int32_t kFnInvalid = INT32_MIN;      // corrupt/truncated record on this chain
+constexpr int32_t kFnFallback = INT32_MIN + 1;  // exit offset not representable
+constexpr int64_t kSupInvalid = -1, kSupFallback = -2;  // super codes; EOF at q -> -3 - q
+
+__global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
+                                                                 const int64_t* chunk_base, const int32_t* chunk_run,
+                                                                 int64_t nchunks, int32_t* fx, int32_t* fn) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * kF1FnWaves + wv;
+  const bool valid = c < nchunks;
+  uint8_t* buf = lds[wv];
+  int r = 0;
+  int64_t n = 0, c0 = 0;
+  if (valid) {
+    r = chunk_run[c];
+    n = nbytes[r];
+    c0 = (c - chunk_base[r]) * kF1Chunk;
+    const uint8_t* p = bases[r];
+    uint32_t w[16];
+    f1_fetch64(p, n, c0 + (int64_t)lane * kF1Bytes, w);
+    f1_stage(buf, lane, w);
+    if (lane == 0) {
+      uint32_t h[16];
+      f1_fetch64(p, n, c0 + kF1Chunk, h);
+      uint32_t* d = reinterpret_cast<uint32_t*>(buf + kF1Chunk);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) d[k] = h[k];
+    }
+  }
+  __syncthreads();
+  if (!valid) return;
+  const int end_rel = (int)min((int64_t)kF1Chunk, n - c0);
+  const int lim = (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo));
+  int64_t pos[4];
+  int32_t cnt[4], code[4];
+  bool act[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pos[j] = lane + 64 * j;
+    cnt[j] = 0;
+    act[j] = pos[j] < end_rel;
+    code[j] = (int32_t)pos[j];
+  }
+  while (act[0] || act[1] || act[2] || act[3]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (act[j]) {
+        const int64_t sz = f1_record(buf, (int)pos[j], lim, n - (c0 + pos[j]));
+        if (sz <= 0) {
+          code[j] = sz == 0 ? (int32_t)(-1 - pos[j]) : kFnInvalid;
+          act[j] = false;
+        } else {
+          pos[j] += sz;
+          ++cnt[j];
+          if (pos[j] >= end_rel) {
+            act[j] = false;
+            code[j] = pos[j] > (int64_t)INT32_MAX ? kFnFallback : (int32_t)pos[j];
+          }
+        }
+      }
+    }
+  }
+  int32_t* x = fx + c * kF1Entries;
+  int32_t* m = fn + c * kF1Entries;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[lane + 64 * j] = code[j];
+    m[lane + 64 * j] = cnt[j];
+  }
+}
+
+__global__ void __launch_bounds__(256) f1_super_kernel(const int64_t* nbytes, const int64_t* chunk_base,
+                                                       const int64_t* sup_base, const int32_t* sup_run, int64_t nsup,
+                                                       const int32_t* fx, const int32_t* fn, int64_t* sx,
+                                                       int64_t* sn) {
+  const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sidx >= nsup) return;
+  const int r = sup_run[sidx];
+  const int64_t n = nbytes[r];
+  const int64_t cb = chunk_base[r];
+  const int64_t nch = chunk_base[r + 1] - cb;
+  const int64_t first = (sidx - sup_base[r]) * kF1Super;
+  const int64_t last = min(first + kF1Super, nch);
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    const int e = lane + 64 * j;
+    int64_t p = first * kF1Chunk + e, cnt = 0, res;
+    for (;;) {
+      if (p >= n) {
+        res = p;
+        break;
+      }
+      const int64_t lc = p / kF1Chunk;
+      if (lc >= last) {
+        res = p;
+        break;
+      }
+      const int64_t rel = p - lc * kF1Chunk;
+      if (rel >= kF1Entries) {
+        res = kSupFallback;
+        break;
+      }
+      const int64_t slot = (cb + lc) * kF1Entries + rel;
+      const int32_t x = fx[slot];
+      cnt += fn[slot];
+      if (x < 0) {
+        res = x == kFnInvalid ? kSupInvalid : x == kFnFallback ? kSupFallback : -3 - (lc * kF1Chunk + (-1 - (int64_t)x));
+        break;
+      }
+      p = lc * kF1Chunk + x;
+    }
+    sx[sidx * kF1Entries + e] = res;
+    sn[sidx * kF1Entries + e] = cnt;
+  }
+}
+
+__global__ void __launch_bounds__(64) f1_top_kernel(const int64_t* nbytes, const int64_t* sup_base, int nruns,
+                                                    const int64_t* sx, const int64_t* sn, int64_t* sup_entry,
+                                                    int64_t* sup_first, int64_t* counts, int64_t* rec_bytes,
+                                                    int* status) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= nruns) return;
+  const int64_t n = nbytes[r];
+  const int64_t sb = sup_base[r];
+  const int64_t span = (int64_t)kF1Super * kF1Chunk;
+  int64_t p = 0, total = 0, rb = n;
+  int st = 0;
+  while (p < n) {
+    const int64_t sidx = p / span;
+    const int64_t rel = p - sidx * span;
+    if (rel >= kF1Entries) {
+      st = 2;
+      break;
+    }
+    const int64_t slot = (sb + sidx) * kF1Entries + rel;
+    const int64_t code = sx[slot];
+    sup_entry[sb + sidx] = p;
+    sup_first[sb + sidx] = total;
+    total += sn[slot];
+    if (code >= 0) {
+      if (code <= p) {  // no progress: cannot happen on a well-formed table
+        st = 1;
+        break;
+      }
+      p = code;
+      continue;
+    }
+    if (code == kSupInvalid) st = 1;
+    else if (code == kSupFallback) st = 2;
+    else rb = -3 - code;
+    break;
+  }
+  if (st == 0 && p > n) st = 1;
+  counts[r] = total;
+  rec_bytes[r] = rb;
+  status[r] = st;
+}
+
+__global__ void __launch_bounds__(256) f1_expand_kernel(const int64_t* nbytes, const int64_t* chunk_base,
+                                                        const int64_t* sup_base, const int32_t* sup_run, int64_t nsup,
+                                                        const int32_t* fx, const int32_t* fn,
+                                                        const int64_t* sup_entry, const int* status,
+                                                        int64_t* ck_start, int64_t* ck_count) {
+  const int64_t sidx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (sidx >= nsup) return;
+  const int r = sup_run[sidx];
+  if (status[r] != 0) return;  // re-indexed by the serial scan (or corrupt)
+  const int64_t n = nbytes[r];
+  const int64_t cb = chunk_base[r];
+  const int64_t nch = chunk_base[r + 1] - cb;
+  const int64_t first = (sidx - sup_base[r]) * kF1Super;
+  const int64_t last = min(first + kF1Super, nch);
+  int64_t p = sup_entry[sidx];
+  for (int64_t lc = first; lc < last; ++lc) {
+    const int64_t cg = cb + lc;
+    const int64_t rel = p - lc * kF1Chunk;
+    if (p < 0 || p >= n || rel >= kF1Chunk || rel >= kF1Entries || rel < 0) {
+      ck_start[cg] = p < 0 ? 0 : p;
+      ck_count[cg] = 0;
+      continue;
+    }
+    const int64_t slot = cg * kF1Entries + rel;
+    const int32_t x = fx[slot];
+    ck_start[cg] = p;
+    ck_count[cg] = fn[slot];
+    p = x < 0 ? -1 : lc * kF1Chunk + x;
   }
 }
 
@@ -409,14 +615,45 @@ void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStr
 
 void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                     int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
-                    hipStream_t s, uint64_t* prof) {
+                    hipStream_t s, uint64_t* prof, const int* run_ids) {
   if (nruns <= 0) return;
   if (prof)
     hipLaunchKernelGGL(f1_scan_kernel<true>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes, chunk_base,
-                       ck_start, ck_count, counts, rec_bytes, status, prof);
+                       ck_start, ck_count, counts, rec_bytes, status, prof, run_ids);
   else
     hipLaunchKernelGGL(f1_scan_kernel<false>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes,
-                       chunk_base, ck_start, ck_count, counts, rec_bytes, status, prof);
+                       chunk_base, ck_start, ck_count, counts, rec_bytes, status, prof, run_ids);
+}
+
+size_t f1_parallel_workspace(int64_t nchunks, int64_t nsup) {
+  return (size_t)nchunks * kF1Entries * 8 + (size_t)nsup * (kF1Entries * 16 + 16) + 256;
+}
+int64_t f1_super_chunks() { return kF1Super; }
+
+void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
+                        const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
+                        int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
+                        int64_t* rec_bytes, int* status, hipStream_t s) {
+  if (nruns <= 0) return;
+  uint8_t* w = static_cast<uint8_t*>(workspace);
+  int32_t* fx = reinterpret_cast<int32_t*>(w);
+  int32_t* fn = fx + nchunks * kF1Entries;
+  int64_t* sx = reinterpret_cast<int64_t*>(fn + nchunks * kF1Entries);
+  int64_t* sn = sx + nsup * kF1Entries;
+  int64_t* sup_entry = sn + nsup * kF1Entries;
+  int64_t* sup_first = sup_entry + nsup;
+  if (nchunks > 0) {
+    hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWaves - 1) / kF1FnWaves)), dim3(64 * kF1FnWaves),
+                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn);
+    hipLaunchKernelGGL(f1_super_kernel, dim3((unsigned)((nsup + 3) / 4)), dim3(256), 0, s, nbytes, chunk_base,
+                       sup_base, sup_run, nsup, fx, fn, sx, sn);
+    (void)hipMemsetAsync(sup_entry, 0xFF, (size_t)nsup * 8, s);
+  }
+  hipLaunchKernelGGL(f1_top_kernel, dim3((unsigned)((nruns + 63) / 64)), dim3(64), 0, s, nbytes, sup_base, nruns,
+                     sx, sn, sup_entry, sup_first, counts, rec_bytes, status);
+  if (nchunks > 0)
+    hipLaunchKernelGGL(f1_expand_kernel, dim3((unsigned)((nsup + 255) / 256)), dim3(256), 0, s, nbytes, chunk_base,
+                       sup_base, sup_run, nsup, fx, fn, sup_entry, status, ck_start, ck_count);
 }
 
 void launch_f1_index(uint8_t* const* bases, const int64_t* nbytes, const int64_t* chunk_base,

@@ -63,21 +63,57 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   if (nchunks > 0)
     HIP_CHECK(hipMemcpyAsync(d_crun, chunk_run.data(), 4 * (size_t)nchunks, hipMemcpyHostToDevice, s));
   static const bool prof_f1 = std::getenv("UDA_F1_PROFILE") != nullptr;
-  DeviceBuffer d_prof;
-  if (prof_f1) d_prof.alloc((size_t)K * 16);
-  launch_f1_scan(d_bases, d_nbytes, K, d_cbase, d_ckstart, d_ckcount, d_counts, d_recb, d_status, s,
-                 prof_f1 ? d_prof.as<uint64_t>() : nullptr);
-  if (prof_f1) {
-    std::vector<uint64_t> pr((size_t)K * 2);
-    HIP_CHECK(hipMemcpyAsync(pr.data(), d_prof.as(), 16 * K, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    uint64_t a = 0, b = 0;
-    for (int k = 0; k < K; ++k) {
-      a += pr[2 * k];
-      b += pr[2 * k + 1];
+  static const bool serial_f1 = std::getenv("UDA_F1_SERIAL") != nullptr;
+  if (serial_f1 || prof_f1) {
+    DeviceBuffer d_prof;
+    if (prof_f1) d_prof.alloc((size_t)K * 16);
+    launch_f1_scan(d_bases, d_nbytes, K, d_cbase, d_ckstart, d_ckcount, d_counts, d_recb, d_status, s,
+                   prof_f1 ? d_prof.as<uint64_t>() : nullptr);
+    if (prof_f1) {
+      std::vector<uint64_t> pr((size_t)K * 2);
+      HIP_CHECK(hipMemcpyAsync(pr.data(), d_prof.as(), 16 * K, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      uint64_t a = 0, b = 0;
+      for (int k = 0; k < K; ++k) {
+        a += pr[2 * k];
+        b += pr[2 * k + 1];
+      }
+      fprintf(stderr, "[F1 profile] runs=%d mean cycles per run: stage=%.0f walk=%.0f\n", K, (double)a / K,
+              (double)b / K);
     }
-    fprintf(stderr, "[F1 profile] runs=%d mean cycles per run: stage=%.0f walk=%.0f\n", K, (double)a / K,
-            (double)b / K);
+  } else {
+    // parallel form: chunk transfer functions composed per superchunk and per run
+    const int64_t SC = f1_super_chunks();
+    std::vector<int64_t> sup_base(K + 1, 0);
+    for (int k = 0; k < K; ++k) sup_base[k + 1] = sup_base[k] + (chunk_base[k + 1] - chunk_base[k] + SC - 1) / SC;
+    const int64_t nsup = sup_base[K];
+    std::vector<int32_t> sup_run((size_t)std::max<int64_t>(nsup, 1));
+    for (int k = 0; k < K; ++k)
+      for (int64_t j = sup_base[k]; j < sup_base[k + 1]; ++j) sup_run[(size_t)j] = k;
+    const size_t wsb = f1_parallel_workspace(nchunks, nsup) + (size_t)(K + 1) * 8 + (size_t)(nsup + 1) * 4 + 64;
+    if (f1ws_.size() < wsb) f1ws_.alloc(wsb);
+    uint8_t* ws = f1ws_.as<uint8_t>();
+    auto* d_supbase = reinterpret_cast<int64_t*>(ws);
+    auto* d_suprun = reinterpret_cast<int32_t*>(ws + (size_t)(K + 1) * 8);
+    uint8_t* d_fws = ws + (((size_t)(K + 1) * 8 + (size_t)(nsup + 1) * 4 + 255) & ~(size_t)255);
+    HIP_CHECK(hipMemcpyAsync(d_supbase, sup_base.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
+    if (nsup > 0) HIP_CHECK(hipMemcpyAsync(d_suprun, sup_run.data(), 4 * (size_t)nsup, hipMemcpyHostToDevice, s));
+    launch_f1_parallel(d_bases, d_nbytes, K, d_cbase, d_crun, nchunks, d_supbase, d_suprun, nsup, d_fws, d_ckstart,
+                       d_ckcount, d_counts, d_recb, d_status, s);
+    std::vector<int> st(K);
+    HIP_CHECK(hipMemcpyAsync(st.data(), d_status, 4 * K, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<int> redo;
+    for (int k = 0; k < K; ++k)
+      if (st[k] == 2) redo.push_back(k);
+    if (!redo.empty()) {  // records longer than the entry table straddle chunks: serial walk
+      DeviceBuffer d_redo(redo.size() * 4);
+      HIP_CHECK(hipMemcpyAsync(d_redo.as(), redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+      launch_f1_scan(d_bases, d_nbytes, (int)redo.size(), d_cbase, d_ckstart, d_ckcount, d_counts, d_recb, d_status,
+                     s, nullptr, d_redo.as<int>());
+      HIP_CHECK(hipStreamSynchronize(s));
+    }
+    f1_serial_runs_ = (int)redo.size();
   }
   std::vector<int64_t> counts(K), recb(K);
   std::vector<int> status(K);

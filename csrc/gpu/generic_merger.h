@@ -29,9 +29,13 @@ class GenericMerger {
   GenericMergeResult merge(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
                            int kind, uint8_t* out, int64_t out_cap, int64_t kv_buf, hipStream_t s);
 
+  // runs the last merge indexed with the serial F1 walk (records longer than the parallel entry table)
+  int f1_serial_runs() const { return f1_serial_runs_; }
+
  private:
+  int f1_serial_runs_ = 0;
   void reserve(int64_t records, int runs);
-  DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_, side_, ck_;
+  DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_, side_, ck_, f1ws_;
   int64_t cap_records_ = 0;
   int cap_runs_ = 0;
 };

@@ -110,7 +110,16 @@ void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int
 int64_t f1_chunk_bytes();
 void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                     int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
-                    hipStream_t s, uint64_t* prof = nullptr);
+                    hipStream_t s, uint64_t* prof = nullptr, const int* run_ids = nullptr);
+// F1 pass 1, parallel form: same outputs as launch_f1_scan from per-chunk transfer functions
+// composed per superchunk (f1_super_chunks() chunks) and per run. sup_base[r]..sup_base[r+1] are
+// run r's superchunks, sup_run their run. status[r] == 2: the run needs the serial scan.
+size_t f1_parallel_workspace(int64_t nchunks, int64_t nsup);
+int64_t f1_super_chunks();
+void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
+                        const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
+                        int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
+                        int64_t* rec_bytes, int* status, hipStream_t s);
 // F1 pass 2 (one wave per chunk): record offsets; ck_ord = exclusive scan of ck_count (global
 // record ordinal of each chunk's first record), elem_off = first ordinal of each run (nruns+1),
 // chunk_run[c] = run of chunk c. offsets[r] has counts[r]+1 entries (last = record bytes).

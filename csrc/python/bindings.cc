@@ -423,7 +423,7 @@ PYBIND11_MODULE(_uda_native, m) {
     std::string out;
     std::vector<int64_t> cuts;
     int64_t records = 0;
-    int passes = 0;
+    int passes = 0, serial_runs = 0;
     double merge_ms = 0;
     {
       py::gil_scoped_release rel;
@@ -455,8 +455,9 @@ PYBIND11_MODULE(_uda_native, m) {
       cuts = res.cuts;
       records = res.records;
       passes = res.passes;
+      serial_runs = gm.f1_serial_runs();
     }
-    return py::make_tuple(py::bytes(out), cuts, records, passes, merge_ms);
+    return py::make_tuple(py::bytes(out), cuts, records, passes, merge_ms, serial_runs);
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
   // F6: decode Hadoop block-compressed streams on the device; returns (raw streams, blocks, decode_ms)
   m.def("gpu_block_decode", [](const std::string& codec_cls, const std::vector<std::string>& streams, int device) {

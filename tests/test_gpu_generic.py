@@ -1,6 +1,7 @@
 """GPU generic merge (F1 record index, F2 normalize + full-key tie-break, F3 merge tree, F4 scan +
 gather) against the CPU reference heap merge: the merged streams must be byte-identical (both
 break key ties by run order, then position)."""
+import os
 import random
 
 import pytest
@@ -30,6 +31,15 @@ def _cases():
     keys = [[text(pref + bytes([rng.randrange(97, 100)]) * rng.randint(0, 3)) for _ in range(200)] for _ in range(4)]
     yield "long-prefix", datagen.TEXT, [encode_stream(sorted([(k, b"x") for k in ks], key=lambda kv: kv[0][1:]))
                                         for ks in keys]
+    # values longer than the parallel F1 entry table: those runs take the serial index walk
+    big = [encode_stream(sorted([(text(b"k%05d" % rng.randrange(10**5)), os.urandom(rng.randint(200, 3000)))
+                                 for _ in range(150)])) for _ in range(3)]
+    yield "long-values", datagen.TEXT, big
+    mixed = [encode_stream(sorted([(text(b"m%05d" % rng.randrange(10**5)),
+                                    os.urandom(rng.randint(600, 900) if rng.random() < 0.02 else rng.randint(0, 40)))
+                                   for _ in range(5000)]))] + \
+        [s[0] for s in datagen.streams(datagen.wordcount(2, 1, 3000, seed=8))]
+    yield "mixed-long", datagen.TEXT, mixed
     yield "empty-runs", datagen.TEXT, [encode_stream([]), encode_stream([(text(b"a"), b"1")]), encode_stream([])]
 
 
@@ -48,6 +58,28 @@ def test_gpu_merge_many_runs(require_gpu):
     runs = [s[0] for s in datagen.streams(datagen.secondary_sort(300, 1, 60, seed=21))]
     g, _ = ops.merge_runs(runs, datagen.TEXT, "gpu")
     c, _ = ops.merge_runs(runs, datagen.TEXT, "cpu")
+    assert g == c
+
+
+def test_gpu_merge_large_runs_parallel_index(require_gpu, native):
+    """Runs spanning many F1 superchunks (256 KiB): the parallel index must be used (no serial
+    fallback) and match the CPU merge byte for byte."""
+    runs = [r[0] for r in native.generate_runs("secondary", 6, 1, 12000, 77)]
+    assert min(len(r) for r in runs) > 3 * 256 * 1024
+    g, _ = ops.merge_runs(runs, datagen.TEXT, "gpu")
+    assert ops.last_stats["f1_serial_runs"] == 0
+    c, _ = ops.merge_runs(runs, datagen.TEXT, "cpu")
+    assert g == c
+
+
+def test_gpu_merge_serial_fallback_counted(require_gpu):
+    rng = random.Random(5)
+    big = [encode_stream(sorted([(text(b"%06d" % rng.randrange(10**6)), os.urandom(1000)) for _ in range(400)]))
+           for _ in range(2)]
+    small = [s[0] for s in datagen.streams(datagen.wordcount(3, 1, 2000, seed=9))]
+    g, _ = ops.merge_runs(big + small, datagen.TEXT, "gpu")
+    assert ops.last_stats["f1_serial_runs"] == 2
+    c, _ = ops.merge_runs(big + small, datagen.TEXT, "cpu")
     assert g == c
 
 

@@ -20,8 +20,9 @@ def merge_runs(runs: list[bytes], key_class: str, device: str = "gpu", kv_buf: i
     if device == "gpu":
         if n.device_count() <= 0:
             raise RuntimeError("merge_runs(device='gpu'): no HIP device visible")
-        merged, cuts, _records, _passes, merge_ms = n.gpu_merge_runs(list(runs), key_class, kv_buf - 2, gpu_index)
-        last_stats.update(device="gpu", records=_records, passes=_passes, merge_ms=merge_ms)
+        merged, cuts, _records, _passes, merge_ms, serial = n.gpu_merge_runs(list(runs), key_class, kv_buf - 2,
+                                                                             gpu_index)
+        last_stats.update(device="gpu", records=_records, passes=_passes, merge_ms=merge_ms, f1_serial_runs=serial)
         return merged, cuts
     if device == "cpu":
         out, lens = n.cpu_merge(list(runs), key_class, kv_buf)
