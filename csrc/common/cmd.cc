@@ -13,16 +13,27 @@ bool parse_cmd(const std::string& s, HadoopCmd* out) {
     out->header = kExitMsg;
     return true;
   }
+  // count and header must be decimal numbers and the header a known command id (the reference's
+  // atoi would turn a garbled header into EXIT)
+  auto number = [](const std::string& t, int* v) {
+    if (t.empty() || t.size() > 9) return false;
+    for (char c : t)
+      if (c < '0' || c > '9') return false;
+    *v = std::atoi(t.c_str());
+    return true;
+  };
   size_t p = s.find(':');
   if (p == std::string::npos) return false;
-  out->count = std::atoi(s.substr(0, p).c_str());
+  int count = 0, header = 0;
+  if (!number(s.substr(0, p), &count)) return false;
+  out->count = count;
   size_t start = p + 1;
   size_t end = s.find(':', start);
-  if (end == std::string::npos) {
-    out->header = (CmdId)std::atoi(s.substr(start).c_str());
-    return true;
-  }
-  out->header = (CmdId)std::atoi(s.substr(start, end - start).c_str());
+  if (!number(s.substr(start, end == std::string::npos ? std::string::npos : end - start), &header) ||
+      header > (int)kRtLaunched)
+    return false;
+  out->header = (CmdId)header;
+  if (end == std::string::npos) return true;
   start = end + 1;
   // count-1 params; all but the last are ':'-terminated, the last takes the remainder.
   for (int i = 0; i < out->count - 2; ++i) {

@@ -104,3 +104,11 @@ def test_raw_and_bytes_comparators(native):
     bw = lambda s: len(s).to_bytes(4, "big") + s  # noqa: E731
     assert native.key_compare(2, bw(b"abc"), bw(b"abd")) < 0
     assert native.key_compare(2, bw(b"b"), bw(b"abc")) > 0   # length prefix is skipped, not compared
+
+
+def test_parse_cmd_rejects_garbled_headers(native):
+    import pytest as _pytest
+    for bad in ["3:this-is-not-a-command", "x:7:a:b", "2:12:p", "2:-1:p", ":7", "nocolon"]:
+        with _pytest.raises(ValueError):
+            native.parse_cmd(bad)
+    assert native.parse_cmd("2:4:p")[1] == 4

@@ -2,8 +2,8 @@
 """Build the native runtime in-tree for gfx950 (MI355X).
 
 Produces
-  uda_amd/lib/libuda.so                    -- the native library (C ABI `uda_*` + engine + HIP kernels;
-                                              plus the JNI entry points when a JDK's jni.h is found)
+  uda_amd/lib/libuda.so                    -- the native library (C ABI `uda_*` + engine + HIP kernels +
+                                              the UdaBridge JNI entry points, declared in-tree, no JDK needed)
   uda_amd/_uda_native<EXT_SUFFIX>          -- pybind11 module linked against libuda.so
 
 Everything is compiled with hipcc (`--offload-arch=gfx950`); `.hip` files carry device code, `.cc`
@@ -25,17 +25,6 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 
-def find_jni_include() -> list[str]:
-    home = os.environ.get("JAVA_HOME")
-    cands = [home] if home else []
-    cands += glob.glob("/usr/lib/jvm/*")
-    for c in cands:
-        if c and os.path.exists(os.path.join(c, "include", "jni.h")):
-            inc = os.path.join(c, "include")
-            return [inc, os.path.join(inc, "linux")]
-    return []
-
-
 def sources() -> tuple[list[str], list[str]]:
     lib = []
     for pat in ("common/*.cc", "engine/*.cc", "provider/*.cc", "consumer/*.cc", "transport/*.cc",
@@ -49,14 +38,11 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
     import pybind11
 
     lib_srcs, mod_srcs = sources()
-    jni = find_jni_include()
     opt = "-O1 -g" if debug else "-O3 -g1"
     common = (f"-std=c++17 -fPIC {opt} -Wall -Wno-unused-function -Wno-unused-variable "
               f"-Wno-unused-command-line-argument -Wno-pass-failed "
               f"-I{ROOT}/csrc/include -I{ROOT}/csrc -I{ROOT}/csrc/gpu -I{ROCM}/include "
               f"-D__HIP_PLATFORM_AMD__=1")
-    if jni:
-        common += " -DUDA_HAVE_JNI=1 " + " ".join(f"-I{p}" for p in jni)
     host_san = ""
     if sanitize:
         # sanitizers apply to host code only (no GPU ASan on this pool)
