@@ -482,7 +482,8 @@ std::string ReduceTask::stats_json() const {
     << ",\"bytes_fetched\":" << s.bytes_fetched << ",\"bytes_delivered\":" << s.bytes_delivered
     << ",\"records\":" << s.records << ",\"buffers\":" << s.buffers << ",\"lpqs\":" << s.lpqs
     << ",\"spill_bytes\":" << s.spill_bytes << ",\"fetch_ms\":" << s.fetch_ms << ",\"merge_ms\":" << s.merge_ms
-    << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+    << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
+    << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }
 

@@ -41,6 +41,7 @@ struct ReduceStats {
   double fetch_ms = 0, merge_ms = 0, total_ms = 0;
   double wait_ms = 0;             // time the merge waited on the network (total_wait_mem_time)
   int64_t device_decoded_blocks = 0;  // compressed blocks decoded in HBM by the F6 kernels
+  int64_t rpq_rounds = 0;             // GPU hybrid: key-range rounds of the RPQ merge
   std::string backend;
 };
 

@@ -416,6 +416,46 @@ PYBIND11_MODULE(_uda_native, m) {
 
   // ---------------------------------------------------------------- GPU engine
   m.def("device_count", &gpu::device_count);
+  // N8 device discovery: per-pair P2P reachability, link type (HSA_AMD_LINK_INFO_TYPE_*: 2 = xGMI) and
+  // hop count, and the runtime's relative performance rank.
+  m.def("device_topology", []() {
+    py::dict d;
+    int n = gpu::device_count();
+    d["devices"] = n;
+    py::list props, links;
+    for (int i = 0; i < n; ++i) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+      py::dict e;
+      e["name"] = std::string(p.name);
+      e["arch"] = std::string(p.gcnArchName);
+      e["cus"] = p.multiProcessorCount;
+      e["hbm_bytes"] = (int64_t)p.totalGlobalMem;
+      e["lds_bytes"] = (int64_t)p.sharedMemPerBlock;
+      e["l2_bytes"] = p.l2CacheSize;
+      e["pci_bus"] = p.pciBusID;
+      props.append(e);
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        int can = 0, rank = -1;
+        uint32_t type = 0, hops = 0;
+        (void)hipDeviceCanAccessPeer(&can, i, j);
+        (void)hipDeviceGetP2PAttribute(&rank, hipDevP2PAttrPerformanceRank, i, j);
+        (void)hipExtGetLinkTypeAndHopCount(i, j, &type, &hops);
+        py::dict l;
+        l["src"] = i;
+        l["dst"] = j;
+        l["p2p"] = can != 0;
+        l["link_type"] = type;
+        l["hops"] = hops;
+        l["perf_rank"] = rank;
+        links.append(l);
+      }
+    }
+    d["props"] = props;
+    d["links"] = links;
+    return d;
+  });
   m.def("gpu_merge_runs", [](const std::vector<std::string>& runs, const std::string& key_class, int64_t kv_buf,
                              int device) {
     KeyKind kind = key_kind_from_class(key_class.c_str());

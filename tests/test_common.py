@@ -112,3 +112,16 @@ def test_parse_cmd_rejects_garbled_headers(native):
         with _pytest.raises(ValueError):
             native.parse_cmd(bad)
     assert native.parse_cmd("2:4:p")[1] == 4
+
+
+def test_topology_plan_and_peer_order():
+    from uda_amd.utils import topology
+    t = topology.topology()
+    assert t["devices"] >= 0 and isinstance(t["links"], list)
+    for w in (1, 2, 4, 8):
+        for r in range(w):
+            order = topology.peer_order(r, w)
+            assert sorted(s for s, _ in order) == sorted(set(range(w)) - {r})
+            assert sorted(f for _, f in order) == sorted(set(range(w)) - {r})
+    p = topology.shuffle_plan(8, 130 << 30)
+    assert p["rounds"] >= 1 and p["bytes_per_round"] * p["rounds"] <= 130 << 30

@@ -102,3 +102,33 @@ def test_consumer_gpu_backend(require_gpu, tmp_path):
         assert sorted(recs_gpu) == sorted(recs_cpu)
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("tier,codec", [("host", None), ("disk", None), ("disk", "snappy")])
+def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
+    """Reduce input larger than the device budget: LPQ merges on the GPU spill to host DRAM or to
+    the local dirs (AsyncIO), then RPQ key-range rounds merge the spilled runs on the GPU."""
+    from uda_amd.utils.mof import write_mof
+    p = UdaProvider()
+    try:
+        maps = datagen.secondary_sort(num_maps=12, reducers=2, rows_per_map=2000, seed=6)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_h{tier}{codec}_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts, codec=codec)
+            p.add_mof_file(f"job_h{tier}{codec}", mid, path)
+            ids.append(mid)
+        d1 = tmp_path / "ld1"
+        d1.mkdir()
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.merge.bytes": 300_000,
+                "mapred.uda.gpu.spill": tier}
+        recs, st, c = run_reduce("h", f"job_h{tier}{codec}", ids, 0, datagen.TEXT, codec=codec, conf=conf,
+                                 kv_buf_size=8192, local_dirs=(str(d1),))
+        assert st["lpqs"] >= 4 and st["rpq_rounds"] >= 3, st
+        want = sorted((kv for m in maps for kv in m[0]), key=datagen.sort_key(datagen.TEXT))
+        kf = datagen.sort_key(datagen.TEXT)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+        assert sorted(recs) == sorted(want)
+        assert not os.listdir(d1)  # spill files are transient
+    finally:
+        p.close()
