@@ -1,4 +1,5 @@
 #include "reduce_task.h"
+#include "uda/fault.h"
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -238,6 +239,7 @@ void ReduceTask::on_init(const InitParams& p) {
   buffer_size_ = max_buf - max_buf % page;
   if (buffer_size_ <= 0 || buffer_size_ < p.min_buf_bytes) throw UdaError("RDMA Buffer is too small");
   free_pairs_ = num_kv_bufs_ + kExtraBuffers;
+  if (fault_hit("HOST_ALLOC")) throw UdaError("injected allocation failure for the fetch buffer pool");
   kv_buf_size_ = host_->conf_i64("mapred.uda.kv.buf.size", 1 << 20);
   backend_ = host_->get_conf("mapred.uda.merge.backend", "cpu");
   const std::string tr = host_->get_conf("mapred.uda.transport", "loopback");

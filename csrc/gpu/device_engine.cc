@@ -1,5 +1,6 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
+#include "uda/fault.h"
 
 #include <rccl/rccl.h>
 
@@ -39,6 +40,7 @@ DeviceBuffer::~DeviceBuffer() { reset(); }
 void DeviceBuffer::alloc(size_t bytes) {
   reset();
   if (bytes == 0) return;
+  if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
   HIP_CHECK(hipMalloc(&ptr_, bytes));
   size_ = bytes;
 }

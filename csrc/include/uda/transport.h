@@ -90,8 +90,7 @@ std::unique_ptr<ServerTransport> make_loopback_server(const std::string& host);
 std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits);
 std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits);
 
-// Fault injection for tests (env UDA_FAULT_FETCH=<n>: the n-th fetch fails).
+// Fault injection for tests (env UDA_FAULT_FETCH=<n>: the n-th fetch fails; see uda/fault.h).
 bool fault_should_fail_fetch();
-void fault_reset();
 
 }  // namespace uda

@@ -1,5 +1,6 @@
 // AsyncIO backends: io_uring via raw syscalls, and a pread/pwrite thread pool fallback.
 #include "uda/aio.h"
+#include "uda/fault.h"
 
 #include <errno.h>
 #include <fcntl.h>
@@ -311,14 +312,35 @@ class UringIO : public AsyncIO {
 
 }  // namespace
 
+namespace {
+// Fault-injection decorator (UDA_FAULT_AIO=<n>: the n-th operation completes with -EIO).
+class FaultIO : public AsyncIO {
+ public:
+  explicit FaultIO(std::unique_ptr<AsyncIO> in) : in_(std::move(in)) {}
+  void read(int fd, int64_t off, int64_t len, void* dst, IoDone cb) override {
+    if (fault_hit("AIO")) return cb(-EIO);
+    in_->read(fd, off, len, dst, std::move(cb));
+  }
+  void write(int fd, int64_t off, int64_t len, const void* src, IoDone cb) override {
+    if (fault_hit("AIO")) return cb(-EIO);
+    in_->write(fd, off, len, src, std::move(cb));
+  }
+  void drain() override { in_->drain(); }
+  const char* backend() const override { return in_->backend(); }
+  int64_t inflight() const override { return in_->inflight(); }
+
+ private:
+  std::unique_ptr<AsyncIO> in_;
+};
+}  // namespace
+
 std::unique_ptr<AsyncIO> AsyncIO::create(const Options& o) {
   const char* env = std::getenv("UDA_AIO_BACKEND");
   bool uring = o.prefer_uring && !(env && std::string(env) == "threadpool");
-  if (uring) {
-    auto u = UringIO::try_create(o.queue_depth);
-    if (u) return u;
-  }
-  return std::make_unique<PoolIO>(o.threads);
+  std::unique_ptr<AsyncIO> io;
+  if (uring) io = UringIO::try_create(o.queue_depth);
+  if (!io) io = std::make_unique<PoolIO>(o.threads);
+  return std::make_unique<FaultIO>(std::move(io));
 }
 
 }  // namespace uda

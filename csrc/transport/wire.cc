@@ -5,6 +5,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "uda/fault.h"
 #include "uda/transport.h"
 
 namespace uda {
@@ -83,16 +84,6 @@ bool parse_ack(const std::string& s, FetchAck* a) {
 }
 
 // ------------------------------------------------------------------------- fault injection
-namespace {
-std::atomic<long> g_fetch_count{0};
-}
-bool fault_should_fail_fetch() {
-  const char* e = std::getenv("UDA_FAULT_FETCH");
-  if (!e || !*e) return false;
-  long n = std::atol(e);
-  long c = ++g_fetch_count;
-  return n > 0 && c == n;
-}
-void fault_reset() { g_fetch_count = 0; }
+bool fault_should_fail_fetch() { return fault_hit("FETCH"); }
 
 }  // namespace uda

@@ -164,3 +164,24 @@ def test_cpu_merge_binding_matches_python(native):
     out, lens = native.cpu_merge(runs, datagen.TEXT, 4096)
     assert all(n <= 4096 for n in lens) and out.endswith(EOF_MARKER)
     check_output(decode_stream(out), expected(maps, 0, datagen.TEXT), datagen.TEXT)
+
+
+def test_injected_aio_fault_fails_once(provider, tmp_path, monkeypatch):
+    """A disk read error on the provider (io_uring completion -EIO) surfaces as exactly one
+    failureInUda on the consumer (SURVEY §7.4 fault matrix)."""
+    maps = datagen.wordcount(num_maps=3, reducers=1, words_per_map=2000, seed=21)
+    ids = publish(provider, tmp_path, "job_1_0008", maps, on_disk=True)
+    monkeypatch.setenv("UDA_FAULT_AIO", "2")
+    c = UdaConsumer(len(ids), "job_1_0008", "attempt_job_1_0008_r_000000_0", datagen.TEXT, max_buf_kb=16)
+    for m in ids:
+        c.fetch("h", "job_1_0008", m, 0)
+    with pytest.raises(UdaFallback):
+        c.wait(30)
+    c.close()
+    assert c.failure_calls == 1
+
+
+def test_injected_host_alloc_fault_raises_on_init(monkeypatch):
+    monkeypatch.setenv("UDA_FAULT_HOST_ALLOC", "1")
+    with pytest.raises(RuntimeError, match="UdaRuntimeException"):
+        UdaConsumer(2, "job_1_0009", "attempt_job_1_0009_r_000000_0", datagen.TEXT)

@@ -1,0 +1,151 @@
+"""Multi-process paths on the CPU: the torch.distributed control plane the bench uses between GPU
+ranks (gloo, world 2), and the TCP transport with the MOFSupplier and the NetMerger in different
+processes (the reference's cross-node shuffle, RDMAServer/RDMAClient, over sockets)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from uda_amd.bridge import UdaConsumer, UdaFallback
+from uda_amd.utils import datagen
+from uda_amd.utils.ifile import decode_stream  # noqa: F401
+from uda_amd.utils.mof import write_mof
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _control_plane_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import numpy as np
+
+    from uda_amd.parallel.dist import init_from_env
+    from uda_amd.parallel.plan import round_bounds
+    ctx = init_from_env()
+    try:
+        uid = ctx.broadcast_bytes(b"unique-id-from-rank0" if rank == 0 else None)
+        g = ctx.all_gather_object({"rank": rank})
+        sums = ctx.sum_u64([(1 << 63) + rank, 5])
+        mx = ctx.max_float(float(rank) + 0.5)
+        # the bench's bound planning: every rank contributes key samples per destination
+        rng = np.random.default_rng(rank)
+        local = [np.sort(rng.integers(0, 2**63, size=(50, 2), dtype=np.uint64), axis=0) for _ in range(world)]
+        gathered = ctx.all_gather_object(local)
+        per_dest = [np.concatenate([gg[d] for gg in gathered]) for d in range(world)]
+        bounds = round_bounds(per_dest, 4)
+        q.put((rank, uid, [x["rank"] for x in g], sums, mx, bounds.tobytes()))
+        ctx.barrier()
+    finally:
+        ctx.close()
+
+
+def test_control_plane_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_control_plane_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        _, uid, ranks, sums, mx, bounds = res[r]
+        assert uid == b"unique-id-from-rank0"
+        assert ranks == [0, 1]
+        assert sums == [((1 << 63) * 2 + 1) % (1 << 64), 10]
+        assert mx == 1.5
+    assert res[0][5] == res[1][5]  # identical round bounds on every rank
+
+
+PROVIDER = r"""
+import json, sys
+sys.path.insert(0, sys.argv[3])
+from uda_amd.bridge import UdaProvider
+p = UdaProvider(transport="tcp", data_port=int(sys.argv[1]))
+for job, mid, path in json.loads(sys.argv[2]):
+    p.add_mof_file(job, mid, path)
+print("READY", flush=True)
+sys.stdin.read()
+p.close()
+print(p.stats(), flush=True)
+"""
+
+
+@pytest.fixture
+def tcp_provider(tmp_path):
+    procs = []
+
+    def start(mofs):
+        port = _free_port()
+        proc = subprocess.Popen([sys.executable, "-c", PROVIDER, str(port), json.dumps(mofs), ROOT],
+                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        assert proc.stdout.readline().strip() == "READY"
+        procs.append(proc)
+        return port, proc
+
+    yield start
+    for proc in procs:
+        if proc.poll() is None:
+            proc.stdin.close()
+            try:
+                proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+
+
+@pytest.mark.parametrize("codec", [None, "lzo"])
+def test_tcp_transport_across_processes(tmp_path, tcp_provider, codec):
+    maps = datagen.secondary_sort(num_maps=7, reducers=3, rows_per_map=800, seed=17)
+    job = "job_tcp_" + (codec or "raw")
+    mofs = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        path, _ = write_mof(str(tmp_path), mid, parts, codec=codec)
+        mofs.append((job, mid, path))
+    port, proc = tcp_provider(mofs)
+    consumers = [UdaConsumer(len(mofs), job, f"attempt_{job}_r_{r:06d}_0", datagen.TEXT, codec=codec,
+                             transport="tcp", data_port=port, max_buf_kb=16, kv_buf_size=16384)
+                 for r in range(3)]
+    for r, c in enumerate(consumers):  # all reducers fetch concurrently over one connection each
+        for _, mid, _ in mofs:
+            c.fetch("127.0.0.1", job, mid, r)
+    kf = datagen.sort_key(datagen.TEXT)
+    for r, c in enumerate(consumers):
+        recs = c.wait(120)
+        st = c.close()
+        want = sorted((kv for m in maps for kv in m[r]), key=kf)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+        assert sorted(recs) == sorted(want)
+        assert st["maps_fetched"] == len(mofs)
+    proc.stdin.close()
+    assert proc.wait(timeout=30) == 0
+    stats = json.loads(proc.stdout.read().strip().splitlines()[-1])
+    assert stats["bytes_served"] > 0
+
+
+def test_tcp_unreachable_provider_fails_once():
+    port = _free_port()  # nothing listens here
+    c = UdaConsumer(1, "job_tcp_none", "attempt_job_tcp_none_r_000000_0", datagen.TEXT, transport="tcp",
+                    data_port=port)
+    c.fetch("127.0.0.1", "job_tcp_none", "attempt_job_tcp_none_m_000000_0", 0)
+    with pytest.raises(UdaFallback):
+        c.wait(60)
+    c.close()
+    assert c.failure_calls == 1

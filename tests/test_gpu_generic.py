@@ -132,3 +132,28 @@ def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
         assert not os.listdir(d1)  # spill files are transient
     finally:
         p.close()
+
+
+def test_consumer_gpu_device_alloc_fault_fails_once(require_gpu, tmp_path, monkeypatch):
+    from uda_amd.bridge import UdaConsumer, UdaFallback
+    from uda_amd.utils.mof import write_mof
+    p = UdaProvider()
+    try:
+        maps = datagen.wordcount(num_maps=3, reducers=1, words_per_map=1000, seed=2)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_fa_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts)
+            p.add_mof_file("job_fa", mid, path)
+            ids.append(mid)
+        monkeypatch.setenv("UDA_FAULT_DEVICE_ALLOC", "1")
+        c = UdaConsumer(len(ids), "job_fa", "attempt_job_fa_r_000000_0", datagen.TEXT,
+                        conf={"mapred.uda.merge.backend": "gpu"})
+        for m in ids:
+            c.fetch("h", "job_fa", m, 0)
+        with pytest.raises(UdaFallback, match="injected"):
+            c.wait(60)
+        c.close()
+        assert c.failure_calls == 1
+    finally:
+        p.close()
