@@ -8,6 +8,7 @@
   secondary_sort      variable-length Text keys with long common prefixes + partition skew: GPU generic
                       merge (F1/F2/F3/F4 kernels) vs the CPU heap merge on the same runs.
   decode              F6 Snappy / LZO1X block decode on the device vs the host decoder.
+  aio                 AsyncIO (io_uring / thread pool, O_DIRECT) read bandwidth vs sequential pread.
   spill               TeraSort whose map outputs live in pinned host DRAM (the spill tier used when a
                       job exceeds HBM): rounds are streamed H2D, merged on the GPU, delivered D2H.
 
@@ -127,6 +128,20 @@ def decode(args) -> dict:
             "host_1thread_gbps_raw": round(raw / host_s / 1e9, 3), "host_compress_s": round(comp_s, 1)}
 
 
+def aio(args) -> dict:
+    """AsyncIO read bandwidth vs a sequential pread loop (the reference's AIOHandler_test)."""
+    from uda_amd import native
+    path = os.path.join(args.dir, "uda_aio_bench.bin")
+    size = int(args.gb * 1e9) // (1 << 20) * (1 << 20)
+    out = {"config": "AIO microbenchmark (io_uring, O_DIRECT, 1 MiB blocks)", "gb": round(size / 1e9, 3)}
+    for be in ("", "threadpool"):
+        r = native().aio_bench(path, size, 1 << 20, 16, True, be)
+        out[(r["backend"]) + "_mbps"] = round(r["aio_mbps"], 1)
+        out["sequential_mbps"] = round(r["sequential_mbps"], 1)
+        assert r["ok"]
+    return out
+
+
 def spill(args) -> dict:
     import torch  # noqa: F401
     from uda_amd.models.terasort import TeraSortConfig, TeraSortShuffle
@@ -148,7 +163,8 @@ def spill(args) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode"])
+    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode", "aio"])
+    ap.add_argument("--dir", default="/tmp")
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lzo"])
     ap.add_argument("--gb", type=float, default=1.0)
     ap.add_argument("--maps", type=int, default=16)

@@ -58,6 +58,19 @@ struct SpillRun {
   std::vector<std::string> key;   // key bytes of the record at each cut
 };
 
+// Device buffers reused across the merges of one reduce task (LPQ groups, RPQ rounds): HBM is
+// allocated once at the high-water mark instead of per merge (hipMalloc/hipFree of GBs costs ms and
+// hipFree synchronizes the device).
+struct DeviceWorkspace {
+  gpu::DeviceBuffer in, out, packed;
+  gpu::GenericMerger merger;
+  gpu::DeviceBlockDecoder decoder;
+  static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
+    bytes = std::max<int64_t>(bytes, 16);
+    if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
+  }
+};
+
 struct StreamGuard {
   hipStream_t s = nullptr;
   ~StreamGuard() {
@@ -67,9 +80,9 @@ struct StreamGuard {
 
 // Merge host-resident runs on the device. `codec` != kNone: the runs are block-compressed streams
 // decoded in HBM (falls back to a host decode when the framing needs it).
-DeviceMergeOut device_merge(std::vector<std::vector<uint8_t>>* parts_in, const std::vector<const uint8_t*>* views,
-                            const std::vector<int64_t>* view_lens, Codec codec, KeyKind kind, int64_t spacing,
-                            hipStream_t s) {
+DeviceMergeOut device_merge(DeviceWorkspace& ws, std::vector<std::vector<uint8_t>>* parts_in,
+                            const std::vector<const uint8_t*>* views, const std::vector<int64_t>* view_lens, Codec codec,
+                            KeyKind kind, int64_t spacing, hipStream_t s) {
   std::vector<const uint8_t*> ptrs;
   std::vector<int64_t> lens;
   if (parts_in) {
@@ -107,9 +120,12 @@ DeviceMergeOut device_merge(std::vector<std::vector<uint8_t>>* parts_in, const s
   int64_t staged = 0;
   for (auto l : lens) staged += l;
   const int64_t total = decode_on_device ? plan.raw_total : staged;
-  gpu::DeviceBuffer in((size_t)std::max<int64_t>(total, 16)), out((size_t)std::max<int64_t>(total, 16));
-  gpu::DeviceBuffer packed(decode_on_device ? (size_t)std::max<int64_t>(staged, 16) : 0);
-  uint8_t* stage = decode_on_device ? packed.as<uint8_t>() : in.as<uint8_t>();
+  DeviceWorkspace::ensure(ws.in, total);
+  DeviceWorkspace::ensure(ws.out, total);
+  if (decode_on_device) DeviceWorkspace::ensure(ws.packed, staged);
+  gpu::DeviceBuffer& in = ws.in;
+  gpu::DeviceBuffer& out = ws.out;
+  uint8_t* stage = decode_on_device ? ws.packed.as<uint8_t>() : in.as<uint8_t>();
   std::vector<const uint8_t*> runs;
   std::vector<int64_t> bytes;
   int64_t off = 0;
@@ -126,8 +142,7 @@ DeviceMergeOut device_merge(std::vector<std::vector<uint8_t>>* parts_in, const s
   }
   DeviceMergeOut res;
   if (decode_on_device) {
-    gpu::DeviceBlockDecoder dec;
-    dec.decode(codec, plan, packed.as<uint8_t>(), in.as<uint8_t>(), s);
+    ws.decoder.decode(codec, plan, ws.packed.as<uint8_t>(), in.as<uint8_t>(), s);
     res.decoded_blocks = (int64_t)plan.descs.size();
   }
   if (parts_in) {  // the host copies are no longer needed once staged
@@ -136,8 +151,7 @@ DeviceMergeOut device_merge(std::vector<std::vector<uint8_t>>* parts_in, const s
     parts_in->shrink_to_fit();
   }
   host_raw.clear();
-  gpu::GenericMerger merger;
-  gpu::GenericMergeResult r = merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s);
+  gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s);
   res.bytes.resize((size_t)r.bytes);
   if (r.bytes) HIP_CHECK(hipMemcpyAsync(res.bytes.data(), out.as(), (size_t)r.bytes, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -179,6 +193,7 @@ void ReduceTask::merge_gpu() {
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
+  DeviceWorkspace ws;
 
   std::vector<SpillRun> spills;
   std::vector<std::vector<uint8_t>> group;
@@ -201,7 +216,7 @@ void ReduceTask::merge_gpu() {
   // LPQ: merge the current group on the device and spill it with its sparse index
   auto spill_group = [&] {
     if (group.empty()) return;
-    DeviceMergeOut m = device_merge(&group, nullptr, nullptr, stage_codec, kind_, kSampleSpacing, s);
+    DeviceMergeOut m = device_merge(ws, &group, nullptr, nullptr, stage_codec, kind_, kSampleSpacing, s);
     count_decoded(m.decoded_blocks);
     group.clear();
     group_raw = 0;
@@ -347,7 +362,7 @@ void ReduceTask::merge_gpu() {
 
     if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
-      DeviceMergeOut m = device_merge(&group, nullptr, nullptr, stage_codec, kind_, kv, s);
+      DeviceMergeOut m = device_merge(ws, &group, nullptr, nullptr, stage_codec, kind_, kv, s);
       count_decoded(m.decoded_blocks);
       deliver(m, true);
     } else {
@@ -451,7 +466,7 @@ void ReduceTask::merge_gpu() {
           }
           lens.push_back(e - b);
         }
-        DeviceMergeOut m = device_merge(nullptr, &views, &lens, Codec::kNone, kind_, kv, s);
+        DeviceMergeOut m = device_merge(ws, nullptr, &views, &lens, Codec::kNone, kind_, kv, s);
         deliver(m, q + 1 == rounds);
       }
     }

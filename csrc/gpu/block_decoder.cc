@@ -6,6 +6,7 @@
 #include <string>
 
 #include "uda/error.h"
+#include "uda/trace.h"
 
 namespace uda {
 namespace gpu {
@@ -62,6 +63,7 @@ void DeviceBlockDecoder::decode(Codec codec, const BlockPlan& plan, const uint8_
                                 hipStream_t s) {
   const int n = (int)plan.descs.size();
   if (n == 0) return;
+  trace::Range tr("uda.block_decode");
   const size_t bytes = (size_t)n * sizeof(DecodeDesc);
   if (descs_.size() < bytes) descs_.alloc(bytes);
   if (status_.size() < sizeof(int)) status_.alloc(sizeof(int));

@@ -1,6 +1,7 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
 #include "uda/fault.h"
+#include "uda/trace.h"
 
 #include <rccl/rccl.h>
 
@@ -606,6 +607,7 @@ void ShuffleJob::deliver_loop() {
       p = piece_q_.front();
       piece_q_.pop_front();
     }
+    trace::Range tr_piece("uda.deliver_piece");
     HIP_CHECK(hipEventSynchronize(piece_events_[(size_t)p.slot * NS]));  // joins every copy stream
     float ms = 0;
     if (p.bytes > 0 && hipEventElapsedTime(&ms, piece_start_ev_[p.slot], piece_events_[(size_t)p.slot * NS]) == hipSuccess)
@@ -648,6 +650,7 @@ void ShuffleJob::deliver_loop() {
 }
 
 StepStats ShuffleJob::run_step() {
+  trace::Range tr_step("uda.step");
   HIP_CHECK(hipSetDevice(cfg_.device));
   if (!merger_) throw std::runtime_error("run_step before plan()");
   StepStats st;
@@ -680,6 +683,7 @@ StepStats ShuffleJob::run_step() {
 
   int64_t bytes_sent = 0;
   for (int q = 0; q < Q; ++q) {
+    trace::Range tr_round("uda.round");
     const int slot = q % kSlots;
     const RoundPlan& rp = plans[q];
     std::vector<RunDesc> runs;

@@ -1,5 +1,7 @@
 #include "generic_merger.h"
 
+#include "uda/trace.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +27,7 @@ void GenericMerger::reserve(int64_t records, int runs) {
 
 GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
                                         int kind, uint8_t* out, int64_t out_cap, int64_t kv_buf, hipStream_t s) {
+  trace::Range tr("uda.generic_merge");
   GenericMergeResult res;
   const int K = (int)runs.size();
   if (K == 0) {

@@ -351,6 +351,68 @@ PYBIND11_MODULE(_uda_native, m) {
     return py::make_tuple(std::string(io->backend()), bad.load() == 0 && src == dst);
   });
 
+  // AIO microbenchmark (AIOHandler_test parity, src/tests/AIOHandler_test.cc:244-249): read `size`
+  // bytes of `path` in `block` pieces with up to `depth` in flight through AsyncIO (O_DIRECT when
+  // `direct`), then with a sequential pread loop; returns MB/s of both.
+  m.def("aio_bench", [](const std::string& path, int64_t size, int64_t block, int depth, bool direct,
+                        const std::string& backend) {
+    py::gil_scoped_release rel;
+    {
+      int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+      if (fd < 0) throw std::runtime_error("open for write failed");
+      std::vector<uint8_t> buf((size_t)(8 << 20));
+      for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 2654435761u >> 13);
+      for (int64_t off = 0; off < size; off += (int64_t)buf.size()) {
+        const size_t n = (size_t)std::min<int64_t>((int64_t)buf.size(), size - off);
+        if (::pwrite(fd, buf.data(), n, off) != (ssize_t)n) throw std::runtime_error("pwrite failed");
+      }
+      ::fsync(fd);
+      ::close(fd);
+    }
+    if (!backend.empty()) setenv("UDA_AIO_BACKEND", backend.c_str(), 1);
+    AsyncIO::Options o;
+    o.queue_depth = std::max(depth, 1);
+    auto io = AsyncIO::create(o);
+    unsetenv("UDA_AIO_BACKEND");
+    int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
+    if (fd < 0 && direct) fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);  // tmpfs: no O_DIRECT
+    if (fd < 0) throw std::runtime_error("open for read failed");
+    const int nbuf = std::max(depth, 1);
+    std::vector<void*> bufs;
+    for (int i = 0; i < nbuf; ++i) bufs.push_back(aligned_alloc_io((size_t)block));
+    std::atomic<int64_t> bad{0}, got{0};
+    auto t0 = std::chrono::steady_clock::now();
+    int64_t off = 0;
+    while (off < size) {
+      for (int i = 0; i < nbuf && off < size; ++i, off += block)
+        io->read(fd, off, std::min(block, size - off), bufs[(size_t)i], [&](int64_t r) {
+          if (r < 0) bad++;
+          else got += r;
+        });
+      io->drain();
+    }
+    const double aio_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    t0 = std::chrono::steady_clock::now();
+    int64_t seq = 0;
+    for (int64_t o2 = 0; o2 < size; o2 += block) {
+      const ssize_t r = ::pread(fd, bufs[0], (size_t)std::min(block, size - o2), o2);
+      if (r <= 0) break;
+      seq += r;
+    }
+    const double seq_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ::close(fd);
+    for (void* b : bufs) aligned_free_io(b);
+    ::unlink(path.c_str());
+    py::gil_scoped_acquire acq;
+    py::dict d;
+    d["backend"] = std::string(io->backend());
+    d["ok"] = bad.load() == 0 && got.load() == size && seq == size;
+    d["aio_mbps"] = size / aio_s / 1e6;
+    d["sequential_mbps"] = size / seq_s / 1e6;
+    return d;
+  }, py::arg("path"), py::arg("size"), py::arg("block") = 1 << 20, py::arg("depth") = 16, py::arg("direct") = true,
+     py::arg("backend") = "");
+
   // ---------------------------------------------------------------- bridge (C ABI)
   py::class_<PyBridge, std::shared_ptr<PyBridge>>(m, "Bridge")
       .def(py::init([](bool is_net_merger, const std::vector<std::string>& args, int log_level, py::object fetch_over,
