@@ -8,6 +8,8 @@
   secondary_sort      variable-length Text keys with long common prefixes + partition skew: GPU generic
                       merge (F1/F2/F3/F4 kernels) vs the CPU heap merge on the same runs.
   decode              F6 Snappy / LZO1X block decode on the device vs the host decoder.
+  netmerger           secondary-sort data through provider -> NetMerger -> dataFromUda: CPU heap merge vs
+                      GPU backend (online and hybrid LPQ/RPQ).
   aio                 AsyncIO (io_uring / thread pool, O_DIRECT) read bandwidth vs sequential pread.
   spill               TeraSort whose map outputs live in pinned host DRAM (the spill tier used when a
                       job exceeds HBM): rounds are streamed H2D, merged on the GPU, delivered D2H.
@@ -128,6 +130,51 @@ def decode(args) -> dict:
             "host_1thread_gbps_raw": round(raw / host_s / 1e9, 3), "host_compress_s": round(comp_s, 1)}
 
 
+def netmerger(args) -> dict:
+    """Secondary-sort data through the whole plugin path (provider -> loopback fetch -> NetMerger ->
+    dataFromUda): CPU heap merge vs the GPU backend (online, and hybrid LPQ/RPQ with a small device
+    budget)."""
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    n = native()
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    runs = n.generate_runs("secondary", args.maps, 1, rows, 9)
+    prov = UdaProvider()
+    total = 0
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        total += len(data) - 2
+        prov.add_mof_memory("job_nm", f"attempt_nm_m_{m:06d}_0", data, index)
+    out = {"config": "secondary sort through the NetMerger (loopback transport, 1 reducer)",
+           "gb": round(total / 1e9, 3), "maps": args.maps}
+    variants = [("cpu", {}), ("gpu_cold", {"mapred.uda.merge.backend": "gpu"}),
+                ("gpu", {"mapred.uda.merge.backend": "gpu"}),
+                ("gpu_hybrid", {"mapred.uda.merge.backend": "gpu",
+                                "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
+                                "mapred.uda.gpu.spill": "host"})]
+    for i, (name, conf) in enumerate(variants):
+        c = UdaConsumer(args.maps, "job_nm", f"attempt_nm_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
+        t0 = time.perf_counter()
+        for m in range(args.maps):
+            c.fetch("localhost", "job_nm", f"attempt_nm_m_{m:06d}_0", 0)
+        c.wait(3600)
+        wall = time.perf_counter() - t0
+        st = c.close()
+        assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
+        out[name + "_gbps"] = round(total / wall / 1e9, 3)
+        out[name + "_merge_ms"] = round(st["merge_ms"], 1)
+        out[name + "_fetch_ms"] = round(st["fetch_ms"], 1)
+        if name.startswith("gpu"):
+            out[name + "_phases_ms"] = {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")}
+        if name == "gpu_hybrid":
+            out["hybrid_lpqs"] = st["lpqs"]
+            out["hybrid_rpq_rounds"] = st["rpq_rounds"]
+    prov.close()
+    return out
+
+
 def aio(args) -> dict:
     """AsyncIO read bandwidth vs a sequential pread loop (the reference's AIOHandler_test)."""
     from uda_amd import native
@@ -163,7 +210,8 @@ def spill(args) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode", "aio"])
+    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode", "aio",
+                                       "netmerger"])
     ap.add_argument("--dir", default="/tmp")
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lzo"])
     ap.add_argument("--gb", type=float, default=1.0)

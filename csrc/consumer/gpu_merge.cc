@@ -42,11 +42,13 @@ namespace {
 constexpr int64_t kSampleSpacing = 256 << 10;  // LPQ sparse-index granularity
 
 struct DeviceMergeOut {
-  std::vector<uint8_t> bytes;  // merged records (no EOF)
+  int64_t bytes = 0;           // merged records (no EOF), resident in the workspace's `out`
   std::vector<int64_t> cuts;   // whole-record boundaries, <= the requested spacing apart
   int64_t records = 0;
   int64_t decoded_blocks = 0;
 };
+
+constexpr int64_t kPieceBytes = 64 << 20;  // D2H piece of the pinned double buffer
 
 // One merged LPQ output, resident in host memory or in a spill file.
 struct SpillRun {
@@ -65,6 +67,13 @@ struct DeviceWorkspace {
   gpu::DeviceBuffer in, out, packed;
   gpu::GenericMerger merger;
   gpu::DeviceBlockDecoder decoder;
+  gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
+  hipEvent_t piece_ev[2] = {nullptr, nullptr};
+  double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
+  ~DeviceWorkspace() {
+    for (auto e : piece_ev)
+      if (e) (void)hipEventDestroy(e);
+  }
   static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
     bytes = std::max<int64_t>(bytes, 16);
     if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
@@ -83,6 +92,7 @@ struct StreamGuard {
 DeviceMergeOut device_merge(DeviceWorkspace& ws, std::vector<std::vector<uint8_t>>* parts_in,
                             const std::vector<const uint8_t*>* views, const std::vector<int64_t>* view_lens, Codec codec,
                             KeyKind kind, int64_t spacing, hipStream_t s) {
+  auto t0 = std::chrono::steady_clock::now();
   std::vector<const uint8_t*> ptrs;
   std::vector<int64_t> lens;
   if (parts_in) {
@@ -140,24 +150,68 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, std::vector<std::vector<uint8_t
     }
     off += lens[i];
   }
+  HIP_CHECK(hipStreamSynchronize(s));
+  auto t1 = std::chrono::steady_clock::now();
+  ws.h2d_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
   DeviceMergeOut res;
   if (decode_on_device) {
     ws.decoder.decode(codec, plan, ws.packed.as<uint8_t>(), in.as<uint8_t>(), s);
     res.decoded_blocks = (int64_t)plan.descs.size();
   }
   if (parts_in) {  // the host copies are no longer needed once staged
-    HIP_CHECK(hipStreamSynchronize(s));
     parts_in->clear();
     parts_in->shrink_to_fit();
   }
   host_raw.clear();
   gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s);
-  res.bytes.resize((size_t)r.bytes);
-  if (r.bytes) HIP_CHECK(hipMemcpyAsync(res.bytes.data(), out.as(), (size_t)r.bytes, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+  res.bytes = r.bytes;
   res.cuts = std::move(r.cuts);
   res.records = r.records;
   return res;
+}
+
+// Stream the merged output of `m` (in ws.out) to the host in pieces of up to kPieceBytes that end on
+// record boundaries (the cuts), double-buffered through pinned memory: the D2H of piece k+1 runs
+// while fn(piece k) consumes it. fn(ptr, first_cut, last_cut) gets the bytes of cuts
+// [first_cut, last_cut] (ptr = byte cuts[first_cut]).
+template <typename Fn>
+void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&& fn) {
+  const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
+  if (nb == 0) return;
+  if (ws.ring.size() < (size_t)(2 * kPieceBytes)) ws.ring.alloc((size_t)(2 * kPieceBytes));
+  for (auto& e : ws.piece_ev)
+    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // piece boundaries in cut indices
+  std::vector<size_t> pb{0};
+  while (pb.back() < nb) {
+    size_t j = pb.back();
+    const int64_t start = m.cuts[j];
+    size_t k = j + 1;
+    while (k < nb && m.cuts[k + 1] - start <= kPieceBytes) ++k;
+    pb.push_back(k);
+  }
+  auto enqueue = [&](size_t piece) {
+    const int slot = (int)(piece & 1);
+    const int64_t b = m.cuts[pb[piece]], e = m.cuts[pb[piece + 1]];
+    if (e - b > kPieceBytes) throw UdaError("record larger than the D2H piece");
+    HIP_CHECK(hipMemcpyAsync(ws.ring.as<uint8_t>() + slot * kPieceBytes, ws.out.as<uint8_t>() + b, (size_t)(e - b),
+                             hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(ws.piece_ev[slot], s));
+  };
+  const size_t np = pb.size() - 1;
+  enqueue(0);
+  for (size_t piece = 0; piece < np; ++piece) {
+    const int slot = (int)(piece & 1);
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_CHECK(hipEventSynchronize(ws.piece_ev[slot]));
+    auto t1 = std::chrono::steady_clock::now();
+    ws.d2h_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (piece + 1 < np) enqueue(piece + 1);
+    fn(ws.ring.as<uint8_t>() + slot * kPieceBytes, pb[piece], pb[piece + 1]);
+    ws.sink_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+  }
 }
 
 std::string key_at(const uint8_t* p, int64_t avail) {
@@ -221,29 +275,38 @@ void ReduceTask::merge_gpu() {
     group.clear();
     group_raw = 0;
     SpillRun run;
-    run.bytes = (int64_t)m.bytes.size();
-    for (size_t j = 0; j + 1 < m.cuts.size(); ++j) {
-      run.cut.push_back(m.cuts[j]);
-      run.key.push_back(key_at(m.bytes.data() + m.cuts[j], run.bytes - m.cuts[j]));
-    }
-    if (tier == "disk") {
+    run.bytes = m.bytes;
+    const bool disk = tier == "disk";
+    if (disk) {
       if (!aio) aio = AsyncIO::create(AsyncIO::Options{});
       char name[64];
       snprintf(name, sizeof(name), ".gpu-lpq-%03d", (int)spills.size());
       run.path = dirs[spills.size() % dirs.size()] + "/uda." + init_.reduce_task_id + name;
       run.fd = ::open(run.path.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0600);
       if (run.fd < 0) throw UdaError("cannot create spill file " + run.path + ": " + strerror(errno));
-      std::atomic<int64_t> err{0};
-      constexpr int64_t kPiece = 8 << 20;
-      for (int64_t o = 0; o < run.bytes; o += kPiece)
-        aio->write(run.fd, o, std::min(kPiece, run.bytes - o), m.bytes.data() + o, [&err](int64_t r) {
-          if (r < 0) err = r;
-        });
-      aio->drain();
-      if (err.load() < 0) throw UdaError("spill write failed: " + std::string(strerror((int)-err.load())));
     } else {
-      run.mem = std::move(m.bytes);
+      run.mem.resize((size_t)run.bytes);
     }
+    // stream the LPQ output out of HBM: sparse index from every cut, bytes to DRAM or to the file
+    std::atomic<int64_t> err{0};
+    stream_out(ws, m, s, [&](const uint8_t* p, size_t c0, size_t c1) {
+      const int64_t base = m.cuts[c0], len = m.cuts[c1] - base;
+      for (size_t j = c0; j < c1; ++j) {
+        run.cut.push_back(m.cuts[j]);
+        run.key.push_back(key_at(p + (m.cuts[j] - base), m.cuts[c1] - m.cuts[j]));
+      }
+      if (disk) {
+        constexpr int64_t kIo = 8 << 20;
+        for (int64_t o = 0; o < len; o += kIo)
+          aio->write(run.fd, base + o, std::min(kIo, len - o), p + o, [&err](int64_t r) {
+            if (r < 0) err = r;
+          });
+        aio->drain();  // the pinned piece is reused after this returns
+      } else {
+        std::memcpy(run.mem.data() + base, p, (size_t)len);
+      }
+    });
+    if (err.load() < 0) throw UdaError("spill write failed: " + std::string(strerror((int)-err.load())));
     {
       std::lock_guard<std::mutex> g(st_mu_);
       st_.lpqs++;
@@ -336,25 +399,27 @@ void ReduceTask::merge_gpu() {
     std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
     auto deliver = [&](const DeviceMergeOut& m, bool last) {
       const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-      for (size_t j = 0; j < nb; ++j) {
-        if (stop_) throw UdaError("reduce task stopped during merge");
-        const int64_t b = m.cuts[j], e = m.cuts[j + 1];
-        const bool final_buf = last && j + 1 == nb;
-        const uint8_t* p = m.bytes.data() + b;
-        int64_t len = e - b;
-        if (final_buf) {  // copy so the EOF marker can follow the records
-          std::memcpy(tail.data(), p, (size_t)len);
-          tail[(size_t)len] = 0xFF;
-          tail[(size_t)len + 1] = 0xFF;
-          p = tail.data();
-          len += kEofBytes;
-          eof_sent = true;
+      stream_out(ws, m, s, [&](const uint8_t* piece, size_t c0, size_t c1) {
+        for (size_t j = c0; j < c1; ++j) {
+          if (stop_) throw UdaError("reduce task stopped during merge");
+          const int64_t b = m.cuts[j], e = m.cuts[j + 1];
+          const bool final_buf = last && j + 1 == nb;
+          const uint8_t* p = piece + (b - m.cuts[c0]);
+          int64_t len = e - b;
+          if (final_buf) {  // copy so the EOF marker can follow the records
+            std::memcpy(tail.data(), p, (size_t)len);
+            tail[(size_t)len] = 0xFF;
+            tail[(size_t)len + 1] = 0xFF;
+            p = tail.data();
+            len += kEofBytes;
+            eof_sent = true;
+          }
+          if (host_->data_from_uda(p, (int32_t)len) != 0) throw UdaError("dataFromUda callback failed");
+          std::lock_guard<std::mutex> g(st_mu_);
+          st_.buffers++;
+          st_.bytes_delivered += len;
         }
-        if (host_->data_from_uda(p, (int32_t)len) != 0) throw UdaError("dataFromUda callback failed");
-        std::lock_guard<std::mutex> g(st_mu_);
-        st_.buffers++;
-        st_.bytes_delivered += len;
-      }
+      });
       std::lock_guard<std::mutex> g(st_mu_);
       st_.records += m.records;
     };
@@ -479,6 +544,10 @@ void ReduceTask::merge_gpu() {
     }
     cleanup();
     std::lock_guard<std::mutex> g(st_mu_);
+    st_.gpu_h2d_ms = ws.h2d_ms;
+    st_.gpu_device_ms = ws.device_ms;
+    st_.gpu_d2h_wait_ms = ws.d2h_ms;
+    st_.gpu_sink_ms = ws.sink_ms;
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
   } catch (...) {

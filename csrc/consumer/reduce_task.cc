@@ -485,7 +485,9 @@ std::string ReduceTask::stats_json() const {
     << ",\"records\":" << s.records << ",\"buffers\":" << s.buffers << ",\"lpqs\":" << s.lpqs
     << ",\"spill_bytes\":" << s.spill_bytes << ",\"fetch_ms\":" << s.fetch_ms << ",\"merge_ms\":" << s.merge_ms
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
-    << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+    << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
+    << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }
 

@@ -101,7 +101,10 @@ struct PyBridge {
     py::gil_scoped_acquire g;
     try {
       if (self(ctx)->data_from_uda.is_none()) return 0;
-      py::object r = self(ctx)->data_from_uda(py::bytes((const char*)buf, (size_t)len));
+      // zero-copy like the JNI DirectByteBuffer: a read-only view valid only during the call
+      py::memoryview mv = py::memoryview::from_memory(const_cast<void*>(buf), (py::ssize_t)len, true);
+      py::object r = self(ctx)->data_from_uda(mv);
+      mv.attr("release")();
       return r.is_none() ? 0 : r.cast<int>();
     } catch (py::error_already_set& e) {
       e.discard_as_unraisable("data_from_uda");
@@ -518,31 +521,39 @@ PYBIND11_MODULE(_uda_native, m) {
     d["links"] = links;
     return d;
   });
-  m.def("gpu_merge_runs", [](const std::vector<std::string>& runs, const std::string& key_class, int64_t kv_buf,
-                             int device) {
+  // Merge IFile runs (any bytes-like objects, read in place) on the device. Returns
+  // (merged bytes, buffer cuts, records, merge passes, device merge ms, runs indexed serially).
+  m.def("gpu_merge_runs", [](const py::list& runs, const std::string& key_class, int64_t kv_buf, int device) {
     KeyKind kind = key_kind_from_class(key_class.c_str());
     if (kind == KeyKind::kUnsupported) throw py::value_error("unsupported key class");
-    std::string out;
+    std::vector<py::buffer_info> views;
+    std::vector<const uint8_t*> host;
+    std::vector<int64_t> bytes;
+    int64_t total = 0;
+    for (auto h : runs) {
+      views.push_back(py::reinterpret_borrow<py::buffer>(h).request());
+      host.push_back(static_cast<const uint8_t*>(views.back().ptr));
+      bytes.push_back((int64_t)(views.back().size * views.back().itemsize));
+      total += bytes.back();
+    }
     std::vector<int64_t> cuts;
-    int64_t records = 0;
+    int64_t records = 0, out_bytes = 0;
     int passes = 0, serial_runs = 0;
     double merge_ms = 0;
+    gpu::DeviceBuffer in, dout;
+    hipStream_t s = nullptr;
     {
       py::gil_scoped_release rel;
       HIP_CHECK(hipSetDevice(device));
-      int64_t total = 0;
-      for (auto& r : runs) total += (int64_t)r.size();
-      gpu::DeviceBuffer in((size_t)std::max<int64_t>(total, 16)), dout((size_t)std::max<int64_t>(total, 16));
-      hipStream_t s;
+      in.alloc((size_t)std::max<int64_t>(total, 16));
+      dout.alloc((size_t)std::max<int64_t>(total, 16));
       HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       std::vector<const uint8_t*> ptrs;
-      std::vector<int64_t> bytes;
       int64_t off = 0;
-      for (auto& r : runs) {
-        if (!r.empty()) HIP_CHECK(hipMemcpyAsync(in.as<uint8_t>() + off, r.data(), r.size(), hipMemcpyHostToDevice, s));
+      for (size_t i = 0; i < host.size(); ++i) {
+        if (bytes[i]) HIP_CHECK(hipMemcpyAsync(in.as<uint8_t>() + off, host[i], (size_t)bytes[i], hipMemcpyHostToDevice, s));
         ptrs.push_back(in.as<uint8_t>() + off);
-        bytes.push_back((int64_t)r.size());
-        off += (int64_t)r.size();
+        off += bytes[i];
       }
       gpu::GenericMerger gm;
       HIP_CHECK(hipStreamSynchronize(s));
@@ -550,16 +561,26 @@ PYBIND11_MODULE(_uda_native, m) {
       auto res = gm.merge(ptrs, bytes, (int)kind, dout.as<uint8_t>(), total, kv_buf, s);
       HIP_CHECK(hipStreamSynchronize(s));
       merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      out.resize((size_t)res.bytes);
-      if (res.bytes) HIP_CHECK(hipMemcpyAsync(&out[0], dout.as(), (size_t)res.bytes, hipMemcpyDeviceToHost, s));
-      HIP_CHECK(hipStreamSynchronize(s));
-      HIP_CHECK(hipStreamDestroy(s));
       cuts = res.cuts;
       records = res.records;
       passes = res.passes;
+      out_bytes = res.bytes;
       serial_runs = gm.f1_serial_runs();
     }
-    return py::make_tuple(py::bytes(out), cuts, records, passes, merge_ms, serial_runs);
+    views.clear();
+    // the result is copied D2H straight into the bytes object's storage
+    PyObject* o = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)out_bytes);
+    if (!o) throw py::error_already_set();
+    py::bytes out = py::reinterpret_steal<py::bytes>(o);
+    {
+      py::gil_scoped_release rel;
+      if (out_bytes) HIP_CHECK(hipMemcpyAsync(PyBytes_AS_STRING(o), dout.as(), (size_t)out_bytes, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      HIP_CHECK(hipStreamDestroy(s));
+      in.reset();
+      dout.reset();
+    }
+    return py::make_tuple(out, cuts, records, passes, merge_ms, serial_runs);
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
   // F6: decode Hadoop block-compressed streams on the device; returns (raw streams, blocks, decode_ms)
   m.def("gpu_block_decode", [](const std::string& codec_cls, const std::vector<std::string>& streams, int device) {

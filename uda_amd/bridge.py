@@ -115,14 +115,16 @@ class UdaConsumer:
         self.fetch_over_calls += 1
         self.maps_reported = min(self.num_maps, self.maps_reported + PROGRESS_REPORT_LIMIT)
 
-    def _data(self, buf: bytes):
+    def _data(self, buf: memoryview):
+        # `buf` is a view of the native buffer, valid only during this call (like the DirectByteBuffer
+        # J2CQueue copies from); the reader copies the records out
         self.bytes += len(buf)
         self.buffers += 1
         if self.reader is not None:
             self.reader.feed(buf)
             if self.reader.eof:
                 self._done.set()
-        elif len(buf) >= 2 and buf[-2:] == b"\xff\xff":
+        elif len(buf) >= 2 and bytes(buf[-2:]) == b"\xff\xff":
             self._done.set()
         return 0
 
