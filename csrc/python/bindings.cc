@@ -14,6 +14,7 @@
 
 #include "block_decoder.h"
 #include "device_engine.h"
+#include "exchange.h"
 #include "generic_merger.h"
 #include "uda/aio.h"
 #include "uda/codec.h"
@@ -630,6 +631,20 @@ PYBIND11_MODULE(_uda_native, m) {
     return py::make_tuple(l, blocks, ms);
   }, py::arg("codec"), py::arg("streams"), py::arg("device") = 0);
   m.def("nccl_unique_id", []() { return py::bytes(gpu::nccl_unique_id()); });
+  // RCCL data-plane self test on one GPU: communicator bootstrap from an ncclUniqueId and the grouped
+  // send/recv counts exchange the shuffle plan uses (world 1: the rank exchanges with itself).
+  m.def("rccl_selftest", [](int device, int n) {
+    py::gil_scoped_release rel;
+    HIP_CHECK(hipSetDevice(device));
+    auto ex = gpu::make_rccl_exchange(0, 1, gpu::nccl_unique_id());
+    hipStream_t s;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<int64_t> send((size_t)n), recv((size_t)n, -1);
+    for (int i = 0; i < n; ++i) send[(size_t)i] = (int64_t)i * 1000003 - 7;
+    ex->alltoall_i64(send.data(), recv.data(), (size_t)n, s);
+    HIP_CHECK(hipStreamDestroy(s));
+    return std::string(ex->name()) + (send == recv ? ":ok" : ":mismatch");
+  }, py::arg("device") = 0, py::arg("n") = 4096);
 
   py::class_<CountingSink, std::shared_ptr<CountingSink>>(m, "CountingSink")
       .def(py::init<>())

@@ -120,3 +120,9 @@ def test_host_dram_spill_tier(require_gpu, world):
         for d, st in enumerate(stats):
             assert st["records"] == rec[d] and st["order_errors"] == 0 and st["checksum"] == ck[d]
             assert st["bytes_h2d"] > 0
+
+
+def test_rccl_communicator_selftest(require_gpu, native):
+    """The RCCL data plane of the multi-GPU shuffle on one device: ncclUniqueId bootstrap and the
+    grouped ncclSend/ncclRecv counts exchange (world 1)."""
+    assert native.rccl_selftest(0, 4096) == "rccl:ok"
