@@ -52,7 +52,7 @@ constexpr int64_t kPieceBytes = 64 << 20;  // D2H piece of the pinned double buf
 
 // One merged LPQ output, resident in host memory or in a spill file.
 struct SpillRun {
-  std::vector<uint8_t> mem;
+  uint8_t* mem = nullptr;         // host tier: pinned (spill arena)
   std::string path;
   int fd = -1;
   int64_t bytes = 0;
@@ -89,20 +89,20 @@ struct StreamGuard {
 
 // Merge host-resident runs on the device. `codec` != kNone: the runs are block-compressed streams
 // decoded in HBM (falls back to a host decode when the framing needs it).
-DeviceMergeOut device_merge(DeviceWorkspace& ws, std::vector<std::vector<uint8_t>>* parts_in,
-                            const std::vector<const uint8_t*>* views, const std::vector<int64_t>* view_lens, Codec codec,
-                            KeyKind kind, int64_t spacing, hipStream_t s) {
+// Host spans of the runs to merge (pinned when they come from the arenas).
+struct Span {
+  const uint8_t* p;
+  int64_t len;
+};
+
+DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
+                            int64_t spacing, hipStream_t s) {
   auto t0 = std::chrono::steady_clock::now();
   std::vector<const uint8_t*> ptrs;
   std::vector<int64_t> lens;
-  if (parts_in) {
-    for (auto& p : *parts_in) {
-      ptrs.push_back(p.data());
-      lens.push_back((int64_t)p.size());
-    }
-  } else {
-    ptrs = *views;
-    lens = *view_lens;
+  for (const Span& sp : in_runs) {
+    ptrs.push_back(sp.p);
+    lens.push_back(sp.len);
   }
   gpu::BlockPlan plan;
   bool decode_on_device = false;
@@ -157,10 +157,6 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, std::vector<std::vector<uint8_t
   if (decode_on_device) {
     ws.decoder.decode(codec, plan, ws.packed.as<uint8_t>(), in.as<uint8_t>(), s);
     res.decoded_blocks = (int64_t)plan.descs.size();
-  }
-  if (parts_in) {  // the host copies are no longer needed once staged
-    parts_in->clear();
-    parts_in->shrink_to_fit();
   }
   host_raw.clear();
   gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s);
@@ -250,7 +246,8 @@ void ReduceTask::merge_gpu() {
   DeviceWorkspace ws;
 
   std::vector<SpillRun> spills;
-  std::vector<std::vector<uint8_t>> group;
+  std::vector<Span> group;          // fetched partitions of the current group (pinned, group_mem)
+  gpu::PinnedArena group_mem, spill_mem;
   int64_t group_raw = 0;
   std::unique_ptr<AsyncIO> aio;
   std::vector<std::string> dirs = init_.local_dirs;
@@ -270,9 +267,10 @@ void ReduceTask::merge_gpu() {
   // LPQ: merge the current group on the device and spill it with its sparse index
   auto spill_group = [&] {
     if (group.empty()) return;
-    DeviceMergeOut m = device_merge(ws, &group, nullptr, nullptr, stage_codec, kind_, kSampleSpacing, s);
+    DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kSampleSpacing, s);
     count_decoded(m.decoded_blocks);
     group.clear();
+    group_mem.release_all();  // staged in HBM: the pinned blocks go back to the pool
     group_raw = 0;
     SpillRun run;
     run.bytes = m.bytes;
@@ -285,7 +283,7 @@ void ReduceTask::merge_gpu() {
       run.fd = ::open(run.path.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0600);
       if (run.fd < 0) throw UdaError("cannot create spill file " + run.path + ": " + strerror(errno));
     } else {
-      run.mem.resize((size_t)run.bytes);
+      run.mem = spill_mem.alloc((size_t)std::max<int64_t>(run.bytes, 1));
     }
     // stream the LPQ output out of HBM: sparse index from every cut, bytes to DRAM or to the file
     std::atomic<int64_t> err{0};
@@ -303,7 +301,7 @@ void ReduceTask::merge_gpu() {
           });
         aio->drain();  // the pinned piece is reused after this returns
       } else {
-        std::memcpy(run.mem.data() + base, p, (size_t)len);
+        std::memcpy(run.mem + base, p, (size_t)len);
       }
     });
     if (err.load() < 0) throw UdaError("spill write failed: " + std::string(strerror((int)-err.load())));
@@ -347,48 +345,72 @@ void ReduceTask::merge_gpu() {
         }
       }
       for (auto& f : to_start) f->start();
-      // drain arrived MOFs in parallel (each drain keeps one request in flight ahead)
-      std::vector<std::vector<uint8_t>> got(ready.size());
-      std::vector<std::exception_ptr> errs(ready.size());
-      std::vector<std::thread> ts;
-      for (size_t i = 0; i < ready.size(); ++i)
-        ts.emplace_back([&, i] {
-          try {
-            std::vector<uint8_t> buf((size_t)buffer_size_);
-            for (;;) {
-              int64_t n = ready[i]->pull(buf.data(), (int64_t)buf.size());
-              if (n == 0) break;
-              got[i].insert(got[i].end(), buf.begin(), buf.begin() + n);
+      // Drain arrived MOFs in parallel (each drain keeps one request in flight ahead) straight into
+      // pinned spans of the group arena. Group boundaries are decided before a MOF is drained (on
+      // its partition length), so a group is complete in host memory when it is merged and spilled.
+      size_t next = 0;
+      while (next < ready.size()) {
+        std::vector<size_t> sub;
+        while (next < ready.size()) {
+          const int64_t pl = std::max<int64_t>(ready[next]->part_len(), 0);
+          const int64_t est = pl * (codec_ != Codec::kNone ? 3 : 1);  // decoded size estimate
+          if ((!group.empty() || !sub.empty()) && group_raw + est > budget) break;
+          sub.push_back(next++);
+          group_raw += est;
+        }
+        if (sub.empty()) {  // the group is full: merge and spill it, then admit the MOF
+          spill_group();
+          continue;
+        }
+        std::vector<Span> got(sub.size());
+        std::vector<std::vector<uint8_t>> host_decoded(sub.size());
+        std::vector<uint8_t*> dst(sub.size(), nullptr);
+        std::vector<std::exception_ptr> errs(sub.size());
+        for (size_t k = 0; k < sub.size(); ++k)
+          if (fetch_codec == Codec::kNone)
+            dst[k] = group_mem.alloc((size_t)std::max<int64_t>(ready[sub[k]]->part_len(), 1));
+        std::vector<std::thread> ts;
+        for (size_t k = 0; k < sub.size(); ++k)
+          ts.emplace_back([&, k] {
+            try {
+              MofFetcher& f = *ready[sub[k]];
+              if (dst[k]) {
+                const int64_t cap = f.part_len();
+                int64_t off = 0;
+                for (int64_t n; (n = f.pull(dst[k] + off, std::max<int64_t>(cap - off, 0))) > 0;) off += n;
+                got[k] = Span{dst[k], off};
+              } else {  // host decode: decoded length unknown up front
+                std::vector<uint8_t> buf((size_t)buffer_size_);
+                for (int64_t n; (n = f.pull(buf.data(), (int64_t)buf.size())) > 0;)
+                  host_decoded[k].insert(host_decoded[k].end(), buf.begin(), buf.begin() + n);
+              }
+            } catch (...) {
+              errs[k] = std::current_exception();
             }
-          } catch (...) {
-            errs[i] = std::current_exception();
+          });
+        for (auto& t : ts) t.join();
+        for (auto& e : errs)
+          if (e) std::rethrow_exception(e);
+        for (size_t k = 0; k < sub.size(); ++k) {
+          if (!dst[k]) {
+            uint8_t* p = group_mem.alloc(std::max<size_t>(host_decoded[k].size(), 1));
+            std::memcpy(p, host_decoded[k].data(), host_decoded[k].size());
+            got[k] = Span{p, (int64_t)host_decoded[k].size()};
           }
-        });
-      for (auto& t : ts) t.join();
-      for (auto& e : errs)
-        if (e) std::rethrow_exception(e);
-      for (auto& g : got) {
-        int64_t raw = (int64_t)g.size();
-        if (stage_codec != Codec::kNone) {  // account the decoded size against the budget
-          gpu::BlockPlan p;
-          std::vector<const uint8_t*> v{g.data()};
-          std::vector<int64_t> l{(int64_t)g.size()};
-          if (gpu::plan_block_streams(stage_codec, v, l, &p)) raw = p.raw_total + (int64_t)g.size();
+          group.push_back(got[k]);
+          drained++;
+          progress_count_++;
+          total_count_++;
+          {
+            std::lock_guard<std::mutex> gl(st_mu_);
+            st_.maps_fetched++;
+          }
+          if (progress_count_ == 20 || total_count_ == maps) {
+            host_->fetch_over();
+            progress_count_ = 0;
+          }
         }
-        if (!group.empty() && group_raw + raw > budget) spill_group();
-        group.push_back(std::move(g));
-        group_raw += raw;
-        drained++;
-        progress_count_++;
-        total_count_++;
-        {
-          std::lock_guard<std::mutex> gl(st_mu_);
-          st_.maps_fetched++;
-        }
-        if (progress_count_ == 20 || total_count_ == maps) {
-          host_->fetch_over();
-          progress_count_ = 0;
-        }
+        if (next < ready.size()) spill_group();  // the next MOF did not fit this group
       }
       ready.clear();
     }
@@ -427,7 +449,7 @@ void ReduceTask::merge_gpu() {
 
     if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
-      DeviceMergeOut m = device_merge(ws, &group, nullptr, nullptr, stage_codec, kind_, kv, s);
+      DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kv, s);
       count_decoded(m.decoded_blocks);
       deliver(m, true);
     } else {
@@ -465,7 +487,7 @@ void ReduceTask::merge_gpu() {
       auto read_run = [&](const SpillRun& run, int64_t off, int64_t len, uint8_t* dst) {
         if (len <= 0) return;
         if (run.fd < 0) {
-          std::memcpy(dst, run.mem.data() + off, (size_t)len);
+          std::memcpy(dst, run.mem + off, (size_t)len);
           return;
         }
         std::atomic<int64_t> err{0};
@@ -515,23 +537,22 @@ void ReduceTask::merge_gpu() {
         std::lock_guard<std::mutex> g(st_mu_);
         st_.rpq_rounds = rounds;
       }
+      gpu::PinnedArena slice_mem;
       for (int q = 0; q < rounds; ++q) {
-        std::vector<std::vector<uint8_t>> slices((size_t)R);
-        std::vector<const uint8_t*> views;
-        std::vector<int64_t> lens;
+        std::vector<Span> views;
+        slice_mem.release_all();
         for (int r = 0; r < R; ++r) {
           const SpillRun& run = spills[(size_t)r];
           const int64_t b = bnd[(size_t)r][(size_t)q], e = bnd[(size_t)r][(size_t)q + 1];
           if (run.fd < 0) {
-            views.push_back(run.mem.data() + b);
+            views.push_back(Span{run.mem + b, e - b});
           } else {
-            slices[(size_t)r].resize((size_t)(e - b));
-            read_run(run, b, e - b, slices[(size_t)r].data());
-            views.push_back(slices[(size_t)r].data());
+            uint8_t* p = slice_mem.alloc((size_t)std::max<int64_t>(e - b, 1));
+            read_run(run, b, e - b, p);
+            views.push_back(Span{p, e - b});
           }
-          lens.push_back(e - b);
         }
-        DeviceMergeOut m = device_merge(ws, nullptr, &views, &lens, Codec::kNone, kind_, kv, s);
+        DeviceMergeOut m = device_merge(ws, views, Codec::kNone, kind_, kv, s);
         deliver(m, q + 1 == rounds);
       }
     }

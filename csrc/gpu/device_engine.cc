@@ -54,6 +54,93 @@ void DeviceBuffer::reset() {
 PinnedBuffer::~PinnedBuffer() {
   if (ptr_) (void)hipHostFree(ptr_);
 }
+PinnedPool& PinnedPool::instance() {
+  static PinnedPool* pool = new PinnedPool();  // leaked on purpose: outlives every user at exit
+  return *pool;
+}
+
+PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = free_.lower_bound(min_bytes);
+    if (it != free_.end() && it->first <= 2 * min_bytes + PinnedArena::kBlock) {
+      Block b{it->second, it->first};
+      cached_ -= it->first;
+      free_.erase(it);
+      return b;
+    }
+  }
+  Block b;
+  b.size = (min_bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+  void* p = nullptr;
+  if (hipHostMalloc(&p, b.size, hipHostMallocDefault) != hipSuccess) {
+    // trim the cache and retry once
+    std::multimap<size_t, uint8_t*> drop;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      drop.swap(free_);
+      cached_ = 0;
+    }
+    for (auto& kv : drop) (void)hipHostFree(kv.second);
+    if (hipHostMalloc(&p, b.size, hipHostMallocDefault) != hipSuccess)
+      throw std::runtime_error("pinned host allocation of " + std::to_string(b.size) + " bytes failed");
+  }
+  b.p = static_cast<uint8_t*>(p);
+  return b;
+}
+
+void PinnedPool::release(Block b) {
+  if (!b.p) return;
+  std::lock_guard<std::mutex> g(mu_);
+  if (cached_ + b.size > cap_) {
+    (void)hipHostFree(b.p);
+    return;
+  }
+  free_.emplace(b.size, b.p);
+  cached_ += b.size;
+}
+
+void PinnedPool::set_cache_cap(size_t bytes) {
+  std::lock_guard<std::mutex> g(mu_);
+  cap_ = bytes;
+}
+
+size_t PinnedPool::cached_bytes() {
+  std::lock_guard<std::mutex> g(mu_);
+  return cached_;
+}
+
+uint8_t* PinnedArena::alloc(size_t bytes) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  bytes_ += bytes;
+  if (bytes > kBlock / 4) {  // large request: a dedicated block, kept behind the shared one
+    PinnedPool::Block b = PinnedPool::instance().acquire(std::max<size_t>(bytes, 256));
+    if (last_shared_ && !blocks_.empty()) {
+      blocks_.insert(blocks_.end() - 1, b);
+    } else {
+      blocks_.push_back(b);
+      last_shared_ = false;
+    }
+    return b.p;
+  }
+  if (!last_shared_ || used_ + bytes > blocks_.back().size) {
+    blocks_.push_back(PinnedPool::instance().acquire(kBlock));
+    used_ = 0;
+    last_shared_ = true;
+  }
+  uint8_t* p = blocks_.back().p + used_;
+  used_ += bytes;
+  return p;
+}
+
+void PinnedArena::release_all() {
+  for (auto& b : blocks_) PinnedPool::instance().release(b);
+  blocks_.clear();
+  used_ = 0;
+  last_shared_ = false;
+  bytes_ = 0;
+}
+
 void PinnedBuffer::alloc(size_t bytes) {
   if (ptr_) (void)hipHostFree(ptr_);
   ptr_ = nullptr;

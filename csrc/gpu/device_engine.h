@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -95,6 +96,47 @@ class PinnedBuffer {
  private:
   void* ptr_ = nullptr;
   size_t size_ = 0;
+};
+
+// Process-wide cache of pinned host blocks (hipHostMalloc). The GPU consumer stages fetched
+// partitions and spill slices in them: page-locking / page-faulting and unmapping GBs per reduce
+// task costs more than the merge itself, and a pinned source turns H2D into a direct DMA.
+class PinnedPool {
+ public:
+  struct Block {
+    uint8_t* p = nullptr;
+    size_t size = 0;
+  };
+  static PinnedPool& instance();
+  Block acquire(size_t min_bytes);
+  void release(Block b);
+  void set_cache_cap(size_t bytes);
+  size_t cached_bytes();
+
+ private:
+  std::mutex mu_;
+  std::multimap<size_t, uint8_t*> free_;
+  size_t cached_ = 0;
+  size_t cap_ = (size_t)32 << 30;
+};
+
+// Bump allocator over PinnedPool blocks; release_all() hands the blocks back to the pool.
+class PinnedArena {
+ public:
+  static constexpr size_t kBlock = (size_t)256 << 20;
+  PinnedArena() = default;
+  ~PinnedArena() { release_all(); }
+  PinnedArena(const PinnedArena&) = delete;
+  PinnedArena& operator=(const PinnedArena&) = delete;
+  uint8_t* alloc(size_t bytes);  // 256-byte aligned
+  void release_all();
+  size_t bytes() const { return bytes_; }
+
+ private:
+  std::vector<PinnedPool::Block> blocks_;
+  size_t used_ = 0;   // bytes used in blocks_.back() (shared blocks only)
+  bool last_shared_ = false;
+  size_t bytes_ = 0;
 };
 
 // Merges K sorted FIXED10 runs on one stream. Enqueue-only: never synchronizes the host except

@@ -3,9 +3,11 @@
 #include "uda/trace.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 namespace uda {
 namespace gpu {
@@ -28,6 +30,17 @@ void GenericMerger::reserve(int64_t records, int runs) {
 GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
                                         int kind, uint8_t* out, int64_t out_cap, int64_t kv_buf, hipStream_t s) {
   trace::Range tr("uda.generic_merge");
+  // UDA_GM_PROFILE=1: synchronize after each phase and print the split (diagnostic only)
+  static const bool prof = std::getenv("UDA_GM_PROFILE") != nullptr;
+  auto tp0 = std::chrono::steady_clock::now();
+  std::vector<std::pair<const char*, double>> phases;
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    HIP_CHECK(hipStreamSynchronize(s));
+    auto t = std::chrono::steady_clock::now();
+    phases.push_back({name, std::chrono::duration<double, std::milli>(t - tp0).count()});
+    tp0 = t;
+  };
   GenericMergeResult res;
   const int K = (int)runs.size();
   if (K == 0) {
@@ -94,7 +107,9 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     for (int k = 0; k < K; ++k)
       for (int64_t j = sup_base[k]; j < sup_base[k + 1]; ++j) sup_run[(size_t)j] = k;
     const size_t wsb = f1_parallel_workspace(nchunks, nsup) + (size_t)(K + 1) * 8 + (size_t)(nsup + 1) * 4 + 64;
+    phase("f1_host_tables");
     if (f1ws_.size() < wsb) f1ws_.alloc(wsb);
+    phase("f1_ws_alloc");
     uint8_t* ws = f1ws_.as<uint8_t>();
     auto* d_supbase = reinterpret_cast<int64_t*>(ws);
     auto* d_suprun = reinterpret_cast<int32_t*>(ws + (size_t)(K + 1) * 8);
@@ -106,6 +121,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     std::vector<int> st(K);
     HIP_CHECK(hipMemcpyAsync(st.data(), d_status, 4 * K, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    phase("f1_parallel");
     std::vector<int> redo;
     for (int k = 0; k < K; ++k)
       if (st[k] == 2) redo.push_back(k);
@@ -135,7 +151,9 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   if (bytes > out_cap) throw std::runtime_error("GenericMerger: output capacity too small");
   res.records = total;
   res.bytes = bytes;
+  phase("f1_scan");
   reserve(std::max(total, nchunks), K);
+  phase("reserve");
   // offsets storage: run k gets counts[k]+1 entries
   const int64_t off_elems = total + K;
   if (offsets_.size() < (size_t)off_elems * 8) offsets_.alloc((size_t)off_elems * 8);
@@ -152,6 +170,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     launch_f1_index(d_bases, d_nbytes, d_cbase, d_crun, d_ckstart, d_ckcount, d_ckord, d_eoff, d_recb, d_offp,
                     nchunks, s);
   }
+  phase("f1_index");
   GenericKeyCtx ctx;
   ctx.bases = d_bases;
   ctx.offsets = const_cast<const int64_t* const*>(d_offp);
@@ -171,6 +190,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   Elem* cur = elems_a_.as<Elem>();
   Elem* nxt = elems_b_.as<Elem>();
   launch_normalize_generic(ctx, d_eoff, K, total, cur, s);
+  phase("f2_normalize");
   // ---- F3: merge tree; per-pass descriptors are small host tables uploaded per pass
   std::vector<int64_t> seg(eoff);
   std::vector<DeviceBuffer> pass_tabs;
@@ -201,6 +221,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     seg.swap(next);
     ++res.passes;
   }
+  phase("f3_merge_tree");
   // ---- F4: sizes in merged order -> scan -> gather
   launch_record_sizes(ctx, cur, total, sizes_.as<int64_t>(), s);
   launch_exclusive_scan(sizes_.as<int64_t>(), out_off_.as<int64_t>(), total, scan_tmp_.as<int64_t>(), s);
@@ -228,6 +249,13 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   for (int64_t b : raw)
     if (res.cuts.empty() || b != res.cuts.back()) res.cuts.push_back(b);
   if (res.cuts.back() != bytes) res.cuts.push_back(bytes);
+  phase("f4_gather_cuts");
+  if (prof) {
+    std::string line = "[GM profile] runs=" + std::to_string(K) + " records=" + std::to_string(total) +
+                       " serial_runs=" + std::to_string(f1_serial_runs_);
+    for (auto& ph : phases) line += " " + std::string(ph.first) + "=" + std::to_string(ph.second).substr(0, 6) + "ms";
+    fprintf(stderr, "%s\n", line.c_str());
+  }
   return res;
 }
 
