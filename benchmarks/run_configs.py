@@ -3,6 +3,7 @@
 
   wordcount_loopback  uda_standalone wordcount on CPU loopback: provider + R NetMergers in one
                       process through the UdaBridge C ABI (the JNI plumbing path), heap merge.
+  wordcount_tcp       the same with the MOFSupplier in another process, over the TCP transport.
   cpu_reference       in-house baseline: the reference algorithm (single-threaded heap k-way merge,
                       write_kv_to_stream packing) on TeraSort runs on this host's CPU.
   secondary_sort      variable-length Text keys with long common prefixes + partition skew: GPU generic
@@ -63,6 +64,70 @@ def wordcount_loopback(args) -> dict:
             "maps": maps, "reducers": reducers, "wall_s": round(wall, 3),
             "shuffle_merge_gbps": round(total / wall / 1e9, 3), "gen_s": round(gen_s, 1),
             "records": sum(s["records"] for s in stats), "backend": "cpu heap merge, loopback transport"}
+
+
+TCP_PROVIDER = r"""
+import json, sys
+sys.path.insert(0, sys.argv[3])
+from uda_amd.bridge import UdaProvider
+p = UdaProvider(transport="tcp", data_port=int(sys.argv[1]))
+for job, mid, path in json.loads(sys.argv[2]):
+    p.add_mof_file(job, mid, path)
+print("READY", flush=True)
+sys.stdin.read()
+p.close()
+"""
+
+
+def wordcount_tcp(args) -> dict:
+    """wordcount with the MOFSupplier in another process: the socket transport (the reference's
+    cross-node RDMA path, here TCP over the host's loopback interface)."""
+    import socket
+    import subprocess
+    import tempfile
+
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import write_mof
+    n = native()
+    maps, reducers = args.maps, args.reducers
+    rows = int(args.gb * 1e9 / maps / 17)
+    runs = n.generate_runs("wordcount", maps, reducers, rows, 7)
+    tmp = tempfile.mkdtemp(prefix="uda_tcp_", dir=args.dir)
+    mofs, total = [], 0
+    for m, parts in enumerate(runs):
+        mid = f"attempt_tcp_m_{m:06d}_0"
+        path, _ = write_mof(tmp, mid, parts)
+        mofs.append(("job_tcp", mid, path))
+        total += sum(len(p) - 2 for p in parts)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prov = subprocess.Popen([sys.executable, "-c", TCP_PROVIDER, str(port), json.dumps(mofs), root],
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        assert prov.stdout.readline().strip() == "READY"
+        consumers = [UdaConsumer(maps, "job_tcp", f"attempt_tcp_r_{r:06d}_0", TEXT, keep_records=False,
+                                 transport="tcp", data_port=port) for r in range(reducers)]
+        t0 = time.perf_counter()
+        for r, c in enumerate(consumers):
+            for _, mid, _ in mofs:
+                c.fetch("127.0.0.1", "job_tcp", mid, r)
+        for c in consumers:
+            c.wait(3600)
+        wall = time.perf_counter() - t0
+        stats = [c.close() for c in consumers]
+    finally:
+        prov.stdin.close()
+        prov.wait(timeout=60)
+    delivered = sum(st["bytes_delivered"] for st in stats) - 2 * reducers
+    assert delivered == total, (delivered, total)
+    return {"config": "wordcount, MOFSupplier in a separate process, TCP transport", "gb": round(total / 1e9, 3),
+            "maps": maps, "reducers": reducers, "wall_s": round(wall, 3),
+            "shuffle_merge_gbps": round(total / wall / 1e9, 3)}
 
 
 def cpu_reference(args) -> dict:
@@ -210,7 +275,7 @@ def spill(args) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("config", choices=["wordcount_loopback", "cpu_reference", "secondary_sort", "spill", "decode", "aio",
+    ap.add_argument("config", choices=["wordcount_loopback", "wordcount_tcp", "cpu_reference", "secondary_sort", "spill", "decode", "aio",
                                        "netmerger"])
     ap.add_argument("--dir", default="/tmp")
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lzo"])
