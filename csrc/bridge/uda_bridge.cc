@@ -73,8 +73,8 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
     std::lock_guard<std::mutex> g(g_log_mu);
     g_log_cb = *cb;
     g_log_cb_set = true;
-    uda::log_set_sink(log_trampoline, nullptr);
   }
+  uda::log_set_sink(log_trampoline, nullptr);  // outside g_log_mu: the logger calls us under its own lock
   UDA_LOG(uda::kInfo, "UDA version is %s; role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
   try {
     if (h->is_merger) {

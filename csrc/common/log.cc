@@ -61,7 +61,7 @@ void log_write(int sev, const char* file, int line, const char* func, const char
   char msg[2400];
   snprintf(msg, sizeof(msg), "%s:%d %s() %s", base, line, func, body);
 
-  std::lock_guard<std::mutex> g(g_mu);
+  std::unique_lock<std::mutex> g(g_mu);
   if (g_file) {
     struct timeval tv;
     gettimeofday(&tv, nullptr);
@@ -75,7 +75,12 @@ void log_write(int sev, const char* file, int line, const char* func, const char
     return;
   }
   if (g_sink) {
-    g_sink(g_sink_ctx, msg, sev);
+    // call the host sink (Java logToJava / Python) without holding the logger lock: it may log
+    // or take its own locks
+    const LogSink sink = g_sink;
+    void* ctx = g_sink_ctx;
+    g.unlock();
+    sink(ctx, msg, sev);
     return;
   }
   fprintf(stderr, "[uda %s] %s\n", sev_name(sev), msg);

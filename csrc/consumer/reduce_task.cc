@@ -72,7 +72,12 @@ std::function<void()> MofFetcher::prepare(int b) {
   auto self = shared_from_this();
   uint8_t* dst = bufs_[b].data();
   return [self, b, req, dst] {
-    self->task_->transport()->fetch(self->p_.host, req, dst, [self, b](const FetchAck& a) { self->on_done(b, a); });
+    ReduceTask* t = self->task_;
+    t->fetch_begin();  // the task outlives every completion: exit() waits for fetch_end
+    t->transport()->fetch(self->p_.host, req, dst, [self, b, t](const FetchAck& a) {
+      self->on_done(b, a);
+      t->fetch_end();
+    });
   };
 }
 
@@ -97,8 +102,8 @@ void MofFetcher::on_done(int b, const FetchAck& a) {
       first_done_ = true;
       first = true;
     }
+    cv_.notify_all();  // under the lock: a woken consumer may drop the last reference
   }
-  cv_.notify_all();
   if (first) {
     {
       std::lock_guard<std::mutex> g(task_->mu_);
@@ -260,6 +265,22 @@ void ReduceTask::exit() {
   cv_.notify_all();
   if (merge_thr_.joinable()) merge_thr_.join();
   if (transport_) transport_->close();
+  // completions of requests still in flight (a provider worker may be serving one) touch this task
+  std::unique_lock<std::mutex> lk(inflight_mu_);
+  if (!inflight_cv_.wait_for(lk, std::chrono::seconds(120), [&] { return inflight_ == 0; }))
+    UDA_LOG(kError, "reduce task exit: %ld fetch completions still outstanding", (long)inflight_);
+}
+
+void ReduceTask::fetch_begin() {
+  std::lock_guard<std::mutex> g(inflight_mu_);
+  ++inflight_;
+}
+
+void ReduceTask::fetch_end() {
+  // notify under the lock: once exit() sees zero it may destroy the task (and this cv)
+  std::lock_guard<std::mutex> g(inflight_mu_);
+  --inflight_;
+  inflight_cv_.notify_all();
 }
 
 void ReduceTask::merge_main() {

@@ -62,6 +62,9 @@ class ReduceTask {
 
   // exposed for the fetchers
   ClientTransport* transport() { return transport_.get(); }
+  // in-flight fetch requests (exit() waits for their completions)
+  void fetch_begin();
+  void fetch_end();
 
  private:
   void on_init(const InitParams& p);
@@ -101,6 +104,10 @@ class ReduceTask {
   std::thread merge_thr_;
   bool inited_ = false;
   int next_index_ = 0;
+
+  std::mutex inflight_mu_;
+  std::condition_variable inflight_cv_;
+  int64_t inflight_ = 0;
 
   mutable std::mutex st_mu_;
   ReduceStats st_;

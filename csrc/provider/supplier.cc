@@ -58,9 +58,16 @@ void Supplier::register_mof(const std::string& job, const std::string& map, cons
 void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
   {
     std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(Job{req, dst, std::move(done)});
+    if (!stop_) {
+      q_.push_back(Job{req, dst, std::move(done)});
+      cv_.notify_one();
+      return;
+    }
   }
-  cv_.notify_one();
+  FetchAck a;  // stopped: no worker will take the request, complete it now
+  a.status = -11;
+  a.error = "MOFSupplier stopped";
+  done(a);
 }
 
 void Supplier::worker() {
