@@ -75,7 +75,8 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
     g_log_cb_set = true;
   }
   uda::log_set_sink(log_trampoline, nullptr);  // outside g_log_mu: the logger calls us under its own lock
-  UDA_LOG(uda::kInfo, "UDA version is %s; role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
+  // "The version is <v>" is the line the regression tools parse (tools/regression.py)
+  UDA_LOG(uda::kInfo, "UDA: The version is %s role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
   try {
     if (h->is_merger) {
       h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());

@@ -11,6 +11,7 @@
 //   F6 block decompress    -> snappy_decompress_blocks / lzo1x_decompress_blocks
 // plus TeraGen-shaped synthetic map-output generation and device-side validation.
 #pragma once
+#include "uda/hash.h"
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -179,32 +180,9 @@ void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const Decod
 void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key, int has_prev,
                            Elem* last_key, unsigned long long* stats, hipStream_t s);
 
-// Hash used for order-independent checksums (sum of per-record hashes), host + device.
-__host__ __device__ inline uint64_t mix64(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
-// record_hash over the serialized record bytes, consumed as little-endian 8-byte words (the last
-// one zero padded). Same value on host and device for any alignment.
-__host__ __device__ inline uint64_t record_hash(const uint8_t* p, int64_t len) {
-  uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)len;
-  int64_t i = 0;
-  for (; i + 8 <= len; i += 8) {
-    uint64_t w = 0;
-    for (int b = 7; b >= 0; --b) w = (w << 8) | p[i + b];
-    h = mix64(h ^ w);
-  }
-  if (i < len) {
-    uint64_t w = 0;
-    for (int64_t b = len - 1; b >= i; --b) w = (w << 8) | p[b];
-    h = mix64(h ^ w);
-  }
-  return h;
-}
+// Order-independent checksums: shared with the host (uda/hash.h).
+using ::uda::mix64;
+using ::uda::record_hash;
 
 }  // namespace gpu
 }  // namespace uda

@@ -134,3 +134,34 @@ class KVWriter {
 };
 
 }  // namespace uda
+
+namespace uda {
+
+// ----------------------------------------------------------------------------- validation
+// teravalidate for a merged reducer stream (reference: scripts/regression/mr-dstatExcel.sh:249-291
+// runs Hadoop's TeraValidate on the job output). Buffers arrive as the host receives them
+// (dataFromUda): whole records, the last buffer ending with the EOF marker. Checks the framing,
+// the key order under the job's comparator, and accumulates the order-independent checksum
+// (uda/hash.h) that is compared with the checksum of the map outputs.
+class StreamValidator {
+ public:
+  explicit StreamValidator(KeyKind kind) : kind_(kind) {}
+  void feed(const uint8_t* p, size_t n);
+  int64_t records = 0;
+  int64_t bytes = 0;           // record bytes (EOF excluded)
+  int64_t buffers = 0;
+  int64_t order_errors = 0;    // adjacent pairs out of order
+  int64_t framing_errors = 0;  // partial record in a buffer, data after EOF, corrupt header
+  uint64_t checksum = 0;
+  bool eof = false;
+
+ private:
+  KeyKind kind_;
+  std::string prev_key_;
+  bool has_prev_ = false;
+};
+
+// Records and checksum of one IFile partition stream (stops at EOF or at the end of the bytes).
+uint64_t ifile_checksum(const uint8_t* p, size_t n, int64_t* records, int64_t* bytes);
+
+}  // namespace uda

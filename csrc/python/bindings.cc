@@ -20,6 +20,7 @@
 #include "uda/codec.h"
 #include "uda/datagen.h"
 #include "uda/error.h"
+#include "uda/hash.h"
 #include "uda/ifile.h"
 #include "uda/uda_bridge.h"
 #include "uda/cmd.h"
@@ -241,7 +242,7 @@ PYBIND11_MODULE(_uda_native, m) {
   });
   m.def("record_hash", [](py::bytes b) {
     std::string s = b;
-    return gpu::record_hash(reinterpret_cast<const uint8_t*>(s.data()), (int64_t)s.size());
+    return record_hash(reinterpret_cast<const uint8_t*>(s.data()), (int64_t)s.size());
   });
   m.def("log_set_threshold", &log_set_threshold);
 
@@ -327,6 +328,35 @@ PYBIND11_MODULE(_uda_native, m) {
     std::vector<int64_t> lens;
     py::bytes out = cpu_merge_impl(runs, key_class, buf, &lens);
     return py::make_tuple(out, lens);
+  });
+
+  // teravalidate: framing + order + checksum of a delivered stream, fed buffer by buffer
+  py::class_<StreamValidator, std::shared_ptr<StreamValidator>>(m, "StreamValidator")
+      .def(py::init([](const std::string& key_class) {
+        KeyKind kind = key_kind_from_class(key_class.c_str());
+        if (kind == KeyKind::kUnsupported) throw py::value_error("unsupported key class");
+        return std::make_shared<StreamValidator>(kind);
+      }))
+      .def("feed", [](StreamValidator& v, py::buffer b) {
+        py::buffer_info bi = b.request();
+        v.feed(static_cast<const uint8_t*>(bi.ptr), (size_t)(bi.size * bi.itemsize));
+      })
+      .def_readonly("records", &StreamValidator::records)
+      .def_readonly("bytes", &StreamValidator::bytes)
+      .def_readonly("buffers", &StreamValidator::buffers)
+      .def_readonly("order_errors", &StreamValidator::order_errors)
+      .def_readonly("framing_errors", &StreamValidator::framing_errors)
+      .def_readonly("checksum", &StreamValidator::checksum)
+      .def_readonly("eof", &StreamValidator::eof);
+  m.def("ifile_checksum", [](py::buffer b) {
+    py::buffer_info bi = b.request();
+    int64_t recs = 0, bytes = 0;
+    uint64_t ck;
+    {
+      py::gil_scoped_release r;
+      ck = ifile_checksum(static_cast<const uint8_t*>(bi.ptr), (size_t)(bi.size * bi.itemsize), &recs, &bytes);
+    }
+    return py::make_tuple(recs, bytes, ck);
   });
 
   // ---------------------------------------------------------------- async IO

@@ -84,9 +84,11 @@ class UdaConsumer:
                  local_dirs: tuple[str, ...] = (), transport: str = "loopback", data_port: int = 9011,
                  max_buf_kb: int = 1024, min_buf_kb: int = 16, shuffle_mem: int = 0, lpq_size: int = 0,
                  comp_block_size: int = 256 * 1024, kv_buf_size: int = 1 << 20, log_level: int = 3,
-                 keep_records: bool = True):
+                 keep_records: bool = True, validate: bool = False):
         self.num_maps = num_maps
         self.reader = J2CQueueReader(max_len=kv_buf_size) if keep_records else None
+        # teravalidate in native code (framing, order, checksum) without keeping the records
+        self.validator = native().StreamValidator(key_class) if validate else None
         self.bytes = 0
         self.buffers = 0
         self.maps_reported = 0
@@ -120,6 +122,8 @@ class UdaConsumer:
         # J2CQueue copies from); the reader copies the records out
         self.bytes += len(buf)
         self.buffers += 1
+        if self.validator is not None:
+            self.validator.feed(buf)
         if self.reader is not None:
             self.reader.feed(buf)
             if self.reader.eof:
