@@ -886,8 +886,15 @@ StepStats ShuffleJob::run_step() {
   }
   if (cfg_.deliver_host) {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return step_done_; });
+    while (!cv_.wait_for(lk, std::chrono::milliseconds(100), [&] { return step_done_; })) {
+      if (exchange_) {  // a lost peer must fail the step, not hang it
+        lk.unlock();
+        exchange_->check();
+        lk.lock();
+      }
+    }
   }
+  if (exchange_) exchange_->wait(s_comm_);
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   HIP_CHECK(hipStreamSynchronize(s_comm_));
   for (auto s : s_copy_) HIP_CHECK(hipStreamSynchronize(s));

@@ -2,8 +2,12 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -28,9 +32,10 @@ class RcclExchange : public Exchange {
     std::memcpy(&id, uid.data(), sizeof(id));
     NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
     HIP_CHECK(hipMalloc(&d_counts_, 1));
+    if (const char* t = std::getenv("UDA_RCCL_TIMEOUT_S")) timeout_ = std::chrono::seconds(std::max(1, std::atoi(t)));
   }
   ~RcclExchange() override {
-    if (comm_) ncclCommDestroy(comm_);
+    if (comm_) (aborted_ ? ncclCommAbort(comm_) : ncclCommDestroy(comm_));
     if (d_counts_) (void)hipFree(d_counts_);
   }
   int rank() const override { return rank_; }
@@ -54,7 +59,27 @@ class RcclExchange : public Exchange {
     }
     NCCL_CHECK(ncclGroupEnd());
     HIP_CHECK(hipMemcpyAsync(recv, dr, bytes, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait(s);
+  }
+
+  void check() override {
+    if (aborted_) throw std::runtime_error("RCCL communicator was aborted after an earlier failure");
+    ncclResult_t a = ncclSuccess;
+    NCCL_CHECK(ncclCommGetAsyncError(comm_, &a));
+    if (a != ncclSuccess && a != ncclInProgress) fail(std::string("RCCL asynchronous error: ") + ncclGetErrorString(a));
+  }
+
+  void wait(hipStream_t s) override {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) HIP_CHECK(q);
+      check();
+      if (std::chrono::steady_clock::now() - t0 > timeout_)
+        fail("RCCL exchange timed out after " + std::to_string(timeout_.count()) + " s (peer lost?)");
+      if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
 
   void alltoallv(const uint8_t* send, const int64_t* sb, const int64_t* sd, uint8_t* recv, const int64_t* rb,
@@ -70,8 +95,20 @@ class RcclExchange : public Exchange {
   }
 
  private:
+  // A lost peer leaves kernels of this communicator waiting forever: abort it so the device drains,
+  // then surface the failure (the bridge turns it into failureInUda / a failed step).
+  [[noreturn]] void fail(const std::string& why) {
+    if (!aborted_) {
+      aborted_ = true;
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+    throw std::runtime_error(why);
+  }
   int rank_, world_;
   ncclComm_t comm_ = nullptr;
+  bool aborted_ = false;
+  std::chrono::seconds timeout_{900};
   void* d_counts_ = nullptr;
   size_t counts_cap_ = 0;
 };
@@ -173,6 +210,8 @@ class LocalExchange : public Exchange {
   hipEvent_t ready_ = nullptr, done_ = nullptr;
 };
 }  // namespace
+
+void Exchange::wait(hipStream_t s) { HIP_CHECK(hipStreamSynchronize(s)); }
 
 std::unique_ptr<Exchange> make_rccl_exchange(int rank, int world, const std::string& uid) {
   return std::make_unique<RcclExchange>(rank, world, uid);

@@ -37,6 +37,11 @@ class Exchange {
                          uint8_t* recv, const int64_t* recv_bytes, const int64_t* recv_displ,
                          hipStream_t s) = 0;
   virtual const char* name() const = 0;
+  // Host wait for everything enqueued on `s`, failing instead of hanging when a peer is lost
+  // (RCCL: asynchronous communicator errors and a timeout, UDA_RCCL_TIMEOUT_S, default 900 s).
+  virtual void wait(hipStream_t s);
+  // Throw if the communicator reported an asynchronous error (cheap, non-blocking).
+  virtual void check() {}
 };
 
 std::unique_ptr<Exchange> make_rccl_exchange(int rank, int world, const std::string& unique_id);
