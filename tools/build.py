@@ -34,6 +34,25 @@ def sources() -> tuple[list[str], list[str]]:
     return lib, mod
 
 
+def installed_outputs() -> tuple[str, str]:
+    ext = sysconfig.get_config_var("EXT_SUFFIX")
+    return (os.path.join(ROOT, "uda_amd", "lib", "libuda.so"), os.path.join(ROOT, "uda_amd", "_uda_native" + ext))
+
+
+def staged_outputs(build_dir: str) -> tuple[str, str]:
+    ext = sysconfig.get_config_var("EXT_SUFFIX")
+    return os.path.join(build_dir, "lib", "libuda.so"), os.path.join(build_dir, "_uda_native" + ext)
+
+
+def install(build_dir: str) -> None:
+    """Copy the flavour's link outputs in-tree; os.replace keeps a running process's mapping valid."""
+    for src, dst in zip(staged_outputs(build_dir), installed_outputs()):
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        tmp = dst + ".tmp"
+        shutil.copy2(src, tmp)
+        os.replace(tmp, dst)
+
+
 def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
     import pybind11
 
@@ -48,9 +67,9 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
         # sanitizers apply to host code only (no GPU ASan on this pool)
         host_san = f" -Xarch_host -fsanitize={sanitize} -fno-omit-frame-pointer"
     py_inc = f"-I{pybind11.get_include()} -I{sysconfig.get_paths()['include']}"
-    ext = sysconfig.get_config_var("EXT_SUFFIX")
-    lib_out = os.path.join(ROOT, "uda_amd", "lib", "libuda.so")
-    mod_out = os.path.join(ROOT, "uda_amd", "_uda_native" + ext)
+    # link inside the flavour's build dir; install() copies into uda_amd/ (ninja alone would keep
+    # a stale in-tree .so written by another flavour, its mtime being newer than our objects)
+    lib_out, mod_out = staged_outputs(build_dir)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     lines = [
         "ninja_required_version = 1.5",
@@ -103,6 +122,7 @@ def build(jobs: int | None = None, debug: bool = False, sanitize: str | None = N
     if verbose:
         cmd.append("-v")
     subprocess.run(cmd, check=True)
+    install(build_dir)
 
 
 def main() -> int:
