@@ -244,6 +244,39 @@ void ReduceTask::on_init(const InitParams& p) {
   buffer_size_ = max_buf - max_buf % page;
   if (buffer_size_ <= 0 || buffer_size_ < p.min_buf_bytes) throw UdaError("RDMA Buffer is too small");
   free_pairs_ = num_kv_bufs_ + kExtraBuffers;
+  fetch_buf_ = buffer_size_;
+  int64_t uncomp_buf = buffer_size_;
+  if (codec_ != Codec::kNone) {
+    // compressed: the pair's 2*buffer_size is split between the fetch side and the decoded side
+    // (reducer.cc:463-491): the decoded side gets at least one codec block plus a minimal fetch
+    // buffer, then `mapred.rdma.compression.buffer.ratio` of what is left, plus anything the fetch
+    // side would get above mapred.rdma.buf.size.
+    if (codec_ == Codec::kLzo) {
+      const std::string v = host_->get_conf("io.compression.codec.lzo.decompressor", "LZO1X");
+      if (v != "LZO1X" && v != "LZO1X_SAFE" && v != "LZO1X_ASM" && v != "LZO1X_ASM_SAFE" &&
+          v != "LZO1X_ASM_FAST" && v != "LZO1X_ASM_FAST_SAFE")
+        throw UdaError("unsupported io.compression.codec.lzo.decompressor " + v +
+                       " (the in-tree and device decoders read the LZO1X stream format)");
+    }
+    const double ratio = std::atof(host_->get_conf("mapred.rdma.compression.buffer.ratio", "0.20").c_str());
+    const int64_t max_fetch = host_->conf_i64("mapred.rdma.buf.size", 1024) * 1024;
+    const int64_t min_fetch = p.min_buf_bytes;
+    const int64_t hard_min = p.comp_block_size + min_fetch;
+    const int64_t pair = buffer_size_ * 2;
+    if (pair < hard_min + min_fetch) {
+      // the reference gives up here ("not enough memory to allocate buffers"); our decoders keep
+      // their own block-sized output, so a small pair still works with the whole pair fetching
+      UDA_LOG(kWarn, "buffer pair %ld < codec block %ld + 2 x min buffer %ld: no split, fetch chunk %ld",
+              (long)pair, (long)p.comp_block_size, (long)min_fetch, (long)buffer_size_);
+    } else {
+    const int64_t delta = pair - (hard_min + min_fetch);
+    uncomp_buf = hard_min + (int64_t)((double)delta * std::min(1.0, std::max(0.0, ratio)));
+    fetch_buf_ = pair - uncomp_buf;
+    const int64_t spare = std::max<int64_t>(fetch_buf_ - max_fetch, 0);
+    fetch_buf_ -= spare;
+    uncomp_buf += spare;
+    }
+  }
   if (fault_hit("HOST_ALLOC")) throw UdaError("injected allocation failure for the fetch buffer pool");
   kv_buf_size_ = host_->conf_i64("mapred.uda.kv.buf.size", 1 << 20);
   backend_ = host_->get_conf("mapred.uda.merge.backend", "cpu");
@@ -252,6 +285,8 @@ void ReduceTask::on_init(const InitParams& p) {
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.backend = backend_;
+    st_.fetch_buf_bytes = fetch_buf_;
+    st_.uncomp_buf_bytes = uncomp_buf;
   }
   inited_ = true;
   UDA_LOG(kInfo, "reduce task %s: maps=%d approach=%d lpqs=%d kv_bufs=%d buffer=%ld codec=%s key=%s backend=%s",
@@ -329,7 +364,7 @@ void ReduceTask::fetch_phase(MergeQueue* q, int n) {
       }
       std::shuffle(pending.begin(), pending.end(), rng);
       while (!pending.empty() && free_pairs_ > 0 && sent < n) {
-        to_start.push_back(std::make_shared<MofFetcher>(this, pending.back(), buffer_size_, codec_));
+        to_start.push_back(std::make_shared<MofFetcher>(this, pending.back(), fetch_buf_, codec_));
         pending.pop_back();
         free_pairs_--;
         sent++;
@@ -508,7 +543,8 @@ std::string ReduceTask::stats_json() const {
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
-    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
+    << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }
 

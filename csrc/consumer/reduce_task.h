@@ -45,6 +45,8 @@ struct ReduceStats {
   // GPU backend phase split: H2D staging, device decode+merge, waits on D2H pieces, host consumers
   // (dataFromUda / spill writes) of the pinned pieces
   double gpu_h2d_ms = 0, gpu_device_ms = 0, gpu_d2h_wait_ms = 0, gpu_sink_ms = 0;
+  // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
+  int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;
   std::string backend;
 };
 
@@ -83,6 +85,7 @@ class ReduceTask {
   KeyKind kind_ = KeyKind::kText;
   Codec codec_ = Codec::kNone;
   int64_t buffer_size_ = 0;        // per fetch buffer (pair = 2 of these)
+  int64_t fetch_buf_ = 0;          // fetch chunk (== buffer_size_ uncompressed, the "rdma" half when compressed)
   int64_t kv_buf_size_ = 1 << 20;  // delivery buffer (NETLEV_KV_POOL_EXPO)
   int num_kv_bufs_ = 0;
   int num_lpqs_ = 0;

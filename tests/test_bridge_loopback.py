@@ -96,6 +96,33 @@ def test_compressed_map_outputs(provider, tmp_path, codec):
     check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
 
 
+@pytest.mark.parametrize("ratio", ["0.20", "0.0", "1.0"])
+def test_compressed_buffer_split(provider, tmp_path, ratio):
+    """reducer.cc:463-491: a compressed job splits each 2 x buffer pair into a fetch side and an
+    uncompressed side (codec block + min buffer + ratio of the rest; the fetch side is capped by
+    mapred.rdma.buf.size, the excess moving to the uncompressed side)."""
+    maps = datagen.wordcount(num_maps=4, reducers=1, words_per_map=3000, seed=5)
+    ids = publish(provider, tmp_path, "job_1_0044", maps, codec="snappy")
+    conf = {"mapred.rdma.compression.buffer.ratio": ratio, "mapred.rdma.buf.size": 512}
+    recs, st, c = run_reduce("h", "job_1_0044", ids, 0, datagen.TEXT, codec="snappy", max_buf_kb=512, conf=conf)
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+    pair = 2 * 512 * 1024
+    hard_min = 256 * 1024 + 16 * 1024
+    uncomp = hard_min + int((pair - hard_min - 16 * 1024) * float(ratio))
+    fetch = pair - uncomp
+    spare = max(0, fetch - 512 * 1024)
+    assert (st["fetch_buf_bytes"], st["uncomp_buf_bytes"]) == (fetch - spare, uncomp + spare)
+    assert st["fetch_buf_bytes"] + st["uncomp_buf_bytes"] == pair
+
+
+def test_unsupported_lzo_decompressor_variant_fails(provider, tmp_path):
+    maps = datagen.wordcount(num_maps=2, reducers=1, words_per_map=100, seed=5)
+    publish(provider, tmp_path, "job_1_0045", maps, codec="lzo")
+    with pytest.raises(Exception, match="lzo.decompressor"):
+        UdaConsumer(2, "job_1_0045", "attempt_job_1_0045_r_000000_0", datagen.TEXT, codec="lzo",
+                    conf={"io.compression.codec.lzo.decompressor": "LZO1F"})
+
+
 def test_hybrid_merge_spills_lpqs(provider, tmp_path):
     maps = datagen.terasort(num_maps=23, reducers=1, rows_per_map=200, seed=4)
     ids = publish(provider, tmp_path, "job_1_0005", maps)
