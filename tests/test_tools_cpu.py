@@ -67,3 +67,29 @@ def test_nightly_build_stage_installs_release(tmp_path):
     rep = json.load(open(out / "nightly.json"))
     assert rep["stages"]["build"]["status"] == "PASS"
     assert os.path.exists(os.path.join(ROOT, "uda_amd", "lib", "libuda.so"))
+
+
+def test_telemetry_sampler_writes_csv(tmp_path):
+    import csv
+    import time
+
+    from uda_amd.utils.telemetry import Telemetry
+    path = tmp_path / "t.csv"
+    with Telemetry(str(path), interval=0.05) as t:
+        time.sleep(0.3)
+    rows = list(csv.DictReader(open(path)))
+    assert len(rows) >= 3 and float(rows[-1]["t_s"]) >= 0.25
+    s = t.summary()
+    assert s["samples"] == len(rows) and s["cpu_pct"]["peak"] >= 0 and s["mem_used_gb"]["mean"] > 0
+
+
+def test_regression_records_telemetry(tmp_path):
+    import regression
+    m = tmp_path / "m.csv"
+    m.write_text("name,program,maps,reducers,gb,codec,backend,approach,transport,samples\n"
+                 "wc,wordcount,3,2,0.002,none,cpu,1,loopback,1\n")
+    out = tmp_path / "out"
+    assert regression.main(["--matrix", str(m), "--out", str(out), "--telemetry", "0.05"]) == 0
+    assert (out / "logs" / "wc" / "sample0.dstat.csv").exists()
+    rep = json.load(open(out / "report.json"))
+    assert rep["tests"][0]["telemetry"][0]["samples"] >= 1

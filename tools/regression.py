@@ -60,8 +60,9 @@ def summarize(xs: list[float]) -> dict:
             "min": min(xs), "max": max(xs)}
 
 
-def run_test(row: dict, samples: int, scale: float, out_dir: str, gpu: bool) -> dict:
+def run_test(row: dict, samples: int, scale: float, out_dir: str, gpu: bool, telemetry: float = 0.0) -> dict:
     from uda_amd.models.jobs import ShuffleJobSpec, run_job
+    from uda_amd.utils.telemetry import Telemetry
     name = row["name"]
     spec_fields = {k: v for k, v in row.items() if k not in ("name", "samples")}
     spec = ShuffleJobSpec.from_dict(spec_fields)
@@ -76,11 +77,19 @@ def run_test(row: dict, samples: int, scale: float, out_dir: str, gpu: bool) -> 
     errors = []
     for k in range(samples):
         spec.seed = 7 + k
+        # dstat-equivalent per-sample telemetry (mr-dstatExcel.sh:89-201)
+        tel = Telemetry(os.path.join(log_dir, f"sample{k}.dstat.csv"), telemetry) if telemetry > 0 else None
         try:
+            if tel:
+                tel.start()
             r = run_job(spec)
         except Exception as e:  # noqa: BLE001  (a crashing sample is a failed test, keep going)
             errors.append(f"sample {k}: {type(e).__name__}: {e}")
             continue
+        finally:
+            if tel:
+                tel.stop()
+                res.setdefault("telemetry", []).append(tel.summary())
         with open(os.path.join(log_dir, f"sample{k}.log"), "w") as f:
             f.write("\n".join(r["logs"]) + "\n")
         health = analyze_logs(r["logs"], spec.reducers)
@@ -125,6 +134,8 @@ def main(argv=None) -> int:
     ap.add_argument("--only", action="append", default=[], help="run only these test names")
     ap.add_argument("--samples", type=int, default=0, help="override the matrix NSAMPLES")
     ap.add_argument("--scale", type=float, default=1.0, help="multiply every test's data size")
+    ap.add_argument("--telemetry", type=float, default=0.0, metavar="SECONDS",
+                    help="sample CPU/mem/disk/net/GPU every SECONDS into logs/<test>/sample<k>.dstat.csv")
     a = ap.parse_args(argv)
     from uda_amd import native
     gpu = native().device_count() > 0
@@ -135,7 +146,7 @@ def main(argv=None) -> int:
     for row in rows:
         samples = a.samples or int(row.get("samples") or 1)
         t0 = time.perf_counter()
-        r = run_test(row, samples, a.scale, a.out, gpu)
+        r = run_test(row, samples, a.scale, a.out, gpu, a.telemetry)
         r["elapsed_s"] = time.perf_counter() - t0
         print(f"{r['status']:4s} {r['name']:28s} "
               + (f"{r['gbps']['mean']:.3f} GB/s" if r.get("gbps") else r.get("reason", "")), flush=True)
