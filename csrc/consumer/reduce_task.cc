@@ -2,6 +2,7 @@
 #include "uda/fault.h"
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -9,6 +10,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
+#include <map>
 #include <random>
 #include <sstream>
 
@@ -189,6 +192,10 @@ void ReduceTask::handle(const HadoopCmd& cmd) {
     case kFetchMsg: {
       FetchParams f;
       if (!parse_fetch_params(cmd, &f, &err)) throw ProtocolError(err);
+      if (restored_maps_.count(f.map_id)) {  // already merged into a checkpointed LPQ
+        UDA_LOG(kDebug, "fetch of %s skipped: restored from the LPQ checkpoint", f.map_id.c_str());
+        break;
+      }
       {
         std::lock_guard<std::mutex> g(mu_);
         fetch_list_.push_back(f);
@@ -292,10 +299,60 @@ void ReduceTask::on_init(const InitParams& p) {
   UDA_LOG(kInfo, "reduce task %s: maps=%d approach=%d lpqs=%d kv_bufs=%d buffer=%ld codec=%s key=%s backend=%s",
           p.reduce_task_id.c_str(), maps, net_.online, num_lpqs_, num_kv_bufs_, (long)buffer_size_,
           codec_name(codec_), key_kind_name(kind_), backend_.c_str());
+  checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && net_.online == 2 && backend_ == "cpu";
+  if (checkpoint_) load_checkpoint();
   merge_thr_ = std::thread([this] { merge_main(); });
 }
 
+std::string ReduceTask::checkpoint_path() const {
+  // keyed by job + partition, not by attempt: attempt_<job>_r_<part>_<n> -> drop "_<n>"
+  std::string key = init_.reduce_task_id;
+  const size_t u = key.rfind('_');
+  if (u != std::string::npos && u + 1 < key.size() &&
+      key.find_first_not_of("0123456789", u + 1) == std::string::npos)
+    key.resize(u);
+  const std::string dir = init_.local_dirs.empty() ? std::string("/tmp") : init_.local_dirs[0];
+  return dir + "/uda." + key + ".lpq.manifest";
+}
+
+// Manifest lines: "lpq <index> <bytes> <path> <map_id,map_id,...>". An entry is taken only if it
+// continues the LPQ sequence, its file exists with that size and it holds the MOF count the LPQ
+// geometry gives that index (same num_maps / lpq_size as the failed attempt).
+void ReduceTask::load_checkpoint() {
+  std::ifstream in(checkpoint_path());
+  if (!in) return;
+  const int maps = init_.num_maps;
+  if (num_lpqs_ <= 1 || maps < num_lpqs_) return;
+  const int per = maps / num_lpqs_;
+  const int regular = num_lpqs_ - maps % num_lpqs_;
+  std::string line;
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    std::string tag, path, ids;
+    int idx = -1;
+    long long bytes = -1;
+    if (!(ls >> tag >> idx >> bytes >> path >> ids) || tag != "lpq") break;
+    const int want = (idx < regular) ? per : per + 1;
+    struct stat sb;
+    if (idx != (int)restored_files_.size() || ::stat(path.c_str(), &sb) != 0 || (long long)sb.st_size != bytes) break;
+    std::vector<std::string> v;
+    for (size_t b = 0; b <= ids.size();) {
+      const size_t e = ids.find(',', b);
+      v.push_back(ids.substr(b, e == std::string::npos ? std::string::npos : e - b));
+      if (e == std::string::npos) break;
+      b = e + 1;
+    }
+    if ((int)v.size() != want) break;
+    restored_files_.push_back(path);
+    restored_maps_.insert(v.begin(), v.end());
+  }
+  if (!restored_files_.empty())
+    UDA_LOG(kInfo, "LPQ checkpoint: resuming with %zu LPQs (%zu MOFs) from %s", restored_files_.size(),
+            restored_maps_.size(), checkpoint_path().c_str());
+}
+
 void ReduceTask::exit() {
+  exiting_ = true;
   stop_ = true;
   cv_.notify_all();
   if (merge_thr_.joinable()) merge_thr_.join();
@@ -328,7 +385,9 @@ void ReduceTask::merge_main() {
     else
       merge_online();
   } catch (const std::exception& e) {
-    if (!stop_) host_->fail(e.what());
+    // stop_ alone also means "an internal failure stopped the fetchers": only a host-requested
+    // exit() silences the report
+    if (!exiting_) host_->fail(e.what());
   }
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -344,7 +403,7 @@ std::unique_ptr<Segment> ReduceTask::segment_for(std::shared_ptr<MofFetcher> f, 
   return seg;
 }
 
-void ReduceTask::fetch_phase(MergeQueue* q, int n) {
+void ReduceTask::fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids) {
   std::mt19937_64 rng((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
   int sent = 0, inserted = 0;
   std::vector<FetchParams> pending;
@@ -376,6 +435,7 @@ void ReduceTask::fetch_phase(MergeQueue* q, int n) {
     }
     for (auto& f : to_start) f->start();
     for (auto& f : arrived) {
+      if (map_ids) map_ids->push_back(f->params().map_id);
       q->insert(segment_for(f, next_index_++));
       inserted++;
       total_count_++;
@@ -437,10 +497,21 @@ void ReduceTask::merge_hybrid() {
   ExternalQuotaQueue<std::pair<MergeQueue*, std::string>> pending((size_t)num_parallel_lpqs_);
   std::exception_ptr fetch_err;
   auto t0 = std::chrono::steady_clock::now();
+  const int first = (int)restored_files_.size();  // LPQs restored from a checkpoint
+  std::mutex ids_mu;
+  std::map<std::string, std::vector<std::string>> lpq_ids;  // spill path -> its MOFs
+  if (first > 0) {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.restored_lpqs = first;
+    st_.restored_maps = (int64_t)restored_maps_.size();
+    st_.maps_fetched += (int64_t)restored_maps_.size();
+  }
+  total_count_ += (int)restored_maps_.size();
+  if (first > 0 && total_count_ == maps) host_->fetch_over();
   // LPQ fetcher thread (fetch_lpqs, MergeManager.cc:202-232)
   std::thread fetcher([&] {
     try {
-      for (int i = 0; i < num_lpqs_; ++i) {
+      for (int i = first; i < num_lpqs_; ++i) {
         const int n = (i < regular) ? per : per + 1;
         const std::string& dir = dirs[(size_t)(++dir_counter) % dirs.size()];
         char name[64];
@@ -448,7 +519,12 @@ void ReduceTask::merge_hybrid() {
         std::string path = dir + "/uda." + init_.reduce_task_id + name;
         pending.wait_and_reserve();
         auto* q = new MergeQueue(kind_);
-        fetch_phase(q, n);
+        std::vector<std::string> ids;
+        fetch_phase(q, n, checkpoint_ ? &ids : nullptr);
+        {
+          std::lock_guard<std::mutex> g(ids_mu);
+          lpq_ids[path] = std::move(ids);
+        }
         pending.push_reserved({q, path});
       }
     } catch (...) {
@@ -456,10 +532,16 @@ void ReduceTask::merge_hybrid() {
       pending.push_reserved({nullptr, std::string()});
     }
   });
-  std::vector<std::string> files;
+  std::vector<std::string> files = restored_files_;
+  size_t checkpointed = files.size();  // files[0, checkpointed) are listed in the manifest
+  const std::string manifest = checkpoint_ ? checkpoint_path() : std::string();
+  if (checkpoint_ && first == 0) ::unlink(manifest.c_str());  // stale or unusable: start over
+  auto discard = [&] {  // failure: keep what the manifest lists when checkpointing
+    for (size_t k = checkpoint_ ? checkpointed : 0; k < files.size(); ++k) ::unlink(files[k].c_str());
+  };
   std::vector<uint8_t> buf((size_t)kv_buf_size_);
   try {
-    for (int i = 0; i < num_lpqs_; ++i) {
+    for (int i = first; i < num_lpqs_; ++i) {
       auto item = pending.wait_and_pop_without_dereserve();
       if (!item.first) break;
       std::unique_ptr<MergeQueue> q(item.first);
@@ -485,6 +567,26 @@ void ReduceTask::merge_hybrid() {
         ::close(fd);
         throw UdaError("spill write failed");
       }
+      if (checkpoint_) {
+        // durable before it is listed: a resumed attempt trusts every manifest entry
+        if (::fsync(fd) != 0) {
+          ::close(fd);
+          throw UdaError("spill fsync failed");
+        }
+        std::string ids;
+        {
+          std::lock_guard<std::mutex> g(ids_mu);
+          for (const auto& m : lpq_ids[item.second]) ids += (ids.empty() ? "" : ",") + m;
+        }
+        std::ofstream mf(manifest, std::ios::app);
+        mf << "lpq " << i << " " << written + 2 << " " << item.second << " " << ids << "\n";
+        mf.flush();
+        if (!mf) {
+          ::close(fd);
+          throw UdaError("cannot append to LPQ manifest " + manifest);
+        }
+        checkpointed = files.size();
+      }
       ::close(fd);
       {
         std::lock_guard<std::mutex> g(st_mu_);
@@ -492,18 +594,19 @@ void ReduceTask::merge_hybrid() {
         st_.spill_bytes += written + 2;
       }
       pending.dereserve();
+      if (fault_hit("LPQ_DONE")) throw UdaError("injected failure after an LPQ spill");
     }
   } catch (...) {
     stop_ = true;
     cv_.notify_all();
     pending.dereserve();
     fetcher.join();
-    for (auto& f : files) ::unlink(f.c_str());
+    discard();
     throw;
   }
   fetcher.join();
   if (fetch_err) {
-    for (auto& f : files) ::unlink(f.c_str());
+    discard();
     std::rethrow_exception(fetch_err);
   }
   const double fetch_ms = ms_since(t0);
@@ -523,6 +626,7 @@ void ReduceTask::merge_hybrid() {
   merging_phase(&rpq);
   for (auto& s : srcs) ::close(s->fd);
   for (auto& f : files) ::unlink(f.c_str());  // transient, like SuperSegment's dtor
+  if (checkpoint_) ::unlink(manifest.c_str());
   std::lock_guard<std::mutex> g(st_mu_);
   st_.fetch_ms = fetch_ms;
   st_.merge_ms = ms_since(t0) - fetch_ms;
@@ -544,7 +648,8 @@ std::string ReduceTask::stats_json() const {
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
-    << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+    << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
+    << ",\"restored_maps\":" << s.restored_maps << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }
 

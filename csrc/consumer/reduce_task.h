@@ -15,6 +15,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -47,6 +48,7 @@ struct ReduceStats {
   double gpu_h2d_ms = 0, gpu_device_ms = 0, gpu_d2h_wait_ms = 0, gpu_sink_ms = 0;
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
   int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;
+  int64_t restored_lpqs = 0, restored_maps = 0;  // hybrid resume from an LPQ checkpoint
   std::string backend;
 };
 
@@ -75,7 +77,11 @@ class ReduceTask {
   void merge_hybrid();
   void merge_gpu();
   // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
-  void fetch_phase(MergeQueue* q, int n);
+  void fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids = nullptr);
+  // LPQ checkpoint (mapred.uda.lpq.checkpoint): completed LPQ spill files survive a failed attempt,
+  // listed in a manifest keyed by job + partition; the next attempt skips their MOFs.
+  void load_checkpoint();
+  std::string checkpoint_path() const;
   void merging_phase(MergeQueue* q);
   std::unique_ptr<Segment> segment_for(std::shared_ptr<MofFetcher> f, int index);
 
@@ -90,6 +96,9 @@ class ReduceTask {
   int num_kv_bufs_ = 0;
   int num_lpqs_ = 0;
   int num_parallel_lpqs_ = 3;
+  bool checkpoint_ = false;
+  std::vector<std::string> restored_files_;   // LPQ files of the previous attempt, in LPQ order
+  std::set<std::string> restored_maps_;       // their MOFs (FETCHes for these are dropped)
   std::string backend_ = "cpu";
   std::unique_ptr<ClientTransport> transport_;
 
@@ -103,6 +112,7 @@ class ReduceTask {
   int progress_count_ = 0;
   bool final_ = false;
   std::atomic<bool> stop_{false};
+  std::atomic<bool> exiting_{false};  // exit() from the host (not a failure)
   std::atomic<bool> finished_{false};
   std::thread merge_thr_;
   bool inited_ = false;

@@ -137,6 +137,38 @@ def test_hybrid_merge_spills_lpqs(provider, tmp_path):
     assert not os.listdir(d1) and not os.listdir(d2)  # LPQ files are transient
 
 
+def test_hybrid_lpq_checkpoint_resume(provider, tmp_path, monkeypatch):
+    """mapred.uda.lpq.checkpoint: attempt 0 fails after its 2nd LPQ spill; the LPQ files and the
+    manifest survive; attempt 1 of the same partition restores both LPQs, fetches only the other
+    MOFs and produces the same merged output; everything is removed after success."""
+    maps = datagen.terasort(num_maps=23, reducers=1, rows_per_map=200, seed=4)
+    ids = publish(provider, tmp_path, "job_1_0015", maps)
+    d1 = tmp_path / "ld"
+    d1.mkdir()
+    conf = {"mapred.uda.lpq.checkpoint": 1}
+    kw = dict(approach=2, lpq_size=5, local_dirs=(str(d1),), conf=conf)
+    monkeypatch.setenv("UDA_FAULT_LPQ_DONE", "2")
+    c = UdaConsumer(len(ids), "job_1_0015", "attempt_job_1_0015_r_000000_0", datagen.TEXT, **kw)
+    for m in ids:
+        c.fetch("h", "job_1_0015", m, 0)
+    with pytest.raises(UdaFallback, match="injected"):
+        c.wait(60)
+    c.close()
+    monkeypatch.delenv("UDA_FAULT_LPQ_DONE")
+    manifest = d1 / "uda.attempt_job_1_0015_r_000000.lpq.manifest"
+    lines = manifest.read_text().splitlines()
+    assert [ln.split()[1] for ln in lines] == ["0", "1"]
+    kept = sorted(os.listdir(d1))
+    assert len(kept) == 3  # manifest + 2 LPQ files; the in-progress LPQ was removed
+    restored = {m for ln in lines for m in ln.split()[4].split(",")}
+    assert len(restored) == 8  # 23 maps / lpq 5: LPQ sizes 4,4,5,5,5 (remainder spread)
+    recs, st, _ = run_reduce("h", "job_1_0015", ids, 0, datagen.TEXT, **kw)
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+    assert st["restored_lpqs"] == 2 and st["restored_maps"] == 8 and st["maps_fetched"] == 23
+    assert st["lpqs"] == 3  # only the remaining LPQs were built
+    assert not os.listdir(d1)
+
+
 def test_int_and_bytes_keys(provider, tmp_path):
     import random
     rng = random.Random(8)
