@@ -16,6 +16,7 @@
 //        splitter all fall in the later round, in every run, so ties keep run order.
 // Reference counterpart of the online path: merge_online (MergeManager.cc:184-193).
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
@@ -23,6 +24,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <fstream>
 #include <random>
 #include <thread>
 
@@ -31,6 +33,7 @@
 #include "../gpu/generic_merger.h"
 #include "reduce_task.h"
 #include "uda/aio.h"
+#include "uda/fault.h"
 #include "uda/compare.h"
 #include "uda/ifile.h"
 #include "uda/log.h"
@@ -252,13 +255,25 @@ void ReduceTask::merge_gpu() {
   std::unique_ptr<AsyncIO> aio;
   std::vector<std::string> dirs = init_.local_dirs;
   if (dirs.empty()) dirs.push_back("/tmp");
-  auto cleanup = [&] {
-    for (auto& r : spills) {
+  // LPQ checkpoint (disk tier): spills[0, checkpointed) are fsynced, indexed in <path>.idx and
+  // listed in the manifest; a failed attempt keeps them for the next one
+  const bool ckpt = checkpoint_ && tier == "disk";
+  const std::string manifest = ckpt ? checkpoint_path() : std::string();
+  size_t checkpointed = 0;
+  std::vector<std::string> group_ids;  // MOFs of the current group (for the manifest)
+  auto cleanup = [&](bool ok) {
+    for (size_t i = 0; i < spills.size(); ++i) {
+      SpillRun& r = spills[i];
       if (r.fd >= 0) ::close(r.fd);
-      if (!r.path.empty()) ::unlink(r.path.c_str());
+      const bool keep = !ok && ckpt && i < checkpointed;
+      if (!r.path.empty() && !keep) {
+        ::unlink(r.path.c_str());
+        if (ckpt) ::unlink((r.path + ".idx").c_str());
+      }
       r.fd = -1;
       r.path.clear();
     }
+    if (ok && ckpt) ::unlink(manifest.c_str());
   };
   auto count_decoded = [&](int64_t n) {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -310,13 +325,85 @@ void ReduceTask::merge_gpu() {
       st_.lpqs++;
       st_.spill_bytes += run.bytes;
     }
+    const std::string run_path = run.path;
+    const int run_fd = run.fd;
+    std::vector<int64_t> idx_cut = ckpt ? run.cut : std::vector<int64_t>();
+    std::vector<std::string> idx_key = ckpt ? run.key : std::vector<std::string>();
+    const int64_t run_bytes = run.bytes;
     spills.push_back(std::move(run));
+    std::vector<std::string> ids;
+    ids.swap(group_ids);
+    if (ckpt && disk) {
+      // durable before listed: data, then the sparse index, then the manifest line
+      if (::fsync(run_fd) != 0) throw UdaError("spill fsync failed");
+      const std::string ip = run_path + ".idx";
+      {
+        std::ofstream ix(ip, std::ios::binary | std::ios::trunc);
+        const int64_t n = (int64_t)idx_cut.size();
+        ix.write(reinterpret_cast<const char*>(&n), 8);
+        for (size_t j = 0; j < idx_cut.size(); ++j) {
+          const int32_t kl = (int32_t)idx_key[j].size();
+          ix.write(reinterpret_cast<const char*>(&idx_cut[j]), 8);
+          ix.write(reinterpret_cast<const char*>(&kl), 4);
+          ix.write(idx_key[j].data(), kl);
+        }
+        ix.flush();
+        if (!ix) throw UdaError("cannot write LPQ index " + ip);
+      }
+      const int ifd = ::open(ip.c_str(), O_RDONLY | O_CLOEXEC);
+      if (ifd < 0 || ::fsync(ifd) != 0) throw UdaError("LPQ index fsync failed");
+      ::close(ifd);
+      std::string line = "glpq " + std::to_string(spills.size() - 1) + " " + std::to_string(run_bytes) + " " + run_path + " ";
+      for (size_t j = 0; j < ids.size(); ++j) line += (j ? "," : "") + ids[j];
+      std::ofstream mf(manifest, std::ios::app);
+      mf << line << "\n";
+      mf.flush();
+      if (!mf) throw UdaError("cannot append to LPQ manifest " + manifest);
+      checkpointed = spills.size();
+      if (fault_hit("LPQ_DONE")) throw UdaError("injected failure after an LPQ spill");
+    }
   };
+  // resume: restored LPQ spills (data + sparse index) of a failed attempt
+  if (ckpt && restored_files_.empty()) ::unlink(manifest.c_str());
+  for (const std::string& path : restored_files_) {
+    SpillRun run;
+    run.path = path;
+    run.fd = ::open(path.c_str(), O_RDWR | O_CLOEXEC);
+    struct stat sb;
+    if (run.fd < 0 || ::fstat(run.fd, &sb) != 0) throw UdaError("cannot reopen checkpointed LPQ " + path);
+    run.bytes = (int64_t)sb.st_size;
+    std::ifstream ix(path + ".idx", std::ios::binary);
+    int64_t n = -1;
+    ix.read(reinterpret_cast<char*>(&n), 8);
+    if (!ix || n < 0) throw UdaError("bad LPQ index " + path + ".idx");
+    for (int64_t j = 0; j < n; ++j) {
+      int64_t c = 0;
+      int32_t kl = 0;
+      ix.read(reinterpret_cast<char*>(&c), 8);
+      ix.read(reinterpret_cast<char*>(&kl), 4);
+      if (!ix || kl < 0) throw UdaError("bad LPQ index " + path + ".idx");
+      std::string k((size_t)kl, '\0');
+      ix.read(&k[0], kl);
+      run.cut.push_back(c);
+      run.key.push_back(std::move(k));
+    }
+    spills.push_back(std::move(run));
+  }
+  checkpointed = spills.size();
+  if (!spills.empty()) {
+    if (!aio) aio = AsyncIO::create(AsyncIO::Options{});
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.restored_lpqs = (int64_t)spills.size();
+    st_.restored_maps = (int64_t)restored_maps_.size();
+    st_.maps_fetched += (int64_t)restored_maps_.size();
+  }
 
   try {
     // ---- fetch: start every MOF (bounded by the buffer pool), drain each fully into host memory
     std::mt19937_64 rng((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count());
-    int started = 0, drained = 0;
+    int started = (int)restored_maps_.size(), drained = started;
+    total_count_ += started;
+    if (started > 0 && total_count_ == maps) host_->fetch_over();
     std::vector<FetchParams> pending;
     std::vector<std::shared_ptr<MofFetcher>> ready;
     while (drained < maps) {
@@ -398,6 +485,7 @@ void ReduceTask::merge_gpu() {
             got[k] = Span{p, (int64_t)host_decoded[k].size()};
           }
           group.push_back(got[k]);
+          if (ckpt) group_ids.push_back(ready[sub[k]]->params().map_id);
           drained++;
           progress_count_++;
           total_count_++;
@@ -563,7 +651,7 @@ void ReduceTask::merge_gpu() {
       st_.buffers++;
       st_.bytes_delivered += kEofBytes;
     }
-    cleanup();
+    cleanup(true);
     std::lock_guard<std::mutex> g(st_mu_);
     st_.gpu_h2d_ms = ws.h2d_ms;
     st_.gpu_device_ms = ws.device_ms;
@@ -572,7 +660,7 @@ void ReduceTask::merge_gpu() {
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
   } catch (...) {
-    cleanup();
+    cleanup(false);
     throw;
   }
 }

@@ -299,7 +299,8 @@ void ReduceTask::on_init(const InitParams& p) {
   UDA_LOG(kInfo, "reduce task %s: maps=%d approach=%d lpqs=%d kv_bufs=%d buffer=%ld codec=%s key=%s backend=%s",
           p.reduce_task_id.c_str(), maps, net_.online, num_lpqs_, num_kv_bufs_, (long)buffer_size_,
           codec_name(codec_), key_kind_name(kind_), backend_.c_str());
-  checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && net_.online == 2 && backend_ == "cpu";
+  // CPU: the hybrid (approach 2) LPQ files; GPU: the disk-tier LPQ spills of the GPU hybrid merge
+  checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && (backend_ == "gpu" || net_.online == 2);
   if (checkpoint_) load_checkpoint();
   merge_thr_ = std::thread([this] { merge_main(); });
 }
@@ -322,6 +323,37 @@ void ReduceTask::load_checkpoint() {
   std::ifstream in(checkpoint_path());
   if (!in) return;
   const int maps = init_.num_maps;
+  if (backend_ == "gpu") {  // "glpq <index> <bytes> <path> <ids>": groups are budget-sized, no geometry
+    std::string line;
+    while (std::getline(in, line)) {
+      std::istringstream ls(line);
+      std::string tag, path, ids;
+      int idx = -1;
+      long long bytes = -1;
+      if (!(ls >> tag >> idx >> bytes >> path >> ids) || tag != "glpq") break;
+      struct stat sb, si;
+      if (idx != (int)restored_files_.size() || ::stat(path.c_str(), &sb) != 0 || (long long)sb.st_size != bytes ||
+          ::stat((path + ".idx").c_str(), &si) != 0)
+        break;
+      std::set<std::string> v;
+      for (size_t b = 0;;) {
+        const size_t e = ids.find(',', b);
+        v.insert(ids.substr(b, e == std::string::npos ? std::string::npos : e - b));
+        if (e == std::string::npos) break;
+        b = e + 1;
+      }
+      restored_files_.push_back(path);
+      restored_maps_.insert(v.begin(), v.end());
+    }
+    if ((int)restored_maps_.size() > maps) {  // not this job's shape: start over
+      restored_files_.clear();
+      restored_maps_.clear();
+    }
+    if (!restored_files_.empty())
+      UDA_LOG(kInfo, "GPU LPQ checkpoint: resuming with %zu LPQs (%zu MOFs)", restored_files_.size(),
+              restored_maps_.size());
+    return;
+  }
   if (num_lpqs_ <= 1 || maps < num_lpqs_) return;
   const int per = maps / num_lpqs_;
   const int regular = num_lpqs_ - maps % num_lpqs_;

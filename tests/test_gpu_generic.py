@@ -134,6 +134,49 @@ def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
         p.close()
 
 
+def test_consumer_gpu_hybrid_checkpoint_resume(require_gpu, tmp_path, monkeypatch):
+    """mapred.uda.lpq.checkpoint with the GPU hybrid merge (disk tier): attempt 0 fails after its
+    2nd LPQ spill; attempt 1 restores both spills (data + sparse index), fetches only the other MOFs
+    and delivers the same merged output; nothing is left behind after success."""
+    from uda_amd.bridge import UdaConsumer, UdaFallback
+    from uda_amd.utils.mof import write_mof
+    p = UdaProvider()
+    try:
+        maps = datagen.secondary_sort(num_maps=12, reducers=2, rows_per_map=2000, seed=6)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_hck_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts)
+            p.add_mof_file("job_hck", mid, path)
+            ids.append(mid)
+        d1 = tmp_path / "ld1"
+        d1.mkdir()
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.merge.bytes": 300_000,
+                "mapred.uda.gpu.spill": "disk", "mapred.uda.lpq.checkpoint": 1}
+        kw = dict(conf=conf, kv_buf_size=8192, local_dirs=(str(d1),))
+        monkeypatch.setenv("UDA_FAULT_LPQ_DONE", "2")
+        c = UdaConsumer(len(ids), "job_hck", "attempt_job_hck_r_000000_0", datagen.TEXT, **kw)
+        for m in ids:
+            c.fetch("h", "job_hck", m, 0)
+        with pytest.raises(UdaFallback, match="injected"):
+            c.wait(60)
+        c.close()
+        monkeypatch.delenv("UDA_FAULT_LPQ_DONE")
+        lines = (d1 / "uda.attempt_job_hck_r_000000.lpq.manifest").read_text().splitlines()
+        assert [ln.split()[:2] for ln in lines] == [["glpq", "0"], ["glpq", "1"]]
+        restored = {m for ln in lines for m in ln.split()[4].split(",")}
+        recs, st, _ = run_reduce("h", "job_hck", ids, 0, datagen.TEXT, **kw)
+        assert st["restored_lpqs"] == 2 and st["restored_maps"] == len(restored) > 0, st
+        assert st["maps_fetched"] == len(ids)
+        want = sorted((kv for m in maps for kv in m[0]), key=datagen.sort_key(datagen.TEXT))
+        kf = datagen.sort_key(datagen.TEXT)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+        assert sorted(recs) == sorted(want)
+        assert not os.listdir(d1)
+    finally:
+        p.close()
+
+
 def test_consumer_gpu_device_alloc_fault_fails_once(require_gpu, tmp_path, monkeypatch):
     from uda_amd.bridge import UdaConsumer, UdaFallback
     from uda_amd.utils.mof import write_mof
