@@ -66,7 +66,7 @@ def test_merge_tree_many_runs(require_gpu):
     assert st["merge_passes"] == 9
 
 
-@pytest.mark.parametrize("world,maps,rounds", [(2, 3, 3), (3, 2, 4), (4, 1, 1)])
+@pytest.mark.parametrize("world,maps,rounds", [(2, 3, 3), (3, 2, 4), (4, 1, 1), (8, 2, 16)])
 def test_multirank_schedule_local_group(require_gpu, world, maps, rounds):
     """The multi-GPU shuffle schedule (pack -> all-to-all-v rounds -> merge -> deliver) rehearsed
     with `world` ranks sharing one GPU; every reducer must receive exactly its key range."""
