@@ -31,8 +31,11 @@ def main() -> int:
     ap.add_argument("--rows-per-gpu", type=int, default=1_250_000_000)
     ap.add_argument("--maps-per-gpu", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=16)
-    ap.add_argument("--d2h-piece-mb", type=int, default=64)
-    ap.add_argument("--pinned-slots", type=int, default=6)
+    # D2H staging: 4 x 512 MiB pinned pieces on one copy stream. Swept on MI355X
+    # (profiles/r1_d2h_sweep.json): 64 MiB x6 -> 55.9 GB/s, 512 MiB x4 -> 56.7 GB/s against a
+    # 57.0 GB/s single-copy PCIe roof; two copy streams contend and drop to ~22 GB/s.
+    ap.add_argument("--d2h-piece-mb", type=int, default=512)
+    ap.add_argument("--pinned-slots", type=int, default=4)
     ap.add_argument("--d2h-streams", type=int, default=1)
     ap.add_argument("--device-only", action="store_true",
                     help="ablation: stop after the device merge (no host delivery); not the headline")
