@@ -67,6 +67,20 @@ int main(int argc, char** argv) {
       std::printf(", \"%s_memcpy_%s\": %.2f", fname[f], piece_mb ? (piece_mb == 1 ? "1MiB" : "16MiB") : "whole",
                   reps * bytes / (time_ms(e0, e1) * 1e-3) / 1e9);
     }
+    // 512 MiB pieces at record-aligned (104 B) vs 4 KiB-aligned offsets: does alignment pick the engine?
+    for (size_t shift : {(size_t)104, (size_t)4096}) {
+      const size_t piece = (size_t)512 << 20;
+      const int np = (int)((bytes - shift) / piece);
+      CK(hipEventRecord(e0, s));
+      for (int r = 0; r < reps; ++r)
+        for (int i = 0; i < np; ++i)
+          CK(hipMemcpyAsync((char*)h + shift + i * piece, (char*)d + shift + i * piece, piece - 104,
+                            hipMemcpyDeviceToHost, s));
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      std::printf(", \"%s_memcpy_512MiB_off%zu\": %.2f", fname[f], shift,
+                  (double)reps * np * (piece - 104) / (time_ms(e0, e1) * 1e-3) / 1e9);
+    }
     for (int blocks : {256, 1024, 4096, 16384}) {
       store_to_host<<<blocks, 256, 0, s>>>((const v4u*)d, (v4u*)h, n16);
       CK(hipGetLastError());
