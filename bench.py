@@ -2,14 +2,23 @@
 """Headline benchmark: TeraSort shuffle+merge GB/s, whole node (BASELINE.json).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1 is launched by torchrun: one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE from env)
 
-One step = the whole reduce-side shuffle of a TeraSort job: every GPU's reducer receives its key
-range from every GPU's map outputs (RCCL all-to-all over xGMI in key-range rounds), merges them on
-the GPU and delivers the merged records to the host reducer in <=1 MiB whole-record buffers
-(the `dataFromUda` contract), EOF marker included. Per-GPU data is fixed (weak scaling):
---rows-per-gpu TeraGen rows (104-byte IFile records) per GPU; the default 1.25e9 rows/GPU makes
-N=8 the 1 TB TeraSort config (N=1 moves 130 GB through one GPU).
+One process per GPU. Under torchrun (RANK/LOCAL_RANK/WORLD_SIZE set) this process is one rank;
+otherwise `--gpus N` (N > 1) starts the N rank processes itself (before anything touches the GPU)
+with a 127.0.0.1 rendezvous, and rank 0 prints the result.
+
+One step = the whole reduce-side shuffle of a TeraSort job: every GPU hosts `--reducers` reduce
+tasks; each reducer receives its key range from every GPU's map outputs (RCCL all-to-all over
+xGMI in key-range rounds), merges it on the GPU and its consumer thread receives the merged
+records in <=1 MiB whole-record buffers (the `dataFromUda` contract, EOF marker included). The
+consumer does the Java side's work on every buffer: copy into a 1 MiB KVBuf and walk the records
+by their VInt lengths (J2CQueue); every step checks the parsed record count of every reducer.
+Per-GPU data is fixed (weak scaling): --rows-per-gpu TeraGen rows (104-byte IFile records) per
+GPU; the default 1.25e9 rows/GPU makes N=8 the 1 TB TeraSort config (N=1 moves 130 GB).
+
+After the timed steps one more (untimed) step runs with the device-side validation on: key order
+per reducer, record checksum against the generated data, and (N > 1) per-slice checksums of what
+every peer sent. "validated": true means that step passed.
 
 value = total partition bytes delivered on all GPUs / time per step (GB = 1e9 bytes).
 Data is synthetic (TeraGen-shaped keys/values generated in HBM; see uda_amd/models/terasort.py).
@@ -19,53 +28,107 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
-def main() -> int:
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rows-per-gpu", type=int, default=1_250_000_000)
     ap.add_argument("--maps-per-gpu", type=int, default=32)
-    ap.add_argument("--rounds", type=int, default=16)
-    # D2H staging: 4 x 512 MiB pinned pieces on one copy stream. Swept on MI355X
-    # (profiles/r1_d2h_sweep.json): 64 MiB x6 -> 55.9 GB/s, 512 MiB x4 -> 56.7 GB/s against a
-    # 57.0 GB/s single-copy PCIe roof; two copy streams contend and drop to ~22 GB/s.
-    ap.add_argument("--d2h-piece-mb", type=int, default=512)
-    ap.add_argument("--pinned-slots", type=int, default=4)
-    ap.add_argument("--d2h-streams", type=int, default=1)
+    ap.add_argument("--reducers", type=int, default=8, help="reduce tasks per GPU (each with its own consumer)")
+    ap.add_argument("--rounds", type=int, default=16, help="key cells per reducer = shuffle rounds per step")
+    ap.add_argument("--d2h", choices=("sdma", "hip"), default="sdma",
+                    help="delivery copies: explicit SDMA engines (default) or hipMemcpyAsync")
+    ap.add_argument("--d2h-piece-mb", type=int, default=128)
+    ap.add_argument("--pinned-slots", type=int, default=16)
+    ap.add_argument("--d2h-engines", type=int, default=2)
     ap.add_argument("--device-only", action="store_true",
                     help="ablation: stop after the device merge (no host delivery); not the headline")
-    ap.add_argument("--validate", action="store_true", help="run one extra validated step at the end")
+    ap.add_argument("--no-validate", action="store_true", help="skip the final validated step")
     ap.add_argument("--verbose", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Start one process per GPU (RANK/LOCAL_RANK/WORLD_SIZE in their env); return the worst rc."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, cwd=ROOT))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        if failed:  # one rank died: the others would wait for it in a collective
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.2)
+    return max(abs(rc) for rc in rcs)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)
+    if args.launch_selftest:  # launcher check (CPU tests): report the rank environment, touch no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT")}), flush=True)
+        return 0
 
     import torch  # noqa: F401  (loads the HIP runtime before the native extension)
 
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
     from uda_amd.models.terasort import RECORD_BYTES, TeraSortConfig, TeraSortShuffle
     from uda_amd.parallel.dist import init_from_env
 
     ctx = init_from_env()
     if ctx.world != args.gpus:
-        if ctx.world == 1 and args.gpus > 1:
-            print(f"--gpus {args.gpus} requires a torchrun launch (WORLD_SIZE is 1)", file=sys.stderr)
-            return 2
+        print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
+        return 2
     torch.cuda.set_device(ctx.local_rank)
 
     cfg = TeraSortConfig(rows_per_gpu=args.rows_per_gpu, maps_per_rank=args.maps_per_gpu,
-                         rounds=args.rounds, d2h_piece_bytes=args.d2h_piece_mb << 20,
-                         pinned_slots=args.pinned_slots, d2h_streams=args.d2h_streams,
-                         deliver_host=not args.device_only)
+                         rounds=args.rounds, reducers=args.reducers, d2h=args.d2h,
+                         d2h_piece_bytes=args.d2h_piece_mb << 20, pinned_slots=args.pinned_slots,
+                         d2h_engines=args.d2h_engines, deliver_host=not args.device_only)
     job = TeraSortShuffle(ctx, cfg)
     t_setup = time.perf_counter()
     job.setup()
     t_setup = time.perf_counter() - t_setup
-    if args.verbose and ctx.rank == 0:
+    if ctx.rank == 0:
         print(f"# setup {t_setup:.1f}s {job.setup_s} store={job.job.store_bytes/1e9:.1f}GB "
-              f"max_round_records={job.job.max_round_records}", file=sys.stderr, flush=True)
+              f"max_round_records={job.job.max_round_records} exchange={job.job.exchange_name} "
+              f"delivery={job.job.delivery_name}", file=sys.stderr, flush=True)
 
     for i in range(args.warmup):
         st = job.step()
@@ -84,26 +147,24 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     elapsed = ctx.max_float(elapsed)
     for st in stats:
-        job.check(st)
+        job.check(st)  # consumer record counts / framing / EOF of every timed step
 
     validated = None
-    if args.validate:
-        job.job_validate = True
-        from uda_amd.models.terasort import TeraSortConfig as _C  # noqa: F401
-        vcfg = dict(cfg.__dict__)
-        vcfg["validate"] = True
-        vjob = TeraSortShuffle(ctx, TeraSortConfig(**vcfg))
-        del job  # free HBM before the validation job allocates its own store
-        vjob.setup()
-        vst = vjob.step()
-        vjob.check(vst)
-        validated = True
+    if not args.no_validate:
+        vst = job.step(validate=True)
+        job.check(vst)
+        ok = ctx.all_gather_object(True)
+        validated = all(ok)
+        if args.verbose and ctx.rank == 0:
+            print(f"# validated step: {json.dumps(vst)}", file=sys.stderr, flush=True)
 
     bytes_per_gpu = stats[0]["bytes_in"]
     total_bytes = sum(ctx.all_gather_object(bytes_per_gpu))
+    sent = ctx.all_gather_object(int(sum(s["bytes_sent"] for s in stats) // max(1, len(stats))))
     ms_per_step = elapsed * 1000.0 / max(1, args.steps)
     gbps = total_bytes / (ms_per_step / 1000.0) / 1e9
     mean = lambda k: sum(s[k] for s in stats) / len(stats)  # noqa: E731
+    comm_ranks = job.job.comm_ranks if ctx.world > 1 else None
     if ctx.rank == 0:
         out = {
             "metric": "TeraSort shuffle+merge GB/s whole-node",
@@ -126,13 +187,17 @@ def main() -> int:
                 "rows_per_gpu": args.rows_per_gpu,
                 "total_rows": args.rows_per_gpu * ctx.world,
                 "maps_per_gpu": args.maps_per_gpu,
+                "reducers_per_gpu": args.reducers,
                 "rounds": args.rounds,
-                "shuffle": "rccl-a2a-xgmi" if ctx.world > 1 else "local (single GPU, no all-to-all)",
-                "delivery": "device-only (ablation)" if args.device_only else "host dataFromUda <=1MiB buffers",
+                "shuffle": job.job.exchange_name if ctx.world > 1 else "local (single GPU, no all-to-all)",
+                "delivery": "device-only (ablation)" if args.device_only else
+                            f"{job.job.delivery_name} -> per-reducer J2C consumer (KVBuf memcpy + VInt walk), <=1MiB buffers",
             },
             "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
             "teragen_gbps": round(gbps * 100 / RECORD_BYTES, 3),
-            "breakdown_ms_rank0": {k: round(mean(k), 2) for k in ("split_ms", "comm_ms", "merge_ms", "d2h_ms")},
+            "rccl_ranks": comm_ranks,
+            "bytes_sent_per_rank": sent,
+            "breakdown_ms_rank0": {k: round(mean(k), 2) for k in ("comm_ms", "merge_ms", "d2h_ms", "wait_out_ms")},
             "merge_passes": stats[0]["merge_passes"],
             "buffers_per_step": stats[0]["buffers"],
             "validated": validated,

@@ -1,5 +1,6 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
+#include "merge_plan.h"
 #include "uda/fault.h"
 #include "uda/trace.h"
 
@@ -163,9 +164,10 @@ int device_count() {
   return n;
 }
 
+
 // ------------------------------------------------------------------------------ DeviceMerger
 // Per-round plan blob layout (all int64 unless noted), uploaded with one H2D copy:
-//   RunDesc runs[K] | int64 elem_off[K+1] | uint8_t* bases[K] | per pass p: seg_off, tile_prefix
+//   RunDesc runs[K] | int64 elem_off[K+1] | uint8_t* bases[K] | per pass: pairs[3P], tile_prefix[P+1]
 DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
     : max_records_(max_records), max_runs_(max_runs) {
   elems_a_.alloc((size_t)std::max<int64_t>(max_records, 1) * sizeof(Elem));
@@ -177,8 +179,9 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   HIP_CHECK(hipMemset(flag_.as(), 0, sizeof(int)));
   int passes = 1;
   while ((1 << passes) < max_runs) ++passes;
+  ++passes;  // groups that are not a power of two may need one extra copy-through level
   slot_bytes_ = (size_t)max_runs * (sizeof(RunDesc) + 2 * sizeof(int64_t) + sizeof(uint8_t*)) +
-                (size_t)(passes + 1) * (2 * (max_runs + 2)) * sizeof(int64_t) + 256;
+                (size_t)passes * (4 * (size_t)max_runs + 4) * sizeof(int64_t) + 64 * (size_t)(passes + 4);
   slots_.resize(4);
   for (auto& s : slots_) {
     s.host.alloc(slot_bytes_);
@@ -198,10 +201,13 @@ bool DeviceMerger::bad_layout() {
   return v != 0;
 }
 
-int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, uint8_t* out, hipStream_t s) {
+int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::vector<int>& group_first,
+                                  uint8_t* out, hipStream_t s) {
   const int K = (int)runs.size();
   if (K > max_runs_) throw std::runtime_error("DeviceMerger: too many runs");
   if (K > 65536) throw std::runtime_error("DeviceMerger: FIXED10 mode supports <= 65536 runs");
+  if (group_first.empty() || group_first.front() != 0 || group_first.back() != K)
+    throw std::runtime_error("DeviceMerger: bad run groups");
   int64_t total = 0;
   for (const auto& r : runs) total += r.nrec;
   if (total > max_records_) throw std::runtime_error("DeviceMerger: round exceeds capacity");
@@ -234,35 +240,19 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, uint8_t* out
     eoff[k + 1] = eoff[k] + runs[k].nrec;
     bases[k] = const_cast<uint8_t*>(runs[k].base);
   }
-  // merge-tree passes over segment boundaries
-  struct PassHost {
-    size_t o_seg, o_tp;
-    int nseg, npairs, ntiles;
-  };
-  std::vector<PassHost> passes;
-  std::vector<int64_t> seg(eoff, eoff + K + 1);
-  while ((int)seg.size() - 1 > 1) {
-    const int S = (int)seg.size() - 1;
-    const int P = (S + 1) / 2;
-    PassHost ph;
-    ph.nseg = S;
-    ph.npairs = P;
-    ph.o_seg = carve(sizeof(int64_t) * (S + 1));
-    ph.o_tp = carve(sizeof(int64_t) * (P + 1));
-    std::memcpy(h + ph.o_seg, seg.data(), sizeof(int64_t) * (S + 1));
-    int64_t* tp = reinterpret_cast<int64_t*>(h + ph.o_tp);
-    tp[0] = 0;
-    std::vector<int64_t> next;
-    next.push_back(0);
-    for (int p = 0; p < P; ++p) {
-      const int64_t beg = seg[2 * p];
-      const int64_t end = seg[std::min(2 * p + 2, S)];
-      tp[p + 1] = tp[p] + (end - beg + kMergeTile - 1) / kMergeTile;
-      next.push_back(end);
-    }
-    ph.ntiles = (int)tp[P];
-    passes.push_back(ph);
-    seg.swap(next);
+  const std::vector<MergePassPlan> plan = plan_merge_passes(std::vector<int64_t>(eoff, eoff + K + 1), group_first);
+  std::vector<PassDesc> pds;
+  for (const auto& mp : plan) {
+    const size_t o_pairs = carve(sizeof(int64_t) * mp.pairs.size());
+    const size_t o_tp = carve(sizeof(int64_t) * mp.tile_prefix.size());
+    std::memcpy(h + o_pairs, mp.pairs.data(), sizeof(int64_t) * mp.pairs.size());
+    std::memcpy(h + o_tp, mp.tile_prefix.data(), sizeof(int64_t) * mp.tile_prefix.size());
+    PassDesc pd;
+    pd.pairs = reinterpret_cast<const int64_t*>(d + o_pairs);
+    pd.tile_prefix = reinterpret_cast<const int64_t*>(d + o_tp);
+    pd.npairs = mp.npairs;
+    pd.ntiles = mp.ntiles;
+    pds.push_back(pd);
   }
   HIP_CHECK(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipEventRecord(slot.uploaded, s));
@@ -270,22 +260,15 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, uint8_t* out
   // ---- F2: keys
   Elem* cur = elems_a_.as<Elem>();
   Elem* nxt = elems_b_.as<Elem>();
-  launch_extract_fixed(reinterpret_cast<const RunDesc*>(d + o_runs),
-                       reinterpret_cast<const int64_t*>(d + o_eoff), K, total, cur,
-                       flag_.as<int>(), s);
-  // ---- F3: merge tree
-  for (const auto& ph : passes) {
-    PassDesc pd;
-    pd.seg_off = reinterpret_cast<const int64_t*>(d + ph.o_seg);
-    pd.tile_prefix = reinterpret_cast<const int64_t*>(d + ph.o_tp);
-    pd.nseg = ph.nseg;
-    pd.npairs = ph.npairs;
-    pd.ntiles = ph.ntiles;
+  launch_extract_fixed(reinterpret_cast<const RunDesc*>(d + o_runs), reinterpret_cast<const int64_t*>(d + o_eoff), K,
+                       total, cur, flag_.as<int>(), s);
+  // ---- F3: merge tree (pairs never cross groups)
+  for (const auto& pd : pds) {
     launch_merge_partition(cur, pd, splits_.as<int64_t>(), s);
     launch_merge_pass(cur, nxt, pd, splits_.as<int64_t>(), s);
     std::swap(cur, nxt);
   }
-  last_passes_ = (int)passes.size();
+  last_passes_ = (int)pds.size();
   // ---- F4: gather records into merged order
   launch_gather_fixed(cur, total, reinterpret_cast<uint8_t* const*>(d + o_bases), out, s);
   return total;
@@ -297,18 +280,28 @@ ShuffleJob::ShuffleJob(const ShuffleConfig& cfg) : cfg_(cfg) {
     throw std::runtime_error("ShuffleJob: bad rank/world");
   if (cfg_.maps_per_rank < 1) throw std::runtime_error("ShuffleJob: maps_per_rank < 1");
   if (cfg_.rounds < 1) cfg_.rounds = 1;
-  if (cfg_.d2h_streams < 1) cfg_.d2h_streams = 1;
+  if (cfg_.reducers < 1) cfg_.reducers = 1;
+  if (cfg_.pinned_slots < 2) cfg_.pinned_slots = 2;
+  if (cfg_.d2h != "sdma" && cfg_.d2h != "hip") throw std::runtime_error("ShuffleJob: d2h must be sdma or hip");
+  if (cfg_.store != "hbm" && cfg_.store != "host") throw std::runtime_error("unknown store tier " + cfg_.store);
+  R_ = cfg_.reducers;
+  Q_ = cfg_.rounds;
+  C_ = R_ * Q_;
+  if ((int64_t)R_ * cfg_.world * cfg_.maps_per_rank > 65536)
+    throw std::runtime_error("ShuffleJob: reducers * world * maps_per_rank must be <= 65536 (merge run index)");
   HIP_CHECK(hipSetDevice(cfg_.device));
   int lo_prio = 0, hi_prio = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
   HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, hi_prio));
   HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
-  s_copy_.resize(cfg_.d2h_streams);
-  for (auto& s : s_copy_) HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   buf_records_ = std::max<int64_t>(1, cfg_.kv_buf_bytes / kTeraRecordBytes);
   const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
   piece_bytes_ = std::max<int64_t>(1, cfg_.d2h_piece_bytes / buf_bytes) * buf_bytes;
-  eof_buf_.alloc((size_t)buf_bytes + 16);
+  merged_ev_.resize(kSlots);
+  comm_ev_.resize(kSlots);
+  for (auto& e : merged_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : comm_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
 ShuffleJob::~ShuffleJob() {
@@ -318,16 +311,20 @@ ShuffleJob::~ShuffleJob() {
   }
   cv_.notify_all();
   if (copy_thr_.joinable()) copy_thr_.join();
-  if (deliver_thr_.joinable()) deliver_thr_.join();
+  for (auto& t : consumers_)
+    if (t.joinable()) t.join();
   (void)hipDeviceSynchronize();
-  for (auto e : piece_events_) (void)hipEventDestroy(e);
-  for (auto e : piece_start_ev_) (void)hipEventDestroy(e);
-  for (auto e : out_free_ev_) (void)hipEventDestroy(e);
-  for (auto e : join_ev_) (void)hipEventDestroy(e);
-  for (auto& d : desc_slots_)
-    if (d.uploaded) (void)hipEventDestroy(d.uploaded);
+  for (auto e : merged_ev_) (void)hipEventDestroy(e);
+  for (auto e : comm_ev_) (void)hipEventDestroy(e);
+  for (auto e : piece_ev_) (void)hipEventDestroy(e);
+  if (sdma_) {
+    for (auto sg : piece_sig_) sdma_->destroy_signal(sg);
+    sdma_->free_host(ring_);
+    ring_ = nullptr;
+    sdma_.reset();
+  }
   exchange_.reset();
-  for (auto s : s_copy_) (void)hipStreamDestroy(s);
+  if (s_copy_) (void)hipStreamDestroy(s_copy_);
   if (s_comm_) (void)hipStreamDestroy(s_comm_);
   if (s_compute_) (void)hipStreamDestroy(s_compute_);
 }
@@ -343,6 +340,12 @@ void ShuffleJob::init_local() {
   if (cfg_.local_group.empty()) throw std::runtime_error("init_local: config.local_group is empty");
   HIP_CHECK(hipSetDevice(cfg_.device));
   exchange_ = make_local_exchange(cfg_.local_group, cfg_.rank, cfg_.world);
+}
+
+std::string ShuffleJob::delivery_name() const {
+  if (!cfg_.deliver_host) return "none";
+  if (sdma_) return sdma_->describe();
+  return cfg_.d2h;
 }
 
 void ShuffleJob::generate() {
@@ -371,11 +374,9 @@ void ShuffleJob::generate() {
     void* dp = nullptr;
     HIP_CHECK(hipHostGetDevicePointer(&dp, store_base_, 0));
     store_dev_base_ = reinterpret_cast<uint8_t*>(dp);
-  } else if (cfg_.store == "hbm") {
+  } else {
     store_.alloc((size_t)store_bytes_);
     store_base_ = store_dev_base_ = store_.as<uint8_t>();
-  } else {
-    throw std::runtime_error("unknown store tier " + cfg_.store);
   }
 
   std::vector<uint8_t*> bases(nruns), gen_bases(nruns);
@@ -398,8 +399,8 @@ void ShuffleJob::generate() {
       seeds[r] = cfg_.seed ^ (0x9E3779B97F4A7C15ull * (gmap + 1)) ^ (0xC2B2AE3D27D4EB4Full * (d + 1));
       max_n = std::max(max_n, run_nrec_[r]);
     }
-  DeviceBuffer d_b(nruns * sizeof(uint8_t*)), d_n(nruns * 8), d_lo(nruns * 8), d_sp(nruns * 8),
-      d_sd(nruns * 8), d_ck(nruns * 8);
+  DeviceBuffer d_b(nruns * sizeof(uint8_t*)), d_n(nruns * 8), d_lo(nruns * 8), d_sp(nruns * 8), d_sd(nruns * 8),
+      d_ck(nruns * 8);
   HIP_CHECK(hipMemcpy(d_b.as(), gen_bases.data(), nruns * sizeof(uint8_t*), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_n.as(), run_nrec_.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_lo.as(), key_lo.data(), nruns * 8, hipMemcpyHostToDevice));
@@ -475,8 +476,8 @@ std::vector<std::vector<uint64_t>> ShuffleJob::sample_keys(int64_t every) {
   if (total == 0) return out;
   DeviceBuffer d_off((nruns + 1) * 8), d_out(total * sizeof(Elem));
   HIP_CHECK(hipMemcpy(d_off.as(), soff.data(), (nruns + 1) * 8, hipMemcpyHostToDevice));
-  launch_sample_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), nruns, every,
-                      d_off.as<int64_t>(), total, d_out.as<Elem>(), s_compute_);
+  launch_sample_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), nruns, every, d_off.as<int64_t>(), total,
+                      d_out.as<Elem>(), s_compute_);
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   std::vector<Elem> h(total);
   HIP_CHECK(hipMemcpy(h.data(), d_out.as(), total * sizeof(Elem), hipMemcpyDeviceToHost));
@@ -491,431 +492,542 @@ std::vector<std::vector<uint64_t>> ShuffleJob::sample_keys(int64_t every) {
 }
 
 void ShuffleJob::set_bounds(const std::vector<uint64_t>& bounds) {
-  const int W = cfg_.world, Q = cfg_.rounds;
-  if ((int64_t)bounds.size() != (int64_t)W * (Q - 1) * 2)
-    throw std::runtime_error("set_bounds: expected world*(rounds-1)*2 values");
+  const int W = cfg_.world;
+  if ((int64_t)bounds.size() != (int64_t)W * (C_ - 1) * 2)
+    throw std::runtime_error("set_bounds: expected world*(reducers*rounds-1)*2 values");
   bounds_ = bounds;
-  if (Q > 1) {
+  if (C_ > 1) {
     d_bounds_.alloc(bounds.size() * 8);
     HIP_CHECK(hipMemcpy(d_bounds_.as(), bounds.data(), bounds.size() * 8, hipMemcpyHostToDevice));
   }
 }
 
-void ShuffleJob::compute_round_plans(std::vector<RoundPlan>* plans, double* ms) {
-  const double t0 = now_ms();
-  const int M = cfg_.maps_per_rank, W = cfg_.world, Q = cfg_.rounds;
+// Round volumes, once per job: the cell split of every local run, the counts exchange (every
+// reducer learns what each peer will send it in each round) and, for world > 1, the checksum of
+// every slice a peer will send (exchange verification in validated steps).
+void ShuffleJob::compute_plans() {
+  const int M = cfg_.maps_per_rank, W = cfg_.world, me = cfg_.rank;
   const int nruns = M * W;
-  if (Q > 1 && bounds_.empty()) throw std::runtime_error("rounds > 1 requires set_bounds()");
-  const int64_t per = Q + 1;
-  if (d_split_out_.size() < (size_t)nruns * per * 8) d_split_out_.alloc((size_t)nruns * per * 8);
-  launch_split_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(),
-                     Q > 1 ? d_bounds_.as<Elem>() : nullptr, d_bound_set_.as<int>(), nruns, Q - 1,
-                     d_split_out_.as<int64_t>(), s_compute_);
-  std::vector<int64_t> pos((size_t)nruns * per);
-  HIP_CHECK(hipMemcpyAsync(pos.data(), d_split_out_.as(), pos.size() * 8, hipMemcpyDeviceToHost,
+  if (C_ > 1 && bounds_.empty()) throw std::runtime_error("reducers*rounds > 1 requires set_bounds()");
+  const int64_t per = C_ + 1;
+  d_split_out_.alloc((size_t)nruns * per * 8);
+  launch_split_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), C_ > 1 ? d_bounds_.as<Elem>() : nullptr,
+                     d_bound_set_.as<int>(), nruns, C_ - 1, d_split_out_.as<int64_t>(), s_compute_);
+  split_pos_.assign((size_t)nruns * per, 0);
+  HIP_CHECK(hipMemcpyAsync(split_pos_.data(), d_split_out_.as(), split_pos_.size() * 8, hipMemcpyDeviceToHost,
                            s_compute_));
   HIP_CHECK(hipStreamSynchronize(s_compute_));
-  plans->assign(Q, RoundPlan());
-  // send side and my-own counts; counts to exchange: [peer p][q][m]
-  std::vector<int64_t> send_counts((size_t)W * Q * M), recv_counts((size_t)W * Q * M);
-  for (int q = 0; q < Q; ++q) {
-    auto& rp = (*plans)[q];
-    rp.send_beg.assign((size_t)W * M, 0);
-    rp.send_end.assign((size_t)W * M, 0);
-    for (int p = 0; p < W; ++p)
-      for (int m = 0; m < M; ++m) {
-        const int r = m * W + p;
-        rp.send_beg[p * M + m] = pos[(size_t)r * per + q];
-        rp.send_end[p * M + m] = pos[(size_t)r * per + q + 1];
-        send_counts[((size_t)p * Q + q) * M + m] = rp.send_end[p * M + m] - rp.send_beg[p * M + m];
-      }
-  }
+  auto pos = [&](int r, int c) { return split_pos_[(size_t)r * per + c]; };
+  const size_t n_per_peer = (size_t)Q_ * R_ * M;  // counts per (peer): [q][i][m]
+  std::vector<int64_t> send_counts((size_t)W * n_per_peer), recv_counts((size_t)W * n_per_peer);
+  for (int p = 0; p < W; ++p)
+    for (int q = 0; q < Q_; ++q)
+      for (int i = 0; i < R_; ++i)
+        for (int m = 0; m < M; ++m) {
+          const int r = m * W + p, c = i * Q_ + q;
+          send_counts[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = pos(r, c + 1) - pos(r, c);
+        }
+  std::vector<int64_t> recv_ck;
   if (W == 1) {
     recv_counts = send_counts;
   } else {
     if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
-    exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), (size_t)Q * M, s_comm_);
+    exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), n_per_peer, s_comm_);
+    // checksums of every slice this rank sends, in the same [p][q][i][m] layout
+    std::vector<RunDesc> sl((size_t)W * n_per_peer);
+    int64_t max_n = 0;
+    for (int p = 0; p < W; ++p)
+      for (int q = 0; q < Q_; ++q)
+        for (int i = 0; i < R_; ++i)
+          for (int m = 0; m < M; ++m) {
+            const int r = m * W + p, c = i * Q_ + q;
+            RunDesc d;
+            d.base = store_dev_base_ + run_off_[r] + pos(r, c) * kTeraRecordBytes;
+            d.nrec = pos(r, c + 1) - pos(r, c);
+            d.nbytes = d.nrec * kTeraRecordBytes;
+            d.offsets = nullptr;
+            max_n = std::max(max_n, d.nrec);
+            sl[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = d;
+          }
+    DeviceBuffer d_sl(sl.size() * sizeof(RunDesc)), d_ck(sl.size() * 8);
+    HIP_CHECK(hipMemcpy(d_sl.as(), sl.data(), sl.size() * sizeof(RunDesc), hipMemcpyHostToDevice));
+    for (size_t b = 0; b < sl.size(); b += 65535) {
+      const int n = (int)std::min<size_t>(65535, sl.size() - b);
+      launch_slice_checksums(d_sl.as<RunDesc>() + b, n, max_n, d_ck.as<unsigned long long>() + b, s_compute_);
+    }
+    HIP_CHECK(hipGetLastError());
+    std::vector<int64_t> send_ck(sl.size());
+    HIP_CHECK(hipStreamSynchronize(s_compute_));
+    HIP_CHECK(hipMemcpy(send_ck.data(), d_ck.as(), send_ck.size() * 8, hipMemcpyDeviceToHost));
+    recv_ck.assign(send_ck.size(), 0);
+    exchange_->alltoall_i64(send_ck.data(), recv_ck.data(), n_per_peer, s_comm_);
   }
-  for (int q = 0; q < Q; ++q) {
-    auto& rp = (*plans)[q];
-    rp.recv_cnt.assign((size_t)W * M, 0);
-    rp.recv_records = 0;
+
+  plans_.assign(Q_, RoundPlan());
+  reducer_records_.assign(R_, 0);
+  max_round_records_ = 0;
+  int64_t max_slot_bytes = 0, max_send = 0;
+  verify_n_.assign(Q_, 0);
+  verify_max_nrec_.assign(Q_, 0);
+  std::vector<std::vector<RunDesc>> vruns(Q_);
+  std::vector<std::vector<int64_t>> vexp(Q_);
+  for (int q = 0; q < Q_; ++q) {
+    RoundPlan& rp = plans_[q];
+    rp.send.assign(W, {});
+    rp.self_beg.assign((size_t)R_ * M, 0);
+    for (int i = 0; i < R_; ++i)
+      for (int m = 0; m < M; ++m) rp.self_beg[(size_t)i * M + m] = pos(m * W + me, i * Q_ + q);
+    for (int k = 1; k < W; ++k) {
+      const int p = (me + k) % W;
+      for (int i = 0; i < R_; ++i)
+        for (int m = 0; m < M; ++m) {
+          const int r = m * W + p, c = i * Q_ + q;
+          const int64_t cnt = pos(r, c + 1) - pos(r, c);
+          if (cnt <= 0) continue;
+          rp.send[p].push_back(Span{store_base_ + run_off_[r] + pos(r, c) * kTeraRecordBytes, cnt * kTeraRecordBytes});
+          rp.send_bytes += cnt * kTeraRecordBytes;
+        }
+    }
+    max_send = std::max(max_send, rp.send_bytes);
+    rp.recv_cnt.assign((size_t)W * R_ * M, 0);
+    rp.recv_off.assign((size_t)W * R_ * M, -1);
+    rp.group_recs.assign(R_, 0);
+    int64_t off = 0;
     for (int s = 0; s < W; ++s)
-      for (int j = 0; j < M; ++j) {
-        const int64_t c = recv_counts[((size_t)s * Q + q) * M + j];
-        rp.recv_cnt[s * M + j] = c;
-        rp.recv_records += c;
+      for (int i = 0; i < R_; ++i)
+        for (int j = 0; j < M; ++j) {
+          const size_t x = ((size_t)s * R_ + i) * M + j;
+          const int64_t cnt = recv_counts[(size_t)s * n_per_peer + ((size_t)q * R_ + i) * M + j];
+          rp.recv_cnt[x] = cnt;
+          rp.group_recs[i] += cnt;
+          if (s == me && !host_store()) continue;  // read in place from the HBM store
+          rp.recv_off[x] = off;
+          off += cnt * kTeraRecordBytes;
+        }
+    max_slot_bytes = std::max(max_slot_bytes, off);
+    for (int i = 0; i < R_; ++i) {
+      rp.recv_records += rp.group_recs[i];
+      reducer_records_[i] += rp.group_recs[i];
+    }
+    max_round_records_ = std::max(max_round_records_, rp.recv_records);
+    if (W > 1) {
+      for (int s = 0; s < W; ++s) {
+        if (s == me) continue;
+        for (int i = 0; i < R_; ++i)
+          for (int j = 0; j < M; ++j) {
+            const size_t x = ((size_t)s * R_ + i) * M + j;
+            if (rp.recv_cnt[x] <= 0) continue;
+            RunDesc d;
+            d.base = nullptr;  // filled in once the receive slots exist
+            d.nrec = rp.recv_cnt[x];
+            d.nbytes = rp.recv_off[x];  // temporarily: offset in the slot
+            d.offsets = nullptr;
+            vruns[q].push_back(d);
+            vexp[q].push_back(recv_ck[(size_t)s * n_per_peer + ((size_t)q * R_ + i) * M + j]);
+            verify_max_nrec_[q] = std::max(verify_max_nrec_[q], d.nrec);
+          }
       }
+      verify_n_[q] = (int)vruns[q].size();
+    }
   }
-  if (ms) *ms = now_ms() - t0;
+
+  // ---- buffers
+  merger_.reset(new DeviceMerger(max_round_records_, R_ * W * M));
+  const size_t out_bytes = (size_t)std::max<int64_t>(1, max_round_records_) * kTeraRecordBytes;
+  out_slots_.clear();
+  out_slots_.resize(kSlots);
+  for (auto& b : out_slots_) b.alloc(out_bytes);
+  recv_slots_.clear();
+  if (staged()) {
+    recv_slots_.resize(kSlots);
+    for (auto& b : recv_slots_) b.alloc((size_t)std::max<int64_t>(max_slot_bytes, 16));
+  }
+  if (W > 1 && host_store() && std::string(exchange_->name()).rfind("rccl", 0) == 0)
+    send_staging_.alloc((size_t)std::max<int64_t>(max_send, 16));
+  if (W > 1) exchange_->reserve(max_send);
+  d_validate_.alloc(64 + (size_t)2 * R_ * sizeof(Elem));
+  // exchange verification tables
+  d_verify_runs_.clear();
+  d_verify_expect_.clear();
+  d_verify_runs_.resize(Q_);
+  d_verify_expect_.resize(Q_);
+  int max_v = 0;
+  for (int q = 0; q < Q_; ++q) {
+    if (verify_n_[q] == 0) continue;
+    for (auto& d : vruns[q]) {
+      d.base = recv_slots_[q % kSlots].as<uint8_t>() + d.nbytes;
+      d.nbytes = d.nrec * kTeraRecordBytes;
+    }
+    d_verify_runs_[q].alloc(vruns[q].size() * sizeof(RunDesc));
+    d_verify_expect_[q].alloc(vexp[q].size() * 8);
+    HIP_CHECK(hipMemcpy(d_verify_runs_[q].as(), vruns[q].data(), vruns[q].size() * sizeof(RunDesc),
+                        hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_verify_expect_[q].as(), vexp[q].data(), vexp[q].size() * 8, hipMemcpyHostToDevice));
+    max_v = std::max(max_v, verify_n_[q]);
+  }
+  if (max_v > 65535) throw std::runtime_error("exchange verification: too many slices per round");
+  if (max_v > 0) d_verify_got_.alloc((size_t)max_v * 8);
 }
 
 void ShuffleJob::plan() {
   HIP_CHECK(hipSetDevice(cfg_.device));
-  compute_round_plans(&plans_, nullptr);
-  max_round_records_ = 0;
-  for (const auto& rp : plans_) max_round_records_ = std::max(max_round_records_, rp.recv_records);
-  const int M = cfg_.maps_per_rank, W = cfg_.world;
-  merger_.reset(new DeviceMerger(max_round_records_, M * W));
-  const size_t slot_bytes = (size_t)std::max<int64_t>(1, max_round_records_) * kTeraRecordBytes;
-  out_slots_.clear();
-  recv_slots_.clear();
-  out_slots_.resize(kSlots);
-  for (auto& b : out_slots_) b.alloc(slot_bytes);
-  if (W > 1 || host_store()) {
-    recv_slots_.resize(kSlots);
-    for (auto& b : recv_slots_) b.alloc(slot_bytes);
-    desc_slots_.resize(4);
-    for (auto& d : desc_slots_) {
-      d.host.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
-      d.dev.alloc(sizeof(CopyDesc) * (size_t)M * W + 64);
-      HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
+  compute_plans();
+  if (cfg_.deliver_host && !copy_thr_.joinable()) {
+    const size_t ring_bytes = (size_t)piece_bytes_ * cfg_.pinned_slots;
+    if (cfg_.d2h == "sdma") {
+      sdma_.reset(new SdmaEngine(cfg_.device));
+      ring_ = static_cast<uint8_t*>(sdma_->alloc_host(ring_bytes));
+      piece_sig_.resize(cfg_.pinned_slots);
+      for (auto& sg : piece_sig_) sg = sdma_->make_signal();
+    } else {
+      ring_hip_.alloc(ring_bytes);
+      ring_ = ring_hip_.as<uint8_t>();
+      piece_ev_.resize(cfg_.pinned_slots);
+      for (auto& e : piece_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-  }
-  if (W > 1) {
-    max_send_bytes_ = 0;
-    for (const auto& rp : plans_) {
-      int64_t sb = 0;
-      for (int p = 0; p < W; ++p)
-        if (p != cfg_.rank)
-          for (int m = 0; m < M; ++m) sb += (rp.send_end[p * M + m] - rp.send_beg[p * M + m]) * kTeraRecordBytes;
-      max_send_bytes_ = std::max(max_send_bytes_, sb);
-    }
-    pack_slots_.clear();
-    pack_slots_.resize(kSlots);
-    for (auto& b : pack_slots_) b.alloc((size_t)std::max<int64_t>(max_send_bytes_, 16));
-  }
-  d_validate_.alloc(256);
-  if (cfg_.deliver_host && pinned_.size() == 0) {
-    pinned_.alloc((size_t)piece_bytes_ * cfg_.pinned_slots);
     pinned_free_.assign(cfg_.pinned_slots, true);
-    piece_events_.resize((size_t)cfg_.pinned_slots * cfg_.d2h_streams);
-    piece_start_ev_.resize(cfg_.pinned_slots);
-    for (auto& e : piece_events_) HIP_CHECK(hipEventCreate(&e));
-    for (auto& e : piece_start_ev_) HIP_CHECK(hipEventCreate(&e));
-    join_ev_.resize(cfg_.d2h_streams);
-    for (auto& e : join_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    out_free_ev_.resize(kSlots);
-    for (auto& e : out_free_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    items_.assign(R_, {});
+    eof_bufs_.clear();
+    for (int i = 0; i < R_; ++i) eof_bufs_.emplace_back(new uint8_t[(size_t)cfg_.kv_buf_bytes + 16]);
     copy_thr_ = std::thread([this] { copy_loop(); });
-    deliver_thr_ = std::thread([this] { deliver_loop(); });
+    for (int i = 0; i < R_; ++i) consumers_.emplace_back([this, i] { consume_loop(i); });
   }
-  UDA_LOG(kInfo, "rank %d planned %d rounds, max round %ld records", cfg_.rank, cfg_.rounds,
-          (long)max_round_records_);
+  UDA_LOG(kInfo, "rank %d planned %d reducers x %d rounds, max round %ld records, delivery %s", cfg_.rank, R_, Q_,
+          (long)max_round_records_, delivery_name().c_str());
 }
 
-// Copy thread: turns merged rounds into D2H pieces in the pinned ring (FIFO order).
+void ShuffleJob::wait_exchange_ok() {
+  if (exchange_) exchange_->check();
+}
+
+// Copy thread: merged rounds -> D2H pieces in the pinned ring, per reducer, in round order.
 void ShuffleJob::copy_loop() {
-  HIP_CHECK(hipSetDevice(cfg_.device));
-  const int NS = (int)s_copy_.size();
-  for (;;) {
-    RoundOut r;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !round_q_.empty(); });
-      if (stop_) return;
-      r = round_q_.front();
-      round_q_.pop_front();
-    }
-    for (auto s : s_copy_) HIP_CHECK(hipStreamWaitEvent(s, r.merged, 0));
-    const int64_t total = r.records * kTeraRecordBytes;
-    const bool last_round = (r.q == cfg_.rounds - 1);
-    const uint8_t* src = out_slots_[r.out_slot].as<uint8_t>();
-    int64_t off = 0;
-    do {
-      const int64_t len = std::min(piece_bytes_, total - off);
-      int k = -1;
+  try {
+    bind_thread_to_numa(sdma_ ? sdma_->numa_node() : device_numa_node(cfg_.device));
+    HIP_CHECK(hipSetDevice(cfg_.device));
+    for (;;) {
+      RoundOut r;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] {
-          if (stop_) return true;
-          for (int i = 0; i < (int)pinned_free_.size(); ++i)
-            if (pinned_free_[i]) return true;
-          return false;
-        });
+        cv_.wait(lk, [&] { return stop_ || !round_q_.empty(); });
         if (stop_) return;
-        for (int i = 0; i < (int)pinned_free_.size(); ++i)
-          if (pinned_free_[i]) {
-            k = i;
-            break;
+        r = std::move(round_q_.front());
+        round_q_.pop_front();
+      }
+      HIP_CHECK(hipEventSynchronize(merged_ev_[r.slot]));
+      const uint8_t* src = out_slots_[r.slot].as<uint8_t>();
+      const bool last_round = (r.q == Q_ - 1);
+      std::vector<int> used;
+      int64_t goff = 0;
+      for (int i = 0; i < R_; ++i) {
+        const int64_t bytes = r.group_recs[i] * kTeraRecordBytes;
+        if (bytes == 0 && last_round) {
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            items_[i].push_back(Item{-1, 0, true, now_ms()});
           }
-        pinned_free_[k] = false;
+          cv_.notify_all();
+        }
+        for (int64_t off = 0; off < bytes;) {
+          const int64_t len = std::min(piece_bytes_, bytes - off);
+          int k = -1;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] {
+              if (stop_) return true;
+              for (bool f : pinned_free_)
+                if (f) return true;
+              return false;
+            });
+            if (stop_) return;
+            for (int x = 0; x < (int)pinned_free_.size(); ++x)
+              if (pinned_free_[x]) {
+                k = x;
+                break;
+              }
+            pinned_free_[k] = false;
+          }
+          uint8_t* dst = ring_ + (int64_t)k * piece_bytes_;
+          const uint8_t* from = src + goff + off;
+          if (sdma_) {
+            SdmaEngine::arm(piece_sig_[k], sdma_->parts((size_t)len, cfg_.d2h_engines));
+            sdma_->copy_d2h(dst, from, (size_t)len, piece_sig_[k], cfg_.d2h_engines);
+          } else {
+            HIP_CHECK(hipMemcpyAsync(dst, from, (size_t)len, hipMemcpyDeviceToHost, s_copy_));
+            HIP_CHECK(hipEventRecord(piece_ev_[k], s_copy_));
+          }
+          off += len;
+          used.push_back(k);
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            items_[i].push_back(Item{k, len, last_round && off >= bytes, now_ms()});
+          }
+          cv_.notify_all();
+        }
+        goff += bytes;
       }
-      uint8_t* dst = pinned_.as<uint8_t>() + (int64_t)k * piece_bytes_;
-      HIP_CHECK(hipEventRecord(piece_start_ev_[k], s_copy_[0]));
-      // split the piece over the copy streams on whole-record boundaries
-      const int64_t recs = len / kTeraRecordBytes;
-      int64_t done = 0;
-      // every copy stream starts the piece after the start event (stream 0); stream 0 then joins the
-      // others, so piece_events_[k*NS] marks the whole piece and start->end is a same-stream interval
-      for (int i = 0; i < NS; ++i) {
-        const int64_t part = (i == NS - 1) ? (recs - done) : recs / NS;
-        if (i > 0) HIP_CHECK(hipStreamWaitEvent(s_copy_[i], piece_start_ev_[k], 0));
-        if (part > 0)
-          HIP_CHECK(hipMemcpyAsync(dst + done * kTeraRecordBytes, src + off + done * kTeraRecordBytes,
-                                   part * kTeraRecordBytes, hipMemcpyDeviceToHost, s_copy_[i]));
-        if (i > 0) HIP_CHECK(hipEventRecord(piece_events_[(size_t)k * NS + i], s_copy_[i]));
-        done += part;
+      // the output slot is free once every piece of this round has landed in the ring
+      for (int k : used) {
+        if (sdma_)
+          SdmaEngine::wait(piece_sig_[k]);
+        else
+          HIP_CHECK(hipEventSynchronize(piece_ev_[k]));
       }
-      for (int i = 1; i < NS; ++i) HIP_CHECK(hipStreamWaitEvent(s_copy_[0], piece_events_[(size_t)k * NS + i], 0));
-      HIP_CHECK(hipEventRecord(piece_events_[(size_t)k * NS], s_copy_[0]));
-      off += len;
       {
         std::lock_guard<std::mutex> g(mu_);
-        piece_q_.push_back(Piece{k, len, last_round && off >= total, nullptr});
+        out_free_[r.q] = 1;
       }
       cv_.notify_all();
-    } while (off < total);
-    for (int i = 1; i < NS; ++i) {  // join the other copy streams before freeing the out slot
-      HIP_CHECK(hipEventRecord(join_ev_[i], s_copy_[i]));
-      HIP_CHECK(hipStreamWaitEvent(s_copy_[0], join_ev_[i], 0));
     }
-    HIP_CHECK(hipEventRecord(out_free_ev_[r.out_slot], s_copy_[0]));
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      d2h_enqueued_[r.q] = 1;
-    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (step_error_msg_.empty()) step_error_msg_ = std::string("delivery copy thread: ") + e.what();
+    stop_ = true;
     cv_.notify_all();
   }
 }
 
-// Deliver thread: the "Java side" hand-off. Buffers hold whole records and are at most
-// kv_buf_bytes; the final buffer carries the IFile EOF marker (-1,-1).
-void ShuffleJob::deliver_loop() {
-  HIP_CHECK(hipSetDevice(cfg_.device));
-  const int NS = (int)s_copy_.size();
-  const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
-  for (;;) {
-    Piece p;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !piece_q_.empty(); });
-      if (stop_) return;
-      p = piece_q_.front();
-      piece_q_.pop_front();
-    }
-    trace::Range tr_piece("uda.deliver_piece");
-    HIP_CHECK(hipEventSynchronize(piece_events_[(size_t)p.slot * NS]));  // joins every copy stream
-    float ms = 0;
-    if (p.bytes > 0 && hipEventElapsedTime(&ms, piece_start_ev_[p.slot], piece_events_[(size_t)p.slot * NS]) == hipSuccess)
-      step_d2h_ms_ += ms;
-    const uint8_t* base = pinned_.as<uint8_t>() + (int64_t)p.slot * piece_bytes_;
-    int err = 0;
-    int64_t nb = 0;
-    for (int64_t off = 0; off < p.bytes; off += buf_bytes) {
-      const int64_t len = std::min(buf_bytes, p.bytes - off);
-      const bool final_chunk = p.last && off + len >= p.bytes;
-      if (final_chunk && len + kEofBytes <= cfg_.kv_buf_bytes) {
-        uint8_t* e = eof_buf_.as<uint8_t>();
-        std::memcpy(e, base + off, (size_t)len);
-        e[len] = 0xFF;
-        e[len + 1] = 0xFF;
-        if (sink_ && !err) err = sink_(e, len + kEofBytes);
-        ++nb;
-        p.bytes = -1;  // EOF already delivered
-        break;
+// Consumer thread of reducer i: the "Java side" hand-off. Buffers hold whole records and are at
+// most kv_buf_bytes; the reducer's final buffer carries the IFile EOF marker (-1, -1).
+void ShuffleJob::consume_loop(int i) {
+  try {
+    bind_thread_to_numa(sdma_ ? sdma_->numa_node() : device_numa_node(cfg_.device));
+    HIP_CHECK(hipSetDevice(cfg_.device));
+    const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
+    uint8_t* eb = eof_bufs_[i].get();
+    for (;;) {
+      Item it;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !items_[i].empty(); });
+        if (stop_) return;
+        it = items_[i].front();
+        items_[i].pop_front();
       }
-      if (sink_ && !err) err = sink_(base + off, len);
-      ++nb;
+      int err = 0;
+      int64_t nb = 0;
+      double waited = 0;
+      bool eof_sent = false;
+      if (it.pslot >= 0) {
+        if (sdma_)
+          SdmaEngine::wait(piece_sig_[it.pslot]);
+        else
+          HIP_CHECK(hipEventSynchronize(piece_ev_[it.pslot]));
+        waited = now_ms() - it.issued_ms;
+        const uint8_t* base = ring_ + (int64_t)it.pslot * piece_bytes_;
+        for (int64_t off = 0; off < it.bytes; off += buf_bytes) {
+          const int64_t len = std::min(buf_bytes, it.bytes - off);
+          const bool final_chunk = it.last && off + len >= it.bytes;
+          if (final_chunk && len + kEofBytes <= cfg_.kv_buf_bytes) {
+            std::memcpy(eb, base + off, (size_t)len);
+            eb[len] = 0xFF;
+            eb[len + 1] = 0xFF;
+            if (sink_ && !err) err = sink_(i, eb, len + kEofBytes);
+            eof_sent = true;
+          } else if (sink_ && !err) {
+            err = sink_(i, base + off, len);
+          }
+          ++nb;
+        }
+      }
+      if (it.last && !eof_sent) {  // EOF did not fit (or no final data): a separate buffer
+        eb[0] = 0xFF;
+        eb[1] = 0xFF;
+        if (sink_ && !err) err = sink_(i, eb, kEofBytes);
+        ++nb;
+      }
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (it.pslot >= 0) pinned_free_[it.pslot] = true;
+        step_buffers_ += nb;
+        step_d2h_ms_ += waited;
+        if (err && !step_error_) step_error_ = err;
+        if (it.last) ++eof_count_;
+      }
+      cv_.notify_all();
     }
-    if (p.last && p.bytes >= 0) {  // EOF did not fit (or empty final piece): separate buffer
-      uint8_t* e = eof_buf_.as<uint8_t>();
-      e[0] = 0xFF;
-      e[1] = 0xFF;
-      if (sink_ && !err) err = sink_(e, kEofBytes);
-      ++nb;
-    }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      pinned_free_[p.slot] = true;
-      step_buffers_ += nb;
-      if (err) step_error_ = err;
-      if (p.last) step_done_ = true;
-    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (step_error_msg_.empty()) step_error_msg_ = std::string("delivery consumer thread: ") + e.what();
+    stop_ = true;
     cv_.notify_all();
   }
 }
 
-StepStats ShuffleJob::run_step() {
+StepStats ShuffleJob::run_step(bool validate) {
   trace::Range tr_step("uda.step");
   HIP_CHECK(hipSetDevice(cfg_.device));
   if (!merger_) throw std::runtime_error("run_step before plan()");
   StepStats st;
+  st.validated = validate;
   const double t0 = now_ms();
-  const int M = cfg_.maps_per_rank, W = cfg_.world, Q = cfg_.rounds, me = cfg_.rank;
-
-  std::vector<RoundPlan> plans;
-  compute_round_plans(&plans, &st.split_ms);
-  for (int q = 0; q < Q; ++q)
-    if (plans[q].recv_records > max_round_records_)
-      throw std::runtime_error("round volume exceeds planned capacity");
-
+  const int M = cfg_.maps_per_rank, W = cfg_.world, me = cfg_.rank;
+  const bool deliver = cfg_.deliver_host;
   {
     std::lock_guard<std::mutex> g(mu_);
-    d2h_enqueued_.assign(Q, 0);
-    step_done_ = false;
+    if (stop_) throw std::runtime_error("delivery pipeline stopped: " + step_error_msg_);
+    out_free_.assign(Q_, 0);
+    eof_count_ = 0;
     step_buffers_ = 0;
     step_error_ = 0;
     step_d2h_ms_ = 0;
   }
-  std::vector<hipEvent_t> ev(4 * Q);
+  std::vector<hipEvent_t> ev(4 * (size_t)Q_);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
-  std::vector<hipEvent_t> merged(kSlots), comm_done(kSlots);
-  for (auto& e : merged) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (auto& e : comm_done) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (cfg_.validate) HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 256, s_compute_));
   unsigned long long* vstats = d_validate_.as<unsigned long long>();
   Elem* vprev = reinterpret_cast<Elem*>(d_validate_.as<uint8_t>() + 64);
-  Elem* vlast = reinterpret_cast<Elem*>(d_validate_.as<uint8_t>() + 128);
+  Elem* vlast = vprev + R_;
+  std::vector<bool> has_prev(R_, false);
+  if (validate) HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 64, s_compute_));
+  const bool rccl_staging = send_staging_.size() > 0;
 
-  int64_t bytes_sent = 0;
-  for (int q = 0; q < Q; ++q) {
-    trace::Range tr_round("uda.round");
-    const int slot = q % kSlots;
-    const RoundPlan& rp = plans[q];
-    std::vector<RunDesc> runs;
-    if (W == 1 && !host_store()) {
-      HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_compute_));
-      HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_compute_));
-      for (int m = 0; m < M; ++m) {
-        RunDesc d;
-        d.base = run_base(m, 0) + rp.send_beg[m] * kTeraRecordBytes;
-        d.nrec = rp.send_end[m] - rp.send_beg[m];
-        d.nbytes = d.nrec * kTeraRecordBytes;
-        d.offsets = nullptr;
-        runs.push_back(d);
-      }
-    } else {
-      uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
-      uint8_t* pbuf = W > 1 ? pack_slots_[slot].as<uint8_t>() : nullptr;
-      if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged[slot], 0));
-      HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
-      std::vector<int64_t> roff((size_t)W * M + 1, 0);
-      for (int i = 0; i < W * M; ++i) roff[i + 1] = roff[i] + rp.recv_cnt[i] * kTeraRecordBytes;
-      // pack: per destination, this rank's slices of the round in map order, destinations in
-      // rotating order; the self partition goes straight to its place in the receive slot
-      DescSlot& ds = desc_slots_[next_desc_];
-      next_desc_ = (next_desc_ + 1) % (int)desc_slots_.size();
-      if (ds.used) HIP_CHECK(hipEventSynchronize(ds.uploaded));
-      ds.used = true;
-      CopyDesc* descs = ds.host.as<CopyDesc>();
-      int nd = 0;
-      int64_t max_bytes = 0;
-      std::vector<int64_t> sb(W, 0), sd(W, 0), rb(W, 0), rd(W, 0);
-      int64_t packed = 0;
-      for (int k = 1; k < W; ++k) {
-        const int to = (me + k) % W;
-        sd[to] = packed;
-        for (int m = 0; m < M; ++m) {
-          const int64_t c = rp.send_end[to * M + m] - rp.send_beg[to * M + m];
-          if (c <= 0) continue;
-          descs[nd++] = CopyDesc{run_base(m, to) + rp.send_beg[to * M + m] * kTeraRecordBytes, pbuf + packed,
-                                 c * kTeraRecordBytes};
-          max_bytes = std::max(max_bytes, c * kTeraRecordBytes);
-          packed += c * kTeraRecordBytes;
-        }
-        sb[to] = packed - sd[to];
-      }
-      for (int m = 0; m < M; ++m) {
-        const int64_t c = rp.send_end[me * M + m] - rp.send_beg[me * M + m];
-        if (c <= 0) continue;
-        descs[nd++] = CopyDesc{run_base(m, me) + rp.send_beg[me * M + m] * kTeraRecordBytes, rbuf + roff[me * M + m],
-                               c * kTeraRecordBytes};
-        max_bytes = std::max(max_bytes, c * kTeraRecordBytes);
-      }
-      for (int s = 0; s < W; ++s) {
-        if (s == me) continue;
-        rd[s] = roff[s * M];
-        rb[s] = roff[(s + 1) * M] - roff[s * M];
-      }
-      bytes_sent += packed;
-      if (nd > 0 && !host_store()) {
-        HIP_CHECK(hipMemcpyAsync(ds.dev.as(), descs, sizeof(CopyDesc) * nd, hipMemcpyHostToDevice, s_comm_));
-        HIP_CHECK(hipEventRecord(ds.uploaded, s_comm_));
-        launch_batched_copy(ds.dev.as<CopyDesc>(), nd, max_bytes, s_comm_);
-      } else if (nd > 0) {
-        // spill tier: the slices stream H2D over PCIe (SDMA) straight into the pack / receive slots
-        for (int i = 0; i < nd; ++i)
-          HIP_CHECK(hipMemcpyAsync(descs[i].dst, descs[i].src, (size_t)descs[i].bytes, hipMemcpyHostToDevice, s_comm_));
-        HIP_CHECK(hipEventRecord(ds.uploaded, s_comm_));
-        st.bytes_h2d += [&] {
-          int64_t b = 0;
-          for (int i = 0; i < nd; ++i) b += descs[i].bytes;
-          return b;
-        }();
-      }
-      if (W > 1) exchange_->alltoallv(pbuf, sb.data(), sd.data(), rbuf, rb.data(), rd.data(), s_comm_);
-      HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
-      HIP_CHECK(hipEventRecord(comm_done[slot], s_comm_));
-      HIP_CHECK(hipStreamWaitEvent(s_compute_, comm_done[slot], 0));
-      for (int i = 0; i < W * M; ++i) {
-        RunDesc d;
-        d.base = rbuf + roff[i];
-        d.nrec = rp.recv_cnt[i];
-        d.nbytes = d.nrec * kTeraRecordBytes;
-        d.offsets = nullptr;
-        runs.push_back(d);
+  auto wait_until = [&](const std::function<bool()>& ready) {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!cv_.wait_for(lk, std::chrono::milliseconds(100), [&] { return ready() || stop_; })) {
+      if (exchange_) {  // a lost peer must fail the step, not hang it
+        lk.unlock();
+        wait_exchange_ok();
+        lk.lock();
       }
     }
-    // output slot reuse: the D2H of round q-kSlots must be enqueued (and is then waited on)
-    if (cfg_.deliver_host && q >= kSlots) {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return d2h_enqueued_[q - kSlots] != 0 || step_error_ != 0; });
-      lk.unlock();
-      HIP_CHECK(hipStreamWaitEvent(s_compute_, out_free_ev_[slot], 0));
+    if (stop_) throw std::runtime_error("delivery pipeline failed: " + step_error_msg_);
+  };
+
+  for (int q = 0; q < Q_; ++q) {
+    trace::Range tr_round("uda.round");
+    const int slot = q % kSlots;
+    const RoundPlan& rp = plans_[q];
+    uint8_t* rbuf = staged() ? recv_slots_[slot].as<uint8_t>() : nullptr;
+    if (staged()) {
+      if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged_ev_[slot], 0));  // slot consumed
+      HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
+      if (host_store()) {  // spill tier: this round's own cells stream H2D (SDMA) into the slot
+        for (int i = 0; i < R_; ++i)
+          for (int j = 0; j < M; ++j) {
+            const size_t x = ((size_t)me * R_ + i) * M + j;
+            const int64_t cnt = rp.recv_cnt[x];
+            if (cnt <= 0) continue;
+            HIP_CHECK(hipMemcpyAsync(rbuf + rp.recv_off[x], run_base(j, me) + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes,
+                                     (size_t)(cnt * kTeraRecordBytes), hipMemcpyHostToDevice, s_comm_));
+            st.bytes_h2d += cnt * kTeraRecordBytes;
+          }
+      }
+      if (W > 1) {
+        std::vector<std::vector<Span>> recv(W);
+        for (int s = 0; s < W; ++s) {
+          if (s == me) continue;
+          for (int i = 0; i < R_; ++i)
+            for (int j = 0; j < M; ++j) {
+              const size_t x = ((size_t)s * R_ + i) * M + j;
+              if (rp.recv_cnt[x] > 0) recv[s].push_back(Span{rbuf + rp.recv_off[x], rp.recv_cnt[x] * kTeraRecordBytes});
+            }
+        }
+        if (rccl_staging) {  // spill tier over RCCL: stage outgoing slices per peer, one message each
+          std::vector<std::vector<Span>> send(W);
+          int64_t off = 0;
+          for (int p = 0; p < W; ++p) {
+            const int64_t beg = off;
+            for (const Span& sp : rp.send[p]) {
+              HIP_CHECK(hipMemcpyAsync(send_staging_.as<uint8_t>() + off, sp.ptr, (size_t)sp.bytes,
+                                       hipMemcpyHostToDevice, s_comm_));
+              off += sp.bytes;
+            }
+            if (off > beg) send[p].push_back(Span{send_staging_.as<uint8_t>() + beg, off - beg});
+          }
+          st.bytes_h2d += off;
+          exchange_->exchange(send, recv, s_comm_);
+        } else {
+          exchange_->exchange(rp.send, recv, s_comm_);
+        }
+        st.bytes_sent += rp.send_bytes;
+      }
+      HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
+      HIP_CHECK(hipEventRecord(comm_ev_[slot], s_comm_));
+      HIP_CHECK(hipStreamWaitEvent(s_compute_, comm_ev_[slot], 0));
+    }
+    // runs of this round, grouped by reducer: group i = cell (i, q) from every source map
+    std::vector<RunDesc> runs;
+    std::vector<int> group_first{0};
+    runs.reserve((size_t)R_ * W * M);
+    for (int i = 0; i < R_; ++i) {
+      for (int s = 0; s < W; ++s)
+        for (int j = 0; j < M; ++j) {
+          const size_t x = ((size_t)s * R_ + i) * M + j;
+          RunDesc d;
+          d.nrec = rp.recv_cnt[x];
+          d.nbytes = d.nrec * kTeraRecordBytes;
+          d.offsets = nullptr;
+          if (rp.recv_off[x] >= 0)
+            d.base = rbuf + rp.recv_off[x];
+          else  // own cell, read in place from the HBM store
+            d.base = store_dev_base_ + run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+          runs.push_back(d);
+        }
+      group_first.push_back((int)runs.size());
+    }
+    // output slot reuse: every D2H piece of round q-kSlots must have landed
+    if (deliver && q >= kSlots) {
+      const double tw = now_ms();
+      wait_until([&] { return out_free_[q - kSlots] != 0; });
+      st.wait_out_ms += now_ms() - tw;
     }
     HIP_CHECK(hipEventRecord(ev[4 * q + 2], s_compute_));
     uint8_t* out = out_slots_[slot].as<uint8_t>();
-    const int64_t n = merger_->merge_fixed(runs, out, s_compute_);
+    const int64_t n = merger_->merge_fixed(runs, group_first, out, s_compute_);
     HIP_CHECK(hipGetLastError());
     st.merge_passes = std::max(st.merge_passes, merger_->last_passes());
-    if (cfg_.validate && n > 0) {
-      launch_validate_fixed(out, n, vprev, q > 0 ? 1 : 0, vlast, vstats, s_compute_);
-      HIP_CHECK(hipMemcpyAsync(vprev, vlast, sizeof(Elem), hipMemcpyDeviceToDevice, s_compute_));
+    if (validate) {
+      int64_t goff = 0;
+      for (int i = 0; i < R_; ++i) {
+        const int64_t g = rp.group_recs[i];
+        if (g > 0) {
+          launch_validate_fixed(out + goff * kTeraRecordBytes, g, vprev + i, has_prev[i] ? 1 : 0, vlast + i, vstats,
+                                s_compute_);
+          HIP_CHECK(hipMemcpyAsync(vprev + i, vlast + i, sizeof(Elem), hipMemcpyDeviceToDevice, s_compute_));
+          has_prev[i] = true;
+        }
+        goff += g;
+      }
+      if (W > 1 && verify_n_[q] > 0) {
+        launch_slice_checksums(d_verify_runs_[q].as<RunDesc>(), verify_n_[q], verify_max_nrec_[q],
+                               d_verify_got_.as<unsigned long long>(), s_compute_);
+        launch_count_mismatch(d_verify_got_.as<unsigned long long>(), d_verify_expect_[q].as<unsigned long long>(),
+                              verify_n_[q], vstats + 2, s_compute_);
+      }
+      HIP_CHECK(hipGetLastError());
     }
     HIP_CHECK(hipEventRecord(ev[4 * q + 3], s_compute_));
-    HIP_CHECK(hipEventRecord(merged[slot], s_compute_));
+    HIP_CHECK(hipEventRecord(merged_ev_[slot], s_compute_));
     st.records += n;
-    if (cfg_.deliver_host) {
+    if (deliver) {
       {
         std::lock_guard<std::mutex> g(mu_);
-        round_q_.push_back(RoundOut{q, slot, n, merged[slot]});
+        round_q_.push_back(RoundOut{q, slot, rp.group_recs});
       }
       cv_.notify_all();
     }
   }
-  if (cfg_.deliver_host) {
-    std::unique_lock<std::mutex> lk(mu_);
-    while (!cv_.wait_for(lk, std::chrono::milliseconds(100), [&] { return step_done_; })) {
-      if (exchange_) {  // a lost peer must fail the step, not hang it
-        lk.unlock();
-        exchange_->check();
-        lk.lock();
-      }
-    }
-  }
+  if (deliver) wait_until([&] { return eof_count_ == R_; });
   if (exchange_) exchange_->wait(s_comm_);
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   HIP_CHECK(hipStreamSynchronize(s_comm_));
-  for (auto s : s_copy_) HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipStreamSynchronize(s_copy_));
   st.wall_ms = now_ms() - t0;
-  for (int q = 0; q < Q; ++q) {
+  for (int q = 0; q < Q_; ++q) {
     float a = 0, b = 0;
-    if (hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
+    if (staged() && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
     if (hipEventElapsedTime(&b, ev[4 * q + 2], ev[4 * q + 3]) == hipSuccess) st.merge_ms += b;
   }
   for (auto e : ev) (void)hipEventDestroy(e);
-  for (auto e : merged) (void)hipEventDestroy(e);
-  for (auto e : comm_done) (void)hipEventDestroy(e);
   st.d2h_ms = step_d2h_ms_;
   st.bytes_in = st.records * kTeraRecordBytes;
-  st.bytes_sent = bytes_sent;
   st.buffers = step_buffers_;
-  if (cfg_.validate) {
-    unsigned long long v[2];
+  if (validate) {
+    unsigned long long v[3];
     HIP_CHECK(hipMemcpy(v, vstats, sizeof(v), hipMemcpyDeviceToHost));
     st.order_errors = (int64_t)v[0];
     st.checksum = v[1];
+    st.exchange_errors = W > 1 ? (int64_t)v[2] : 0;
   }
   st.bad_layout = merger_->bad_layout();
   if (step_error_) throw std::runtime_error("delivery sink reported error " + std::to_string(step_error_));

@@ -2,20 +2,27 @@
 //
 // Reference roles replaced:
 //   * MOFSupplier DataEngine (src/MOFServer/IndexInfo.cc:141-376) reading MOF chunks from disk with
-//     libaio and RDMA-writing them to reducers  ->  map-output partitions resident in HBM
-//     (`PartitionStore`), shipped by an RCCL all-to-all over xGMI in key-range rounds.
+//     libaio and RDMA-writing them to reducers  ->  map-output partitions resident in HBM (or the
+//     pinned-DRAM tier), shipped by an RCCL all-to-all over xGMI in key-range rounds.
 //   * NetMerger MergeManager online merge (src/Merger/MergeManager.cc:47-193) with a CPU heap
 //     k-way merge  ->  `DeviceMerger` (F2 keys, F3 merge-path tree, F4 gather) per round.
-//   * merge_do_merging_phase -> dataFromUda (src/Merger/MergeManager.cc:155-182): merged records are
-//     streamed D2H into a pinned-host ring on a copy stream and handed to the host sink in
-//     <= kv_buf_size buffers of whole records, the last one ending with the IFile EOF marker.
+//   * merge_do_merging_phase -> dataFromUda (src/Merger/MergeManager.cc:155-182): merged records go
+//     device -> host on the SDMA copy engines into a NUMA-local pinned ring and are handed to each
+//     reduce task's consumer thread in <= kv_buf_size buffers of whole records, the last one
+//     ending with the IFile EOF marker.
+//
+// Reduce tasks: every GPU hosts `reducers` reduce tasks (R); reducer i of GPU d owns the i-th
+// contiguous slice of GPU d's key range (TotalOrderPartitioner semantics: the concatenation of all
+// reducer outputs is globally sorted). Each reducer's range is cut into Q cells; cell (i, q) is
+// shipped and merged in round q ("horizontal" rounds), so every round feeds all R consumers at
+// once. Cell bounds come from a key sample taken when the job is planned (TeraSort's sampler).
 //
 // Pipeline per step (one process per GPU, W ranks):
-//   comm stream    : [a2a round q+1] .......
-//   compute stream : [extract+merge+gather round q] ....
-//   copy stream    : [D2H pieces of round q-1] ..........  -> deliver thread -> sink
-// Round q of reducer d holds the keys in [bound(d,q), bound(d,q+1)); bounds come from a key sample
-// taken when the job is planned (the TeraSort range-partition sampler's role).
+//   comm stream    : [a2a round q+1] ...
+//   compute stream : [extract + merge + gather round q (R independent groups)] ...
+//   SDMA engines   : [D2H pieces of round q-1] ...   -> R consumer threads -> sink
+// Round volumes are computed once in plan() (the map-side index records of the reference); a step
+// only enqueues work and waits on the delivery handoff.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -33,6 +40,7 @@
 
 #include "exchange.h"
 #include "kernels.h"
+#include "sdma.h"
 
 namespace uda {
 namespace gpu {
@@ -145,8 +153,11 @@ class DeviceMerger {
  public:
   DeviceMerger(int64_t max_records, int max_runs);
   ~DeviceMerger();
-  // Merge `runs` (device-resident) into `out` (n*104 bytes). Returns the record count.
-  int64_t merge_fixed(const std::vector<RunDesc>& runs, uint8_t* out, hipStream_t s);
+  // Merge `runs` (device-resident) into `out` (n*104 bytes). Runs are grouped: group g is runs
+  // [group_first[g], group_first[g+1]) and merges into its own contiguous output range, groups in
+  // order. Returns the record count.
+  int64_t merge_fixed(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
+                      hipStream_t s);
   // Number of merge-tree passes used by the last call.
   int last_passes() const { return last_passes_; }
   bool bad_layout();  // synchronizes; true if any record was not TeraSort-shaped
@@ -169,9 +180,9 @@ class DeviceMerger {
   size_t slot_bytes_ = 0;
 };
 
-// Delivery sink: called from the deliver thread with whole-record buffers (<= kv_buf_size).
-// Return nonzero to abort the step.
-using SinkFn = std::function<int(const uint8_t* buf, int64_t len)>;
+// Delivery sink: called from reducer r's consumer thread with whole-record buffers
+// (<= kv_buf_size). Return nonzero to abort the step.
+using SinkFn = std::function<int(int reducer, const uint8_t* buf, int64_t len)>;
 
 struct ShuffleConfig {
   int device = 0;
@@ -179,32 +190,36 @@ struct ShuffleConfig {
   int world = 1;
   int maps_per_rank = 32;
   int64_t records_per_map = 1 << 20;
-  int rounds = 8;
+  int rounds = 8;                        // Q: cells per reducer
+  int reducers = 1;                      // R: reduce tasks hosted by this GPU
   uint64_t seed = 0x5eed;
   int64_t kv_buf_bytes = 1 << 20;        // delivery buffer size (J2CQueue kv_buf_size)
-  int64_t d2h_piece_bytes = 64ll << 20;  // D2H granule (rounded down to whole buffers)
-  int pinned_slots = 6;
-  int d2h_streams = 1;                   // split each piece over this many copy streams
+  int64_t d2h_piece_bytes = 128ll << 20; // D2H granule (rounded down to whole buffers)
+  int pinned_slots = 16;
+  int d2h_engines = 2;                   // SDMA engines a piece is split over
+  std::string d2h = "sdma";              // "sdma" (explicit copy engines) or "hip" (hipMemcpyAsync)
   bool deliver_host = true;              // false: stop after the device merge (ablation)
-  bool validate = false;                 // device-side order + checksum check per round
+  bool validate = false;                 // device-side order/checksum/exchange checks every step
   std::string local_group;               // world > 1 without RCCL: ranks are threads of one process
   std::string store = "hbm";             // map-output store: "hbm" or "host" (pinned DRAM spill tier)
 };
 
 struct StepStats {
   double wall_ms = 0;          // host wall time of the whole step
-  double split_ms = 0;         // round split + counts exchange (host wall)
-  double comm_ms = 0;          // sum of per-round all-to-all time (device events)
-  double merge_ms = 0;         // sum of per-round merge time (device events)
-  double d2h_ms = 0;           // copy-stream busy time (device events, summed over pieces)
-  int64_t bytes_in = 0;        // partition bytes delivered to this reducer (records only)
+  double comm_ms = 0;          // sum of per-round exchange time (device events on the comm stream)
+  double merge_ms = 0;         // sum of per-round merge time (device events on the compute stream)
+  double d2h_ms = 0;           // host time the delivery copies were outstanding (summed per piece)
+  double wait_out_ms = 0;      // host time the merge waited for a free output slot (D2H-bound)
+  int64_t bytes_in = 0;        // partition bytes delivered to this GPU's reducers (records only)
   int64_t records = 0;
   int64_t bytes_sent = 0;      // bytes this rank sent to peers (excl. self)
   int64_t bytes_h2d = 0;       // spill tier: bytes streamed host -> device
   int64_t buffers = 0;         // sink invocations
   int merge_passes = 0;
+  bool validated = false;      // the checks below ran
   int64_t order_errors = -1;   // validate only
   uint64_t checksum = 0;       // validate only: sum of record hashes seen by the device
+  int64_t exchange_errors = -1;  // validate only: received slices whose checksum differs from the sender's
   bool bad_layout = false;
 };
 
@@ -218,49 +233,63 @@ class ShuffleJob {
   void init_comm(const std::string& uid);
   // Single-process rehearsal: ranks are threads sharing this device (config.local_group).
   void init_local();
-  // Map phase stand-in: generate maps_per_rank TeraSort MOFs into the HBM partition store.
+  // Map phase stand-in: generate maps_per_rank TeraSort MOFs into the partition store.
   void generate();
-  // Every `every`-th key of every local run, grouped by destination reducer:
+  // Every `every`-th key of every local run, grouped by destination GPU:
   // result[d] = flat (hi, lo) pairs.
   std::vector<std::vector<uint64_t>> sample_keys(int64_t every);
-  // bounds: world x (rounds-1) x 2 u64 (hi, lo16<<48), ascending per destination.
+  // bounds: world x (reducers*rounds - 1) x 2 u64 (hi, lo16<<48), ascending per destination GPU;
+  // cell c = i*rounds + q of GPU d is [bound(d, c-1), bound(d, c)).
   void set_bounds(const std::vector<uint64_t>& bounds);
-  // Compute exact per-round volumes and allocate the round buffers. Collective when world > 1.
+  // Compute the exact per-round volumes (cell splits + counts exchange), allocate the round buffers
+  // and start the delivery threads. Collective when world > 1.
   void plan();
   void set_sink(SinkFn sink) { sink_ = std::move(sink); }
   // One shuffle+merge+deliver pass over the whole dataset. Collective when world > 1.
-  StepStats run_step();
+  // validate: run the device-side order / checksum / exchange checks in this step.
+  StepStats run_step(bool validate);
 
-  // Per-destination checksum of locally generated records (sum of record_hash).
+  // Per-destination-GPU checksum of locally generated records (sum of record_hash).
   std::vector<uint64_t> local_dest_checksums() const { return dest_checksum_; }
   std::vector<int64_t> local_dest_records() const { return dest_records_; }
+  // Records each of this GPU's reducers receives per step (after plan()).
+  std::vector<int64_t> reducer_records() const { return reducer_records_; }
   int64_t store_bytes() const { return store_bytes_; }
   int64_t max_round_records() const { return max_round_records_; }
-  // Index record of (local map m, reducer d): offset, rawLength, partLength within MOF m.
+  int comm_ranks() const { return exchange_ ? exchange_->comm_ranks() : 1; }
+  std::string exchange_name() const { return exchange_ ? exchange_->name() : "none"; }
+  std::string delivery_name() const;
+  // Index record of (local map m, destination GPU d): offset, rawLength, partLength within MOF m.
   std::vector<int64_t> index_record(int m, int d) const;
   // Copy a MOF partition (records + EOF) to host (tests / provider fallback path).
   std::vector<uint8_t> read_partition(int m, int d) const;
 
  private:
   struct RoundPlan {
-    // send side: per (dest p, local map m): record range [beg, end) in run (m, p)
-    std::vector<int64_t> send_beg, send_end;  // index p*M + m
-    // recv side: per (src s, map j of s): record count
-    std::vector<int64_t> recv_cnt;  // index s*M + j
+    // send[p]: slices to GPU p, order (reducer i, local map m); empty for p == me
+    std::vector<std::vector<Span>> send;
+    int64_t send_bytes = 0;
+    // recv_cnt[(s*R + i)*M + j]: records of source s's map j for my reducer i
+    std::vector<int64_t> recv_cnt;
+    std::vector<int64_t> recv_off;     // byte offset of that slice in the receive slot (s-major)
+    std::vector<int64_t> self_beg;     // [i*M + m] first record of my own cell (i, q) in run (m, me)
+    std::vector<int64_t> group_recs;   // records per reducer this round
     int64_t recv_records = 0;
   };
-  void compute_round_plans(std::vector<RoundPlan>* plans, double* ms);
-  void deliver_loop();
+  void compute_plans();
   void copy_loop();
+  void consume_loop(int reducer);
+  void wait_exchange_ok();
   // Host-visible address of a run (device address for the HBM store, host address for the host
   // tier); kernels use the device-mapped addresses in d_run_bases_.
   uint8_t* run_base(int m, int d) const { return store_base_ + run_off_[m * cfg_.world + d]; }
   bool host_store() const { return cfg_.store == "host"; }
+  bool staged() const { return cfg_.world > 1 || host_store(); }
 
   ShuffleConfig cfg_;
+  int R_ = 1, Q_ = 1, C_ = 1;  // reducers, rounds, cells (R*Q) per GPU
   std::unique_ptr<Exchange> exchange_;
-  hipStream_t s_comm_ = nullptr, s_compute_ = nullptr;
-  std::vector<hipStream_t> s_copy_;
+  hipStream_t s_comm_ = nullptr, s_compute_ = nullptr, s_copy_ = nullptr;
   DeviceBuffer store_;
   PinnedBuffer hstore_;
   uint8_t* store_base_ = nullptr;      // where run_base() points
@@ -269,58 +298,59 @@ class ShuffleJob {
   std::vector<int64_t> mof_off_, run_off_, run_nrec_;  // run index m*W + d
   std::vector<uint64_t> dest_checksum_;
   std::vector<int64_t> dest_records_;
-  std::vector<uint64_t> bounds_;  // W x (Q-1) x 2
+  std::vector<int64_t> reducer_records_;
+  std::vector<uint64_t> bounds_;  // W x (C-1) x 2
   DeviceBuffer d_bounds_, d_run_bases_, d_run_nrec_, d_bound_set_, d_split_out_;
+  std::vector<int64_t> split_pos_;  // [run r][cell c .. C]: (C+1) record positions per run
   std::vector<RoundPlan> plans_;
   int64_t max_round_records_ = 0;
-  std::vector<DeviceBuffer> recv_slots_, out_slots_, pack_slots_;
-  int64_t max_send_bytes_ = 0;
-  // copy-descriptor upload ring (pinned host -> device), guarded by events
-  struct DescSlot {
-    PinnedBuffer host;
-    DeviceBuffer dev;
-    hipEvent_t uploaded = nullptr;
-    bool used = false;
-  };
-  std::vector<DescSlot> desc_slots_;
-  int next_desc_ = 0;
+  std::vector<DeviceBuffer> recv_slots_, out_slots_;
+  DeviceBuffer send_staging_;  // host store + RCCL: this round's outgoing slices, per peer contiguous
+  std::vector<hipEvent_t> merged_ev_, comm_ev_;  // per slot
   std::unique_ptr<DeviceMerger> merger_;
-  DeviceBuffer d_validate_;  // stats[2] + prev key + last key
-  PinnedBuffer pinned_;
-  int64_t piece_bytes_ = 0;
+  DeviceBuffer d_validate_;  // stats[4] | prev key[R] | last key[R]
+  // exchange verification (validate steps, world > 1): per round, the received peer slices and
+  // the checksums their senders computed at plan()
+  std::vector<DeviceBuffer> d_verify_runs_, d_verify_expect_;
+  std::vector<int> verify_n_;
+  std::vector<int64_t> verify_max_nrec_;
+  DeviceBuffer d_verify_got_;
   int64_t buf_records_ = 0;
+  int64_t piece_bytes_ = 0;
 
-  // host pipeline state
-  struct Piece {
-    int slot;
-    int64_t bytes;
-    bool last;
-    hipEvent_t done;
-  };
+  // ---- delivery: copy thread -> pinned ring (SDMA) -> per-reducer consumer threads
+  std::unique_ptr<SdmaEngine> sdma_;
+  uint8_t* ring_ = nullptr;          // pinned_slots x piece_bytes_
+  PinnedBuffer ring_hip_;            // ring for the "hip" delivery mode
+  std::vector<hsa_signal_t> piece_sig_;
+  std::vector<hipEvent_t> piece_ev_;
   struct RoundOut {
     int q;
-    int out_slot;
-    int64_t records;
-    hipEvent_t merged;
+    int slot;
+    std::vector<int64_t> group_recs;
+  };
+  struct Item {
+    int pslot;          // pinned slot, -1 for an EOF-only item
+    int64_t bytes;
+    bool last;          // this reducer's final data: append EOF
+    double issued_ms;
   };
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<RoundOut> round_q_;
-  std::deque<Piece> piece_q_;
+  std::vector<std::deque<Item>> items_;  // per reducer
   std::vector<bool> pinned_free_;
-  std::vector<hipEvent_t> piece_events_;
-  std::vector<hipEvent_t> out_free_ev_;   // recorded on copy stream after a round's D2H
-  std::vector<int> d2h_enqueued_;         // per round: 1 once its D2H is enqueued
-  std::thread copy_thr_, deliver_thr_;
+  std::vector<int> out_free_;  // per round: its output slot may be reused
+  std::thread copy_thr_;
+  std::vector<std::thread> consumers_;
   bool stop_ = false;
-  bool step_done_ = false;
+  int eof_count_ = 0;
   int64_t step_buffers_ = 0;
   int step_error_ = 0;
+  std::string step_error_msg_;
   double step_d2h_ms_ = 0;
-  std::vector<hipEvent_t> piece_start_ev_;
-  std::vector<hipEvent_t> join_ev_;
   SinkFn sink_;
-  PinnedBuffer eof_buf_;
+  std::vector<std::unique_ptr<uint8_t[]>> eof_bufs_;  // per reducer: final chunk + EOF marker
 };
 
 // ncclUniqueId as bytes (rank 0 creates, others receive it out of band).

@@ -7,10 +7,10 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
 #include <map>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "device_engine.h"
 
@@ -23,6 +23,12 @@ void nccl_check(ncclResult_t r, const char* what) {
 }
 #define NCCL_CHECK(x) nccl_check((x), #x)
 
+bool env_flag(const char* name, bool dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atoi(v) != 0;
+}
+
 // ------------------------------------------------------------------------------------ RCCL
 class RcclExchange : public Exchange {
  public:
@@ -31,25 +37,29 @@ class RcclExchange : public Exchange {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
-    HIP_CHECK(hipMalloc(&d_counts_, 1));
     if (const char* t = std::getenv("UDA_RCCL_TIMEOUT_S")) timeout_ = std::chrono::seconds(std::max(1, std::atoi(t)));
+    pack_ = env_flag("UDA_RCCL_PACK", true);
+    descs_.resize(4);
+    for (auto& d : descs_) HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
   }
   ~RcclExchange() override {
     if (comm_) (aborted_ ? ncclCommAbort(comm_) : ncclCommDestroy(comm_));
-    if (d_counts_) (void)hipFree(d_counts_);
+    for (auto& d : descs_)
+      if (d.uploaded) (void)hipEventDestroy(d.uploaded);
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
-  const char* name() const override { return "rccl"; }
+  int comm_ranks() const override {
+    int n = 0;
+    if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+    return n;
+  }
+  const char* name() const override { return pack_ ? "rccl" : "rccl-zero-copy"; }
 
   void alltoall_i64(const int64_t* send, int64_t* recv, size_t n, hipStream_t s) override {
     const size_t bytes = n * (size_t)world_ * 8;
-    if (bytes * 2 > counts_cap_) {
-      if (d_counts_) HIP_CHECK(hipFree(d_counts_));
-      HIP_CHECK(hipMalloc(&d_counts_, bytes * 2));
-      counts_cap_ = bytes * 2;
-    }
-    int64_t* ds = (int64_t*)d_counts_;
+    if (counts_.size() < bytes * 2) counts_.alloc(bytes * 2);
+    int64_t* ds = counts_.as<int64_t>();
     int64_t* dr = ds + n * world_;
     HIP_CHECK(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, s));
     NCCL_CHECK(ncclGroupStart());
@@ -60,6 +70,10 @@ class RcclExchange : public Exchange {
     NCCL_CHECK(ncclGroupEnd());
     HIP_CHECK(hipMemcpyAsync(recv, dr, bytes, hipMemcpyDeviceToHost, s));
     wait(s);
+  }
+
+  void reserve(int64_t bytes) override {
+    if (pack_ && (int64_t)staging_.size() < bytes) staging_.alloc((size_t)std::max<int64_t>(bytes, 16));
   }
 
   void check() override {
@@ -82,14 +96,68 @@ class RcclExchange : public Exchange {
     }
   }
 
-  void alltoallv(const uint8_t* send, const int64_t* sb, const int64_t* sd, uint8_t* recv, const int64_t* rb,
-                 const int64_t* rd, hipStream_t s) override {
+  void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
+                hipStream_t s) override {
+    if ((int)send.size() != world_ || (int)recv.size() != world_) throw std::runtime_error("exchange: bad peer lists");
+    if (!send[rank_].empty() || !recv[rank_].empty()) throw std::runtime_error("exchange: self slices");
+    std::vector<Span> one_send(world_, Span{nullptr, 0}), one_recv(world_, Span{nullptr, 0});
+    if (pack_) {
+      // stage every peer's slices contiguously (rotating peer order) with one batched-copy launch
+      DescSlot& ds = descs_[next_desc_];
+      next_desc_ = (next_desc_ + 1) % (int)descs_.size();
+      if (ds.used) HIP_CHECK(hipEventSynchronize(ds.uploaded));
+      size_t nd = 0;
+      for (int p = 0; p < world_; ++p) nd += send[p].size();
+      if (ds.host.size() < nd * sizeof(CopyDesc)) {
+        ds.host.alloc(std::max<size_t>(nd, 64) * sizeof(CopyDesc));
+        ds.dev.alloc(std::max<size_t>(nd, 64) * sizeof(CopyDesc));
+      }
+      ds.used = true;
+      CopyDesc* d = ds.host.as<CopyDesc>();
+      int n = 0;
+      int64_t off = 0, max_bytes = 0;
+      for (int k = 1; k < world_; ++k) {
+        const int to = (rank_ + k) % world_;
+        const int64_t beg = off;
+        for (const Span& sp : send[to]) {
+          if (off + sp.bytes > (int64_t)staging_.size()) throw std::runtime_error("exchange: staging too small");
+          d[n++] = CopyDesc{sp.ptr, staging_.as<uint8_t>() + off, sp.bytes};
+          max_bytes = std::max(max_bytes, sp.bytes);
+          off += sp.bytes;
+        }
+        one_send[to] = Span{staging_.as<uint8_t>() + beg, off - beg};
+      }
+      if (n > 0) {
+        HIP_CHECK(hipMemcpyAsync(ds.dev.as(), d, sizeof(CopyDesc) * n, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipEventRecord(ds.uploaded, s));
+        launch_batched_copy(ds.dev.as<CopyDesc>(), n, max_bytes, s);
+      }
+      for (int p = 0; p < world_; ++p) {
+        if (p == rank_ || recv[p].empty()) continue;
+        int64_t total = 0;
+        for (const Span& sp : recv[p]) {
+          if (sp.ptr != recv[p][0].ptr + total)
+            throw std::runtime_error("exchange: packed mode needs contiguous receive slices per peer");
+          total += sp.bytes;
+        }
+        one_recv[p] = Span{recv[p][0].ptr, total};
+      }
+    }
     NCCL_CHECK(ncclGroupStart());
     for (int k = 1; k < world_; ++k) {
-      const int to = (rank_ + k) % world_;      // rotating order spreads the xGMI link load
+      const int to = (rank_ + k) % world_;  // rotating order spreads the xGMI link load
       const int from = (rank_ - k + world_) % world_;
-      if (sb[to] > 0) NCCL_CHECK(ncclSend(send + sd[to], (size_t)sb[to], ncclUint8, to, comm_, s));
-      if (rb[from] > 0) NCCL_CHECK(ncclRecv(recv + rd[from], (size_t)rb[from], ncclUint8, from, comm_, s));
+      if (pack_) {
+        if (one_send[to].bytes > 0)
+          NCCL_CHECK(ncclSend(one_send[to].ptr, (size_t)one_send[to].bytes, ncclUint8, to, comm_, s));
+        if (one_recv[from].bytes > 0)
+          NCCL_CHECK(ncclRecv(const_cast<uint8_t*>(one_recv[from].ptr), (size_t)one_recv[from].bytes, ncclUint8, from,
+                              comm_, s));
+      } else {
+        for (const Span& sp : send[to]) NCCL_CHECK(ncclSend(sp.ptr, (size_t)sp.bytes, ncclUint8, to, comm_, s));
+        for (const Span& sp : recv[from])
+          NCCL_CHECK(ncclRecv(const_cast<uint8_t*>(sp.ptr), (size_t)sp.bytes, ncclUint8, from, comm_, s));
+      }
     }
     NCCL_CHECK(ncclGroupEnd());
   }
@@ -105,39 +173,51 @@ class RcclExchange : public Exchange {
     }
     throw std::runtime_error(why);
   }
+  struct DescSlot {
+    PinnedBuffer host;
+    DeviceBuffer dev;
+    hipEvent_t uploaded = nullptr;
+    bool used = false;
+  };
   int rank_, world_;
   ncclComm_t comm_ = nullptr;
   bool aborted_ = false;
+  bool pack_ = true;
   std::chrono::seconds timeout_{900};
-  void* d_counts_ = nullptr;
-  size_t counts_cap_ = 0;
+  DeviceBuffer counts_, staging_;
+  std::vector<DescSlot> descs_;
+  int next_desc_ = 0;
 };
 
 // ------------------------------------------------------------------------------------ local group
+// Threads of one process meet at barriers. A rank that fails between barriers aborts the group so
+// the others throw instead of waiting forever; the group is erased with its last member.
 struct Group {
   int world = 0;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   uint64_t generation = 0;
-  struct Post {
-    const void* send = nullptr;
-    const int64_t* sb = nullptr;
-    const int64_t* sd = nullptr;
-    hipEvent_t ready = nullptr;  // sender's data is packed
-    hipEvent_t done = nullptr;   // this rank finished reading its peers' data
-  };
-  std::vector<Post> posts;
+  bool aborted = false;
+  std::vector<const std::vector<std::vector<Span>>*> sends;  // per rank, valid between barriers
+  std::vector<const int64_t*> counts;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
+    if (aborted) throw std::runtime_error("local exchange group aborted by another rank");
     const uint64_t gen = generation;
     if (++arrived == world) {
       arrived = 0;
       ++generation;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return generation != gen; });
+      cv.wait(lk, [&] { return generation != gen || aborted; });
+      if (aborted) throw std::runtime_error("local exchange group aborted by another rank");
     }
+  }
+  void abort() {
+    std::lock_guard<std::mutex> g(mu);
+    aborted = true;
+    cv.notify_all();
   }
 };
 
@@ -146,22 +226,22 @@ std::map<std::string, std::shared_ptr<Group>> g_groups;
 
 class LocalExchange : public Exchange {
  public:
-  LocalExchange(const std::string& name, int rank, int world) : rank_(rank), world_(world) {
+  LocalExchange(const std::string& name, int rank, int world) : name_(name), rank_(rank), world_(world) {
     std::lock_guard<std::mutex> g(g_groups_mu);
     auto& grp = g_groups[name];
-    if (!grp) {
+    if (!grp || grp->aborted) {
       grp = std::make_shared<Group>();
       grp->world = world;
-      grp->posts.resize(world);
+      grp->sends.assign(world, nullptr);
+      grp->counts.assign(world, nullptr);
     }
     if (grp->world != world) throw std::runtime_error("local exchange: world mismatch");
     group_ = grp;
-    HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   }
   ~LocalExchange() override {
-    (void)hipEventDestroy(ready_);
-    (void)hipEventDestroy(done_);
+    std::lock_guard<std::mutex> g(g_groups_mu);
+    auto it = g_groups.find(name_);
+    if (it != g_groups.end() && it->second == group_ && group_.use_count() <= 2) g_groups.erase(it);
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
@@ -169,45 +249,42 @@ class LocalExchange : public Exchange {
 
   void alltoall_i64(const int64_t* send, int64_t* recv, size_t n, hipStream_t) override {
     Group& g = *group_;
-    g.posts[rank_].send = send;
+    g.counts[rank_] = send;
     g.barrier();
-    for (int p = 0; p < world_; ++p)
-      std::memcpy(recv + p * n, (const int64_t*)g.posts[p].send + (size_t)rank_ * n, n * 8);
+    for (int p = 0; p < world_; ++p) std::memcpy(recv + p * n, g.counts[p] + (size_t)rank_ * n, n * 8);
     g.barrier();
   }
 
-  void alltoallv(const uint8_t* send, const int64_t* sb, const int64_t* sd, uint8_t* recv, const int64_t* rb,
-                 const int64_t* rd, hipStream_t s) override {
+  void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
+                hipStream_t s) override {
     Group& g = *group_;
-    HIP_CHECK(hipEventRecord(ready_, s));
-    g.posts[rank_].send = send;
-    g.posts[rank_].sb = sb;
-    g.posts[rank_].sd = sd;
-    g.posts[rank_].ready = ready_;
-    g.posts[rank_].done = done_;
+    g.sends[rank_] = &send;
     g.barrier();
-    for (int k = 1; k < world_; ++k) {
-      const int from = (rank_ - k + world_) % world_;
-      const auto& p = g.posts[from];
-      if (p.sb[rank_] != rb[from])
-        throw std::runtime_error("local exchange: size mismatch between sender and receiver plans");
-      if (rb[from] <= 0) continue;
-      HIP_CHECK(hipStreamWaitEvent(s, p.ready, 0));
-      HIP_CHECK(hipMemcpyAsync(recv + rd[from], (const uint8_t*)p.send + p.sd[rank_], (size_t)rb[from],
-                               hipMemcpyDeviceToDevice, s));
+    try {
+      for (int k = 1; k < world_; ++k) {
+        const int from = (rank_ - k + world_) % world_;
+        const auto& theirs = (*g.sends[from])[rank_];
+        const auto& mine = recv[from];
+        if (theirs.size() != mine.size())
+          throw std::runtime_error("local exchange: slice count mismatch between sender and receiver plans");
+        for (size_t i = 0; i < mine.size(); ++i) {
+          if (theirs[i].bytes != mine[i].bytes)
+            throw std::runtime_error("local exchange: slice size mismatch between sender and receiver plans");
+          HIP_CHECK(hipMemcpyAsync(const_cast<uint8_t*>(mine[i].ptr), theirs[i].ptr, (size_t)mine[i].bytes,
+                                   hipMemcpyDefault, s));
+        }
+      }
+    } catch (...) {
+      g.abort();
+      throw;
     }
-    HIP_CHECK(hipEventRecord(done_, s));
-    g.barrier();
-    // send completion: my packed buffer may be reused only after every receiver copied it
-    for (int p = 0; p < world_; ++p)
-      if (p != rank_) HIP_CHECK(hipStreamWaitEvent(s, g.posts[p].done, 0));
-    g.barrier();  // posts (and events) stay valid until everyone enqueued its waits
+    g.barrier();  // peers' send lists are no longer read
   }
 
  private:
+  std::string name_;
   int rank_, world_;
   std::shared_ptr<Group> group_;
-  hipEvent_t ready_ = nullptr, done_ = nullptr;
 };
 }  // namespace
 

@@ -1,17 +1,27 @@
 // Device all-to-all-v exchange used by the shuffle rounds.
 //
-// Reference analogue: the M x R point-to-point RDMA WRITEs. On MI355X one round
-// of the shuffle is an all-to-all-v over xGMI: every rank packs, per destination, the slices of its
-// map outputs that fall in the round's key range into one contiguous region, then each pair of
-// ranks exchanges one message per direction (ncclSend/ncclRecv grouped: the pattern RCCL's
-// all-to-all uses, so all 7 xGMI links of a GPU are driven at once).
+// Reference analogue: the M x R point-to-point RDMA WRITEs of MOF chunks into reducer buffers
+// (src/DataNet/RDMAServer.cc:537-631 rdma_write_mof_send_ack, src/DataNet/RDMAClient.cc:559-600
+// start_fetch_req). On MI355X one round of the shuffle is an all-to-all-v over xGMI: every rank
+// sends, per destination, the slices of its map outputs that fall in the round's key cells, and
+// receives its own cells from every peer.
+//
+// Contract of exchange(): send[p] / recv[p] are the ordered non-empty slices to / from peer p
+// (p != me; the self entry must be empty). The k-th slice this rank sends to p pairs with the
+// k-th slice p receives from this rank; sizes must agree. Slices stay valid and unchanged until
+// the enqueued work on `s` has passed this exchange.
 //
 // Implementations:
 //   RcclExchange   - one process per GPU, RCCL communicator bootstrapped from an ncclUniqueId.
+//                    Default: the slices to each peer are packed on the comm stream into one
+//                    staging region and sent as ONE ncclSend per peer per round (RCCL pairs
+//                    operations, not bytes, and a large message per peer is what keeps all xGMI
+//                    links busy); the receiver's slices from a peer must then be contiguous.
+//                    UDA_RCCL_PACK=0 sends every slice as its own ncclSend (zero-copy).
 //   LocalExchange  - W ranks as threads of one process sharing a device (tests / single-GPU
-//                    rehearsal of the multi-rank schedule): copies are device memcpys, and the
-//                    completion semantics of a send (sender may reuse its buffer only once every
-//                    receiver has copied) are reproduced with cross-stream events.
+//                    rehearsal of the multi-rank schedule): each receiver pulls its slices from
+//                    the senders' memory with copies on its own stream. Requires the send slices
+//                    to be immutable for the whole step (true for store-resident map outputs).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -25,17 +35,25 @@ typedef struct ncclComm* ncclComm_t;
 namespace uda {
 namespace gpu {
 
+struct Span {
+  const uint8_t* ptr;
+  int64_t bytes;
+};
+
 class Exchange {
  public:
   virtual ~Exchange() = default;
   virtual int rank() const = 0;
   virtual int world() const = 0;
+  // Ranks the underlying communicator reports (ncclCommCount for RCCL).
+  virtual int comm_ranks() const { return world(); }
   // Blocking exchange of `n` int64 per peer: recv[p*n..] <- peer p's send[me*n..].
   virtual void alltoall_i64(const int64_t* send, int64_t* recv, size_t n, hipStream_t s) = 0;
-  // Enqueue an all-to-all-v on stream s. Byte counts/displacements per peer; self entries must be 0.
-  virtual void alltoallv(const uint8_t* send, const int64_t* send_bytes, const int64_t* send_displ,
-                         uint8_t* recv, const int64_t* recv_bytes, const int64_t* recv_displ,
-                         hipStream_t s) = 0;
+  // Size internal staging for rounds sending at most `bytes` to all peers together.
+  virtual void reserve(int64_t bytes) { (void)bytes; }
+  // Enqueue one all-to-all-v round on stream s (see the contract above).
+  virtual void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
+                        hipStream_t s) = 0;
   virtual const char* name() const = 0;
   // Host wait for everything enqueued on `s`, failing instead of hanging when a peer is lost
   // (RCCL: asynchronous communicator errors and a timeout, UDA_RCCL_TIMEOUT_S, default 900 s).

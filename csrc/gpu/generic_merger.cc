@@ -1,4 +1,5 @@
 #include "generic_merger.h"
+#include "merge_plan.h"
 
 #include "uda/trace.h"
 
@@ -192,33 +193,20 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   launch_normalize_generic(ctx, d_eoff, K, total, cur, s);
   phase("f2_normalize");
   // ---- F3: merge tree; per-pass descriptors are small host tables uploaded per pass
-  std::vector<int64_t> seg(eoff);
   std::vector<DeviceBuffer> pass_tabs;
-  while ((int)seg.size() - 1 > 1) {
-    const int S = (int)seg.size() - 1;
-    const int P = (S + 1) / 2;
-    std::vector<int64_t> tab(S + 1 + P + 1);
-    std::copy(seg.begin(), seg.end(), tab.begin());
-    int64_t* tp = tab.data() + S + 1;
-    tp[0] = 0;
-    std::vector<int64_t> next{0};
-    for (int p = 0; p < P; ++p) {
-      const int64_t beg = seg[2 * p], end = seg[std::min(2 * p + 2, S)];
-      tp[p + 1] = tp[p] + (end - beg + kMergeTile - 1) / kMergeTile;
-      next.push_back(end);
-    }
+  for (const MergePassPlan& mp : plan_merge_passes(eoff, {0, (int)eoff.size() - 1})) {
+    std::vector<int64_t> tab(mp.pairs);
+    tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
     pass_tabs.emplace_back(tab.size() * 8);
     HIP_CHECK(hipMemcpyAsync(pass_tabs.back().as(), tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
     PassDesc pd;
-    pd.seg_off = pass_tabs.back().as<int64_t>();
-    pd.tile_prefix = pass_tabs.back().as<int64_t>() + S + 1;
-    pd.nseg = S;
-    pd.npairs = P;
-    pd.ntiles = (int)tp[P];
+    pd.pairs = pass_tabs.back().as<int64_t>();
+    pd.tile_prefix = pass_tabs.back().as<int64_t>() + mp.pairs.size();
+    pd.npairs = mp.npairs;
+    pd.ntiles = mp.ntiles;
     launch_merge_partition_generic(cur, pd, splits_.as<int64_t>(), ctx, s);
     launch_merge_pass_generic(cur, nxt, pd, splits_.as<int64_t>(), ctx, s);
     std::swap(cur, nxt);
-    seg.swap(next);
     ++res.passes;
   }
   phase("f3_merge_tree");

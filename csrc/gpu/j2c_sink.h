@@ -1,0 +1,98 @@
+// Native stand-in for the Java reducer that consumes the merged stream: per reduce task, every
+// delivered buffer is copied into a 1 MiB KVBuf (two of them, alternating) and its records are
+// walked by their VInt key/value lengths, exactly the work UdaPluginRT.dataFromUda and
+// J2CQueue.next do (plugins/shared/com/mellanox/hadoop/mapred/UdaPlugin.java:369-402,498-538).
+// Each reduce task is consumed by its own thread (the engine's per-reducer consumer), so the sink
+// keeps per-reducer state only and needs no locks on the hot path.
+//
+// It also validates the delivery contract: every buffer holds whole records, is at most
+// kv_buf_bytes long, and each reducer's stream ends with exactly one EOF marker (-1, -1).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "uda/vint.h"
+
+namespace uda {
+namespace gpu {
+
+class J2CSink {
+ public:
+  enum Error : int { kOk = 0, kTooLong = 1, kBadFraming = 2, kAfterEof = 3 };
+
+  J2CSink(int reducers, int64_t kv_buf_bytes) : kv_(kv_buf_bytes), st_(reducers) {
+    for (auto& s : st_) {
+      s.buf[0].reset(new uint8_t[(size_t)kv_buf_bytes]);
+      s.buf[1].reset(new uint8_t[(size_t)kv_buf_bytes]);
+    }
+  }
+
+  int reducers() const { return (int)st_.size(); }
+
+  // Called from reducer r's consumer thread only.
+  int consume(int r, const uint8_t* data, int64_t len) {
+    State& s = st_[(size_t)r];
+    if (len > kv_) return fail(s, kTooLong);
+    if (s.eof) return fail(s, kAfterEof);
+    uint8_t* kb = s.buf[s.cur].get();
+    s.cur ^= 1;
+    std::memcpy(kb, data, (size_t)len);  // dataFromUda: DirectByteBuffer -> KVBuf
+    int64_t p = 0, recs = 0;
+    while (p < len) {  // J2CQueue.next: readVInt key length, readVInt value length, skip bytes
+      int64_t kl = 0, vl = 0;
+      const int a = vint_decode(kb + p, (size_t)(len - p), &kl);
+      if (a <= 0) return fail(s, kBadFraming);
+      const int b = vint_decode(kb + p + a, (size_t)(len - p - a), &vl);
+      if (b <= 0) return fail(s, kBadFraming);
+      if (kl == -1 && vl == -1) {
+        if (p + a + b != len) return fail(s, kBadFraming);
+        s.eof = true;
+        p = len;
+        break;
+      }
+      if (kl < 0 || vl < 0) return fail(s, kBadFraming);
+      p += a + b + kl + vl;
+      s.key_bytes += kl;
+      ++recs;
+    }
+    if (p != len) return fail(s, kBadFraming);
+    s.records += recs;
+    s.bytes += len;
+    s.buffers += 1;
+    return kOk;
+  }
+
+  void reset() {
+    for (auto& s : st_) {
+      s.records = s.bytes = s.buffers = s.key_bytes = 0;
+      s.eof = false;
+      s.error = kOk;
+    }
+  }
+  int64_t records(int r) const { return st_[(size_t)r].records; }
+  int64_t bytes(int r) const { return st_[(size_t)r].bytes; }
+  int64_t buffers(int r) const { return st_[(size_t)r].buffers; }
+  bool eof(int r) const { return st_[(size_t)r].eof; }
+  int error(int r) const { return st_[(size_t)r].error; }
+
+ private:
+  struct alignas(64) State {
+    std::unique_ptr<uint8_t[]> buf[2];
+    int cur = 0;
+    int64_t records = 0, bytes = 0, buffers = 0, key_bytes = 0;
+    bool eof = false;
+    int error = kOk;
+  };
+  static int fail(State& s, int e) {
+    if (s.error == kOk) s.error = e;
+    return e;
+  }
+  int64_t kv_;
+  std::vector<State> st_;
+};
+
+}  // namespace gpu
+}  // namespace uda

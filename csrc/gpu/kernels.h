@@ -72,13 +72,14 @@ void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nrun
 
 // ---------------------------------------------------------------- merge tree (F3)
 constexpr int kMergeTile = 2048;  // output elements per workgroup (256 threads x 8)
-// One merge pass over S sorted segments (segment k = [seg_off[k], seg_off[k+1])): segments
-// (2p, 2p+1) merge into pair p (an odd last segment is copied through). Pair p produces tiles
-// [tile_prefix[p], tile_prefix[p+1]) of kMergeTile outputs each (last tile of a pair may be short).
+// One merge pass. Pair p merges the adjacent sorted element ranges A = [pairs[3p], pairs[3p+1]) and
+// B = [pairs[3p+1], pairs[3p+2]) into the same index range of the output (B may be empty: the range
+// is copied through). Pair p produces tiles [tile_prefix[p], tile_prefix[p+1]) of kMergeTile
+// outputs each (the last tile of a pair may be short). Pairs are planned on the host
+// (merge_plan.h) so that segments of different groups (reducers) never merge.
 struct PassDesc {
-  const int64_t* seg_off;      // S+1 entries
-  const int64_t* tile_prefix;  // P+1 entries, P = ceil(S/2)
-  int nseg;
+  const int64_t* pairs;        // 3 * npairs entries
+  const int64_t* tile_prefix;  // npairs + 1 entries
   int npairs;
   int ntiles;
 };
@@ -179,6 +180,13 @@ void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const Decod
 // stats[1] += checksum. Writes the last key to *last_key.
 void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key, int has_prev,
                            Elem* last_key, unsigned long long* stats, hipStream_t s);
+
+// out[i] = sum of record hashes of FIXED10 slice runs[i] (device array of n RunDesc; out zeroed
+// here). max_nrec sizes the grid.
+void launch_slice_checksums(const RunDesc* runs, int n, int64_t max_nrec, unsigned long long* out, hipStream_t s);
+// *errors += number of i with a[i] != b[i].
+void launch_count_mismatch(const unsigned long long* a, const unsigned long long* b, int n,
+                           unsigned long long* errors, hipStream_t s);
 
 // Order-independent checksums: shared with the host (uda/hash.h).
 using ::uda::mix64;

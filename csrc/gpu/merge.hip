@@ -154,12 +154,9 @@ __device__ __forceinline__ TileGeo tile_geo(const PassDesc& pd, int t) {
   }
   TileGeo g;
   g.pair = lo;
-  const int sa = 2 * lo;
-  const int sb = (sa + 1 < pd.nseg) ? sa + 1 : pd.nseg;
-  const int se = (sa + 2 < pd.nseg) ? sa + 2 : pd.nseg;
-  g.a0 = pd.seg_off[sa];
-  g.a_len = pd.seg_off[sb] - g.a0;
-  g.b_len = pd.seg_off[se] - pd.seg_off[sb];
+  g.a0 = pd.pairs[3 * lo];
+  g.a_len = pd.pairs[3 * lo + 1] - g.a0;
+  g.b_len = pd.pairs[3 * lo + 2] - pd.pairs[3 * lo + 1];
   g.d0 = (int64_t)(t - pd.tile_prefix[lo]) * kMergeTile;
   return g;
 }
@@ -310,6 +307,28 @@ __global__ void __launch_bounds__(256) validate_fixed_kernel(const uint8_t* recs
   }
 }
 
+// Sum of record hashes of every FIXED10 slice (exchange verification): grid.y = slice.
+__global__ void __launch_bounds__(256) slice_checksum_kernel(const RunDesc* runs, unsigned long long* out) {
+  const RunDesc r = runs[blockIdx.y];
+  unsigned long long h = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.nrec; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(r.base + i * kTeraRecordBytes);
+    uint64_t hh = 0x9E3779B97F4A7C15ULL ^ (uint64_t)kTeraRecordBytes;
+#pragma unroll
+    for (int j = 0; j < 13; ++j) hh = mix64(hh ^ w[j]);
+    h += hh;
+  }
+  h = wave_sum_u64(h);
+  if ((threadIdx.x & 63) == 0 && h) atomicAdd(out + blockIdx.y, h);
+}
+
+__global__ void __launch_bounds__(256) count_mismatch_kernel(const unsigned long long* a,
+                                                             const unsigned long long* b, int n,
+                                                             unsigned long long* errors) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && a[i] != b[i]) atomicAdd(errors, 1ull);
+}
+
 }  // namespace
 
 void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nruns, int64_t total,
@@ -361,5 +380,24 @@ void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key,
                      recs, n, prev_key, has_prev, last_key, stats);
 }
 
+}  // namespace gpu
+}  // namespace uda
+
+namespace uda {
+namespace gpu {
+void launch_slice_checksums(const RunDesc* runs, int n, int64_t max_nrec, unsigned long long* out, hipStream_t s) {
+  if (n <= 0) return;
+  (void)hipMemsetAsync(out, 0, sizeof(unsigned long long) * (size_t)n, s);
+  int64_t bx = (max_nrec + 4095) / 4096;
+  if (bx < 1) bx = 1;
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(slice_checksum_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, s, runs, out);
+}
+
+void launch_count_mismatch(const unsigned long long* a, const unsigned long long* b, int n,
+                           unsigned long long* errors, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(count_mismatch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, b, n, errors);
+}
 }  // namespace gpu
 }  // namespace uda

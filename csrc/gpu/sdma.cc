@@ -1,0 +1,262 @@
+// Explicit SDMA delivery copies and NUMA-local pinned memory. See sdma.h.
+#include "sdma.h"
+
+#include <hip/hip_runtime.h>
+#include <sched.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+#include "uda/log.h"
+
+namespace uda {
+namespace gpu {
+
+namespace {
+void hsa_check(hsa_status_t s, const char* what) {
+  if (s != HSA_STATUS_SUCCESS) {
+    const char* msg = nullptr;
+    hsa_status_string(s, &msg);
+    throw std::runtime_error(std::string("HSA error in ") + what + ": " + (msg ? msg : "?"));
+  }
+}
+
+struct PciAddr {
+  unsigned domain = 0, bus = 0, dev = 0, func = 0;
+  bool ok = false;
+};
+
+PciAddr hip_pci(int device) {
+  PciAddr a;
+  char buf[64] = {0};
+  if (hipDeviceGetPCIBusId(buf, sizeof(buf), device) != hipSuccess) return a;
+  if (std::sscanf(buf, "%x:%x:%x.%x", &a.domain, &a.bus, &a.dev, &a.func) == 4) a.ok = true;
+  return a;
+}
+
+struct AgentScan {
+  PciAddr want;
+  std::vector<hsa_agent_t> gpus, cpus;
+  hsa_agent_t match{};
+  bool found = false;
+};
+
+hsa_status_t scan_agent(hsa_agent_t agent, void* data) {
+  auto* sc = static_cast<AgentScan*>(data);
+  hsa_device_type_t type;
+  if (hsa_agent_get_info(agent, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (type == HSA_DEVICE_TYPE_CPU) {
+    sc->cpus.push_back(agent);
+  } else if (type == HSA_DEVICE_TYPE_GPU) {
+    sc->gpus.push_back(agent);
+    uint32_t bdf = 0, domain = 0;
+    if (sc->want.ok &&
+        hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS) {
+      (void)hsa_agent_get_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &domain);
+      const uint32_t want = (sc->want.bus << 8) | (sc->want.dev << 3) | sc->want.func;
+      if (bdf == want && domain == sc->want.domain && !sc->found) {
+        sc->match = agent;
+        sc->found = true;
+      }
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+struct PoolScan {
+  hsa_amd_memory_pool_t coarse{}, fine{};
+  bool has_coarse = false, has_fine = false;
+};
+
+hsa_status_t scan_pool(hsa_amd_memory_pool_t pool, void* data) {
+  auto* ps = static_cast<PoolScan*>(data);
+  hsa_amd_segment_t seg;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  bool alloc_ok = false;
+  (void)hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc_ok);
+  if (!alloc_ok) return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  (void)hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && !ps->has_coarse) {
+    ps->coarse = pool;
+    ps->has_coarse = true;
+  } else if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) &&
+             !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) && !ps->has_fine) {
+    ps->fine = pool;
+    ps->has_fine = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+std::string read_line(const std::string& path) {
+  std::ifstream f(path);
+  std::string s;
+  if (f) std::getline(f, s);
+  return s;
+}
+}  // namespace
+
+int device_numa_node(int device) {
+  const PciAddr a = hip_pci(device);
+  if (!a.ok) return -1;
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/bus/pci/devices/%04x:%02x:%02x.%x/numa_node", a.domain, a.bus, a.dev,
+                a.func);
+  const std::string s = read_line(path);
+  if (s.empty()) return -1;
+  return std::atoi(s.c_str());
+}
+
+void bind_thread_to_numa(int node) {
+  if (node < 0) return;
+  const std::string list = read_line("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  if (list.empty()) return;
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+  std::stringstream ss(list);
+  std::string tok;
+  int n = 0;
+  while (std::getline(ss, tok, ',')) {
+    int lo = 0, hi = 0;
+    if (std::sscanf(tok.c_str(), "%d-%d", &lo, &hi) != 2) hi = lo = std::atoi(tok.c_str());
+    for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) {
+        CPU_SET(c, &want);
+        ++n;
+      }
+  }
+  if (n > 0) (void)sched_setaffinity(0, sizeof(want), &want);
+}
+
+SdmaEngine::SdmaEngine(int device) {
+  hsa_check(hsa_init(), "hsa_init");  // reference counted: HIP already initialised the runtime
+  hsa_inited_ = true;
+  AgentScan sc;
+  sc.want = hip_pci(device);
+  hsa_check(hsa_iterate_agents(scan_agent, &sc), "hsa_iterate_agents");
+  if (!sc.found) {
+    if (sc.gpus.size() == 1) {
+      sc.match = sc.gpus[0];
+    } else {
+      throw std::runtime_error("SdmaEngine: no HSA GPU agent matches HIP device " + std::to_string(device));
+    }
+  }
+  gpu_ = sc.match;
+  if (sc.cpus.empty()) throw std::runtime_error("SdmaEngine: no HSA CPU agent");
+  hsa_agent_t near{};
+  if (hsa_agent_get_info(gpu_, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NEAREST_CPU, &near) == HSA_STATUS_SUCCESS &&
+      near.handle != 0)
+    cpu_ = near;
+  else
+    cpu_ = sc.cpus[0];
+  PoolScan ps;
+  hsa_check(hsa_amd_agent_iterate_memory_pools(cpu_, scan_pool, &ps), "iterate host pools");
+  if (ps.has_coarse)
+    host_pool_ = ps.coarse;
+  else if (ps.has_fine)
+    host_pool_ = ps.fine;
+  else
+    throw std::runtime_error("SdmaEngine: no allocatable host memory pool on the nearest CPU agent");
+  numa_node_ = device_numa_node(device);
+  uint32_t mask = 0, pref = 0;
+  if (hsa_amd_memory_copy_engine_status(cpu_, gpu_, &mask) != HSA_STATUS_SUCCESS) mask = 0;
+  if (hsa_amd_memory_get_preferred_copy_engine(cpu_, gpu_, &pref) != HSA_STATUS_SUCCESS) pref = 0;
+  const uint32_t use = (pref & mask) ? (pref & mask) : mask;
+  for (int b = 0; b < 16; ++b)
+    if (use & (1u << b)) engine_ids_.push_back(1u << b);
+  UDA_LOG(kInfo, "SDMA delivery: device %d numa %d engines mask 0x%x preferred 0x%x", device, numa_node_, mask, pref);
+}
+
+SdmaEngine::~SdmaEngine() {
+  if (hsa_inited_) (void)hsa_shut_down();
+}
+
+void* SdmaEngine::alloc_host(size_t bytes) {
+  void* p = nullptr;
+  hsa_check(hsa_amd_memory_pool_allocate(host_pool_, bytes, 0, &p), "host pool allocate");
+  hsa_status_t s = hsa_amd_agents_allow_access(1, &gpu_, nullptr, p);
+  if (s != HSA_STATUS_SUCCESS) {
+    (void)hsa_amd_memory_pool_free(p);
+    hsa_check(s, "agents_allow_access");
+  }
+  return p;
+}
+
+void SdmaEngine::free_host(void* p) {
+  if (p) (void)hsa_amd_memory_pool_free(p);
+}
+
+hsa_signal_t SdmaEngine::make_signal() {
+  hsa_signal_t s;
+  hsa_check(hsa_signal_create(0, 0, nullptr, &s), "signal_create");
+  return s;
+}
+
+void SdmaEngine::destroy_signal(hsa_signal_t s) {
+  if (s.handle) (void)hsa_signal_destroy(s);
+}
+
+void SdmaEngine::arm(hsa_signal_t s, int64_t parts) { hsa_signal_store_screlease(s, parts); }
+
+void SdmaEngine::wait(hsa_signal_t s) {
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  if (v < 0) throw std::runtime_error("SDMA copy reported an error (completion signal < 0)");
+}
+
+int SdmaEngine::parts(size_t bytes, int ways) const {
+  if (bytes == 0) return 0;
+  if (ways < 1) ways = 1;
+  const size_t min_part = (size_t)8 << 20;  // smaller parts do not pay for an extra engine
+  int n = (int)std::min<size_t>((size_t)ways, (bytes + min_part - 1) / min_part);
+  return n < 1 ? 1 : n;
+}
+
+int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways) {
+  const int n = parts(bytes, ways);
+  if (n == 0) return 0;
+  size_t per = (bytes + n - 1) / n;
+  per = (per + 4095) & ~(size_t)4095;
+  size_t off = 0;
+  int issued = 0;
+  for (int k = 0; k < n && off < bytes; ++k) {
+    const size_t len = std::min(per, bytes - off);
+    void* d = static_cast<uint8_t*>(dst_host) + off;
+    const void* s = static_cast<const uint8_t*>(src_dev) + off;
+    hsa_status_t st = HSA_STATUS_ERROR;
+    if (!engine_ids_.empty()) {
+      const uint32_t eng = engine_ids_[(size_t)next_engine_ % engine_ids_.size()];
+      next_engine_ = (next_engine_ + 1) % (int)engine_ids_.size();
+      st = hsa_amd_memory_async_copy_on_engine(d, cpu_, s, gpu_, len, 0, nullptr, sig,
+                                               (hsa_amd_sdma_engine_id_t)eng, false);
+    }
+    if (st != HSA_STATUS_SUCCESS) st = hsa_amd_memory_async_copy(d, cpu_, s, gpu_, len, 0, nullptr, sig);
+    hsa_check(st, "memory_async_copy (D2H)");
+    off += len;
+    ++issued;
+  }
+  // parts() may overestimate when the aligned split leaves a part empty: release the surplus
+  for (int k = issued; k < n; ++k) hsa_signal_subtract_screlease(sig, 1);
+  return n;
+}
+
+std::string SdmaEngine::describe() const {
+  std::string e;
+  for (auto id : engine_ids_) {
+    if (!e.empty()) e += ",";
+    int b = 0;
+    while (b < 16 && !(id & (1u << b))) ++b;
+    e += std::to_string(b);
+  }
+  return "sdma[numa=" + std::to_string(numa_node_) + " engines=" + (e.empty() ? "auto" : e) + "]";
+}
+
+}  // namespace gpu
+}  // namespace uda

@@ -16,6 +16,7 @@
 #include "device_engine.h"
 #include "exchange.h"
 #include "generic_merger.h"
+#include "j2c_sink.h"
 #include "uda/aio.h"
 #include "uda/codec.h"
 #include "uda/datagen.h"
@@ -36,10 +37,10 @@ namespace {
 py::dict stats_to_dict(const gpu::StepStats& s) {
   py::dict d;
   d["wall_ms"] = s.wall_ms;
-  d["split_ms"] = s.split_ms;
   d["comm_ms"] = s.comm_ms;
   d["merge_ms"] = s.merge_ms;
   d["d2h_ms"] = s.d2h_ms;
+  d["wait_out_ms"] = s.wait_out_ms;
   d["bytes_in"] = s.bytes_in;
   d["records"] = s.records;
   d["bytes_sent"] = s.bytes_sent;
@@ -48,6 +49,8 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   d["merge_passes"] = s.merge_passes;
   d["order_errors"] = s.order_errors;
   d["checksum"] = s.checksum;
+  d["exchange_errors"] = s.exchange_errors;
+  d["validated"] = s.validated;
   d["bad_layout"] = s.bad_layout;
   return d;
 }
@@ -63,25 +66,19 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("maps_per_rank", c.maps_per_rank);
   get("records_per_map", c.records_per_map);
   get("rounds", c.rounds);
+  get("reducers", c.reducers);
   get("seed", c.seed);
   get("kv_buf_bytes", c.kv_buf_bytes);
   get("d2h_piece_bytes", c.d2h_piece_bytes);
   get("pinned_slots", c.pinned_slots);
-  get("d2h_streams", c.d2h_streams);
+  get("d2h_engines", c.d2h_engines);
+  get("d2h", c.d2h);
   get("deliver_host", c.deliver_host);
   get("validate", c.validate);
   get("local_group", c.local_group);
   get("store", c.store);
   return c;
 }
-
-// Native sink that counts bytes and buffers (the bench's reducer stand-in: it receives the
-// merged stream zero-copy, as J2CQueue would after its memcpy).
-struct CountingSink {
-  std::atomic<int64_t> bytes{0};
-  std::atomic<int64_t> buffers{0};
-  std::atomic<int64_t> max_len{0};
-};
 
 // Python host for the C ABI (the "fake JVM"): Python callables stand in for the UdaBridge.java
 // static callbacks. Native threads take the GIL for each callback; bridge entry points release it.
@@ -676,16 +673,15 @@ PYBIND11_MODULE(_uda_native, m) {
     return std::string(ex->name()) + (send == recv ? ":ok" : ":mismatch");
   }, py::arg("device") = 0, py::arg("n") = 4096);
 
-  py::class_<CountingSink, std::shared_ptr<CountingSink>>(m, "CountingSink")
-      .def(py::init<>())
-      .def_property_readonly("bytes", [](CountingSink& s) { return s.bytes.load(); })
-      .def_property_readonly("buffers", [](CountingSink& s) { return s.buffers.load(); })
-      .def_property_readonly("max_len", [](CountingSink& s) { return s.max_len.load(); })
-      .def("reset", [](CountingSink& s) {
-        s.bytes = 0;
-        s.buffers = 0;
-        s.max_len = 0;
-      });
+  py::class_<gpu::J2CSink, std::shared_ptr<gpu::J2CSink>>(m, "J2CSink")
+      .def(py::init<int, int64_t>(), py::arg("reducers"), py::arg("kv_buf_bytes") = 1 << 20)
+      .def_property_readonly("reducers", &gpu::J2CSink::reducers)
+      .def("records", &gpu::J2CSink::records)
+      .def("bytes", &gpu::J2CSink::bytes)
+      .def("buffers", &gpu::J2CSink::buffers)
+      .def("eof", &gpu::J2CSink::eof)
+      .def("error", &gpu::J2CSink::error)
+      .def("reset", &gpu::J2CSink::reset);
 
   py::class_<gpu::ShuffleJob>(m, "ShuffleJob")
       .def(py::init([](const py::dict& cfg) { return new gpu::ShuffleJob(config_from_dict(cfg)); }))
@@ -710,36 +706,42 @@ PYBIND11_MODULE(_uda_native, m) {
              j.set_bounds(v);
            })
       .def("plan", &gpu::ShuffleJob::plan, py::call_guard<py::gil_scoped_release>())
-      .def("set_counting_sink",
-           [](gpu::ShuffleJob& j, std::shared_ptr<CountingSink> s) {
-             j.set_sink([s](const uint8_t*, int64_t len) {
-               s->bytes += len;
-               s->buffers += 1;
-               int64_t cur = s->max_len.load();
-               while (len > cur && !s->max_len.compare_exchange_weak(cur, len)) {
-               }
-               return 0;
-             });
+      .def("set_j2c_sink",
+           [](gpu::ShuffleJob& j, std::shared_ptr<gpu::J2CSink> s) {
+             if (s->reducers() != j.config().reducers) throw py::value_error("J2CSink reducer count mismatch");
+             j.set_sink([s](int r, const uint8_t* buf, int64_t len) { return s->consume(r, buf, len); });
            })
       .def("set_python_sink",
-           [](gpu::ShuffleJob& j, py::function fn) {
+           [](gpu::ShuffleJob& j, py::function fn, bool with_reducer) {
              auto holder = std::make_shared<py::function>(fn);
-             j.set_sink([holder](const uint8_t* buf, int64_t len) {
+             j.set_sink([holder, with_reducer](int r, const uint8_t* buf, int64_t len) {
                py::gil_scoped_acquire g;
-               py::object r = (*holder)(py::bytes(reinterpret_cast<const char*>(buf), (size_t)len));
-               return r.is_none() ? 0 : r.cast<int>();
+               try {
+                 py::bytes b(reinterpret_cast<const char*>(buf), (size_t)len);
+                 py::object res = with_reducer ? (*holder)(r, b) : (*holder)(b);
+                 return res.is_none() ? 0 : res.cast<int>();
+               } catch (py::error_already_set& e) {
+                 e.discard_as_unraisable("ShuffleJob python sink");
+                 return -1;
+               }
              });
-           })
+           },
+           py::arg("fn"), py::arg("with_reducer") = false)
       .def("clear_sink", [](gpu::ShuffleJob& j) { j.set_sink(nullptr); })
       .def("run_step",
-           [](gpu::ShuffleJob& j) {
-             gpu::StepStats s;
+           [](gpu::ShuffleJob& j, bool validate) {
+             gpu::StepStats st;
              {
                py::gil_scoped_release r;
-               s = j.run_step();
+               st = j.run_step(validate);
              }
-             return stats_to_dict(s);
-           })
+             return stats_to_dict(st);
+           },
+           py::arg("validate") = false)
+      .def("reducer_records", &gpu::ShuffleJob::reducer_records)
+      .def_property_readonly("comm_ranks", &gpu::ShuffleJob::comm_ranks)
+      .def_property_readonly("exchange_name", &gpu::ShuffleJob::exchange_name)
+      .def_property_readonly("delivery_name", &gpu::ShuffleJob::delivery_name)
       .def("local_dest_checksums", &gpu::ShuffleJob::local_dest_checksums)
       .def("local_dest_records", &gpu::ShuffleJob::local_dest_records)
       .def("index_record", &gpu::ShuffleJob::index_record)

@@ -149,3 +149,31 @@ def test_tcp_unreachable_provider_fails_once():
         c.wait(60)
     c.close()
     assert c.failure_calls == 1
+
+
+def test_bench_self_launches_one_process_per_gpu():
+    """`python bench.py --gpus N` without torchrun starts N rank processes itself."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--launch-selftest"],
+                         capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    ranks = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    assert sorted(int(r["RANK"]) for r in ranks) == [0, 1, 2]
+    assert {r["WORLD_SIZE"] for r in ranks} == {"3"}
+    assert {r["MASTER_ADDR"] for r in ranks} == {"127.0.0.1"}
+    assert len({r["MASTER_PORT"] for r in ranks}) == 1
+    assert all(r["LOCAL_RANK"] == r["RANK"] for r in ranks)
+
+
+def test_bench_refuses_world_mismatch():
+    """A launcher that started a different number of ranks than --gpus asks for is an error."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 2
+    assert "launcher started 1 rank" in out.stderr

@@ -1,7 +1,7 @@
-"""GPU end-to-end: TeraSort shuffle+merge on one MI355X (HIP kernels F2/F3/F4 + D2H delivery).
+"""GPU end-to-end: TeraSort shuffle+merge on one MI355X (HIP kernels F2/F3/F4 + SDMA delivery).
 
-Numerics oracle: the delivered stream is decoded by a J2CQueue-equivalent reader and compared to
-a plain Python sort of all generated records (read back from the HBM partition store).
+Numerics oracle: the delivered stream of every reducer is decoded by a J2CQueue-equivalent reader
+and compared to a plain Python sort of all generated records (read back from the partition store).
 """
 import pytest
 
@@ -24,38 +24,61 @@ def _text_content(key: bytes) -> bytes:
     return key[1:]  # Text VInt(10) prefix
 
 
-@pytest.mark.parametrize("maps,rounds", [(1, 1), (3, 2), (8, 4), (33, 3)])
-def test_terasort_stream_matches_python_sort(require_gpu, native, maps, rounds):
+def _sorted_all(parts):
+    recs = []
+    for p in parts:
+        recs += decode_stream(p)
+    return sorted(recs, key=lambda kv: _text_content(kv[0]))
+
+
+SMALL = dict(kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
+
+
+@pytest.mark.parametrize("maps,rounds,reducers", [(1, 1, 1), (3, 2, 1), (8, 4, 1), (33, 3, 1), (5, 3, 4), (4, 1, 3)])
+def test_terasort_stream_matches_python_sort(require_gpu, native, maps, rounds, reducers):
     rows = 20000 * maps
-    j = _job(rows, maps, rounds, kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
-    reader = J2CQueueReader(max_len=64 << 10)
-    j.job.set_python_sink(lambda b: reader.feed(b))
+    j = _job(rows, maps, rounds, reducers=reducers, **SMALL)
+    readers = [J2CQueueReader(max_len=64 << 10) for _ in range(reducers)]
+    j.use_python_sink(lambda r, b: readers[r].feed(b), with_reducer=True)
     st = j.step()
     j.check(st)
-    assert reader.eof
-    # oracle: every generated record, sorted by key (stable on map order)
-    recs = []
-    for m in range(maps):
-        recs += decode_stream(j.job.read_partition(m, 0))
-    expect = sorted(recs, key=lambda kv: _text_content(kv[0]))
-    assert len(reader.records) == len(expect) == st["records"]
-    assert reader.records == expect
+    assert all(r.eof for r in readers)
+    # oracle: every generated record, sorted by key; reducer outputs concatenate to the total order
+    expect = _sorted_all(j.job.read_partition(m, 0) for m in range(maps))
+    got = [kv for r in readers for kv in r.records]
+    assert len(got) == len(expect) == st["records"]
+    assert got == expect
+    assert [len(r.records) for r in readers] == list(j.job.reducer_records())
     assert st["order_errors"] == 0
     assert st["checksum"] == j.expected_checksum
 
 
-def test_terasort_repeat_steps_and_device_only(require_gpu):
-    j = _job(100000, 5, 3)
+def test_terasort_repeat_steps_j2c_sink_and_device_only(require_gpu):
+    j = _job(100000, 5, 3, reducers=2)
     a = j.step()
     b = j.step()
-    j.check(a)
+    j.check(a)  # includes the native J2C consumer's record counts, framing and EOF per reducer
     j.check(b)
     assert a["checksum"] == b["checksum"] == j.expected_checksum
+    assert sum(a["consumer_records"]) == a["records"]
     assert a["buffers"] >= a["bytes_in"] // (1 << 20)
+    c = j.step(validate=False)
+    j.check(c)
+    assert not c["validated"]
     d = _job(100000, 5, 3, deliver_host=False)
     s = d.step()
     d.check(s)
     assert s["buffers"] == 0
+
+
+@pytest.mark.parametrize("mode", ["sdma", "hip"])
+def test_delivery_modes(require_gpu, mode):
+    """Both delivery copy paths (explicit SDMA engines / hipMemcpyAsync) deliver the same stream."""
+    j = _job(60000, 3, 2, reducers=2, d2h=mode, d2h_engines=2, **SMALL)
+    st = j.step()
+    j.check(st)
+    name = j.job.delivery_name
+    assert name.startswith("sdma") if mode == "sdma" else name == "hip"
 
 
 def test_merge_tree_many_runs(require_gpu):
@@ -66,64 +89,67 @@ def test_merge_tree_many_runs(require_gpu):
     assert st["merge_passes"] == 9
 
 
-@pytest.mark.parametrize("world,maps,rounds", [
-    (2, 3, 3), (3, 2, 4), (4, 1, 1),
-    # Known intermittent checksum mismatch (records and order correct) in the 8-thread local-group
-    # rehearsal; see docs/BENCHMARKS.md "Known issue". Not the RCCL path bench.py uses.
-    pytest.param(8, 2, 16, marks=pytest.mark.xfail(strict=False, reason="intermittent local-group checksum race")),
+@pytest.mark.parametrize("world,maps,rounds,reducers", [
+    (2, 3, 3, 1), (3, 2, 4, 1), (4, 1, 1, 1), (8, 2, 16, 1), (4, 3, 4, 3), (8, 2, 4, 2),
 ])
-def test_multirank_schedule_local_group(require_gpu, world, maps, rounds):
-    """The multi-GPU shuffle schedule (pack -> all-to-all-v rounds -> merge -> deliver) rehearsed
-    with `world` ranks sharing one GPU; every reducer must receive exactly its key range."""
-    from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
-    cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, validate=True,
-                         sample_every=64, kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
-    jobs, ck, rec = make_local_group(world, cfg, group=f"t{world}{maps}{rounds}")
-    readers = [J2CQueueReader(max_len=64 << 10) for _ in range(world)]
-    for j, r in zip(jobs, readers):
-        j.set_python_sink(r.feed)
+def test_multirank_schedule_local_group(require_gpu, world, maps, rounds, reducers):
+    """The multi-GPU shuffle schedule (cell split -> all-to-all-v rounds -> grouped merge ->
+    deliver) rehearsed with `world` ranks sharing one GPU; every reducer must receive exactly its
+    key range, and every received slice must hash to what its sender computed."""
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, reducers=reducers,
+                         validate=True, sample_every=64, **SMALL)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"t{world}{maps}{rounds}{reducers}")
+    readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(reducers)] for _ in range(world)]
+
+    def attach(d):
+        jobs[d].set_python_sink(lambda r, b: readers[d][r].feed(b), True)
+
+    for d in range(world):
+        attach(d)
     for step in range(2):
-        stats = run_collective(jobs, lambda j: j.run_step())
+        stats = run_collective(jobs, lambda j: j.run_step(True))
         for d, st in enumerate(stats):
-            assert st["records"] == rec[d]
-            assert st["order_errors"] == 0
-            assert st["checksum"] == ck[d]
+            check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+            assert st["exchange_errors"] == 0
             if world > 1:
                 assert st["bytes_sent"] > 0
         if step == 0:
             for d in range(world):
-                recs = []
-                for j in jobs:  # global map order = (rank, local map)
-                    for m in range(maps):
-                        recs += decode_stream(j.read_partition(m, d))
-                expect = sorted(recs, key=lambda kv: _text_content(kv[0]))
-                assert readers[d].records == expect
-                readers[d] = J2CQueueReader(max_len=64 << 10)
-                jobs[d].set_python_sink(readers[d].feed)
+                expect = _sorted_all(j.read_partition(m, d) for j in jobs for m in range(maps))
+                got = [kv for r in readers[d] for kv in r.records]
+                assert got == expect
+                readers[d] = [J2CQueueReader(max_len=64 << 10) for _ in range(reducers)]
+                attach(d)
 
 
 @pytest.mark.parametrize("world", [1, 2])
 def test_host_dram_spill_tier(require_gpu, world):
     """Map outputs in pinned host DRAM (jobs larger than HBM): rounds stream H2D, then merge."""
-    from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
-    cfg = TeraSortConfig(rows_per_gpu=40000, maps_per_rank=4, rounds=3, validate=True, sample_every=64,
-                         kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10, store="host")
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    cfg = TeraSortConfig(rows_per_gpu=40000, maps_per_rank=4, rounds=3, reducers=2, validate=True, sample_every=64,
+                         store="host", **SMALL)
     if world == 1:
-        j = _job(40000, 4, 3, store="host", kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
-        reader = J2CQueueReader(max_len=64 << 10)
-        j.job.set_python_sink(reader.feed)
+        j = _job(40000, 4, 3, store="host", reducers=2, **SMALL)
+        readers = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
+        j.use_python_sink(lambda r, b: readers[r].feed(b), with_reducer=True)
         st = j.step()
         j.check(st)
         assert st["bytes_h2d"] == st["bytes_in"]
-        recs = []
-        for m in range(4):
-            recs += decode_stream(j.job.read_partition(m, 0))
-        assert reader.records == sorted(recs, key=lambda kv: _text_content(kv[0]))
+        got = [kv for r in readers for kv in r.records]
+        assert got == _sorted_all(j.job.read_partition(m, 0) for m in range(4))
     else:
         jobs, ck, rec = make_local_group(world, cfg, group="spill2")
-        stats = run_collective(jobs, lambda j: j.run_step())
+        sinks = []
+        for j in jobs:
+            from uda_amd import native
+            s = native().J2CSink(2, cfg.kv_buf_bytes)
+            j.set_j2c_sink(s)
+            sinks.append(s)
+        stats = run_collective(jobs, lambda j: j.run_step(True))
         for d, st in enumerate(stats):
-            assert st["records"] == rec[d] and st["order_errors"] == 0 and st["checksum"] == ck[d]
+            check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+            assert [sinks[d].records(i) for i in range(2)] == list(jobs[d].reducer_records())
             assert st["bytes_h2d"] > 0
 
 

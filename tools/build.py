@@ -83,7 +83,7 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
         f"rule cxxpy\n  command = $hipcc $cflags $pyflags -MD -MF $out.d -c $in -o $out\n"
         f"  depfile = $out.d\n  deps = gcc\n  description = CXX(py) $in",
         f"rule solib\n  command = $hipcc -shared -fPIC --offload-arch={ARCH}{host_san} $in -o $out "
-        f"-L{ROCM}/lib -lrccl -lamdhip64 -lpthread -ldl -Wl,-rpath,{ROCM}/lib -Wl,-soname,libuda.so\n"
+        f"-L{ROCM}/lib -lrccl -lamdhip64 -lhsa-runtime64 -lpthread -ldl -Wl,-rpath,{ROCM}/lib -Wl,-soname,libuda.so\n"
         f"  description = LINK $out",
         f"rule pymod\n  command = $hipcc -shared -fPIC{host_san} $in -o $out -L{os.path.dirname(lib_out)} "
         f"-luda -Wl,-rpath,'$$ORIGIN/lib' -L{ROCM}/lib -lamdhip64\n  description = LINK $out",

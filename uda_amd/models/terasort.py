@@ -6,10 +6,15 @@ the Java reducer through `dataFromUda` in 1 MiB buffers.
 
 Here (one process per GPU, W GPUs):
   * each GPU holds `maps_per_rank` TeraSort MOFs in HBM (the MOFSupplier's store),
-  * reducer d = GPU d; its partition is shipped in key-range rounds by an RCCL all-to-all,
-  * each round is merged on the GPU (F2 keys -> F3 merge tree -> F4 gather),
-  * merged records go D2H into a pinned ring and are handed to the host sink as whole-record
-    buffers of <= 1 MiB, the last one carrying the IFile EOF marker.
+  * each GPU hosts `reducers` reduce tasks; reducer i of GPU d owns the i-th contiguous slice of
+    GPU d's key range (total order: concatenated reducer outputs are globally sorted),
+  * every reducer range is cut into `rounds` cells; round q ships cell q of every reducer with an
+    RCCL all-to-all over xGMI and merges it on the GPU (F2 keys -> F3 merge tree -> F4 gather,
+    one merge group per reducer),
+  * merged records go device -> host on the SDMA engines into a NUMA-local pinned ring and each
+    reducer's consumer thread receives whole-record buffers of <= 1 MiB, the last one carrying the
+    IFile EOF marker. The native J2C sink does what the Java side does with every buffer: copy it
+    into a 1 MiB KVBuf and walk the records by their VInt lengths (UdaPlugin.java:369-402,498-538).
 Data is synthetic and TeraGen-shaped (10-byte keys, 90-byte values, 104-byte IFile records).
 """
 from __future__ import annotations
@@ -34,9 +39,11 @@ class TeraSortConfig:
     rounds: int = 16
     seed: int = 0x5EED
     kv_buf_bytes: int = 1 << 20         # J2CQueue kv_buf_size (UdaPlugin.java:168)
-    d2h_piece_bytes: int = 64 << 20
-    pinned_slots: int = 6
-    d2h_streams: int = 1
+    reducers: int = 1                   # reduce tasks per GPU
+    d2h_piece_bytes: int = 128 << 20
+    pinned_slots: int = 16
+    d2h_engines: int = 2
+    d2h: str = "sdma"                   # "sdma" (explicit copy engines) or "hip" (hipMemcpyAsync)
     deliver_host: bool = True
     validate: bool = False
     sample_every: int = 4096
@@ -54,11 +61,11 @@ class TeraSortShuffle:
         self.job = n.ShuffleJob(dict(
             device=self.device, rank=ctx.rank, world=ctx.world,
             maps_per_rank=cfg.maps_per_rank, records_per_map=records_per_map,
-            rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
+            rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
             d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
-            d2h_streams=cfg.d2h_streams, deliver_host=cfg.deliver_host, validate=cfg.validate,
-            store=cfg.store))
-        self.sink = n.CountingSink()
+            d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host,
+            validate=cfg.validate, store=cfg.store))
+        self.sink = n.J2CSink(cfg.reducers, cfg.kv_buf_bytes)
         self.expected_checksum = None
         self.expected_records = None
         self.setup_s = {}
@@ -80,7 +87,7 @@ class TeraSortShuffle:
         for d in range(self.ctx.world):
             parts = [g[d] for g in gathered if g[d].size]
             per_dest.append(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64))
-        bounds = round_bounds(per_dest, self.cfg.rounds)
+        bounds = round_bounds(per_dest, self.cfg.rounds * self.cfg.reducers)
         self.job.set_bounds(np.ascontiguousarray(bounds.reshape(-1)))
         self.job.plan()
         t3 = time.perf_counter()
@@ -89,38 +96,65 @@ class TeraSortShuffle:
         rec = self.ctx.sum_u64(self.job.local_dest_records())
         self.expected_checksum = ck[self.ctx.rank]
         self.expected_records = rec[self.ctx.rank]
-        self.job.set_counting_sink(self.sink)
+        self.job.set_j2c_sink(self.sink)
         self.setup_s = dict(comm_init=t1 - t0, generate=t2 - t1, plan=t3 - t2)
 
-    def step(self) -> dict:
-        return self.job.run_step()
+    def step(self, validate: bool | None = None) -> dict:
+        """One shuffle+merge+deliver pass. Every step checks what the consumers parsed (records per
+        reducer, framing, EOF); validate=True also runs the device order/checksum/exchange checks."""
+        if self.sink is not None and self.cfg.deliver_host:
+            self.sink.reset()
+        st = self.job.run_step(self.cfg.validate if validate is None else validate)
+        if self.sink is not None and self.cfg.deliver_host:
+            st["consumer_records"] = [self.sink.records(i) for i in range(self.cfg.reducers)]
+            st["consumer_errors"] = [self.sink.error(i) for i in range(self.cfg.reducers)]
+            st["consumer_eof"] = [self.sink.eof(i) for i in range(self.cfg.reducers)]
+        return st
+
+    def use_python_sink(self, fn, with_reducer: bool = False) -> None:
+        """Deliver to a Python callable instead of the native J2C sink (tests)."""
+        self.sink = None
+        self.job.set_python_sink(fn, with_reducer)
 
     def check(self, stats: dict) -> None:
-        """Raise if a validated step lost, duplicated, corrupted or mis-ordered records."""
-        if stats["records"] != self.expected_records:
-            raise AssertionError(f"records {stats['records']} != expected {self.expected_records}")
-        if stats["bad_layout"]:
-            raise AssertionError("non-TeraSort record layout seen by the merge")
-        if self.cfg.validate:
-            if stats["order_errors"] != 0:
-                raise AssertionError(f"{stats['order_errors']} out-of-order records")
-            if stats["checksum"] != self.expected_checksum:
-                raise AssertionError("checksum mismatch")
+        """Raise if a step lost, duplicated, corrupted or mis-ordered records."""
+        check_stats(stats, self.expected_records, self.expected_checksum, self.job.reducer_records())
+
+
+def check_stats(stats: dict, expected_records: int, expected_checksum: int, reducer_records) -> None:
+    if stats["records"] != expected_records:
+        raise AssertionError(f"records {stats['records']} != expected {expected_records}")
+    if stats["bad_layout"]:
+        raise AssertionError("non-TeraSort record layout seen by the merge")
+    if "consumer_records" in stats:
+        if list(stats["consumer_records"]) != list(reducer_records):
+            raise AssertionError(f"consumers parsed {stats['consumer_records']} records, expected {reducer_records}")
+        if any(stats["consumer_errors"]):
+            raise AssertionError(f"consumer framing errors {stats['consumer_errors']}")
+        if not all(stats["consumer_eof"]):
+            raise AssertionError("a reducer did not receive its EOF marker")
+    if stats["validated"]:
+        if stats["order_errors"] != 0:
+            raise AssertionError(f"{stats['order_errors']} out-of-order records")
+        if stats["exchange_errors"] != 0:
+            raise AssertionError(f"{stats['exchange_errors']} received slices differ from what their sender sent")
+        if stats["checksum"] != expected_checksum:
+            raise AssertionError("checksum mismatch")
 
 
 def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: str = "local"):
     """Single-process rehearsal of a `world`-rank shuffle: every rank is a ShuffleJob on `device`
     driven from its own thread, exchanging rounds through device memcpys with the same pack /
     all-to-all-v schedule as the RCCL path. Returns (jobs, expected_checksums, expected_records)."""
-    import threading
 
     n = native()
     records_per_map = max(1, cfg.rows_per_gpu // cfg.maps_per_rank)
     jobs = [n.ShuffleJob(dict(
         device=device, rank=r, world=world, maps_per_rank=cfg.maps_per_rank,
-        records_per_map=records_per_map, rounds=cfg.rounds, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
-        d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots, d2h_streams=cfg.d2h_streams,
-        deliver_host=cfg.deliver_host, validate=cfg.validate, local_group=group, store=cfg.store))
+        records_per_map=records_per_map, rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed,
+        kv_buf_bytes=cfg.kv_buf_bytes, d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
+        d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host, validate=cfg.validate,
+        local_group=group, store=cfg.store))
         for r in range(world)]
     for j in jobs:
         j.init_local()
@@ -130,7 +164,7 @@ def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: st
     for d in range(world):
         parts = [np.asarray(s[d]) for s in local if np.asarray(s[d]).size]
         per_dest.append(np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64))
-    bounds = np.ascontiguousarray(round_bounds(per_dest, cfg.rounds).reshape(-1))
+    bounds = np.ascontiguousarray(round_bounds(per_dest, cfg.rounds * cfg.reducers).reshape(-1))
     for j in jobs:
         j.set_bounds(bounds)
     run_collective(jobs, lambda j: j.plan())

@@ -1,8 +1,9 @@
 """Key-range round planning (the TeraSort range-partition sampler's role).
 
-Reducer d owns a key range; its shuffle is cut into Q rounds, round q holding the keys in
-[bound(d, q), bound(d, q+1)). Bounds are quantiles of a key sample gathered from every rank, so
-rounds carry near-equal volume even under key skew. Ties go to the upper round (lower_bound).
+GPU d owns a key range, cut into C = reducers x rounds cells: cell c holds the keys in
+[bound(d, c-1), bound(d, c)); reducer i owns cells [i*rounds, (i+1)*rounds) and round q ships cell
+i*rounds + q of every reducer. Bounds are quantiles of a key sample gathered from every rank, so
+cells carry near-equal volume even under key skew. Ties go to the upper cell (lower_bound).
 """
 from __future__ import annotations
 
@@ -24,7 +25,8 @@ def quantile_bounds(samples: np.ndarray, rounds: int) -> np.ndarray:
 
 
 def round_bounds(per_dest_samples: list[np.ndarray], rounds: int) -> np.ndarray:
-    """per_dest_samples[d]: (n_d, 2) samples for reducer d (already gathered from all ranks).
+    """per_dest_samples[d]: (n_d, 2) samples for GPU d (already gathered from all ranks);
+    `rounds` = number of cells per GPU.
 
     Returns a (world, rounds-1, 2) uint64 array."""
     out = [quantile_bounds(s, rounds) for s in per_dest_samples]
