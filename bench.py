@@ -49,10 +49,12 @@ def parse_args(argv=None):
                     help="delivery copies: explicit SDMA engines (default) or hipMemcpyAsync")
     ap.add_argument("--d2h-piece-mb", type=int, default=128)
     ap.add_argument("--pinned-slots", type=int, default=16)
-    ap.add_argument("--d2h-engines", type=int, default=2)
+    ap.add_argument("--d2h-engines", type=int, default=1)
     ap.add_argument("--device-only", action="store_true",
                     help="ablation: stop after the device merge (no host delivery); not the headline")
     ap.add_argument("--no-validate", action="store_true", help="skip the final validated step")
+    ap.add_argument("--sink", choices=("j2c", "none"), default="j2c",
+                    help="ablation: 'none' drops delivered buffers unread (measures the copy path alone)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -124,9 +126,12 @@ def main(argv=None) -> int:
     job = TeraSortShuffle(ctx, cfg)
     t_setup = time.perf_counter()
     job.setup()
+    if args.sink == "none":
+        job.drop_sink()
     t_setup = time.perf_counter() - t_setup
     if ctx.rank == 0:
-        print(f"# setup {t_setup:.1f}s {job.setup_s} store={job.job.store_bytes/1e9:.1f}GB "
+        print(f"# setup {t_setup:.1f}s cpus={len(os.sched_getaffinity(0))} {job.setup_s} "
+              f"store={job.job.store_bytes/1e9:.1f}GB "
               f"max_round_records={job.job.max_round_records} exchange={job.job.exchange_name} "
               f"delivery={job.job.delivery_name}", file=sys.stderr, flush=True)
 
@@ -191,6 +196,7 @@ def main(argv=None) -> int:
                 "rounds": args.rounds,
                 "shuffle": job.job.exchange_name if ctx.world > 1 else "local (single GPU, no all-to-all)",
                 "delivery": "device-only (ablation)" if args.device_only else
+                            f"{job.job.delivery_name} -> buffers dropped unread (ablation)" if args.sink == "none" else
                             f"{job.job.delivery_name} -> per-reducer J2C consumer (KVBuf memcpy + VInt walk), <=1MiB buffers",
             },
             "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),

@@ -317,6 +317,7 @@ ShuffleJob::~ShuffleJob() {
   for (auto e : merged_ev_) (void)hipEventDestroy(e);
   for (auto e : comm_ev_) (void)hipEventDestroy(e);
   for (auto e : piece_ev_) (void)hipEventDestroy(e);
+  if (!sdma_ && ring_) (void)hipHostFree(ring_);
   if (sdma_) {
     for (auto sg : piece_sig_) sdma_->destroy_signal(sg);
     sdma_->free_host(ring_);
@@ -344,8 +345,8 @@ void ShuffleJob::init_local() {
 
 std::string ShuffleJob::delivery_name() const {
   if (!cfg_.deliver_host) return "none";
-  if (sdma_) return sdma_->describe();
-  return cfg_.d2h;
+  if (sdma_) return sdma_->describe() + " ring=" + ring_numa_;
+  return "hip[numa=" + std::to_string(device_numa_node(cfg_.device)) + "] ring=" + ring_numa_;
 }
 
 void ShuffleJob::generate() {
@@ -680,11 +681,13 @@ void ShuffleJob::plan() {
       piece_sig_.resize(cfg_.pinned_slots);
       for (auto& sg : piece_sig_) sg = sdma_->make_signal();
     } else {
-      ring_hip_.alloc(ring_bytes);
-      ring_ = ring_hip_.as<uint8_t>();
+      ring_ = static_cast<uint8_t*>(hip_host_alloc_on_node(ring_bytes, device_numa_node(cfg_.device)));
       piece_ev_.resize(cfg_.pinned_slots);
       for (auto& e : piece_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    // first touch from this thread: the pages land where the allocation policy put them
+    for (size_t o = 0; o < ring_bytes; o += 4096) ring_[o] = 0;
+    ring_numa_ = numa_residency(ring_);
     pinned_free_.assign(cfg_.pinned_slots, true);
     items_.assign(R_, {});
     eof_bufs_.clear();

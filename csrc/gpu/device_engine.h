@@ -196,7 +196,7 @@ struct ShuffleConfig {
   int64_t kv_buf_bytes = 1 << 20;        // delivery buffer size (J2CQueue kv_buf_size)
   int64_t d2h_piece_bytes = 128ll << 20; // D2H granule (rounded down to whole buffers)
   int pinned_slots = 16;
-  int d2h_engines = 2;                   // SDMA engines a piece is split over
+  int d2h_engines = 1;                   // SDMA engines a piece is split over (if several are enabled)
   std::string d2h = "sdma";              // "sdma" (explicit copy engines) or "hip" (hipMemcpyAsync)
   bool deliver_host = true;              // false: stop after the device merge (ablation)
   bool validate = false;                 // device-side order/checksum/exchange checks every step
@@ -321,7 +321,7 @@ class ShuffleJob {
   // ---- delivery: copy thread -> pinned ring (SDMA) -> per-reducer consumer threads
   std::unique_ptr<SdmaEngine> sdma_;
   uint8_t* ring_ = nullptr;          // pinned_slots x piece_bytes_
-  PinnedBuffer ring_hip_;            // ring for the "hip" delivery mode
+  std::string ring_numa_;            // where the ring's pages live (/proc/self/numa_maps)
   std::vector<hsa_signal_t> piece_sig_;
   std::vector<hipEvent_t> piece_ev_;
   struct RoundOut {

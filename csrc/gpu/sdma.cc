@@ -3,9 +3,12 @@
 
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -135,6 +138,63 @@ void bind_thread_to_numa(int node) {
   if (n > 0) (void)sched_setaffinity(0, sizeof(want), &want);
 }
 
+void* hip_host_alloc_on_node(size_t bytes, int node) {
+  void* p = nullptr;
+  if (node < 0 || node >= 64) {
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) throw std::runtime_error("hipHostMalloc failed");
+    return p;
+  }
+  const unsigned long mask = 1ul << node;
+  constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+  const bool policy = syscall(SYS_set_mempolicy, kMpolPreferred, &mask, sizeof(mask) * 8) == 0;
+  const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault | hipHostMallocNumaUser);
+  if (policy) (void)syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0);
+  if (e != hipSuccess) throw std::runtime_error("hipHostMalloc (NUMA node " + std::to_string(node) + ") failed");
+  return p;
+}
+
+std::string numa_residency(const void* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::ifstream maps("/proc/self/maps");
+  std::string line;
+  uintptr_t start = 0;
+  bool found = false;
+  while (std::getline(maps, line)) {
+    unsigned long lo = 0, hi = 0;
+    if (std::sscanf(line.c_str(), "%lx-%lx", &lo, &hi) == 2 && a >= lo && a < hi) {
+      start = lo;
+      found = true;
+      break;
+    }
+  }
+  if (!found) return "unknown";
+  std::ifstream nm("/proc/self/numa_maps");
+  while (std::getline(nm, line)) {
+    unsigned long lo = 0;
+    if (std::sscanf(line.c_str(), "%lx", &lo) != 1 || lo != start) continue;
+    std::stringstream ss(line);
+    std::string tok;
+    std::vector<std::pair<int, long>> nodes;
+    long total = 0;
+    while (ss >> tok) {
+      int n = 0;
+      long c = 0;
+      if (std::sscanf(tok.c_str(), "N%d=%ld", &n, &c) == 2) {
+        nodes.push_back({n, c});
+        total += c;
+      }
+    }
+    if (total == 0) return "untouched";
+    std::string out;
+    for (auto& nc : nodes) {
+      if (!out.empty()) out += ",";
+      out += "N" + std::to_string(nc.first) + "=" + std::to_string((nc.second * 100 + total / 2) / total) + "%";
+    }
+    return out;
+  }
+  return "unknown";
+}
+
 SdmaEngine::SdmaEngine(int device) {
   hsa_check(hsa_init(), "hsa_init");  // reference counted: HIP already initialised the runtime
   hsa_inited_ = true;
@@ -168,7 +228,15 @@ SdmaEngine::SdmaEngine(int device) {
   uint32_t mask = 0, pref = 0;
   if (hsa_amd_memory_copy_engine_status(cpu_, gpu_, &mask) != HSA_STATUS_SUCCESS) mask = 0;
   if (hsa_amd_memory_get_preferred_copy_engine(cpu_, gpu_, &pref) != HSA_STATUS_SUCCESS) pref = 0;
-  const uint32_t use = (pref & mask) ? (pref & mask) : mask;
+  // One engine: on MI355X a single SDMA engine streams device -> host at the PCIe roof
+  // (55.5-55.7 GB/s for engines 0, 1 or 2), two engines at once contend (47-50 GB/s) and engines 4-7
+  // reach only 25 GB/s (profiles/r2_sdma_engine_sweep.md). Prefer the runtime's recommendation.
+  uint32_t use = (pref & mask) ? (pref & mask) : mask;
+  use &= (~use + 1u);  // lowest set bit
+  if (const char* e = std::getenv("UDA_SDMA_ENGINE_MASK")) {  // operator override / sweeps
+    const uint32_t want = (uint32_t)std::strtoul(e, nullptr, 0);
+    if (want & mask) use = want & mask;
+  }
   for (int b = 0; b < 16; ++b)
     if (use & (1u << b)) engine_ids_.push_back(1u << b);
   UDA_LOG(kInfo, "SDMA delivery: device %d numa %d engines mask 0x%x preferred 0x%x", device, numa_node_, mask, pref);

@@ -64,6 +64,12 @@ class SdmaEngine {
 // CPUs of that node (no-op when unknown). Used for the delivery/consumer threads.
 int device_numa_node(int device);
 void bind_thread_to_numa(int node);
+// Pinned host allocation placed on NUMA node `node` (hipHostMalloc under a preferred-node memory
+// policy, hipHostMallocNumaUser); plain hipHostMalloc when node < 0. Free with hipHostFree.
+void* hip_host_alloc_on_node(size_t bytes, int node);
+// Where the pages of the mapping containing `p` live, from /proc/self/numa_maps: "N1=100%" style
+// summary (or "unknown").
+std::string numa_residency(const void* p);
 
 }  // namespace gpu
 }  // namespace uda

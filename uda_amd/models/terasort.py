@@ -42,7 +42,7 @@ class TeraSortConfig:
     reducers: int = 1                   # reduce tasks per GPU
     d2h_piece_bytes: int = 128 << 20
     pinned_slots: int = 16
-    d2h_engines: int = 2
+    d2h_engines: int = 1
     d2h: str = "sdma"                   # "sdma" (explicit copy engines) or "hip" (hipMemcpyAsync)
     deliver_host: bool = True
     validate: bool = False
@@ -110,6 +110,11 @@ class TeraSortShuffle:
             st["consumer_errors"] = [self.sink.error(i) for i in range(self.cfg.reducers)]
             st["consumer_eof"] = [self.sink.eof(i) for i in range(self.cfg.reducers)]
         return st
+
+    def drop_sink(self) -> None:
+        """Ablation: delivered buffers are released unread (no consumer work)."""
+        self.sink = None
+        self.job.clear_sink()
 
     def use_python_sink(self, fn, with_reducer: bool = False) -> None:
         """Deliver to a Python callable instead of the native J2C sink (tests)."""
