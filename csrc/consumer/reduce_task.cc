@@ -192,9 +192,20 @@ void ReduceTask::handle(const HadoopCmd& cmd) {
     case kFetchMsg: {
       FetchParams f;
       if (!parse_fetch_params(cmd, &f, &err)) throw ProtocolError(err);
-      if (restored_maps_.count(f.map_id)) {  // already merged into a checkpointed LPQ
-        UDA_LOG(kDebug, "fetch of %s skipped: restored from the LPQ checkpoint", f.map_id.c_str());
-        break;
+      if (!restored_tasks_.empty()) {
+        // restored LPQs are matched by map *task*: a re-executed map (new attempt id) must not be
+        // merged next to the LPQ that already holds its old attempt's records
+        auto it = restored_tasks_.find(map_task_of(f.map_id));
+        if (it != restored_tasks_.end()) {
+          if (it->second == f.map_id) {  // already merged into a checkpointed LPQ
+            UDA_LOG(kDebug, "fetch of %s skipped: restored from the LPQ checkpoint", f.map_id.c_str());
+            break;
+          }
+          const std::string had = it->second;  // discard_checkpoint() clears the map
+          discard_checkpoint();
+          throw UdaError("map task re-executed since the LPQ checkpoint (" + had + " -> " + f.map_id +
+                         "): checkpoint discarded, the next attempt starts clean");
+        }
       }
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -305,6 +316,27 @@ void ReduceTask::on_init(const InitParams& p) {
   merge_thr_ = std::thread([this] { merge_main(); });
 }
 
+// attempt_<jt>_<job>_m_<task>_<n> -> attempt_<jt>_<job>_m_<task> (the map task, any attempt)
+std::string map_task_of(const std::string& attempt) {
+  const size_t u = attempt.rfind('_');
+  if (u != std::string::npos && u + 1 < attempt.size() &&
+      attempt.find_first_not_of("0123456789", u + 1) == std::string::npos)
+    return attempt.substr(0, u);
+  return attempt;
+}
+
+// The manifest and every LPQ file it lists are removed; nothing of the failed attempt is reused.
+void ReduceTask::discard_checkpoint() {
+  for (const auto& f : restored_files_) {
+    ::unlink(f.c_str());
+    ::unlink((f + ".idx").c_str());
+  }
+  ::unlink(checkpoint_path().c_str());
+  restored_files_.clear();
+  restored_maps_.clear();
+  restored_tasks_.clear();
+}
+
 std::string ReduceTask::checkpoint_path() const {
   // keyed by job + partition, not by attempt: attempt_<job>_r_<part>_<n> -> drop "_<n>"
   std::string key = init_.reduce_task_id;
@@ -349,6 +381,7 @@ void ReduceTask::load_checkpoint() {
       restored_files_.clear();
       restored_maps_.clear();
     }
+    for (const auto& m : restored_maps_) restored_tasks_[map_task_of(m)] = m;
     if (!restored_files_.empty())
       UDA_LOG(kInfo, "GPU LPQ checkpoint: resuming with %zu LPQs (%zu MOFs)", restored_files_.size(),
               restored_maps_.size());
@@ -378,6 +411,7 @@ void ReduceTask::load_checkpoint() {
     restored_files_.push_back(path);
     restored_maps_.insert(v.begin(), v.end());
   }
+  for (const auto& m : restored_maps_) restored_tasks_[map_task_of(m)] = m;
   if (!restored_files_.empty())
     UDA_LOG(kInfo, "LPQ checkpoint: resuming with %zu LPQs (%zu MOFs) from %s", restored_files_.size(),
             restored_maps_.size(), checkpoint_path().c_str());

@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -30,6 +31,9 @@
 namespace uda {
 
 class MofFetcher;
+
+// Map task id of a map attempt id (drops the trailing "_<attempt>").
+std::string map_task_of(const std::string& attempt);
 
 struct ReduceStats {
   int64_t maps_fetched = 0;
@@ -99,6 +103,8 @@ class ReduceTask {
   bool checkpoint_ = false;
   std::vector<std::string> restored_files_;   // LPQ files of the previous attempt, in LPQ order
   std::set<std::string> restored_maps_;       // their MOFs (FETCHes for these are dropped)
+  std::map<std::string, std::string> restored_tasks_;  // map task -> attempt merged into a restored LPQ
+  void discard_checkpoint();
   std::string backend_ = "cpu";
   std::unique_ptr<ClientTransport> transport_;
 

@@ -244,3 +244,41 @@ def test_injected_host_alloc_fault_raises_on_init(monkeypatch):
     monkeypatch.setenv("UDA_FAULT_HOST_ALLOC", "1")
     with pytest.raises(RuntimeError, match="UdaRuntimeException"):
         UdaConsumer(2, "job_1_0009", "attempt_job_1_0009_r_000000_0", datagen.TEXT)
+
+
+def test_checkpoint_resume_refuses_reexecuted_map(provider, tmp_path, monkeypatch):
+    """A map re-executed between reduce attempts (new attempt id) must not be merged next to the
+    restored LPQ that holds its old attempt: the checkpoint is discarded and the attempt fails over
+    (fallback), and a clean attempt then produces the right output."""
+    maps = datagen.terasort(num_maps=23, reducers=1, rows_per_map=200, seed=4)
+    ids = publish(provider, tmp_path, "job_1_0016", maps)
+    d1 = tmp_path / "ld"
+    d1.mkdir()
+    kw = dict(approach=2, lpq_size=5, local_dirs=(str(d1),), conf={"mapred.uda.lpq.checkpoint": 1})
+    monkeypatch.setenv("UDA_FAULT_LPQ_DONE", "2")
+    c = UdaConsumer(len(ids), "job_1_0016", "attempt_job_1_0016_r_000000_0", datagen.TEXT, **kw)
+    for m in ids:
+        c.fetch("h", "job_1_0016", m, 0)
+    with pytest.raises(UdaFallback, match="injected"):
+        c.wait(60)
+    c.close()
+    monkeypatch.delenv("UDA_FAULT_LPQ_DONE")
+    manifest = d1 / "uda.attempt_job_1_0016_r_000000.lpq.manifest"
+    restored = sorted({m for ln in manifest.read_text().splitlines() for m in ln.split()[4].split(",")})
+    # map attempt _0 of one restored task is re-executed as attempt _1 (same data)
+    old = restored[0]
+    new = old[:-1] + "1"
+    mof = maps[ids.index(old)]
+    from uda_amd.utils.mof import write_mof
+    path, _ = write_mof(str(tmp_path), new, datagen.streams([mof])[0])
+    provider.add_mof_file("job_1_0016", new, path)
+    ids2 = [new if m == old else m for m in ids]
+    c = UdaConsumer(len(ids2), "job_1_0016", "attempt_job_1_0016_r_000000_1", datagen.TEXT, **kw)
+    with pytest.raises(Exception, match="re-executed"):
+        for m in ids2:
+            c.fetch("h", "job_1_0016", m, 0)
+    c.close()
+    assert not os.listdir(d1)  # manifest and restored LPQ files are gone
+    recs, st, _ = run_reduce("h", "job_1_0016", ids2, 0, datagen.TEXT, **kw)
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+    assert st["restored_lpqs"] == 0 and st["maps_fetched"] == 23
