@@ -55,6 +55,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-validate", action="store_true", help="skip the final validated step")
     ap.add_argument("--sink", choices=("j2c", "none"), default="j2c",
                     help="ablation: 'none' drops delivered buffers unread (measures the copy path alone)")
+    ap.add_argument("--api", action="store_true",
+                    help="drive the shuffle only through the UdaBridge C ABI (uda_start/INIT/FETCH/dataFromUda) "
+                         "with HBM-resident MOFs: one NetMerger handle per reduce task (1 GPU)")
+    ap.add_argument("--round-mb", type=int, default=2048, help="--api: device merge round size per reduce task")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -118,6 +122,8 @@ def main(argv=None) -> int:
         print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
         return 2
     torch.cuda.set_device(ctx.local_rank)
+    if args.api:
+        return run_api(args, ctx)
 
     cfg = TeraSortConfig(rows_per_gpu=args.rows_per_gpu, maps_per_rank=args.maps_per_gpu,
                          rounds=args.rounds, reducers=args.reducers, d2h=args.d2h,
@@ -211,6 +217,76 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     ctx.close()
+    return 0
+
+
+def run_api(args, ctx) -> int:
+    """TeraSort through the C ABI: the same reduce-side work, entered the way the Hadoop plugins enter
+    it (csrc/gpu/api_bench.cc)."""
+    import torch
+
+    from uda_amd import native
+    from uda_amd.models.terasort import RECORD_BYTES
+    if ctx.world != 1:
+        print("bench: --api runs on one GPU (cross-GPU providers are exercised by the RCCL path)", file=sys.stderr)
+        return 2
+    b = native().ApiTeraSortBench(dict(device=ctx.local_rank, maps=args.maps_per_gpu, reducers=args.reducers,
+                                       records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
+                                       round_bytes=args.round_mb << 20))
+    t = time.perf_counter()
+    b.setup()
+    print(f"# api setup {time.perf_counter() - t:.1f}s store={b.store_bytes/1e9:.1f}GB", file=sys.stderr, flush=True)
+    for i in range(args.warmup):
+        st = b.step(False)
+        if args.verbose:
+            print(f"# warmup {i}: {json.dumps(st)}", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [b.step(False) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    validated = None
+    if not args.no_validate:
+        vst = b.step(True)
+        validated = vst["order_errors"] == 0
+        if args.verbose:
+            print(f"# validated step: {json.dumps(vst)}", file=sys.stderr, flush=True)
+    records = int(stats[0]["records"])
+    ms_per_step = elapsed * 1000.0 / max(1, args.steps)
+    gbps = records * RECORD_BYTES / (ms_per_step / 1000.0) / 1e9
+    out = {
+        "metric": "TeraSort shuffle+merge GB/s whole-node",
+        "value": round(gbps, 3),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bytes",
+        "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+        "config": {
+            "model": "terasort",
+            "global_batch": records,
+            "seq_len": RECORD_BYTES,
+            "parallelism": "dp1",
+            "rows_per_gpu": records,
+            "maps_per_gpu": args.maps_per_gpu,
+            "reducers_per_gpu": args.reducers,
+            "shuffle": "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
+                       "(descriptor fetch, merged in place)",
+            "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) per reduce task",
+        },
+        "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
+        "close_ms": round(sum(s["close_ms"] for s in stats) / len(stats), 2),
+        "buffers_per_step": int(stats[0]["buffers"]),
+        "task0_stats": json.loads(stats[0]["task0_stats"]) if stats[0]["task0_stats"] else None,
+        "validated": validated,
+        "reference_envelope_gbps_per_node": 5.0,
+    }
+    print(json.dumps(out), flush=True)
     return 0
 
 

@@ -149,15 +149,24 @@ const char* uda_last_error(uda_handle* h) { return h ? h->last_error.c_str() : "
 
 int uda_provider_register_mof(uda_handle* h, const char* job_id, const char* map_id, const void* data, int64_t len,
                               const int64_t* index, int32_t num_partitions) {
+  return uda_provider_register_mof_device(h, job_id, map_id, data, len, index, num_partitions, -1);
+}
+
+int uda_provider_register_mof_device(uda_handle* h, const char* job_id, const char* map_id, const void* data,
+                                     int64_t len, const int64_t* index, int32_t num_partitions, int32_t device) {
   if (!h || !h->supplier) return -1;
   std::vector<uda::IndexRec> recs((size_t)num_partitions);
   for (int i = 0; i < num_partitions; ++i) {
     recs[i].start_offset = index[3 * i];
     recs[i].raw_length = index[3 * i + 1];
     recs[i].part_length = index[3 * i + 2];
-    recs[i].path = std::string("mem:") + job_id + "/" + map_id;
+    recs[i].path = std::string(device >= 0 ? "hbm:" : "mem:") + job_id + "/" + map_id;
   }
-  h->supplier->register_mof(job_id, map_id, (const uint8_t*)data, len, std::move(recs));
+  try {
+    h->supplier->register_mof(job_id, map_id, (const uint8_t*)data, len, std::move(recs), device);
+  } catch (const std::exception& e) {
+    return fail_call(h, e.what());
+  }
   return 0;
 }
 
@@ -168,7 +177,8 @@ int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
     s = h->task->stats_json();
   } else if (h->supplier) {
     s = "{\"role\":\"mof_supplier\",\"requests\":" + std::to_string(h->supplier->requests()) +
-        ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) + ",\"port\":" +
+        ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) +
+        ",\"descriptors_served\":" + std::to_string(h->supplier->descriptors_served()) + ",\"port\":" +
         std::to_string(h->supplier->port()) + ",\"io\":\"" + h->supplier->io_backend() + "\"}";
   } else {
     s = "{}";

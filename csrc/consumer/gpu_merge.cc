@@ -29,6 +29,8 @@
 #include <thread>
 
 #include "../gpu/block_decoder.h"
+#include "../gpu/device_ptr.h"
+#include "../gpu/device_reduce.h"
 #include "../gpu/device_engine.h"
 #include "../gpu/generic_merger.h"
 #include "reduce_task.h"
@@ -228,6 +230,10 @@ int cmp_key(KeyKind kind, const std::string& a, const std::string& b) {
 
 void ReduceTask::merge_gpu() {
   if (gpu::device_count() <= 0) throw UdaError("mapred.uda.merge.backend=gpu but no HIP device is visible");
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.merge_path = "staged";
+  }
   auto t0 = std::chrono::steady_clock::now();
   const int maps = init_.num_maps;
   const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
@@ -663,6 +669,239 @@ void ReduceTask::merge_gpu() {
     cleanup(false);
     throw;
   }
+}
+
+// GPU backend, device fetch (mapred.uda.gpu.fetch=device, uncompressed map outputs): every FETCH is
+// a descriptor fetch, so partitions the provider holds in HBM are merged where they live (same
+// process: the address; another process on the node: an IPC mapping) and never cross PCIe on the
+// way in. MOFs that are not device-resident are fetched as bytes and copied to the device.
+// TeraSort-shaped inputs go through the key-range-round FIXED10 merge with SDMA delivery
+// (device_reduce.cc); other key classes through the generic merge tree.
+// Reference: start_fetch_req / RDMA WRITE into the reducer buffer (src/DataNet/RDMAClient.cc:559-600,
+// src/DataNet/RDMAServer.cc:537-631) and merge_online (src/Merger/MergeManager.cc:184-193).
+bool ReduceTask::merge_gpu_device(bool probe) {
+  if (gpu::device_count() <= 0) throw UdaError("mapred.uda.merge.backend=gpu but no HIP device is visible");
+  auto t0 = std::chrono::steady_clock::now();
+  const int maps = init_.num_maps;
+  const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+  HIP_CHECK(hipSetDevice(device));
+  StreamGuard sg;
+  HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+  hipStream_t s = sg.s;
+  struct Part {
+    const uint8_t* dptr = nullptr;
+    int64_t part_len = 0;
+    gpu::DeviceBuffer own;  // bytes fetched from a host-resident MOF
+  };
+  std::vector<std::unique_ptr<Part>> parts;
+  int64_t host_bytes = 0, descriptors = 0;
+  gpu::PinnedBuffer chunk;
+
+  // bytes of a MOF the provider does not hold in device memory: chunked fetches -> H2D
+  auto fetch_bytes = [&](const FetchParams& f, int64_t part_len, Part* part) {
+    part->own.alloc((size_t)std::max<int64_t>(part_len, 16));
+    part->dptr = part->own.as<uint8_t>();
+    part->part_len = part_len;
+    if (chunk.size() < (size_t)buffer_size_) chunk.alloc((size_t)buffer_size_);
+    for (int64_t off = 0; off < part_len;) {
+      FetchRequest req;
+      req.job_id = f.job_id;
+      req.map_id = f.map_id;
+      req.reduce_id = f.reduce_id;
+      req.fetched = off;
+      req.buf_len = buffer_size_;
+      std::mutex m;
+      std::condition_variable c;
+      bool done = false;
+      FetchAck got;
+      fetch_begin();
+      transport_->fetch(f.host, req, chunk.as<uint8_t>(), [&](const FetchAck& a) {
+        std::lock_guard<std::mutex> g(m);
+        got = a;
+        done = true;
+        c.notify_all();
+        fetch_end();
+      });
+      {
+        std::unique_lock<std::mutex> lk(m);
+        c.wait(lk, [&] { return done; });
+      }
+      if (got.status != 0) throw UdaError("fetch of " + f.map_id + " failed: " + got.error);
+      if (got.sent <= 0) throw UdaError("fetch of " + f.map_id + ": provider sent no data");
+      HIP_CHECK(hipMemcpy(part->own.as<uint8_t>() + off, chunk.as(), (size_t)got.sent, hipMemcpyHostToDevice));
+      off += got.sent;
+      host_bytes += got.sent;
+    }
+  };
+
+  // ---- fetch phase: descriptors for every MOF as its FETCH arrives
+  int resolved = 0;
+  while (resolved < maps) {
+    std::vector<FetchParams> batch;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !fetch_list_.empty(); });
+      if (stop_) throw UdaError("reduce task stopped during fetch");
+      while (!fetch_list_.empty()) {
+        batch.push_back(fetch_list_.front());
+        fetch_list_.pop_front();
+      }
+    }
+    std::vector<FetchAck> acks(batch.size());
+    std::mutex m;
+    std::condition_variable c;
+    size_t left = batch.size();
+    for (size_t i = 0; i < batch.size(); ++i) {
+      FetchRequest req;
+      req.job_id = batch[i].job_id;
+      req.map_id = batch[i].map_id;
+      req.reduce_id = batch[i].reduce_id;
+      req.buf_len = kDescriptorFetch;
+      fetch_begin();
+      transport_->fetch(batch[i].host, req, nullptr, [&, i](const FetchAck& a) {
+        std::lock_guard<std::mutex> g(m);
+        acks[i] = a;
+        --left;
+        c.notify_all();
+        fetch_end();
+      });
+    }
+    {
+      std::unique_lock<std::mutex> lk(m);
+      c.wait(lk, [&] { return left == 0; });
+    }
+    if (probe && resolved == 0 && descriptors == 0) {
+      // auto mode: the first answers decide; host-resident map outputs keep the staged path
+      bool any_device = false;
+      for (const auto& a : acks) any_device |= a.status == 0 && gpu::is_device_descriptor(a.path);
+      if (!any_device) {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto it = batch.rbegin(); it != batch.rend(); ++it) fetch_list_.push_front(*it);
+        return false;
+      }
+    }
+    for (size_t i = 0; i < batch.size(); ++i) {
+      const FetchAck& a = acks[i];
+      auto part = std::make_unique<Part>();
+      if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
+        part->dptr = gpu::resolve_device_descriptor(a.path, device);
+        part->part_len = a.part_len;
+        ++descriptors;
+      } else if (a.status == kNotDeviceResident) {
+        fetch_bytes(batch[i], a.part_len, part.get());
+      } else {
+        throw UdaError("fetch of " + batch[i].map_id + " failed: " + (a.status ? a.error : "no device descriptor"));
+      }
+      parts.push_back(std::move(part));
+      resolved++;
+      progress_count_++;
+      total_count_++;
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.maps_fetched++;
+        st_.bytes_fetched += parts.back()->part_len;
+      }
+      if (progress_count_ == 20 || total_count_ == maps) {
+        host_->fetch_over();
+        progress_count_ = 0;
+      }
+    }
+  }
+  const double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.device_descriptors = descriptors;
+    st_.host_fetched_bytes = host_bytes;
+  }
+
+  auto sink = [&](const uint8_t* p, int64_t len) -> int {
+    if (stop_) throw UdaError("reduce task stopped during merge");
+    const int r = host_->data_from_uda(p, (int32_t)len);
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.buffers++;
+    st_.bytes_delivered += len;
+    return r;
+  };
+  // ---- TeraSort-shaped input: FIXED10 rounds straight over the partitions
+  bool fixed = kind_ == KeyKind::kText;
+  std::vector<gpu::RunDesc> runs;
+  for (const auto& p : parts) {
+    const int64_t rec_bytes = p->part_len - kEofBytes;
+    if (rec_bytes < 0 || rec_bytes % gpu::kTeraRecordBytes != 0) fixed = false;
+    gpu::RunDesc d;
+    d.base = p->dptr;
+    d.nbytes = std::max<int64_t>(rec_bytes, 0);
+    d.nrec = d.nbytes / gpu::kTeraRecordBytes;
+    d.offsets = nullptr;
+    runs.push_back(d);
+  }
+  if (fixed && gpu::runs_are_fixed10(runs, s)) {
+    gpu::DeviceReduceConfig cfg;
+    cfg.device = device;
+    cfg.kv_buf_bytes = kv_buf_size_;
+    cfg.round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+    gpu::DeviceReduceStats ds = gpu::device_reduce_fixed(cfg, runs, sink);
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.records = ds.records;
+    st_.rpq_rounds = ds.rounds;
+    st_.gpu_device_ms = ds.plan_ms + ds.merge_wait_ms;
+    st_.gpu_d2h_wait_ms = ds.d2h_wait_ms;
+    st_.gpu_sink_ms = ds.sink_ms;
+    st_.fetch_ms = fetch_ms;
+    st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
+    st_.merge_path = "device-fixed10";
+    return true;
+  }
+  // ---- any other key class: the generic merge tree over device copies of the partitions
+  DeviceWorkspace ws;
+  int64_t total = 0;
+  for (const auto& p : parts) total += p->part_len;
+  DeviceWorkspace::ensure(ws.in, total);
+  DeviceWorkspace::ensure(ws.out, total);
+  std::vector<const uint8_t*> rptr;
+  std::vector<int64_t> rlen;
+  int64_t off = 0;
+  for (const auto& p : parts) {
+    if (p->part_len > 0)
+      HIP_CHECK(hipMemcpyAsync(ws.in.as<uint8_t>() + off, p->dptr, (size_t)p->part_len, hipMemcpyDefault, s));
+    rptr.push_back(ws.in.as<uint8_t>() + off);
+    rlen.push_back(p->part_len);
+    off += p->part_len;
+  }
+  const int64_t kv = kv_buf_size_ - kEofBytes;
+  gpu::GenericMergeResult r = ws.merger.merge(rptr, rlen, (int)kind_, ws.out.as<uint8_t>(), total, kv, s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  DeviceMergeOut m;
+  m.bytes = r.bytes;
+  m.cuts = std::move(r.cuts);
+  m.records = r.records;
+  std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
+  bool eof_sent = false;
+  const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
+  stream_out(ws, m, s, [&](const uint8_t* piece, size_t c0, size_t c1) {
+    for (size_t j = c0; j < c1; ++j) {
+      const uint8_t* p = piece + (m.cuts[j] - m.cuts[c0]);
+      int64_t len = m.cuts[j + 1] - m.cuts[j];
+      if (j + 1 == nb) {
+        std::memcpy(tail.data(), p, (size_t)len);
+        tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
+        p = tail.data();
+        len += kEofBytes;
+        eof_sent = true;
+      }
+      if (sink(p, len) != 0) throw UdaError("dataFromUda callback failed");
+    }
+  });
+  if (!eof_sent) {
+    tail[0] = tail[1] = 0xFF;
+    if (sink(tail.data(), kEofBytes) != 0) throw UdaError("dataFromUda callback failed");
+  }
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.records = m.records;
+  st_.fetch_ms = fetch_ms;
+  st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
+  st_.merge_path = "device-generic";
+  return true;
 }
 
 }  // namespace uda

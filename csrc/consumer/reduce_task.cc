@@ -444,8 +444,13 @@ void ReduceTask::fetch_end() {
 void ReduceTask::merge_main() {
   auto t0 = std::chrono::steady_clock::now();
   try {
-    if (backend_ == "gpu")
+    const std::string gfetch = host_->get_conf("mapred.uda.gpu.fetch", "auto");  // auto | device | host
+    if (backend_ == "gpu" && codec_ == Codec::kNone && net_.online != 2 && gfetch != "host" &&
+        merge_gpu_device(gfetch == "auto")) {
+      // done: partitions merged where the provider holds them
+    } else if (backend_ == "gpu") {
       merge_gpu();
+    }
     else if (net_.online == 2)
       merge_hybrid();
     else
@@ -715,7 +720,9 @@ std::string ReduceTask::stats_json() const {
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
-    << ",\"restored_maps\":" << s.restored_maps << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
+    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors
+    << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"merge_path\":\"" << s.merge_path << "\""
+    << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }
 

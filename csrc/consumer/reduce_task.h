@@ -53,6 +53,9 @@ struct ReduceStats {
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
   int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;
   int64_t restored_lpqs = 0, restored_maps = 0;  // hybrid resume from an LPQ checkpoint
+  int64_t device_descriptors = 0;     // GPU device fetch: partitions merged in the provider's HBM
+  int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
+  std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)
   std::string backend;
 };
 
@@ -80,6 +83,9 @@ class ReduceTask {
   void merge_online();
   void merge_hybrid();
   void merge_gpu();
+  // Device fetch (descriptors, merge in place). probe: return false before consuming anything if the
+  // first MOFs are not device-resident (the caller then runs merge_gpu()).
+  bool merge_gpu_device(bool probe);
   // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
   void fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids = nullptr);
   // LPQ checkpoint (mapred.uda.lpq.checkpoint): completed LPQ spill files survive a failed attempt,

@@ -1,0 +1,248 @@
+// TeraSort through the C ABI with HBM-resident MOFs. See api_bench.h.
+#include "api_bench.h"
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "device_engine.h"
+#include "j2c_sink.h"
+#include "uda/cmd.h"
+#include "uda/uda_bridge.h"
+
+namespace uda {
+namespace gpu {
+
+namespace {
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// get_conf of both roles: a fixed table (the JobConf of this benchmark job).
+struct ConfTable {
+  std::map<std::string, std::string> kv;
+};
+int conf_cb(void* ctx, const char* key, const char* dflt, char* out, int32_t outlen) {
+  auto* t = static_cast<ConfTable*>(ctx);
+  std::string v = dflt ? dflt : "";
+  auto it = t->kv.find(key);
+  if (it != t->kv.end()) v = it->second;
+  const int32_t n = (int32_t)std::min<size_t>(v.size(), (size_t)outlen - 1);
+  std::memcpy(out, v.data(), (size_t)n);
+  out[n] = 0;
+  return n;
+}
+
+// One reduce task's host side (the ReduceTask JVM): its dataFromUda feeds the J2C consumer.
+struct TaskHost {
+  ConfTable* conf = nullptr;
+  J2CSink* sink = nullptr;
+  int reducer = 0;
+  std::mutex* mu = nullptr;
+  std::condition_variable* cv = nullptr;
+  int* done = nullptr;
+  std::string failure;
+  bool finished = false;
+};
+int data_cb(void* ctx, const void* buf, int32_t len) {
+  auto* t = static_cast<TaskHost*>(ctx);
+  const int r = t->sink->consume(t->reducer, static_cast<const uint8_t*>(buf), len);
+  if (r == 0 && t->sink->eof(t->reducer)) {
+    std::lock_guard<std::mutex> g(*t->mu);
+    t->finished = true;
+    ++*t->done;
+    t->cv->notify_all();
+  }
+  return r;
+}
+void failure_cb(void* ctx, const char* reason) {
+  auto* t = static_cast<TaskHost*>(ctx);
+  std::lock_guard<std::mutex> g(*t->mu);
+  t->failure = reason ? reason : "failure";
+  if (!t->finished) {
+    t->finished = true;
+    ++*t->done;
+  }
+  t->cv->notify_all();
+}
+int task_conf_cb(void* ctx, const char* key, const char* dflt, char* out, int32_t outlen) {
+  return conf_cb(static_cast<TaskHost*>(ctx)->conf, key, dflt, out, outlen);
+}
+void log_cb(void*, const char* msg, int32_t sev) {
+  if (sev <= 2) std::fprintf(stderr, "[uda api] %s\n", msg);
+}
+
+ConfTable& bench_conf(const ApiBenchConfig& c) {
+  static ConfTable t;
+  t.kv = {{"mapred.uda.transport", "loopback"},
+          {"mapred.uda.loopback.host", "*"},
+          {"mapred.uda.merge.backend", "gpu"},
+          {"mapred.uda.gpu.fetch", "device"},
+          {"mapred.uda.gpu.device", std::to_string(c.device)},
+          {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
+          {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)}};
+  return t;
+}
+
+std::vector<const char*> cargs(const std::vector<std::string>& v) {
+  std::vector<const char*> out;
+  for (auto& s : v) out.push_back(s.c_str());
+  return out;
+}
+}  // namespace
+
+ApiTeraSortBench::ApiTeraSortBench(const ApiBenchConfig& cfg) : cfg_(cfg) {}
+
+ApiTeraSortBench::~ApiTeraSortBench() {
+  if (provider_) {
+    uda_handle* h = static_cast<uda_handle*>(provider_);
+    (void)uda_do_command(h, form_cmd(kExitMsg, {}).c_str());
+    uda_destroy(h);
+  }
+}
+
+int64_t ApiTeraSortBench::store_bytes() const { return gen_ ? gen_->store_bytes() : 0; }
+
+void ApiTeraSortBench::setup() {
+  // map phase stand-in: `maps` MOFs x `reducers` total-order partitions in HBM
+  ShuffleConfig sc;
+  sc.device = cfg_.device;
+  sc.world = cfg_.reducers;  // partitions per MOF (no exchange is ever run on this job)
+  sc.rank = 0;
+  sc.maps_per_rank = cfg_.maps;
+  sc.records_per_map = cfg_.records_per_map;
+  sc.seed = cfg_.seed;
+  sc.deliver_host = false;
+  gen_.reset(new ShuffleJob(sc));
+  gen_->generate();
+  expected_ = gen_->local_dest_records();
+  // MOFSupplier handle (TaskTracker / NodeManager side)
+  ConfTable& conf = bench_conf(cfg_);
+  uda_callbacks cb{};
+  cb.ctx = &conf;
+  cb.get_conf = conf_cb;
+  cb.log = log_cb;
+  const std::vector<std::string> args = {"-w", "256", "-r", "9011", "-m", "1", "-g", "/tmp", "-s", "1024"};
+  auto av = cargs(args);
+  uda_handle* h = uda_start(0, (int)av.size(), av.data(), 2, 0, &cb);
+  if (!h) throw std::runtime_error("api bench: uda_start (provider) failed");
+  provider_ = h;
+  map_ids_.clear();
+  for (int m = 0; m < cfg_.maps; ++m) {
+    char id[96];
+    std::snprintf(id, sizeof(id), "attempt_%s_m_%06d_0", cfg_.job.c_str() + 4, m);
+    map_ids_.push_back(id);
+    std::vector<int64_t> index;
+    for (int r = 0; r < cfg_.reducers; ++r) {
+      const auto ir = gen_->index_record(m, r);
+      index.insert(index.end(), ir.begin(), ir.end());
+    }
+    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id, gen_->mof_device_ptr(m), gen_->mof_bytes(m),
+                                         index.data(), cfg_.reducers, cfg_.device) != 0)
+      throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
+  }
+}
+
+std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string* info) {
+  const int R = cfg_.reducers;
+  J2CSink sink(R, cfg_.kv_buf_bytes);
+  sink.set_check_order(validate);
+  ConfTable& conf = bench_conf(cfg_);
+  std::mutex mu;
+  std::condition_variable cv;
+  int done = 0;
+  std::vector<TaskHost> hosts(R);
+  std::vector<uda_handle*> handles(R, nullptr);
+  std::vector<std::string> errors(R);
+  const double t0 = now_ms();
+  // every reduce task is its own "JVM" thread driving its handle: start, INIT, FETCH per map
+  std::vector<std::thread> ts;
+  for (int r = 0; r < R; ++r) {
+    ts.emplace_back([&, r] {
+      TaskHost& th = hosts[r];
+      th.conf = &conf;
+      th.sink = &sink;
+      th.reducer = r;
+      th.mu = &mu;
+      th.cv = &cv;
+      th.done = &done;
+      uda_callbacks cb{};
+      cb.ctx = &th;
+      cb.data_from_uda = data_cb;
+      cb.get_conf = task_conf_cb;
+      cb.failure = failure_cb;
+      cb.log = log_cb;
+      const std::vector<std::string> args = {"-w", "256", "-r", "9011", "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"};
+      auto av = cargs(args);
+      uda_handle* h = uda_start(1, (int)av.size(), av.data(), 2, 0, &cb);
+      handles[r] = h;
+      auto fail = [&](const std::string& why) {
+        std::lock_guard<std::mutex> g(mu);
+        errors[r] = why;
+        if (!th.finished) {
+          th.finished = true;
+          ++done;
+        }
+        cv.notify_all();
+      };
+      if (!h) return fail("uda_start failed");
+      char rt[96];
+      std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, r);
+      const std::vector<std::string> init = {std::to_string(cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
+                                             std::to_string(16 << 10), "org.apache.hadoop.io.Text", "null",
+                                             std::to_string(256 << 10), "0", "0"};
+      if (uda_do_command(h, form_cmd(kInitMsg, init).c_str()) != 0) return fail(uda_last_error(h));
+      for (int m = 0; m < cfg_.maps; ++m) {
+        const std::vector<std::string> f = {"localhost", cfg_.job, map_ids_[m], std::to_string(r)};
+        if (uda_do_command(h, form_cmd(kFetchMsg, f).c_str()) != 0) return fail(uda_last_error(h));
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!cv.wait_for(lk, std::chrono::seconds(900), [&] { return done == R; }))
+      throw std::runtime_error("api bench: reduce tasks did not finish within 900 s");
+  }
+  const double t1 = now_ms();
+  std::string paths;
+  for (int r = 0; r < R; ++r) {
+    if (!handles[r]) continue;
+    (void)uda_reduce_exit(handles[r]);  // joins the merge thread: its stats are final after this
+    char js[4096];
+    if (r == 0 && uda_stats_json(handles[r], js, sizeof(js)) > 0) paths = js;
+    uda_destroy(handles[r]);
+  }
+  const double t2 = now_ms();
+  for (int r = 0; r < R; ++r) {
+    if (!errors[r].empty()) throw std::runtime_error("reduce task " + std::to_string(r) + ": " + errors[r]);
+    if (!hosts[r].failure.empty()) throw std::runtime_error("reduce task " + std::to_string(r) + " failed: " + hosts[r].failure);
+    if (sink.error(r) != 0) throw std::runtime_error("reduce task " + std::to_string(r) + ": consumer framing error");
+    if (sink.records(r) != expected_[r])
+      throw std::runtime_error("reduce task " + std::to_string(r) + ": consumer parsed " + std::to_string(sink.records(r)) +
+                               " records, expected " + std::to_string(expected_[r]));
+  }
+  std::map<std::string, double> out;
+  double bytes = 0, recs = 0, bufs = 0, oerr = 0;
+  for (int r = 0; r < R; ++r) {
+    bytes += (double)sink.bytes(r);
+    recs += (double)sink.records(r);
+    bufs += (double)sink.buffers(r);
+    oerr += (double)sink.order_errors(r);
+  }
+  out["wall_ms"] = t1 - t0;
+  out["close_ms"] = t2 - t1;
+  out["bytes"] = bytes;
+  out["records"] = recs;
+  out["buffers"] = bufs;
+  out["order_errors"] = validate ? oerr : -1;
+  if (info) *info = paths;
+  return out;
+}
+
+}  // namespace gpu
+}  // namespace uda

@@ -255,6 +255,9 @@ class ShuffleJob {
   // Records each of this GPU's reducers receives per step (after plan()).
   std::vector<int64_t> reducer_records() const { return reducer_records_; }
   int64_t store_bytes() const { return store_bytes_; }
+  // Device address / size of MOF m in the partition store (host address for the host tier).
+  const uint8_t* mof_device_ptr(int m) const { return store_dev_base_ + mof_off_.at(m); }
+  int64_t mof_bytes(int m) const { return mof_off_.at(m + 1) - mof_off_.at(m); }
   int64_t max_round_records() const { return max_round_records_; }
   int comm_ranks() const { return exchange_ ? exchange_->comm_ranks() : 1; }
   std::string exchange_name() const { return exchange_ ? exchange_->name() : "none"; }

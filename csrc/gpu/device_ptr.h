@@ -1,0 +1,34 @@
+// HBM-resident map outputs shared with reducers: the "memory region + rkey" analogue of the
+// reference's registered RDMA buffers (src/DataNet/RDMAComm.cc:67-154, rkey exchange in the
+// connection private data, RDMAComm.h:35-39).
+//
+// A provider that registers a MOF living in device memory answers a descriptor fetch (RTS with a
+// negative buffer length) with the partition's device address instead of its bytes. The descriptor
+// travels in the ACK's path field, so both transports carry it unchanged:
+//   hbm@<device>@<pid>@<hex address>@<hex IPC handle or ->@<offset from the IPC base>
+// A reducer in the same process uses the address directly (peer access enabled when the devices
+// differ, so xGMI carries the reads); a reducer in another process on the node maps the
+// provider's allocation with hipIpcOpenMemHandle (cached per handle) and adds the offset.
+#pragma once
+#include <cstdint>
+#include <string>
+
+namespace uda {
+namespace gpu {
+
+// IPC export of the allocation containing `ptr`: handle (hex) and the allocation base.
+struct IpcExport {
+  std::string handle_hex;  // "-" when the allocation cannot be shared across processes
+  const uint8_t* base = nullptr;
+};
+IpcExport ipc_export(const void* ptr);
+
+std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc);
+bool is_device_descriptor(const std::string& s);
+// Device address (usable on `my_device`) of a descriptor; throws if it cannot be mapped.
+const uint8_t* resolve_device_descriptor(const std::string& desc, int my_device);
+// Copy device memory at `src` (any device) to host `dst`.
+void copy_device_to_host(void* dst, const void* src, int64_t bytes);
+
+}  // namespace gpu
+}  // namespace uda

@@ -1,0 +1,53 @@
+// One reduce task's device merge over HBM-resident map-output partitions, delivered to the host
+// reducer: the NetMerger online merge (merge_online + merge_do_merging_phase,
+// src/Merger/MergeManager.cc:155-193) for partitions that never leave device memory.
+//
+// Input: K sorted runs in device memory (the provider's HBM partitions, read in place: the RDMA
+// WRITE of the reference is replaced by a pointer, or an IPC-mapped pointer across processes).
+// FIXED10 (TeraSort-shaped Text records) inputs are merged in key-range rounds so device memory
+// stays bounded: a key sample gives Q-1 bounds, every run is split at them on the device, and round
+// q merges the q-th slice of every run (F2 -> F3 -> F4) into one of two output slots while the host
+// delivers round q-1: SDMA pieces into a pinned ring, cut into <= kv_buf whole-record buffers handed
+// to the sink, the last one carrying the IFile EOF marker.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace uda {
+namespace gpu {
+
+struct DeviceReduceConfig {
+  int device = 0;
+  int64_t kv_buf_bytes = 1 << 20;
+  int64_t round_bytes = 2ll << 30;    // target merged bytes per round (two output slots of this size)
+  int64_t piece_bytes = 64ll << 20;   // D2H granule
+  int pinned_slots = 4;
+  int64_t sample_every = 4096;        // one key sampled per this many records for the round bounds
+};
+
+struct DeviceReduceStats {
+  int64_t records = 0;
+  int64_t bytes = 0;          // record bytes delivered (EOF excluded)
+  int64_t buffers = 0;
+  int rounds = 0;
+  int merge_passes = 0;
+  double plan_ms = 0, merge_wait_ms = 0, d2h_wait_ms = 0, sink_ms = 0;
+};
+
+// True if every run holds whole TeraSort-shaped records (VInt 11, VInt 91, Text 10 + 90 bytes).
+// Synchronizes `s`.
+bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s);
+
+// Merge `runs` and call sink(buf, len) with every delivery buffer (EOF included in the last).
+// A nonzero sink return aborts with an exception.
+DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::vector<RunDesc>& runs,
+                                      const std::function<int(const uint8_t*, int64_t)>& sink);
+
+}  // namespace gpu
+}  // namespace uda

@@ -8,6 +8,7 @@
 // It also validates the delivery contract: every buffer holds whole records, is at most
 // kv_buf_bytes long, and each reducer's stream ends with exactly one EOF marker (-1, -1).
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstring>
@@ -41,6 +42,7 @@ class J2CSink {
     s.cur ^= 1;
     std::memcpy(kb, data, (size_t)len);  // dataFromUda: DirectByteBuffer -> KVBuf
     int64_t p = 0, recs = 0;
+    const bool order = check_order_;
     while (p < len) {  // J2CQueue.next: readVInt key length, readVInt value length, skip bytes
       int64_t kl = 0, vl = 0;
       const int a = vint_decode(kb + p, (size_t)(len - p), &kl);
@@ -54,6 +56,19 @@ class J2CSink {
         break;
       }
       if (kl < 0 || vl < 0) return fail(s, kBadFraming);
+      if (p + a + b + kl + vl > len) return fail(s, kBadFraming);
+      if (order) {  // serialized key bytes ascend within a reducer
+        const uint8_t* k = kb + p + a + b;
+        const int kn = (int)std::min<int64_t>(kl, (int64_t)sizeof(s.last_key));
+        if (s.has_last) {
+          const int n = std::min(kn, s.last_len);
+          const int c = std::memcmp(s.last_key, k, (size_t)n);
+          if (c > 0 || (c == 0 && s.last_len > kn)) ++s.order_errors;
+        }
+        std::memcpy(s.last_key, k, (size_t)kn);
+        s.last_len = kn;
+        s.has_last = true;
+      }
       p += a + b + kl + vl;
       s.key_bytes += kl;
       ++recs;
@@ -67,11 +82,16 @@ class J2CSink {
 
   void reset() {
     for (auto& s : st_) {
-      s.records = s.bytes = s.buffers = s.key_bytes = 0;
+      s.records = s.bytes = s.buffers = s.key_bytes = s.order_errors = 0;
       s.eof = false;
+      s.has_last = false;
       s.error = kOk;
     }
   }
+  // Also check that serialized keys ascend bytewise within every reducer (the first 64 bytes). That
+  // is the key order for fixed-length keys such as TeraSort's 10-byte Text keys.
+  void set_check_order(bool on) { check_order_ = on; }
+  int64_t order_errors(int r) const { return st_[(size_t)r].order_errors; }
   int64_t records(int r) const { return st_[(size_t)r].records; }
   int64_t bytes(int r) const { return st_[(size_t)r].bytes; }
   int64_t buffers(int r) const { return st_[(size_t)r].buffers; }
@@ -82,15 +102,19 @@ class J2CSink {
   struct alignas(64) State {
     std::unique_ptr<uint8_t[]> buf[2];
     int cur = 0;
-    int64_t records = 0, bytes = 0, buffers = 0, key_bytes = 0;
+    int64_t records = 0, bytes = 0, buffers = 0, key_bytes = 0, order_errors = 0;
     bool eof = false;
     int error = kOk;
+    bool has_last = false;
+    int last_len = 0;
+    uint8_t last_key[64];
   };
   static int fail(State& s, int e) {
     if (s.error == kOk) s.error = e;
     return e;
   }
   int64_t kv_;
+  bool check_order_ = false;
   std::vector<State> st_;
 };
 

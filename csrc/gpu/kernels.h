@@ -184,6 +184,8 @@ void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key,
 // out[i] = sum of record hashes of FIXED10 slice runs[i] (device array of n RunDesc; out zeroed
 // here). max_nrec sizes the grid.
 void launch_slice_checksums(const RunDesc* runs, int n, int64_t max_nrec, unsigned long long* out, hipStream_t s);
+// *bad = 1 if any record of the n runs is not TeraSort-shaped (FIXED10 header check).
+void launch_check_fixed(const RunDesc* runs, int n, int64_t max_nrec, int* bad, hipStream_t s);
 // *errors += number of i with a[i] != b[i].
 void launch_count_mismatch(const unsigned long long* a, const unsigned long long* b, int n,
                            unsigned long long* errors, hipStream_t s);

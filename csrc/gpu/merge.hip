@@ -322,6 +322,19 @@ __global__ void __launch_bounds__(256) slice_checksum_kernel(const RunDesc* runs
   if ((threadIdx.x & 63) == 0 && h) atomicAdd(out + blockIdx.y, h);
 }
 
+// FIXED10 layout check of every record of every run: grid.y = run.
+__global__ void __launch_bounds__(256) check_fixed_kernel(const RunDesc* runs, int* bad) {
+  const RunDesc r = runs[blockIdx.y];
+  int b = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.nrec; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t* rec = r.base + i * kTeraRecordBytes;
+    const uint64_t w0 = *reinterpret_cast<const uint64_t*>(rec);
+    const uint64_t w1 = *reinterpret_cast<const uint64_t*>(rec + 8);
+    if ((w0 & 0xFFFFFF) != 0x0A5B0B || ((w1 >> 40) & 0xFF) != 0x5A) b = 1;
+  }
+  if (b) *bad = 1;
+}
+
 __global__ void __launch_bounds__(256) count_mismatch_kernel(const unsigned long long* a,
                                                              const unsigned long long* b, int n,
                                                              unsigned long long* errors) {
@@ -398,6 +411,18 @@ void launch_count_mismatch(const unsigned long long* a, const unsigned long long
                            unsigned long long* errors, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(count_mismatch_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, b, n, errors);
+}
+}  // namespace gpu
+}  // namespace uda
+
+namespace uda {
+namespace gpu {
+void launch_check_fixed(const RunDesc* runs, int n, int64_t max_nrec, int* bad, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t bx = (max_nrec + 4095) / 4096;
+  if (bx < 1) bx = 1;
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(check_fixed_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, s, runs, bad);
 }
 }  // namespace gpu
 }  // namespace uda

@@ -246,6 +246,34 @@ SdmaEngine::~SdmaEngine() {
   if (hsa_inited_) (void)hsa_shut_down();
 }
 
+SdmaEngine& SdmaEngine::for_device(int device) {
+  static std::mutex mu;
+  static std::map<int, SdmaEngine*>* engines = new std::map<int, SdmaEngine*>();  // leaked on purpose
+  std::lock_guard<std::mutex> g(mu);
+  auto it = engines->find(device);
+  if (it == engines->end()) it = engines->emplace(device, new SdmaEngine(device)).first;
+  return *it->second;
+}
+
+void* SdmaEngine::acquire_ring(size_t bytes) {
+  {
+    std::lock_guard<std::mutex> g(ring_mu_);
+    auto it = ring_cache_.find(bytes);
+    if (it != ring_cache_.end()) {
+      void* p = it->second;
+      ring_cache_.erase(it);
+      return p;
+    }
+  }
+  return alloc_host(bytes);
+}
+
+void SdmaEngine::release_ring(void* p, size_t bytes) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(ring_mu_);
+  ring_cache_.emplace(bytes, p);
+}
+
 void* SdmaEngine::alloc_host(size_t bytes) {
   void* p = nullptr;
   hsa_check(hsa_amd_memory_pool_allocate(host_pool_, bytes, 0, &p), "host pool allocate");
@@ -300,8 +328,7 @@ int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_
     const void* s = static_cast<const uint8_t*>(src_dev) + off;
     hsa_status_t st = HSA_STATUS_ERROR;
     if (!engine_ids_.empty()) {
-      const uint32_t eng = engine_ids_[(size_t)next_engine_ % engine_ids_.size()];
-      next_engine_ = (next_engine_ + 1) % (int)engine_ids_.size();
+      const uint32_t eng = engine_ids_[(size_t)(next_engine_.fetch_add(1) & 0x7fffffff) % engine_ids_.size()];
       st = hsa_amd_memory_async_copy_on_engine(d, cpu_, s, gpu_, len, 0, nullptr, sig,
                                                (hsa_amd_sdma_engine_id_t)eng, false);
     }

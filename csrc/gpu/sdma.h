@@ -16,7 +16,10 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <atomic>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -25,6 +28,9 @@ namespace gpu {
 
 class SdmaEngine {
  public:
+  // Process-wide engine of a device (created on first use, never destroyed): reduce tasks of one
+  // process share the device's delivery engine and its cache of pinned ring blocks.
+  static SdmaEngine& for_device(int device);
   // `device` is a HIP ordinal; the HSA GPU agent is matched by PCI domain/BDF.
   explicit SdmaEngine(int device);
   ~SdmaEngine();
@@ -34,6 +40,9 @@ class SdmaEngine {
   // Pinned host memory on the GPU's nearest NUMA node, accessible to the GPU (SDMA target).
   void* alloc_host(size_t bytes);
   void free_host(void* p);
+  // Cached variant for per-task rings: blocks of exactly `bytes` are reused after release_ring().
+  void* acquire_ring(size_t bytes);
+  void release_ring(void* p, size_t bytes);
 
   // Completion signal (value counts outstanding copies; 0 = done).
   hsa_signal_t make_signal();
@@ -56,8 +65,10 @@ class SdmaEngine {
   hsa_amd_memory_pool_t host_pool_{};
   std::vector<uint32_t> engine_ids_;  // SDMA engine bits usable for CPU <- GPU copies
   int numa_node_ = -1;
-  int next_engine_ = 0;
+  std::atomic<int> next_engine_{0};
   bool hsa_inited_ = false;
+  std::mutex ring_mu_;
+  std::multimap<size_t, void*> ring_cache_;
 };
 
 // Linux NUMA node of the HIP device (sysfs), -1 if unknown; and pinning the calling thread to the

@@ -43,6 +43,11 @@ struct FetchAck {
 };
 
 constexpr int kMofPathMax = 600;       // NETLEV_MOF_PATH_MAX_SIZE (NetlevComm.h:31)
+// FetchRequest.buf_len of a descriptor fetch: the provider answers with the partition's device
+// address in FetchAck.path (see csrc/gpu/device_ptr.h) and sends no bytes; a MOF that is not
+// device-resident answers kNotDeviceResident and the reducer fetches bytes instead.
+constexpr int64_t kDescriptorFetch = -1;
+constexpr int kNotDeviceResident = -12;
 constexpr int kFetchReqMax = 800;      // NETLEV_FETCH_REQSIZE (NetlevComm.h:30)
 
 std::string format_rts(const FetchRequest& r, uint64_t remote_addr, uint64_t req_ptr);

@@ -76,6 +76,14 @@ int uda_provider_register_mof(uda_handle* h, const char* job_id, const char* map
                               const void* data, int64_t len, const int64_t* index,
                               int32_t num_partitions);
 
+/* Provider extension: register an HBM-resident MOF: `data` is device memory of HIP device `device`
+ * (-1 = host memory, same as uda_provider_register_mof). Reducers on the GPU backend fetch a
+ * descriptor of each partition (device address, or an IPC handle across processes) and merge it in
+ * place; other reducers get the bytes through a device-to-host copy. */
+int uda_provider_register_mof_device(uda_handle* h, const char* job_id, const char* map_id,
+                                     const void* data, int64_t len, const int64_t* index,
+                                     int32_t num_partitions, int32_t device);
+
 /* Consumer/provider statistics as a JSON object (bytes fetched, GB/s, wait time, ...). */
 int uda_stats_json(uda_handle* h, char* out, int32_t outlen);
 

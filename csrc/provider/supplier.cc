@@ -5,6 +5,7 @@
 
 #include <cstring>
 
+#include "../gpu/device_ptr.h"
 #include "uda/log.h"
 
 namespace uda {
@@ -50,9 +51,16 @@ void Supplier::stop() {
 }
 
 void Supplier::register_mof(const std::string& job, const std::string& map, const uint8_t* data, int64_t len,
-                            std::vector<IndexRec> index) {
+                            std::vector<IndexRec> index, int device) {
+  MemMof m{data, len, std::move(index)};
+  m.device = device;
+  if (device >= 0) {
+    const gpu::IpcExport ex = gpu::ipc_export(data);
+    m.ipc_handle = ex.handle_hex;
+    m.ipc_base = ex.base;
+  }
   std::lock_guard<std::mutex> g(idx_mu_);
-  mem_[job + "|" + map] = MemMof{data, len, std::move(index)};
+  mem_[job + "|" + map] = std::move(m);
 }
 
 void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
@@ -168,6 +176,25 @@ void Supplier::process(Job& j) {
   ack.part_len = rec.part_length;
   ack.mof_offset = rec.start_offset;
   ack.path = rec.path;
+  if (j.req.buf_len == kDescriptorFetch) {
+    // zero-copy fetch: the reducer reads the partition where it lives (RDMA WRITE analogue)
+    if (!mem || mem->device < 0) {
+      ack.status = kNotDeviceResident;
+      ack.error = "MOF is not device-resident";
+    } else if (rec.start_offset + rec.part_length > mem->len) {
+      ack.status = -4;
+      ack.error = "index beyond registered MOF";
+    } else {
+      gpu::IpcExport ex;
+      ex.handle_hex = mem->ipc_handle;
+      ex.base = mem->ipc_base;
+      ack.path = gpu::make_device_descriptor(mem->device, mem->data + rec.start_offset, ex);
+      ack.sent = 0;
+      descriptors_++;
+    }
+    j.done(ack);
+    return;
+  }
   const int64_t remaining = rec.part_length - j.req.fetched;
   const int64_t len = std::max<int64_t>(0, std::min<int64_t>(remaining, j.req.buf_len));
   ack.sent = len;
@@ -183,7 +210,10 @@ void Supplier::process(Job& j) {
       j.done(ack);
       return;
     }
-    std::memcpy(j.dst, mem->data + off, (size_t)len);
+    if (mem->device >= 0)
+      gpu::copy_device_to_host(j.dst, mem->data + off, len);
+    else
+      std::memcpy(j.dst, mem->data + off, (size_t)len);
     bytes_ += len;
     j.done(ack);
     return;

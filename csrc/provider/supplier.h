@@ -42,14 +42,17 @@ class Supplier : public DataServer {
   void start();
   void stop();
 
-  // In-memory MOF registration: index[p] = {start_offset, raw_length, part_length}.
+  // In-memory MOF registration: index[p] = {start_offset, raw_length, part_length}. device >= 0:
+  // `data` is device memory of that HIP device (an HBM-resident MOF): descriptor fetches get its
+  // address / IPC handle instead of bytes, byte fetches are served by a device-to-host copy.
   void register_mof(const std::string& job, const std::string& map, const uint8_t* data, int64_t len,
-                    std::vector<IndexRec> index);
+                    std::vector<IndexRec> index, int device = -1);
   void serve(const FetchRequest& req, uint8_t* dst, FetchDone done) override;
 
   int port() const { return server_ ? server_->port() : -1; }
   int64_t requests() const { return requests_.load(); }
   int64_t bytes_served() const { return bytes_.load(); }
+  int64_t descriptors_served() const { return descriptors_.load(); }
   const char* io_backend() const { return aio_ ? aio_->backend() : "none"; }
 
  private:
@@ -62,6 +65,9 @@ class Supplier : public DataServer {
     const uint8_t* data;
     int64_t len;
     std::vector<IndexRec> index;
+    int device = -1;
+    std::string ipc_handle;           // device MOFs: IPC handle (hex) of the containing allocation
+    const uint8_t* ipc_base = nullptr;
   };
   struct OpenFile {
     int fd = -1;
@@ -90,7 +96,7 @@ class Supplier : public DataServer {
   std::mutex fd_mu_;
   std::unordered_map<std::string, OpenFile> fds_;
   uint64_t fd_clock_ = 0;
-  std::atomic<int64_t> requests_{0}, bytes_{0};
+  std::atomic<int64_t> requests_{0}, bytes_{0}, descriptors_{0};
 };
 
 }  // namespace uda

@@ -15,6 +15,7 @@
 #include "block_decoder.h"
 #include "device_engine.h"
 #include "exchange.h"
+#include "api_bench.h"
 #include "generic_merger.h"
 #include "j2c_sink.h"
 #include "uda/aio.h"
@@ -500,6 +501,12 @@ PYBIND11_MODULE(_uda_native, m) {
              return uda_provider_register_mof(b.h, job.c_str(), map.c_str(), keep->data(), (int64_t)keep->size(),
                                               index.data(), (int32_t)(index.size() / 3));
            })
+      .def("register_mof_device",
+           [](PyBridge& b, const std::string& job, const std::string& map, uintptr_t dev_ptr, int64_t len,
+              const std::vector<int64_t>& index, int device) {
+             return uda_provider_register_mof_device(b.h, job.c_str(), map.c_str(), reinterpret_cast<const void*>(dev_ptr),
+                                                     len, index.data(), (int32_t)(index.size() / 3), device);
+           })
       .def("stats", [](PyBridge& b) {
         std::vector<char> buf(4096);
         uda_stats_json(b.h, buf.data(), (int32_t)buf.size());
@@ -681,7 +688,42 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("buffers", &gpu::J2CSink::buffers)
       .def("eof", &gpu::J2CSink::eof)
       .def("error", &gpu::J2CSink::error)
+      .def("order_errors", &gpu::J2CSink::order_errors)
+      .def("set_check_order", &gpu::J2CSink::set_check_order)
       .def("reset", &gpu::J2CSink::reset);
+
+  py::class_<gpu::ApiTeraSortBench>(m, "ApiTeraSortBench")
+      .def(py::init([](const py::dict& d) {
+        gpu::ApiBenchConfig c;
+        auto get = [&](const char* k, auto& field) {
+          if (d.contains(k)) field = d[k].cast<std::decay_t<decltype(field)>>();
+        };
+        get("device", c.device);
+        get("maps", c.maps);
+        get("reducers", c.reducers);
+        get("records_per_map", c.records_per_map);
+        get("seed", c.seed);
+        get("kv_buf_bytes", c.kv_buf_bytes);
+        get("round_bytes", c.round_bytes);
+        return new gpu::ApiTeraSortBench(c);
+      }))
+      .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
+      .def("step",
+           [](gpu::ApiTeraSortBench& b, bool validate) {
+             std::string info;
+             std::map<std::string, double> r;
+             {
+               py::gil_scoped_release g;
+               r = b.step(validate, &info);
+             }
+             py::dict d;
+             for (auto& kv : r) d[kv.first.c_str()] = kv.second;
+             d["task0_stats"] = info;
+             return d;
+           },
+           py::arg("validate") = false)
+      .def("expected_records", &gpu::ApiTeraSortBench::expected_records)
+      .def_property_readonly("store_bytes", &gpu::ApiTeraSortBench::store_bytes);
 
   py::class_<gpu::ShuffleJob>(m, "ShuffleJob")
       .def(py::init([](const py::dict& cfg) { return new gpu::ShuffleJob(config_from_dict(cfg)); }))
@@ -750,6 +792,8 @@ PYBIND11_MODULE(_uda_native, m) {
              auto v = j.read_partition(mp, d);
              return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
            })
+      .def("mof_device_ptr", [](gpu::ShuffleJob& j, int m) { return (uintptr_t)j.mof_device_ptr(m); })
+      .def("mof_bytes", &gpu::ShuffleJob::mof_bytes)
       .def_property_readonly("store_bytes", &gpu::ShuffleJob::store_bytes)
       .def_property_readonly("max_round_records", &gpu::ShuffleJob::max_round_records);
 }

@@ -62,6 +62,21 @@ class UdaProvider:
         if self.bridge.register_mof(job_id, map_id, data, flat) != 0:
             raise RuntimeError("register_mof failed")
 
+    def add_mof_device(self, job_id: str, map_id: str, data: bytes, index: list, device: int = 0):
+        """Register an HBM-resident MOF: `data` is copied to device `device` (a torch tensor kept
+        alive by the provider) and reducers on the GPU backend merge its partitions in place."""
+        import torch
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(f"cuda:{device}")
+        self._keep = getattr(self, "_keep", [])
+        self._keep.append(t)
+        self.add_mof_device_ptr(job_id, map_id, t.data_ptr(), t.numel(), index, device)
+        return t
+
+    def add_mof_device_ptr(self, job_id: str, map_id: str, ptr: int, nbytes: int, index: list, device: int = 0):
+        flat = [v for rec in index for v in rec]
+        if self.bridge.register_mof_device(job_id, map_id, ptr, nbytes, flat, device) != 0:
+            raise RuntimeError("register_mof_device failed")
+
     def _get_path(self, job_id: str, map_id: str, reduce_id: int):
         ent = self.mofs.get((job_id, map_id))
         if ent is None or reduce_id >= len(ent[1]):
