@@ -50,6 +50,11 @@ def parse_args(argv=None):
     ap.add_argument("--d2h-piece-mb", type=int, default=128)
     ap.add_argument("--pinned-slots", type=int, default=16)
     ap.add_argument("--d2h-engines", type=int, default=1)
+    ap.add_argument("--store", choices=("hbm", "host", "disk"), default="hbm",
+                    help="map-output store: HBM (default), pinned host DRAM, or MOF files on --local-dirs")
+    ap.add_argument("--local-dirs", default="/tmp", help="--store disk: comma-separated directories")
+    ap.add_argument("--max-round-gb", type=float, default=0.0,
+                    help="bound the HBM staging per round (raises --rounds so a round is at most this size)")
     ap.add_argument("--device-only", action="store_true",
                     help="ablation: stop after the device merge (no host delivery); not the headline")
     ap.add_argument("--no-validate", action="store_true", help="skip the final validated step")
@@ -125,8 +130,12 @@ def main(argv=None) -> int:
     if args.api:
         return run_api(args, ctx)
 
+    rounds = args.rounds
+    if args.max_round_gb > 0:
+        rounds = max(rounds, -(-int(args.rows_per_gpu * RECORD_BYTES) // int(args.max_round_gb * 1e9)))
     cfg = TeraSortConfig(rows_per_gpu=args.rows_per_gpu, maps_per_rank=args.maps_per_gpu,
-                         rounds=args.rounds, reducers=args.reducers, d2h=args.d2h,
+                         rounds=rounds, reducers=args.reducers, d2h=args.d2h, store=args.store,
+                         local_dirs=args.local_dirs,
                          d2h_piece_bytes=args.d2h_piece_mb << 20, pinned_slots=args.pinned_slots,
                          d2h_engines=args.d2h_engines, deliver_host=not args.device_only)
     job = TeraSortShuffle(ctx, cfg)
@@ -139,6 +148,7 @@ def main(argv=None) -> int:
         print(f"# setup {t_setup:.1f}s cpus={len(os.sched_getaffinity(0))} {job.setup_s} "
               f"store={job.job.store_bytes/1e9:.1f}GB "
               f"max_round_records={job.job.max_round_records} exchange={job.job.exchange_name} "
+              f"store={job.job.store_name} "
               f"delivery={job.job.delivery_name}", file=sys.stderr, flush=True)
 
     for i in range(args.warmup):
@@ -190,6 +200,8 @@ def main(argv=None) -> int:
             "vs_baseline": None,
             "dtype": "bytes",
             "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "breakdown_note": "comm/merge: device-event spans per round; d2h: summed piece latency; "
+                              "wait_out: merge waiting for a free output slot (delivery-bound)",
             "config": {
                 "model": "terasort",
                 "global_batch": int(args.rows_per_gpu) * ctx.world,
@@ -199,7 +211,8 @@ def main(argv=None) -> int:
                 "total_rows": args.rows_per_gpu * ctx.world,
                 "maps_per_gpu": args.maps_per_gpu,
                 "reducers_per_gpu": args.reducers,
-                "rounds": args.rounds,
+                "rounds": rounds,
+                "store": job.job.store_name,
                 "shuffle": job.job.exchange_name if ctx.world > 1 else "local (single GPU, no all-to-all)",
                 "delivery": "device-only (ablation)" if args.device_only else
                             f"{job.job.delivery_name} -> buffers dropped unread (ablation)" if args.sink == "none" else

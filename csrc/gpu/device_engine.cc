@@ -5,6 +5,7 @@
 #include "uda/trace.h"
 
 #include <rccl/rccl.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -283,7 +284,8 @@ ShuffleJob::ShuffleJob(const ShuffleConfig& cfg) : cfg_(cfg) {
   if (cfg_.reducers < 1) cfg_.reducers = 1;
   if (cfg_.pinned_slots < 2) cfg_.pinned_slots = 2;
   if (cfg_.d2h != "sdma" && cfg_.d2h != "hip") throw std::runtime_error("ShuffleJob: d2h must be sdma or hip");
-  if (cfg_.store != "hbm" && cfg_.store != "host") throw std::runtime_error("unknown store tier " + cfg_.store);
+  if (cfg_.store != "hbm" && cfg_.store != "host" && cfg_.store != "disk")
+    throw std::runtime_error("unknown store tier " + cfg_.store);
   R_ = cfg_.reducers;
   Q_ = cfg_.rounds;
   C_ = R_ * Q_;
@@ -339,6 +341,8 @@ void ShuffleJob::init_comm(const std::string& uid) {
 void ShuffleJob::init_local() {
   if (cfg_.world == 1) return;
   if (cfg_.local_group.empty()) throw std::runtime_error("init_local: config.local_group is empty");
+  if (disk_store())  // peers would pull from a staging buffer this rank reuses next round
+    throw std::runtime_error("init_local: the disk store needs the RCCL exchange (one process per GPU)");
   HIP_CHECK(hipSetDevice(cfg_.device));
   exchange_ = make_local_exchange(cfg_.local_group, cfg_.rank, cfg_.world);
 }
@@ -369,7 +373,18 @@ void ShuffleJob::generate() {
   }
   mof_off_[M] = off;
   store_bytes_ = off;
-  if (host_store()) {
+  if (disk_store()) {
+    std::vector<std::string> dirs;
+    for (size_t b = 0; b <= cfg_.local_dirs.size();) {
+      const size_t e = cfg_.local_dirs.find(',', b);
+      const std::string d = cfg_.local_dirs.substr(b, e == std::string::npos ? std::string::npos : e - b);
+      if (!d.empty()) dirs.push_back(d);
+      if (e == std::string::npos) break;
+      b = e + 1;
+    }
+    disk_.reset(new DiskStore(cfg_.device, dirs, std::to_string(getpid()) + "." + std::to_string(cfg_.rank), M));
+    store_base_ = store_dev_base_ = nullptr;
+  } else if (host_store()) {
     hstore_.alloc((size_t)store_bytes_);
     store_base_ = hstore_.as<uint8_t>();
     void* dp = nullptr;
@@ -384,16 +399,16 @@ void ShuffleJob::generate() {
   std::vector<uint64_t> key_lo(nruns), key_span(nruns), seeds(nruns);
   const uint64_t step = (W == 1) ? ~0ull : (~0ull / (uint64_t)W);
   int64_t max_n = 0, max_mof = 0;
-  DeviceBuffer tmp;  // host tier: one MOF at a time is generated in HBM, then copied out
-  if (host_store()) {
+  DeviceBuffer tmp;  // host/disk tier: one MOF at a time is generated in HBM, then copied out
+  if (spilled()) {
     for (int m = 0; m < M; ++m) max_mof = std::max(max_mof, mof_off_[m + 1] - mof_off_[m]);
     tmp.alloc((size_t)max_mof);
   }
   for (int m = 0; m < M; ++m)
     for (int d = 0; d < W; ++d) {
       const int r = m * W + d;
-      bases[r] = store_dev_base_ + run_off_[r];
-      gen_bases[r] = host_store() ? tmp.as<uint8_t>() + (run_off_[r] - mof_off_[m]) : bases[r];
+      bases[r] = disk_store() ? nullptr : store_dev_base_ + run_off_[r];
+      gen_bases[r] = spilled() ? tmp.as<uint8_t>() + (run_off_[r] - mof_off_[m]) : bases[r];
       key_lo[r] = step * (uint64_t)d;
       key_span[r] = step;
       const uint64_t gmap = (uint64_t)cfg_.rank * M + m;
@@ -408,7 +423,7 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(d_sp.as(), key_span.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sd.as(), seeds.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemset(d_ck.as(), 0, nruns * 8));
-  if (!host_store()) {
+  if (!spilled()) {
     launch_teragen(d_b.as<uint8_t*>(), d_n.as<int64_t>(), d_lo.as<uint64_t>(), d_sp.as<uint64_t>(),
                    d_sd.as<uint64_t>(), nruns, max_n, d_ck.as<unsigned long long>(), s_compute_);
     HIP_CHECK(hipGetLastError());
@@ -419,8 +434,11 @@ void ShuffleJob::generate() {
                      d_sp.as<uint64_t>() + m * W, d_sd.as<uint64_t>() + m * W, W, max_n,
                      d_ck.as<unsigned long long>() + m * W, s_compute_);
       HIP_CHECK(hipGetLastError());
-      HIP_CHECK(hipMemcpyAsync(store_base_ + mof_off_[m], tmp.as(), (size_t)(mof_off_[m + 1] - mof_off_[m]),
-                               hipMemcpyDeviceToHost, s_compute_));
+      if (disk_store())  // map output written to its MOF file (O_DIRECT through io_uring)
+        disk_->write_file(m, tmp.as<uint8_t>(), mof_off_[m + 1] - mof_off_[m], s_compute_);
+      else
+        HIP_CHECK(hipMemcpyAsync(store_base_ + mof_off_[m], tmp.as(), (size_t)(mof_off_[m + 1] - mof_off_[m]),
+                                 hipMemcpyDeviceToHost, s_compute_));
     }
     HIP_CHECK(hipStreamSynchronize(s_compute_));
   }
@@ -443,7 +461,32 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(d_run_nrec_.as(), run_nrec_.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_bound_set_.as(), bset.data(), nruns * sizeof(int), hipMemcpyHostToDevice));
   UDA_LOG(kInfo, "rank %d generated %d MOFs, %ld bytes in %s", cfg_.rank, M, (long)store_bytes_,
-          host_store() ? "pinned host DRAM" : "HBM");
+          store_name().c_str());
+}
+
+std::string ShuffleJob::store_name() const {
+  if (disk_) return disk_->describe();
+  return host_store() ? "pinned host DRAM" : "HBM";
+}
+
+void ShuffleJob::for_run_batches(
+    const std::function<void(int, int, uint8_t* const*, const int64_t*, const int*)>& fn) {
+  const int M = cfg_.maps_per_rank, W = cfg_.world;
+  if (!disk_store()) {
+    fn(0, M * W, d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), d_bound_set_.as<int>());
+    return;
+  }
+  int64_t max_mof = 0;
+  for (int m = 0; m < M; ++m) max_mof = std::max(max_mof, mof_off_[m + 1] - mof_off_[m]);
+  DeviceBuffer tmp((size_t)max_mof), d_b((size_t)W * sizeof(uint8_t*));
+  std::vector<uint8_t*> b(W);
+  for (int m = 0; m < M; ++m) {
+    disk_->stage({DiskStore::Piece{m, 0, mof_off_[m + 1] - mof_off_[m], tmp.as<uint8_t>()}}, s_compute_);
+    for (int d = 0; d < W; ++d) b[d] = tmp.as<uint8_t>() + (run_off_[m * W + d] - mof_off_[m]);
+    HIP_CHECK(hipMemcpyAsync(d_b.as(), b.data(), (size_t)W * sizeof(uint8_t*), hipMemcpyHostToDevice, s_compute_));
+    fn(m * W, W, d_b.as<uint8_t*>(), d_run_nrec_.as<int64_t>() + m * W, d_bound_set_.as<int>() + m * W);
+    HIP_CHECK(hipStreamSynchronize(s_compute_));  // tmp is reused by the next MOF
+  }
 }
 
 std::vector<int64_t> ShuffleJob::index_record(int m, int d) const {
@@ -456,6 +499,7 @@ std::vector<int64_t> ShuffleJob::index_record(int m, int d) const {
 
 std::vector<uint8_t> ShuffleJob::read_partition(int m, int d) const {
   auto ir = index_record(m, d);
+  if (disk_) return disk_->read_host(m, ir[0], ir[2]);
   std::vector<uint8_t> out((size_t)ir[2]);
   HIP_CHECK(hipMemcpy(out.data(), store_base_ + mof_off_[m] + ir[0], out.size(),
                       host_store() ? hipMemcpyHostToHost : hipMemcpyDeviceToHost));
@@ -476,9 +520,15 @@ std::vector<std::vector<uint64_t>> ShuffleJob::sample_keys(int64_t every) {
   std::vector<std::vector<uint64_t>> out(W);
   if (total == 0) return out;
   DeviceBuffer d_off((nruns + 1) * 8), d_out(total * sizeof(Elem));
-  HIP_CHECK(hipMemcpy(d_off.as(), soff.data(), (nruns + 1) * 8, hipMemcpyHostToDevice));
-  launch_sample_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), nruns, every, d_off.as<int64_t>(), total,
-                      d_out.as<Elem>(), s_compute_);
+  for_run_batches([&](int r0, int nr, uint8_t* const* bases, const int64_t* nrec, const int*) {
+    std::vector<int64_t> rel(nr + 1);  // this batch's sample offsets, relative to its first sample
+    for (int k = 0; k <= nr; ++k) rel[k] = soff[r0 + k] - soff[r0];
+    if (rel[nr] == 0) return;
+    HIP_CHECK(hipMemcpyAsync(d_off.as<int64_t>() + r0, rel.data(), (nr + 1) * 8, hipMemcpyHostToDevice, s_compute_));
+    launch_sample_fixed(bases, nrec, nr, every, d_off.as<int64_t>() + r0, rel[nr], d_out.as<Elem>() + soff[r0],
+                        s_compute_);
+    HIP_CHECK(hipStreamSynchronize(s_compute_));  // rel is reused
+  });
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   std::vector<Elem> h(total);
   HIP_CHECK(hipMemcpy(h.data(), d_out.as(), total * sizeof(Elem), hipMemcpyDeviceToHost));
@@ -512,8 +562,10 @@ void ShuffleJob::compute_plans() {
   if (C_ > 1 && bounds_.empty()) throw std::runtime_error("reducers*rounds > 1 requires set_bounds()");
   const int64_t per = C_ + 1;
   d_split_out_.alloc((size_t)nruns * per * 8);
-  launch_split_fixed(d_run_bases_.as<uint8_t*>(), d_run_nrec_.as<int64_t>(), C_ > 1 ? d_bounds_.as<Elem>() : nullptr,
-                     d_bound_set_.as<int>(), nruns, C_ - 1, d_split_out_.as<int64_t>(), s_compute_);
+  for_run_batches([&](int r0, int nr, uint8_t* const* bases, const int64_t* nrec, const int* bset) {
+    launch_split_fixed(bases, nrec, C_ > 1 ? d_bounds_.as<Elem>() : nullptr, bset, nr, C_ - 1,
+                       d_split_out_.as<int64_t>() + (size_t)r0 * per, s_compute_);
+  });
   split_pos_.assign((size_t)nruns * per, 0);
   HIP_CHECK(hipMemcpyAsync(split_pos_.data(), d_split_out_.as(), split_pos_.size() * 8, hipMemcpyDeviceToHost,
                            s_compute_));
@@ -534,32 +586,42 @@ void ShuffleJob::compute_plans() {
   } else {
     if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
     exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), n_per_peer, s_comm_);
-    // checksums of every slice this rank sends, in the same [p][q][i][m] layout
-    std::vector<RunDesc> sl((size_t)W * n_per_peer);
-    int64_t max_n = 0;
+    // checksums of every slice this rank sends: per (run, cell) in run batches, then laid out
+    // [p][q][i][m] like the counts
+    std::vector<int64_t> cell_ck((size_t)nruns * C_, 0);
+    DeviceBuffer d_sl((size_t)nruns * C_ * sizeof(RunDesc)), d_ck((size_t)nruns * C_ * 8);
+    for_run_batches([&](int r0, int nr, uint8_t* const* bases, const int64_t*, const int*) {
+      std::vector<uint8_t*> hb(nr);
+      HIP_CHECK(hipMemcpyAsync(hb.data(), bases, (size_t)nr * sizeof(uint8_t*), hipMemcpyDeviceToHost, s_compute_));
+      HIP_CHECK(hipStreamSynchronize(s_compute_));
+      std::vector<RunDesc> sl((size_t)nr * C_);
+      int64_t max_n = 0;
+      for (int k = 0; k < nr; ++k)
+        for (int c = 0; c < C_; ++c) {
+          RunDesc& d = sl[(size_t)k * C_ + c];
+          d.base = hb[k] + pos(r0 + k, c) * kTeraRecordBytes;
+          d.nrec = pos(r0 + k, c + 1) - pos(r0 + k, c);
+          d.nbytes = d.nrec * kTeraRecordBytes;
+          d.offsets = nullptr;
+          max_n = std::max(max_n, d.nrec);
+        }
+      HIP_CHECK(hipMemcpyAsync(d_sl.as(), sl.data(), sl.size() * sizeof(RunDesc), hipMemcpyHostToDevice, s_compute_));
+      for (size_t b = 0; b < sl.size(); b += 65535) {
+        const int n = (int)std::min<size_t>(65535, sl.size() - b);
+        launch_slice_checksums(d_sl.as<RunDesc>() + b, n, max_n, d_ck.as<unsigned long long>() + b, s_compute_);
+      }
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpyAsync(cell_ck.data() + (size_t)r0 * C_, d_ck.as(), sl.size() * 8, hipMemcpyDeviceToHost,
+                               s_compute_));
+      HIP_CHECK(hipStreamSynchronize(s_compute_));
+    });
+    std::vector<int64_t> sl((size_t)W * n_per_peer);
     for (int p = 0; p < W; ++p)
       for (int q = 0; q < Q_; ++q)
         for (int i = 0; i < R_; ++i)
-          for (int m = 0; m < M; ++m) {
-            const int r = m * W + p, c = i * Q_ + q;
-            RunDesc d;
-            d.base = store_dev_base_ + run_off_[r] + pos(r, c) * kTeraRecordBytes;
-            d.nrec = pos(r, c + 1) - pos(r, c);
-            d.nbytes = d.nrec * kTeraRecordBytes;
-            d.offsets = nullptr;
-            max_n = std::max(max_n, d.nrec);
-            sl[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = d;
-          }
-    DeviceBuffer d_sl(sl.size() * sizeof(RunDesc)), d_ck(sl.size() * 8);
-    HIP_CHECK(hipMemcpy(d_sl.as(), sl.data(), sl.size() * sizeof(RunDesc), hipMemcpyHostToDevice));
-    for (size_t b = 0; b < sl.size(); b += 65535) {
-      const int n = (int)std::min<size_t>(65535, sl.size() - b);
-      launch_slice_checksums(d_sl.as<RunDesc>() + b, n, max_n, d_ck.as<unsigned long long>() + b, s_compute_);
-    }
-    HIP_CHECK(hipGetLastError());
-    std::vector<int64_t> send_ck(sl.size());
-    HIP_CHECK(hipStreamSynchronize(s_compute_));
-    HIP_CHECK(hipMemcpy(send_ck.data(), d_ck.as(), send_ck.size() * 8, hipMemcpyDeviceToHost));
+          for (int m = 0; m < M; ++m)
+            sl[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = cell_ck[(size_t)(m * W + p) * C_ + i * Q_ + q];
+    const std::vector<int64_t>& send_ck = sl;
     recv_ck.assign(send_ck.size(), 0);
     exchange_->alltoall_i64(send_ck.data(), recv_ck.data(), n_per_peer, s_comm_);
   }
@@ -585,6 +647,7 @@ void ShuffleJob::compute_plans() {
           const int r = m * W + p, c = i * Q_ + q;
           const int64_t cnt = pos(r, c + 1) - pos(r, c);
           if (cnt <= 0) continue;
+          // disk store: the span holds the file offset (staged at run time, see run_step)
           rp.send[p].push_back(Span{store_base_ + run_off_[r] + pos(r, c) * kTeraRecordBytes, cnt * kTeraRecordBytes});
           rp.send_bytes += cnt * kTeraRecordBytes;
         }
@@ -601,7 +664,7 @@ void ShuffleJob::compute_plans() {
           const int64_t cnt = recv_counts[(size_t)s * n_per_peer + ((size_t)q * R_ + i) * M + j];
           rp.recv_cnt[x] = cnt;
           rp.group_recs[i] += cnt;
-          if (s == me && !host_store()) continue;  // read in place from the HBM store
+          if (s == me && !spilled()) continue;  // read in place from the HBM store
           rp.recv_off[x] = off;
           off += cnt * kTeraRecordBytes;
         }
@@ -643,7 +706,7 @@ void ShuffleJob::compute_plans() {
     recv_slots_.resize(kSlots);
     for (auto& b : recv_slots_) b.alloc((size_t)std::max<int64_t>(max_slot_bytes, 16));
   }
-  if (W > 1 && host_store() && std::string(exchange_->name()).rfind("rccl", 0) == 0)
+  if (W > 1 && spilled() && std::string(exchange_->name()).rfind("rccl", 0) == 0)
     send_staging_.alloc((size_t)std::max<int64_t>(max_send, 16));
   if (W > 1) exchange_->reserve(max_send);
   d_validate_.alloc(64 + (size_t)2 * R_ * sizeof(Elem));
@@ -904,16 +967,22 @@ StepStats ShuffleJob::run_step(bool validate) {
     if (staged()) {
       if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged_ev_[slot], 0));  // slot consumed
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
-      if (host_store()) {  // spill tier: this round's own cells stream H2D (SDMA) into the slot
+      if (spilled()) {  // spill tiers: this round's own cells stream into the slot (SDMA H2D)
+        std::vector<DiskStore::Piece> pieces;
         for (int i = 0; i < R_; ++i)
           for (int j = 0; j < M; ++j) {
             const size_t x = ((size_t)me * R_ + i) * M + j;
             const int64_t cnt = rp.recv_cnt[x];
             if (cnt <= 0) continue;
-            HIP_CHECK(hipMemcpyAsync(rbuf + rp.recv_off[x], run_base(j, me) + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes,
-                                     (size_t)(cnt * kTeraRecordBytes), hipMemcpyHostToDevice, s_comm_));
+            const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+            if (disk_store())
+              pieces.push_back(DiskStore::Piece{j, at - mof_off_[j], cnt * kTeraRecordBytes, rbuf + rp.recv_off[x]});
+            else
+              HIP_CHECK(hipMemcpyAsync(rbuf + rp.recv_off[x], store_base_ + at, (size_t)(cnt * kTeraRecordBytes),
+                                       hipMemcpyHostToDevice, s_comm_));
             st.bytes_h2d += cnt * kTeraRecordBytes;
           }
+        if (!pieces.empty()) disk_->stage(pieces, s_comm_);  // io_uring reads overlap the merge of q-1
       }
       if (W > 1) {
         std::vector<std::vector<Span>> recv(W);
@@ -927,16 +996,24 @@ StepStats ShuffleJob::run_step(bool validate) {
         }
         if (rccl_staging) {  // spill tier over RCCL: stage outgoing slices per peer, one message each
           std::vector<std::vector<Span>> send(W);
+          std::vector<DiskStore::Piece> pieces;
           int64_t off = 0;
           for (int p = 0; p < W; ++p) {
             const int64_t beg = off;
             for (const Span& sp : rp.send[p]) {
-              HIP_CHECK(hipMemcpyAsync(send_staging_.as<uint8_t>() + off, sp.ptr, (size_t)sp.bytes,
-                                       hipMemcpyHostToDevice, s_comm_));
+              if (disk_store()) {  // the span holds the store offset of the slice
+                const int64_t at = (int64_t)(uintptr_t)sp.ptr;
+                const int m = (int)(std::upper_bound(mof_off_.begin(), mof_off_.end(), at) - mof_off_.begin()) - 1;
+                pieces.push_back(DiskStore::Piece{m, at - mof_off_[m], sp.bytes, send_staging_.as<uint8_t>() + off});
+              } else {
+                HIP_CHECK(hipMemcpyAsync(send_staging_.as<uint8_t>() + off, sp.ptr, (size_t)sp.bytes,
+                                         hipMemcpyHostToDevice, s_comm_));
+              }
               off += sp.bytes;
             }
             if (off > beg) send[p].push_back(Span{send_staging_.as<uint8_t>() + beg, off - beg});
           }
+          if (!pieces.empty()) disk_->stage(pieces, s_comm_);
           st.bytes_h2d += off;
           exchange_->exchange(send, recv, s_comm_);
         } else {

@@ -40,6 +40,7 @@
 
 #include "exchange.h"
 #include "kernels.h"
+#include "disk_store.h"
 #include "sdma.h"
 
 namespace uda {
@@ -201,7 +202,8 @@ struct ShuffleConfig {
   bool deliver_host = true;              // false: stop after the device merge (ablation)
   bool validate = false;                 // device-side order/checksum/exchange checks every step
   std::string local_group;               // world > 1 without RCCL: ranks are threads of one process
-  std::string store = "hbm";             // map-output store: "hbm" or "host" (pinned DRAM spill tier)
+  std::string store = "hbm";             // map-output store: "hbm", "host" (pinned DRAM) or "disk"
+  std::string local_dirs;                // store=disk: comma-separated directories for the MOF files
 };
 
 struct StepStats {
@@ -264,6 +266,7 @@ class ShuffleJob {
   std::string delivery_name() const;
   // Index record of (local map m, destination GPU d): offset, rawLength, partLength within MOF m.
   std::vector<int64_t> index_record(int m, int d) const;
+  std::string store_name() const;
   // Copy a MOF partition (records + EOF) to host (tests / provider fallback path).
   std::vector<uint8_t> read_partition(int m, int d) const;
 
@@ -287,11 +290,17 @@ class ShuffleJob {
   // tier); kernels use the device-mapped addresses in d_run_bases_.
   uint8_t* run_base(int m, int d) const { return store_base_ + run_off_[m * cfg_.world + d]; }
   bool host_store() const { return cfg_.store == "host"; }
-  bool staged() const { return cfg_.world > 1 || host_store(); }
+  bool disk_store() const { return cfg_.store == "disk"; }
+  bool spilled() const { return host_store() || disk_store(); }  // own cells are staged, not read in place
+  bool staged() const { return cfg_.world > 1 || spilled(); }
+  // fn(r0, nr, bases, nrec, bound_set) over batches of runs whose records are device-readable: all
+  // runs at once for the HBM / host stores, one MOF at a time (loaded from disk) for the disk store.
+  void for_run_batches(const std::function<void(int, int, uint8_t* const*, const int64_t*, const int*)>& fn);
 
   ShuffleConfig cfg_;
   int R_ = 1, Q_ = 1, C_ = 1;  // reducers, rounds, cells (R*Q) per GPU
   std::unique_ptr<Exchange> exchange_;
+  std::unique_ptr<DiskStore> disk_;
   hipStream_t s_comm_ = nullptr, s_compute_ = nullptr, s_copy_ = nullptr;
   DeviceBuffer store_;
   PinnedBuffer hstore_;

@@ -78,6 +78,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("validate", c.validate);
   get("local_group", c.local_group);
   get("store", c.store);
+  get("local_dirs", c.local_dirs);
   return c;
 }
 
@@ -784,6 +785,7 @@ PYBIND11_MODULE(_uda_native, m) {
       .def_property_readonly("comm_ranks", &gpu::ShuffleJob::comm_ranks)
       .def_property_readonly("exchange_name", &gpu::ShuffleJob::exchange_name)
       .def_property_readonly("delivery_name", &gpu::ShuffleJob::delivery_name)
+      .def_property_readonly("store_name", &gpu::ShuffleJob::store_name)
       .def("local_dest_checksums", &gpu::ShuffleJob::local_dest_checksums)
       .def("local_dest_records", &gpu::ShuffleJob::local_dest_records)
       .def("index_record", &gpu::ShuffleJob::index_record)

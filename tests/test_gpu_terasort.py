@@ -157,3 +157,34 @@ def test_rccl_communicator_selftest(require_gpu, native):
     """The RCCL data plane of the multi-GPU shuffle on one device: ncclUniqueId bootstrap and the
     grouped ncclSend/ncclRecv counts exchange (world 1)."""
     assert native.rccl_selftest(0, 4096) == "rccl:ok"
+
+
+@pytest.mark.parametrize("reducers,rounds", [(1, 3), (3, 2)])
+def test_disk_store_tier(require_gpu, tmp_path, reducers, rounds):
+    """Map outputs as MOF files on local disks (the tier for jobs larger than HBM + DRAM): each
+    round's cells are read with io_uring O_DIRECT into a pinned chunk ring and copied to HBM."""
+    d1, d2 = tmp_path / "d1", tmp_path / "d2"
+    d1.mkdir()
+    d2.mkdir()
+    j = _job(30000, 5, rounds, store="disk", local_dirs=f"{d1},{d2}", reducers=reducers, **SMALL)
+    assert j.job.store_name.startswith("disk[")
+    assert len(list(d1.iterdir())) == 3 and len(list(d2.iterdir())) == 2  # MOF files striped
+    readers = [J2CQueueReader(max_len=64 << 10) for _ in range(reducers)]
+    j.use_python_sink(lambda r, b: readers[r].feed(b), with_reducer=True)
+    st = j.step()
+    j.check(st)
+    assert st["bytes_h2d"] == st["bytes_in"]
+    got = [kv for r in readers for kv in r.records]
+    assert got == _sorted_all(j.job.read_partition(m, 0) for m in range(5))
+    del j
+    import gc
+    gc.collect()
+    assert not list(d1.iterdir()) and not list(d2.iterdir())  # files removed with the store
+
+
+def test_disk_store_refuses_local_group(require_gpu, tmp_path):
+    from uda_amd.models.terasort import TeraSortConfig, make_local_group
+    cfg = TeraSortConfig(rows_per_gpu=4000, maps_per_rank=2, rounds=2, store="disk", local_dirs=str(tmp_path),
+                         sample_every=64, **SMALL)
+    with pytest.raises(Exception, match="RCCL"):
+        make_local_group(2, cfg, group="disk2")

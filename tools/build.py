@@ -78,9 +78,9 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
         f"pyflags = {py_inc}",
         f"rule hip\n  command = $hipcc -x hip --offload-arch={ARCH} $cflags -MD -MF $out.d -c $in -o $out\n"
         f"  depfile = $out.d\n  deps = gcc\n  description = HIPCC $in",
-        f"rule cxx\n  command = $hipcc $cflags -MD -MF $out.d -c $in -o $out\n"
+        f"rule cxx\n  command = $hipcc --offload-arch={ARCH} $cflags -MD -MF $out.d -c $in -o $out\n"
         f"  depfile = $out.d\n  deps = gcc\n  description = CXX $in",
-        f"rule cxxpy\n  command = $hipcc $cflags $pyflags -MD -MF $out.d -c $in -o $out\n"
+        f"rule cxxpy\n  command = $hipcc --offload-arch={ARCH} $cflags $pyflags -MD -MF $out.d -c $in -o $out\n"
         f"  depfile = $out.d\n  deps = gcc\n  description = CXX(py) $in",
         f"rule solib\n  command = $hipcc -shared -fPIC --offload-arch={ARCH}{host_san} $in -o $out "
         f"-L{ROCM}/lib -lrccl -lamdhip64 -lhsa-runtime64 -lpthread -ldl -Wl,-rpath,{ROCM}/lib -Wl,-soname,libuda.so\n"
