@@ -23,7 +23,7 @@ int64_t align_upio(int64_t v) { return (v + kAioAlignment - 1) / kAioAlignment *
 
 DiskStore::DiskStore(int device, const std::vector<std::string>& dirs, const std::string& tag, int nfiles,
                      int chunks, int64_t chunk_bytes)
-    : device_(device), nchunks_(std::max(2, chunks)), chunk_(align_upio(std::max<int64_t>(chunk_bytes, 1 << 20))) {
+    : nchunks_(std::max(2, chunks)), chunk_(align_upio(std::max<int64_t>(chunk_bytes, 1 << 20))) {
   std::vector<std::string> d = dirs.empty() ? std::vector<std::string>{"/tmp"} : dirs;
   for (int f = 0; f < nfiles; ++f) {
     const std::string p = d[(size_t)f % d.size()] + "/uda.store." + tag + "." + std::to_string(f);

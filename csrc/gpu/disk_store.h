@@ -52,7 +52,6 @@ class DiskStore {
   std::string describe() const;
 
  private:
-  int device_;
   std::vector<std::string> paths_;
   std::vector<int> fds_;
   std::vector<int64_t> sizes_;  // padded file sizes

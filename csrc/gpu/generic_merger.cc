@@ -16,7 +16,7 @@ namespace gpu {
 void GenericMerger::reserve(int64_t records, int runs) {
   if (records <= cap_records_ && runs <= cap_runs_) return;
   records = std::max<int64_t>(records, 1);
-  const int64_t max_tiles = records / kMergeTile + runs + 2;
+  const int64_t max_tiles = records / kGenericMergeTile + runs + 2;
   elems_a_.alloc((size_t)records * sizeof(Elem));
   elems_b_.alloc((size_t)records * sizeof(Elem));
   splits_.alloc((size_t)max_tiles * 8);
@@ -194,7 +194,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   phase("f2_normalize");
   // ---- F3: merge tree; per-pass descriptors are small host tables uploaded per pass
   std::vector<DeviceBuffer> pass_tabs;
-  for (const MergePassPlan& mp : plan_merge_passes(eoff, {0, (int)eoff.size() - 1})) {
+  for (const MergePassPlan& mp : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
     std::vector<int64_t> tab(mp.pairs);
     tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
     pass_tabs.emplace_back(tab.size() * 8);

@@ -71,7 +71,8 @@ void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nrun
                           Elem* out, int* bad_layout, hipStream_t s);
 
 // ---------------------------------------------------------------- merge tree (F3)
-constexpr int kMergeTile = 2048;  // output elements per workgroup (256 threads x 8)
+constexpr int kMergeTile = 2048;         // FIXED10: output elements per workgroup (256 threads x 8)
+constexpr int kGenericMergeTile = 1024;  // GENERIC: smaller tiles leave LDS for the staged key bytes
 // One merge pass. Pair p merges the adjacent sorted element ranges A = [pairs[3p], pairs[3p+1]) and
 // B = [pairs[3p+1], pairs[3p+2]) into the same index range of the output (B may be empty: the range
 // is copied through). Pair p produces tiles [tile_prefix[p], tile_prefix[p+1]) of kMergeTile

@@ -143,6 +143,7 @@ struct TileGeo {
   int64_t a0, a_len, b_len, d0;
   int pair;
 };
+template <int TILE>
 __device__ __forceinline__ TileGeo tile_geo(const PassDesc& pd, int t) {
   int lo = 0, hi = pd.npairs;  // tile_prefix[lo] <= t < tile_prefix[lo+1]
   while (hi - lo > 1) {
@@ -157,16 +158,16 @@ __device__ __forceinline__ TileGeo tile_geo(const PassDesc& pd, int t) {
   g.a0 = pd.pairs[3 * lo];
   g.a_len = pd.pairs[3 * lo + 1] - g.a0;
   g.b_len = pd.pairs[3 * lo + 2] - pd.pairs[3 * lo + 1];
-  g.d0 = (int64_t)(t - pd.tile_prefix[lo]) * kMergeTile;
+  g.d0 = (int64_t)(t - pd.tile_prefix[lo]) * TILE;
   return g;
 }
 
-template <class Cmp>
+template <int TILE, class Cmp>
 __global__ void __launch_bounds__(256) merge_partition_kernel(const Elem* in, PassDesc pd,
                                                               int64_t* splits, Cmp cmp) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= pd.ntiles) return;
-  const TileGeo g = tile_geo(pd, t);
+  const TileGeo g = tile_geo<TILE>(pd, t);
   const Elem* A = in + g.a0;
   splits[t] = merge_path_global(cmp, A, g.a_len, A + g.a_len, g.b_len, g.d0);
 }
@@ -179,7 +180,7 @@ __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, El
                                                               const int64_t* splits, Cmp cmp) {
   __shared__ __attribute__((aligned(16))) Elem lds[kMergeTile];
   const int t = blockIdx.x;
-  const TileGeo g = tile_geo(pd, t);
+  const TileGeo g = tile_geo<kMergeTile>(pd, t);
   const int64_t pair_len = g.a_len + g.b_len;
   const int64_t d0 = g.d0;
   const int64_t d1 = (d0 + kMergeTile < pair_len) ? d0 + kMergeTile : pair_len;
@@ -236,6 +237,138 @@ __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, El
 #pragma unroll
   for (int k = 0; k < kItems; ++k)
     if (k < todo) st_elem(lds + diag + k, Elem{rh[k], rl[k]});
+  __syncthreads();
+  Elem* O = out + g.a0 + d0;
+  for (int k = threadIdx.x; k < cnt; k += kThreads) st_elem(O + k, lds[k]);
+}
+
+// GENERIC merge pass with LDS-staged key bytes. Every key of a tile lies between the first and last
+// element of its A and B slices (both sorted), so the longest common prefix P of those four keys is a
+// prefix of every key in the tile. Each element's key bytes [P, P+24) are staged in LDS once (three
+// big-endian words, zero padded past the key end); comparisons then run on LDS words and reach HBM
+// only for keys that still tie after P+24 bytes. Order = content bytes, then length, then ordinal:
+// the same total order as GenericCmp (used by the partition kernel).
+constexpr int kGenItems = kGenericMergeTile / kThreads;  // 4
+constexpr uint64_t kOrdMask = 0xFFFFFFFFFFFFull;
+
+__device__ __forceinline__ int key_lcp(const uint8_t* a, int la, const uint8_t* b, int lb, int limit) {
+  const int n = min(min(la, lb), limit);
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x, y;
+    __builtin_memcpy(&x, a + i, 8);
+    __builtin_memcpy(&y, b + i, 8);
+    if (x != y) return i + (__builtin_ctzll(x ^ y) >> 3);  // little-endian: first differing byte
+  }
+  while (i < n && a[i] == b[i]) ++i;
+  return i;
+}
+
+__global__ void __launch_bounds__(kThreads) merge_pass_generic_lds_kernel(const Elem* in, Elem* out, PassDesc pd,
+                                                                          const int64_t* splits, GenericKeyCtx ctx) {
+  constexpr int TILE = kGenericMergeTile;
+  __shared__ __attribute__((aligned(16))) Elem lds[TILE];
+  __shared__ uint64_t w0[TILE], w1[TILE], w2[TILE];
+  __shared__ int32_t klen[TILE];
+  __shared__ int tile_p;
+  const int t = blockIdx.x;
+  const TileGeo g = tile_geo<TILE>(pd, t);
+  const int64_t pair_len = g.a_len + g.b_len;
+  const int64_t d0 = g.d0;
+  const int64_t d1 = (d0 + TILE < pair_len) ? d0 + TILE : pair_len;
+  const int64_t i0 = splits[t];
+  const bool last_of_pair = (t + 1 >= (int)pd.tile_prefix[g.pair + 1]);
+  const int64_t i1 = last_of_pair ? g.a_len : splits[t + 1];
+  const int cnt = (int)(d1 - d0);
+  const int la = (int)(i1 - i0);
+  const int lb = cnt - la;
+  const Elem* A = in + g.a0 + i0;
+  const Elem* B = in + g.a0 + g.a_len + (d0 - i0);
+  for (int k = threadIdx.x; k < cnt; k += kThreads) {
+    const Elem e = (k < la) ? ld_elem(A + k) : ld_elem(B + (k - la));
+    st_elem(lds + k, e);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ends[4], ne = 0;
+    if (la > 0) { ends[ne++] = 0; ends[ne++] = la - 1; }
+    if (lb > 0) { ends[ne++] = la; ends[ne++] = cnt - 1; }
+    int p = 1 << 30;
+    if (ne > 0) {
+      const uint64_t g0 = lds[ends[0]].lo & kOrdMask;
+      const uint8_t* k0 = ctx.keyptr[g0];
+      const int l0 = ctx.keylen[g0];
+      p = l0;
+      for (int x = 1; x < ne; ++x) {
+        const uint64_t gx = lds[ends[x]].lo & kOrdMask;
+        p = key_lcp(k0, l0, ctx.keyptr[gx], ctx.keylen[gx], p);
+      }
+    }
+    tile_p = (ne > 0) ? p : 0;
+  }
+  __syncthreads();
+  const int P = tile_p;
+  for (int k = threadIdx.x; k < cnt; k += kThreads) {
+    const uint64_t gk = lds[k].lo & kOrdMask;
+    const uint8_t* kp = ctx.keyptr[gk];
+    const int l = ctx.keylen[gk];
+    klen[k] = l;
+    const int rem = l - P;
+    w0[k] = rem > 0 ? load_be8(kp + P, rem) : 0;
+    w1[k] = rem > 8 ? load_be8(kp + P + 8, rem - 8) : 0;
+    w2[k] = rem > 16 ? load_be8(kp + P + 16, rem - 16) : 0;
+  }
+  __syncthreads();
+  auto le = [&](int x, int y) -> bool {
+    if (w0[x] != w0[y]) return w0[x] < w0[y];
+    if (w1[x] != w1[y]) return w1[x] < w1[y];
+    if (w2[x] != w2[y]) return w2[x] < w2[y];
+    const int lx = klen[x], ly = klen[y];
+    if (lx > P + 24 && ly > P + 24) {
+      const uint8_t* px = ctx.keyptr[lds[x].lo & kOrdMask];
+      const uint8_t* py = ctx.keyptr[lds[y].lo & kOrdMask];
+      const int n = lx < ly ? lx : ly;
+      for (int i = P + 24; i < n; i += 8) {
+        const uint64_t a = load_be8(px + i, n - i), b = load_be8(py + i, n - i);
+        if (a != b) return a < b;
+      }
+    }
+    if (lx != ly) return lx < ly;
+    return (lds[x].lo & kOrdMask) <= (lds[y].lo & kOrdMask);
+  };
+  const int diag = threadIdx.x * kGenItems;
+  int res[kGenItems];
+  int todo = 0;
+  if (diag < cnt) {
+    int lo = diag > lb ? diag - lb : 0;
+    int hi = diag < la ? diag : la;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (le(mid, la + diag - 1 - mid))
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    int ia = lo, ib = diag - lo;
+    todo = (cnt - diag) < kGenItems ? (cnt - diag) : kGenItems;
+#pragma unroll
+    for (int k = 0; k < kGenItems; ++k) {
+      const bool take_a = (ib >= lb) || (ia < la && le(ia, la + ib));
+      res[k] = take_a ? ia : la + ib;
+      if (take_a)
+        ++ia;
+      else
+        ++ib;
+    }
+  }
+  Elem r[kGenItems];
+#pragma unroll
+  for (int k = 0; k < kGenItems; ++k)
+    if (k < todo) r[k] = lds[res[k]];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kGenItems; ++k)
+    if (k < todo) st_elem(lds + diag + k, r[k]);
   __syncthreads();
   Elem* O = out + g.a0 + d0;
   for (int k = threadIdx.x; k < cnt; k += kThreads) st_elem(O + k, lds[k]);
@@ -353,8 +486,8 @@ void launch_extract_fixed(const RunDesc* runs, const int64_t* elem_off, int nrun
 
 void launch_merge_partition(const Elem* in, PassDesc pd, int64_t* splits, hipStream_t s) {
   if (pd.ntiles <= 0) return;
-  hipLaunchKernelGGL(merge_partition_kernel<FixedCmp>, dim3((unsigned)((pd.ntiles + 255) / 256)), dim3(256),
-                     0, s, in, pd, splits, FixedCmp{});
+  hipLaunchKernelGGL((merge_partition_kernel<kMergeTile, FixedCmp>), dim3((unsigned)((pd.ntiles + 255) / 256)),
+                     dim3(256), 0, s, in, pd, splits, FixedCmp{});
 }
 
 void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
@@ -367,15 +500,15 @@ void launch_merge_pass(const Elem* in, Elem* out, PassDesc pd, const int64_t* sp
 void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits, GenericKeyCtx ctx,
                                     hipStream_t s) {
   if (pd.ntiles <= 0) return;
-  hipLaunchKernelGGL(merge_partition_kernel<GenericCmp>, dim3((unsigned)((pd.ntiles + 255) / 256)),
-                     dim3(256), 0, s, in, pd, splits, GenericCmp{ctx});
+  hipLaunchKernelGGL((merge_partition_kernel<kGenericMergeTile, GenericCmp>),
+                     dim3((unsigned)((pd.ntiles + 255) / 256)), dim3(256), 0, s, in, pd, splits, GenericCmp{ctx});
 }
 
 void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
                                GenericKeyCtx ctx, hipStream_t s) {
   if (pd.ntiles <= 0) return;
-  hipLaunchKernelGGL(merge_pass_kernel<GenericCmp>, dim3((unsigned)pd.ntiles), dim3(kThreads), 0, s, in,
-                     out, pd, splits, GenericCmp{ctx});
+  hipLaunchKernelGGL(merge_pass_generic_lds_kernel, dim3((unsigned)pd.ntiles), dim3(kThreads), 0, s, in, out, pd,
+                     splits, ctx);
 }
 
 void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases, uint8_t* out,

@@ -24,7 +24,8 @@ struct MergePassPlan {
 // segment of every group plus a final S (G+1 entries; groups may be empty). Every pass moves every
 // element (ping-pong buffers), so single segments are copied through as pairs with an empty B.
 // Returns no passes when every group already holds at most one segment.
-inline std::vector<MergePassPlan> plan_merge_passes(std::vector<int64_t> seg, std::vector<int> group_first) {
+inline std::vector<MergePassPlan> plan_merge_passes(std::vector<int64_t> seg, std::vector<int> group_first,
+                                                    int64_t tile = kMergeTile) {
   std::vector<MergePassPlan> passes;
   auto more = [&] {
     for (size_t g = 0; g + 1 < group_first.size(); ++g)
@@ -42,7 +43,7 @@ inline std::vector<MergePassPlan> plan_merge_passes(std::vector<int64_t> seg, st
         const int64_t a0 = seg[s], a1 = seg[s + 1];
         const int64_t b1 = (s + 1 < s1) ? seg[s + 2] : a1;
         p.pairs.insert(p.pairs.end(), {a0, a1, b1});
-        p.tile_prefix.push_back(p.tile_prefix.back() + (b1 - a0 + kMergeTile - 1) / kMergeTile);
+        p.tile_prefix.push_back(p.tile_prefix.back() + (b1 - a0 + tile - 1) / tile);
         nseg.push_back(b1);
       }
       ngroup.push_back((int)nseg.size() - 1);
