@@ -23,6 +23,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -98,6 +101,114 @@ struct StreamGuard {
 struct Span {
   const uint8_t* p;
   int64_t len;
+  const uint8_t* dev = nullptr;  // device copy staged while the fetch went on (EarlyStager)
+};
+
+// Stages fetched partitions to HBM as soon as each one is complete in pinned memory, so the H2D
+// copies overlap the remaining fetches (one issuing thread, one copy stream: the round-1 attempt
+// issued from every drain thread and the copies contended). Device memory comes from a bump
+// arena of 256 MiB blocks (a partition never straddles blocks); reset() recycles it once the
+// group's merge has finished.
+class EarlyStager {
+ public:
+  explicit EarlyStager(int device) : device_(device) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+    thr_ = std::thread([this] { loop(); });
+  }
+  ~EarlyStager() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    thr_.join();
+    (void)hipStreamSynchronize(s_);
+    (void)hipStreamDestroy(s_);
+  }
+  // Device address the partition will be copied to; the copy is issued asynchronously.
+  const uint8_t* submit(const uint8_t* host, int64_t len) {
+    std::lock_guard<std::mutex> g(mu_);
+    uint8_t* d = alloc(len);
+    q_.push_back(Job{host, d, len});
+    cv_.notify_all();
+    return d;
+  }
+  // Every submitted copy has completed.
+  void flush() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return q_.empty() && busy_ == 0; });
+    lk.unlock();
+    HIP_CHECK(hipStreamSynchronize(s_));
+    if (!error_.empty()) throw UdaError("early H2D staging failed: " + error_);
+  }
+  void reset() {
+    flush();
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& b : blocks_) b.used = 0;
+    cur_ = 0;
+  }
+  double issue_ms() const { return issue_ms_; }
+  int64_t bytes() const { return bytes_; }
+
+ private:
+  struct Job {
+    const uint8_t* host;
+    uint8_t* dev;
+    int64_t len;
+  };
+  struct Block {
+    gpu::DeviceBuffer buf;
+    int64_t used = 0;
+  };
+  uint8_t* alloc(int64_t len) {  // mu_ held
+    len = (std::max<int64_t>(len, 1) + 255) & ~(int64_t)255;
+    for (; cur_ < blocks_.size(); ++cur_)
+      if ((int64_t)blocks_[cur_].buf.size() - blocks_[cur_].used >= len) break;
+    if (cur_ == blocks_.size()) {
+      blocks_.emplace_back();
+      HIP_CHECK(hipSetDevice(device_));
+      blocks_.back().buf.alloc((size_t)std::max<int64_t>(len, 256ll << 20));
+    }
+    Block& b = blocks_[cur_];
+    uint8_t* p = b.buf.as<uint8_t>() + b.used;
+    b.used += len;
+    return p;
+  }
+  void loop() {
+    (void)hipSetDevice(device_);
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        j = q_.front();
+        q_.pop_front();
+        ++busy_;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      const hipError_t e = hipMemcpyAsync(j.dev, j.host, (size_t)j.len, hipMemcpyHostToDevice, s_);
+      issue_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      std::lock_guard<std::mutex> g(mu_);
+      if (e != hipSuccess && error_.empty()) error_ = hipGetErrorString(e);
+      bytes_ += j.len;
+      --busy_;
+      cv_.notify_all();
+    }
+  }
+  int device_;
+  hipStream_t s_ = nullptr;
+  std::thread thr_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  int busy_ = 0;
+  bool stop_ = false;
+  std::string error_;
+  std::vector<Block> blocks_;
+  size_t cur_ = 0;
+  double issue_ms_ = 0;
+  int64_t bytes_ = 0;
 };
 
 DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
@@ -105,9 +216,30 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   auto t0 = std::chrono::steady_clock::now();
   std::vector<const uint8_t*> ptrs;
   std::vector<int64_t> lens;
+  bool all_staged = codec == Codec::kNone && !in_runs.empty();
   for (const Span& sp : in_runs) {
     ptrs.push_back(sp.p);
     lens.push_back(sp.len);
+    all_staged = all_staged && sp.dev != nullptr;
+  }
+  if (all_staged) {  // the partitions reached HBM while the fetch went on
+    int64_t total = 0;
+    std::vector<const uint8_t*> runs;
+    for (const Span& sp : in_runs) {
+      runs.push_back(sp.dev);
+      total += sp.len;
+    }
+    DeviceWorkspace::ensure(ws.out, total);
+    auto t1 = std::chrono::steady_clock::now();
+    ws.h2d_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    gpu::GenericMergeResult r = ws.merger.merge(runs, lens, (int)kind, ws.out.as<uint8_t>(), total, spacing, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    DeviceMergeOut res;
+    res.bytes = r.bytes;
+    res.cuts = std::move(r.cuts);
+    res.records = r.records;
+    return res;
   }
   gpu::BlockPlan plan;
   bool decode_on_device = false;
@@ -253,6 +385,11 @@ void ReduceTask::merge_gpu() {
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
   DeviceWorkspace ws;
+  // uncompressed partitions go to HBM as soon as each one is complete (overlapping the fetch)
+  std::unique_ptr<EarlyStager> stager;
+  if (fetch_codec == Codec::kNone && stage_codec == Codec::kNone && host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0)
+    stager.reset(new EarlyStager(device));
+  const int depth = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.fetch.depth", 4));
 
   std::vector<SpillRun> spills;
   std::vector<Span> group;          // fetched partitions of the current group (pinned, group_mem)
@@ -288,8 +425,10 @@ void ReduceTask::merge_gpu() {
   // LPQ: merge the current group on the device and spill it with its sparse index
   auto spill_group = [&] {
     if (group.empty()) return;
+    if (stager) stager->flush();
     DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kSampleSpacing, s);
     count_decoded(m.decoded_blocks);
+    if (stager) stager->reset();  // the merge read the staged copies; recycle their HBM
     group.clear();
     group_mem.release_all();  // staged in HBM: the pinned blocks go back to the pool
     group_raw = 0;
@@ -468,10 +607,12 @@ void ReduceTask::merge_gpu() {
             try {
               MofFetcher& f = *ready[sub[k]];
               if (dst[k]) {
+                // first chunk from the fetcher, the rest straight into the pinned span
                 const int64_t cap = f.part_len();
-                int64_t off = 0;
-                for (int64_t n; (n = f.pull(dst[k] + off, std::max<int64_t>(cap - off, 0))) > 0;) off += n;
+                int64_t off = f.take_first(dst[k], cap);
+                if (off < cap) off = fetch_direct(f.params(), dst[k], off, cap, depth);
                 got[k] = Span{dst[k], off};
+                if (stager) got[k].dev = stager->submit(dst[k], off);
               } else {  // host decode: decoded length unknown up front
                 std::vector<uint8_t> buf((size_t)buffer_size_);
                 for (int64_t n; (n = f.pull(buf.data(), (int64_t)buf.size())) > 0;)
@@ -543,6 +684,7 @@ void ReduceTask::merge_gpu() {
 
     if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
+      if (stager) stager->flush();
       DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kv, s);
       count_decoded(m.decoded_blocks);
       deliver(m, true);
@@ -646,7 +788,7 @@ void ReduceTask::merge_gpu() {
             views.push_back(Span{p, e - b});
           }
         }
-        DeviceMergeOut m = device_merge(ws, views, Codec::kNone, kind_, kv, s);
+        DeviceMergeOut m = device_merge(ws, views, Codec::kNone, kind_, kv, s);  // views: host spans
         deliver(m, q + 1 == rounds);
       }
     }

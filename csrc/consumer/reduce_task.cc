@@ -150,6 +150,69 @@ int64_t MofFetcher::pull_raw(uint8_t* dst, int64_t cap) {
   return n;
 }
 
+int64_t MofFetcher::take_first(uint8_t* dst, int64_t cap) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return ready_[0] || !error_.empty(); });
+  if (!error_.empty()) throw UdaError("fetch of " + p_.map_id + " failed: " + error_);
+  const int64_t n = std::min(len_[0], cap);
+  std::memcpy(dst, bufs_[0].data(), (size_t)n);
+  consumed_ = n;
+  ready_[0] = false;
+  lk.unlock();
+  {
+    std::lock_guard<std::mutex> g(task_->st_mu_);
+    task_->st_.bytes_fetched += n;
+  }
+  release_pair();
+  return n;
+}
+
+int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth) {
+  std::mutex m;
+  std::condition_variable c;
+  int inflight = 0;
+  std::string err;
+  int64_t next = off;
+  auto issue = [&](int64_t at) {
+    FetchRequest req;
+    req.job_id = f.job_id;
+    req.map_id = f.map_id;
+    req.reduce_id = f.reduce_id;
+    req.fetched = at;
+    req.buf_len = std::min(buffer_size_, end - at);
+    const int64_t want = req.buf_len;
+    fetch_begin();
+    transport_->fetch(f.host, req, dst + at, [&, want](const FetchAck& a) {
+      std::lock_guard<std::mutex> g(m);
+      if (a.status != 0 && err.empty()) err = a.error.empty() ? "fetch failed" : a.error;
+      if (a.status == 0 && a.sent != want && err.empty()) err = "short fetch";
+      --inflight;
+      c.notify_all();
+      fetch_end();
+    });
+  };
+  std::unique_lock<std::mutex> lk(m);
+  for (;;) {
+    while (next < end && inflight < depth && err.empty() && !stop_) {
+      const int64_t at = next;
+      next += std::min(buffer_size_, end - at);
+      ++inflight;
+      lk.unlock();
+      issue(at);  // a transport may complete inline
+      lk.lock();
+    }
+    const bool can_issue = next < end && err.empty() && !stop_;
+    if (!can_issue && inflight == 0) break;
+    c.wait(lk, [&] { return inflight == 0 || (can_issue && inflight < depth); });
+  }
+  if (!err.empty()) throw UdaError("fetch of " + f.map_id + " failed: " + err);
+  if (next < end) throw UdaError("reduce task stopped during fetch");
+  lk.unlock();
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.bytes_fetched += end - off;
+  return end;
+}
+
 void MofFetcher::release_pair() {
   if (released_.exchange(true)) return;  // buffers go back to the pool once
   {

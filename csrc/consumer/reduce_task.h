@@ -73,6 +73,9 @@ class ReduceTask {
 
   // exposed for the fetchers
   ClientTransport* transport() { return transport_.get(); }
+  // Fetch [off, end) of a partition straight into dst + off (the RDMA-WRITE-into-the-reducer-buffer
+  // analogue), `depth` requests of buffer_size_ in flight. Returns end.
+  int64_t fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth);
   // in-flight fetch requests (exit() waits for their completions)
   void fetch_begin();
   void fetch_end();
@@ -147,6 +150,9 @@ class MofFetcher : public std::enable_shared_from_this<MofFetcher> {
   void start();
   // ChunkSource: blocks until the next chunk is available; returns bytes (0 at end).
   int64_t pull(uint8_t* dst, int64_t cap);
+  // GPU staging: copy the first chunk (the only one fetched so far) to dst and hand the buffer pair
+  // back; the caller fetches the rest of the partition straight into its own memory.
+  int64_t take_first(uint8_t* dst, int64_t cap);
   bool first_arrived() const { return first_done_; }
   const FetchParams& params() const { return p_; }
   int64_t part_len() const { return part_len_; }

@@ -30,7 +30,7 @@ namespace uda {
 class Supplier : public DataServer {
  public:
   struct Options {
-    int workers = 2;             // DataEngine threads
+    int workers = 8;             // DataEngine threads (mapred.uda.provider.workers)
     int io_threads = 4;          // AsyncIO pool size (blocked.threads.per.disk analogue)
     bool odirect = false;        // read MOF files with O_DIRECT (4 KiB aligned bounce chunks)
     int max_open_files = 512;    // fd cache bound (rlimit analogue)
