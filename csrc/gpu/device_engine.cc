@@ -30,6 +30,12 @@ double now_ms() {
 }
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+int64_t total_records(const std::vector<RunDesc>& runs) {
+  int64_t t = 0;
+  for (const auto& r : runs) t += r.nrec;
+  return t;
+}
 }  // namespace
 
 void hip_check(hipError_t e, const char* what, const char* file, int line) {
@@ -183,6 +189,11 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   ++passes;  // groups that are not a power of two may need one extra copy-through level
   slot_bytes_ = (size_t)max_runs * (sizeof(RunDesc) + 2 * sizeof(int64_t) + sizeof(uint8_t*)) +
                 (size_t)passes * (4 * (size_t)max_runs + 4) * sizeof(int64_t) + 64 * (size_t)(passes + 4);
+  // single-pass K-way tables: runs, bases, counts, sample offsets, bound sets, group / cell tables
+  slot_bytes_ += (size_t)max_runs * (sizeof(RunDesc) + 4 * sizeof(int64_t) + 2 * sizeof(int)) + 64 * 16;
+  if (const char* e = std::getenv("UDA_KWAY")) kway_ = std::atoi(e) != 0;
+  kw_overflow_.alloc(sizeof(int));
+  HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
   slots_.resize(4);
   for (auto& s : slots_) {
     s.host.alloc(slot_bytes_);
@@ -194,6 +205,12 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
 DeviceMerger::~DeviceMerger() {
   for (auto& s : slots_)
     if (s.uploaded) (void)hipEventDestroy(s.uploaded);
+}
+
+int DeviceMerger::kway_overflow_cells() {
+  int v = 0;
+  HIP_CHECK(hipMemcpy(&v, kw_overflow_.as(), sizeof(int), hipMemcpyDeviceToHost));
+  return v;
 }
 
 bool DeviceMerger::bad_layout() {
@@ -214,6 +231,11 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
   if (total > max_records_) throw std::runtime_error("DeviceMerger: round exceeds capacity");
   last_passes_ = 0;
   if (total == 0) return 0;
+  if (kway_) {
+    int kmax = 0;
+    for (size_t g = 0; g + 1 < group_first.size(); ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
+    if (kmax <= 128) return merge_kway(runs, group_first, out, s);
+  }
 
   Slot& slot = slots_[next_slot_];
   next_slot_ = (next_slot_ + 1) % (int)slots_.size();
@@ -273,6 +295,120 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
   // ---- F4: gather records into merged order
   launch_gather_fixed(cur, total, reinterpret_cast<uint8_t* const*>(d + o_bases), out, s);
   return total;
+}
+
+// Single-pass K-way merge (kway.hip): sample -> merge the samples per group -> splitters ->
+// per-run cell splits -> one workgroup per cell doing F2 + F3 + F4 in LDS.
+int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
+                                 hipStream_t s) {
+  const int K = (int)runs.size();
+  const int G = (int)group_first.size() - 1;
+  int kmax = 1;
+  for (int g = 0; g < G; ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
+  int64_t T = kKwCap / 2;  // target records per cell
+  if (const char* e = std::getenv("UDA_KWAY_TARGET")) T = std::max<int64_t>(1, std::atoll(e));  // tests: force the PQ path
+  const int64_t step = std::max<int64_t>(1, (kKwCap - std::min<int64_t>(T, kKwCap)) / (kmax + 2));  // cell <= T + K*step
+  std::vector<int64_t> soff(K + 1, 0), nrec(K);
+  std::vector<uint8_t*> bases(K);
+  std::vector<int> bset(K);
+  for (int g = 0; g < G; ++g)
+    for (int r = group_first[g]; r < group_first[g + 1]; ++r) bset[r] = g;
+  for (int r = 0; r < K; ++r) {
+    nrec[r] = runs[r].nrec;
+    bases[r] = const_cast<uint8_t*>(runs[r].base);
+    const int64_t c = nrec[r] > step / 2 ? (nrec[r] - step / 2 + step - 1) / step : 0;
+    soff[r + 1] = soff[r] + c;
+  }
+  const int64_t ns = soff[K];
+  std::vector<int64_t> gcells(G), cell_first(G + 1, 0), gsamp(G + 1, 0), gout(G, 0);
+  int64_t nbmax = 0, acc = 0;
+  for (int g = 0; g < G; ++g) {
+    int64_t ng = 0;
+    for (int r = group_first[g]; r < group_first[g + 1]; ++r) ng += nrec[r];
+    gcells[g] = std::max<int64_t>(1, (ng + T - 1) / T);
+    cell_first[g + 1] = cell_first[g] + gcells[g];
+    gsamp[g] = soff[group_first[g]];
+    gout[g] = acc;
+    acc += ng;
+    nbmax = std::max(nbmax, gcells[g] - 1);
+  }
+  gsamp[G] = soff[K];
+  const int64_t per = nbmax + 2;
+  auto ensure = [](DeviceBuffer& b, size_t bytes) {
+    if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+  };
+  ensure(samp_a_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(samp_b_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(kw_bounds_, (size_t)std::max<int64_t>((int64_t)G * nbmax, 1) * sizeof(Elem));
+  ensure(kw_split_, (size_t)K * per * sizeof(int64_t));
+
+  Slot& slot = slots_[next_slot_];
+  next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+  if (slot.used) HIP_CHECK(hipEventSynchronize(slot.uploaded));
+  slot.used = true;
+  uint8_t* h = slot.host.as();
+  uint8_t* d = slot.dev.as();
+  size_t off = 0;
+  auto carve = [&](const void* src, size_t bytes) {
+    const size_t o = off;
+    off = (size_t)align_up((int64_t)(off + bytes), 16);
+    if (off > slot_bytes_) throw std::runtime_error("DeviceMerger: plan blob overflow (k-way)");
+    std::memcpy(h + o, src, bytes);
+    return o;
+  };
+  const size_t o_runs = carve(runs.data(), sizeof(RunDesc) * K);
+  const size_t o_bases = carve(bases.data(), sizeof(uint8_t*) * K);
+  const size_t o_nrec = carve(nrec.data(), 8 * K);
+  const size_t o_soff = carve(soff.data(), 8 * (K + 1));
+  const size_t o_bset = carve(bset.data(), sizeof(int) * K);
+  const size_t o_gf = carve(group_first.data(), sizeof(int) * (G + 1));
+  const size_t o_cf = carve(cell_first.data(), 8 * (G + 1));
+  const size_t o_gs = carve(gsamp.data(), 8 * (G + 1));
+  const size_t o_gc = carve(gcells.data(), 8 * G);
+  const size_t o_go = carve(gout.data(), 8 * G);
+  std::vector<PassDesc> pds;
+  for (const auto& mp : plan_merge_passes(soff, group_first)) {
+    const size_t o_pairs = carve(mp.pairs.data(), 8 * mp.pairs.size());
+    const size_t o_tp = carve(mp.tile_prefix.data(), 8 * mp.tile_prefix.size());
+    PassDesc pd;
+    pd.pairs = reinterpret_cast<const int64_t*>(d + o_pairs);
+    pd.tile_prefix = reinterpret_cast<const int64_t*>(d + o_tp);
+    pd.npairs = mp.npairs;
+    pd.ntiles = mp.ntiles;
+    pds.push_back(pd);
+  }
+  HIP_CHECK(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipEventRecord(slot.uploaded, s));
+
+  // splitters: a regular sample of every run, merged per group, every (ns_g / C_g)-th kept
+  Elem* sa = samp_a_.as<Elem>();
+  Elem* sb = samp_b_.as<Elem>();
+  if (ns > 0)
+    launch_sample_fixed(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec), K,
+                        step, reinterpret_cast<const int64_t*>(d + o_soff), ns, sa, s);
+  for (const auto& pd : pds) {
+    launch_merge_partition(sa, pd, splits_.as<int64_t>(), s);
+    launch_merge_pass(sa, sb, pd, splits_.as<int64_t>(), s);
+    std::swap(sa, sb);
+  }
+  launch_pick_splitters(sa, reinterpret_cast<const int64_t*>(d + o_gs), reinterpret_cast<const int64_t*>(d + o_gc), G,
+                        (int)nbmax, kw_bounds_.as<Elem>(), s);
+  launch_split_fixed(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec),
+                     nbmax > 0 ? kw_bounds_.as<Elem>() : nullptr, reinterpret_cast<const int*>(d + o_bset), K,
+                     (int)nbmax, kw_split_.as<int64_t>(), s);
+  KwayDesc kd;
+  kd.runs = reinterpret_cast<const RunDesc*>(d + o_runs);
+  kd.group_first = reinterpret_cast<const int*>(d + o_gf);
+  kd.cell_first = reinterpret_cast<const int64_t*>(d + o_cf);
+  kd.split = kw_split_.as<int64_t>();
+  kd.nbmax = (int)nbmax;
+  kd.group_out = reinterpret_cast<const int64_t*>(d + o_go);
+  kd.G = G;
+  kd.overflow = kw_overflow_.as<int>();
+  kd.bad_layout = flag_.as<int>();
+  launch_kway_tiles(kd, cell_first[G], out, s);
+  last_passes_ = 1;
+  return total_records(runs);
 }
 
 // -------------------------------------------------------------------------------- ShuffleJob

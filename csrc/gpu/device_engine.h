@@ -163,8 +163,13 @@ class DeviceMerger {
   int last_passes() const { return last_passes_; }
   bool bad_layout();  // synchronizes; true if any record was not TeraSort-shaped
   int64_t max_records() const { return max_records_; }
+  // Cells the single-pass K-way merge handed to its wave-level PQ so far (synchronizes).
+  int kway_overflow_cells();
+  bool kway_enabled() const { return kway_; }
 
  private:
+  int64_t merge_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
+                     hipStream_t s);
   struct Slot {
     PinnedBuffer host;
     DeviceBuffer dev;
@@ -175,6 +180,9 @@ class DeviceMerger {
   int max_runs_;
   DeviceBuffer elems_a_, elems_b_, splits_;
   DeviceBuffer flag_;
+  // single-pass K-way merge (kway.hip): samples (ping-pong), splitters, cell split table, overflow
+  bool kway_ = true;
+  DeviceBuffer samp_a_, samp_b_, kw_bounds_, kw_split_, kw_overflow_;
   std::vector<Slot> slots_;
   int next_slot_ = 0;
   int last_passes_ = 0;

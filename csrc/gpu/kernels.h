@@ -106,6 +106,26 @@ void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits
 void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
                                GenericKeyCtx ctx, hipStream_t s);
 
+// ---------------------------------------------------------------- single-pass K-way merge (F2+F3+F4)
+constexpr int kKwCap = 2048;       // records per cell (LDS capacity of one workgroup)
+constexpr int kKwMaxRuns = 1024;   // runs per group on the LDS path
+struct KwayDesc {
+  const RunDesc* runs;        // every run of the round, grouped by reducer
+  const int* group_first;     // G+1
+  const int64_t* cell_first;  // G+1: first cell (workgroup) of each group
+  const int64_t* split;       // [run][nbmax+2]: split[r*(nbmax+2) + c] = first record of cell c in run r
+  int nbmax;
+  const int64_t* group_out;   // G: first output record of each group
+  int G;
+  int* overflow;              // cells merged by the wave-level PQ (did not fit LDS)
+  int* bad_layout;            // set if a record is not TeraSort-shaped
+};
+// bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
+// +infinity for j >= C_g - 1.
+void launch_pick_splitters(const Elem* samples, const int64_t* gsamp_off, const int64_t* gcells, int G, int nbmax,
+                           Elem* bounds, hipStream_t s);
+void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s);
+
 // ---------------------------------------------------------------- GENERIC record path (F1/F2/F4)
 // F1 pass 1 (one wave per run): chunk checkpoints ck_start/ck_count for the chunks of run r at
 // [chunk_base[r], chunk_base[r+1]) (chunks of f1_chunk_bytes()), records per run, record bytes

@@ -1,0 +1,280 @@
+// Single-pass K-way merge of FIXED10 (TeraSort) runs: F2 + F3 + F4 fused per output cell.
+//
+// Reference hot loop replaced: PriorityQueue::downHeap + MergeQueue::next/adjustPriorityQueue
+// (src/Merger/MergeQueue.h:238-269, 299-321, 390-419) over all segments of a reduce task, and the
+// record serialization behind it (write_kv_to_stream, src/Merger/StreamRW.cc:151-225).
+//
+// Design (gfx950):
+//  * Cells by sampling. Every s-th key of every run is sampled; the samples of a group (reducer)
+//    are merged and every (samples / cells)-th becomes a splitter; lower_bound of each splitter in
+//    each run gives the cell slices. With s = (cap - T) / (K + 2) a cell holds at most
+//    T + K*s <= cap records (T = target), so it always fits LDS; output offsets are the sums of the
+//    lower bounds, no scan needed.
+//  * One workgroup per cell (256 threads, cap = 2048 records): the slices' keys are loaded once
+//    from the records into LDS as 16-byte elements (F2), the K sorted slices are merged pairwise
+//    inside LDS (log2 K levels, merge path per thread, ping-pong between two 32 KiB buffers: no HBM
+//    traffic between levels), and the records are gathered straight to the output (F4): one wave
+//    per 64 output records, 13 consecutive 8-byte words per record, 512-byte coalesced stores.
+//    HBM traffic per record: its key cache line, then one record read and one record write.
+//  * A cell that would not fit LDS (only possible with massively duplicated keys) is merged by a
+//    wave-level priority queue: lanes own runs, a wave argmin picks the next record each step.
+#include "kernels.h"
+
+namespace uda {
+namespace gpu {
+
+namespace {
+constexpr int kKwThreads = 256;
+constexpr int kKwWaves = kKwThreads / 64;
+constexpr int kKwItems = kKwCap / kKwThreads;  // 8
+
+__device__ __forceinline__ bool kle(const Elem& a, const Elem& b) {
+  return a.hi < b.hi || (a.hi == b.hi && a.lo <= b.lo);
+}
+
+__device__ __forceinline__ Elem load_key_elem(const uint8_t* rec, int run, int64_t pos, int* bad) {
+  const uint64_t w0 = *reinterpret_cast<const uint64_t*>(rec);
+  const uint64_t w1 = *reinterpret_cast<const uint64_t*>(rec + 8);
+  if ((w0 & 0xFFFFFF) != 0x0A5B0B || ((w1 >> 40) & 0xFF) != 0x5A) *bad = 1;
+  const uint64_t b0 = __builtin_bswap64(w0), b1 = __builtin_bswap64(w1);
+  Elem e;
+  e.hi = (b0 << 24) | (b1 >> 40);
+  e.lo = (((b1 >> 24) & 0xFFFF) << 48) | ((uint64_t)run << 32) | (uint64_t)pos;
+  return e;
+}
+
+__global__ void __launch_bounds__(256) pick_splitters_kernel(const Elem* samples, const int64_t* gsamp_off,
+                                                             const int64_t* gcells, int G, int nbmax, Elem* bounds) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)G * nbmax) return;
+  const int g = (int)(t / nbmax), j = (int)(t % nbmax);
+  const int64_t C = gcells[g];
+  const int64_t ns = gsamp_off[g + 1] - gsamp_off[g];
+  Elem b{~0ull, ~0ull};
+  if (j < C - 1 && ns > 0) {
+    int64_t idx = (int64_t)(j + 1) * ns / C;
+    if (idx > ns - 1) idx = ns - 1;
+    const Elem s = samples[gsamp_off[g] + idx];
+    b.hi = s.hi;
+    b.lo = s.lo & (0xFFFFull << 48);
+  }
+  bounds[t] = b;
+}
+
+// Exclusive scan of the K slice lengths into seg[0..K] and the sum of the slice starts (wave 0).
+__device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int ncell, int r0, int K, int* seg,
+                                          int64_t* beg, int64_t* start_sum) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const int per = kd.nbmax + 2;
+  int carry = 0;
+  unsigned long long bsum = 0;
+  if (lane == 0) seg[0] = 0;
+  for (int base = 0; base < K; base += 64) {
+    const int k = base + lane;
+    int len = 0;
+    if (k < K) {
+      const int r = r0 + k;
+      const int64_t b = c == 0 ? 0 : kd.split[(int64_t)r * per + c];
+      const int64_t e = (c + 1 == ncell) ? kd.runs[r].nrec : kd.split[(int64_t)r * per + c + 1];
+      beg[k] = b;
+      len = (int)(e - b);
+      bsum += (unsigned long long)b;
+    }
+    int x = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (k < K) seg[k + 1] = carry + x;
+    carry += __shfl(x, 63, 64);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) bsum += __shfl_xor(bsum, off, 64);
+  if (lane == 0) *start_sum = (int64_t)bsum;
+}
+
+// 13 x 8-byte words per record, one wave per 64 consecutive output records.
+__device__ __forceinline__ void kw_gather64(const KwayDesc& kd, const Elem* cur, int base, int valid, uint8_t* dst) {
+  constexpr int kWords = kTeraRecordBytes / 8;
+  const int lane = threadIdx.x & 63;
+  unsigned long long src = 0;
+  if (lane < valid) {
+    const Elem e = cur[base + lane];
+    const int run = (int)((e.lo >> 32) & 0xFFFF);
+    src = (unsigned long long)(kd.runs[run].base + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes);
+  }
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+  const int words = valid * kWords;
+#pragma unroll
+  for (int j = 0; j < kWords; ++j) {
+    const int w = j * 64 + lane;
+    const int r = w / kWords;
+    const int wi = w - r * kWords;
+    const unsigned long long s = __shfl(src, r < 64 ? r : 63, 64);
+    if (w < words) d[w] = reinterpret_cast<const uint64_t*>(s)[wi];
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kKwThreads) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
+  __shared__ __attribute__((aligned(16))) Elem bufA[kKwCap];
+  __shared__ __attribute__((aligned(16))) Elem bufB[kKwCap];
+  __shared__ int seg[kKwMaxRuns + 1];
+  __shared__ int64_t beg[kKwMaxRuns];
+  __shared__ int64_t s_start;
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = kd.G;  // cell_first[lo] <= b < cell_first[lo + 1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (kd.cell_first[mid] <= b)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const int g = lo;
+  const int c = (int)(b - kd.cell_first[g]);
+  const int ncell = (int)(kd.cell_first[g + 1] - kd.cell_first[g]);
+  const int r0 = kd.group_first[g], K = kd.group_first[g + 1] - r0;
+  kw_slices(kd, g, c, ncell, r0, K, seg, beg, &s_start);
+  __syncthreads();
+  const int n = seg[K];
+  uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
+  if (n > kKwCap) {  // uniform across the block
+    if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
+    // wave-level priority queue: lanes own runs; each step a wave argmin picks the next record
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    constexpr int kWords = kTeraRecordBytes / 8;
+    // positions: beg[k] advances in place; ends from the slice table
+    for (int64_t i = 0; i < n; ++i) {
+      Elem best{~0ull, ~0ull};
+      int bk = -1;
+      for (int k = lane; k < K; k += 64) {
+        const int64_t p = beg[k];
+        const int64_t end = (c + 1 == ncell) ? kd.runs[r0 + k].nrec
+                                              : kd.split[(int64_t)(r0 + k) * (kd.nbmax + 2) + c + 1];
+        if (p < end) {
+          const Elem e = load_key_elem(kd.runs[r0 + k].base + p * kTeraRecordBytes, r0 + k, p, kd.bad_layout);
+          if (bk < 0 || kle(e, best)) {
+            best = e;
+            bk = k;
+          }
+        }
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t oh = __shfl_xor(best.hi, off, 64), ol = __shfl_xor(best.lo, off, 64);
+        const int ok = __shfl_xor(bk, off, 64);
+        const bool take = ok >= 0 && (bk < 0 || oh < best.hi || (oh == best.hi && ol < best.lo));
+        if (take) {
+          best.hi = oh;
+          best.lo = ol;
+          bk = ok;
+        }
+      }
+      const int run = (int)((best.lo >> 32) & 0xFFFF);
+      const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(kd.runs[run].base + pos * kTeraRecordBytes);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
+      if (lane < kWords) dst[lane] = src[lane];
+      if (lane == 0) beg[bk] = pos + 1;
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+    }
+    return;
+  }
+  // ---- F2: keys of every slice into LDS
+  for (int i = threadIdx.x; i < n; i += kKwThreads) {
+    int sl = 0, sh = K;  // seg[sl] <= i < seg[sl + 1]
+    while (sh - sl > 1) {
+      const int mid = (sl + sh) >> 1;
+      if (seg[mid] <= i)
+        sl = mid;
+      else
+        sh = mid;
+    }
+    const int64_t pos = beg[sl] + (i - seg[sl]);
+    bufA[i] = load_key_elem(kd.runs[r0 + sl].base + pos * kTeraRecordBytes, r0 + sl, pos, kd.bad_layout);
+  }
+  __syncthreads();
+  // ---- F3: pairwise merge levels inside LDS
+  Elem* src = bufA;
+  Elem* dst = bufB;
+  const int o0 = threadIdx.x * kKwItems;
+  for (int w = 1; w < K; w <<= 1) {
+    if (o0 < n) {
+      const int npairs = (K + 2 * w - 1) / (2 * w);
+      // pair p covers segments [2pw, 2pw + 2w): find the pair holding output o0
+      int pl = 0, ph = npairs;
+      while (ph - pl > 1) {
+        const int mid = (pl + ph) >> 1;
+        if (seg[min(2 * mid * w, K)] <= o0)
+          pl = mid;
+        else
+          ph = mid;
+      }
+      int p = pl;
+      int a0 = seg[min(2 * p * w, K)], a1 = seg[min((2 * p + 1) * w, K)], b1 = seg[min((2 * p + 2) * w, K)];
+      // merge path at diagonal o0 - a0 within the pair
+      int d = o0 - a0, la = a1 - a0, lb = b1 - a1;
+      int ml = d > lb ? d - lb : 0, mh = d < la ? d : la;
+      while (ml < mh) {
+        const int mid = (ml + mh) >> 1;
+        if (kle(src[a0 + mid], src[a1 + d - 1 - mid]))
+          ml = mid + 1;
+        else
+          mh = mid;
+      }
+      int ia = ml, ib = d - ml;
+      const int todo = min(kKwItems, n - o0);
+      for (int k = 0; k < todo; ++k) {
+        const int o = o0 + k;
+        while (o == b1) {  // next pair (empty pairs are skipped)
+          ++p;
+          a0 = b1;
+          a1 = seg[min((2 * p + 1) * w, K)];
+          b1 = seg[min((2 * p + 2) * w, K)];
+          la = a1 - a0;
+          lb = b1 - a1;
+          ia = 0;
+          ib = 0;
+        }
+        const bool take_a = ib >= lb || (ia < la && kle(src[a0 + ia], src[a1 + ib]));
+        dst[o] = take_a ? src[a0 + ia] : src[a1 + ib];
+        if (take_a)
+          ++ia;
+        else
+          ++ib;
+      }
+    }
+    __syncthreads();
+    Elem* t = src;
+    src = dst;
+    dst = t;
+  }
+  // ---- F4: records in merged order straight to the output
+  const int wave = threadIdx.x >> 6;
+  for (int base = wave * 64; base < n; base += kKwWaves * 64) {
+    const int valid = min(64, n - base);
+    kw_gather64(kd, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+  }
+}
+
+void launch_pick_splitters(const Elem* samples, const int64_t* gsamp_off, const int64_t* gcells, int G, int nbmax,
+                           Elem* bounds, hipStream_t s) {
+  const int64_t n = (int64_t)G * nbmax;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pick_splitters_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, samples, gsamp_off,
+                     gcells, G, nbmax, bounds);
+}
+
+void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
+  if (ncells <= 0) return;
+  hipLaunchKernelGGL(kway_tile_kernel, dim3((unsigned)ncells), dim3(kKwThreads), 0, s, kd, out);
+}
+
+}  // namespace gpu
+}  // namespace uda

@@ -188,3 +188,26 @@ def test_disk_store_refuses_local_group(require_gpu, tmp_path):
                          sample_every=64, **SMALL)
     with pytest.raises(Exception, match="RCCL"):
         make_local_group(2, cfg, group="disk2")
+
+
+@pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}])
+def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
+    """The single-pass K-way merge (default) and the pairwise merge-path tree (UDA_KWAY=0) order
+    records identically; UDA_KWAY_TARGET above the LDS capacity routes every cell through the
+    wave-level priority queue, which must give the same stream."""
+    ref = _job(60000, 6, 2, reducers=2, **SMALL)
+    readers = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
+    ref.use_python_sink(lambda r, b: readers[r].feed(b), with_reducer=True)
+    st = ref.step()
+    ref.check(st)
+    assert st["merge_passes"] == 1  # single pass
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alt = _job(60000, 6, 2, reducers=2, **SMALL)
+    readers2 = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
+    alt.use_python_sink(lambda r, b: readers2[r].feed(b), with_reducer=True)
+    st2 = alt.step()
+    alt.check(st2)
+    assert [r.records for r in readers2] == [r.records for r in readers]
+    if "UDA_KWAY" in env:
+        assert st2["merge_passes"] == 3  # ceil(log2(6)) pairwise passes
