@@ -439,49 +439,6 @@ __global__ void __launch_bounds__(256) f1_expand_kernel(const int64_t* nbytes, c
   }
 }
 
-// Pass 2: one wave per chunk; ck_ord[c] = global ordinal of the chunk's first record (exclusive
-// scan of ck_count); chunk_run[c] = its run. Writes offsets[run][ord - run_first] for its records.
-__global__ void __launch_bounds__(kF1Lanes) f1_index_kernel(uint8_t* const* bases, const int64_t* nbytes,
-                                                            const int64_t* chunk_base, const int32_t* chunk_run,
-                                                            const int64_t* ck_start, const int64_t* ck_count,
-                                                            const int64_t* ck_ord, const int64_t* elem_off,
-                                                            const int64_t* rec_bytes, int64_t* const* offsets,
-                                                            int64_t total_chunks) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kF1Chunk + 2 * 64];
-  const int64_t c = blockIdx.x;
-  if (c >= total_chunks) return;
-  const int64_t here = ck_count[c];
-  const int r = chunk_run[c];
-  const int64_t n = nbytes[r];
-  const uint8_t* p = bases[r];
-  const int64_t c0 = (c - chunk_base[r]) * kF1Chunk;
-  const int lane = threadIdx.x;
-  if (here > 0) {
-    uint32_t w[16];
-    f1_fetch64(p, n, c0 + (int64_t)lane * kF1Bytes, w);
-    f1_stage(buf, lane, w);
-    if (lane == 0) {
-      uint32_t h[16];
-      f1_fetch64(p, n, c0 + kF1Chunk, h);
-      uint32_t* d = reinterpret_cast<uint32_t*>(buf + kF1Chunk);
-#pragma unroll
-      for (int k = 0; k < kF1Halo / 4; ++k) d[k] = h[k];
-    }
-    __syncthreads();
-    if (lane == 0) {
-      const int lim = (int)((n - c0) < (int64_t)(kF1Chunk + kF1Halo) ? (n - c0) : (kF1Chunk + kF1Halo));
-      int64_t* out = offsets[r] + (ck_ord[c] - elem_off[r]);
-      int64_t pos = ck_start[c];
-      for (int64_t i = 0; i < here; ++i) {
-        out[i] = pos;
-        pos += f1_record(buf, (int)(pos - c0), lim, n - pos);
-      }
-    }
-  }
-  // the first chunk of a run writes the run's terminating offset (record bytes from pass 1)
-  if (c == chunk_base[r] && lane == 0) offsets[r][elem_off[r + 1] - elem_off[r]] = rec_bytes[r];
-}
-
 // Pass 2, one lane per chunk: the chunk's records are walked straight from memory (each lane streams
 // its own 4 KiB chunk through the caches), so 64 chunks progress per wave instead of one.
 __global__ void __launch_bounds__(256) f1_index_lane_kernel(uint8_t* const* bases, const int64_t* nbytes,
