@@ -85,3 +85,13 @@ def test_async_io_backends(native, tmp_path, backend):
     assert ok
     if backend == "threadpool":
         assert name == "threadpool"
+
+
+@pytest.mark.parametrize("name", [v[0] for v in __import__("tests.lzo_vectors", fromlist=["VECTORS"]).VECTORS])
+def test_lzo1x_spec_vectors(native, name):
+    """Hand-assembled LZO1X streams (independent of the in-tree encoder) decode to the output the
+    format defines, through the raw decoder and the Hadoop block framing."""
+    from tests.lzo_vectors import VECTORS, hadoop_block
+    stream, want = {v[0]: (v[1], v[2]) for v in VECTORS}[name]
+    assert native.lzo1x_decompress(stream, len(want)) == want
+    assert native.block_decompress(2, hadoop_block(want, stream), 7) == want

@@ -104,3 +104,12 @@ def test_consumer_gpu_backend_decodes_on_device(require_gpu, tmp_path, codec):
         assert sorted(recs) == sorted(want)
     finally:
         p.close()
+
+
+def test_lzo1x_spec_vectors_on_device(require_gpu, native):
+    """The device LZO1X decoder on hand-assembled streams (not produced by our encoder)."""
+    from tests.lzo_vectors import VECTORS, hadoop_block
+    streams = [hadoop_block(want, st) for _, st, want in VECTORS]
+    outs, blocks, _ = native.gpu_block_decode("lzo", streams)
+    assert blocks == len(VECTORS)
+    assert outs == [want for _, _, want in VECTORS]
