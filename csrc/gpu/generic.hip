@@ -203,26 +203,16 @@ constexpr int32_t kFnInvalid = INT32_MIN;      // corrupt/truncated record on th
 constexpr int32_t kFnFallback = INT32_MIN + 1;  // exit offset not representable
 constexpr int64_t kSupInvalid = -1, kSupFallback = -2;  // super codes; EOF at q -> -3 - q
 
-// Chains that reach the same record start continue identically, so the 256 chains of a chunk are
-// walked with ownership marks in LDS: the first chain to reach a position owns it (mark = chain id
-// and its record count there); a later chain stops and inherits the owner's exit, adding the
-// owner's remaining records. Walk work drops from 256 chains x records to ~ records + merges.
-constexpr int kF1FnWavesM = 2;
-
-__global__ void __launch_bounds__(64 * kF1FnWavesM) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
+__global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                                  const int64_t* chunk_base, const int32_t* chunk_run,
                                                                  int64_t nchunks, int32_t* fx, int32_t* fn) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWavesM][kF1Chunk + 64];
-  __shared__ uint32_t mark[kF1FnWavesM][kF1Chunk];
-  __shared__ int32_t s_code[kF1FnWavesM][kF1Entries], s_cnt[kF1FnWavesM][kF1Entries];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * kF1FnWavesM + wv;
+  const int64_t c = (int64_t)blockIdx.x * kF1FnWaves + wv;
   const bool valid = c < nchunks;
   uint8_t* buf = lds[wv];
-  uint32_t* mk = mark[wv];
   int r = 0;
   int64_t n = 0, c0 = 0;
-  for (int k = lane; k < kF1Chunk; k += 64) mk[k] = 0;
   if (valid) {
     r = chunk_run[c];
     n = nbytes[r];
@@ -240,83 +230,44 @@ __global__ void __launch_bounds__(64 * kF1FnWavesM) f1_fn_kernel(uint8_t* const*
     }
   }
   __syncthreads();
-  const int end_rel = valid ? (int)min((int64_t)kF1Chunk, n - c0) : 0;
-  const int lim = valid ? (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo)) : 0;
-  int32_t pos[4], cnt[4], code[4], owner[4], at_cnt[4];
+  if (!valid) return;
+  const int end_rel = (int)min((int64_t)kF1Chunk, n - c0);
+  const int lim = (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo));
+  int64_t pos[4];
+  int32_t cnt[4], code[4];
   bool act[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int e = lane + 64 * j;
-    pos[j] = e;
+    pos[j] = lane + 64 * j;
     cnt[j] = 0;
-    owner[j] = -1;
-    at_cnt[j] = 0;
-    act[j] = e < end_rel;
-    code[j] = e;
-    if (act[j]) mk[e] = ((uint32_t)(e + 1) << 16);  // every chain owns its entry (count 0)
+    act[j] = pos[j] < end_rel;
+    code[j] = (int32_t)pos[j];
   }
-  __syncthreads();
   while (act[0] || act[1] || act[2] || act[3]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (!act[j]) continue;
-      const int64_t sz = f1_record(buf, pos[j], lim, n - (c0 + pos[j]));
-      if (sz <= 0) {
-        code[j] = sz == 0 ? (int32_t)(-1 - pos[j]) : kFnInvalid;
-        act[j] = false;
-        continue;
-      }
-      const int64_t np = (int64_t)pos[j] + sz;
-      ++cnt[j];
-      if (np >= end_rel) {
-        act[j] = false;
-        code[j] = np > (int64_t)INT32_MAX ? kFnFallback : (int32_t)np;
-        pos[j] = (int32_t)min(np, (int64_t)INT32_MAX);
-        continue;
-      }
-      pos[j] = (int32_t)np;
-      const uint32_t mine = ((uint32_t)(lane + 64 * j + 1) << 16) | (uint32_t)cnt[j];
-      const uint32_t old = atomicCAS(&mk[np], 0u, mine);
-      if (old != 0) {  // another chain was here first: same walk from now on
-        owner[j] = (int)(old >> 16) - 1;
-        at_cnt[j] = (int)(old & 0xFFFF);
-        act[j] = false;
-      }
-    }
-  }
-  // resolve joins (owners first; chains only join earlier-claimed positions, so no cycles)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = lane + 64 * j;
-    s_code[wv][e] = owner[j] < 0 ? code[j] : kFnInvalid;
-    s_cnt[wv][e] = owner[j] < 0 ? cnt[j] : -1;
-  }
-  __syncthreads();
-  for (int it = 0; it < kF1Entries; ++it) {
-    int pending = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = lane + 64 * j;
-      if (owner[j] >= 0 && s_cnt[wv][e] < 0) {
-        const int oc = s_cnt[wv][owner[j]];
-        if (oc >= 0) {
-          s_code[wv][e] = s_code[wv][owner[j]];
-          s_cnt[wv][e] = cnt[j] + (oc - at_cnt[j]);
+      if (act[j]) {
+        const int64_t sz = f1_record(buf, (int)pos[j], lim, n - (c0 + pos[j]));
+        if (sz <= 0) {
+          code[j] = sz == 0 ? (int32_t)(-1 - pos[j]) : kFnInvalid;
+          act[j] = false;
         } else {
-          pending = 1;
+          pos[j] += sz;
+          ++cnt[j];
+          if (pos[j] >= end_rel) {
+            act[j] = false;
+            code[j] = pos[j] > (int64_t)INT32_MAX ? kFnFallback : (int32_t)pos[j];
+          }
         }
       }
     }
-    if (!__syncthreads_or(pending)) break;
   }
-  if (!valid) return;
   int32_t* x = fx + c * kF1Entries;
   int32_t* m = fn + c * kF1Entries;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int e = lane + 64 * j;
-    x[e] = s_code[wv][e];
-    m[e] = s_cnt[wv][e] < 0 ? 0 : s_cnt[wv][e];
+    x[lane + 64 * j] = code[j];
+    m[lane + 64 * j] = cnt[j];
   }
 }
 
@@ -675,8 +626,8 @@ void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns,
   int64_t* sup_entry = sn + nsup * kF1Entries;
   int64_t* sup_first = sup_entry + nsup;
   if (nchunks > 0) {
-    hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWavesM - 1) / kF1FnWavesM)),
-                       dim3(64 * kF1FnWavesM), 0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn);
+    hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWaves - 1) / kF1FnWaves)), dim3(64 * kF1FnWaves),
+                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn);
     hipLaunchKernelGGL(f1_super_kernel, dim3((unsigned)((nsup + 3) / 4)), dim3(256), 0, s, nbytes, chunk_base,
                        sup_base, sup_run, nsup, fx, fn, sx, sn);
     (void)hipMemsetAsync(sup_entry, 0xFF, (size_t)nsup * 8, s);

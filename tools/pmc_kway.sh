@@ -13,3 +13,6 @@ for mode in kway tree; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc2_$mode -o run -- $S > /dev/null 2>&1 || exit 4
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc3_$mode -o run -- $S > /dev/null 2>&1 || exit 5
 done
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_generic.py tests/test_gpu_api_device.py > gpurun_out/pt7.log 2>&1 || exit 6
+timeout -k 10 200 python benchmarks/run_configs.py secondary_sort --gb 2 --maps 64 > gpurun_out/sec2.log 2>&1 || exit 7
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_sec -o run -- python benchmarks/run_configs.py secondary_sort --gb 2 --maps 64 > /dev/null 2>&1 || exit 8
