@@ -192,6 +192,9 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   // single-pass K-way tables: runs, bases, counts, sample offsets, bound sets, group / cell tables
   slot_bytes_ += (size_t)max_runs * (sizeof(RunDesc) + 4 * sizeof(int64_t) + 2 * sizeof(int)) + 64 * 16;
   if (const char* e = std::getenv("UDA_KWAY")) kway_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("UDA_KWAY_CAP")) kw_cap_ = std::atoi(e);
+  if (const char* e = std::getenv("UDA_KWAY_THREADS")) kw_threads_ = std::atoi(e) == 512 ? 512 : 256;
+  if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536 or 2048");
   kw_overflow_.alloc(sizeof(int));
   HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
   slots_.resize(4);
@@ -234,7 +237,7 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
   if (kway_) {
     int kmax = 0;
     for (size_t g = 0; g + 1 < group_first.size(); ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
-    if (kmax <= 128) return merge_kway(runs, group_first, out, s);
+    if (kmax <= kKwMaxRuns) return merge_kway(runs, group_first, out, s);
   }
 
   Slot& slot = slots_[next_slot_];
@@ -297,6 +300,33 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
   return total;
 }
 
+// Tools: mean per-cell time of the k-way kernel phases (slices, F2 keys, F3 LDS merge, F4 gather)
+// and the kernel span, from the per-workgroup wall-clock stamps. Synchronizes `s`.
+static void report_kway_phases(const unsigned long long* dprof, int64_t ncells, hipStream_t s) {
+  std::vector<unsigned long long> h((size_t)ncells * 5);
+  HIP_CHECK(hipMemcpyAsync(h.data(), dprof, h.size() * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  int dev = 0, khz = 100000;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  double sum[4] = {0, 0, 0, 0};
+  unsigned long long t_min = ~0ull, t_max = 0;
+  int64_t n = 0;
+  for (int64_t c = 0; c < ncells; ++c) {
+    const unsigned long long* p = &h[(size_t)c * 5];
+    if (!p[4]) continue;  // overflow cells (PQ path) end early
+    for (int k = 0; k < 4; ++k) sum[k] += (double)(p[k + 1] - p[k]);
+    t_min = std::min(t_min, p[0]);
+    t_max = std::max(t_max, p[4]);
+    ++n;
+  }
+  if (!n) return;
+  const double us = 1000.0 / khz;
+  std::fprintf(stderr, "kway phases (mean us/cell over %lld cells): slices %.2f f2 %.2f f3 %.2f f4 %.2f | span %.1f us\n",
+               (long long)n, sum[0] / n * us, sum[1] / n * us, sum[2] / n * us, sum[3] / n * us,
+               (double)(t_max - t_min) * us);
+}
+
 // Single-pass K-way merge (kway.hip): sample -> merge the samples per group -> splitters ->
 // per-run cell splits -> one workgroup per cell doing F2 + F3 + F4 in LDS.
 int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
@@ -305,9 +335,10 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   const int G = (int)group_first.size() - 1;
   int kmax = 1;
   for (int g = 0; g < G; ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
-  int64_t T = kKwCap / 2;  // target records per cell
+  const int64_t cap = kw_cap_;
+  int64_t T = cap / 2;  // target records per cell
   if (const char* e = std::getenv("UDA_KWAY_TARGET")) T = std::max<int64_t>(1, std::atoll(e));  // tests: force the PQ path
-  const int64_t step = std::max<int64_t>(1, (kKwCap - std::min<int64_t>(T, kKwCap)) / (kmax + 2));  // cell <= T + K*step
+  const int64_t step = std::max<int64_t>(1, (cap - std::min<int64_t>(T, cap)) / (kmax + 2));  // cell <= T + K*step
   std::vector<int64_t> soff(K + 1, 0), nrec(K);
   std::vector<uint8_t*> bases(K);
   std::vector<int> bset(K);
@@ -339,6 +370,7 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   };
   ensure(samp_a_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
   ensure(samp_b_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(samp_runs_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
   ensure(kw_bounds_, (size_t)std::max<int64_t>((int64_t)G * nbmax, 1) * sizeof(Elem));
   ensure(kw_split_, (size_t)K * per * sizeof(int64_t));
 
@@ -380,22 +412,27 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   HIP_CHECK(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipEventRecord(slot.uploaded, s));
 
-  // splitters: a regular sample of every run, merged per group, every (ns_g / C_g)-th kept
-  Elem* sa = samp_a_.as<Elem>();
-  Elem* sb = samp_b_.as<Elem>();
+  // splitters: a regular sample of every run, merged per group, every (ns_g / C_g)-th kept; the
+  // per-run sample stays intact (first merge pass reads it) and brackets the split searches
+  Elem* sr = samp_runs_.as<Elem>();
+  Elem* sbuf[2] = {samp_a_.as<Elem>(), samp_b_.as<Elem>()};
   if (ns > 0)
     launch_sample_fixed(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec), K,
-                        step, reinterpret_cast<const int64_t*>(d + o_soff), ns, sa, s);
+                        step, reinterpret_cast<const int64_t*>(d + o_soff), ns, sr, s);
+  const Elem* merged = sr;
+  int w = 0;
   for (const auto& pd : pds) {
-    launch_merge_partition(sa, pd, splits_.as<int64_t>(), s);
-    launch_merge_pass(sa, sb, pd, splits_.as<int64_t>(), s);
-    std::swap(sa, sb);
+    launch_merge_partition(merged, pd, splits_.as<int64_t>(), s);
+    launch_merge_pass(merged, sbuf[w], pd, splits_.as<int64_t>(), s);
+    merged = sbuf[w];
+    w ^= 1;
   }
-  launch_pick_splitters(sa, reinterpret_cast<const int64_t*>(d + o_gs), reinterpret_cast<const int64_t*>(d + o_gc), G,
-                        (int)nbmax, kw_bounds_.as<Elem>(), s);
-  launch_split_fixed(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec),
-                     nbmax > 0 ? kw_bounds_.as<Elem>() : nullptr, reinterpret_cast<const int*>(d + o_bset), K,
-                     (int)nbmax, kw_split_.as<int64_t>(), s);
+  launch_pick_splitters(merged, reinterpret_cast<const int64_t*>(d + o_gs), reinterpret_cast<const int64_t*>(d + o_gc),
+                        G, (int)nbmax, kw_bounds_.as<Elem>(), s);
+  launch_split_sampled(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec), sr,
+                       reinterpret_cast<const int64_t*>(d + o_soff), step,
+                       nbmax > 0 ? kw_bounds_.as<Elem>() : nullptr, reinterpret_cast<const int*>(d + o_bset), K,
+                       (int)nbmax, kw_split_.as<int64_t>(), s);
   KwayDesc kd;
   kd.runs = reinterpret_cast<const RunDesc*>(d + o_runs);
   kd.group_first = reinterpret_cast<const int*>(d + o_gf);
@@ -406,7 +443,16 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   kd.G = G;
   kd.overflow = kw_overflow_.as<int>();
   kd.bad_layout = flag_.as<int>();
+  kd.cap = (int)cap;
+  kd.threads = kw_threads_;
+  static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
+  if (prof) {
+    ensure(kw_prof_, (size_t)cell_first[G] * 5 * 8);
+    HIP_CHECK(hipMemsetAsync(kw_prof_.as(), 0, (size_t)cell_first[G] * 5 * 8, s));
+    kd.prof = kw_prof_.as<unsigned long long>();
+  }
   launch_kway_tiles(kd, cell_first[G], out, s);
+  if (prof) report_kway_phases(kd.prof, cell_first[G], s);
   last_passes_ = 1;
   return total_records(runs);
 }

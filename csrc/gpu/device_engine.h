@@ -182,7 +182,9 @@ class DeviceMerger {
   DeviceBuffer flag_;
   // single-pass K-way merge (kway.hip): samples (ping-pong), splitters, cell split table, overflow
   bool kway_ = true;
-  DeviceBuffer samp_a_, samp_b_, kw_bounds_, kw_split_, kw_overflow_;
+  int kw_cap_ = 1536;  // records per k-way cell (UDA_KWAY_CAP): 3 workgroups per CU fit LDS
+  int kw_threads_ = 256;  // k-way workgroup size (UDA_KWAY_THREADS)
+  DeviceBuffer kw_prof_, samp_runs_, samp_a_, samp_b_, kw_bounds_, kw_split_, kw_overflow_;
   std::vector<Slot> slots_;
   int next_slot_ = 0;
   int last_passes_ = 0;

@@ -108,7 +108,7 @@ void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int
 
 // ---------------------------------------------------------------- single-pass K-way merge (F2+F3+F4)
 constexpr int kKwCap = 2048;       // records per cell (LDS capacity of one workgroup)
-constexpr int kKwMaxRuns = 1024;   // runs per group on the LDS path
+constexpr int kKwMaxRuns = 128;    // runs per group on the single-pass path
 struct KwayDesc {
   const RunDesc* runs;        // every run of the round, grouped by reducer
   const int* group_first;     // G+1
@@ -119,12 +119,21 @@ struct KwayDesc {
   int G;
   int* overflow;              // cells merged by the wave-level PQ (did not fit LDS)
   int* bad_layout;            // set if a record is not TeraSort-shaped
+  int cap = kKwCap;           // records per cell on the LDS path (kway_cap_supported)
+  int threads = 256;          // workgroup size: 256 or 512
+  unsigned long long* prof = nullptr;  // optional [cell][5] phase timestamps (UDA_KWAY_PROF)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.
 void launch_pick_splitters(const Elem* samples, const int64_t* gsamp_off, const int64_t* gcells, int G, int nbmax,
                            Elem* bounds, hipStream_t s);
 void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s);
+int kway_cap_supported(int cap);
+// split[r][c] for the k-way cells, bracketed by the run's own regular sample (soff / every as given
+// to launch_sample_fixed; samples in per-run order, not merged).
+void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem* samples, const int64_t* soff,
+                          int64_t every, const Elem* bounds, const int* run_bound_set, int nruns, int nb, int64_t* out,
+                          hipStream_t s);
 
 // ---------------------------------------------------------------- GENERIC record path (F1/F2/F4)
 // F1 pass 1 (one wave per run): chunk checkpoints ck_start/ck_count for the chunks of run r at

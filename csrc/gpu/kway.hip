@@ -10,36 +10,54 @@
 //    each run gives the cell slices. With s = (cap - T) / (K + 2) a cell holds at most
 //    T + K*s <= cap records (T = target), so it always fits LDS; output offsets are the sums of the
 //    lower bounds, no scan needed.
-//  * One workgroup per cell (256 threads, cap = 2048 records): the slices' keys are loaded once
-//    from the records into LDS as 16-byte elements (F2), the K sorted slices are merged pairwise
-//    inside LDS (log2 K levels, merge path per thread, ping-pong between two 32 KiB buffers: no HBM
-//    traffic between levels), and the records are gathered straight to the output (F4): one wave
-//    per 64 output records, 13 consecutive 8-byte words per record, 512-byte coalesced stores.
-//    HBM traffic per record: its key cache line, then one record read and one record write.
+//  * One workgroup per cell (256 threads; cap = 1536 records by default, 512..2048 selectable):
+//    the slices' keys are loaded once from the records into LDS as 16-byte elements (F2), the K
+//    sorted slices are merged pairwise inside LDS (log2 K levels, merge path per thread, ping-pong
+//    between two cap x 16-byte buffers: no HBM traffic between levels), and the records are
+//    gathered straight to the output (F4): one wave per 64 output records, 13 consecutive 8-byte
+//    words per record, 512-byte coalesced stores. HBM traffic per record: its key line, then one
+//    record read and one record write.
+//  * The kernel is latency-bound (PMC: 66% of wave cycles waiting, HBM at ~3.5 TB/s read+write),
+//    so every phase keeps its loads in flight together: F2 issues all of a thread's key loads
+//    before the first LDS write, F4 all 13 word loads of a lane before its first store (with no
+//    per-lane guards on full waves, which would split the stores into blocks that each drain
+//    vmcnt). 1536-record cells fit 3 workgroups per CU (51 KiB LDS each, 91 VGPRs); per-phase
+//    timings come from UDA_KWAY_PROF (profiles/r2_kway_tuning.md).
 //  * A cell that would not fit LDS (only possible with massively duplicated keys) is merged by a
 //    wave-level priority queue: lanes own runs, a wave argmin picks the next record each step.
 #include "kernels.h"
+
+#include <mutex>
+#include <stdexcept>
+#include <string>
 
 namespace uda {
 namespace gpu {
 
 namespace {
-constexpr int kKwThreads = 256;
-constexpr int kKwWaves = kKwThreads / 64;
-constexpr int kKwItems = kKwCap / kKwThreads;  // 8
 
 __device__ __forceinline__ bool kle(const Elem& a, const Elem& b) {
   return a.hi < b.hi || (a.hi == b.hi && a.lo <= b.lo);
 }
 
-__device__ __forceinline__ Elem load_key_elem(const uint8_t* rec, int run, int64_t pos, int* bad) {
-  const uint64_t w0 = *reinterpret_cast<const uint64_t*>(rec);
-  const uint64_t w1 = *reinterpret_cast<const uint64_t*>(rec + 8);
-  if ((w0 & 0xFFFFFF) != 0x0A5B0B || ((w1 >> 40) & 0xFF) != 0x5A) *bad = 1;
+typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
+// Run pointers are generic; the records live in global memory, so load through that address space.
+__device__ __forceinline__ const GlobalU64* gptr(const void* p) { return (const GlobalU64*)(uintptr_t)p; }
+
+__device__ __forceinline__ Elem key_elem(uint64_t w0, uint64_t w1, int run, int64_t pos, int& bad) {
+  bad |= (w0 & 0xFFFFFF) != 0x0A5B0B || ((w1 >> 40) & 0xFF) != 0x5A;
   const uint64_t b0 = __builtin_bswap64(w0), b1 = __builtin_bswap64(w1);
   Elem e;
   e.hi = (b0 << 24) | (b1 >> 40);
   e.lo = (((b1 >> 24) & 0xFFFF) << 48) | ((uint64_t)run << 32) | (uint64_t)pos;
+  return e;
+}
+
+__device__ __forceinline__ Elem load_key_elem(const uint8_t* rec, int run, int64_t pos, int* bad) {
+  const GlobalU64* w = gptr(rec);
+  int b = 0;
+  const Elem e = key_elem(w[0], w[1], run, pos, b);
+  if (b) *bad = 1;
   return e;
 }
 
@@ -59,6 +77,56 @@ __global__ void __launch_bounds__(256) pick_splitters_kernel(const Elem* samples
     b.lo = s.lo & (0xFFFFull << 48);
   }
   bounds[t] = b;
+}
+
+// Cell split points: split[r][c] = first record of run r with key >= splitter c-1 of its group. The
+// run's own regular sample (sample j = record j*every + every/2, sorted like the run) brackets the
+// answer first, so only ~log2(every) probes touch the 104-byte records; the dense 16-byte samples
+// stay in L2. (A plain binary search over the run costs ~log2(nrec) scattered record lines.)
+__global__ void __launch_bounds__(256) split_sampled_kernel(uint8_t* const* bases, const int64_t* nrec,
+                                                            const Elem* samples, const int64_t* soff, int64_t every,
+                                                            const Elem* bounds, const int* run_bound_set, int nruns,
+                                                            int nb, int64_t* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = nb + 2;
+  if (t >= (int64_t)nruns * per) return;
+  const int r = (int)(t / per);
+  const int b = (int)(t % per);
+  const int64_t n = nrec[r];
+  if (b == 0 || b == nb + 1) {
+    out[t] = b == 0 ? 0 : n;
+    return;
+  }
+  const Elem bound = bounds[(int64_t)run_bound_set[r] * nb + (b - 1)];
+  const uint64_t btail = bound.lo >> 48;
+  // first sample with key >= bound
+  const Elem* smp = samples + soff[r];
+  int64_t lo = 0, hi = soff[r + 1] - soff[r];
+  const int64_t ns = hi;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const Elem e = smp[mid];
+    if (e.hi < bound.hi || (e.hi == bound.hi && (e.lo >> 48) < btail))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  // samples lo-1 < bound <= sample lo: the answer lies in (pos(lo-1), pos(lo)]
+  int64_t a = lo > 0 ? (lo - 1) * every + every / 2 + 1 : 0;
+  int64_t z = lo < ns ? lo * every + every / 2 : n;
+  if (z > n) z = n;
+  const uint8_t* base = bases[r];
+  while (a < z) {
+    const int64_t mid = (a + z) >> 1;
+    const GlobalU64* w = gptr(base + mid * kTeraRecordBytes);
+    const uint64_t b0 = __builtin_bswap64(w[0]), b1 = __builtin_bswap64(w[1]);
+    const uint64_t kh = (b0 << 24) | (b1 >> 40), kl = (b1 >> 24) & 0xFFFF;
+    if (kh < bound.hi || (kh == bound.hi && kl < btail))
+      a = mid + 1;
+    else
+      z = mid;
+  }
+  out[t] = a;
 }
 
 // Exclusive scan of the K slice lengths into seg[0..K] and the sum of the slice starts (wave 0).
@@ -95,37 +163,70 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int 
   if (lane == 0) *start_sum = (int64_t)bsum;
 }
 
-// 13 x 8-byte words per record, one wave per 64 consecutive output records.
-__device__ __forceinline__ void kw_gather64(const KwayDesc& kd, const Elem* cur, int base, int valid, uint8_t* dst) {
+// 13 x 8-byte words per record, one wave per 64 consecutive output records. All 13 loads of a
+// lane are issued before its first store: written as load -> store pairs, the compiler must assume
+// the store may alias the next load and serializes 13 HBM round trips per 64 records.
+__device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0, const Elem* cur, int base, int valid,
+                                            uint8_t* dst) {
   constexpr int kWords = kTeraRecordBytes / 8;
   const int lane = threadIdx.x & 63;
   unsigned long long src = 0;
   if (lane < valid) {
     const Elem e = cur[base + lane];
     const int run = (int)((e.lo >> 32) & 0xFFFF);
-    src = (unsigned long long)(kd.runs[run].base + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes);
+    src = (unsigned long long)(rbase[run - r0] + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes);
   }
   uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+  uint64_t v[kWords];
+  if (valid == 64) {  // straight-line: per-lane guards would split the stores into blocks that each drain vmcnt
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) {
+      const int w = j * 64 + lane;
+      const int r = w / kWords;
+      v[j] = ((const GlobalU64*)__shfl(src, r, 64))[w - r * kWords];
+    }
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) d[j * 64 + lane] = v[j];
+    return;
+  }
   const int words = valid * kWords;
 #pragma unroll
   for (int j = 0; j < kWords; ++j) {
     const int w = j * 64 + lane;
     const int r = w / kWords;
-    const int wi = w - r * kWords;
     const unsigned long long s = __shfl(src, r < 64 ? r : 63, 64);
-    if (w < words) d[w] = reinterpret_cast<const uint64_t*>(s)[wi];
+    v[j] = w < words ? ((const GlobalU64*)s)[w - r * kWords] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kWords; ++j) {
+    const int w = j * 64 + lane;
+    if (w < words) d[w] = v[j];
   }
 }
 
 }  // namespace
 
-__global__ void __launch_bounds__(kKwThreads) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
-  __shared__ __attribute__((aligned(16))) Elem bufA[kKwCap];
-  __shared__ __attribute__((aligned(16))) Elem bufB[kKwCap];
+// ITEMS records per thread: the cell capacity is ITEMS * 256 and the two LDS buffers are dynamic
+// (2 * cap * 16 bytes), so smaller capacities fit more workgroups per CU.
+template <int ITEMS, int THREADS>
+__global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
+  constexpr int kKwItems = ITEMS;
+  constexpr int kKwThreads = THREADS;
+  constexpr int kKwWaves = THREADS / 64;
+  constexpr int kCap = ITEMS * kKwThreads;
+  extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
+  Elem* bufA = kw_dyn;
+  Elem* bufB = kw_dyn + kCap;
   __shared__ int seg[kKwMaxRuns + 1];
   __shared__ int64_t beg[kKwMaxRuns];
+  __shared__ const uint8_t* rbase[kKwMaxRuns];
   __shared__ int64_t s_start;
   const int64_t b = blockIdx.x;
+  // phase timestamps (tools only: kd.prof is null in production launches)
+  auto stamp = [&](int k) {
+    if (kd.prof && threadIdx.x == 0) kd.prof[b * 5 + k] = wall_clock64();
+  };
+  stamp(0);
   int lo = 0, hi = kd.G;  // cell_first[lo] <= b < cell_first[lo + 1]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -139,10 +240,12 @@ __global__ void __launch_bounds__(kKwThreads) kway_tile_kernel(KwayDesc kd, uint
   const int ncell = (int)(kd.cell_first[g + 1] - kd.cell_first[g]);
   const int r0 = kd.group_first[g], K = kd.group_first[g + 1] - r0;
   kw_slices(kd, g, c, ncell, r0, K, seg, beg, &s_start);
+  for (int k = threadIdx.x; k < K; k += kKwThreads) rbase[k] = kd.runs[r0 + k].base;
   __syncthreads();
+  stamp(1);
   const int n = seg[K];
   uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
-  if (n > kKwCap) {  // uniform across the block
+  if (n > kCap) {  // uniform across the block
     if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
     // wave-level priority queue: lanes own runs; each step a wave argmin picks the next record
     if (threadIdx.x >= 64) return;
@@ -186,20 +289,42 @@ __global__ void __launch_bounds__(kKwThreads) kway_tile_kernel(KwayDesc kd, uint
     }
     return;
   }
-  // ---- F2: keys of every slice into LDS
-  for (int i = threadIdx.x; i < n; i += kKwThreads) {
-    int sl = 0, sh = K;  // seg[sl] <= i < seg[sl + 1]
-    while (sh - sl > 1) {
-      const int mid = (sl + sh) >> 1;
-      if (seg[mid] <= i)
-        sl = mid;
-      else
-        sh = mid;
+  // ---- F2: keys of every slice into LDS (all of a thread's key loads in flight at once)
+  if (n > 0) {
+    uint64_t w0[kKwItems], w1[kKwItems];
+    int slv[kKwItems];
+    int64_t posv[kKwItems];
+#pragma unroll
+    for (int k = 0; k < kKwItems; ++k) {
+      // items past n re-read item n - 1: unguarded loads stay in one block and all stay in flight
+      const int i = min(threadIdx.x + k * kKwThreads, n - 1);
+      int sl = 0, sh = K;  // seg[sl] <= i < seg[sl + 1]
+      while (sh - sl > 1) {
+        const int mid = (sl + sh) >> 1;
+        if (seg[mid] <= i)
+          sl = mid;
+        else
+          sh = mid;
+      }
+      slv[k] = sl;
+      posv[k] = beg[sl] + (i - seg[sl]);
     }
-    const int64_t pos = beg[sl] + (i - seg[sl]);
-    bufA[i] = load_key_elem(kd.runs[r0 + sl].base + pos * kTeraRecordBytes, r0 + sl, pos, kd.bad_layout);
+#pragma unroll
+    for (int k = 0; k < kKwItems; ++k) {
+      const GlobalU64* rec = gptr(rbase[slv[k]] + posv[k] * kTeraRecordBytes);
+      w0[k] = rec[0];
+      w1[k] = rec[1];
+    }
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < kKwItems; ++k) {
+      const int i = threadIdx.x + k * kKwThreads;
+      if (i < n) bufA[i] = key_elem(w0[k], w1[k], r0 + slv[k], posv[k], bad);
+    }
+    if (bad) *kd.bad_layout = 1;
   }
   __syncthreads();
+  stamp(2);
   // ---- F3: pairwise merge levels inside LDS
   Elem* src = bufA;
   Elem* dst = bufB;
@@ -255,11 +380,17 @@ __global__ void __launch_bounds__(kKwThreads) kway_tile_kernel(KwayDesc kd, uint
     src = dst;
     dst = t;
   }
+  stamp(3);
   // ---- F4: records in merged order straight to the output
   const int wave = threadIdx.x >> 6;
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
-    kw_gather64(kd, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+    kw_gather64(rbase, r0, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+  }
+  if (kd.prof) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    stamp(4);
   }
 }
 
@@ -271,9 +402,41 @@ void launch_pick_splitters(const Elem* samples, const int64_t* gsamp_off, const 
                      gcells, G, nbmax, bounds);
 }
 
+void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem* samples, const int64_t* soff,
+                          int64_t every, const Elem* bounds, const int* run_bound_set, int nruns, int nb, int64_t* out,
+                          hipStream_t s) {
+  const int64_t total = (int64_t)nruns * (nb + 2);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(split_sampled_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, bases, nrec,
+                     samples, soff, every, bounds, run_bound_set, nruns, nb, out);
+}
+
+int kway_cap_supported(int cap) { return cap == 2048 || cap == 1536 || cap == 1024 || cap == 512; }
+
+namespace {
+template <int ITEMS, int THREADS>
+void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
+  const size_t lds = 2 * sizeof(Elem) * (size_t)(ITEMS * THREADS);
+  static std::once_flag once;
+  std::call_once(once, [] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, THREADS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(2 * sizeof(Elem) * ITEMS * THREADS));
+  });
+  hipLaunchKernelGGL((kway_tile_kernel<ITEMS, THREADS>), dim3((unsigned)ncells), dim3(THREADS), lds, s, kd, out);
+}
+}  // namespace
+
 void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
   if (ncells <= 0) return;
-  hipLaunchKernelGGL(kway_tile_kernel, dim3((unsigned)ncells), dim3(kKwThreads), 0, s, kd, out);
+  const bool wide = kd.threads == 512;
+  switch (kd.cap) {
+    case 2048: wide ? launch_kway<4, 512>(kd, ncells, out, s) : launch_kway<8, 256>(kd, ncells, out, s); break;
+    case 1536: wide ? launch_kway<3, 512>(kd, ncells, out, s) : launch_kway<6, 256>(kd, ncells, out, s); break;
+    case 1024: wide ? launch_kway<2, 512>(kd, ncells, out, s) : launch_kway<4, 256>(kd, ncells, out, s); break;
+    case 512: wide ? launch_kway<1, 512>(kd, ncells, out, s) : launch_kway<2, 256>(kd, ncells, out, s); break;
+    default: throw std::runtime_error("kway: unsupported cell capacity " + std::to_string(kd.cap));
+  }
 }
 
 }  // namespace gpu

@@ -392,14 +392,32 @@ __global__ void __launch_bounds__(256) gather_fixed_kernel(const Elem* elems, in
     src = (unsigned long long)(run_bases[run] + pos * kTeraRecordBytes);
   }
   uint64_t* dst = reinterpret_cast<uint64_t*>(out + rec0 * kTeraRecordBytes);
+  // every load of the lane before its first store (a load -> store chain serializes on aliasing),
+  // and no per-lane guards on full waves (guarded stores each drain vmcnt)
+  uint64_t v[kWords];
+  if (valid == 64) {
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) {
+      const int w = j * 64 + lane;
+      const int r = w / kWords;
+      v[j] = ((const __attribute__((address_space(1))) uint64_t*)__shfl(src, r, 64))[w - r * kWords];
+    }
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) dst[j * 64 + lane] = v[j];
+    return;
+  }
   const int words = valid * kWords;
 #pragma unroll
   for (int j = 0; j < kWords; ++j) {
     const int w = j * 64 + lane;
     const int r = w / kWords;
-    const int wi = w - r * kWords;
     const unsigned long long s = __shfl(src, r < 64 ? r : 63, 64);
-    if (w < words) dst[w] = reinterpret_cast<const uint64_t*>(s)[wi];
+    v[j] = w < words ? reinterpret_cast<const uint64_t*>(s)[w - r * kWords] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kWords; ++j) {
+    const int w = j * 64 + lane;
+    if (w < words) dst[w] = v[j];
   }
 }
 
