@@ -25,6 +25,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <cstring>
 #include <fstream>
@@ -82,6 +84,7 @@ struct DeviceWorkspace {
     for (auto e : piece_ev)
       if (e) (void)hipEventDestroy(e);
   }
+  void reset_stats() { h2d_ms = device_ms = d2h_ms = sink_ms = 0; }
   static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
     bytes = std::max<int64_t>(bytes, 16);
     if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
@@ -146,6 +149,8 @@ class EarlyStager {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& b : blocks_) b.used = 0;
     cur_ = 0;
+    issue_ms_ = 0;
+    bytes_ = 0;
   }
   double issue_ms() const { return issue_ms_; }
   int64_t bytes() const { return bytes_; }
@@ -209,6 +214,53 @@ class EarlyStager {
   size_t cur_ = 0;
   double issue_ms_ = 0;
   int64_t bytes_ = 0;
+};
+
+// Process-wide cache of the per-device objects a GPU reduce task builds (HBM workspaces, the
+// pinned D2H ring, the early-staging arena and its copy thread): one reducer process runs many
+// reduce tasks in sequence, and building these costs tens of ms per task (pinning a 128 MiB ring,
+// hipMalloc of GBs, hipFree synchronizing the device). An object goes back to the cache only
+// after a task that used it ended cleanly.
+template <class T>
+class DevicePool {
+ public:
+  static DevicePool& get() {
+    static DevicePool* p = new DevicePool;  // never destroyed: HIP may be torn down first at exit
+    return *p;
+  }
+  template <class Make>
+  std::unique_ptr<T> acquire(int device, Make&& make) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = idle_[device];
+      if (!v.empty()) {
+        std::unique_ptr<T> o = std::move(v.back());
+        v.pop_back();
+        return o;
+      }
+    }
+    return make();
+  }
+  void release(int device, std::unique_ptr<T> o) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& v = idle_[device];
+    if (v.size() < kMaxIdle) v.push_back(std::move(o));
+  }
+
+ private:
+  static constexpr size_t kMaxIdle = 4;
+  std::mutex mu_;
+  std::map<int, std::vector<std::unique_ptr<T>>> idle_;
+};
+
+template <class T>
+struct PoolLease {
+  int device;
+  std::unique_ptr<T> obj;
+  bool clean = false;  // set when the task ended without an error
+  ~PoolLease() {
+    if (obj && clean) DevicePool<T>::get().release(device, std::move(obj));
+  }
 };
 
 DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
@@ -384,11 +436,18 @@ void ReduceTask::merge_gpu() {
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
-  DeviceWorkspace ws;
+  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
+                                                  device, [] { return std::make_unique<DeviceWorkspace>(); })};
+  DeviceWorkspace& ws = *ws_lease.obj;
+  ws.reset_stats();
   // uncompressed partitions go to HBM as soon as each one is complete (overlapping the fetch)
-  std::unique_ptr<EarlyStager> stager;
-  if (fetch_codec == Codec::kNone && stage_codec == Codec::kNone && host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0)
-    stager.reset(new EarlyStager(device));
+  PoolLease<EarlyStager> stager_lease{device, nullptr};
+  EarlyStager* stager = nullptr;
+  if (fetch_codec == Codec::kNone && stage_codec == Codec::kNone && host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0) {
+    stager_lease.obj = DevicePool<EarlyStager>::get().acquire(device, [device] { return std::make_unique<EarlyStager>(device); });
+    stager = stager_lease.obj.get();
+    stager->reset();
+  }
   const int depth = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.fetch.depth", 4));
 
   std::vector<SpillRun> spills;
@@ -684,7 +743,11 @@ void ReduceTask::merge_gpu() {
 
     if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
-      if (stager) stager->flush();
+      if (stager) {
+        const auto tf = std::chrono::steady_clock::now();
+        stager->flush();
+        ws.h2d_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
+      }
       DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kv, s);
       count_decoded(m.decoded_blocks);
       deliver(m, true);
@@ -800,6 +863,9 @@ void ReduceTask::merge_gpu() {
       st_.bytes_delivered += kEofBytes;
     }
     cleanup(true);
+    HIP_CHECK(hipStreamSynchronize(s));
+    ws_lease.clean = true;
+    stager_lease.clean = true;
     std::lock_guard<std::mutex> g(st_mu_);
     st_.gpu_h2d_ms = ws.h2d_ms;
     st_.gpu_device_ms = ws.device_ms;
@@ -994,22 +1060,20 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     st_.merge_path = "device-fixed10";
     return true;
   }
-  // ---- any other key class: the generic merge tree over device copies of the partitions
-  DeviceWorkspace ws;
+  // ---- any other key class: the generic merge tree, reading the partitions where they live
+  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
+                                                  device, [] { return std::make_unique<DeviceWorkspace>(); })};
+  DeviceWorkspace& ws = *ws_lease.obj;
+  ws.reset_stats();
   int64_t total = 0;
-  for (const auto& p : parts) total += p->part_len;
-  DeviceWorkspace::ensure(ws.in, total);
-  DeviceWorkspace::ensure(ws.out, total);
   std::vector<const uint8_t*> rptr;
   std::vector<int64_t> rlen;
-  int64_t off = 0;
   for (const auto& p : parts) {
-    if (p->part_len > 0)
-      HIP_CHECK(hipMemcpyAsync(ws.in.as<uint8_t>() + off, p->dptr, (size_t)p->part_len, hipMemcpyDefault, s));
-    rptr.push_back(ws.in.as<uint8_t>() + off);
+    rptr.push_back(p->dptr);
     rlen.push_back(p->part_len);
-    off += p->part_len;
+    total += p->part_len;
   }
+  DeviceWorkspace::ensure(ws.out, total);
   const int64_t kv = kv_buf_size_ - kEofBytes;
   gpu::GenericMergeResult r = ws.merger.merge(rptr, rlen, (int)kind_, ws.out.as<uint8_t>(), total, kv, s);
   HIP_CHECK(hipStreamSynchronize(s));
@@ -1038,6 +1102,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     tail[0] = tail[1] = 0xFF;
     if (sink(tail.data(), kEofBytes) != 0) throw UdaError("dataFromUda callback failed");
   }
+  HIP_CHECK(hipStreamSynchronize(s));
+  ws_lease.clean = true;
   std::lock_guard<std::mutex> g(st_mu_);
   st_.records = m.records;
   st_.fetch_ms = fetch_ms;
