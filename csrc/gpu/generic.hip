@@ -54,13 +54,17 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 
-// Load bytes [at, at+64) of a run (zero beyond n) into registers.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 __attribute__((aligned(1))) u32x4_u;  // unaligned 16-byte access (legal for global memory)
+
+// Load bytes [at, at+64) of a run (zero beyond n) into registers. Runs start at any byte, so the
+// full-width case uses unaligned 16-byte loads (a byte-at-a-time fallback costs 64 loads per lane).
 __device__ __forceinline__ void f1_fetch64(const uint8_t* p, int64_t n, int64_t at, uint32_t (&w)[16]) {
-  if (at + 64 <= n && (((uintptr_t)(p + at)) & 15) == 0) {
-    const uint4* q = reinterpret_cast<const uint4*>(p + at);
+  if (at + 64 <= n) {
+    const u32x4_u* q = reinterpret_cast<const u32x4_u*>(p + at);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint4 v = q[k];
+      const u32x4 v = q[k];
       w[4 * k] = v.x;
       w[4 * k + 1] = v.y;
       w[4 * k + 2] = v.z;
@@ -199,14 +203,17 @@ __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases
 constexpr int kF1Entries = 256;
 constexpr int kF1Super = 64;
 constexpr int kF1FnWaves = 4;
+constexpr int kF1Warm = 2;  // lockstep steps of all chains before the survivors are compacted
 constexpr int32_t kFnInvalid = INT32_MIN;      // corrupt/truncated record on this chain
 constexpr int32_t kFnFallback = INT32_MIN + 1;  // exit offset not representable
 constexpr int64_t kSupInvalid = -1, kSupFallback = -2;  // super codes; EOF at q -> -3 - q
 
 __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                                  const int64_t* chunk_base, const int32_t* chunk_run,
-                                                                 int64_t nchunks, int32_t* fx, int32_t* fn) {
+                                                                 int64_t nchunks, int32_t* fx, int32_t* fn,
+                                                                 int key_kind) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
+  __shared__ int f1_live[kF1FnWaves][3 * kF1Entries];  // surviving chains: entry, position, count
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * kF1FnWaves + wv;
   const bool valid = c < nchunks;
@@ -233,41 +240,97 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
   if (!valid) return;
   const int end_rel = (int)min((int64_t)kF1Chunk, n - c0);
   const int lim = (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo));
-  int64_t pos[4];
-  int32_t cnt[4], code[4];
-  bool act[4];
+  const int64_t nrel64 = n - c0;
+  const int nrel = (int)min(nrel64, (int64_t)(1 << 30));  // records must end by here (fast path)
+  // One step of a chain: decode the record at pos (two sign-extending LDS byte reads and a few
+  // 32-bit ops in the common case; multi-byte VInt headers go to the general decoder).
+  auto step = [&](int& pos, int& cnt, int& code, bool& alive) {
+    const int p = alive ? pos : 0;
+    const int b0 = (int8_t)buf[p], b1 = (int8_t)buf[p + 1];  // p + 1 <= kF1Chunk: inside the staged chunk
+    int sz = 2 + b0 + b1;
+    bool fallback = false;
+    if (alive && ((b0 | b1) < 0 || p + 2 > lim)) {  // multi-byte VInt, EOF marker, or the run's tail
+      const int64_t s64 = f1_record(buf, p, lim, nrel64 - p);
+      fallback = s64 > (int64_t)(1 << 30);
+      sz = fallback ? 1 : (int)s64;
+    } else if (p + sz > nrel) {
+      sz = -1;
+    }
+    // Key framing check (fast path, lengths < 128): a Text key starts with its own VInt length
+    // (klen - 1), a BytesWritable key with a 4-byte big-endian klen - 4. A chain entered at a byte
+    // that is not a record start almost never passes, so garbage chains end after one step. A
+    // failing chain ends as "fallback", never "corrupt": if it were the true chain, the run is
+    // re-indexed by the serial scan, which does not apply the check.
+    if (key_kind == (int)KeyKind::kText && (b0 | b1) >= 0 && p + 3 <= lim)
+      fallback = fallback || !(b0 >= 1 && (int)(int8_t)buf[p + 2] == b0 - 1);
+    else if (key_kind == (int)KeyKind::kBytes && (b0 | b1) >= 0 && p + 6 <= lim)
+      fallback = fallback || !(b0 >= 4 && buf[p + 2] == 0 && buf[p + 3] == 0 && buf[p + 4] == 0 &&
+                               (int)buf[p + 5] == b0 - 4);
+    const bool bad = sz <= 0;
+    const int np = p + sz;
+    const bool fin = !bad && (np >= end_rel || fallback);
+    if (alive) {
+      code = bad ? (sz == 0 ? -1 - p : kFnInvalid) : fallback ? kFnFallback : fin ? np : code;
+      pos = bad ? pos : np;
+      cnt += bad ? 0 : 1;
+    }
+    alive = alive && !(bad || fin);
+  };
+  int32_t* x = fx + c * kF1Entries;
+  int32_t* m = fn + c * kF1Entries;
+  // Phase 1: all kF1Entries chains (4 per lane) for a few lockstep steps. Chains from offsets that
+  // are not record starts decode garbage lengths and die within ~2-3 steps; only the true chain and
+  // the few that fall onto it survive.
+  int pos[4], cnt[4], code[4];
+  bool alive[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     pos[j] = lane + 64 * j;
     cnt[j] = 0;
-    act[j] = pos[j] < end_rel;
-    code[j] = (int32_t)pos[j];
+    code[j] = pos[j];
+    alive[j] = pos[j] < end_rel;
   }
-  while (act[0] || act[1] || act[2] || act[3]) {
+  for (int it = 0; it < kF1Warm; ++it) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (act[j]) {
-        const int64_t sz = f1_record(buf, (int)pos[j], lim, n - (c0 + pos[j]));
-        if (sz <= 0) {
-          code[j] = sz == 0 ? (int32_t)(-1 - pos[j]) : kFnInvalid;
-          act[j] = false;
-        } else {
-          pos[j] += sz;
-          ++cnt[j];
-          if (pos[j] >= end_rel) {
-            act[j] = false;
-            code[j] = pos[j] > (int64_t)INT32_MAX ? kFnFallback : (int32_t)pos[j];
-          }
-        }
-      }
-    }
+    for (int j = 0; j < 4; ++j) step(pos[j], cnt[j], code[j], alive[j]);
   }
-  int32_t* x = fx + c * kF1Entries;
-  int32_t* m = fn + c * kF1Entries;
+  // Compaction: finished chains write their result; survivors go to a per-wave LDS list, so phase 2
+  // walks them 64 per lockstep slot instead of keeping all 256 lanes-slots busy to the chunk end.
+  int* list = f1_live[wv];
+  int nlive = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    x[lane + 64 * j] = code[j];
-    m[lane + 64 * j] = cnt[j];
+    const uint64_t mask = __ballot(alive[j]);
+    if (alive[j]) {
+      const int idx = nlive + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+      list[3 * idx] = lane + 64 * j;
+      list[3 * idx + 1] = pos[j];
+      list[3 * idx + 2] = cnt[j];
+    } else {
+      x[lane + 64 * j] = code[j];
+      m[lane + 64 * j] = cnt[j];
+    }
+    nlive += __popcll(mask);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the list is visible to the whole wave
+  __builtin_amdgcn_wave_barrier();
+  // Phase 2: survivors to the end of the chunk.
+  for (int s0 = 0; s0 < nlive; s0 += 64) {
+    const int i = s0 + lane;
+    bool al = i < nlive;
+    int e = 0, ps = 0, ct = 0;
+    if (al) {
+      e = list[3 * i];
+      ps = list[3 * i + 1];
+      ct = list[3 * i + 2];
+    }
+    int cd = ps;
+    while (__any(al)) step(ps, ct, cd, al);
+    if (i < nlive) {
+      x[e] = cd;
+      m[e] = ct;
+    }
   }
 }
 
@@ -539,25 +602,60 @@ __global__ void __launch_bounds__(kScanThreads) scan_apply_kernel(const int64_t*
 }
 
 // ---- variable-length gather: one wave per 64 records, all lanes on each record
+// One lane per record (in merged order). Records are byte-aligned anywhere, so the copy uses
+// unaligned 16-byte accesses (legal for global memory on gfx950; the compiler emits the same for a
+// 16-byte memcpy): a record of L >= 16 bytes moves as ceil(L/16) chunks, the last one shifted back
+// to end at L (it overlaps its predecessor and rewrites the same bytes). Up to 8 chunks (128 bytes)
+// are loaded before the first is stored, and loads and stores are unguarded (offsets clamped):
+// guarded stores would each wait for every earlier store, since stores count in vmcnt on CDNA.
+__device__ __forceinline__ void copy_small(const uint8_t* s, uint8_t* d, int L) {
+  if (L >= 8) {
+    uint64_t a, b;
+    __builtin_memcpy(&a, s, 8);
+    __builtin_memcpy(&b, s + L - 8, 8);
+    __builtin_memcpy(d, &a, 8);
+    __builtin_memcpy(d + L - 8, &b, 8);
+  } else if (L >= 4) {
+    uint32_t a, b;
+    __builtin_memcpy(&a, s, 4);
+    __builtin_memcpy(&b, s + L - 4, 4);
+    __builtin_memcpy(d, &a, 4);
+    __builtin_memcpy(d + L - 4, &b, 4);
+  } else if (L >= 2) {
+    uint16_t a, b;
+    __builtin_memcpy(&a, s, 2);
+    __builtin_memcpy(&b, s + L - 2, 2);
+    __builtin_memcpy(d, &a, 2);
+    __builtin_memcpy(d + L - 2, &b, 2);
+  } else if (L == 1) {
+    d[0] = s[0];
+  }
+}
+
 __global__ void __launch_bounds__(256) gather_var_kernel(GenericKeyCtx ctx, const Elem* elems, int64_t n,
                                                          const int64_t* out_off, uint8_t* out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t rec0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
-  if (rec0 >= n) return;
-  const int valid = (n - rec0) < 64 ? (int)(n - rec0) : 64;
-  unsigned long long src = 0;
-  long long len = 0, dst = 0;
-  if (lane < valid) {
-    const uint64_t g = elems[rec0 + lane].lo & 0xFFFFFFFFFFFFull;
-    src = (unsigned long long)ctx.recptr[g];
-    len = ctx.reclen[g];
-    dst = out_off[rec0 + lane];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = elems[i].lo & 0xFFFFFFFFFFFFull;
+  const uint8_t* src = ctx.recptr[g];
+  const int L = ctx.reclen[g];
+  uint8_t* dst = out + out_off[i];
+  if (L < 16) {
+    copy_small(src, dst, L);
+    return;
   }
-  for (int r = 0; r < valid; ++r) {
-    const uint8_t* s = reinterpret_cast<const uint8_t*>(__shfl(src, r, 64));
-    const long long l = __shfl(len, r, 64);
-    uint8_t* d = out + __shfl(dst, r, 64);
-    for (long long i = lane; i < l; i += 64) d[i] = s[i];
+  for (int base = 0; base < L; base += 128) {
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int off = min(base + 16 * k, L - 16);
+      v[k] = *reinterpret_cast<const u32x4_u*>(src + off);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int off = min(base + 16 * k, L - 16);
+      *reinterpret_cast<u32x4_u*>(dst + off) = v[k];
+    }
   }
 }
 
@@ -616,7 +714,7 @@ int64_t f1_super_chunks() { return kF1Super; }
 void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                         const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
                         int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
-                        int64_t* rec_bytes, int* status, hipStream_t s) {
+                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind) {
   if (nruns <= 0) return;
   uint8_t* w = static_cast<uint8_t*>(workspace);
   int32_t* fx = reinterpret_cast<int32_t*>(w);
@@ -627,7 +725,7 @@ void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns,
   int64_t* sup_first = sup_entry + nsup;
   if (nchunks > 0) {
     hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWaves - 1) / kF1FnWaves)), dim3(64 * kF1FnWaves),
-                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn);
+                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn, key_kind);
     hipLaunchKernelGGL(f1_super_kernel, dim3((unsigned)((nsup + 3) / 4)), dim3(256), 0, s, nbytes, chunk_base,
                        sup_base, sup_run, nsup, fx, fn, sx, sn);
     (void)hipMemsetAsync(sup_entry, 0xFF, (size_t)nsup * 8, s);
@@ -680,9 +778,8 @@ void launch_exclusive_scan(const int64_t* in, int64_t* out, int64_t n, int64_t* 
 void launch_gather_var(GenericKeyCtx ctx, const Elem* elems, int64_t n, const int64_t* out_off, uint8_t* out,
                        hipStream_t s) {
   if (n <= 0) return;
-  const int64_t waves = (n + 63) / 64;
-  hipLaunchKernelGGL(gather_var_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, ctx, elems, n,
-                     out_off, out);
+  hipLaunchKernelGGL(gather_var_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ctx, elems, n, out_off,
+                     out);
 }
 
 void launch_buffer_cuts(const int64_t* out_off, int64_t n, int64_t chunk, int64_t nbuf, int64_t* cuts,

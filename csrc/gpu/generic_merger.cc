@@ -118,7 +118,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     HIP_CHECK(hipMemcpyAsync(d_supbase, sup_base.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
     if (nsup > 0) HIP_CHECK(hipMemcpyAsync(d_suprun, sup_run.data(), 4 * (size_t)nsup, hipMemcpyHostToDevice, s));
     launch_f1_parallel(d_bases, d_nbytes, K, d_cbase, d_crun, nchunks, d_supbase, d_suprun, nsup, d_fws, d_ckstart,
-                       d_ckcount, d_counts, d_recb, d_status, s);
+                       d_ckcount, d_counts, d_recb, d_status, s, kind);
     std::vector<int> st(K);
     HIP_CHECK(hipMemcpyAsync(st.data(), d_status, 4 * K, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));

@@ -151,7 +151,7 @@ int64_t f1_super_chunks();
 void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                         const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
                         int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
-                        int64_t* rec_bytes, int* status, hipStream_t s);
+                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind = -1);
 // F1 pass 2 (one wave per chunk): record offsets; ck_ord = exclusive scan of ck_count (global
 // record ordinal of each chunk's first record), elem_off = first ordinal of each run (nruns+1),
 // chunk_run[c] = run of chunk c. offsets[r] has counts[r]+1 entries (last = record bytes).
