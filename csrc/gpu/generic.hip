@@ -31,7 +31,8 @@ constexpr int kF1Halo = 32;
 constexpr int kF1Lanes = 64;
 constexpr int kF1Bytes = kF1Chunk / kF1Lanes;  // 64 bytes per lane
 
-__device__ __forceinline__ int lds_vint(const uint8_t* b, int p, int lim, int64_t* v) {
+template <class BP>
+__device__ __forceinline__ int lds_vint(BP b, int p, int lim, int64_t* v) {
   if (p >= lim) return 0;
   const int8_t f = (int8_t)b[p];
   if (f >= -112) {
@@ -113,6 +114,22 @@ __device__ __forceinline__ int64_t f1_record(const uint8_t* buf, int i, int lim,
   const int64_t sz = a + b + kl + vl;
   return sz > remain ? -1 : sz;
 }
+
+// The general decoder alone (multi-byte VInt headers, the EOF marker, a record at the run's tail):
+// reads only bytes below lim.
+template <class BP>
+__device__ __forceinline__ int64_t f1_record_slow(BP buf, int i, int lim, int64_t remain) {
+  int64_t kl = 0, vl = 0;
+  const int a = lds_vint(buf, i, lim, &kl);
+  const int b = a ? lds_vint(buf, i + a, lim, &vl) : 0;
+  if (a == 0 || b == 0) return -1;
+  if (kl == -1 && vl == -1) return 0;
+  if (kl < 0 || vl < 0) return -1;
+  const int64_t sz = a + b + kl + vl;
+  return sz > remain ? -1 : sz;
+}
+
+typedef __attribute__((address_space(1))) const uint8_t GlobalU8;
 
 template <bool kProf>
 __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases, const int64_t* nbytes,
@@ -204,14 +221,53 @@ constexpr int kF1Entries = 256;
 constexpr int kF1Super = 64;
 constexpr int kF1FnWaves = 4;
 constexpr int kF1Warm = 2;  // lockstep steps of all chains before the survivors are compacted
+constexpr int kF1Chase = 8;  // survivors per chunk handed to f1_chase_kernel (more: walked in f1_fn)
 constexpr int32_t kFnInvalid = INT32_MIN;      // corrupt/truncated record on this chain
 constexpr int32_t kFnFallback = INT32_MIN + 1;  // exit offset not representable
 constexpr int64_t kSupInvalid = -1, kSupFallback = -2;  // super codes; EOF at q -> -3 - q
 
+// One step of an F1 chain inside chunk-relative bytes buf[0, lim): decode the record at pos (two
+// sign-extending byte reads and a few 32-bit ops in the common case; multi-byte VInt headers go to
+// the general decoder). Key framing check (lengths < 128): a Text key starts with its own VInt
+// length (klen - 1), a BytesWritable key with a 4-byte big-endian klen - 4. A chain entered at a
+// byte that is not a record start almost never passes, so garbage chains end after one step; a
+// failing chain ends as "fallback", never "corrupt": if it were the true chain, the run is
+// re-indexed by the serial scan, which does not apply the check. kGuard: reads at or past lim
+// return 0 (global memory, where bytes past the run are not ours; the LDS stage is zero-padded).
+template <bool kGuard, class BP>
+__device__ __forceinline__ void f1_step(BP buf, int lim, int64_t nrel64, int nrel, int end_rel, int key_kind, int& pos,
+                                        int& cnt, int& code, bool& alive) {
+  auto rd = [&](int i) -> int { return kGuard && i >= lim ? 0 : (int)(int8_t)buf[i]; };
+  const int p = alive ? pos : 0;
+  const int b0 = rd(p), b1 = rd(p + 1);
+  int sz = 2 + b0 + b1;
+  bool fallback = false;
+  if (alive && ((b0 | b1) < 0 || p + 2 > lim)) {
+    const int64_t s64 = f1_record_slow(buf, p, lim, nrel64 - p);
+    fallback = s64 > (int64_t)(1 << 30);
+    sz = fallback ? 1 : (int)s64;
+  } else if (p + sz > nrel) {
+    sz = -1;
+  }
+  if (key_kind == (int)KeyKind::kText && (b0 | b1) >= 0 && p + 3 <= lim)
+    fallback = fallback || !(b0 >= 1 && rd(p + 2) == b0 - 1);
+  else if (key_kind == (int)KeyKind::kBytes && (b0 | b1) >= 0 && p + 6 <= lim)
+    fallback = fallback || !(b0 >= 4 && rd(p + 2) == 0 && rd(p + 3) == 0 && rd(p + 4) == 0 && (rd(p + 5) & 0xFF) == b0 - 4);
+  const bool bad = sz <= 0;
+  const int np = p + sz;
+  const bool fin = !bad && (np >= end_rel || fallback);
+  if (alive) {
+    code = bad ? (sz == 0 ? -1 - p : kFnInvalid) : fallback ? kFnFallback : fin ? np : code;
+    pos = bad ? pos : np;
+    cnt += bad ? 0 : 1;
+  }
+  alive = alive && !(bad || fin);
+}
+
 __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                                  const int64_t* chunk_base, const int32_t* chunk_run,
                                                                  int64_t nchunks, int32_t* fx, int32_t* fn,
-                                                                 int key_kind) {
+                                                                 int key_kind, int32_t* chase, int32_t* chase_n) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
   __shared__ int f1_live[kF1FnWaves][3 * kF1Entries];  // surviving chains: entry, position, count
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -242,39 +298,8 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
   const int lim = (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo));
   const int64_t nrel64 = n - c0;
   const int nrel = (int)min(nrel64, (int64_t)(1 << 30));  // records must end by here (fast path)
-  // One step of a chain: decode the record at pos (two sign-extending LDS byte reads and a few
-  // 32-bit ops in the common case; multi-byte VInt headers go to the general decoder).
   auto step = [&](int& pos, int& cnt, int& code, bool& alive) {
-    const int p = alive ? pos : 0;
-    const int b0 = (int8_t)buf[p], b1 = (int8_t)buf[p + 1];  // p + 1 <= kF1Chunk: inside the staged chunk
-    int sz = 2 + b0 + b1;
-    bool fallback = false;
-    if (alive && ((b0 | b1) < 0 || p + 2 > lim)) {  // multi-byte VInt, EOF marker, or the run's tail
-      const int64_t s64 = f1_record(buf, p, lim, nrel64 - p);
-      fallback = s64 > (int64_t)(1 << 30);
-      sz = fallback ? 1 : (int)s64;
-    } else if (p + sz > nrel) {
-      sz = -1;
-    }
-    // Key framing check (fast path, lengths < 128): a Text key starts with its own VInt length
-    // (klen - 1), a BytesWritable key with a 4-byte big-endian klen - 4. A chain entered at a byte
-    // that is not a record start almost never passes, so garbage chains end after one step. A
-    // failing chain ends as "fallback", never "corrupt": if it were the true chain, the run is
-    // re-indexed by the serial scan, which does not apply the check.
-    if (key_kind == (int)KeyKind::kText && (b0 | b1) >= 0 && p + 3 <= lim)
-      fallback = fallback || !(b0 >= 1 && (int)(int8_t)buf[p + 2] == b0 - 1);
-    else if (key_kind == (int)KeyKind::kBytes && (b0 | b1) >= 0 && p + 6 <= lim)
-      fallback = fallback || !(b0 >= 4 && buf[p + 2] == 0 && buf[p + 3] == 0 && buf[p + 4] == 0 &&
-                               (int)buf[p + 5] == b0 - 4);
-    const bool bad = sz <= 0;
-    const int np = p + sz;
-    const bool fin = !bad && (np >= end_rel || fallback);
-    if (alive) {
-      code = bad ? (sz == 0 ? -1 - p : kFnInvalid) : fallback ? kFnFallback : fin ? np : code;
-      pos = bad ? pos : np;
-      cnt += bad ? 0 : 1;
-    }
-    alive = alive && !(bad || fin);
+    f1_step<false>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive);
   };
   int32_t* x = fx + c * kF1Entries;
   int32_t* m = fn + c * kF1Entries;
@@ -315,7 +340,21 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the list is visible to the whole wave
   __builtin_amdgcn_wave_barrier();
-  // Phase 2: survivors to the end of the chunk.
+  // Few survivors (the usual case once the framing check has run): hand them to f1_chase_kernel,
+  // which walks them one lane each with all lanes busy, instead of keeping this wave (and its LDS
+  // stage) alive for ~chunk/record-size lockstep steps with 2-3 of 64 lanes active.
+  if (nlive <= kF1Chase) {
+    if (lane < nlive) {
+      int32_t* o = chase + (c * kF1Chase + lane) * 3;
+      o[0] = list[3 * lane];
+      o[1] = list[3 * lane + 1];
+      o[2] = list[3 * lane + 2];
+    }
+    if (lane == 0) chase_n[c] = nlive;
+    return;
+  }
+  if (lane == 0) chase_n[c] = 0;
+  // Phase 2 (many survivors): walk them here, 64 per lockstep slot.
   for (int s0 = 0; s0 < nlive; s0 += 64) {
     const int i = s0 + lane;
     bool al = i < nlive;
@@ -332,6 +371,33 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
       m[e] = ct;
     }
   }
+}
+
+// Survivors of f1_fn_kernel, one lane each, walked to the end of their chunk straight from the
+// run in global memory (the chunk's bytes are L2-resident from the stage).
+__global__ void __launch_bounds__(256) f1_chase_kernel(uint8_t* const* bases, const int64_t* nbytes,
+                                                       const int64_t* chunk_base, const int32_t* chunk_run,
+                                                       int64_t nchunks, const int32_t* chase, const int32_t* chase_n,
+                                                       int32_t* fx, int32_t* fn, int key_kind) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = t / kF1Chase;
+  const int i = (int)(t % kF1Chase);
+  if (c >= nchunks || i >= chase_n[c]) return;
+  const int r = chunk_run[c];
+  const int64_t n = nbytes[r];
+  const int64_t c0 = (c - chunk_base[r]) * kF1Chunk;
+  const GlobalU8* buf = (const GlobalU8*)(uintptr_t)(bases[r] + c0);
+  const int end_rel = (int)min((int64_t)kF1Chunk, n - c0);
+  const int lim = (int)min(n - c0, (int64_t)(kF1Chunk + kF1Halo));
+  const int64_t nrel64 = n - c0;
+  const int nrel = (int)min(nrel64, (int64_t)(1 << 30));
+  const int32_t* in = chase + (c * kF1Chase + i) * 3;
+  const int e = in[0];
+  int pos = in[1], cnt = in[2], code = pos;
+  bool alive = true;
+  while (alive) f1_step<true>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive);
+  fx[c * kF1Entries + e] = code;
+  fn[c * kF1Entries + e] = cnt;
 }
 
 __global__ void __launch_bounds__(256) f1_super_kernel(const int64_t* nbytes, const int64_t* chunk_base,
@@ -707,7 +773,8 @@ void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, con
 }
 
 size_t f1_parallel_workspace(int64_t nchunks, int64_t nsup) {
-  return (size_t)nchunks * kF1Entries * 8 + (size_t)nsup * (kF1Entries * 16 + 16) + 256;
+  return (size_t)nchunks * kF1Entries * 8 + (size_t)nsup * (kF1Entries * 16 + 16) + 256 +
+         (size_t)nchunks * (kF1Chase * 3 + 1) * 4 + 256;
 }
 int64_t f1_super_chunks() { return kF1Super; }
 
@@ -723,9 +790,14 @@ void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns,
   int64_t* sn = sx + nsup * kF1Entries;
   int64_t* sup_entry = sn + nsup * kF1Entries;
   int64_t* sup_first = sup_entry + nsup;
+  int32_t* chase = reinterpret_cast<int32_t*>(sup_first + nsup + 32);
+  int32_t* chase_n = chase + nchunks * kF1Chase * 3;
   if (nchunks > 0) {
     hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWaves - 1) / kF1FnWaves)), dim3(64 * kF1FnWaves),
-                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn, key_kind);
+                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn, key_kind, chase, chase_n);
+    const int64_t lanes = nchunks * kF1Chase;
+    hipLaunchKernelGGL(f1_chase_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, bases, nbytes,
+                       chunk_base, chunk_run, nchunks, chase, chase_n, fx, fn, key_kind);
     hipLaunchKernelGGL(f1_super_kernel, dim3((unsigned)((nsup + 3) / 4)), dim3(256), 0, s, nbytes, chunk_base,
                        sup_base, sup_run, nsup, fx, fn, sx, sn);
     (void)hipMemsetAsync(sup_entry, 0xFF, (size_t)nsup * 8, s);

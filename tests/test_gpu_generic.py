@@ -83,6 +83,21 @@ def test_gpu_merge_serial_fallback_counted(require_gpu):
     assert g == c
 
 
+def test_gpu_merge_misframed_text_keys_fall_back(require_gpu):
+    """The parallel F1 walk ends chains whose key does not start with its Text length (that is how
+    it drops chains entered at non-record bytes). Keys declared Text but not framed as Text (raw
+    bytes) must then take the serial index walk and still merge exactly like the CPU."""
+    rng = random.Random(11)
+    raw = [encode_stream(sorted([(bytes(rng.randrange(200, 256) for _ in range(rng.randint(3, 12))), b"v" * 30)
+                                 for _ in range(3000)], key=lambda kv: kv[0][1:]))
+           for _ in range(3)]
+    good = [s[0] for s in datagen.streams(datagen.secondary_sort(4, 1, 3000, seed=3))]
+    g, _ = ops.merge_runs(raw + good, datagen.TEXT, "gpu")
+    assert ops.last_stats["f1_serial_runs"] == 3
+    c, _ = ops.merge_runs(raw + good, datagen.TEXT, "cpu")
+    assert g == c
+
+
 def test_consumer_gpu_backend(require_gpu, tmp_path):
     from uda_amd.utils.mof import write_mof
     p = UdaProvider()
