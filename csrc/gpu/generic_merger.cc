@@ -1,6 +1,7 @@
 #include "generic_merger.h"
 #include "merge_plan.h"
 
+#include "uda/log.h"
 #include "uda/trace.h"
 
 #include <algorithm>
@@ -26,6 +27,81 @@ void GenericMerger::reserve(int64_t records, int runs) {
   side_.alloc((size_t)records * 24);  // keyptr(8) recptr(8) keylen(4) reclen(4)
   cap_records_ = records;
   cap_runs_ = std::max(runs, cap_runs_);
+}
+
+// One level of the single-pass K-way merge (generic_kway.hip): runs in[off[k], off[k+1]) (sorted),
+// merged into out. The regular sample of the runs is merged by a recursive level when it is large
+// (it has the same shape: K sorted runs), else by the pairwise passes. Returns false if a cell
+// exceeded its capacity (out is then incomplete). Synchronizes `s`.
+bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int64_t>& off, const int64_t* d_off,
+                               const int64_t* d_ord_off, Elem* out, const GenericKeyCtx& ctx, hipStream_t s) {
+  const int K = (int)off.size() - 1;
+  const int64_t total = off[K];
+  const int64_t cap = generic_kway_cap(), T = cap / 2;
+  const int64_t step = std::max<int64_t>(1, (cap - T) / (K + 2));  // a cell holds <= T + K * step <= cap
+  std::vector<int64_t> soff(K + 1, 0);
+  for (int k = 0; k < K; ++k) {
+    const int64_t n = off[k + 1] - off[k];
+    soff[k + 1] = soff[k] + (n > step / 2 ? (n - step / 2 + step - 1) / step : 0);
+  }
+  const int64_t ns = soff[K];
+  const int64_t C = ns == 0 ? 1 : std::max<int64_t>(1, (total + T - 1) / T);
+  if (gk_.size() < 3) gk_.resize(3);  // depth <= 2; sized up front so `b` stays valid across recursion
+  KwayBuffers& b = gk_[(size_t)depth];
+  auto ensure = [](DeviceBuffer& x, size_t bytes) {
+    if (x.size() < bytes) x.alloc(bytes + bytes / 8 + 64);
+  };
+  const size_t ns_b = sizeof(Elem) * (size_t)std::max<int64_t>(ns, 1);
+  ensure(b.tab, 8 * (size_t)(K + 1));
+  ensure(b.samp, ns_b);
+  ensure(b.sa, ns_b);
+  ensure(b.sb, ns_b);
+  ensure(b.bounds, sizeof(Elem) * (size_t)std::max<int64_t>(C, 1));
+  ensure(b.split, 8 * (size_t)K * (size_t)(C + 1));
+  ensure(b.hist, sizeof(int) * (size_t)K * (size_t)C);
+  ensure(b.flag, 64);
+  int64_t* d_soff = b.tab.as<int64_t>();
+  HIP_CHECK(hipMemcpyAsync(d_soff, soff.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
+  const Elem* m = b.samp.as<Elem>();
+  std::vector<DeviceBuffer> pass_tabs;
+  if (ns > 0) {
+    launch_gk_sample(in, d_off, d_soff, K, step, ns, b.samp.as<Elem>(), s);
+    bool done = false;
+    const char* rv = std::getenv("UDA_GKWAY_RECURSE");  // tests force recursion on small inputs
+    const int64_t recurse_at = rv && *rv ? std::max<int64_t>(1, std::atoll(rv)) : kGkRecurseSamples;
+    if (ns > recurse_at && depth < 2) {
+      done = kway_level(depth + 1, b.samp.as<Elem>(), soff, d_soff, d_ord_off, b.sa.as<Elem>(), ctx, s);
+      if (done) m = b.sa.as<Elem>();
+    }
+    if (!done) {
+      Elem* sbuf[2] = {b.sa.as<Elem>(), b.sb.as<Elem>()};
+      int w = 0;
+      for (const MergePassPlan& mp : plan_merge_passes(soff, {0, K}, kGenericMergeTile)) {
+        std::vector<int64_t> tab(mp.pairs);
+        tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
+        pass_tabs.emplace_back(tab.size() * 8);
+        HIP_CHECK(hipMemcpyAsync(pass_tabs.back().as(), tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
+        PassDesc pd;
+        pd.pairs = pass_tabs.back().as<int64_t>();
+        pd.tile_prefix = pass_tabs.back().as<int64_t>() + mp.pairs.size();
+        pd.npairs = mp.npairs;
+        pd.ntiles = mp.ntiles;
+        launch_merge_partition_generic(m, pd, splits_.as<int64_t>(), ctx, s);
+        launch_merge_pass_generic(m, sbuf[w], pd, splits_.as<int64_t>(), ctx, s);
+        m = sbuf[w];
+        w ^= 1;
+      }
+    }
+    launch_gk_pick(m, ns, C, b.bounds.as<Elem>(), s);
+  }
+  launch_gk_split_hist(ctx, in, d_off, d_ord_off, m, ns, d_soff, step, K, b.bounds.as<Elem>(), C, b.hist.as<int>(),
+                       b.split.as<int64_t>(), s);
+  HIP_CHECK(hipMemsetAsync(b.flag.as(), 0, 4, s));
+  launch_gk_cells(ctx, in, d_off, K, b.split.as<int64_t>(), C, out, b.flag.as<int>(), s);
+  int overflow = 0;
+  HIP_CHECK(hipMemcpyAsync(&overflow, b.flag.as(), 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return overflow == 0;
 }
 
 GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
@@ -192,9 +268,10 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   Elem* nxt = elems_b_.as<Elem>();
   launch_normalize_generic(ctx, d_eoff, K, total, cur, s);
   phase("f2_normalize");
-  // ---- F3: merge tree; per-pass descriptors are small host tables uploaded per pass
+  // ---- F3: single-pass K-way merge (generic_kway.hip) when K allows, else the pairwise tree;
+  // per-pass descriptors are small host tables uploaded per pass
   std::vector<DeviceBuffer> pass_tabs;
-  for (const MergePassPlan& mp : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
+  auto upload_pass = [&](const MergePassPlan& mp) {
     std::vector<int64_t> tab(mp.pairs);
     tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
     pass_tabs.emplace_back(tab.size() * 8);
@@ -204,6 +281,23 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     pd.tile_prefix = pass_tabs.back().as<int64_t>() + mp.pairs.size();
     pd.npairs = mp.npairs;
     pd.ntiles = mp.ntiles;
+    return pd;
+  };
+  const char* gk_env = std::getenv("UDA_GKWAY");  // 0: pairwise tree only (A/B and tests)
+  const bool gk_on = !(gk_env && *gk_env && std::atoi(gk_env) == 0);
+  bool merged = false;
+  if (gk_on && K >= 2 && K <= kGkMaxRuns) {
+    if (kway_level(0, cur, eoff, d_eoff, d_eoff, nxt, ctx, s)) {
+      std::swap(cur, nxt);
+      res.passes = 1;
+      merged = true;
+    } else {
+      UDA_LOG(kWarn, "generic k-way: a cell above capacity, falling back to the pairwise merge");
+    }
+  }
+  for (const MergePassPlan& mp : merged ? std::vector<MergePassPlan>{}
+                                        : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
+    const PassDesc pd = upload_pass(mp);
     launch_merge_partition_generic(cur, pd, splits_.as<int64_t>(), ctx, s);
     launch_merge_pass_generic(cur, nxt, pd, splits_.as<int64_t>(), ctx, s);
     std::swap(cur, nxt);

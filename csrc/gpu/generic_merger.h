@@ -36,6 +36,16 @@ class GenericMerger {
   int f1_serial_runs_ = 0;
   void reserve(int64_t records, int runs);
   DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_, side_, ck_, f1ws_;
+  // single-pass K-way (generic_kway.hip), per recursion level: sample offsets, per-run samples,
+  // merged samples (ping-pong), splitters, per-run cell splits, sample histogram, overflow flag
+  struct KwayBuffers {
+    DeviceBuffer tab, samp, sa, sb, bounds, split, hist, flag;
+  };
+  std::vector<KwayBuffers> gk_;
+  static constexpr int64_t kGkRecurseSamples = 1 << 18;  // larger samples are merged by a K-way level
+  // d_off: element offsets of the level's runs; d_ord_off: run boundaries in record ordinals (level 0)
+  bool kway_level(int depth, const Elem* in, const std::vector<int64_t>& off, const int64_t* d_off,
+                  const int64_t* d_ord_off, Elem* out, const GenericKeyCtx& ctx, hipStream_t s);
   int64_t cap_records_ = 0;
   int cap_runs_ = 0;
 };

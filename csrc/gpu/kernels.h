@@ -106,6 +106,22 @@ void launch_merge_partition_generic(const Elem* in, PassDesc pd, int64_t* splits
 void launch_merge_pass_generic(const Elem* in, Elem* out, PassDesc pd, const int64_t* splits,
                                GenericKeyCtx ctx, hipStream_t s);
 
+// ---------------------------------------------------------------- single-pass K-way merge, generic keys
+constexpr int kGkMaxRuns = 128;  // runs per merge on the generic single-pass path
+int generic_kway_cap();          // elements per cell
+// samples[soff[r] + j] = cur[eoff[r] + j * step + step / 2]
+void launch_gk_sample(const Elem* cur, const int64_t* eoff, const int64_t* soff, int K, int64_t step, int64_t ns,
+                      Elem* out, hipStream_t s);
+void launch_gk_pick(const Elem* merged, int64_t ns, int64_t C, Elem* bounds, hipStream_t s);
+// split[r * (C + 1) + j] = first element of run r not below splitter j - 1 (0 / run length at the
+// ends), from a histogram of the merged samples by run (hist: K * C ints of scratch).
+// eoff: element offsets of the runs at this level; ord_off: run boundaries in record ordinals.
+void launch_gk_split_hist(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff, const int64_t* ord_off,
+                          const Elem* merged, int64_t ns, const int64_t* soff, int64_t step, int K, const Elem* bounds,
+                          int64_t C, int* hist, int64_t* split, hipStream_t s);
+void launch_gk_cells(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff, int K, const int64_t* split, int64_t C,
+                     Elem* out, int* overflow, hipStream_t s);
+
 // ---------------------------------------------------------------- single-pass K-way merge (F2+F3+F4)
 constexpr int kKwCap = 2048;       // records per cell (LDS capacity of one workgroup)
 constexpr int kKwMaxRuns = 128;    // runs per group on the single-pass path

@@ -18,6 +18,7 @@
 //  * F4: one final gather moves each 104-byte record once: a wave owns 64 consecutive output
 //    records and streams them as 832 consecutive 8-byte words (13 per record), so every store
 //    instruction writes 512 contiguous bytes and every load reads whole record spans.
+#include "generic_cmp.h"
 #include "kernels.h"
 #include "uda/compare.h"
 #include "uda/vint.h"
@@ -36,37 +37,10 @@ struct FixedCmp {
   __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const { return elem_le(a, b); }
 };
 
-// GENERIC: prefix ties between two keys longer than 8 bytes are settled on the raw key bytes,
-// read through the per-record side tables 8 bytes at a time.
-__device__ __forceinline__ uint64_t load_be8(const uint8_t* p, int n) {
-  uint64_t v = 0;
-  if (n >= 8) {
-    uint64_t w;
-    __builtin_memcpy(&w, p, 8);
-    return __builtin_bswap64(w);
-  }
-  for (int i = 0; i < 8; ++i) v = (v << 8) | (uint64_t)(i < n ? p[i] : 0);
-  return v;
-}
-
+// GENERIC: the total order of generic_cmp.h.
 struct GenericCmp {
   GenericKeyCtx ctx;
-  __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const {
-    if (a.hi != b.hi) return a.hi < b.hi;
-    if ((a.lo >> 48) > 8 && (b.lo >> 48) > 8) {
-      const uint64_t ga = a.lo & 0xFFFFFFFFFFFFull, gb = b.lo & 0xFFFFFFFFFFFFull;
-      const uint8_t* pa = ctx.keyptr[ga];
-      const uint8_t* pb = ctx.keyptr[gb];
-      const int la = ctx.keylen[ga], lb = ctx.keylen[gb];
-      const int n = la < lb ? la : lb;
-      for (int i = 8; i < n; i += 8) {
-        const uint64_t x = load_be8(pa + i, n - i), y = load_be8(pb + i, n - i);
-        if (x != y) return x < y;
-      }
-      if (la != lb) return la < lb;
-    }
-    return a.lo <= b.lo;
-  }
+  __device__ __forceinline__ bool le(const Elem& a, const Elem& b) const { return generic_le(ctx, a, b); }
 };
 
 __device__ __forceinline__ Elem ld_elem(const Elem* p) {
@@ -249,20 +223,7 @@ __global__ void __launch_bounds__(kThreads) merge_pass_kernel(const Elem* in, El
 // only for keys that still tie after P+24 bytes. Order = content bytes, then length, then ordinal:
 // the same total order as GenericCmp (used by the partition kernel).
 constexpr int kGenItems = kGenericMergeTile / kThreads;  // 4
-constexpr uint64_t kOrdMask = 0xFFFFFFFFFFFFull;
-
-__device__ __forceinline__ int key_lcp(const uint8_t* a, int la, const uint8_t* b, int lb, int limit) {
-  const int n = min(min(la, lb), limit);
-  int i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t x, y;
-    __builtin_memcpy(&x, a + i, 8);
-    __builtin_memcpy(&y, b + i, 8);
-    if (x != y) return i + (__builtin_ctzll(x ^ y) >> 3);  // little-endian: first differing byte
-  }
-  while (i < n && a[i] == b[i]) ++i;
-  return i;
-}
+constexpr uint64_t kOrdMask = kGenOrdMask;
 
 __global__ void __launch_bounds__(kThreads) merge_pass_generic_lds_kernel(const Elem* in, Elem* out, PassDesc pd,
                                                                           const int64_t* splits, GenericKeyCtx ctx) {

@@ -215,3 +215,33 @@ def test_consumer_gpu_device_alloc_fault_fails_once(require_gpu, tmp_path, monke
         assert c.failure_calls == 1
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("maps", [2, 5, 64, 128])
+def test_generic_kway_matches_pairwise_tree(require_gpu, monkeypatch, maps):
+    """The single-pass K-way merge of generic keys (sampled cells, LDS-staged key bytes after the
+    cell's common prefix) orders records exactly like the pairwise merge tree (UDA_GKWAY=0) and the
+    CPU heap merge, for long common prefixes, duplicate-heavy keys and fixed-width keys."""
+    sec = [s[0] for s in datagen.streams(datagen.secondary_sort(maps, 1, 400, seed=maps))]
+    wc = [s[0] for s in datagen.streams(datagen.wordcount(maps, 1, 300, seed=maps))]
+    for runs in (sec, wc):
+        g, _ = ops.merge_runs(runs, datagen.TEXT, "gpu")
+        assert ops.last_stats["passes"] == 1
+        monkeypatch.setenv("UDA_GKWAY", "0")
+        t, _ = ops.merge_runs(runs, datagen.TEXT, "gpu")
+        assert ops.last_stats["passes"] > 1 or maps <= 2
+        monkeypatch.delenv("UDA_GKWAY")
+        c, _ = ops.merge_runs(runs, datagen.TEXT, "cpu")
+        assert g == t == c
+
+
+@pytest.mark.parametrize("recurse", ["64", "8"])
+def test_generic_kway_recursive_sample_merge(require_gpu, monkeypatch, recurse):
+    """Large samples are merged by a nested K-way level (two levels with the lower threshold); the
+    result must still equal the CPU heap merge."""
+    monkeypatch.setenv("UDA_GKWAY_RECURSE", recurse)
+    runs = [s[0] for s in datagen.streams(datagen.secondary_sort(24, 1, 1500, seed=31))]
+    g, _ = ops.merge_runs(runs, datagen.TEXT, "gpu")
+    assert ops.last_stats["passes"] == 1
+    c, _ = ops.merge_runs(runs, datagen.TEXT, "cpu")
+    assert g == c
