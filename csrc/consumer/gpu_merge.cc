@@ -83,8 +83,15 @@ struct DeviceWorkspace {
   ~DeviceWorkspace() {
     for (auto e : piece_ev)
       if (e) (void)hipEventDestroy(e);
+    if (cs) (void)hipStreamDestroy(cs);
   }
   void reset_stats() { h2d_ms = device_ms = d2h_ms = sink_ms = 0; }
+  // D2H stream of streamed deliveries (the merge stream is busy with the next round)
+  hipStream_t copy_stream() {
+    if (!cs) HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    return cs;
+  }
+  hipStream_t cs = nullptr;
   static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
     bytes = std::max<int64_t>(bytes, 16);
     if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
@@ -263,8 +270,18 @@ struct PoolLease {
   }
 };
 
+// on_round: deliver the merged output in key-range rounds while the device merges the next one
+// (GenericMerger::merge); time spent in it is not counted as device time.
 DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
-                            int64_t spacing, hipStream_t s) {
+                            int64_t spacing, hipStream_t s, const gpu::GenericMerger::RoundFn& on_round = nullptr) {
+  double round_ms = 0;
+  gpu::GenericMerger::RoundFn timed;
+  if (on_round)
+    timed = [&](const std::vector<int64_t>& cuts, int64_t records, bool last) {
+      const auto tr = std::chrono::steady_clock::now();
+      on_round(cuts, records, last);
+      round_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
+    };
   auto t0 = std::chrono::steady_clock::now();
   std::vector<const uint8_t*> ptrs;
   std::vector<int64_t> lens;
@@ -284,9 +301,10 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
     DeviceWorkspace::ensure(ws.out, total);
     auto t1 = std::chrono::steady_clock::now();
     ws.h2d_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    gpu::GenericMergeResult r = ws.merger.merge(runs, lens, (int)kind, ws.out.as<uint8_t>(), total, spacing, s);
+    gpu::GenericMergeResult r =
+        ws.merger.merge(runs, lens, (int)kind, ws.out.as<uint8_t>(), total, spacing, s, timed);
     HIP_CHECK(hipStreamSynchronize(s));
-    ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count() - round_ms;
     DeviceMergeOut res;
     res.bytes = r.bytes;
     res.cuts = std::move(r.cuts);
@@ -348,9 +366,9 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
     res.decoded_blocks = (int64_t)plan.descs.size();
   }
   host_raw.clear();
-  gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s);
+  gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s, timed);
   HIP_CHECK(hipStreamSynchronize(s));
-  ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+  ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count() - round_ms;
   res.bytes = r.bytes;
   res.cuts = std::move(r.cuts);
   res.records = r.records;
@@ -713,9 +731,9 @@ void ReduceTask::merge_gpu() {
     // ---- delivery of merged rounds; EOF rides in the very last buffer
     bool eof_sent = false;
     std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
-    auto deliver = [&](const DeviceMergeOut& m, bool last) {
+    auto deliver = [&](const DeviceMergeOut& m, bool last, hipStream_t ds) {
       const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-      stream_out(ws, m, s, [&](const uint8_t* piece, size_t c0, size_t c1) {
+      stream_out(ws, m, ds, [&](const uint8_t* piece, size_t c0, size_t c1) {
         for (size_t j = c0; j < c1; ++j) {
           if (stop_) throw UdaError("reduce task stopped during merge");
           const int64_t b = m.cuts[j], e = m.cuts[j + 1];
@@ -748,9 +766,15 @@ void ReduceTask::merge_gpu() {
         stager->flush();
         ws.h2d_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
       }
-      DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kv, s);
+      // rounds of the merged output go out on the copy stream while the next round merges
+      DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kv, s,
+                                      [&](const std::vector<int64_t>& cuts, int64_t records, bool last) {
+                                        DeviceMergeOut r;
+                                        r.cuts = cuts;
+                                        r.records = records;
+                                        deliver(r, last, ws.copy_stream());
+                                      });
       count_decoded(m.decoded_blocks);
-      deliver(m, true);
     } else {
       // ---- hybrid: last LPQ, then RPQ rounds over the spilled runs
       spill_group();
@@ -852,7 +876,7 @@ void ReduceTask::merge_gpu() {
           }
         }
         DeviceMergeOut m = device_merge(ws, views, Codec::kNone, kind_, kv, s);  // views: host spans
-        deliver(m, q + 1 == rounds);
+        deliver(m, q + 1 == rounds, s);
       }
     }
     if (!eof_sent) {  // empty final round (or empty input): EOF alone

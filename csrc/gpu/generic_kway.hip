@@ -135,9 +135,39 @@ __global__ void __launch_bounds__(256) gk_split_hist_kernel(GenericKeyCtx ctx, c
   split[t] = a;
 }
 
+// Output rounds over cell ranges: for round boundary q at cell cb[q], elem[q] = sum over runs of
+// the run's split there (merged elements before the boundary) and byte[q] = the record bytes before
+// it (the F1 record offsets at the split). One block per boundary.
+__global__ void __launch_bounds__(128) gk_round_bounds_kernel(const int64_t* split, int K, int64_t C, const int64_t* cb,
+                                                              const int64_t* const* rec_off, int64_t* elem,
+                                                              int64_t* bytes) {
+  __shared__ unsigned long long se[128], sb[128];
+  const int64_t c = cb[blockIdx.x];
+  unsigned long long e = 0, b = 0;
+  for (int k = threadIdx.x; k < K; k += 128) {
+    const int64_t x = split[(int64_t)k * (C + 1) + c];
+    e += (unsigned long long)x;
+    b += (unsigned long long)rec_off[k][x];
+  }
+  se[threadIdx.x] = e;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int off = 64; off >= 1; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      se[threadIdx.x] += se[threadIdx.x + off];
+      sb[threadIdx.x] += sb[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    elem[blockIdx.x] = (int64_t)se[0];
+    bytes[blockIdx.x] = (int64_t)sb[0];
+  }
+}
+
 __global__ void __launch_bounds__(kGkThreads) gk_cell_kernel(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff,
-                                                             int K, const int64_t* split, int64_t C, Elem* out,
-                                                             int* overflow) {
+                                                             int K, const int64_t* split, int64_t C, int64_t c_first,
+                                                             Elem* out, int* overflow) {
   __shared__ __attribute__((aligned(16))) Elem E[kGkCap];
   __shared__ uint64_t w0[kGkCap], w1[kGkCap], w2[kGkCap];
   __shared__ int32_t klen[kGkCap];
@@ -146,7 +176,7 @@ __global__ void __launch_bounds__(kGkThreads) gk_cell_kernel(GenericKeyCtx ctx, 
   __shared__ int64_t beg[kGkMaxRuns];
   __shared__ int64_t s_start;
   __shared__ int s_p, s_bad;
-  const int64_t c = blockIdx.x;
+  const int64_t c = c_first + blockIdx.x;
   const int lane = threadIdx.x & 63;
   // ---- slices of this cell (wave 0): lengths scanned into seg, global start of each slice
   if (threadIdx.x < 64) {
@@ -351,10 +381,17 @@ void launch_gk_split_hist(GenericKeyCtx ctx, const Elem* cur, const int64_t* eof
 }
 
 void launch_gk_cells(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff, int K, const int64_t* split, int64_t C,
-                     Elem* out, int* overflow, hipStream_t s) {
-  if (C <= 0) return;
-  hipLaunchKernelGGL(gk_cell_kernel, dim3((unsigned)C), dim3(kGkThreads), 0, s, ctx, cur, eoff, K, split, C, out,
-                     overflow);
+                     int64_t c_first, int64_t c_count, Elem* out, int* overflow, hipStream_t s) {
+  if (c_count <= 0) return;
+  hipLaunchKernelGGL(gk_cell_kernel, dim3((unsigned)c_count), dim3(kGkThreads), 0, s, ctx, cur, eoff, K, split, C,
+                     c_first, out, overflow);
+}
+
+void launch_gk_round_bounds(const int64_t* split, int K, int64_t C, const int64_t* cb, int nb,
+                            const int64_t* const* rec_off, int64_t* elem, int64_t* bytes, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(gk_round_bounds_kernel, dim3((unsigned)nb), dim3(128), 0, s, split, K, C, cb, rec_off, elem,
+                     bytes);
 }
 
 }  // namespace gpu

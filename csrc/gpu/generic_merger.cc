@@ -29,12 +29,17 @@ void GenericMerger::reserve(int64_t records, int runs) {
   cap_runs_ = std::max(runs, cap_runs_);
 }
 
+GenericMerger::~GenericMerger() {
+  for (hipEvent_t e : round_ev_) (void)hipEventDestroy(e);
+}
+
 // One level of the single-pass K-way merge (generic_kway.hip): runs in[off[k], off[k+1]) (sorted),
 // merged into out. The regular sample of the runs is merged by a recursive level when it is large
 // (it has the same shape: K sorted runs), else by the pairwise passes. Returns false if a cell
 // exceeded its capacity (out is then incomplete). Synchronizes `s`.
 bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int64_t>& off, const int64_t* d_off,
-                               const int64_t* d_ord_off, Elem* out, const GenericKeyCtx& ctx, hipStream_t s) {
+                               const int64_t* d_ord_off, Elem* out, const GenericKeyCtx& ctx, hipStream_t s,
+                               bool launch_cells, int64_t* cells) {
   const int K = (int)off.size() - 1;
   const int64_t total = off[K];
   const int64_t cap = generic_kway_cap(), T = cap / 2;
@@ -45,7 +50,10 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
     soff[k + 1] = soff[k] + (n > step / 2 ? (n - step / 2 + step - 1) / step : 0);
   }
   const int64_t ns = soff[K];
-  const int64_t C = ns == 0 ? 1 : std::max<int64_t>(1, (total + T - 1) / T);
+  // at least (K + 1) / 2 cells: with fewer, the sample rounding (up to K * step / 2 elements per
+  // cell) could exceed the (K + 2) * step slack of the capacity bound
+  const int64_t C = ns == 0 ? 1 : std::max<int64_t>({1, (total + T - 1) / T, (int64_t)(K + 1) / 2});
+  if (cells) *cells = C;
   if (gk_.size() < 3) gk_.resize(3);  // depth <= 2; sized up front so `b` stays valid across recursion
   KwayBuffers& b = gk_[(size_t)depth];
   auto ensure = [](DeviceBuffer& x, size_t bytes) {
@@ -96,8 +104,9 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
   }
   launch_gk_split_hist(ctx, in, d_off, d_ord_off, m, ns, d_soff, step, K, b.bounds.as<Elem>(), C, b.hist.as<int>(),
                        b.split.as<int64_t>(), s);
+  if (!launch_cells) return true;
   HIP_CHECK(hipMemsetAsync(b.flag.as(), 0, 4, s));
-  launch_gk_cells(ctx, in, d_off, K, b.split.as<int64_t>(), C, out, b.flag.as<int>(), s);
+  launch_gk_cells(ctx, in, d_off, K, b.split.as<int64_t>(), C, 0, C, out, b.flag.as<int>(), s);
   int overflow = 0;
   HIP_CHECK(hipMemcpyAsync(&overflow, b.flag.as(), 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -105,7 +114,8 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
 }
 
 GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
-                                        int kind, uint8_t* out, int64_t out_cap, int64_t kv_buf, hipStream_t s) {
+                                        int kind, uint8_t* out, int64_t out_cap, int64_t kv_buf, hipStream_t s,
+                                        const RoundFn& on_round, int64_t round_bytes) {
   trace::Range tr("uda.generic_merge");
   // UDA_GM_PROFILE=1: synchronize after each phase and print the split (diagnostic only)
   static const bool prof = std::getenv("UDA_GM_PROFILE") != nullptr;
@@ -238,7 +248,8 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   for (int k = 0; k < K; ++k) offp[k] = offsets_.as<int64_t>() + eoff[k] + k;
   HIP_CHECK(hipMemcpyAsync(d_offp, offp.data(), 8 * K, hipMemcpyHostToDevice, s));
   // ---- F1 pass 2: every chunk re-walked in parallel from its checkpoint
-  int64_t* d_eoff = out_off_.as<int64_t>();
+  if (eoff_.size() < (size_t)(K + 1) * 8) eoff_.alloc((size_t)(K + 1) * 8);
+  int64_t* d_eoff = eoff_.as<int64_t>();
   HIP_CHECK(hipMemcpyAsync(d_eoff, eoff.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
   for (int k = 0; k < K; ++k)  // empty runs have no chunk to write their terminating offset
     if (run_bytes[k] == 0) HIP_CHECK(hipMemsetAsync(offp[k], 0, 8, s));
@@ -263,7 +274,7 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
     res.cuts = {0};
     return res;
   }
-  // ---- F2: normalize (elem_off lives in the out_off scratch until the size scan reuses it)
+  // ---- F2: normalize
   Elem* cur = elems_a_.as<Elem>();
   Elem* nxt = elems_b_.as<Elem>();
   launch_normalize_generic(ctx, d_eoff, K, total, cur, s);
@@ -285,52 +296,124 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   };
   const char* gk_env = std::getenv("UDA_GKWAY");  // 0: pairwise tree only (A/B and tests)
   const bool gk_on = !(gk_env && *gk_env && std::atoi(gk_env) == 0);
-  bool merged = false;
-  if (gk_on && K >= 2 && K <= kGkMaxRuns) {
-    if (kway_level(0, cur, eoff, d_eoff, d_eoff, nxt, ctx, s)) {
-      std::swap(cur, nxt);
-      res.passes = 1;
-      merged = true;
-    } else {
-      UDA_LOG(kWarn, "generic k-way: a cell above capacity, falling back to the pairwise merge");
-    }
-  }
-  for (const MergePassPlan& mp : merged ? std::vector<MergePassPlan>{}
-                                        : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
-    const PassDesc pd = upload_pass(mp);
-    launch_merge_partition_generic(cur, pd, splits_.as<int64_t>(), ctx, s);
-    launch_merge_pass_generic(cur, nxt, pd, splits_.as<int64_t>(), ctx, s);
-    std::swap(cur, nxt);
-    ++res.passes;
-  }
-  phase("f3_merge_tree");
-  // ---- F4: sizes in merged order -> scan -> gather
-  launch_record_sizes(ctx, cur, total, sizes_.as<int64_t>(), s);
-  launch_exclusive_scan(sizes_.as<int64_t>(), out_off_.as<int64_t>(), total, scan_tmp_.as<int64_t>(), s);
-  launch_gather_var(ctx, cur, total, out_off_.as<int64_t>(), out, s);
-  // ---- delivery cuts: records whose output offset starts in [j*chunk, (j+1)*chunk) form buffer j;
-  // chunk = kv_buf - longest record keeps every buffer within kv_buf
-  int64_t max_rec = 0;
-  {
-    unsigned long long* d_max = reinterpret_cast<unsigned long long*>(scan_tmp_.as<int64_t>());  // free again
+  const bool gk = gk_on && K >= 2 && K <= kGkMaxRuns;
+  // chunk = kv_buf - longest record keeps every delivery buffer within kv_buf
+  auto chunk_bytes = [&](const Elem* order) {
+    launch_record_sizes(ctx, order, total, sizes_.as<int64_t>(), s);
+    unsigned long long* d_max = reinterpret_cast<unsigned long long*>(scan_tmp_.as<int64_t>());
     launch_max_i64(sizes_.as<int64_t>(), total, d_max, s);
     unsigned long long m = 0;
     HIP_CHECK(hipMemcpyAsync(&m, d_max, 8, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    max_rec = (int64_t)m;
+    if ((int64_t)m > kv_buf) throw std::runtime_error("record larger than the delivery buffer");
+    return std::max<int64_t>(1, kv_buf - (int64_t)m);
+  };
+  // F4 for merged elements [e0, e0 + n) whose records start at output byte b0: sizes -> scan ->
+  // gather, then the delivery cuts of that range (relative) into host `raw` (pinned; complete once
+  // the stream passes this point). Enqueued only.
+  auto f4_enqueue = [&](const Elem* order, int64_t e0, int64_t n, int64_t b0, int64_t nbytes, int64_t chunk,
+                        int64_t* d_cuts, int64_t* raw) {
+    launch_record_sizes(ctx, order + e0, n, sizes_.as<int64_t>() + e0, s);
+    launch_exclusive_scan(sizes_.as<int64_t>() + e0, out_off_.as<int64_t>() + e0, n, scan_tmp_.as<int64_t>(), s);
+    launch_gather_var(ctx, order + e0, n, out_off_.as<int64_t>() + e0, out + b0, s);
+    const int64_t nbuf = (nbytes + chunk - 1) / chunk;
+    launch_buffer_cuts(out_off_.as<int64_t>() + e0, n, chunk, nbuf, d_cuts, s);
+    HIP_CHECK(hipMemcpyAsync(raw, d_cuts, 8 * (nbuf + 1), hipMemcpyDeviceToHost, s));
+    return nbuf;
+  };
+  auto absolute_cuts = [](const int64_t* raw, int64_t nbuf, int64_t b0, int64_t nbytes, std::vector<int64_t>* cuts) {
+    cuts->clear();
+    for (int64_t i = 0; i <= nbuf; ++i)
+      if (cuts->empty() || b0 + raw[i] != cuts->back()) cuts->push_back(b0 + raw[i]);
+    if (cuts->back() != b0 + nbytes) cuts->push_back(b0 + nbytes);
+  };
+  auto reserve_cuts = [&](int64_t entries) {
+    if (cuts_.size() < (size_t)entries * 8) cuts_.alloc((size_t)entries * 8 + 4096);
+    if (cuts_host_.size() < (size_t)entries * 8) cuts_host_.alloc((size_t)entries * 8 + 4096);
+  };
+  int64_t C = 0;
+  if (gk && on_round && kway_level(0, cur, eoff, d_eoff, d_eoff, nxt, ctx, s, /*launch_cells=*/false, &C)) {
+    // ---- streamed: key-range rounds of cells; round q's output is handed over (on_round) while the
+    // device merges round q + 1, so the caller's D2H overlaps the merge
+    res.passes = 1;
+    const int64_t chunk = chunk_bytes(cur);
+    int Q = (int)std::min<int64_t>(C, std::max<int64_t>(1, (bytes + round_bytes - 1) / std::max<int64_t>(round_bytes, 1)));
+    std::vector<int64_t> cb(Q + 1);
+    for (int q = 0; q <= Q; ++q) cb[q] = C * q / Q;
+    if (rounds_.size() < (size_t)(Q + 1) * 24) rounds_.alloc((size_t)(Q + 1) * 24);
+    int64_t* d_cb = rounds_.as<int64_t>();
+    int64_t* d_re = d_cb + (Q + 1);
+    int64_t* d_rb = d_re + (Q + 1);
+    HIP_CHECK(hipMemcpyAsync(d_cb, cb.data(), 8 * (Q + 1), hipMemcpyHostToDevice, s));
+    launch_gk_round_bounds(gk_[0].split.as<int64_t>(), K, C, d_cb, Q + 1,
+                           const_cast<const int64_t* const*>(d_offp), d_re, d_rb, s);
+    std::vector<int64_t> re(Q + 1), rb(Q + 1);
+    HIP_CHECK(hipMemcpyAsync(re.data(), d_re, 8 * (Q + 1), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(rb.data(), d_rb, 8 * (Q + 1), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemsetAsync(gk_[0].flag.as(), 0, 4, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    // per-round slices of the cut buffers, and one completion event per round
+    std::vector<int64_t> coff(Q + 1, 0);
+    for (int q = 0; q < Q; ++q) coff[q + 1] = coff[q] + (rb[q + 1] - rb[q] + chunk - 1) / chunk + 1;
+    reserve_cuts(coff[Q]);
+    if ((int)round_ev_.size() < Q)
+      for (int q = (int)round_ev_.size(); q < Q; ++q) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        round_ev_.push_back(e);
+      }
+    std::vector<int64_t> nbufs(Q);
+    auto enqueue = [&](int q) {
+      launch_gk_cells(ctx, cur, d_eoff, K, gk_[0].split.as<int64_t>(), C, cb[q], cb[q + 1] - cb[q], nxt,
+                      gk_[0].flag.as<int>(), s);
+      nbufs[q] = f4_enqueue(nxt, re[q], re[q + 1] - re[q], rb[q], rb[q + 1] - rb[q], chunk,
+                            cuts_.as<int64_t>() + coff[q], cuts_host_.as<int64_t>() + coff[q]);
+      HIP_CHECK(hipEventRecord(round_ev_[(size_t)q], s));
+    };
+    res.cuts = {0};
+    std::vector<int64_t> rc;
+    enqueue(0);
+    for (int q = 0; q < Q; ++q) {
+      if (q + 1 < Q) enqueue(q + 1);  // the device runs ahead while round q is delivered
+      HIP_CHECK(hipEventSynchronize(round_ev_[(size_t)q]));
+      int overflow = 0;
+      HIP_CHECK(hipMemcpy(&overflow, gk_[0].flag.as(), 4, hipMemcpyDeviceToHost));
+      if (overflow) throw std::runtime_error("generic k-way: a cell above capacity in a streamed round");
+      absolute_cuts(cuts_host_.as<int64_t>() + coff[q], nbufs[q], rb[q], rb[q + 1] - rb[q], &rc);
+      on_round(rc, re[q + 1] - re[q], q + 1 == Q);
+      res.cuts.insert(res.cuts.end(), rc.begin() + 1, rc.end());
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    phase("f3_f4_rounds");
+  } else {
+    // ---- whole: F3 (K-way, else the pairwise tree), then F4 over everything
+    bool merged = false;
+    if (gk) {
+      if (kway_level(0, cur, eoff, d_eoff, d_eoff, nxt, ctx, s, /*launch_cells=*/true, &C)) {
+        std::swap(cur, nxt);
+        res.passes = 1;
+        merged = true;
+      } else {
+        UDA_LOG(kWarn, "generic k-way: a cell above capacity, falling back to the pairwise merge");
+      }
+    }
+    for (const MergePassPlan& mp : merged ? std::vector<MergePassPlan>{}
+                                          : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
+      const PassDesc pd = upload_pass(mp);
+      launch_merge_partition_generic(cur, pd, splits_.as<int64_t>(), ctx, s);
+      launch_merge_pass_generic(cur, nxt, pd, splits_.as<int64_t>(), ctx, s);
+      std::swap(cur, nxt);
+      ++res.passes;
+    }
+    phase("f3_merge");
+    const int64_t chunk = chunk_bytes(cur);
+    const int64_t nbuf = (bytes + chunk - 1) / chunk;
+    reserve_cuts(nbuf + 1);
+    f4_enqueue(cur, 0, total, 0, bytes, chunk, cuts_.as<int64_t>(), cuts_host_.as<int64_t>());
+    HIP_CHECK(hipStreamSynchronize(s));
+    absolute_cuts(cuts_host_.as<int64_t>(), nbuf, 0, bytes, &res.cuts);
+    if (on_round) on_round(res.cuts, total, true);
   }
-  if (max_rec > kv_buf) throw std::runtime_error("record larger than the delivery buffer");
-  const int64_t chunk = std::max<int64_t>(1, kv_buf - max_rec);
-  const int64_t nbuf = (bytes + chunk - 1) / chunk;
-  if (cuts_.size() < (size_t)(nbuf + 1) * 8) cuts_.alloc((size_t)(nbuf + 1) * 8);
-  launch_buffer_cuts(out_off_.as<int64_t>(), total, chunk, nbuf, cuts_.as<int64_t>(), s);
-  std::vector<int64_t> raw(nbuf + 1);
-  HIP_CHECK(hipMemcpyAsync(raw.data(), cuts_.as(), 8 * (nbuf + 1), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  res.cuts.clear();
-  for (int64_t b : raw)
-    if (res.cuts.empty() || b != res.cuts.back()) res.cuts.push_back(b);
-  if (res.cuts.back() != bytes) res.cuts.push_back(bytes);
   phase("f4_gather_cuts");
   if (prof) {
     std::string line = "[GM profile] runs=" + std::to_string(K) + " records=" + std::to_string(total) +

@@ -119,8 +119,12 @@ void launch_gk_pick(const Elem* merged, int64_t ns, int64_t C, Elem* bounds, hip
 void launch_gk_split_hist(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff, const int64_t* ord_off,
                           const Elem* merged, int64_t ns, const int64_t* soff, int64_t step, int K, const Elem* bounds,
                           int64_t C, int* hist, int64_t* split, hipStream_t s);
+// Cells [c_first, c_first + c_count) of C.
 void launch_gk_cells(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff, int K, const int64_t* split, int64_t C,
-                     Elem* out, int* overflow, hipStream_t s);
+                     int64_t c_first, int64_t c_count, Elem* out, int* overflow, hipStream_t s);
+// For each of nb cell boundaries cb[i]: merged elements and record bytes before it.
+void launch_gk_round_bounds(const int64_t* split, int K, int64_t C, const int64_t* cb, int nb,
+                            const int64_t* const* rec_off, int64_t* elem, int64_t* bytes, hipStream_t s);
 
 // ---------------------------------------------------------------- single-pass K-way merge (F2+F3+F4)
 constexpr int kKwCap = 2048;       // records per cell (LDS capacity of one workgroup)
