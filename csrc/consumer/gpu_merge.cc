@@ -522,8 +522,20 @@ void ReduceTask::merge_gpu() {
     } else {
       run.mem = spill_mem.alloc((size_t)std::max<int64_t>(run.bytes, 1));
     }
-    // stream the LPQ output out of HBM: sparse index from every cut, bytes to DRAM or to the file
+    // stream the LPQ output out of HBM: sparse index from every cut, bytes to DRAM or to the file.
+    // The DRAM tier is pinned, so the LPQ lands there by one DMA (no bounce through the ring).
     std::atomic<int64_t> err{0};
+    if (!disk) {
+      const auto td = std::chrono::steady_clock::now();
+      if (m.bytes > 0)
+        HIP_CHECK(hipMemcpyAsync(run.mem, ws.out.as<uint8_t>(), (size_t)m.bytes, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      ws.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
+      for (size_t j = 0; j + 1 < m.cuts.size(); ++j) {
+        run.cut.push_back(m.cuts[j]);
+        run.key.push_back(key_at(run.mem + m.cuts[j], m.cuts[j + 1] - m.cuts[j]));
+      }
+    } else
     stream_out(ws, m, s, [&](const uint8_t* p, size_t c0, size_t c1) {
       const int64_t base = m.cuts[c0], len = m.cuts[c1] - base;
       for (size_t j = c0; j < c1; ++j) {
