@@ -33,11 +33,11 @@ __global__ void __launch_bounds__(kCopyThreads) batched_copy_kernel(const CopyDe
 }
 }  // namespace
 
-void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s) {
+void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s, int max_blocks) {
   if (n <= 0 || max_bytes <= 0) return;
   // enough workgroups per descriptor to keep ~16 KiB per workgroup, capped for huge slices
   int64_t blocks = (max_bytes + (16 << 10) - 1) / (16 << 10);
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > max_blocks) blocks = max_blocks;
   hipLaunchKernelGGL(batched_copy_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(kCopyThreads), 0, s, descs);
 }
 

@@ -1,6 +1,7 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
 #include "merge_plan.h"
+#include "sdma.h"
 #include "uda/fault.h"
 #include "uda/trace.h"
 
@@ -476,8 +477,12 @@ ShuffleJob::ShuffleJob(const ShuffleConfig& cfg) : cfg_(cfg) {
   HIP_CHECK(hipSetDevice(cfg_.device));
   int lo_prio = 0, hi_prio = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-  HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, hi_prio));
-  HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+  // HBM store: the comm stream carries RCCL and gets the high priority. Spill tiers: it carries the
+  // round's H2D staging (a copy kernel reading host memory), which must not hold back the merge of
+  // the previous round: the merge stream gets the high priority instead.
+  const bool spill = cfg_.store != "hbm";
+  HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, spill ? lo_prio : hi_prio));
+  HIP_CHECK(hipStreamCreateWithPriority(&s_compute_, hipStreamNonBlocking, spill ? hi_prio : lo_prio));
   HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   buf_records_ = std::max<int64_t>(1, cfg_.kv_buf_bytes / kTeraRecordBytes);
   const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
@@ -913,6 +918,45 @@ void ShuffleJob::compute_plans() {
   }
   if (max_v > 65535) throw std::runtime_error("exchange verification: too many slices per round");
   if (max_v > 0) d_verify_got_.alloc((size_t)max_v * 8);
+  // pinned-DRAM tier: each round's H2D (own cells into the receive slot, and for W > 1 the outgoing
+  // slices into the send staging) is one batched-copy launch over fixed descriptors. The kernel reads
+  // the pinned store over PCIe; hipMemcpyAsync would queue these copies on the same SDMA engine as
+  // the D2H delivery and serialize the two directions of the link.
+  h2d_descs_.clear();
+  if (const char* e = std::getenv("UDA_H2D_BLOCKS")) h2d_blocks_ = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("UDA_H2D_SDMA")) sdma_h2d_ = std::atoi(e) != 0;
+  h2d_n_.assign(Q_, 0);
+  h2d_max_.assign(Q_, 0);
+  if (host_store()) {
+    const int me = cfg_.rank;
+    h2d_descs_.resize(Q_);
+    for (int q = 0; q < Q_; ++q) {
+      const RoundPlan& rp = plans_[q];
+      uint8_t* rbuf = recv_slots_[q % kSlots].as<uint8_t>();
+      std::vector<CopyDesc> v;
+      for (int i = 0; i < R_; ++i)
+        for (int j = 0; j < M; ++j) {
+          const size_t x = ((size_t)me * R_ + i) * M + j;
+          const int64_t cnt = rp.recv_cnt[x];
+          if (cnt <= 0) continue;
+          const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+          v.push_back(CopyDesc{store_dev_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
+        }
+      if (W > 1 && send_staging_.size() > 0) {
+        int64_t off = 0;
+        for (int p2 = 0; p2 < W; ++p2)
+          for (const Span& sp : rp.send[p2]) {
+            v.push_back(CopyDesc{store_dev_base_ + (sp.ptr - store_base_), send_staging_.as<uint8_t>() + off, sp.bytes});
+            off += sp.bytes;
+          }
+      }
+      for (const CopyDesc& d : v) h2d_max_[q] = std::max(h2d_max_[q], d.bytes);
+      h2d_n_[q] = (int)v.size();
+      if (v.empty()) continue;
+      h2d_descs_[q].alloc(v.size() * sizeof(CopyDesc));
+      HIP_CHECK(hipMemcpy(h2d_descs_[q].as(), v.data(), v.size() * sizeof(CopyDesc), hipMemcpyHostToDevice));
+    }
+  }
 }
 
 void ShuffleJob::plan() {
@@ -1141,12 +1185,88 @@ StepStats ShuffleJob::run_step(bool validate) {
     if (stop_) throw std::runtime_error("delivery pipeline failed: " + step_error_msg_);
   };
 
+  // Pinned-DRAM tier, one rank: a staging thread copies each round's own cells into its receive
+  // slot on an SDMA engine of its own, as soon as the slot's previous merge has finished. A copy
+  // kernel (or hipMemcpyAsync, which runs as one) reading host memory stalls the merge kernels
+  // running beside it in the CU memory pipeline; on the copy engines, staging overlaps delivery
+  // (the link's two directions) and the merge. The round loop waits for staged_round[q] instead of
+  // a stream dependency.
+  const bool sdma_stage = host_store() && W == 1 && sdma_h2d_;
+  std::vector<char> staged_round(Q_, 0), merge_recorded(Q_, 0);
+  double stage_ms = 0;
+  std::thread stage_thr;
+  if (sdma_stage)
+    stage_thr = std::thread([&] {
+      try {
+        HIP_CHECK(hipSetDevice(cfg_.device));
+        SdmaEngine& eng = SdmaEngine::for_device(cfg_.device);
+        hsa_signal_t sig = eng.make_signal();
+        for (int q = 0; q < Q_; ++q) {
+          const int slot = q % kSlots;
+          if (q >= kSlots) {
+            {
+              std::unique_lock<std::mutex> lk(mu_);
+              cv_.wait(lk, [&] { return merge_recorded[q - kSlots] != 0 || stop_; });
+              if (stop_) break;
+            }
+            HIP_CHECK(hipEventSynchronize(merged_ev_[slot]));  // the slot's previous round is merged
+          }
+          const double ts = now_ms();
+          const RoundPlan& rp = plans_[q];
+          uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
+          std::vector<CopyDesc> pieces;
+          for (int i = 0; i < R_; ++i)
+            for (int j = 0; j < M; ++j) {
+              const size_t x = ((size_t)me * R_ + i) * M + j;
+              const int64_t cnt = rp.recv_cnt[x];
+              if (cnt <= 0) continue;
+              const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+              pieces.push_back(CopyDesc{store_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
+            }
+          SdmaEngine::arm(sig, (int64_t)pieces.size());
+          for (const CopyDesc& d : pieces) eng.copy_h2d(d.dst, d.src, (size_t)d.bytes, sig);
+          SdmaEngine::wait(sig);
+          std::lock_guard<std::mutex> g(mu_);
+          staged_round[q] = 1;
+          stage_ms += now_ms() - ts;
+          cv_.notify_all();
+        }
+        eng.destroy_signal(sig);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!stop_) step_error_msg_ = std::string("H2D staging: ") + e.what();
+        stop_ = true;
+        cv_.notify_all();
+      }
+    });
+  struct JoinGuard {
+    std::thread& t;
+    std::mutex& mu;
+    std::condition_variable& cv;
+    bool& stop;
+    ~JoinGuard() {
+      if (!t.joinable()) return;
+      if (std::uncaught_exceptions() > 0) {  // the round loop failed: release the stager
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+        cv.notify_all();
+      }
+      t.join();
+    }
+  } stage_guard{stage_thr, mu_, cv_, stop_};
+
   for (int q = 0; q < Q_; ++q) {
     trace::Range tr_round("uda.round");
     const int slot = q % kSlots;
     const RoundPlan& rp = plans_[q];
     uint8_t* rbuf = staged() ? recv_slots_[slot].as<uint8_t>() : nullptr;
-    if (staged()) {
+    if (sdma_stage) {
+      for (int i = 0; i < R_; ++i)
+        for (int j = 0; j < M; ++j) st.bytes_h2d += rp.recv_cnt[((size_t)me * R_ + i) * M + j] * kTeraRecordBytes;
+      HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
+      HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
+      wait_until([&] { return staged_round[q] != 0; });
+    } else if (staged()) {
       if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged_ev_[slot], 0));  // slot consumed
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
       if (spilled()) {  // spill tiers: this round's own cells stream into the slot (SDMA H2D)
@@ -1159,12 +1279,11 @@ StepStats ShuffleJob::run_step(bool validate) {
             const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
             if (disk_store())
               pieces.push_back(DiskStore::Piece{j, at - mof_off_[j], cnt * kTeraRecordBytes, rbuf + rp.recv_off[x]});
-            else
-              HIP_CHECK(hipMemcpyAsync(rbuf + rp.recv_off[x], store_base_ + at, (size_t)(cnt * kTeraRecordBytes),
-                                       hipMemcpyHostToDevice, s_comm_));
             st.bytes_h2d += cnt * kTeraRecordBytes;
           }
         if (!pieces.empty()) disk_->stage(pieces, s_comm_);  // io_uring reads overlap the merge of q-1
+        if (host_store())  // own cells (and, for W > 1, the outgoing slices) in one launch
+          launch_batched_copy(h2d_descs_[q].as<CopyDesc>(), h2d_n_[q], h2d_max_[q], s_comm_, h2d_blocks_);
       }
       if (W > 1) {
         std::vector<std::vector<Span>> recv(W);
@@ -1187,10 +1306,7 @@ StepStats ShuffleJob::run_step(bool validate) {
                 const int64_t at = (int64_t)(uintptr_t)sp.ptr;
                 const int m = (int)(std::upper_bound(mof_off_.begin(), mof_off_.end(), at) - mof_off_.begin()) - 1;
                 pieces.push_back(DiskStore::Piece{m, at - mof_off_[m], sp.bytes, send_staging_.as<uint8_t>() + off});
-              } else {
-                HIP_CHECK(hipMemcpyAsync(send_staging_.as<uint8_t>() + off, sp.ptr, (size_t)sp.bytes,
-                                         hipMemcpyHostToDevice, s_comm_));
-              }
+              }  // pinned DRAM: copied by the round's batched-copy launch above
               off += sp.bytes;
             }
             if (off > beg) send[p].push_back(Span{send_staging_.as<uint8_t>() + beg, off - beg});
@@ -1260,6 +1376,11 @@ StepStats ShuffleJob::run_step(bool validate) {
     }
     HIP_CHECK(hipEventRecord(ev[4 * q + 3], s_compute_));
     HIP_CHECK(hipEventRecord(merged_ev_[slot], s_compute_));
+    if (sdma_stage) {
+      std::lock_guard<std::mutex> g(mu_);
+      merge_recorded[q] = 1;
+      cv_.notify_all();
+    }
     st.records += n;
     if (deliver) {
       {
@@ -1274,11 +1395,25 @@ StepStats ShuffleJob::run_step(bool validate) {
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   HIP_CHECK(hipStreamSynchronize(s_comm_));
   HIP_CHECK(hipStreamSynchronize(s_copy_));
+  if (stage_thr.joinable()) stage_thr.join();
   st.wall_ms = now_ms() - t0;
+  if (sdma_stage) st.comm_ms = stage_ms;
   for (int q = 0; q < Q_; ++q) {
     float a = 0, b = 0;
-    if (staged() && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
+    if (staged() && !sdma_stage && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
     if (hipEventElapsedTime(&b, ev[4 * q + 2], ev[4 * q + 3]) == hipSuccess) st.merge_ms += b;
+  }
+  static const bool round_trace = std::getenv("UDA_ROUND_TRACE") != nullptr;  // tools: per-round timeline
+  if (round_trace && staged()) {
+    std::string line = "[round trace ms: comm start-end | merge start-end]";
+    for (int q = 0; q < Q_; ++q) {
+      float t[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], ev[0], ev[4 * q + k]);
+      char b[96];
+      snprintf(b, sizeof(b), " q%d %.0f-%.0f|%.0f-%.0f", q, t[0], t[1], t[2], t[3]);
+      line += b;
+    }
+    fprintf(stderr, "%s\n", line.c_str());
   }
   for (auto e : ev) (void)hipEventDestroy(e);
   st.d2h_ms = step_d2h_ms_;

@@ -337,6 +337,12 @@ class ShuffleJob {
   std::vector<int> verify_n_;
   std::vector<int64_t> verify_max_nrec_;
   DeviceBuffer d_verify_got_;
+  // pinned-DRAM tier: per-round batched H2D copy descriptors (device), their count and largest size
+  std::vector<DeviceBuffer> h2d_descs_;
+  std::vector<int> h2d_n_;
+  std::vector<int64_t> h2d_max_;
+  int h2d_blocks_ = 2048;  // workgroups per descriptor (UDA_H2D_BLOCKS)
+  bool sdma_h2d_ = true;   // pinned-DRAM tier, W == 1: stage on an SDMA engine (UDA_H2D_SDMA)
   int64_t buf_records_ = 0;
   int64_t piece_bytes_ = 0;
 

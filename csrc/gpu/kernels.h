@@ -209,7 +209,7 @@ struct CopyDesc {
   int64_t bytes;
 };
 // descs: device array of n descriptors; max_bytes: largest descriptor (sizes the grid).
-void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s);
+void launch_batched_copy(const CopyDesc* descs, int n, int64_t max_bytes, hipStream_t s, int max_blocks = 2048);
 
 // ---------------------------------------------------------------- block decode (F6)
 // One Hadoop compressed block: chunks [u32 BE clen][clen bytes]... in [src, src_end) of the

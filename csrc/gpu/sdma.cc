@@ -239,6 +239,11 @@ SdmaEngine::SdmaEngine(int device) {
   }
   for (int b = 0; b < 16; ++b)
     if (use & (1u << b)) engine_ids_.push_back(1u << b);
+  uint32_t hmask = 0;
+  if (hsa_amd_memory_copy_engine_status(gpu_, cpu_, &hmask) != HSA_STATUS_SUCCESS) hmask = 0;
+  const uint32_t other = hmask & ~use;  // staging on a different engine than delivery
+  const uint32_t pick = other ? other : hmask;
+  h2d_engine_ = pick & (~pick + 1u);
   UDA_LOG(kInfo, "SDMA delivery: device %d numa %d engines mask 0x%x preferred 0x%x", device, numa_node_, mask, pref);
 }
 
@@ -340,6 +345,15 @@ int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_
   // parts() may overestimate when the aligned split leaves a part empty: release the surplus
   for (int k = issued; k < n; ++k) hsa_signal_subtract_screlease(sig, 1);
   return n;
+}
+
+void SdmaEngine::copy_h2d(void* dst_dev, const void* src_host, size_t bytes, hsa_signal_t sig) {
+  hsa_status_t st = HSA_STATUS_ERROR;
+  if (h2d_engine_)
+    st = hsa_amd_memory_async_copy_on_engine(dst_dev, gpu_, src_host, cpu_, bytes, 0, nullptr, sig,
+                                             (hsa_amd_sdma_engine_id_t)h2d_engine_, false);
+  if (st != HSA_STATUS_SUCCESS) st = hsa_amd_memory_async_copy(dst_dev, gpu_, src_host, cpu_, bytes, 0, nullptr, sig);
+  hsa_check(st, "memory_async_copy (H2D)");
 }
 
 std::string SdmaEngine::describe() const {

@@ -52,6 +52,9 @@ class SdmaEngine {
   int copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways);
   // Parts copy_d2h(bytes, ways) will issue.
   int parts(size_t bytes, int ways) const;
+  // Host -> device copy (one part) on an SDMA engine other than the delivery engine when the device
+  // has one, so staging from pinned DRAM and D2H delivery use the two directions of the link at once.
+  void copy_h2d(void* dst_dev, const void* src_host, size_t bytes, hsa_signal_t sig);
   static void arm(hsa_signal_t s, int64_t parts);
   // Block until the signal reaches 0; throws on a copy error (negative value).
   static void wait(hsa_signal_t s);
@@ -64,6 +67,7 @@ class SdmaEngine {
   hsa_agent_t gpu_{}, cpu_{};
   hsa_amd_memory_pool_t host_pool_{};
   std::vector<uint32_t> engine_ids_;  // SDMA engine bits usable for CPU <- GPU copies
+  uint32_t h2d_engine_ = 0;           // SDMA engine bit for GPU <- CPU staging (0: runtime's choice)
   int numa_node_ = -1;
   std::atomic<int> next_engine_{0};
   bool hsa_inited_ = false;
