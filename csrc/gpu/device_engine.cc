@@ -504,6 +504,7 @@ ShuffleJob::~ShuffleJob() {
     if (t.joinable()) t.join();
   (void)hipDeviceSynchronize();
   for (auto e : merged_ev_) (void)hipEventDestroy(e);
+  if (s_stage_) (void)hipStreamDestroy(s_stage_);
   for (auto e : comm_ev_) (void)hipEventDestroy(e);
   for (auto e : piece_ev_) (void)hipEventDestroy(e);
   if (!sdma_ && ring_) (void)hipHostFree(ring_);
@@ -1191,7 +1192,10 @@ StepStats ShuffleJob::run_step(bool validate) {
   // running beside it in the CU memory pipeline; on the copy engines, staging overlaps delivery
   // (the link's two directions) and the merge. The round loop waits for staged_round[q] instead of
   // a stream dependency.
-  const bool sdma_stage = host_store() && W == 1 && sdma_h2d_;
+  // The disk tier stages from the same thread (io_uring reads into the pinned chunk ring, then H2D on
+  // a stream of its own), so the round loop is never blocked in disk reads.
+  const bool sdma_stage = W == 1 && ((host_store() && sdma_h2d_) || disk_store());
+  if (sdma_stage && disk_store() && !s_stage_) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_, hipStreamNonBlocking));
   std::vector<char> staged_round(Q_, 0), merge_recorded(Q_, 0);
   double stage_ms = 0;
   std::thread stage_thr;
@@ -1199,8 +1203,9 @@ StepStats ShuffleJob::run_step(bool validate) {
     stage_thr = std::thread([&] {
       try {
         HIP_CHECK(hipSetDevice(cfg_.device));
-        SdmaEngine& eng = SdmaEngine::for_device(cfg_.device);
-        hsa_signal_t sig = eng.make_signal();
+        SdmaEngine* eng = host_store() ? &SdmaEngine::for_device(cfg_.device) : nullptr;
+        hsa_signal_t sig{};
+        if (eng) sig = eng->make_signal();
         for (int q = 0; q < Q_; ++q) {
           const int slot = q % kSlots;
           if (q >= kSlots) {
@@ -1215,23 +1220,32 @@ StepStats ShuffleJob::run_step(bool validate) {
           const RoundPlan& rp = plans_[q];
           uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
           std::vector<CopyDesc> pieces;
+          std::vector<DiskStore::Piece> dpieces;
           for (int i = 0; i < R_; ++i)
             for (int j = 0; j < M; ++j) {
               const size_t x = ((size_t)me * R_ + i) * M + j;
               const int64_t cnt = rp.recv_cnt[x];
               if (cnt <= 0) continue;
               const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
-              pieces.push_back(CopyDesc{store_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
+              if (eng)
+                pieces.push_back(CopyDesc{store_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
+              else
+                dpieces.push_back(DiskStore::Piece{j, at - mof_off_[j], cnt * kTeraRecordBytes, rbuf + rp.recv_off[x]});
             }
-          SdmaEngine::arm(sig, (int64_t)pieces.size());
-          for (const CopyDesc& d : pieces) eng.copy_h2d(d.dst, d.src, (size_t)d.bytes, sig);
-          SdmaEngine::wait(sig);
+          if (eng) {
+            SdmaEngine::arm(sig, (int64_t)pieces.size());
+            for (const CopyDesc& d : pieces) eng->copy_h2d(d.dst, d.src, (size_t)d.bytes, sig);
+            SdmaEngine::wait(sig);
+          } else {
+            if (!dpieces.empty()) disk_->stage(dpieces, s_stage_);
+            HIP_CHECK(hipStreamSynchronize(s_stage_));
+          }
           std::lock_guard<std::mutex> g(mu_);
           staged_round[q] = 1;
           stage_ms += now_ms() - ts;
           cv_.notify_all();
         }
-        eng.destroy_signal(sig);
+        if (eng) eng->destroy_signal(sig);
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu_);
         if (!stop_) step_error_msg_ = std::string("H2D staging: ") + e.what();

@@ -343,6 +343,7 @@ class ShuffleJob {
   std::vector<int64_t> h2d_max_;
   int h2d_blocks_ = 2048;  // workgroups per descriptor (UDA_H2D_BLOCKS)
   bool sdma_h2d_ = true;   // pinned-DRAM tier, W == 1: stage on an SDMA engine (UDA_H2D_SDMA)
+  hipStream_t s_stage_ = nullptr;  // disk tier, W == 1: H2D of the staging thread
   int64_t buf_records_ = 0;
   int64_t piece_bytes_ = 0;
 
