@@ -1111,29 +1111,32 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   }
   DeviceWorkspace::ensure(ws.out, total);
   const int64_t kv = kv_buf_size_ - kEofBytes;
-  gpu::GenericMergeResult r = ws.merger.merge(rptr, rlen, (int)kind_, ws.out.as<uint8_t>(), total, kv, s);
-  HIP_CHECK(hipStreamSynchronize(s));
-  DeviceMergeOut m;
-  m.bytes = r.bytes;
-  m.cuts = std::move(r.cuts);
-  m.records = r.records;
   std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
   bool eof_sent = false;
-  const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-  stream_out(ws, m, s, [&](const uint8_t* piece, size_t c0, size_t c1) {
-    for (size_t j = c0; j < c1; ++j) {
-      const uint8_t* p = piece + (m.cuts[j] - m.cuts[c0]);
-      int64_t len = m.cuts[j + 1] - m.cuts[j];
-      if (j + 1 == nb) {
-        std::memcpy(tail.data(), p, (size_t)len);
-        tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
-        p = tail.data();
-        len += kEofBytes;
-        eof_sent = true;
+  // merged key-range rounds go out on the copy stream while the next round merges
+  auto deliver_round = [&](const std::vector<int64_t>& cuts, int64_t, bool last) {
+    DeviceMergeOut m;
+    m.cuts = cuts;
+    const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
+    stream_out(ws, m, ws.copy_stream(), [&](const uint8_t* piece, size_t c0, size_t c1) {
+      for (size_t j = c0; j < c1; ++j) {
+        const uint8_t* p = piece + (m.cuts[j] - m.cuts[c0]);
+        int64_t len = m.cuts[j + 1] - m.cuts[j];
+        if (last && j + 1 == nb) {
+          std::memcpy(tail.data(), p, (size_t)len);
+          tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
+          p = tail.data();
+          len += kEofBytes;
+          eof_sent = true;
+        }
+        if (sink(p, len) != 0) throw UdaError("dataFromUda callback failed");
       }
-      if (sink(p, len) != 0) throw UdaError("dataFromUda callback failed");
-    }
-  });
+    });
+  };
+  gpu::GenericMergeResult r =
+      ws.merger.merge(rptr, rlen, (int)kind_, ws.out.as<uint8_t>(), total, kv, s, deliver_round);
+  DeviceMergeOut m;
+  m.records = r.records;
   if (!eof_sent) {
     tail[0] = tail[1] = 0xFF;
     if (sink(tail.data(), kEofBytes) != 0) throw UdaError("dataFromUda callback failed");
