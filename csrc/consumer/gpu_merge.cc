@@ -500,15 +500,14 @@ void ReduceTask::merge_gpu() {
     st_.device_decoded_blocks += n;
   };
   // LPQ: merge the current group on the device and spill it with its sparse index
-  auto spill_group = [&] {
-    if (group.empty()) return;
+  // LPQ: merge one group on the device and spill it with its sparse index. Runs on the LPQ thread,
+  // one group at a time, while the fetch fills the next group (the reference's fetcher running ahead
+  // of the LPQ merges, MergeManager.cc:202-288).
+  auto merge_spill = [&](std::vector<Span> jg, std::vector<std::string> ids) {
     if (stager) stager->flush();
-    DeviceMergeOut m = device_merge(ws, group, stage_codec, kind_, kSampleSpacing, s);
+    DeviceMergeOut m = device_merge(ws, jg, stage_codec, kind_, kSampleSpacing, s);
     count_decoded(m.decoded_blocks);
     if (stager) stager->reset();  // the merge read the staged copies; recycle their HBM
-    group.clear();
-    group_mem.release_all();  // staged in HBM: the pinned blocks go back to the pool
-    group_raw = 0;
     SpillRun run;
     run.bytes = m.bytes;
     const bool disk = tier == "disk";
@@ -565,8 +564,6 @@ void ReduceTask::merge_gpu() {
     std::vector<std::string> idx_key = ckpt ? run.key : std::vector<std::string>();
     const int64_t run_bytes = run.bytes;
     spills.push_back(std::move(run));
-    std::vector<std::string> ids;
-    ids.swap(group_ids);
     if (ckpt && disk) {
       // durable before listed: data, then the sparse index, then the manifest line
       if (::fsync(run_fd) != 0) throw UdaError("spill fsync failed");
@@ -596,6 +593,50 @@ void ReduceTask::merge_gpu() {
       checkpointed = spills.size();
       if (fault_hit("LPQ_DONE")) throw UdaError("injected failure after an LPQ spill");
     }
+  };
+  // The group being fetched lives in fill_mem; the one being merged in job_mem. While an LPQ merge
+  // runs, new partitions are not staged early (its HBM is in use); the next group then goes H2D at
+  // its own merge.
+  gpu::PinnedArena group_mem2;
+  gpu::PinnedArena* fill_mem = &group_mem;
+  gpu::PinnedArena* job_mem = &group_mem2;
+  std::thread lpq_thr;
+  std::exception_ptr lpq_err;
+  std::atomic<bool> lpq_running{false};
+  auto lpq_wait = [&] {
+    if (lpq_thr.joinable()) lpq_thr.join();
+    if (lpq_err) {
+      std::exception_ptr e = lpq_err;
+      lpq_err = nullptr;
+      std::rethrow_exception(e);
+    }
+  };
+  struct LpqJoin {
+    std::thread& t;
+    ~LpqJoin() {
+      if (t.joinable()) t.join();
+    }
+  } lpq_join{lpq_thr};
+  auto spill_group = [&] {
+    if (group.empty()) return;
+    lpq_wait();               // one LPQ merge at a time (device workspace, stream s)
+    job_mem->release_all();   // the previous LPQ's inputs are merged
+    std::swap(fill_mem, job_mem);
+    std::vector<Span> jg;
+    jg.swap(group);
+    std::vector<std::string> ids;
+    ids.swap(group_ids);
+    group_raw = 0;
+    lpq_running = true;
+    lpq_thr = std::thread([&, device, jg = std::move(jg), ids = std::move(ids)]() mutable {
+      try {
+        if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
+        merge_spill(std::move(jg), std::move(ids));
+      } catch (...) {
+        lpq_err = std::current_exception();
+      }
+      lpq_running = false;
+    });
   };
   // resume: restored LPQ spills (data + sparse index) of a failed attempt
   if (ckpt && restored_files_.empty()) ::unlink(manifest.c_str());
@@ -689,7 +730,7 @@ void ReduceTask::merge_gpu() {
         std::vector<std::exception_ptr> errs(sub.size());
         for (size_t k = 0; k < sub.size(); ++k)
           if (fetch_codec == Codec::kNone)
-            dst[k] = group_mem.alloc((size_t)std::max<int64_t>(ready[sub[k]]->part_len(), 1));
+            dst[k] = fill_mem->alloc((size_t)std::max<int64_t>(ready[sub[k]]->part_len(), 1));
         std::vector<std::thread> ts;
         for (size_t k = 0; k < sub.size(); ++k)
           ts.emplace_back([&, k] {
@@ -701,7 +742,7 @@ void ReduceTask::merge_gpu() {
                 int64_t off = f.take_first(dst[k], cap);
                 if (off < cap) off = fetch_direct(f.params(), dst[k], off, cap, depth);
                 got[k] = Span{dst[k], off};
-                if (stager) got[k].dev = stager->submit(dst[k], off);
+                if (stager && !lpq_running) got[k].dev = stager->submit(dst[k], off);
               } else {  // host decode: decoded length unknown up front
                 std::vector<uint8_t> buf((size_t)buffer_size_);
                 for (int64_t n; (n = f.pull(buf.data(), (int64_t)buf.size())) > 0;)
@@ -716,7 +757,7 @@ void ReduceTask::merge_gpu() {
           if (e) std::rethrow_exception(e);
         for (size_t k = 0; k < sub.size(); ++k) {
           if (!dst[k]) {
-            uint8_t* p = group_mem.alloc(std::max<size_t>(host_decoded[k].size(), 1));
+            uint8_t* p = fill_mem->alloc(std::max<size_t>(host_decoded[k].size(), 1));
             std::memcpy(p, host_decoded[k].data(), host_decoded[k].size());
             got[k] = Span{p, (int64_t)host_decoded[k].size()};
           }
@@ -771,6 +812,7 @@ void ReduceTask::merge_gpu() {
     };
     const int64_t kv = kv_buf_size_ - kEofBytes;
 
+    lpq_wait();  // an LPQ of the fetch phase may still be merging
     if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
       if (stager) {
@@ -790,6 +832,7 @@ void ReduceTask::merge_gpu() {
     } else {
       // ---- hybrid: last LPQ, then RPQ rounds over the spilled runs
       spill_group();
+      lpq_wait();
       const int R = (int)spills.size();
       struct Sample {
         int run;
@@ -910,6 +953,7 @@ void ReduceTask::merge_gpu() {
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
   } catch (...) {
+    if (lpq_thr.joinable()) lpq_thr.join();  // the LPQ thread uses this frame's state
     cleanup(false);
     throw;
   }
