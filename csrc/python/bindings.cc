@@ -691,7 +691,19 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("error", &gpu::J2CSink::error)
       .def("order_errors", &gpu::J2CSink::order_errors)
       .def("set_check_order", &gpu::J2CSink::set_check_order)
-      .def("reset", &gpu::J2CSink::reset);
+      .def("reset", &gpu::J2CSink::reset)
+      // one dataFromUda buffer for reducer r (returns the sink's status code, 0 = ok); reps > 1
+      // consumes the same buffer again (micro-benchmarks; EOF buffers only once)
+      .def("consume", [](gpu::J2CSink& s, int r, py::buffer b, int reps) {
+        py::buffer_info bi = b.request();
+        const auto* p = static_cast<const uint8_t*>(bi.ptr);
+        const int64_t n = (int64_t)(bi.size * bi.itemsize);
+        if (r < 0 || r >= s.reducers()) throw py::index_error("reducer out of range");
+        py::gil_scoped_release rel;
+        int rc = 0;
+        for (int i = 0; i < std::max(1, reps) && rc == 0; ++i) rc = s.consume(r, p, n);
+        return rc;
+      }, py::arg("reducer"), py::arg("data"), py::arg("reps") = 1);
 
   py::class_<gpu::ApiTeraSortBench>(m, "ApiTeraSortBench")
       .def(py::init([](const py::dict& d) {
