@@ -43,7 +43,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rows-per-gpu", type=int, default=1_250_000_000)
     ap.add_argument("--maps-per-gpu", type=int, default=32)
-    ap.add_argument("--reducers", type=int, default=8, help="reduce tasks per GPU (each with its own consumer)")
+    ap.add_argument("--reducers", type=int, default=16,
+                    help="reduce tasks per GPU (each with its own consumer thread; 16 leaves the host side "
+                         "headroom when 8 GPUs stream into one node's DRAM)")
     ap.add_argument("--rounds", type=int, default=16, help="key cells per reducer = shuffle rounds per step")
     ap.add_argument("--d2h", choices=("sdma", "hip"), default="sdma",
                     help="delivery copies: explicit SDMA engines (default) or hipMemcpyAsync")
