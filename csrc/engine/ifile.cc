@@ -122,13 +122,24 @@ bool StreamSegment::next() {
 }
 
 // ---------------------------------------------------------------------------- MergeQueue
+// Keys compare on their cached 16-byte normalized prefix first (two integer compares); only ties
+// between longer keys read the key bytes (reference comparator semantics: CompareFunc.cc:70-91).
 bool MergeQueue::less(const Segment* a, const Segment* b) {
   ++compares_;
-  const RecordView& x = a->cur();
-  const RecordView& y = b->cur();
-  int c = key_compare(kind_, x.key, x.klen, y.key, y.klen);
+  bool full = false;
+  int c = keynorm_compare(a->norm, b->norm, &full);
+  if (full) {
+    const RecordView& x = a->cur();
+    const RecordView& y = b->cur();
+    c = key_compare(kind_, x.key, x.klen, y.key, y.klen);
+  }
   if (c != 0) return c < 0;
   return a->index < b->index;
+}
+
+void MergeQueue::normalize(Segment* s) {
+  const RecordView& r = s->cur();
+  s->norm = key_normalize(kind_, r.key, r.klen);
 }
 
 void MergeQueue::up(size_t i) {
@@ -154,6 +165,7 @@ void MergeQueue::down(size_t i) {
 
 void MergeQueue::insert(std::unique_ptr<Segment> s) {
   if (!s->next()) return;  // empty segment
+  normalize(s.get());
   heap_.push_back(std::move(s));
   up(heap_.size() - 1);
 }
@@ -161,6 +173,7 @@ void MergeQueue::insert(std::unique_ptr<Segment> s) {
 bool MergeQueue::next() {
   if (pending_advance_ && !heap_.empty()) {
     if (heap_[0]->next()) {
+      normalize(heap_[0].get());
       down(0);
     } else {
       std::swap(heap_[0], heap_.back());

@@ -55,9 +55,19 @@ UDA_HD int key_compare(KeyKind kind, const uint8_t* a, int la, const uint8_t* b,
 
 // Big-endian load of up to 8 bytes, zero padded on the right.
 UDA_HD uint64_t load_be_prefix(const uint8_t* p, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
   uint64_t v = 0;
   for (int i = 0; i < 8; ++i) v = (v << 8) | (uint64_t)(i < n ? p[i] : 0);
   return v;
+#else
+  // host: one unaligned load (or a short copy into a zeroed word) and a byte swap
+  uint64_t w = 0;
+  if (n >= 8)
+    __builtin_memcpy(&w, p, 8);
+  else if (n > 0)
+    __builtin_memcpy(&w, p, (size_t)n);
+  return __builtin_bswap64(w);
+#endif
 }
 
 // Normalized key: the first 16 content bytes (big-endian, zero padded) and the content length.

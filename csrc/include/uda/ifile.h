@@ -49,6 +49,7 @@ class Segment {
   const RecordView& cur() const { return cur_; }
   int index = 0;          // stable tie-break (fetch order / map order)
   int64_t records = 0;    // records produced so far
+  KeyNorm norm{};         // normalized current key (first 16 content bytes), kept by MergeQueue
  protected:
   RecordView cur_;
 };
@@ -106,6 +107,7 @@ class MergeQueue {
 
  private:
   bool less(const Segment* a, const Segment* b);
+  void normalize(Segment* s);  // refresh the cached normalized key of the segment's current record
   void up(size_t i);
   void down(size_t i);
   KeyKind kind_;
