@@ -52,6 +52,9 @@ def parse_args(argv=None):
     ap.add_argument("--d2h-piece-mb", type=int, default=128)
     ap.add_argument("--pinned-slots", type=int, default=16)
     ap.add_argument("--d2h-engines", type=int, default=1)
+    ap.add_argument("--no-replan", dest="replan", action="store_false",
+                    help="reuse the setup-time cell splits instead of recomputing them (and re-exchanging "
+                         "the slice counts) inside every timed step")
     ap.add_argument("--store", choices=("hbm", "host", "disk"), default="hbm",
                     help="map-output store: HBM (default), pinned host DRAM, or MOF files on --local-dirs")
     ap.add_argument("--local-dirs", default="/tmp", help="--store disk: comma-separated directories")
@@ -139,7 +142,8 @@ def main(argv=None) -> int:
                          rounds=rounds, reducers=args.reducers, d2h=args.d2h, store=args.store,
                          local_dirs=args.local_dirs,
                          d2h_piece_bytes=args.d2h_piece_mb << 20, pinned_slots=args.pinned_slots,
-                         d2h_engines=args.d2h_engines, deliver_host=not args.device_only)
+                         d2h_engines=args.d2h_engines, deliver_host=not args.device_only,
+                         replan=args.replan)
     job = TeraSortShuffle(ctx, cfg)
     t_setup = time.perf_counter()
     job.setup()
@@ -224,7 +228,9 @@ def main(argv=None) -> int:
             "teragen_gbps": round(gbps * 100 / RECORD_BYTES, 3),
             "rccl_ranks": comm_ranks,
             "bytes_sent_per_rank": sent,
-            "breakdown_ms_rank0": {k: round(mean(k), 2) for k in ("comm_ms", "merge_ms", "d2h_ms", "wait_out_ms")},
+            "breakdown_ms_rank0": {k: round(mean(k), 2) for k in ("plan_ms", "comm_ms", "merge_ms", "d2h_ms",
+                                                                  "wait_out_ms")},
+            "replan_in_step": bool(args.replan),
             "merge_passes": stats[0]["merge_passes"],
             "buffers_per_step": stats[0]["buffers"],
             "validated": validated,

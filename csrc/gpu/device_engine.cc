@@ -1147,6 +1147,38 @@ void ShuffleJob::consume_loop(int i) {
   }
 }
 
+void ShuffleJob::refresh_plan() {
+  const int M = cfg_.maps_per_rank, W = cfg_.world;
+  const int nruns = M * W;
+  const int64_t per = C_ + 1;
+  for_run_batches([&](int r0, int nr, uint8_t* const* bases, const int64_t* nrec, const int* bset) {
+    launch_split_fixed(bases, nrec, C_ > 1 ? d_bounds_.as<Elem>() : nullptr, bset, nr, C_ - 1,
+                       d_split_out_.as<int64_t>() + (size_t)r0 * per, s_compute_);
+  });
+  std::vector<int64_t> pos((size_t)nruns * per);
+  HIP_CHECK(hipMemcpyAsync(pos.data(), d_split_out_.as(), pos.size() * 8, hipMemcpyDeviceToHost, s_compute_));
+  HIP_CHECK(hipStreamSynchronize(s_compute_));
+  if (pos != split_pos_) throw std::runtime_error("replan: the map outputs changed since plan()");
+  if (W == 1) return;
+  const size_t n_per_peer = (size_t)Q_ * R_ * M;
+  std::vector<int64_t> send((size_t)W * n_per_peer), recv((size_t)W * n_per_peer);
+  for (int p = 0; p < W; ++p)
+    for (int q = 0; q < Q_; ++q)
+      for (int i = 0; i < R_; ++i)
+        for (int m = 0; m < M; ++m) {
+          const int r = m * W + p, c = i * Q_ + q;
+          send[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = pos[(size_t)r * per + c + 1] - pos[(size_t)r * per + c];
+        }
+  exchange_->alltoall_i64(send.data(), recv.data(), n_per_peer, s_comm_);
+  for (int q = 0; q < Q_; ++q)
+    for (int s = 0; s < W; ++s)
+      for (int i = 0; i < R_; ++i)
+        for (int j = 0; j < M; ++j)
+          if (recv[(size_t)s * n_per_peer + ((size_t)q * R_ + i) * M + j] !=
+              plans_[q].recv_cnt[((size_t)s * R_ + i) * M + j])
+            throw std::runtime_error("replan: a peer's counts changed since plan()");
+}
+
 StepStats ShuffleJob::run_step(bool validate) {
   trace::Range tr_step("uda.step");
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -1173,6 +1205,11 @@ StepStats ShuffleJob::run_step(bool validate) {
   std::vector<bool> has_prev(R_, false);
   if (validate) HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 64, s_compute_));
   const bool rccl_staging = send_staging_.size() > 0;
+  if (cfg_.replan) {
+    const double tp = now_ms();
+    refresh_plan();
+    st.plan_ms = now_ms() - tp;
+  }
 
   auto wait_until = [&](const std::function<bool()>& ready) {
     std::unique_lock<std::mutex> lk(mu_);

@@ -214,6 +214,7 @@ struct ShuffleConfig {
   std::string local_group;               // world > 1 without RCCL: ranks are threads of one process
   std::string store = "hbm";             // map-output store: "hbm", "host" (pinned DRAM) or "disk"
   std::string local_dirs;                // store=disk: comma-separated directories for the MOF files
+  bool replan = false;                   // every step recomputes the cell splits and exchanges the counts
 };
 
 struct StepStats {
@@ -222,6 +223,7 @@ struct StepStats {
   double merge_ms = 0;         // sum of per-round merge time (device events on the compute stream)
   double d2h_ms = 0;           // host time the delivery copies were outstanding (summed per piece)
   double wait_out_ms = 0;      // host time the merge waited for a free output slot (D2H-bound)
+  double plan_ms = 0;          // replan: cell splits + counts exchange inside the step
   int64_t bytes_in = 0;        // partition bytes delivered to this GPU's reducers (records only)
   int64_t records = 0;
   int64_t bytes_sent = 0;      // bytes this rank sent to peers (excl. self)
@@ -260,6 +262,9 @@ class ShuffleJob {
   // One shuffle+merge+deliver pass over the whole dataset. Collective when world > 1.
   // validate: run the device-side order / checksum / exchange checks in this step.
   StepStats run_step(bool validate);
+  // The step's metadata again (cfg.replan): split every map output at the cell bounds and exchange
+  // the per-slice counts, checked against the plan (the map outputs must not change between steps).
+  void refresh_plan();
 
   // Per-destination-GPU checksum of locally generated records (sum of record_hash).
   std::vector<uint64_t> local_dest_checksums() const { return dest_checksum_; }

@@ -39,6 +39,7 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   py::dict d;
   d["wall_ms"] = s.wall_ms;
   d["comm_ms"] = s.comm_ms;
+  d["plan_ms"] = s.plan_ms;
   d["merge_ms"] = s.merge_ms;
   d["d2h_ms"] = s.d2h_ms;
   d["wait_out_ms"] = s.wait_out_ms;
@@ -79,6 +80,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("local_group", c.local_group);
   get("store", c.store);
   get("local_dirs", c.local_dirs);
+  get("replan", c.replan);
   return c;
 }
 

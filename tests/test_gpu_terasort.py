@@ -211,3 +211,18 @@ def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
     assert [r.records for r in readers2] == [r.records for r in readers]
     if "UDA_KWAY" in env:
         assert st2["merge_passes"] == 3  # ceil(log2(6)) pairwise passes
+
+
+@pytest.mark.parametrize("world,store", [(1, "hbm"), (1, "host"), (2, "hbm")])
+def test_replan_every_step(require_gpu, world, store):
+    """replan=True: each step recomputes the cell splits from the map outputs (and, for world>1,
+    re-exchanges the slice counts) inside the timed step; unchanged outputs must reproduce the plan."""
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    cfg = TeraSortConfig(rows_per_gpu=40000, maps_per_rank=3, rounds=3, reducers=2, validate=True, sample_every=64,
+                         store=store, replan=True, **SMALL)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"replan{world}{store}")
+    for _ in range(2):
+        stats = run_collective(jobs, lambda j: j.run_step(True))
+        for d, st in enumerate(stats):
+            check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+            assert st["plan_ms"] > 0

@@ -49,6 +49,7 @@ class TeraSortConfig:
     sample_every: int = 4096
     store: str = "hbm"                  # "hbm", "host" (pinned DRAM) or "disk" (MOF files, jobs > HBM + DRAM)
     local_dirs: str = "/tmp"            # store="disk": comma-separated directories for the MOF files
+    replan: bool = False                # every step recomputes the cell splits and exchanges the counts
 
 
 class TeraSortShuffle:
@@ -65,7 +66,7 @@ class TeraSortShuffle:
             rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
             d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
             d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host,
-            validate=cfg.validate, store=cfg.store, local_dirs=cfg.local_dirs))
+            validate=cfg.validate, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan))
         self.sink = n.J2CSink(cfg.reducers, cfg.kv_buf_bytes)
         self.expected_checksum = None
         self.expected_records = None
@@ -160,7 +161,7 @@ def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: st
         records_per_map=records_per_map, rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed,
         kv_buf_bytes=cfg.kv_buf_bytes, d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
         d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host, validate=cfg.validate,
-        local_group=group, store=cfg.store, local_dirs=cfg.local_dirs))
+        local_group=group, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan))
         for r in range(world)]
     for j in jobs:
         j.init_local()
