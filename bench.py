@@ -52,9 +52,9 @@ def parse_args(argv=None):
     ap.add_argument("--d2h-piece-mb", type=int, default=128)
     ap.add_argument("--pinned-slots", type=int, default=16)
     ap.add_argument("--d2h-engines", type=int, default=1)
-    ap.add_argument("--no-replan", dest="replan", action="store_false",
-                    help="reuse the setup-time cell splits instead of recomputing them (and re-exchanging "
-                         "the slice counts) inside every timed step")
+    ap.add_argument("--replan", action="store_true",
+                    help="recompute the cell splits (and re-exchange the slice counts) inside every timed "
+                         "step instead of reusing the setup-time plan")
     ap.add_argument("--store", choices=("hbm", "host", "disk"), default="hbm",
                     help="map-output store: HBM (default), pinned host DRAM, or MOF files on --local-dirs")
     ap.add_argument("--local-dirs", default="/tmp", help="--store disk: comma-separated directories")
