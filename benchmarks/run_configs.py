@@ -216,6 +216,7 @@ def netmerger(args) -> dict:
            "gb": round(total / 1e9, 3), "maps": args.maps}
     variants = [("cpu", {}), ("gpu_cold", {"mapred.uda.merge.backend": "gpu"}),
                 ("gpu", {"mapred.uda.merge.backend": "gpu"}),
+                ("gpu_stage_8m", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.early.h2d.step": 8 << 20}),
                 ("gpu_hybrid", {"mapred.uda.merge.backend": "gpu",
                                 "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
                                 "mapred.uda.gpu.spill": "host"})]
@@ -236,6 +237,42 @@ def netmerger(args) -> dict:
         if name == "gpu_hybrid":
             out["hybrid_lpqs"] = st["lpqs"]
             out["hybrid_rpq_rounds"] = st["rpq_rounds"]
+    prov.close()
+    if args.reducers > 1:
+        out.update(_netmerger_concurrent(args, rows))
+    return out
+
+
+def _netmerger_concurrent(args, rows: int) -> dict:
+    """The node view of the same path: `reducers` reduce tasks of one job run at once on one GPU (a
+    TaskTracker's reduce slots), each its own NetMerger over its partition of every MOF. One task's
+    input H2D overlaps another's output D2H, so the node uses both PCIe directions."""
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    n, R = native(), args.reducers
+    runs = n.generate_runs("secondary", args.maps, R, rows, 11)
+    prov = UdaProvider()
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        prov.add_mof_memory("job_nmc", f"attempt_nmc_m_{m:06d}_0", data, index)
+    del runs
+    out = {}
+    for attempt in ("cold", "warm"):
+        cons = [UdaConsumer(args.maps, "job_nmc", f"attempt_nmc_r_{r:06d}_{attempt}", TEXT,
+                            conf={"mapred.uda.merge.backend": "gpu"}, keep_records=False) for r in range(R)]
+        t0 = time.perf_counter()
+        for m in range(args.maps):
+            for r, c in enumerate(cons):
+                c.fetch("localhost", "job_nmc", f"attempt_nmc_m_{m:06d}_0", r)
+        for c in cons:
+            c.wait(3600)
+        wall = time.perf_counter() - t0
+        stats = [c.close() for c in cons]
+        total = sum(st["bytes_delivered"] - 2 for st in stats)
+        out[f"gpu_{R}tasks_{attempt}_gbps"] = round(total / wall / 1e9, 3)
+    out[f"gpu_{R}tasks_gb"] = round(total / 1e9, 3)
     prov.close()
     return out
 

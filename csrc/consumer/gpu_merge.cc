@@ -28,6 +28,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -38,6 +40,7 @@
 #include "../gpu/device_reduce.h"
 #include "../gpu/device_engine.h"
 #include "../gpu/generic_merger.h"
+#include "../gpu/sdma.h"
 #include "reduce_task.h"
 #include "uda/aio.h"
 #include "uda/fault.h"
@@ -121,8 +124,22 @@ struct Span {
 // group's merge has finished.
 class EarlyStager {
  public:
+  // SDMA (default, UDA_EARLY_H2D_SDMA=0 for hipMemcpyAsync): the copies run on a copy engine. A
+  // hipMemcpyAsync H2D from pinned memory runs as a blit kernel whose host reads slowed the
+  // concurrent fetch memcpys into the same arena about 8x when partitions were staged piecewise.
   explicit EarlyStager(int device) : device_(device) {
     HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+    const char* e = std::getenv("UDA_EARLY_H2D_SDMA");
+    if (!e || std::atoi(e) != 0) {
+      try {
+        sdma_ = &gpu::SdmaEngine::for_device(device);
+        sig_ = sdma_->make_signal();
+        gpu::SdmaEngine::arm(sig_, 0);
+      } catch (const std::exception& ex) {
+        UDA_LOG(kWarn, "early staging: no SDMA engine (%s); using hipMemcpyAsync", ex.what());
+        sdma_ = nullptr;
+      }
+    }
     thr_ = std::thread([this] { loop(); });
   }
   ~EarlyStager() {
@@ -134,14 +151,31 @@ class EarlyStager {
     thr_.join();
     (void)hipStreamSynchronize(s_);
     (void)hipStreamDestroy(s_);
+    if (sdma_) {
+      try {
+        gpu::SdmaEngine::wait(sig_);
+      } catch (...) {
+      }
+      sdma_->destroy_signal(sig_);
+    }
   }
+  const char* engine() const { return sdma_ ? "sdma" : "hip"; }
   // Device address the partition will be copied to; the copy is issued asynchronously.
   const uint8_t* submit(const uint8_t* host, int64_t len) {
-    std::lock_guard<std::mutex> g(mu_);
-    uint8_t* d = alloc(len);
-    q_.push_back(Job{host, d, len});
-    cv_.notify_all();
+    uint8_t* d = reserve(len);
+    copy(host, d, len);
     return d;
+  }
+  // A partition's device span, filled piecewise by copy() as its bytes land in pinned memory.
+  uint8_t* reserve(int64_t len) {
+    std::lock_guard<std::mutex> g(mu_);
+    return alloc(len);
+  }
+  void copy(const uint8_t* host, uint8_t* dev, int64_t len) {
+    if (len <= 0) return;
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(Job{host, dev, len});
+    cv_.notify_all();
   }
   // Every submitted copy has completed.
   void flush() {
@@ -149,6 +183,14 @@ class EarlyStager {
     cv_.wait(lk, [&] { return q_.empty() && busy_ == 0; });
     lk.unlock();
     HIP_CHECK(hipStreamSynchronize(s_));
+    if (sdma_) {
+      try {
+        gpu::SdmaEngine::wait(sig_);
+      } catch (const std::exception& ex) {
+        gpu::SdmaEngine::arm(sig_, 0);
+        throw UdaError(std::string("early H2D staging failed: ") + ex.what());
+      }
+    }
     if (!error_.empty()) throw UdaError("early H2D staging failed: " + error_);
   }
   void reset() {
@@ -157,9 +199,11 @@ class EarlyStager {
     for (auto& b : blocks_) b.used = 0;
     cur_ = 0;
     issue_ms_ = 0;
+    copies_ = 0;
     bytes_ = 0;
   }
   double issue_ms() const { return issue_ms_; }
+  int64_t copies() const { return copies_; }
   int64_t bytes() const { return bytes_; }
 
  private:
@@ -199,17 +243,32 @@ class EarlyStager {
         ++busy_;
       }
       const auto t0 = std::chrono::steady_clock::now();
-      const hipError_t e = hipMemcpyAsync(j.dev, j.host, (size_t)j.len, hipMemcpyHostToDevice, s_);
+      std::string err;
+      if (sdma_) {
+        gpu::SdmaEngine::add(sig_, 1);
+        try {
+          sdma_->copy_h2d(j.dev, j.host, (size_t)j.len, sig_);
+        } catch (const std::exception& ex) {
+          gpu::SdmaEngine::add(sig_, -1);
+          err = ex.what();
+        }
+      } else {
+        const hipError_t e = hipMemcpyAsync(j.dev, j.host, (size_t)j.len, hipMemcpyHostToDevice, s_);
+        if (e != hipSuccess) err = hipGetErrorString(e);
+      }
       issue_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       std::lock_guard<std::mutex> g(mu_);
-      if (e != hipSuccess && error_.empty()) error_ = hipGetErrorString(e);
+      if (!err.empty() && error_.empty()) error_ = err;
       bytes_ += j.len;
+      ++copies_;
       --busy_;
       cv_.notify_all();
     }
   }
   int device_;
   hipStream_t s_ = nullptr;
+  gpu::SdmaEngine* sdma_ = nullptr;
+  hsa_signal_t sig_{};  // outstanding SDMA copies
   std::thread thr_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -220,6 +279,7 @@ class EarlyStager {
   std::vector<Block> blocks_;
   size_t cur_ = 0;
   double issue_ms_ = 0;
+  int64_t copies_ = 0;
   int64_t bytes_ = 0;
 };
 
@@ -467,6 +527,12 @@ void ReduceTask::merge_gpu() {
     stager->reset();
   }
   const int depth = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.fetch.depth", 4));
+  // early staging granularity: <= 0 (default) copies each partition once it is complete; > 0 copies
+  // every `step` bytes of its landed prefix. Measured on the 2 GB secondary sort, copies that overlap
+  // the fetch slowed the fetch from 22 ms to 100-200 ms with either copy path (SDMA or blit), while a
+  // standalone probe (tools/host_dma_contention.py) shows CPU copies into pinned memory unaffected by
+  // a concurrent H2D, so the cause is not understood and piecewise staging stays opt-in.
+  const int64_t stage_step = host_->conf_i64("mapred.uda.gpu.early.h2d.step", 0);
 
   std::vector<SpillRun> spills;
   std::vector<Span> group;          // fetched partitions of the current group (pinned, group_mem)
@@ -738,11 +804,20 @@ void ReduceTask::merge_gpu() {
               MofFetcher& f = *ready[sub[k]];
               if (dst[k]) {
                 // first chunk from the fetcher, the rest straight into the pinned span
+                // With early staging the partition is copied to HBM once complete, or (stage_step > 0)
+                // every stage_step bytes of its landed prefix while the rest is still in flight.
                 const int64_t cap = f.part_len();
+                uint8_t* dev = stager && !lpq_running ? stager->reserve(cap) : nullptr;
                 int64_t off = f.take_first(dst[k], cap);
-                if (off < cap) off = fetch_direct(f.params(), dst[k], off, cap, depth);
-                got[k] = Span{dst[k], off};
-                if (stager && !lpq_running) got[k].dev = stager->submit(dst[k], off);
+                if (dev && stage_step > 0) stager->copy(dst[k], dev, off);
+                if (off < cap) {
+                  std::function<void(int64_t, int64_t)> on_prefix;
+                  if (dev && stage_step > 0)
+                    on_prefix = [&, k, dev](int64_t a, int64_t b) { stager->copy(dst[k] + a, dev + a, b - a); };
+                  off = fetch_direct(f.params(), dst[k], off, cap, depth, on_prefix, stage_step);
+                }
+                if (dev && stage_step <= 0) stager->copy(dst[k], dev, off);
+                got[k] = Span{dst[k], off, dev};
               } else {  // host decode: decoded length unknown up front
                 std::vector<uint8_t> buf((size_t)buffer_size_);
                 for (int64_t n; (n = f.pull(buf.data(), (int64_t)buf.size())) > 0;)
@@ -780,6 +855,10 @@ void ReduceTask::merge_gpu() {
       ready.clear();
     }
     const double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stager && std::getenv("UDA_STAGE_TRACE"))
+      std::fprintf(stderr, "[stage] fetch %.1f ms, early H2D (%s) %lld copies of %.1f MB issued in %.1f ms, step %lld\n",
+                   fetch_ms, stager->engine(), (long long)stager->copies(), stager->bytes() / 1e6, stager->issue_ms(),
+                   (long long)stage_step);
 
     // ---- delivery of merged rounds; EOF rides in the very last buffer
     bool eof_sent = false;

@@ -167,12 +167,26 @@ int64_t MofFetcher::take_first(uint8_t* dst, int64_t cap) {
   return n;
 }
 
-int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth) {
+int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth,
+                                 const std::function<void(int64_t, int64_t)>& on_prefix, int64_t prefix_step) {
   std::mutex m;
   std::condition_variable c;
   int inflight = 0;
   std::string err;
   int64_t next = off;
+  // landed-prefix tracking (requests complete out of order): [off, prefix) has landed, `done` holds
+  // the later completed requests, [reported, prefix) has not been handed to on_prefix yet
+  std::map<int64_t, int64_t> done;
+  int64_t prefix = off, reported = off;
+  auto landed = [&](int64_t at, int64_t len) {  // m held
+    if (!on_prefix) return;
+    done[at] = len;
+    for (auto it = done.begin(); it != done.end() && it->first == prefix; it = done.erase(it)) prefix += it->second;
+    if (prefix - reported >= std::max<int64_t>(prefix_step, 1) || prefix == end) {
+      on_prefix(reported, prefix);
+      reported = prefix;
+    }
+  };
   auto issue = [&](int64_t at) {
     FetchRequest req;
     req.job_id = f.job_id;
@@ -182,10 +196,11 @@ int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off
     req.buf_len = std::min(buffer_size_, end - at);
     const int64_t want = req.buf_len;
     fetch_begin();
-    transport_->fetch(f.host, req, dst + at, [&, want](const FetchAck& a) {
+    transport_->fetch(f.host, req, dst + at, [&, want, at](const FetchAck& a) {
       std::lock_guard<std::mutex> g(m);
       if (a.status != 0 && err.empty()) err = a.error.empty() ? "fetch failed" : a.error;
       if (a.status == 0 && a.sent != want && err.empty()) err = "short fetch";
+      if (err.empty()) landed(at, want);
       --inflight;
       c.notify_all();
       fetch_end();

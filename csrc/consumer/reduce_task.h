@@ -75,7 +75,11 @@ class ReduceTask {
   ClientTransport* transport() { return transport_.get(); }
   // Fetch [off, end) of a partition straight into dst + off (the RDMA-WRITE-into-the-reducer-buffer
   // analogue), `depth` requests of buffer_size_ in flight. Returns end.
-  int64_t fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth);
+  // Fetch [off, end) of a partition straight into dst with `depth` requests in flight. on_prefix(a, b):
+  // bytes [a, b) have landed (called in order, each call after at least `prefix_step` new bytes, and
+  // once more at the end, from a transport thread).
+  int64_t fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off, int64_t end, int depth,
+                       const std::function<void(int64_t, int64_t)>& on_prefix = nullptr, int64_t prefix_step = 0);
   // in-flight fetch requests (exit() waits for their completions)
   void fetch_begin();
   void fetch_end();

@@ -305,6 +305,7 @@ void SdmaEngine::destroy_signal(hsa_signal_t s) {
 }
 
 void SdmaEngine::arm(hsa_signal_t s, int64_t parts) { hsa_signal_store_screlease(s, parts); }
+void SdmaEngine::add(hsa_signal_t s, int64_t parts) { hsa_signal_add_screlease(s, parts); }
 
 void SdmaEngine::wait(hsa_signal_t s) {
   const hsa_signal_value_t v =

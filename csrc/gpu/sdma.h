@@ -56,6 +56,8 @@ class SdmaEngine {
   // has one, so staging from pinned DRAM and D2H delivery use the two directions of the link at once.
   void copy_h2d(void* dst_dev, const void* src_host, size_t bytes, hsa_signal_t sig);
   static void arm(hsa_signal_t s, int64_t parts);
+  // Count `parts` more outstanding copies on a signal that may already have some in flight.
+  static void add(hsa_signal_t s, int64_t parts);
   // Block until the signal reaches 0; throws on a copy error (negative value).
   static void wait(hsa_signal_t s);
 
