@@ -1,5 +1,8 @@
 // Python bindings (pybind11) for the native runtime: the "fake JVM" host used by tests and the
 // bench drives the same C ABI / engine objects a JNI host would.
+#include <map>
+#include <memory>
+#include <mutex>
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -593,7 +596,14 @@ PYBIND11_MODULE(_uda_native, m) {
         ptrs.push_back(in.as<uint8_t>() + off);
         off += bytes[i];
       }
-      gpu::GenericMerger gm;
+      // one merger (and its HBM workspace) per device for the process, like the NetMerger's pooled
+      // DeviceWorkspace: a reducer process merges many times, so only the first call allocates
+      static std::mutex gm_mu;
+      static auto* gm_cache = new std::map<int, std::unique_ptr<gpu::GenericMerger>>();  // outlives HIP at exit
+      std::unique_lock<std::mutex> gm_lock(gm_mu);
+      auto& gm_slot = (*gm_cache)[device];
+      if (!gm_slot) gm_slot.reset(new gpu::GenericMerger());
+      gpu::GenericMerger& gm = *gm_slot;
       HIP_CHECK(hipStreamSynchronize(s));
       auto t0 = std::chrono::steady_clock::now();
       auto res = gm.merge(ptrs, bytes, (int)kind, dout.as<uint8_t>(), total, kv_buf, s);
