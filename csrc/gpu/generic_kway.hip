@@ -110,10 +110,13 @@ __global__ void __launch_bounds__(256) gk_hist_scan_kernel(int* hist, int64_t C)
 __global__ void __launch_bounds__(256) gk_split_hist_kernel(GenericKeyCtx ctx, const Elem* cur, const int64_t* eoff,
                                                             const int64_t* soff, int64_t step, int K, const Elem* bounds,
                                                             int64_t C, const int* hist, int64_t* split) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)K * (C + 1)) return;
-  const int r = (int)(t / (C + 1));
-  const int64_t j = t % (C + 1);
+  // lanes of a wave take consecutive runs for the same splitter: the splitter's key bytes, read on
+  // every prefix tie, are then one broadcast load instead of 64 scattered ones
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= (int64_t)K * (C + 1)) return;
+  const int r = (int)(u % K);
+  const int64_t j = u / K;
+  const int64_t t = (int64_t)r * (C + 1) + j;
   const int64_t n = eoff[r + 1] - eoff[r];
   if (j == 0 || j == C) {
     split[t] = j == 0 ? 0 : n;
