@@ -787,6 +787,42 @@ __global__ void __launch_bounds__(256) max_kernel(const int64_t* v, int64_t n, u
 
 }  // namespace
 
+// Max of n int32 (record lengths), four per 16-byte load, four loads in flight per lane; one atomic
+// per block (same-address atomics serialize in L2: one per wave cost ~80 us for 16M lengths).
+__global__ void __launch_bounds__(256) max_i32_kernel(const int32_t* v, int64_t n, unsigned int* out) {
+  __shared__ unsigned int wmax[4];
+  unsigned int m = 0;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32x4_u* v4 = reinterpret_cast<const u32x4_u*>(v);  // v need not be 16-byte aligned
+  int64_t i = t;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const u32x4 a = v4[i], b = v4[i + stride], c = v4[i + 2 * stride], d = v4[i + 3 * stride];
+    const u32x4 x = __builtin_elementwise_max(__builtin_elementwise_max(a, b), __builtin_elementwise_max(c, d));
+    m = max(m, max(max(x[0], x[1]), max(x[2], x[3])));
+  }
+  for (; i < n4; i += stride) {
+    const u32x4 x = v4[i];
+    m = max(m, max(max(x[0], x[1]), max(x[2], x[3])));
+  }
+  for (int64_t k = n4 * 4 + t; k < n; k += stride) m = max(m, (unsigned int)v[k]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, off, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
+}
+
+void launch_max_i32(const int32_t* v, int64_t n, unsigned int* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(unsigned int), s);
+  if (n <= 0) return;
+  int64_t blocks = (n / 16 + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(max_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, v, n, out);
+}
+
 void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStream_t s) {
   (void)hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
   if (n <= 0) return;

@@ -298,12 +298,12 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   const bool gk_on = !(gk_env && *gk_env && std::atoi(gk_env) == 0);
   const bool gk = gk_on && K >= 2 && K <= kGkMaxRuns;
   // chunk = kv_buf - longest record keeps every delivery buffer within kv_buf
-  auto chunk_bytes = [&](const Elem* order) {
-    launch_record_sizes(ctx, order, total, sizes_.as<int64_t>(), s);
-    unsigned long long* d_max = reinterpret_cast<unsigned long long*>(scan_tmp_.as<int64_t>());
-    launch_max_i64(sizes_.as<int64_t>(), total, d_max, s);
-    unsigned long long m = 0;
-    HIP_CHECK(hipMemcpyAsync(&m, d_max, 8, hipMemcpyDeviceToHost, s));
+  // (the longest record does not depend on the order: max over the side table's record lengths)
+  auto chunk_bytes = [&](const Elem*) {
+    unsigned int* d_max = reinterpret_cast<unsigned int*>(scan_tmp_.as<int64_t>());
+    launch_max_i32(ctx.reclen, total, d_max, s);
+    unsigned int m = 0;
+    HIP_CHECK(hipMemcpyAsync(&m, d_max, 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if ((int64_t)m > kv_buf) throw std::runtime_error("record larger than the delivery buffer");
     return std::max<int64_t>(1, kv_buf - (int64_t)m);

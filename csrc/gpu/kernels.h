@@ -192,6 +192,8 @@ void launch_gather_var(GenericKeyCtx ctx, const Elem* elems, int64_t n, const in
                        hipStream_t s);
 // *out = max(v[0..n)) (zeroed first).
 void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStream_t s);
+// *out = max of n non-negative int32.
+void launch_max_i32(const int32_t* v, int64_t n, unsigned int* out, hipStream_t s);
 // Delivery cut points: cuts[j] = output byte offset of the first record whose offset >= j*chunk
 // (cuts[nbuf] = total bytes), j = 0..nbuf.
 void launch_buffer_cuts(const int64_t* out_off, int64_t n, int64_t chunk, int64_t nbuf, int64_t* cuts,
