@@ -23,6 +23,7 @@ import argparse
 import json
 import sys
 import threading
+import resource
 import time
 import os
 
@@ -219,18 +220,26 @@ def netmerger(args) -> dict:
     out = {"config": "secondary sort through the NetMerger (loopback transport, 1 reducer)",
            "gb": round(total / 1e9, 3), "maps": args.maps}
     variants = [("cpu", {}), ("gpu_cold", {"mapred.uda.merge.backend": "gpu"}),
+                ("gpu_second", {"mapred.uda.merge.backend": "gpu"}),
                 ("gpu", {"mapred.uda.merge.backend": "gpu"}),
-                ("gpu_stage_8m", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.early.h2d.step": 8 << 20}),
+                ("gpu_drains_all", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": 0}),
+                ("gpu_drains8_step8m", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": 8,
+                                        "mapred.uda.gpu.early.h2d.step": 8 << 20}),
                 ("gpu_hybrid", {"mapred.uda.merge.backend": "gpu",
                                 "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
                                 "mapred.uda.gpu.spill": "host"})]
     for i, (name, conf) in enumerate(variants):
         c = UdaConsumer(args.maps, "job_nm", f"attempt_nm_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         for m in range(args.maps):
             c.fetch("localhost", "job_nm", f"attempt_nm_m_{m:06d}_0", 0)
         c.wait(3600)
         wall = time.perf_counter() - t0
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        # CPU seconds the task burned (all threads): the GPU box runs under a 16-CPU CFS quota, and a
+        # process that exceeds it inside a 100 ms period is stalled until the next one
+        out[name + "_cpu_s"] = round(r1.ru_utime + r1.ru_stime - r0.ru_utime - r0.ru_stime, 3)
         st = c.close()
         assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
         out[name + "_gbps"] = round(total / wall / 1e9, 3)
