@@ -38,7 +38,7 @@ class RcclExchange : public Exchange {
     std::memcpy(&id, uid.data(), sizeof(id));
     NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
     if (const char* t = std::getenv("UDA_RCCL_TIMEOUT_S")) timeout_ = std::chrono::seconds(std::max(1, std::atoi(t)));
-    pack_ = env_flag("UDA_RCCL_PACK", true);
+    pack_ = env_flag("UDA_RCCL_PACK", false);
     descs_.resize(4);
     for (auto& d : descs_) HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
   }
@@ -182,7 +182,7 @@ class RcclExchange : public Exchange {
   int rank_, world_;
   ncclComm_t comm_ = nullptr;
   bool aborted_ = false;
-  bool pack_ = true;
+  bool pack_ = false;
   std::chrono::seconds timeout_{900};
   DeviceBuffer counts_, staging_;
   std::vector<DescSlot> descs_;

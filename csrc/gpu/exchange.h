@@ -13,11 +13,14 @@
 //
 // Implementations:
 //   RcclExchange   - one process per GPU, RCCL communicator bootstrapped from an ncclUniqueId.
-//                    Default: the slices to each peer are packed on the comm stream into one
-//                    staging region and sent as ONE ncclSend per peer per round (RCCL pairs
-//                    operations, not bytes, and a large message per peer is what keeps all xGMI
-//                    links busy); the receiver's slices from a peer must then be contiguous.
-//                    UDA_RCCL_PACK=0 sends every slice as its own ncclSend (zero-copy).
+//                    Default (zero-copy): every slice is its own ncclSend straight from the map
+//                    output in the store into its receive slot, all of a round's sends and
+//                    receives inside one ncclGroupStart/End, peers in rotating order. A TeraSort
+//                    slice is tens of MB (130 GB / (16 rounds x 8 peers x 32 maps) = 32 MB), so
+//                    per-operation overhead is noise, and no CU time or HBM bandwidth goes to a pack.
+//                    UDA_RCCL_PACK=1 packs each peer's slices on the comm stream into one staging
+//                    region and sends one message per peer (for jobs with many tiny slices); the
+//                    receiver's slices from a peer must then be contiguous.
 //   LocalExchange  - W ranks as threads of one process sharing a device (tests / single-GPU
 //                    rehearsal of the multi-rank schedule): each receiver pulls its slices from
 //                    the senders' memory with copies on its own stream. Requires the send slices

@@ -752,7 +752,9 @@ PYBIND11_MODULE(_uda_native, m) {
 
   py::class_<gpu::ShuffleJob>(m, "ShuffleJob")
       .def(py::init([](const py::dict& cfg) { return new gpu::ShuffleJob(config_from_dict(cfg)); }))
-      .def("init_comm", [](gpu::ShuffleJob& j, py::bytes uid) { j.init_comm(uid); },
+      // std::string, not py::bytes: the argument is converted while the GIL is held (a py::bytes would
+      // be read and released inside the GIL-free call)
+      .def("init_comm", [](gpu::ShuffleJob& j, const std::string& uid) { j.init_comm(uid); },
            py::call_guard<py::gil_scoped_release>())
       .def("init_local", &gpu::ShuffleJob::init_local, py::call_guard<py::gil_scoped_release>())
       .def("generate", &gpu::ShuffleJob::generate, py::call_guard<py::gil_scoped_release>())
