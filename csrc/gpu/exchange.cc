@@ -54,7 +54,7 @@ class RcclExchange : public Exchange {
     if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
     return n;
   }
-  const char* name() const override { return pack_ ? "rccl" : "rccl-zero-copy"; }
+  const char* name() const override { return pack_ ? "rccl-packed" : "rccl"; }
 
   void alltoall_i64(const int64_t* send, int64_t* recv, size_t n, hipStream_t s) override {
     const size_t bytes = n * (size_t)world_ * 8;
