@@ -119,6 +119,34 @@ def test_consumer_gpu_backend(require_gpu, tmp_path):
         p.close()
 
 
+@pytest.mark.parametrize("drains,step", [(0, 0), (1, 0), (3, 0), (3, 40_000), (0, 20_000)])
+def test_consumer_gpu_fetch_drains_and_piecewise_staging(require_gpu, drains, step):
+    """Uncompressed in-memory MOFs fetched in 16 KiB requests: the GPU backend's drain-thread count
+    and piecewise early H2D staging (landed prefixes copied to HBM while the rest is in flight)
+    must deliver exactly the CPU merge's stream."""
+    from uda_amd.utils.mof import encode_partitions
+    p = UdaProvider()
+    try:
+        maps = datagen.secondary_sort(num_maps=9, reducers=2, rows_per_map=1500, seed=11)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_d_m_{i:06d}_0"
+            data, index = encode_partitions(parts)
+            p.add_mof_memory("job_d", mid, data, index)
+            ids.append(mid)
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": drains,
+                "mapred.uda.gpu.early.h2d.step": step}
+        recs_gpu, st, _ = run_reduce("h", "job_d", ids, 0, datagen.TEXT, conf=conf, max_buf_kb=16, min_buf_kb=16,
+                                     kv_buf_size=8192)
+        recs_cpu, _, _ = run_reduce("h", "job_d", ids, 0, datagen.TEXT, max_buf_kb=16, min_buf_kb=16,
+                                    kv_buf_size=8192)
+        assert st["backend"] == "gpu"
+        assert [k for k, _ in recs_gpu] == [k for k, _ in recs_cpu]  # equal keys may come in any run order
+        assert sorted(recs_gpu) == sorted(recs_cpu)
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("tier,codec", [("host", None), ("disk", None), ("disk", "snappy")])
 def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
     """Reduce input larger than the device budget: LPQ merges on the GPU spill to host DRAM or to
