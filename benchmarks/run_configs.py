@@ -251,8 +251,43 @@ def netmerger(args) -> dict:
             out["hybrid_lpqs"] = st["lpqs"]
             out["hybrid_rpq_rounds"] = st["rpq_rounds"]
     prov.close()
+    out.update(_netmerger_device_mofs(args, runs))
     if args.reducers > 1:
         out.update(_netmerger_concurrent(args, rows))
+    return out
+
+
+def _netmerger_device_mofs(args, runs) -> dict:
+    """The same data with HBM-resident MOFs (the provider registers device memory): the reducer fetches
+    partition descriptors and merges the partitions where they live, so only the merged output
+    crosses PCIe (device fetch, generic-key merge with key-range rounds streamed out)."""
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    prov = UdaProvider()
+    total = 0
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        total += len(data) - 2
+        prov.add_mof_device("job_nmd", f"attempt_nmd_m_{m:06d}_0", data, index)
+    out = {}
+    conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch": "device"}
+    for attempt in ("cold", "warm", "warm2"):
+        c = UdaConsumer(args.maps, "job_nmd", f"attempt_nmd_r_000000_{attempt}", TEXT, conf=conf, keep_records=False)
+        t0 = time.perf_counter()
+        for m in range(args.maps):
+            c.fetch("localhost", "job_nmd", f"attempt_nmd_m_{m:06d}_0", 0)
+        c.wait(3600)
+        wall = time.perf_counter() - t0
+        st = c.close()
+        assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
+        out[f"gpu_hbm_mofs_{attempt}_gbps"] = round(total / wall / 1e9, 3)
+        if attempt != "cold":
+            out[f"gpu_hbm_mofs_{attempt}_stats"] = {k: st[k] for k in ("merge_path", "device_descriptors",
+                                                                       "host_fetched_bytes", "gpu_device_ms",
+                                                                       "gpu_d2h_wait_ms", "merge_ms", "fetch_ms")
+                                                   if k in st}
+    prov.close()
     return out
 
 
