@@ -225,6 +225,9 @@ def netmerger(args) -> dict:
                 ("gpu_drains_all", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": 0}),
                 ("gpu_drains8_step8m", {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": 8,
                                         "mapred.uda.gpu.early.h2d.step": 8 << 20}),
+                ("gpu_hybrid_first", {"mapred.uda.merge.backend": "gpu",
+                                      "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
+                                      "mapred.uda.gpu.spill": "host"}),
                 ("gpu_hybrid", {"mapred.uda.merge.backend": "gpu",
                                 "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
                                 "mapred.uda.gpu.spill": "host"})]

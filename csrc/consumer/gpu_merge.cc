@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <future>
 #include <random>
 #include <thread>
 
@@ -315,7 +316,7 @@ class DevicePool {
   }
 
  private:
-  static constexpr size_t kMaxIdle = 4;
+  static constexpr size_t kMaxIdle = 8;  // e.g. 4 concurrent hybrid tasks: 4 workspaces, 8 stagers
   std::mutex mu_;
   std::map<int, std::vector<std::unique_ptr<T>>> idle_;
 };
@@ -518,9 +519,14 @@ void ReduceTask::merge_gpu() {
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
+  PoolLease<DeviceWorkspace> ws2_lease{device, nullptr};  // second workspace of the pipelined RPQ rounds
+  DeviceWorkspace* ws2 = nullptr;
   // uncompressed partitions go to HBM as soon as each one is complete (overlapping the fetch)
-  PoolLease<EarlyStager> stager_lease{device, nullptr};
+  // Two stagers: the group being fetched is staged by `stager` while the LPQ thread merges the
+  // previous group out of `job_stager`'s arena; spill_group swaps them.
+  PoolLease<EarlyStager> stager_lease{device, nullptr}, stager_lease2{device, nullptr};
   EarlyStager* stager = nullptr;
+  EarlyStager* job_stager = nullptr;
   if (fetch_codec == Codec::kNone && stage_codec == Codec::kNone && host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0) {
     stager_lease.obj = DevicePool<EarlyStager>::get().acquire(device, [device] { return std::make_unique<EarlyStager>(device); });
     stager = stager_lease.obj.get();
@@ -572,11 +578,11 @@ void ReduceTask::merge_gpu() {
   // LPQ: merge one group on the device and spill it with its sparse index. Runs on the LPQ thread,
   // one group at a time, while the fetch fills the next group (the reference's fetcher running ahead
   // of the LPQ merges, MergeManager.cc:202-288).
-  auto merge_spill = [&](std::vector<Span> jg, std::vector<std::string> ids) {
-    if (stager) stager->flush();
+  auto merge_spill = [&](std::vector<Span> jg, std::vector<std::string> ids, EarlyStager* st) {
+    if (st) st->flush();
     DeviceMergeOut m = device_merge(ws, jg, stage_codec, kind_, kSampleSpacing, s);
     count_decoded(m.decoded_blocks);
-    if (stager) stager->reset();  // the merge read the staged copies; recycle their HBM
+    if (st) st->reset();  // the merge read the staged copies; recycle their HBM
     SpillRun run;
     run.bytes = m.bytes;
     const bool disk = tier == "disk";
@@ -663,9 +669,8 @@ void ReduceTask::merge_gpu() {
       if (fault_hit("LPQ_DONE")) throw UdaError("injected failure after an LPQ spill");
     }
   };
-  // The group being fetched lives in fill_mem; the one being merged in job_mem. While an LPQ merge
-  // runs, new partitions are not staged early (its HBM is in use); the next group then goes H2D at
-  // its own merge.
+  // The group being fetched lives in fill_mem (and is staged to HBM by `stager`); the one being merged
+  // in job_mem (its HBM copies in job_stager's arena), so the next group's H2D overlaps an LPQ merge.
   gpu::PinnedArena group_mem2;
   gpu::PinnedArena* fill_mem = &group_mem;
   gpu::PinnedArena* job_mem = &group_mem2;
@@ -691,16 +696,23 @@ void ReduceTask::merge_gpu() {
     lpq_wait();               // one LPQ merge at a time (device workspace, stream s)
     job_mem->release_all();   // the previous LPQ's inputs are merged
     std::swap(fill_mem, job_mem);
+    if (stager && !job_stager) {  // first LPQ: the second stager (online merges never need one)
+      stager_lease2.obj = DevicePool<EarlyStager>::get().acquire(device, [device] { return std::make_unique<EarlyStager>(device); });
+      job_stager = stager_lease2.obj.get();
+      job_stager->reset();
+    }
+    std::swap(stager, job_stager);  // the group's staged copies go with it; the next group stages into the other
     std::vector<Span> jg;
     jg.swap(group);
     std::vector<std::string> ids;
     ids.swap(group_ids);
     group_raw = 0;
     lpq_running = true;
-    lpq_thr = std::thread([&, device, jg = std::move(jg), ids = std::move(ids)]() mutable {
+    EarlyStager* st = job_stager;
+    lpq_thr = std::thread([&, device, st, jg = std::move(jg), ids = std::move(ids)]() mutable {
       try {
         if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
-        merge_spill(std::move(jg), std::move(ids));
+        merge_spill(std::move(jg), std::move(ids), st);
       } catch (...) {
         lpq_err = std::current_exception();
       }
@@ -811,7 +823,7 @@ void ReduceTask::merge_gpu() {
                 // With early staging the partition is copied to HBM once complete, or (stage_step > 0)
                 // every stage_step bytes of its landed prefix while the rest is still in flight.
                 const int64_t cap = f.part_len();
-                uint8_t* dev = stager && !lpq_running ? stager->reserve(cap) : nullptr;
+                uint8_t* dev = stager ? stager->reserve(cap) : nullptr;
                 int64_t off = f.take_first(dst[k], cap);
                 if (dev && stage_step > 0) stager->copy(dst[k], dev, off);
                 if (off < cap) {
@@ -873,9 +885,9 @@ void ReduceTask::merge_gpu() {
     // ---- delivery of merged rounds; EOF rides in the very last buffer
     bool eof_sent = false;
     std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
-    auto deliver = [&](const DeviceMergeOut& m, bool last, hipStream_t ds) {
+    auto deliver = [&](const DeviceMergeOut& m, bool last, hipStream_t ds, DeviceWorkspace& w) {
       const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-      stream_out(ws, m, ds, [&](const uint8_t* piece, size_t c0, size_t c1) {
+      stream_out(w, m, ds, [&](const uint8_t* piece, size_t c0, size_t c1) {
         for (size_t j = c0; j < c1; ++j) {
           if (stop_) throw UdaError("reduce task stopped during merge");
           const int64_t b = m.cuts[j], e = m.cuts[j + 1];
@@ -915,7 +927,7 @@ void ReduceTask::merge_gpu() {
                                         DeviceMergeOut r;
                                         r.cuts = cuts;
                                         r.records = records;
-                                        deliver(r, last, ws.copy_stream());
+                                        deliver(r, last, ws.copy_stream(), ws);
                                       });
       count_decoded(m.decoded_blocks);
     } else {
@@ -1004,23 +1016,39 @@ void ReduceTask::merge_gpu() {
         std::lock_guard<std::mutex> g(st_mu_);
         st_.rpq_rounds = rounds;
       }
-      gpu::PinnedArena slice_mem;
-      for (int q = 0; q < rounds; ++q) {
+      // RPQ rounds, pipelined over two workspaces: round q + 1's slices are read, copied to HBM and
+      // merged on a helper thread (workspace and stream of parity q + 1) while round q is delivered.
+      ws2_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
+      ws2 = ws2_lease.obj.get();
+      ws2->reset_stats();
+      StreamGuard sg2;
+      HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
+      DeviceWorkspace* wsv[2] = {&ws, ws2};
+      hipStream_t sv[2] = {s, sg2.s};
+      gpu::PinnedArena slice_mem[2];
+      auto prep = [&](int q) {
+        if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
         std::vector<Span> views;
-        slice_mem.release_all();
+        gpu::PinnedArena& sm = slice_mem[q & 1];
+        sm.release_all();  // round q - 2's slices: copied to HBM before its merge returned
         for (int r = 0; r < R; ++r) {
           const SpillRun& run = spills[(size_t)r];
           const int64_t b = bnd[(size_t)r][(size_t)q], e = bnd[(size_t)r][(size_t)q + 1];
           if (run.fd < 0) {
             views.push_back(Span{run.mem + b, e - b});
           } else {
-            uint8_t* p = slice_mem.alloc((size_t)std::max<int64_t>(e - b, 1));
+            uint8_t* p = sm.alloc((size_t)std::max<int64_t>(e - b, 1));
             read_run(run, b, e - b, p);
             views.push_back(Span{p, e - b});
           }
         }
-        DeviceMergeOut m = device_merge(ws, views, Codec::kNone, kind_, kv, s);  // views: host spans
-        deliver(m, q + 1 == rounds, s);
+        return device_merge(*wsv[q & 1], views, Codec::kNone, kind_, kv, sv[q & 1]);  // views: host spans
+      };
+      std::future<DeviceMergeOut> next = std::async(std::launch::async, prep, 0);
+      for (int q = 0; q < rounds; ++q) {
+        DeviceMergeOut m = next.get();
+        if (q + 1 < rounds) next = std::async(std::launch::async, prep, q + 1);
+        deliver(m, q + 1 == rounds, sv[q & 1], *wsv[q & 1]);
       }
     }
     if (!eof_sent) {  // empty final round (or empty input): EOF alone
@@ -1033,12 +1061,14 @@ void ReduceTask::merge_gpu() {
     cleanup(true);
     HIP_CHECK(hipStreamSynchronize(s));
     ws_lease.clean = true;
+    ws2_lease.clean = true;
     stager_lease.clean = true;
+    stager_lease2.clean = true;
     std::lock_guard<std::mutex> g(st_mu_);
-    st_.gpu_h2d_ms = ws.h2d_ms;
-    st_.gpu_device_ms = ws.device_ms;
-    st_.gpu_d2h_wait_ms = ws.d2h_ms;
-    st_.gpu_sink_ms = ws.sink_ms;
+    st_.gpu_h2d_ms = ws.h2d_ms + (ws2 ? ws2->h2d_ms : 0);
+    st_.gpu_device_ms = ws.device_ms + (ws2 ? ws2->device_ms : 0);
+    st_.gpu_d2h_wait_ms = ws.d2h_ms + (ws2 ? ws2->d2h_ms : 0);
+    st_.gpu_sink_ms = ws.sink_ms + (ws2 ? ws2->sink_ms : 0);
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
   } catch (...) {
