@@ -676,7 +676,6 @@ void ReduceTask::merge_gpu() {
   gpu::PinnedArena* job_mem = &group_mem2;
   std::thread lpq_thr;
   std::exception_ptr lpq_err;
-  std::atomic<bool> lpq_running{false};
   auto lpq_wait = [&] {
     if (lpq_thr.joinable()) lpq_thr.join();
     if (lpq_err) {
@@ -707,7 +706,6 @@ void ReduceTask::merge_gpu() {
     std::vector<std::string> ids;
     ids.swap(group_ids);
     group_raw = 0;
-    lpq_running = true;
     EarlyStager* st = job_stager;
     lpq_thr = std::thread([&, device, st, jg = std::move(jg), ids = std::move(ids)]() mutable {
       try {
@@ -716,7 +714,6 @@ void ReduceTask::merge_gpu() {
       } catch (...) {
         lpq_err = std::current_exception();
       }
-      lpq_running = false;
     });
   };
   // resume: restored LPQ spills (data + sparse index) of a failed attempt
