@@ -55,6 +55,10 @@ def parse_args(argv=None):
     ap.add_argument("--replan", action="store_true",
                     help="recompute the cell splits (and re-exchange the slice counts) inside every timed "
                          "step instead of reusing the setup-time plan")
+    ap.add_argument("--map-sort", action=argparse.BooleanOptionalAction, default=True,
+                    help="setup generates unsorted TeraGen map input (uniform random keys) and sorts every "
+                         "map-output partition on the device (F8 radix sort), like a map task's sort before "
+                         "its spill (default); --no-map-sort generates the sorted runs directly")
     ap.add_argument("--store", choices=("hbm", "host", "disk"), default="hbm",
                     help="map-output store: HBM (default), pinned host DRAM, or MOF files on --local-dirs")
     ap.add_argument("--local-dirs", default="/tmp", help="--store disk: comma-separated directories")
@@ -143,7 +147,7 @@ def main(argv=None) -> int:
                          local_dirs=args.local_dirs,
                          d2h_piece_bytes=args.d2h_piece_mb << 20, pinned_slots=args.pinned_slots,
                          d2h_engines=args.d2h_engines, deliver_host=not args.device_only,
-                         replan=args.replan)
+                         replan=args.replan, map_sort=args.map_sort)
     job = TeraSortShuffle(ctx, cfg)
     t_setup = time.perf_counter()
     job.setup()
@@ -155,7 +159,8 @@ def main(argv=None) -> int:
               f"store={job.job.store_bytes/1e9:.1f}GB "
               f"max_round_records={job.job.max_round_records} exchange={job.job.exchange_name} "
               f"store={job.job.store_name} "
-              f"delivery={job.job.delivery_name}", file=sys.stderr, flush=True)
+              f"delivery={job.job.delivery_name}"
+              + (f" map_sort_ms={job.job.map_sort_ms:.1f}" if args.map_sort else ""), file=sys.stderr, flush=True)
 
     for i in range(args.warmup):
         st = job.step()
@@ -205,7 +210,10 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bytes",
-            "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "data": ("synthetic TeraGen-shaped (uniform random 10B keys, 90B values, 104B IFile records "
+                     "generated in HBM; map outputs sorted by the device radix sort at setup)") if args.map_sort else
+                    "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "map_sort_ms": round(job.job.map_sort_ms, 1) if args.map_sort else None,
             "breakdown_note": "comm/merge: device-event spans per round; d2h: summed piece latency; "
                               "wait_out: merge waiting for a free output slot (delivery-bound)",
             "config": {

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256) teragen_kernel(uint8_t* const* bases, con
                                                       const uint64_t* key_lo,
                                                       const uint64_t* key_span,
                                                       const uint64_t* seeds,
-                                                      unsigned long long* run_checksum) {
+                                                      unsigned long long* run_checksum, int unsorted) {
   const int r = blockIdx.y;
   const int64_t n = nrec[r];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -51,8 +51,14 @@ __global__ void __launch_bounds__(256) teragen_kernel(uint8_t* const* bases, con
     uint64_t st = seeds[r] ^ (0xD1B54A32D192ED03ULL * (uint64_t)(i + 1));
     const uint64_t span = key_span[r];
     const uint64_t stride = span / (uint64_t)n;
-    const uint64_t jitter = stride ? splitmix64(st) % stride : 0;
-    const uint64_t hi = key_lo[r] + (uint64_t)i * stride + jitter;
+    uint64_t hi;
+    if (unsorted) {  // map input: keys in generation order, sorted by launch_sort_fixed_run
+      const uint64_t draw = splitmix64(st);
+      hi = key_lo[r] + (span == ~0ull ? draw : draw % span);
+    } else {
+      const uint64_t jitter = stride ? splitmix64(st) % stride : 0;
+      hi = key_lo[r] + (uint64_t)i * stride + jitter;
+    }
     const uint64_t lo16 = splitmix64(st) & 0xFFFF;
     // Record layout: [0x0B keyLen=11][0x5B valLen=91][0x0A][k0..k9][0x5A][v0..v89]
     uint64_t w[13];
@@ -163,11 +169,11 @@ void launch_sample_fixed(uint8_t* const* bases, const int64_t* nrec, int nruns, 
 
 void launch_teragen(uint8_t* const* bases, const int64_t* nrec, const uint64_t* key_lo,
                     const uint64_t* key_span, const uint64_t* seeds, int nruns, int64_t max_nrec,
-                    unsigned long long* run_checksum, hipStream_t s) {
+                    unsigned long long* run_checksum, hipStream_t s, int unsorted) {
   if (nruns <= 0 || max_nrec <= 0) return;
   dim3 grid((unsigned)((max_nrec + 255) / 256), (unsigned)nruns);
   hipLaunchKernelGGL(teragen_kernel, grid, dim3(256), 0, s, bases, nrec, key_lo, key_span, seeds,
-                     run_checksum);
+                     run_checksum, unsorted);
 }
 
 void launch_split_fixed(uint8_t* const* bases, const int64_t* nrec, const Elem* bounds,

@@ -215,6 +215,7 @@ struct ShuffleConfig {
   std::string store = "hbm";             // map-output store: "hbm", "host" (pinned DRAM) or "disk"
   std::string local_dirs;                // store=disk: comma-separated directories for the MOF files
   bool replan = false;                   // every step recomputes the cell splits and exchanges the counts
+  bool map_sort = false;                 // setup: generate unsorted map input and sort it on the device (F8)
 };
 
 struct StepStats {
@@ -272,6 +273,7 @@ class ShuffleJob {
   // Records each of this GPU's reducers receives per step (after plan()).
   std::vector<int64_t> reducer_records() const { return reducer_records_; }
   int64_t store_bytes() const { return store_bytes_; }
+  double map_sort_ms() const { return map_sort_ms_; }  // cfg.map_sort: device time of the map-side sorts
   // Device address / size of MOF m in the partition store (host address for the host tier).
   const uint8_t* mof_device_ptr(int m) const { return store_dev_base_ + mof_off_.at(m); }
   int64_t mof_bytes(int m) const { return mof_off_.at(m + 1) - mof_off_.at(m); }
@@ -322,6 +324,7 @@ class ShuffleJob {
   uint8_t* store_base_ = nullptr;      // where run_base() points
   uint8_t* store_dev_base_ = nullptr;  // device-accessible alias for kernels
   int64_t store_bytes_ = 0;
+  double map_sort_ms_ = 0;
   std::vector<int64_t> mof_off_, run_off_, run_nrec_;  // run index m*W + d
   std::vector<uint64_t> dest_checksum_;
   std::vector<int64_t> dest_records_;

@@ -49,9 +49,17 @@ struct RunDesc {
 // with random jitter, so the K runs of one reducer interleave randomly), random 2 trailing key
 // bytes and 90 printable value bytes, followed by the 2-byte EOF marker. Accumulates an
 // order-independent checksum (sum of record_hash) per run into `run_checksum[r]` (zero it first).
+// unsorted != 0: keys uniform in the same range in generation order (a map task's input before its
+// sort; launch_sort_fixed_run turns each run into a sorted map-output partition).
 void launch_teragen(uint8_t* const* bases, const int64_t* nrec, const uint64_t* key_lo,
                     const uint64_t* key_span, const uint64_t* seeds, int nruns, int64_t max_nrec,
-                    unsigned long long* run_checksum, hipStream_t s);
+                    unsigned long long* run_checksum, hipStream_t s, int unsorted = 0);
+
+// ---------------------------------------------------------------- F8 map-side sort (radix.hip)
+// Sort the n TeraSort records at `base` by their 10-byte key (stable LSD radix sort, 8-bit digits,
+// then one record gather). `ws` holds sort_fixed_ws_bytes(n) bytes of device memory; n < 2^32.
+int64_t sort_fixed_ws_bytes(int64_t n);
+void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s);
 
 // ---------------------------------------------------------------- round splitting
 // For each (run r, boundary b): out[r*(nb+2) + 1 + b] = lower_bound of boundary key (hi, lo16)

@@ -84,6 +84,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("store", c.store);
   get("local_dirs", c.local_dirs);
   get("replan", c.replan);
+  get("map_sort", c.map_sort);
   return c;
 }
 
@@ -630,6 +631,45 @@ PYBIND11_MODULE(_uda_native, m) {
     }
     return py::make_tuple(out, cuts, records, passes, merge_ms, serial_runs);
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
+  // F8: sort TeraSort records (104-byte IFile records, no EOF marker) by their 10-byte key on the
+  // device; returns (sorted bytes, device ms of the sort).
+  m.def("gpu_sort_fixed", [](py::buffer b, int device) {
+    py::buffer_info v = b.request();
+    const int64_t bytes = (int64_t)(v.size * v.itemsize);
+    if (bytes % gpu::kTeraRecordBytes) throw py::value_error("not a whole number of 104-byte records");
+    const int64_t n = bytes / gpu::kTeraRecordBytes;
+    if (n >= (int64_t)UINT32_MAX) throw py::value_error("too many records");
+    PyObject* o = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)bytes);
+    if (!o) throw py::error_already_set();
+    py::bytes out = py::reinterpret_steal<py::bytes>(o);
+    float ms = 0;
+    {
+      py::gil_scoped_release rel;
+      HIP_CHECK(hipSetDevice(device));
+      gpu::DeviceBuffer d, ws;
+      d.alloc((size_t)std::max<int64_t>(bytes, 16));
+      ws.alloc((size_t)gpu::sort_fixed_ws_bytes(std::max<int64_t>(n, 1)));
+      hipStream_t s = nullptr;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreate(&e0));
+      HIP_CHECK(hipEventCreate(&e1));
+      if (bytes) HIP_CHECK(hipMemcpyAsync(d.as(), v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
+      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s);  // warm-up (first launch loads code)
+      if (bytes) HIP_CHECK(hipMemcpyAsync(d.as(), v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipEventRecord(e0, s));
+      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipEventRecord(e1, s));
+      if (bytes) HIP_CHECK(hipMemcpyAsync(PyBytes_AS_STRING(o), d.as(), (size_t)bytes, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      (void)hipStreamDestroy(s);
+    }
+    return py::make_tuple(out, (double)ms);
+  }, py::arg("records"), py::arg("device") = 0);
   // F6: decode Hadoop block-compressed streams on the device; returns (raw streams, blocks, decode_ms)
   m.def("gpu_block_decode", [](const std::string& codec_cls, const std::vector<std::string>& streams, int device) {
     bool unsup = false;
@@ -823,5 +863,6 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("mof_device_ptr", [](gpu::ShuffleJob& j, int m) { return (uintptr_t)j.mof_device_ptr(m); })
       .def("mof_bytes", &gpu::ShuffleJob::mof_bytes)
       .def_property_readonly("store_bytes", &gpu::ShuffleJob::store_bytes)
+      .def_property_readonly("map_sort_ms", &gpu::ShuffleJob::map_sort_ms)
       .def_property_readonly("max_round_records", &gpu::ShuffleJob::max_round_records);
 }

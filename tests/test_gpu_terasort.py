@@ -89,17 +89,19 @@ def test_merge_tree_many_runs(require_gpu):
     assert st["merge_passes"] == 9
 
 
-@pytest.mark.parametrize("world,maps,rounds,reducers", [
-    (2, 3, 3, 1), (3, 2, 4, 1), (4, 1, 1, 1), (8, 2, 16, 1), (4, 3, 4, 3), (8, 2, 4, 2),
+@pytest.mark.parametrize("world,maps,rounds,reducers,map_sort", [
+    (2, 3, 3, 1, False), (3, 2, 4, 1, False), (4, 1, 1, 1, False), (8, 2, 16, 1, False), (4, 3, 4, 3, False),
+    (8, 2, 4, 2, False), (4, 3, 4, 3, True), (8, 2, 16, 2, True),
 ])
-def test_multirank_schedule_local_group(require_gpu, world, maps, rounds, reducers):
+def test_multirank_schedule_local_group(require_gpu, world, maps, rounds, reducers, map_sort):
     """The multi-GPU shuffle schedule (cell split -> all-to-all-v rounds -> grouped merge ->
     deliver) rehearsed with `world` ranks sharing one GPU; every reducer must receive exactly its
-    key range, and every received slice must hash to what its sender computed."""
+    key range, and every received slice must hash to what its sender computed. map_sort: the map
+    outputs come from the device radix sort of unsorted map input (the bench default)."""
     from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
     cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, reducers=reducers,
-                         validate=True, sample_every=64, **SMALL)
-    jobs, ck, rec = make_local_group(world, cfg, group=f"t{world}{maps}{rounds}{reducers}")
+                         validate=True, sample_every=64, map_sort=map_sort, **SMALL)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"t{world}{maps}{rounds}{reducers}{int(map_sort)}")
     readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(reducers)] for _ in range(world)]
 
     def attach(d):

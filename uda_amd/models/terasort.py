@@ -50,6 +50,7 @@ class TeraSortConfig:
     store: str = "hbm"                  # "hbm", "host" (pinned DRAM) or "disk" (MOF files, jobs > HBM + DRAM)
     local_dirs: str = "/tmp"            # store="disk": comma-separated directories for the MOF files
     replan: bool = False                # every step recomputes the cell splits and exchanges the counts
+    map_sort: bool = False              # setup: unsorted map input sorted on the device (F8 radix sort)
 
 
 class TeraSortShuffle:
@@ -66,7 +67,8 @@ class TeraSortShuffle:
             rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed, kv_buf_bytes=cfg.kv_buf_bytes,
             d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
             d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host,
-            validate=cfg.validate, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan))
+            validate=cfg.validate, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan,
+            map_sort=cfg.map_sort))
         self.sink = n.J2CSink(cfg.reducers, cfg.kv_buf_bytes)
         self.expected_checksum = None
         self.expected_records = None
@@ -161,7 +163,8 @@ def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: st
         records_per_map=records_per_map, rounds=cfg.rounds, reducers=cfg.reducers, seed=cfg.seed,
         kv_buf_bytes=cfg.kv_buf_bytes, d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
         d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host, validate=cfg.validate,
-        local_group=group, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan))
+        local_group=group, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan,
+        map_sort=cfg.map_sort))
         for r in range(world)]
     for j in jobs:
         j.init_local()
