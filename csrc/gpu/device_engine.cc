@@ -611,29 +611,11 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(d_sp.as(), key_span.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sd.as(), seeds.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemset(d_ck.as(), 0, nruns * 8));
-  // cfg.map_sort: the map side's own work — unsorted map input, each partition sorted on the device
-  // (F8 LSD radix sort) before the reducers see it. The checksums are order-independent.
-  const int unsorted = cfg_.map_sort ? 1 : 0;
-  DeviceBuffer sort_ws;
+  // cfg.map_sort: the map side's own work — each partition is generated unsorted into the sort
+  // workspace and the device radix sort (F8) gathers it, sorted, into the store. The checksums are
+  // order-independent.
+  DeviceBuffer sort_ws, d_stage;
   hipEvent_t sort_t0 = nullptr, sort_t1 = nullptr;
-  if (cfg_.map_sort) {
-    if (max_n >= (int64_t)UINT32_MAX) throw std::runtime_error("map_sort: a run has 2^32 or more records");
-    sort_ws.alloc((size_t)sort_fixed_ws_bytes(max_n));
-    HIP_CHECK(hipEventCreate(&sort_t0));
-    HIP_CHECK(hipEventCreate(&sort_t1));
-  }
-  map_sort_ms_ = 0;
-  auto sort_runs = [&](int r0, int r1) {  // sort runs [r0, r1) where generated (gen_bases)
-    if (!cfg_.map_sort) return;
-    HIP_CHECK(hipEventRecord(sort_t0, s_compute_));
-    for (int r = r0; r < r1; ++r) launch_sort_fixed_run(gen_bases[r], run_nrec_[r], sort_ws.as(), s_compute_);
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(sort_t1, s_compute_));
-    HIP_CHECK(hipEventSynchronize(sort_t1));
-    float ms = 0;
-    HIP_CHECK(hipEventElapsedTime(&ms, sort_t0, sort_t1));
-    map_sort_ms_ += ms;
-  };
   struct EvGuard {
     hipEvent_t* a;
     hipEvent_t* b;
@@ -642,19 +624,45 @@ void ShuffleJob::generate() {
       if (*b) (void)hipEventDestroy(*b);
     }
   } ev_guard{&sort_t0, &sort_t1};
+  if (cfg_.map_sort) {
+    if (max_n >= (int64_t)UINT32_MAX) throw std::runtime_error("map_sort: a run has 2^32 or more records");
+    sort_ws.alloc((size_t)sort_fixed_ws_bytes(max_n));
+    uint8_t* recs = sort_fixed_ws_records(sort_ws.as(), max_n);
+    d_stage.alloc(sizeof(uint8_t*));
+    HIP_CHECK(hipMemcpy(d_stage.as(), &recs, sizeof(uint8_t*), hipMemcpyHostToDevice));
+    HIP_CHECK(hipEventCreate(&sort_t0));
+    HIP_CHECK(hipEventCreate(&sort_t1));
+  }
+  map_sort_ms_ = 0;
+  auto gen_runs = [&](int r0, int r1) {  // generate runs [r0, r1) at gen_bases
+    if (!cfg_.map_sort) {
+      launch_teragen(d_b.as<uint8_t*>() + r0, d_n.as<int64_t>() + r0, d_lo.as<uint64_t>() + r0,
+                     d_sp.as<uint64_t>() + r0, d_sd.as<uint64_t>() + r0, r1 - r0, max_n,
+                     d_ck.as<unsigned long long>() + r0, s_compute_);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+    for (int r = r0; r < r1; ++r) {
+      if (run_nrec_[r] <= 0) continue;
+      launch_teragen(d_stage.as<uint8_t*>(), d_n.as<int64_t>() + r, d_lo.as<uint64_t>() + r, d_sp.as<uint64_t>() + r,
+                     d_sd.as<uint64_t>() + r, 1, run_nrec_[r], d_ck.as<unsigned long long>() + r, s_compute_,
+                     /*unsorted=*/1);
+      HIP_CHECK(hipEventRecord(sort_t0, s_compute_));
+      launch_sort_fixed_run(gen_bases[r], run_nrec_[r], sort_ws.as(), s_compute_, /*staged=*/true);
+      HIP_CHECK(hipEventRecord(sort_t1, s_compute_));
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipEventSynchronize(sort_t1));  // the next run reuses the workspace's record area
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, sort_t0, sort_t1));
+      map_sort_ms_ += ms;
+    }
+  };
   if (!spilled()) {
-    launch_teragen(d_b.as<uint8_t*>(), d_n.as<int64_t>(), d_lo.as<uint64_t>(), d_sp.as<uint64_t>(),
-                   d_sd.as<uint64_t>(), nruns, max_n, d_ck.as<unsigned long long>(), s_compute_, unsorted);
-    HIP_CHECK(hipGetLastError());
-    sort_runs(0, nruns);
+    gen_runs(0, nruns);
     HIP_CHECK(hipStreamSynchronize(s_compute_));
   } else {
     for (int m = 0; m < M; ++m) {
-      launch_teragen(d_b.as<uint8_t*>() + m * W, d_n.as<int64_t>() + m * W, d_lo.as<uint64_t>() + m * W,
-                     d_sp.as<uint64_t>() + m * W, d_sd.as<uint64_t>() + m * W, W, max_n,
-                     d_ck.as<unsigned long long>() + m * W, s_compute_, unsorted);
-      HIP_CHECK(hipGetLastError());
-      sort_runs(m * W, (m + 1) * W);
+      gen_runs(m * W, (m + 1) * W);
       if (disk_store())  // map output written to its MOF file (O_DIRECT through io_uring)
         disk_->write_file(m, tmp.as<uint8_t>(), mof_off_[m + 1] - mof_off_[m], s_compute_);
       else

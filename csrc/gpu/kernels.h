@@ -58,8 +58,11 @@ void launch_teragen(uint8_t* const* bases, const int64_t* nrec, const uint64_t* 
 // ---------------------------------------------------------------- F8 map-side sort (radix.hip)
 // Sort the n TeraSort records at `base` by their 10-byte key (stable LSD radix sort, 8-bit digits,
 // then one record gather). `ws` holds sort_fixed_ws_bytes(n) bytes of device memory; n < 2^32.
+// staged: the unsorted records were written to sort_fixed_ws_records(ws, n) instead (no copy aside);
+// the sorted run lands at `base` followed by the IFile EOF marker.
 int64_t sort_fixed_ws_bytes(int64_t n);
-void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s);
+uint8_t* sort_fixed_ws_records(void* ws, int64_t n);
+void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s, bool staged = false);
 
 // ---------------------------------------------------------------- round splitting
 // For each (run r, boundary b): out[r*(nb+2) + 1 + b] = lower_bound of boundary key (hi, lo16)

@@ -206,12 +206,17 @@ __global__ void __launch_bounds__(kThreads) rs_scatter_kernel(const SortKey* __r
 }
 
 __global__ void __launch_bounds__(kThreads) rs_gather_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
-                                                             const SortKey* __restrict__ keys, int64_t n) {
+                                                             const SortKey* __restrict__ keys, int64_t n, int eof) {
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int64_t i = g / kWords;
   if (i >= n) return;
   const int w = (int)(g - i * kWords);
   dst[i * kWords + w] = src[(int64_t)keys[i].idx * kWords + w];
+  if (eof && g == 0) {  // IFile EOF marker VInt(-1) VInt(-1) after the last record
+    uint8_t* e = reinterpret_cast<uint8_t*>(dst + n * kWords);
+    e[0] = 0xFF;
+    e[1] = 0xFF;
+  }
 }
 
 int64_t tiles_of(int64_t n) { return (n + kTile - 1) / kTile; }
@@ -225,8 +230,14 @@ int64_t sort_fixed_ws_bytes(int64_t n) {
   return keys + hist + recs;
 }
 
-void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s) {
-  if (n <= 1) return;
+uint8_t* sort_fixed_ws_records(void* ws, int64_t n) {
+  const int64_t kb = (n * (int64_t)sizeof(SortKey) + 255) & ~255ll;
+  return static_cast<uint8_t*>(ws) + 2 * kb + ((tiles_of(n) * kBins * 4 + 255) & ~255ll) + 1024;
+}
+
+void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s, bool staged) {
+  if (n <= 0) return;
+  if (n == 1 && !staged) return;
   uint8_t* p = static_cast<uint8_t*>(ws);
   const int64_t kb = (n * (int64_t)sizeof(SortKey) + 255) & ~255ll;
   SortKey* a = reinterpret_cast<SortKey*>(p);
@@ -234,8 +245,11 @@ void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s) {
   const int64_t ntiles = tiles_of(n);
   uint32_t* hist = reinterpret_cast<uint32_t*>(p + 2 * kb);
   uint32_t* totals = reinterpret_cast<uint32_t*>(p + 2 * kb + ((ntiles * kBins * 4 + 255) & ~255ll));
-  uint8_t* recs = p + 2 * kb + ((ntiles * kBins * 4 + 255) & ~255ll) + 1024;
-  hipLaunchKernelGGL(rs_extract_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, base, n, a);
+  uint8_t* recs = sort_fixed_ws_records(ws, n);
+  // staged: the unsorted records are in the workspace's record area and the sort gathers them into
+  // `base` (plus the EOF marker); otherwise they are at `base` and are copied aside first
+  const uint8_t* src = staged ? recs : base;
+  hipLaunchKernelGGL(rs_extract_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, src, n, a);
   for (int pass = 0; pass < kPasses; ++pass) {
     hipLaunchKernelGGL(rs_hist_kernel, dim3((unsigned)ntiles), dim3(kThreads), 0, s, a, n, pass, hist, (int)ntiles);
     hipLaunchKernelGGL(rs_scan_kernel, dim3(kBins), dim3(kThreads), 0, s, hist, (int)ntiles, totals);
@@ -246,10 +260,10 @@ void launch_sort_fixed_run(uint8_t* base, int64_t n, void* ws, hipStream_t s) {
     b = t;
   }
   // kPasses is even: the sorted keys are back in the first buffer
-  (void)hipMemcpyAsync(recs, base, (size_t)(n * kTeraRecordBytes), hipMemcpyDeviceToDevice, s);
+  if (!staged) (void)hipMemcpyAsync(recs, base, (size_t)(n * kTeraRecordBytes), hipMemcpyDeviceToDevice, s);
   const int64_t words = n * kWords;
   hipLaunchKernelGGL(rs_gather_kernel, dim3((unsigned)((words + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
-                     reinterpret_cast<const uint64_t*>(recs), reinterpret_cast<uint64_t*>(base), a, n);
+                     reinterpret_cast<const uint64_t*>(recs), reinterpret_cast<uint64_t*>(base), a, n, staged ? 1 : 0);
 }
 
 }  // namespace gpu

@@ -633,7 +633,7 @@ PYBIND11_MODULE(_uda_native, m) {
   }, py::arg("runs"), py::arg("key_class"), py::arg("kv_buf") = 1 << 20, py::arg("device") = 0);
   // F8: sort TeraSort records (104-byte IFile records, no EOF marker) by their 10-byte key on the
   // device; returns (sorted bytes, device ms of the sort).
-  m.def("gpu_sort_fixed", [](py::buffer b, int device) {
+  m.def("gpu_sort_fixed", [](py::buffer b, int device, bool staged) {
     py::buffer_info v = b.request();
     const int64_t bytes = (int64_t)(v.size * v.itemsize);
     if (bytes % gpu::kTeraRecordBytes) throw py::value_error("not a whole number of 104-byte records");
@@ -647,18 +647,20 @@ PYBIND11_MODULE(_uda_native, m) {
       py::gil_scoped_release rel;
       HIP_CHECK(hipSetDevice(device));
       gpu::DeviceBuffer d, ws;
-      d.alloc((size_t)std::max<int64_t>(bytes, 16));
+      d.alloc((size_t)std::max<int64_t>(bytes + 2, 16));
       ws.alloc((size_t)gpu::sort_fixed_ws_bytes(std::max<int64_t>(n, 1)));
       hipStream_t s = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreate(&e0));
       HIP_CHECK(hipEventCreate(&e1));
-      if (bytes) HIP_CHECK(hipMemcpyAsync(d.as(), v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
-      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s);  // warm-up (first launch loads code)
-      if (bytes) HIP_CHECK(hipMemcpyAsync(d.as(), v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
+      // staged: input in the workspace's record area, sorted run gathered into d (+ EOF marker)
+      uint8_t* in = staged ? gpu::sort_fixed_ws_records(ws.as(), std::max<int64_t>(n, 1)) : d.as<uint8_t>();
+      if (bytes) HIP_CHECK(hipMemcpyAsync(in, v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
+      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s, staged);  // warm-up (first launch loads code)
+      if (bytes) HIP_CHECK(hipMemcpyAsync(in, v.ptr, (size_t)bytes, hipMemcpyHostToDevice, s));
       HIP_CHECK(hipEventRecord(e0, s));
-      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s);
+      gpu::launch_sort_fixed_run(d.as<uint8_t>(), n, ws.as(), s, staged);
       HIP_CHECK(hipGetLastError());
       HIP_CHECK(hipEventRecord(e1, s));
       if (bytes) HIP_CHECK(hipMemcpyAsync(PyBytes_AS_STRING(o), d.as(), (size_t)bytes, hipMemcpyDeviceToHost, s));
@@ -669,7 +671,7 @@ PYBIND11_MODULE(_uda_native, m) {
       (void)hipStreamDestroy(s);
     }
     return py::make_tuple(out, (double)ms);
-  }, py::arg("records"), py::arg("device") = 0);
+  }, py::arg("records"), py::arg("device") = 0, py::arg("staged") = false);
   // F6: decode Hadoop block-compressed streams on the device; returns (raw streams, blocks, decode_ms)
   m.def("gpu_block_decode", [](const std::string& codec_cls, const std::vector<std::string>& streams, int device) {
     bool unsup = false;

@@ -32,11 +32,14 @@ def _oracle(r):
     return r[order].tobytes()
 
 
+@pytest.mark.parametrize("staged", [False, True])
 @pytest.mark.parametrize("n,distinct", [(1, None), (2, None), (255, None), (4096, None), (4097, None),
                                         (100_003, None), (50_000, 3), (70_000, 1)])
-def test_sort_fixed_matches_stable_python_sort(require_gpu, native, n, distinct):
+def test_sort_fixed_matches_stable_python_sort(require_gpu, native, n, distinct, staged):
+    """staged=False: records sorted where they are; staged=True: the engine's map-sort layout (unsorted
+    records in the sort workspace, gathered sorted into the store)."""
     r = _records(n, seed=n, key_values=distinct)
-    out, ms = native.gpu_sort_fixed(r.tobytes())
+    out, ms = native.gpu_sort_fixed(r.tobytes(), staged=staged)
     assert out == _oracle(r)
     assert ms >= 0
 
