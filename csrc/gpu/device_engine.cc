@@ -446,6 +446,11 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   kd.bad_layout = flag_.as<int>();
   kd.cap = (int)cap;
   kd.threads = kw_threads_;
+  static const int xcd = [] {
+    const char* e = std::getenv("UDA_KWAY_XCD");  // default on: +0.5 % device-only (profiles/r2_kway_xcd_ab.md)
+    return e ? std::atoi(e) : 1;
+  }();
+  kd.xcd_swizzle = xcd;
   static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
   if (prof) {
     ensure(kw_prof_, (size_t)cell_first[G] * 5 * 8);

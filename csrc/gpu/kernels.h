@@ -153,6 +153,7 @@ struct KwayDesc {
   int cap = kKwCap;           // records per cell on the LDS path (kway_cap_supported)
   int threads = 256;          // workgroup size: 256 or 512
   unsigned long long* prof = nullptr;  // optional [cell][5] phase timestamps (UDA_KWAY_PROF)
+  int xcd_swizzle = 0;        // map consecutive cells to one XCD (workgroups are dealt round-robin over 8 XCDs)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

@@ -221,7 +221,14 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   __shared__ int64_t beg[kKwMaxRuns];
   __shared__ const uint8_t* rbase[kKwMaxRuns];
   __shared__ int64_t s_start;
-  const int64_t b = blockIdx.x;
+  // The dispatcher deals workgroups round-robin over the 8 XCDs (each with its own L2); with the
+  // swizzle, XCD x takes a contiguous block of cells, so neighbouring cells of a group (adjacent
+  // slices of the same runs, sharing the boundary record lines) meet in one L2.
+  int64_t b = blockIdx.x;
+  if (kd.xcd_swizzle) {
+    const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+    b = x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+  }
   // phase timestamps (tools only: kd.prof is null in production launches)
   auto stamp = [&](int k) {
     if (kd.prof && threadIdx.x == 0) kd.prof[b * 5 + k] = wall_clock64();
