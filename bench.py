@@ -55,6 +55,9 @@ def parse_args(argv=None):
     ap.add_argument("--replan", action="store_true",
                     help="recompute the cell splits (and re-exchange the slice counts) inside every timed "
                          "step instead of reusing the setup-time plan")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="--api with N ranks: every rank uses GPU 0 (rehearsal of the multi-rank API path on a "
+                         "one-GPU machine; the RCCL path cannot share a GPU)")
     ap.add_argument("--map-sort", action=argparse.BooleanOptionalAction, default=True,
                     help="setup generates unsorted TeraGen map input (uniform random keys) and sorts every "
                          "map-output partition on the device (F8 radix sort), like a map task's sort before "
@@ -135,9 +138,13 @@ def main(argv=None) -> int:
     if ctx.world != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
         return 2
-    torch.cuda.set_device(ctx.local_rank)
     if args.api:
+        torch.cuda.set_device(0 if args.one_gpu else ctx.local_rank)
         return run_api(args, ctx)
+    if args.one_gpu and ctx.world > 1:
+        print("bench: --one-gpu is for --api (RCCL refuses two ranks on one GPU)", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(ctx.local_rank)
 
     rounds = args.rounds
     if args.max_round_gb > 0:
@@ -249,73 +256,101 @@ def main(argv=None) -> int:
     return 0
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def run_api(args, ctx) -> int:
     """TeraSort through the C ABI: the same reduce-side work, entered the way the Hadoop plugins enter
-    it (csrc/gpu/api_bench.cc)."""
+    it (csrc/gpu/api_bench.cc). With N ranks every rank runs a MOFSupplier (TCP, its maps' outputs in
+    its HBM) and `--reducers` reduce tasks that fetch their partition of every rank's maps as device
+    descriptors (another rank's HBM is mapped over hipIpc, so the merge reads it over xGMI)."""
     import torch
 
     from uda_amd import native
     from uda_amd.models.terasort import RECORD_BYTES
-    if ctx.world != 1:
-        print("bench: --api runs on one GPU (cross-GPU providers are exercised by the RCCL path)", file=sys.stderr)
-        return 2
-    b = native().ApiTeraSortBench(dict(device=ctx.local_rank, maps=args.maps_per_gpu, reducers=args.reducers,
+    device = 0 if args.one_gpu else ctx.local_rank
+    world, rank, R = ctx.world, ctx.rank, args.reducers
+    # one provider per rank, all on one port at 127.0.0.<rank + 1> (providers of different hosts share the
+    # port in Hadoop; -r of every reduce task)
+    port = ctx.all_gather_object(_free_port() if rank == 0 else 0)[0] if world > 1 else 0
+    b = native().ApiTeraSortBench(dict(device=device, maps=args.maps_per_gpu, reducers=R,
                                        records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
-                                       round_bytes=args.round_mb << 20))
+                                       round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
+                                       transport="tcp" if world > 1 else "loopback",
+                                       bind_addr=f"127.0.0.{rank + 1}" if world > 1 else ""))
     t = time.perf_counter()
     b.setup()
-    print(f"# api setup {time.perf_counter() - t:.1f}s store={b.store_bytes/1e9:.1f}GB", file=sys.stderr, flush=True)
+    if world > 1:  # provider addresses and every task's expected record count (summed over the ranks' maps)
+        b.set_peers([f"127.0.0.{p + 1}" for p in range(world)])
+        parts = ctx.all_gather_object([int(x) for x in b.local_partition_records()])
+        total = [sum(pr[g] for pr in parts) for g in range(world * R)]
+        b.set_expected(total[rank * R:(rank + 1) * R])
+    if rank == 0:
+        print(f"# api setup {time.perf_counter() - t:.1f}s store={b.store_bytes/1e9:.1f}GB per rank, {world} rank(s)"
+              f"{' on one GPU (rehearsal)' if args.one_gpu and world > 1 else ''}", file=sys.stderr, flush=True)
     for i in range(args.warmup):
+        ctx.barrier()
         st = b.step(False)
-        if args.verbose:
+        if args.verbose and rank == 0:
             print(f"# warmup {i}: {json.dumps(st)}", file=sys.stderr, flush=True)
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stats = [b.step(False) for _ in range(args.steps)]
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    ctx.barrier()
+    elapsed = ctx.max_float(time.perf_counter() - t0)
     validated = None
     if not args.no_validate:
         vst = b.step(True)
-        validated = vst["order_errors"] == 0
-        if args.verbose:
+        validated = all(ctx.all_gather_object(vst["order_errors"] == 0))
+        if args.verbose and rank == 0:
             print(f"# validated step: {json.dumps(vst)}", file=sys.stderr, flush=True)
-    records = int(stats[0]["records"])
+    records = sum(ctx.all_gather_object(int(stats[0]["records"])))
     ms_per_step = elapsed * 1000.0 / max(1, args.steps)
     gbps = records * RECORD_BYTES / (ms_per_step / 1000.0) / 1e9
-    out = {
-        "metric": "TeraSort shuffle+merge GB/s whole-node",
-        "value": round(gbps, 3),
-        "unit": "GB/s",
-        "n_gpus": 1,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bytes",
-        "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
-        "config": {
-            "model": "terasort",
-            "global_batch": records,
-            "seq_len": RECORD_BYTES,
-            "parallelism": "dp1",
-            "rows_per_gpu": records,
-            "maps_per_gpu": args.maps_per_gpu,
-            "reducers_per_gpu": args.reducers,
-            "shuffle": "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
-                       "(descriptor fetch, merged in place)",
-            "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) per reduce task",
-        },
-        "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
-        "close_ms": round(sum(s["close_ms"] for s in stats) / len(stats), 2),
-        "buffers_per_step": int(stats[0]["buffers"]),
-        "task0_stats": json.loads(stats[0]["task0_stats"]) if stats[0]["task0_stats"] else None,
-        "validated": validated,
-        "reference_envelope_gbps_per_node": 5.0,
-    }
-    print(json.dumps(out), flush=True)
+    ctx.barrier()  # every rank's reduce tasks are done with the other ranks' providers
+    if rank == 0:
+        out = {
+            "metric": "TeraSort shuffle+merge GB/s whole-node",
+            "value": round(gbps, 3),
+            "unit": "GB/s",
+            "n_gpus": 1 if args.one_gpu else world,
+            "ranks": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bytes",
+            "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "config": {
+                "model": "terasort",
+                "global_batch": records,
+                "seq_len": RECORD_BYTES,
+                "parallelism": f"dp{world}",
+                "rows_per_gpu": args.rows_per_gpu,
+                "maps_per_gpu": args.maps_per_gpu,
+                "reducers_per_gpu": R,
+                "shuffle": "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
+                           "(descriptor fetch, merged in place" + ("; other ranks' MOFs mapped over hipIpc, "
+                                                                    "fetch control over TCP)" if world > 1 else ")"),
+                "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) per reduce task",
+            },
+            "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
+            "close_ms": round(sum(s["close_ms"] for s in stats) / len(stats), 2),
+            "buffers_per_step": int(stats[0]["buffers"]),
+            "task0_stats": json.loads(stats[0]["task0_stats"]) if stats[0]["task0_stats"] else None,
+            "validated": validated,
+            "reference_envelope_gbps_per_node": 5.0,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
     return 0
 
 

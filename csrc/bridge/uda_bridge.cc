@@ -84,6 +84,7 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
       uda::Supplier::Options so;
       so.transport = h->host->get_conf("mapred.uda.transport", "loopback");
       so.loopback_host = h->host->get_conf("mapred.uda.loopback.host", "*");
+      so.bind_addr = h->host->get_conf("mapred.uda.provider.bind.address", "");
       so.io_threads = (int)h->host->conf_i64("mapred.uda.provider.blocked.threads.per.disk", 4);
       so.workers = (int)h->host->conf_i64("mapred.uda.provider.workers", 8);
       so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);

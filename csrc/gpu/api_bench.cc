@@ -78,13 +78,14 @@ void log_cb(void*, const char* msg, int32_t sev) {
 
 ConfTable& bench_conf(const ApiBenchConfig& c) {
   static ConfTable t;
-  t.kv = {{"mapred.uda.transport", "loopback"},
+  t.kv = {{"mapred.uda.transport", c.transport},
           {"mapred.uda.loopback.host", "*"},
           {"mapred.uda.merge.backend", "gpu"},
           {"mapred.uda.gpu.fetch", "device"},
           {"mapred.uda.gpu.device", std::to_string(c.device)},
           {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
-          {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)}};
+          {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)},
+          {"mapred.uda.provider.bind.address", c.bind_addr}};
   return t;
 }
 
@@ -107,48 +108,64 @@ ApiTeraSortBench::~ApiTeraSortBench() {
 
 int64_t ApiTeraSortBench::store_bytes() const { return gen_ ? gen_->store_bytes() : 0; }
 
+std::vector<int64_t> ApiTeraSortBench::local_partition_records() const {
+  return gen_ ? gen_->local_dest_records() : std::vector<int64_t>();
+}
+
+std::string ApiTeraSortBench::map_id(int global_map) const {
+  char id[96];
+  std::snprintf(id, sizeof(id), "attempt_%s_m_%06d_0", cfg_.job.c_str() + 4, global_map);
+  return id;
+}
+
 void ApiTeraSortBench::setup() {
-  // map phase stand-in: `maps` MOFs x `reducers` total-order partitions in HBM
+  if (cfg_.world < 1 || cfg_.rank < 0 || cfg_.rank >= cfg_.world) throw std::runtime_error("api bench: bad rank/world");
+  if (cfg_.world > 1 && cfg_.transport != "tcp") throw std::runtime_error("api bench: world > 1 needs the tcp transport");
+  // map phase stand-in: `maps` MOFs x (world * reducers) total-order partitions in this rank's HBM
+  const int P = cfg_.world * cfg_.reducers;
   ShuffleConfig sc;
   sc.device = cfg_.device;
-  sc.world = cfg_.reducers;  // partitions per MOF (no exchange is ever run on this job)
-  sc.rank = 0;
+  sc.world = P;              // partitions per MOF (no exchange is ever run on this job)
+  sc.rank = cfg_.rank;       // seeds the rank's maps
   sc.maps_per_rank = cfg_.maps;
   sc.records_per_map = cfg_.records_per_map;
   sc.seed = cfg_.seed;
   sc.deliver_host = false;
   gen_.reset(new ShuffleJob(sc));
   gen_->generate();
-  expected_ = gen_->local_dest_records();
+  if (cfg_.world == 1) expected_ = gen_->local_dest_records();
   // MOFSupplier handle (TaskTracker / NodeManager side)
   ConfTable& conf = bench_conf(cfg_);
   uda_callbacks cb{};
   cb.ctx = &conf;
   cb.get_conf = conf_cb;
   cb.log = log_cb;
-  const std::vector<std::string> args = {"-w", "256", "-r", "9011", "-m", "1", "-g", "/tmp", "-s", "1024"};
+  const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
+                                         "-m", "1", "-g", "/tmp", "-s", "1024"};
   auto av = cargs(args);
   uda_handle* h = uda_start(0, (int)av.size(), av.data(), 2, 0, &cb);
   if (!h) throw std::runtime_error("api bench: uda_start (provider) failed");
   provider_ = h;
   map_ids_.clear();
   for (int m = 0; m < cfg_.maps; ++m) {
-    char id[96];
-    std::snprintf(id, sizeof(id), "attempt_%s_m_%06d_0", cfg_.job.c_str() + 4, m);
+    const std::string id = map_id(cfg_.rank * cfg_.maps + m);
     map_ids_.push_back(id);
     std::vector<int64_t> index;
-    for (int r = 0; r < cfg_.reducers; ++r) {
+    for (int r = 0; r < P; ++r) {
       const auto ir = gen_->index_record(m, r);
       index.insert(index.end(), ir.begin(), ir.end());
     }
-    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id, gen_->mof_device_ptr(m), gen_->mof_bytes(m),
-                                         index.data(), cfg_.reducers, cfg_.device) != 0)
+    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), gen_->mof_device_ptr(m), gen_->mof_bytes(m),
+                                         index.data(), P, cfg_.device) != 0)
       throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
   }
 }
 
 std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string* info) {
   const int R = cfg_.reducers;
+  const int W = cfg_.world;
+  if ((int)expected_.size() != R) throw std::runtime_error("api bench: expected record counts not set");
+  if (W > 1 && (int)peers_.size() != W) throw std::runtime_error("api bench: provider addresses not set");
   J2CSink sink(R, cfg_.kv_buf_bytes);
   sink.set_check_order(validate);
   ConfTable& conf = bench_conf(cfg_);
@@ -176,7 +193,8 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
       cb.get_conf = task_conf_cb;
       cb.failure = failure_cb;
       cb.log = log_cb;
-      const std::vector<std::string> args = {"-w", "256", "-r", "9011", "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"};
+      const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
+                                             "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"};
       auto av = cargs(args);
       uda_handle* h = uda_start(1, (int)av.size(), av.data(), 2, 0, &cb);
       handles[r] = h;
@@ -190,15 +208,21 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
         cv.notify_all();
       };
       if (!h) return fail("uda_start failed");
+      const int g = cfg_.rank * R + r;  // the job's reduce task index
       char rt[96];
-      std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, r);
-      const std::vector<std::string> init = {std::to_string(cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
+      std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, g);
+      const std::vector<std::string> init = {std::to_string(W * cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
                                              std::to_string(16 << 10), "org.apache.hadoop.io.Text", "null",
                                              std::to_string(256 << 10), "0", "0"};
       if (uda_do_command(h, form_cmd(kInitMsg, init).c_str()) != 0) return fail(uda_last_error(h));
-      for (int m = 0; m < cfg_.maps; ++m) {
-        const std::vector<std::string> f = {"localhost", cfg_.job, map_ids_[m], std::to_string(r)};
-        if (uda_do_command(h, form_cmd(kFetchMsg, f).c_str()) != 0) return fail(uda_last_error(h));
+      // rotating rank order: the tasks of rank d start with rank d + 1's maps, spreading the load
+      for (int k = 0; k < W; ++k) {
+        const int p = (cfg_.rank + 1 + k) % W;
+        const std::string host = W == 1 ? "localhost" : peers_[(size_t)p];
+        for (int m = 0; m < cfg_.maps; ++m) {
+          const std::vector<std::string> f = {host, cfg_.job, map_id(p * cfg_.maps + m), std::to_string(g)};
+          if (uda_do_command(h, form_cmd(kFetchMsg, f).c_str()) != 0) return fail(uda_last_error(h));
+        }
       }
     });
   }

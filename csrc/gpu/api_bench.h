@@ -1,6 +1,6 @@
 // TeraSort driven only through the UdaBridge C ABI (uda_start / INIT / FETCH / reduce_exit and the
 // dataFromUda callback), with HBM-resident map outputs: the integration the plugin layer uses,
-// measured end to end. One process, one GPU:
+// measured end to end. One process per GPU (world = 1: loopback transport inside the process):
 //   * map phase stand-in: `maps` MOFs with `reducers` total-order partitions each are generated in
 //     HBM (ShuffleJob's TeraGen kernel) and registered with a MOFSupplier handle as device MOFs;
 //   * one step = `reducers` reduce tasks, each its own NetMerger handle (one per ReduceTask JVM in
@@ -8,6 +8,12 @@
 //     in the provider's HBM (descriptor fetch) and streams whole-record buffers to dataFromUda;
 //   * dataFromUda is the J2C consumer (KVBuf copy + VInt walk, J2CSink), record counts per reducer
 //     are checked every step, key order as well when `validate`.
+// world > 1 (one process per GPU, the Hadoop node shape): every rank runs its own MOFSupplier on a
+// TCP port with its maps' outputs in its HBM, and `reducers` reduce tasks whose INIT names every
+// rank's maps; each task FETCHes its partition of every map from the rank that holds it. The
+// answers are device descriptors: a provider in another process is mapped with hipIpcOpenMemHandle
+// (peer access: on a multi-GPU node the merge reads the other GPUs' HBM over xGMI), so the map
+// outputs never cross PCIe and only the merged records go to the host.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -30,6 +36,11 @@ struct ApiBenchConfig {
   int64_t kv_buf_bytes = 1 << 20;
   int64_t round_bytes = 2ll << 30;   // mapred.uda.gpu.round.bytes of every reduce task
   std::string job = "job_202610160000_0001";
+  int rank = 0;                      // this process's rank (world > 1: one per GPU)
+  int world = 1;
+  int port = 0;                      // world > 1: the TCP port of every rank's MOFSupplier
+  std::string bind_addr;             // world > 1: this rank's provider address (127.0.0.<rank + 1>)
+  std::string transport = "loopback";
 };
 
 class ApiTeraSortBench {
@@ -42,6 +53,12 @@ class ApiTeraSortBench {
   std::map<std::string, double> step(bool validate, std::string* info = nullptr);
   std::vector<int64_t> expected_records() const { return expected_; }
   int64_t store_bytes() const;
+  // world > 1: records this rank's maps hold for each of the world * reducers reduce tasks (summed
+  // over the ranks by the caller), the expected counts of this rank's tasks, and every rank's
+  // provider address ("host:port", by rank).
+  std::vector<int64_t> local_partition_records() const;
+  void set_expected(const std::vector<int64_t>& e) { expected_ = e; }
+  void set_peers(const std::vector<std::string>& hosts) { peers_ = hosts; }
 
  private:
   ApiBenchConfig cfg_;
@@ -49,6 +66,8 @@ class ApiTeraSortBench {
   void* provider_ = nullptr;  // uda_handle*
   std::vector<int64_t> expected_;
   std::vector<std::string> map_ids_;
+  std::vector<std::string> peers_;
+  std::string map_id(int global_map) const;
 };
 
 }  // namespace gpu

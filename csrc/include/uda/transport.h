@@ -92,7 +92,9 @@ std::unique_ptr<ServerTransport> make_loopback_server(const std::string& host);
 
 // TCP backend. The server listens on `port` (0 = ephemeral); clients connect to host:port with
 // up to `credits` requests in flight per connection.
-std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits);
+// bind_addr: IPv4 listen address ("" = any). Several providers on one host (one per GPU) listen on
+// the same port at different addresses, as providers on different hosts do.
+std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr = std::string());
 std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits);
 
 // Fault injection for tests (env UDA_FAULT_FETCH=<n>: the n-th fetch fails; see uda/fault.h).

@@ -25,7 +25,7 @@ void Supplier::start() {
   }
   for (int i = 0; i < std::max(1, opt_.workers); ++i) workers_.emplace_back([this] { worker(); });
   if (opt_.transport == "tcp")
-    server_ = make_tcp_server(net_.data_port, net_.wqes_per_conn);
+    server_ = make_tcp_server(net_.data_port, net_.wqes_per_conn, opt_.bind_addr);
   else
     server_ = make_loopback_server(opt_.loopback_host);
   server_->start(this);

@@ -36,6 +36,7 @@ class Supplier : public DataServer {
     int max_open_files = 512;    // fd cache bound (rlimit analogue)
     std::string transport = "loopback";  // loopback | tcp
     std::string loopback_host = "*";
+    std::string bind_addr;       // tcp: listen address (mapred.uda.provider.bind.address; empty = any)
   };
   Supplier(const NetlevOptions& net, const Options& o, Host* host);
   ~Supplier() override;

@@ -772,6 +772,11 @@ PYBIND11_MODULE(_uda_native, m) {
         get("seed", c.seed);
         get("kv_buf_bytes", c.kv_buf_bytes);
         get("round_bytes", c.round_bytes);
+        get("rank", c.rank);
+        get("world", c.world);
+        get("port", c.port);
+        get("transport", c.transport);
+        get("bind_addr", c.bind_addr);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
@@ -790,6 +795,9 @@ PYBIND11_MODULE(_uda_native, m) {
            },
            py::arg("validate") = false)
       .def("expected_records", &gpu::ApiTeraSortBench::expected_records)
+      .def("local_partition_records", &gpu::ApiTeraSortBench::local_partition_records)
+      .def("set_expected", &gpu::ApiTeraSortBench::set_expected)
+      .def("set_peers", &gpu::ApiTeraSortBench::set_peers)
       .def_property_readonly("store_bytes", &gpu::ApiTeraSortBench::store_bytes);
 
   py::class_<gpu::ShuffleJob>(m, "ShuffleJob")

@@ -77,7 +77,8 @@ void tune(int fd) {
 // ------------------------------------------------------------------------------------ server
 class TcpServer : public ServerTransport {
  public:
-  TcpServer(int port, int credits) : port_(port), credits_(credits) {}
+  TcpServer(int port, int credits, const std::string& bind_addr)
+      : port_(port), credits_(credits), bind_addr_(bind_addr) {}
   ~TcpServer() override { stop(); }
 
   void start(DataServer* s) override {
@@ -89,9 +90,12 @@ class TcpServer : public ServerTransport {
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (!bind_addr_.empty() && inet_pton(AF_INET, bind_addr_.c_str(), &a.sin_addr) != 1)
+      throw std::runtime_error("bad provider bind address '" + bind_addr_ + "'");
     a.sin_port = htons((uint16_t)port_);
     if (::bind(lfd_, (sockaddr*)&a, sizeof(a)) != 0)
-      throw std::runtime_error("bind(" + std::to_string(port_) + ") failed: " + strerror(errno));
+      throw std::runtime_error("bind(" + (bind_addr_.empty() ? std::string("*") : bind_addr_) + ":" +
+                               std::to_string(port_) + ") failed: " + strerror(errno));
     if (::listen(lfd_, 128) != 0) throw std::runtime_error("listen failed");
     socklen_t len = sizeof(a);
     getsockname(lfd_, (sockaddr*)&a, &len);
@@ -184,6 +188,7 @@ class TcpServer : public ServerTransport {
   }
 
   int port_;
+  std::string bind_addr_;
   int credits_;
   int lfd_ = -1;
   std::atomic<bool> running_{false};
@@ -361,8 +366,8 @@ class TcpClient : public ClientTransport {
 };
 }  // namespace
 
-std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits) {
-  return std::make_unique<TcpServer>(port, credits > 0 ? credits : 256);
+std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr) {
+  return std::make_unique<TcpServer>(port, credits > 0 ? credits : 256, bind_addr);
 }
 std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits) {
   return std::make_unique<TcpClient>(default_port, credits);

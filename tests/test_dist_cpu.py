@@ -177,3 +177,35 @@ def test_bench_refuses_world_mismatch():
                          capture_output=True, text=True, env=env, timeout=300)
     assert out.returncode == 2
     assert "launcher started 1 rank" in out.stderr
+
+
+def test_tcp_providers_share_a_port_on_distinct_addresses():
+    """One provider per GPU on one node: each listens on the job's data port at its own loopback
+    address (mapred.uda.provider.bind.address), as providers of different hosts do; a reduce task
+    fetches each map from the provider that holds it."""
+    import socket
+
+    from uda_amd.bridge import UdaProvider
+    from uda_amd.utils.mof import encode_partitions
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    maps = datagen.secondary_sort(num_maps=6, reducers=2, rows_per_map=500, seed=23)
+    job = "job_bind_0001"
+    provs = [UdaProvider(conf={"mapred.uda.provider.bind.address": f"127.0.0.{k + 1}"}, transport="tcp",
+                         data_port=port) for k in range(2)]
+    try:
+        for i, parts in enumerate(datagen.streams(maps)):
+            data, index = encode_partitions(parts)
+            provs[i % 2].add_mof_memory(job, f"attempt_{job}_m_{i:06d}_0", data, index)
+        c = UdaConsumer(len(maps), job, f"attempt_{job}_r_000001_0", datagen.TEXT, transport="tcp", data_port=port)
+        for i in range(len(maps)):
+            c.fetch(f"127.0.0.{i % 2 + 1}", job, f"attempt_{job}_m_{i:06d}_0", 1)
+        recs = c.wait(60)
+        c.close()
+        kf = datagen.sort_key(datagen.TEXT)
+        want = sorted((kv for m in maps for kv in m[1]), key=kf)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+    finally:
+        for p in provs:
+            p.close()

@@ -156,3 +156,20 @@ def test_api_terasort_bench_small(require_gpu, native):
         if validate:
             assert st["order_errors"] == 0
         assert '"merge_path":"device-fixed10"' in st["task0_stats"]
+
+
+def test_api_bench_two_ranks_share_providers(require_gpu):
+    """`bench.py --api --gpus 2 --one-gpu`: two processes, each a MOFSupplier (TCP) with its maps in
+    HBM plus reduce tasks that fetch their partition of both ranks' maps as device descriptors (the
+    other rank's HBM mapped over hipIpc). Every task's record count is checked against the sum over
+    both ranks' maps, key order in the validated step."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--gpus", "2", "--one-gpu",
+                          "--steps", "1", "--warmup", "1", "--rows-per-gpu", "1800000", "--maps-per-gpu", "6",
+                          "--reducers", "3", "--round-mb", "16"],
+                         capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["ranks"] == 2 and res["validated"] is True
+    assert res["config"]["global_batch"] == 2 * 1_800_000
+    assert res["task0_stats"]["merge_path"] == "device-fixed10"
