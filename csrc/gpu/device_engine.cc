@@ -1,5 +1,6 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
+#include "device_ptr.h"
 #include "merge_plan.h"
 #include "sdma.h"
 #include "uda/fault.h"
@@ -584,7 +585,8 @@ void ShuffleJob::generate() {
     HIP_CHECK(hipHostGetDevicePointer(&dp, store_base_, 0));
     store_dev_base_ = reinterpret_cast<uint8_t*>(dp);
   } else {
-    store_.alloc((size_t)store_bytes_);
+    // the UdaBridge API path exports the store to other processes over hipIpc (device_ptr.h)
+    store_.alloc(ipc_safe_bytes((size_t)store_bytes_));
     store_base_ = store_dev_base_ = store_.as<uint8_t>();
   }
 

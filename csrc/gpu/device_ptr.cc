@@ -77,6 +77,12 @@ IpcExport ipc_export(const void* ptr) {
   return ex;
 }
 
+size_t ipc_safe_bytes(size_t bytes) {
+  const uint64_t r = (uint64_t)bytes & 0xFFFFFFFFull;
+  if (r < (1ull << 31)) return bytes;
+  return bytes + ((1ull << 32) - r) + (64ull << 20);  // remainder 64 MiB
+}
+
 std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc) {
   char head[96];
   std::snprintf(head, sizeof(head), "hbm@%d@%d@%llx@", device, (int)getpid(),

@@ -22,6 +22,12 @@ struct IpcExport {
   const uint8_t* base = nullptr;
 };
 IpcExport ipc_export(const void* ptr);
+// Size to allocate for a block that other processes will map over hipIpc. On the ROCm 7 / dmabuf IPC
+// path a block whose size modulo 2^32 lies in [2^31, 2^32) hangs the importing process in
+// hipIpcOpenMemHandle or its first access (2.1 and 3.0 GiB hang, 1.9 and 4.2 GiB map fine;
+// tools/ipc_size_probe.py, profiles/r2_ipc_size_probe.log), so such sizes are padded past the next
+// multiple of 2^32.
+size_t ipc_safe_bytes(size_t bytes);
 
 std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc);
 bool is_device_descriptor(const std::string& s);

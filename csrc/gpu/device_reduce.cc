@@ -1,6 +1,11 @@
 // Device merge-and-deliver of one reduce task over HBM-resident partitions. See device_reduce.h.
 #include "device_reduce.h"
 
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -162,6 +167,10 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
     max_round = std::max(max_round, round_recs[q]);
   }
   st.rounds = Q;
+  static const bool trace_rounds = std::getenv("UDA_DEVICE_REDUCE_TRACE") != nullptr;  // tools: progress lines
+  if (trace_rounds)
+    std::fprintf(stderr, "[device_reduce pid %d] planned %d runs x %d rounds, %lld records, max round %lld\n", (int)getpid(),
+                 K, Q, (long long)N, (long long)max_round);
   DeviceMerger merger(max_round, K);
   DeviceBuffer out[2];
   for (auto& o : out) o.alloc((size_t)std::max<int64_t>(max_round, 1) * kTeraRecordBytes);
@@ -230,7 +239,9 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
     const double a = now_ms();
     HIP_CHECK(hipEventSynchronize(merged.e[q % 2]));
     st.merge_wait_ms += now_ms() - a;
+    if (trace_rounds) std::fprintf(stderr, "[device_reduce pid %d] round %d merged\n", (int)getpid(), q);
     deliver_round(q);
+    if (trace_rounds) std::fprintf(stderr, "[device_reduce pid %d] round %d delivered\n", (int)getpid(), q);
   }
   if (merger.bad_layout()) throw std::runtime_error("device reduce: non-TeraSort record in a FIXED10 run");
   st.records = N;
