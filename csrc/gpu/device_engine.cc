@@ -52,7 +52,9 @@ void DeviceBuffer::alloc(size_t bytes) {
   reset();
   if (bytes == 0) return;
   if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
-  HIP_CHECK(hipMalloc(&ptr_, bytes));
+  // Blocks another process may map over hipIpc (our descriptor fetch, RCCL's peer registration of
+  // send/receive buffers) must stay out of the size range that hangs the importer (device_ptr.h).
+  HIP_CHECK(hipMalloc(&ptr_, ipc_safe_bytes(bytes)));
   size_ = bytes;
 }
 void DeviceBuffer::reset() {
@@ -585,8 +587,7 @@ void ShuffleJob::generate() {
     HIP_CHECK(hipHostGetDevicePointer(&dp, store_base_, 0));
     store_dev_base_ = reinterpret_cast<uint8_t*>(dp);
   } else {
-    // the UdaBridge API path exports the store to other processes over hipIpc (device_ptr.h)
-    store_.alloc(ipc_safe_bytes((size_t)store_bytes_));
+    store_.alloc((size_t)store_bytes_);  // padded for hipIpc export by DeviceBuffer::alloc
     store_base_ = store_dev_base_ = store_.as<uint8_t>();
   }
 
