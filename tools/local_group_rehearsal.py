@@ -17,9 +17,10 @@ ap.add_argument("--rows-per-rank", type=int, default=20_000_000)
 ap.add_argument("--reducers", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=16)
 ap.add_argument("--steps", type=int, default=2)
+ap.add_argument("--no-map-sort", action="store_true", help="generate sorted runs directly (bench --no-map-sort)")
 a = ap.parse_args()
 cfg = TeraSortConfig(rows_per_gpu=a.rows_per_rank, maps_per_rank=32, rounds=a.rounds, reducers=a.reducers,
-                     validate=True)
+                     validate=True, map_sort=not a.no_map_sort)
 t = time.perf_counter()
 jobs, ck, rec = make_local_group(a.world, cfg, group="rehearsal")
 setup = time.perf_counter() - t
