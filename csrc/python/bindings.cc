@@ -17,6 +17,7 @@
 
 #include "block_decoder.h"
 #include "device_engine.h"
+#include "device_ptr.h"
 #include "exchange.h"
 #include "api_bench.h"
 #include "generic_merger.h"
@@ -523,6 +524,7 @@ PYBIND11_MODULE(_uda_native, m) {
 
   // ---------------------------------------------------------------- GPU engine
   m.def("device_count", &gpu::device_count);
+  m.def("ipc_safe_bytes", [](uint64_t b) { return (uint64_t)gpu::ipc_safe_bytes((size_t)b); });
   // N8 device discovery: per-pair P2P reachability, link type (HSA_AMD_LINK_INFO_TYPE_*: 2 = xGMI) and
   // hop count, and the runtime's relative performance rank.
   m.def("device_topology", []() {

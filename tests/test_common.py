@@ -125,3 +125,17 @@ def test_topology_plan_and_peer_order():
             assert sorted(f for _, f in order) == sorted(set(range(w)) - {r})
     p = topology.shuffle_plan(8, 130 << 30)
     assert p["rounds"] >= 1 and p["bytes_per_round"] * p["rounds"] <= 130 << 30
+
+
+def test_ipc_safe_bytes_avoids_the_hanging_size_range(native):
+    """Blocks mapped by another process over hipIpc must not have size % 2^32 in [2^31, 2^32): that
+    range hangs the importer on this ROCm (tools/ipc_size_probe.py). Sizes outside it are unchanged."""
+    G = 1 << 30
+    for size in [1, 1 << 20, G, 2 * G - 1, 4 * G, 4 * G + G, 130 * 10**9]:
+        if (size % (4 * G)) < 2 * G:
+            assert native.ipc_safe_bytes(size) == size
+    for size in [2 * G, 2 * G + 1, 3 * G, 4 * G - 1, 8 * 10**9, 6 * G + 12345]:
+        padded = native.ipc_safe_bytes(size)
+        assert padded >= size
+        assert padded % (4 * G) < 2 * G
+        assert padded - size <= 2 * G + (64 << 20)
