@@ -55,6 +55,12 @@ def parse_args(argv=None):
     ap.add_argument("--replan", action="store_true",
                     help="recompute the cell splits (and re-exchange the slice counts) inside every timed "
                          "step instead of reusing the setup-time plan")
+    ap.add_argument("--api-host-mofs", action="store_true",
+                    help="--api: map outputs registered from host memory (fetched as bytes, staged to HBM)")
+    ap.add_argument("--api-fetch", choices=("device", "host", "auto"), default=None,
+                    help="--api: mapred.uda.gpu.fetch of the reduce tasks (default: device, host with --api-host-mofs)")
+    ap.add_argument("--api-gpu-slots", type=int, default=0,
+                    help="--api: mapred.uda.gpu.max.concurrent.merges (staged GPU merges admitted at once; 0: all)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="--api with N ranks: every rank uses GPU 0 (rehearsal of the multi-rank API path on a "
                          "one-GPU machine; the RCCL path cannot share a GPU)")
@@ -281,7 +287,9 @@ def run_api(args, ctx) -> int:
                                        records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
                                        round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
                                        transport="tcp" if world > 1 else "loopback",
-                                       bind_addr=f"127.0.0.{rank + 1}" if world > 1 else ""))
+                                       bind_addr=f"127.0.0.{rank + 1}" if world > 1 else "",
+                                       host_mofs=args.api_host_mofs, max_concurrent_merges=args.api_gpu_slots,
+                                       fetch=args.api_fetch or ("host" if args.api_host_mofs else "device")))
     t = time.perf_counter()
     b.setup()
     if world > 1:  # provider addresses and every task's expected record count (summed over the ranks' maps)
@@ -337,7 +345,10 @@ def run_api(args, ctx) -> int:
                 "rows_per_gpu": args.rows_per_gpu,
                 "maps_per_gpu": args.maps_per_gpu,
                 "reducers_per_gpu": R,
-                "shuffle": "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
+                "shuffle": ("UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, MOFs in host memory fetched "
+                            f"as bytes (mapred.uda.gpu.fetch={args.api_fetch or 'host'}), merged on the GPU")
+                           if args.api_host_mofs else
+                           "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
                            "(descriptor fetch, merged in place" + ("; other ranks' MOFs mapped over hipIpc, "
                                                                     "fetch control over TCP)" if world > 1 else ")"),
                 "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) per reduce task",

@@ -331,6 +331,63 @@ struct PoolLease {
   }
 };
 
+// Admission of staged GPU reduce tasks per device (mapred.uda.gpu.max.concurrent.merges = cap > 0).
+// Reduce tasks started together run their phases in lockstep: all fetch and copy to HBM at once (the
+// H2D direction of PCIe busy, D2H idle), then all merge, then all deliver (D2H busy, H2D idle). With
+// at most `cap` tasks admitted, in arrival order, a task's fetch and H2D overlap the merge and D2H of
+// the tasks ahead of it, so both PCIe directions stay busy. Tasks wait in FIFO order of arrival.
+class DeviceGate {
+ public:
+  static DeviceGate& get() {
+    static DeviceGate* g = new DeviceGate;  // never destroyed: reduce tasks may outlive static teardown
+    return *g;
+  }
+  // false if `stopped` became true while waiting
+  template <class Stop>
+  bool acquire(int device, int cap, Stop&& stopped) {
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev& d = devs_[device];
+    const uint64_t me = d.next_ticket++;
+    d.waiting.push_back(me);
+    for (;;) {
+      if (d.used < cap && d.waiting.front() == me) {
+        d.waiting.pop_front();
+        ++d.used;
+        cv_.notify_all();
+        return true;
+      }
+      if (stopped()) {
+        d.waiting.erase(std::find(d.waiting.begin(), d.waiting.end(), me));
+        cv_.notify_all();
+        return false;
+      }
+      cv_.wait_for(lk, std::chrono::milliseconds(20));
+    }
+  }
+  void release(int device) {
+    std::lock_guard<std::mutex> g(mu_);
+    --devs_[device].used;
+    cv_.notify_all();
+  }
+
+ private:
+  struct Dev {
+    int used = 0;
+    uint64_t next_ticket = 0;
+    std::deque<uint64_t> waiting;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int, Dev> devs_;
+};
+
+struct GateLease {
+  int device = -1;
+  ~GateLease() {
+    if (device >= 0) DeviceGate::get().release(device);
+  }
+};
+
 // on_round: deliver the merged output in key-range rounds while the device merges the next one
 // (GenericMerger::merge); time spent in it is not counted as device time.
 DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
@@ -501,6 +558,15 @@ void ReduceTask::merge_gpu() {
   const int maps = init_.num_maps;
   const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
   if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
+  GateLease gate;
+  if (const int cap = (int)host_->conf_i64("mapred.uda.gpu.max.concurrent.merges", 0); cap > 0) {
+    const auto w0 = std::chrono::steady_clock::now();
+    if (!DeviceGate::get().acquire(device, cap, [&] { return stop_.load(); }))
+      throw UdaError("reduce task stopped while waiting for a GPU merge slot");
+    gate.device = device;
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.gpu_gate_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  }
   const bool device_decode = codec_ != Codec::kNone && host_->conf_i64("mapred.uda.gpu.decompress", 1) != 0;
   const Codec fetch_codec = device_decode ? Codec::kNone : codec_;
   const Codec stage_codec = device_decode ? codec_ : Codec::kNone;

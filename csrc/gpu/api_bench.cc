@@ -81,11 +81,12 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
   t.kv = {{"mapred.uda.transport", c.transport},
           {"mapred.uda.loopback.host", "*"},
           {"mapred.uda.merge.backend", "gpu"},
-          {"mapred.uda.gpu.fetch", "device"},
+          {"mapred.uda.gpu.fetch", c.fetch},
           {"mapred.uda.gpu.device", std::to_string(c.device)},
           {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
           {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)},
-          {"mapred.uda.provider.bind.address", c.bind_addr}};
+          {"mapred.uda.provider.bind.address", c.bind_addr},
+          {"mapred.uda.gpu.max.concurrent.merges", std::to_string(c.max_concurrent_merges)}};
   return t;
 }
 
@@ -154,6 +155,15 @@ void ApiTeraSortBench::setup() {
     for (int r = 0; r < P; ++r) {
       const auto ir = gen_->index_record(m, r);
       index.insert(index.end(), ir.begin(), ir.end());
+    }
+    if (cfg_.host_mofs) {  // a map output in host memory (page cache / local disk stand-in)
+      host_mofs_.emplace_back((size_t)gen_->mof_bytes(m));
+      HIP_CHECK(hipMemcpy(host_mofs_.back().data(), gen_->mof_device_ptr(m), (size_t)gen_->mof_bytes(m),
+                          hipMemcpyDeviceToHost));
+      if (uda_provider_register_mof(h, cfg_.job.c_str(), id.c_str(), host_mofs_.back().data(), gen_->mof_bytes(m),
+                                    index.data(), P) != 0)
+        throw std::runtime_error(std::string("api bench: register_mof failed: ") + uda_last_error(h));
+      continue;
     }
     if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), gen_->mof_device_ptr(m), gen_->mof_bytes(m),
                                          index.data(), P, cfg_.device) != 0)

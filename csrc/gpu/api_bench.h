@@ -40,6 +40,9 @@ struct ApiBenchConfig {
   int world = 1;
   int port = 0;                      // world > 1: the TCP port of every rank's MOFSupplier
   std::string bind_addr;             // world > 1: this rank's provider address (127.0.0.<rank + 1>)
+  bool host_mofs = false;            // register the MOFs from host memory (fetched as bytes, staged to HBM)
+  std::string fetch = "device";      // mapred.uda.gpu.fetch of the reduce tasks: device | host | auto
+  int max_concurrent_merges = 0;     // mapred.uda.gpu.max.concurrent.merges (staged path; 0 = no limit)
   std::string transport = "loopback";
 };
 
@@ -67,6 +70,7 @@ class ApiTeraSortBench {
   std::vector<int64_t> expected_;
   std::vector<std::string> map_ids_;
   std::vector<std::string> peers_;
+  std::vector<std::vector<uint8_t>> host_mofs_;  // host_mofs: the MOFs' bytes in host memory
   std::string map_id(int global_map) const;
 };
 

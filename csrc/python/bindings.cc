@@ -779,6 +779,9 @@ PYBIND11_MODULE(_uda_native, m) {
         get("port", c.port);
         get("transport", c.transport);
         get("bind_addr", c.bind_addr);
+        get("host_mofs", c.host_mofs);
+        get("fetch", c.fetch);
+        get("max_concurrent_merges", c.max_concurrent_merges);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
