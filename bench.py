@@ -59,8 +59,9 @@ def parse_args(argv=None):
                     help="--api: map outputs registered from host memory (fetched as bytes, staged to HBM)")
     ap.add_argument("--api-fetch", choices=("device", "host", "auto"), default=None,
                     help="--api: mapred.uda.gpu.fetch of the reduce tasks (default: device, host with --api-host-mofs)")
-    ap.add_argument("--api-gpu-slots", type=int, default=0,
-                    help="--api: mapred.uda.gpu.max.concurrent.merges (staged GPU merges admitted at once; 0: all)")
+    ap.add_argument("--api-gpu-slots", type=int, default=-1,
+                    help="--api: mapred.uda.gpu.max.concurrent.merges (staged GPU merges admitted at once; 0: all; "
+                         "default: the native default, 6)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="--api with N ranks: every rank uses GPU 0 (rehearsal of the multi-rank API path on a "
                          "one-GPU machine; the RCCL path cannot share a GPU)")

@@ -85,8 +85,8 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
           {"mapred.uda.gpu.device", std::to_string(c.device)},
           {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
           {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)},
-          {"mapred.uda.provider.bind.address", c.bind_addr},
-          {"mapred.uda.gpu.max.concurrent.merges", std::to_string(c.max_concurrent_merges)}};
+          {"mapred.uda.provider.bind.address", c.bind_addr}};
+  if (c.max_concurrent_merges >= 0) t.kv["mapred.uda.gpu.max.concurrent.merges"] = std::to_string(c.max_concurrent_merges);
   return t;
 }
 

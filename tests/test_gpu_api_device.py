@@ -173,3 +173,20 @@ def test_api_bench_two_ranks_share_providers(require_gpu):
     assert res["ranks"] == 2 and res["validated"] is True
     assert res["config"]["global_batch"] == 2 * 1_800_000
     assert res["task0_stats"]["merge_path"] == "device-fixed10"
+
+
+@pytest.mark.parametrize("slots", [0, 1, 2, -1])
+def test_api_bench_host_mofs_gated(require_gpu, native, slots):
+    """Host-resident MOFs through the staged GPU path, with at most `slots` reduce tasks admitted to
+    the GPU at once (mapred.uda.gpu.max.concurrent.merges; 0 = no limit, -1 = default 6): every task completes with
+    its full, ordered partition."""
+    b = native.ApiTeraSortBench(dict(device=0, maps=6, reducers=4, records_per_map=20000, round_bytes=1 << 20,
+                                     host_mofs=True, fetch="host", max_concurrent_merges=slots))
+    b.setup()
+    st = b.step(True)
+    assert st["records"] == 6 * 20000
+    assert st["order_errors"] == 0
+    t0 = json.loads(st["task0_stats"])
+    assert t0["merge_path"] == "staged"
+    if slots == 0:
+        assert t0["gpu_gate_wait_ms"] == 0
