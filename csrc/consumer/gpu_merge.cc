@@ -564,6 +564,13 @@ void ReduceTask::merge_gpu() {
   // slots (profiles/r2_api_host_mofs_gate_sweep.md); nodes running <= 6 tasks per GPU are unaffected
   if (const int cap = (int)host_->conf_i64("mapred.uda.gpu.max.concurrent.merges", 6); cap > 0) {
     const auto w0 = std::chrono::steady_clock::now();
+    // A task asks for a slot only once every map has been announced (all FETCH commands in): a task
+    // still waiting for map outputs (reduce slow-start) must not hold a slot, and a host that feeds the
+    // tasks' FETCHes one task after another cannot deadlock against the gate.
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      while (!stop_ && !final_ && fetch_cmds_ < maps) cv_.wait_for(lk, std::chrono::milliseconds(50));
+    }
     if (!DeviceGate::get().acquire(device, cap, [&] { return stop_.load(); }))
       throw UdaError("reduce task stopped while waiting for a GPU merge slot");
     gate.device = device;

@@ -270,6 +270,10 @@ void ReduceTask::handle(const HadoopCmd& cmd) {
     case kFetchMsg: {
       FetchParams f;
       if (!parse_fetch_params(cmd, &f, &err)) throw ProtocolError(err);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        ++fetch_cmds_;
+      }
       if (!restored_tasks_.empty()) {
         // restored LPQs are matched by map *task*: a re-executed map (new attempt id) must not be
         // merged next to the LPQ that already holds its old attempt's records

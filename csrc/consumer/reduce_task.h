@@ -126,6 +126,7 @@ class ReduceTask {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<FetchParams> fetch_list_;
+  int fetch_cmds_ = 0;  // FETCH commands received (restored ones included), under mu_
   std::deque<std::shared_ptr<MofFetcher>> fetched_;  // first chunk arrived
   int free_pairs_ = 0;
   int total_count_ = 0;
