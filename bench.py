@@ -62,6 +62,8 @@ def parse_args(argv=None):
     ap.add_argument("--api-gpu-slots", type=int, default=-1,
                     help="--api: mapred.uda.gpu.max.concurrent.merges (staged GPU merges admitted at once; 0: all; "
                          "default: the native default, 6)")
+    ap.add_argument("--api-provider-workers", type=int, default=-1,
+                    help="--api: mapred.uda.provider.workers of the MOFSupplier (default 8)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="--api with N ranks: every rank uses GPU 0 (rehearsal of the multi-rank API path on a "
                          "one-GPU machine; the RCCL path cannot share a GPU)")
@@ -290,6 +292,7 @@ def run_api(args, ctx) -> int:
                                        transport="tcp" if world > 1 else "loopback",
                                        bind_addr=f"127.0.0.{rank + 1}" if world > 1 else "",
                                        host_mofs=args.api_host_mofs, max_concurrent_merges=args.api_gpu_slots,
+                                       provider_workers=args.api_provider_workers,
                                        fetch=args.api_fetch or ("host" if args.api_host_mofs else "device")))
     t = time.perf_counter()
     b.setup()

@@ -86,6 +86,7 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
           {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
           {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)},
           {"mapred.uda.provider.bind.address", c.bind_addr}};
+  if (c.provider_workers > 0) t.kv["mapred.uda.provider.workers"] = std::to_string(c.provider_workers);
   if (c.max_concurrent_merges >= 0) t.kv["mapred.uda.gpu.max.concurrent.merges"] = std::to_string(c.max_concurrent_merges);
   return t;
 }

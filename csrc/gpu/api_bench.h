@@ -42,6 +42,7 @@ struct ApiBenchConfig {
   std::string bind_addr;             // world > 1: this rank's provider address (127.0.0.<rank + 1>)
   bool host_mofs = false;            // register the MOFs from host memory (fetched as bytes, staged to HBM)
   std::string fetch = "device";      // mapred.uda.gpu.fetch of the reduce tasks: device | host | auto
+  int provider_workers = -1;         // mapred.uda.provider.workers (-1 = default)
   int max_concurrent_merges = -1;    // mapred.uda.gpu.max.concurrent.merges (staged path; 0 = no limit, -1 = default)
   std::string transport = "loopback";
 };

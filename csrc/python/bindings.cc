@@ -782,6 +782,7 @@ PYBIND11_MODULE(_uda_native, m) {
         get("host_mofs", c.host_mofs);
         get("fetch", c.fetch);
         get("max_concurrent_merges", c.max_concurrent_merges);
+        get("provider_workers", c.provider_workers);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
