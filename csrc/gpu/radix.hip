@@ -15,8 +15,10 @@
 //             input order) and ranks them inside the wave by an 8-bit ballot match: a lane's peers are
 //             the lanes whose digit equals its own, its rank the peers below it. Per-wave digit counts
 //             go through LDS so a key's slot = digit base + tile offset + earlier rounds + earlier
-//             waves + rank: stable, which LSD needs. Each round's keys are staged in LDS in digit order
-//             first, so the global stores of one digit's keys are consecutive addresses.
+//             waves + rank: stable, which LSD needs. The whole 4096-key tile is staged in LDS (64 KiB)
+//             in digit order before any store, so a digit's ~16 keys leave as one 256-byte run of
+//             addresses (staging one 256-key round at a time left ~1 key per digit per store and
+//             wrote 1.76x the key bytes to HBM: profiles/r2_radix_pmc.md).
 // Then a gather moves each 104-byte record once (13 lanes per record, 8-byte words).
 #include "kernels.h"
 
@@ -149,18 +151,26 @@ __global__ void __launch_bounds__(kThreads) rs_scan_kernel(uint32_t* __restrict_
 __global__ void __launch_bounds__(kThreads) rs_scatter_kernel(const SortKey* __restrict__ in, SortKey* __restrict__ out,
                                                               int64_t n, int pass, const uint32_t* __restrict__ hist,
                                                               const uint32_t* __restrict__ totals, int ntiles) {
-  __shared__ uint32_t gbase[kBins];        // global slot of the tile's first key of each digit
+  __shared__ uint32_t gbase[kBins];         // global slot of the tile's first key of each digit
+  __shared__ uint32_t tstart[kBins];        // the digit's first slot in the tile's LDS staging
+  __shared__ uint32_t run[kBins];           // keys of the digit staged by earlier rounds
   __shared__ uint32_t wcnt[kWaves][kBins];  // per-wave digit counts -> exclusive prefixes
-  __shared__ uint32_t lbase[kBins];        // the round's digit offsets inside the LDS staging
-  __shared__ SortKey stage[kThreads];
+  __shared__ SortKey stage[kTile];          // the whole tile in digit order
   __shared__ uint32_t tmp[kWaves];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, wave = t >> 6;
+  const int b = blockIdx.x;
   {
+    // the scan left hist[d][b] = keys of digit d in tiles before b; the tile's own count is the
+    // difference to the next tile (or to the digit total)
+    const uint32_t h = hist[(size_t)t * ntiles + b];
+    const uint32_t cnt = (b + 1 < ntiles ? hist[(size_t)t * ntiles + b + 1] : totals[t]) - h;
     uint32_t all;
     const uint32_t digit_off = block_exclusive_scan(totals[t], tmp, &all);
-    gbase[t] = digit_off + hist[(size_t)t * ntiles + blockIdx.x];
+    gbase[t] = digit_off + h;
+    tstart[t] = block_exclusive_scan(cnt, tmp, &all);
+    run[t] = 0;
   }
-  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t base = (int64_t)b * kTile;
   for (int k = 0; k < kItems; ++k) {
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) wcnt[w][t] = 0;
@@ -174,7 +184,7 @@ __global__ void __launch_bounds__(kThreads) rs_scatter_kernel(const SortKey* __r
     const uint32_t rank = (uint32_t)__popcll(peers & lanes_below());
     if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
     __syncthreads();
-    // thread t owns digit t: exclusive prefix over the waves, the round's count, its LDS offset
+    // thread t owns digit t: exclusive prefix over the waves and the round's count
     uint32_t s = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
@@ -182,26 +192,19 @@ __global__ void __launch_bounds__(kThreads) rs_scatter_kernel(const SortKey* __r
       wcnt[w][t] = s;
       s += c;
     }
-    uint32_t round_total;
-    const uint32_t loff = block_exclusive_scan(s, tmp, &round_total);
-    lbase[t] = loff;
     __syncthreads();
-    // stage the round's keys in digit order, then store them: a digit's keys are one address run
-    uint32_t slot = 0;
-    if (valid) {
-      slot = lbase[d] + wcnt[wave][d] + rank;
-      stage[slot] = key;
-    }
+    // (round, wave, lane) order is input order: the slot keeps the sort stable
+    if (valid) stage[tstart[d] + run[d] + wcnt[wave][d] + rank] = key;
     __syncthreads();
-    if ((uint32_t)t < round_total) {
-      const SortKey k2 = stage[t];
-      const uint32_t d2 = digit_of(k2, pass);
-      out[(size_t)gbase[d2] + (t - lbase[d2])] = k2;
-    }
-    __syncthreads();
-    gbase[t] += s;  // keys of digit t placed this round
-    (void)lane;
-    (void)slot;
+    run[t] += s;
+  }
+  __syncthreads();
+  // the tile's keys leave in digit order: a digit's keys (16 on average) are one run of addresses
+  const int nt = (int)min<int64_t>(kTile, n - base);
+  for (int x = t; x < nt; x += kThreads) {
+    const SortKey k2 = stage[x];
+    const uint32_t d2 = digit_of(k2, pass);
+    out[(size_t)gbase[d2] + (uint32_t)x - tstart[d2]] = k2;
   }
 }
 
