@@ -65,8 +65,12 @@ def parse_args(argv=None):
     ap.add_argument("--api-provider-workers", type=int, default=-1,
                     help="--api: mapred.uda.provider.workers of the MOFSupplier (default 8)")
     ap.add_argument("--one-gpu", action="store_true",
-                    help="--api with N ranks: every rank uses GPU 0 (rehearsal of the multi-rank API path on a "
-                         "one-GPU machine; the RCCL path cannot share a GPU)")
+                    help="N ranks, every rank on GPU 0: rehearsal of the multi-process path on a one-GPU machine "
+                         "(--exchange ipc or --api; RCCL refuses two ranks on one GPU)")
+    ap.add_argument("--exchange", choices=("ipc", "rccl"), default="ipc",
+                    help="N > 1: all-to-all-v backend of the shuffle rounds: 'ipc' (node-local shared-memory "
+                         "control plane, pull copies from the peers' HBM mapped over hipIpc; default) or 'rccl' "
+                         "(grouped ncclSend/ncclRecv)")
     ap.add_argument("--map-sort", action=argparse.BooleanOptionalAction, default=True,
                     help="setup generates unsorted TeraGen map input (uniform random keys) and sorts every "
                          "map-output partition on the device (F8 radix sort), like a map task's sort before "
@@ -150,10 +154,11 @@ def main(argv=None) -> int:
     if args.api:
         torch.cuda.set_device(0 if args.one_gpu else ctx.local_rank)
         return run_api(args, ctx)
-    if args.one_gpu and ctx.world > 1:
-        print("bench: --one-gpu is for --api (RCCL refuses two ranks on one GPU)", file=sys.stderr)
+    if args.one_gpu and ctx.world > 1 and args.exchange == "rccl":
+        print("bench: --one-gpu needs --exchange ipc (RCCL refuses two ranks on one GPU)", file=sys.stderr)
         return 2
-    torch.cuda.set_device(ctx.local_rank)
+    device = 0 if args.one_gpu else ctx.local_rank
+    torch.cuda.set_device(device)
 
     rounds = args.rounds
     if args.max_round_gb > 0:
@@ -163,8 +168,8 @@ def main(argv=None) -> int:
                          local_dirs=args.local_dirs,
                          d2h_piece_bytes=args.d2h_piece_mb << 20, pinned_slots=args.pinned_slots,
                          d2h_engines=args.d2h_engines, deliver_host=not args.device_only,
-                         replan=args.replan, map_sort=args.map_sort)
-    job = TeraSortShuffle(ctx, cfg)
+                         replan=args.replan, map_sort=args.map_sort, exchange=args.exchange)
+    job = TeraSortShuffle(ctx, cfg, device=device)
     t_setup = time.perf_counter()
     job.setup()
     if args.sink == "none":
@@ -198,11 +203,13 @@ def main(argv=None) -> int:
         job.check(st)  # consumer record counts / framing / EOF of every timed step
 
     validated = None
+    exchange_errors = None
     if not args.no_validate:
         vst = job.step(validate=True)
-        job.check(vst)
-        ok = ctx.all_gather_object(True)
-        validated = all(ok)
+        job.check(vst)  # raises on order / checksum / exchange-checksum errors
+        ok = ctx.all_gather_object(int(vst["exchange_errors"]))
+        exchange_errors = sum(ok)
+        validated = exchange_errors == 0
         if args.verbose and ctx.rank == 0:
             print(f"# validated step: {json.dumps(vst)}", file=sys.stderr, flush=True)
 
@@ -218,7 +225,8 @@ def main(argv=None) -> int:
             "metric": "TeraSort shuffle+merge GB/s whole-node",
             "value": round(gbps, 3),
             "unit": "GB/s",
-            "n_gpus": ctx.world,
+            "n_gpus": 1 if args.one_gpu else ctx.world,
+            "ranks": ctx.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -236,7 +244,8 @@ def main(argv=None) -> int:
                 "model": "terasort",
                 "global_batch": int(args.rows_per_gpu) * ctx.world,
                 "seq_len": RECORD_BYTES,
-                "parallelism": f"dp{ctx.world}",
+                "parallelism": f"dp{ctx.world}" + (" (ranks share GPU 0: rehearsal)" if args.one_gpu and ctx.world > 1
+                                                    else ""),
                 "rows_per_gpu": args.rows_per_gpu,
                 "total_rows": args.rows_per_gpu * ctx.world,
                 "maps_per_gpu": args.maps_per_gpu,
@@ -250,14 +259,16 @@ def main(argv=None) -> int:
             },
             "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
             "teragen_gbps": round(gbps * 100 / RECORD_BYTES, 3),
-            "rccl_ranks": comm_ranks,
+            "exchange": job.job.exchange_name if ctx.world > 1 else None,
+            "comm_ranks": comm_ranks,
             "bytes_sent_per_rank": sent,
             "breakdown_ms_rank0": {k: round(mean(k), 2) for k in ("plan_ms", "comm_ms", "merge_ms", "d2h_ms",
-                                                                  "wait_out_ms")},
+                                                                  "wait_out_ms", "stage_ms")},
             "replan_in_step": bool(args.replan),
             "merge_passes": stats[0]["merge_passes"],
             "buffers_per_step": stats[0]["buffers"],
             "validated": validated,
+            "exchange_errors": exchange_errors,
             "reference_envelope_gbps_per_node": 5.0,
         }
         print(json.dumps(out), flush=True)

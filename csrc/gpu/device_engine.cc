@@ -497,8 +497,10 @@ ShuffleJob::ShuffleJob(const ShuffleConfig& cfg) : cfg_(cfg) {
   piece_bytes_ = std::max<int64_t>(1, cfg_.d2h_piece_bytes / buf_bytes) * buf_bytes;
   merged_ev_.resize(kSlots);
   comm_ev_.resize(kSlots);
+  sent_ev_.resize(2);
   for (auto& e : merged_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : comm_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : sent_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
 ShuffleJob::~ShuffleJob() {
@@ -514,6 +516,7 @@ ShuffleJob::~ShuffleJob() {
   for (auto e : merged_ev_) (void)hipEventDestroy(e);
   if (s_stage_) (void)hipStreamDestroy(s_stage_);
   for (auto e : comm_ev_) (void)hipEventDestroy(e);
+  for (auto e : sent_ev_) (void)hipEventDestroy(e);
   for (auto e : piece_ev_) (void)hipEventDestroy(e);
   if (!sdma_ && ring_) (void)hipHostFree(ring_);
   if (sdma_) {
@@ -537,10 +540,14 @@ void ShuffleJob::init_comm(const std::string& uid) {
 void ShuffleJob::init_local() {
   if (cfg_.world == 1) return;
   if (cfg_.local_group.empty()) throw std::runtime_error("init_local: config.local_group is empty");
-  if (disk_store())  // peers would pull from a staging buffer this rank reuses next round
-    throw std::runtime_error("init_local: the disk store needs the RCCL exchange (one process per GPU)");
   HIP_CHECK(hipSetDevice(cfg_.device));
   exchange_ = make_local_exchange(cfg_.local_group, cfg_.rank, cfg_.world);
+}
+
+void ShuffleJob::init_ipc(const std::string& name) {
+  if (cfg_.world == 1) return;
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  exchange_ = make_ipc_exchange(name, cfg_.rank, cfg_.world, cfg_.device);
 }
 
 std::string ShuffleJob::delivery_name() const {
@@ -943,9 +950,40 @@ void ShuffleJob::compute_plans() {
     recv_slots_.resize(kSlots);
     for (auto& b : recv_slots_) b.alloc((size_t)std::max<int64_t>(max_slot_bytes, 16));
   }
-  if (W > 1 && spilled() && std::string(exchange_->name()).rfind("rccl", 0) == 0)
-    send_staging_.alloc((size_t)std::max<int64_t>(max_send, 16));
+  // spill tiers at world > 1: peers never read the host store (device memory only, for every
+  // exchange backend); the round's outgoing slices are staged into HBM, double-buffered so the
+  // staging of round q+1 overlaps the exchange of round q
+  for (auto& b : send_staging_) b.reset();
+  if (W > 1 && spilled())
+    for (auto& b : send_staging_) b.alloc((size_t)std::max<int64_t>(max_send, 16));
   if (W > 1) exchange_->reserve(max_send);
+  for (int q = 0; q < Q_; ++q) {
+    RoundPlan& rp = plans_[q];
+    rp.staged_send.assign(W, {});
+    rp.staged_recv.assign(W, {});
+    if (W == 1 || !spilled()) continue;
+    int64_t off = 0;
+    for (int p = 0; p < W; ++p) {
+      const int64_t beg = off;
+      for (const Span& sp : rp.send[p]) off += sp.bytes;
+      if (off > beg) rp.staged_send[p].push_back(Span{send_staging_[q & 1].as<uint8_t>() + beg, off - beg});
+    }
+    uint8_t* rbuf = recv_slots_[q % kSlots].as<uint8_t>();
+    for (int s = 0; s < W; ++s) {
+      if (s == me) continue;
+      int64_t first = -1, total = 0;
+      for (int i = 0; i < R_; ++i)
+        for (int j = 0; j < M; ++j) {
+          const size_t x = ((size_t)s * R_ + i) * M + j;
+          const int64_t b = rp.recv_cnt[x] * kTeraRecordBytes;
+          if (b <= 0) continue;
+          if (first < 0) first = rp.recv_off[x];
+          if (rp.recv_off[x] != first + total) throw std::runtime_error("plan: a source's slices are not contiguous");
+          total += b;
+        }
+      if (total > 0) rp.staged_recv[s].push_back(Span{rbuf + first, total});
+    }
+  }
   d_validate_.alloc(64 + (size_t)2 * R_ * sizeof(Elem));
   // exchange verification tables
   d_verify_runs_.clear();
@@ -992,11 +1030,12 @@ void ShuffleJob::compute_plans() {
           const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
           v.push_back(CopyDesc{store_dev_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
         }
-      if (W > 1 && send_staging_.size() > 0) {
+      if (W > 1) {  // outgoing slices into the round's send staging (same layout as staged_send)
         int64_t off = 0;
         for (int p2 = 0; p2 < W; ++p2)
           for (const Span& sp : rp.send[p2]) {
-            v.push_back(CopyDesc{store_dev_base_ + (sp.ptr - store_base_), send_staging_.as<uint8_t>() + off, sp.bytes});
+            v.push_back(CopyDesc{store_dev_base_ + (sp.ptr - store_base_), send_staging_[q & 1].as<uint8_t>() + off,
+                                 sp.bytes});
             off += sp.bytes;
           }
       }
@@ -1253,7 +1292,6 @@ StepStats ShuffleJob::run_step(bool validate) {
   Elem* vlast = vprev + R_;
   std::vector<bool> has_prev(R_, false);
   if (validate) HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 64, s_compute_));
-  const bool rccl_staging = send_staging_.size() > 0;
   if (cfg_.replan) {
     const double tp = now_ms();
     refresh_plan();
@@ -1272,17 +1310,21 @@ StepStats ShuffleJob::run_step(bool validate) {
     if (stop_) throw std::runtime_error("delivery pipeline failed: " + step_error_msg_);
   };
 
-  // Pinned-DRAM tier, one rank: a staging thread copies each round's own cells into its receive
-  // slot on an SDMA engine of its own, as soon as the slot's previous merge has finished. A copy
-  // kernel (or hipMemcpyAsync, which runs as one) reading host memory stalls the merge kernels
-  // running beside it in the CU memory pipeline; on the copy engines, staging overlaps delivery
-  // (the link's two directions) and the merge. The round loop waits for staged_round[q] instead of
-  // a stream dependency.
-  // The disk tier stages from the same thread (io_uring reads into the pinned chunk ring, then H2D on
-  // a stream of its own), so the round loop is never blocked in disk reads.
-  const bool sdma_stage = W == 1 && ((host_store() && sdma_h2d_) || disk_store());
+  // Spill tiers (pinned DRAM, disk): a staging thread fills each round's HBM buffers ahead of the
+  // round loop: the own cells into the receive slot and, at world > 1, the outgoing slices into the
+  // round's send staging (peers only ever read device memory). Pinned DRAM is copied on an SDMA
+  // engine of its own: a copy kernel (or hipMemcpyAsync, which runs as one) reading host memory
+  // stalls the merge kernels beside it in the CU memory pipeline, while on the copy engines staging
+  // overlaps delivery (the link's other direction) and the merge. The disk tier reads through
+  // io_uring into the pinned chunk ring and copies to HBM on a stream of its own. Before reusing a
+  // receive slot the thread waits for the merge that read it; before reusing a send staging parity,
+  // for the exchange that sent it and for the peers' copies (Exchange::wait_sent). The round loop
+  // waits for staged_round[q] instead of a stream dependency, then enqueues the exchange.
+  const bool staged_send = W > 1 && spilled();
+  const bool sdma_stage = spilled() && (disk_store() || (host_store() && sdma_h2d_));
   if (sdma_stage && disk_store() && !s_stage_) HIP_CHECK(hipStreamCreateWithFlags(&s_stage_, hipStreamNonBlocking));
-  std::vector<char> staged_round(Q_, 0), merge_recorded(Q_, 0);
+  const int64_t xbase = xseq_;  // sequence number of this step's first exchange
+  std::vector<char> staged_round(Q_, 0), merge_recorded(Q_, 0), xchg_recorded(Q_, 0);
   double stage_ms = 0;
   std::thread stage_thr;
   if (sdma_stage)
@@ -1292,6 +1334,13 @@ StepStats ShuffleJob::run_step(bool validate) {
         SdmaEngine* eng = host_store() ? &SdmaEngine::for_device(cfg_.device) : nullptr;
         hsa_signal_t sig{};
         if (eng) sig = eng->make_signal();
+        struct SigGuard {
+          SdmaEngine* e;
+          hsa_signal_t s;
+          ~SigGuard() {
+            if (e) e->destroy_signal(s);
+          }
+        } sig_guard{eng, sig};
         for (int q = 0; q < Q_; ++q) {
           const int slot = q % kSlots;
           if (q >= kSlots) {
@@ -1302,22 +1351,44 @@ StepStats ShuffleJob::run_step(bool validate) {
             }
             HIP_CHECK(hipEventSynchronize(merged_ev_[slot]));  // the slot's previous round is merged
           }
+          if (staged_send && q >= 2) {  // send staging parity q & 1 was sent by exchange q-2
+            {
+              std::unique_lock<std::mutex> lk(mu_);
+              cv_.wait(lk, [&] { return xchg_recorded[q - 2] != 0 || stop_; });
+              if (stop_) break;
+            }
+            HIP_CHECK(hipEventSynchronize(sent_ev_[q & 1]));
+            exchange_->wait_sent(xbase + q - 2);
+          }
           const double ts = now_ms();
           const RoundPlan& rp = plans_[q];
           uint8_t* rbuf = recv_slots_[slot].as<uint8_t>();
           std::vector<CopyDesc> pieces;
           std::vector<DiskStore::Piece> dpieces;
+          auto add = [&](int m, int64_t at, int64_t bytes, uint8_t* dst) {  // at: store offset of the bytes
+            if (eng)
+              pieces.push_back(CopyDesc{store_base_ + at, dst, bytes});
+            else
+              dpieces.push_back(DiskStore::Piece{m, at - mof_off_[m], bytes, dst});
+          };
           for (int i = 0; i < R_; ++i)
             for (int j = 0; j < M; ++j) {
               const size_t x = ((size_t)me * R_ + i) * M + j;
               const int64_t cnt = rp.recv_cnt[x];
               if (cnt <= 0) continue;
-              const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
-              if (eng)
-                pieces.push_back(CopyDesc{store_base_ + at, rbuf + rp.recv_off[x], cnt * kTeraRecordBytes});
-              else
-                dpieces.push_back(DiskStore::Piece{j, at - mof_off_[j], cnt * kTeraRecordBytes, rbuf + rp.recv_off[x]});
+              add(j, run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes, cnt * kTeraRecordBytes,
+                  rbuf + rp.recv_off[x]);
             }
+          if (staged_send) {
+            int64_t off = 0;
+            for (int p = 0; p < W; ++p)
+              for (const Span& sp : rp.send[p]) {  // span pointers are store_base_ + store offset
+                const int64_t at = (int64_t)(sp.ptr - store_base_);
+                const int m = (int)(std::upper_bound(mof_off_.begin(), mof_off_.end(), at) - mof_off_.begin()) - 1;
+                add(m, at, sp.bytes, send_staging_[q & 1].as<uint8_t>() + off);
+                off += sp.bytes;
+              }
+          }
           if (eng) {
             SdmaEngine::arm(sig, (int64_t)pieces.size());
             for (const CopyDesc& d : pieces) eng->copy_h2d(d.dst, d.src, (size_t)d.bytes, sig);
@@ -1331,7 +1402,6 @@ StepStats ShuffleJob::run_step(bool validate) {
           stage_ms += now_ms() - ts;
           cv_.notify_all();
         }
-        if (eng) eng->destroy_signal(sig);
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(mu_);
         if (!stop_) step_error_msg_ = std::string("H2D staging: ") + e.what();
@@ -1360,63 +1430,40 @@ StepStats ShuffleJob::run_step(bool validate) {
     const int slot = q % kSlots;
     const RoundPlan& rp = plans_[q];
     uint8_t* rbuf = staged() ? recv_slots_[slot].as<uint8_t>() : nullptr;
-    if (sdma_stage) {
+    if (spilled())
       for (int i = 0; i < R_; ++i)
         for (int j = 0; j < M; ++j) st.bytes_h2d += rp.recv_cnt[((size_t)me * R_ + i) * M + j] * kTeraRecordBytes;
-      HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
-      HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
-      wait_until([&] { return staged_round[q] != 0; });
-    } else if (staged()) {
+    if (staged_send) st.bytes_h2d += rp.send_bytes;
+    if (sdma_stage) wait_until([&] { return staged_round[q] != 0; });
+    if (staged()) {
       if (q >= kSlots) HIP_CHECK(hipStreamWaitEvent(s_comm_, merged_ev_[slot], 0));  // slot consumed
       HIP_CHECK(hipEventRecord(ev[4 * q + 0], s_comm_));
-      if (spilled()) {  // spill tiers: this round's own cells stream into the slot (SDMA H2D)
-        std::vector<DiskStore::Piece> pieces;
-        for (int i = 0; i < R_; ++i)
-          for (int j = 0; j < M; ++j) {
-            const size_t x = ((size_t)me * R_ + i) * M + j;
-            const int64_t cnt = rp.recv_cnt[x];
-            if (cnt <= 0) continue;
-            const int64_t at = run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
-            if (disk_store())
-              pieces.push_back(DiskStore::Piece{j, at - mof_off_[j], cnt * kTeraRecordBytes, rbuf + rp.recv_off[x]});
-            st.bytes_h2d += cnt * kTeraRecordBytes;
-          }
-        if (!pieces.empty()) disk_->stage(pieces, s_comm_);  // io_uring reads overlap the merge of q-1
-        if (host_store())  // own cells (and, for W > 1, the outgoing slices) in one launch
-          launch_batched_copy(h2d_descs_[q].as<CopyDesc>(), h2d_n_[q], h2d_max_[q], s_comm_, h2d_blocks_);
+      if (spilled() && !sdma_stage) {  // pinned DRAM, copy-kernel staging (UDA_H2D_SDMA=0)
+        if (staged_send && q >= 2) exchange_->wait_sent(xbase + q - 2);  // peers done with this parity
+        launch_batched_copy(h2d_descs_[q].as<CopyDesc>(), h2d_n_[q], h2d_max_[q], s_comm_, h2d_blocks_);
       }
       if (W > 1) {
-        std::vector<std::vector<Span>> recv(W);
-        for (int s = 0; s < W; ++s) {
-          if (s == me) continue;
-          for (int i = 0; i < R_; ++i)
-            for (int j = 0; j < M; ++j) {
-              const size_t x = ((size_t)s * R_ + i) * M + j;
-              if (rp.recv_cnt[x] > 0) recv[s].push_back(Span{rbuf + rp.recv_off[x], rp.recv_cnt[x] * kTeraRecordBytes});
-            }
-        }
-        if (rccl_staging) {  // spill tier over RCCL: stage outgoing slices per peer, one message each
-          std::vector<std::vector<Span>> send(W);
-          std::vector<DiskStore::Piece> pieces;
-          int64_t off = 0;
-          for (int p = 0; p < W; ++p) {
-            const int64_t beg = off;
-            for (const Span& sp : rp.send[p]) {
-              if (disk_store()) {  // the span holds the store offset of the slice
-                const int64_t at = (int64_t)(uintptr_t)sp.ptr;
-                const int m = (int)(std::upper_bound(mof_off_.begin(), mof_off_.end(), at) - mof_off_.begin()) - 1;
-                pieces.push_back(DiskStore::Piece{m, at - mof_off_[m], sp.bytes, send_staging_.as<uint8_t>() + off});
-              }  // pinned DRAM: copied by the round's batched-copy launch above
-              off += sp.bytes;
-            }
-            if (off > beg) send[p].push_back(Span{send_staging_.as<uint8_t>() + beg, off - beg});
-          }
-          if (!pieces.empty()) disk_->stage(pieces, s_comm_);
-          st.bytes_h2d += off;
-          exchange_->exchange(send, recv, s_comm_);
+        if (staged_send) {
+          exchange_->exchange(rp.staged_send, rp.staged_recv, s_comm_);
         } else {
+          std::vector<std::vector<Span>> recv(W);
+          for (int s = 0; s < W; ++s) {
+            if (s == me) continue;
+            for (int i = 0; i < R_; ++i)
+              for (int j = 0; j < M; ++j) {
+                const size_t x = ((size_t)s * R_ + i) * M + j;
+                if (rp.recv_cnt[x] > 0) recv[s].push_back(Span{rbuf + rp.recv_off[x], rp.recv_cnt[x] * kTeraRecordBytes});
+              }
+          }
           exchange_->exchange(rp.send, recv, s_comm_);
         }
+        ++xseq_;
+        HIP_CHECK(hipEventRecord(sent_ev_[q & 1], s_comm_));
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          xchg_recorded[q] = 1;
+        }
+        cv_.notify_all();
         st.bytes_sent += rp.send_bytes;
       }
       HIP_CHECK(hipEventRecord(ev[4 * q + 1], s_comm_));
@@ -1496,11 +1543,13 @@ StepStats ShuffleJob::run_step(bool validate) {
   HIP_CHECK(hipStreamSynchronize(s_comm_));
   HIP_CHECK(hipStreamSynchronize(s_copy_));
   if (stage_thr.joinable()) stage_thr.join();
+  // every rank's pulls from this rank's memory are done before any rank reuses or frees it
+  if (exchange_) exchange_->quiesce();
   st.wall_ms = now_ms() - t0;
-  if (sdma_stage) st.comm_ms = stage_ms;
+  st.stage_ms = stage_ms;
   for (int q = 0; q < Q_; ++q) {
     float a = 0, b = 0;
-    if (staged() && !sdma_stage && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
+    if (staged() && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
     if (hipEventElapsedTime(&b, ev[4 * q + 2], ev[4 * q + 3]) == hipSuccess) st.merge_ms += b;
   }
   static const bool round_trace = std::getenv("UDA_ROUND_TRACE") != nullptr;  // tools: per-round timeline

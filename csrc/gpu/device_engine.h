@@ -225,6 +225,7 @@ struct StepStats {
   double d2h_ms = 0;           // host time the delivery copies were outstanding (summed per piece)
   double wait_out_ms = 0;      // host time the merge waited for a free output slot (D2H-bound)
   double plan_ms = 0;          // replan: cell splits + counts exchange inside the step
+  double stage_ms = 0;         // spill tiers: host time of the staging thread's rounds (H2D / disk reads)
   int64_t bytes_in = 0;        // partition bytes delivered to this GPU's reducers (records only)
   int64_t records = 0;
   int64_t bytes_sent = 0;      // bytes this rank sent to peers (excl. self)
@@ -248,6 +249,9 @@ class ShuffleJob {
   void init_comm(const std::string& uid);
   // Single-process rehearsal: ranks are threads sharing this device (config.local_group).
   void init_local();
+  // One process per rank on one node (several may share a GPU): shared-memory control plane named
+  // `name` (agreed by all ranks) + pull copies from the peers' HBM mapped over hipIpc. Collective.
+  void init_ipc(const std::string& name);
   // Map phase stand-in: generate maps_per_rank TeraSort MOFs into the partition store.
   void generate();
   // Every `every`-th key of every local run, grouped by destination GPU:
@@ -298,6 +302,10 @@ class ShuffleJob {
     std::vector<int64_t> self_beg;     // [i*M + m] first record of my own cell (i, q) in run (m, me)
     std::vector<int64_t> group_recs;   // records per reducer this round
     int64_t recv_records = 0;
+    // spill tiers, world > 1: the outgoing slices are staged into HBM, one contiguous region per
+    // peer (send staging of parity q & 1), and travel as one message per peer; the receive side
+    // takes them as one span per source (its slices from a source are contiguous in the slot)
+    std::vector<std::vector<Span>> staged_send, staged_recv;
   };
   void compute_plans();
   void copy_loop();
@@ -335,8 +343,11 @@ class ShuffleJob {
   std::vector<RoundPlan> plans_;
   int64_t max_round_records_ = 0;
   std::vector<DeviceBuffer> recv_slots_, out_slots_;
-  DeviceBuffer send_staging_;  // host store + RCCL: this round's outgoing slices, per peer contiguous
-  std::vector<hipEvent_t> merged_ev_, comm_ev_;  // per slot
+  // spill tiers, world > 1: outgoing slices of round q staged in send_staging_[q & 1] (per peer
+  // contiguous); sent_ev_[q & 1] marks the exchange that reads them on the comm stream
+  DeviceBuffer send_staging_[2];
+  std::vector<hipEvent_t> merged_ev_, comm_ev_, sent_ev_;  // per slot
+  int64_t xseq_ = 0;  // exchanges issued so far (Exchange sequence numbers)
   std::unique_ptr<DeviceMerger> merger_;
   DeviceBuffer d_validate_;  // stats[4] | prev key[R] | last key[R]
   // exchange verification (validate steps, world > 1): per round, the received peer slices and

@@ -6,25 +6,34 @@
 // sends, per destination, the slices of its map outputs that fall in the round's key cells, and
 // receives its own cells from every peer.
 //
-// Contract of exchange(): send[p] / recv[p] are the ordered non-empty slices to / from peer p
-// (p != me; the self entry must be empty). The k-th slice this rank sends to p pairs with the
-// k-th slice p receives from this rank; sizes must agree. Slices stay valid and unchanged until
-// the enqueued work on `s` has passed this exchange.
+// Contract of exchange() (the NCCL point-to-point rules, enforced by every backend):
+//   * send[p] / recv[p] are the ordered non-empty slices to / from peer p; the self entries are empty.
+//   * The k-th slice this rank sends to p pairs with the k-th slice p receives from this rank: the
+//     number of slices and every size must agree (a mismatch is an error, never a partial transfer).
+//   * Slices are device memory (hipMalloc); host-pinned sources are refused.
+//   * Send slices may be written by work enqueued on `s` before the call: every backend orders its
+//     reads after it (RCCL by stream order; pull backends by an event the receivers' streams wait for,
+//     or a host wait before the sender publishes its slice list).
+//   * Receive slices must not be touched before the work enqueued on `s` has passed the exchange.
+//   * Send slices must stay unchanged until wait_sent(seq) of that exchange returned (stream order on
+//     `s` is enough for RCCL; pull-based backends read the sender's memory from the peers' streams).
+// Exchanges are numbered 0, 1, 2, ... per Exchange object (seq).
 //
 // Implementations:
 //   RcclExchange   - one process per GPU, RCCL communicator bootstrapped from an ncclUniqueId.
-//                    Default (zero-copy): every slice is its own ncclSend straight from the map
-//                    output in the store into its receive slot, all of a round's sends and
-//                    receives inside one ncclGroupStart/End, peers in rotating order. A TeraSort
-//                    slice is tens of MB (130 GB / (16 rounds x 8 peers x 32 maps) = 32 MB), so
-//                    per-operation overhead is noise, and no CU time or HBM bandwidth goes to a pack.
-//                    UDA_RCCL_PACK=1 packs each peer's slices on the comm stream into one staging
-//                    region and sends one message per peer (for jobs with many tiny slices); the
-//                    receiver's slices from a peer must then be contiguous.
-//   LocalExchange  - W ranks as threads of one process sharing a device (tests / single-GPU
-//                    rehearsal of the multi-rank schedule): each receiver pulls its slices from
-//                    the senders' memory with copies on its own stream. Requires the send slices
-//                    to be immutable for the whole step (true for store-resident map outputs).
+//                    Default (zero-copy): every slice is its own ncclSend straight from its source
+//                    into its receive slot, all of a round's sends and receives inside one
+//                    ncclGroupStart/End, peers in rotating order. UDA_RCCL_PACK=1 packs each peer's
+//                    slices on the comm stream into one staging region and sends one message per peer.
+//   IpcExchange    - one process per GPU (or several processes sharing one GPU): a node-local
+//                    shared-memory control plane (uda/shm_group.h) plus pull copies straight from
+//                    the peers' HBM, mapped once per allocation over hipIpc (xGMI reads between
+//                    GPUs). Needs no RCCL kernels or CUs beyond the copies, and runs with N ranks on
+//                    one GPU, which RCCL refuses - so the multi-process path is exercised on a
+//                    one-GPU machine.
+//   LocalExchange  - W ranks as threads of one process sharing a device (tests / rehearsal): each
+//                    receiver pulls its slices from the senders' memory on its own stream, with the
+//                    same pairing / device-memory checks as the multi-process backends.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -57,7 +66,13 @@ class Exchange {
   // Enqueue one all-to-all-v round on stream s (see the contract above).
   virtual void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
                         hipStream_t s) = 0;
-  virtual const char* name() const = 0;
+  virtual std::string name() const = 0;
+  // Host wait until every peer has finished reading what this rank sent in exchange `seq` (after
+  // which those send slices may be overwritten). Stream-ordered backends return at once.
+  virtual void wait_sent(int64_t seq) { (void)seq; }
+  // Collective end of a step, called after this rank's streams drained: when it returns no peer
+  // reads this rank's memory any more (buffers may be freed or rewritten).
+  virtual void quiesce() {}
   // Host wait for everything enqueued on `s`, failing instead of hanging when a peer is lost
   // (RCCL: asynchronous communicator errors and a timeout, UDA_RCCL_TIMEOUT_S, default 900 s).
   virtual void wait(hipStream_t s);
@@ -68,6 +83,15 @@ class Exchange {
 std::unique_ptr<Exchange> make_rccl_exchange(int rank, int world, const std::string& unique_id);
 // All ranks of group `group` must call this with the same world; ranks are threads.
 std::unique_ptr<Exchange> make_local_exchange(const std::string& group, int rank, int world);
+// All ranks (processes on one node) call this with the same `name` (agreed out of band, e.g. by a
+// broadcast from rank 0); collective. `device` is this rank's HIP device.
+std::unique_ptr<Exchange> make_ipc_exchange(const std::string& name, int rank, int world, int device);
+
+// Test probe: `rounds` exchanges of synthetic slices (send_sizes[p] / recv_sizes[p]: slice sizes to /
+// from peer p), every received byte checked. Returns "" or the error (pairing, memory-kind, data).
+// host_source: the send slices live in pinned host memory (must be refused).
+std::string exchange_probe(Exchange& ex, int device, const std::vector<std::vector<int64_t>>& send_sizes,
+                           const std::vector<std::vector<int64_t>>& recv_sizes, bool host_source, int rounds);
 
 }  // namespace gpu
 }  // namespace uda

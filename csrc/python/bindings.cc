@@ -33,6 +33,9 @@
 #include "uda/compare.h"
 #include "uda/log.h"
 #include "uda/vint.h"
+#include "uda/shm_group.h"
+#include <atomic>
+#include <thread>
 
 namespace py = pybind11;
 using namespace uda;
@@ -47,6 +50,7 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   d["merge_ms"] = s.merge_ms;
   d["d2h_ms"] = s.d2h_ms;
   d["wait_out_ms"] = s.wait_out_ms;
+  d["stage_ms"] = s.stage_ms;
   d["bytes_in"] = s.bytes_in;
   d["records"] = s.records;
   d["bytes_sent"] = s.bytes_sent;
@@ -520,6 +524,43 @@ PYBIND11_MODULE(_uda_native, m) {
         uda_stats_json(b.h, buf.data(), (int32_t)buf.size());
         return std::string(buf.data());
       });
+  // node-local shared-memory control plane of the IPC exchange (CPU-testable, no HIP)
+  py::class_<ShmGroup>(m, "ShmGroup")
+      .def(py::init<const std::string&, int, int, size_t, size_t, double>(), py::arg("name"), py::arg("rank"),
+           py::arg("world"), py::arg("mailbox_bytes") = 1 << 16, py::arg("outbox_bytes") = 1 << 16,
+           py::arg("timeout_s") = 60.0, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", [](ShmGroup& g) { g.barrier("python"); }, py::call_guard<py::gil_scoped_release>())
+      .def("try_barrier", &ShmGroup::try_barrier, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &ShmGroup::abort)
+      .def("aborted", &ShmGroup::aborted)
+      .def("abort_reason", &ShmGroup::abort_reason)
+      .def("publish", [](ShmGroup& g, int c, int64_t v) { g.publish((ShmGroup::Counter)c, v); })
+      .def("read", [](ShmGroup& g, int c, int peer) { return g.read((ShmGroup::Counter)c, peer); })
+      .def("wait_at_least",
+           [](ShmGroup& g, int c, int peer, int64_t v) { g.wait_at_least((ShmGroup::Counter)c, peer, v, "python"); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("alltoall",
+           [](ShmGroup& g, const std::vector<int64_t>& send) {
+             if (send.size() % (size_t)g.world()) throw std::runtime_error("alltoall: size not a multiple of world");
+             std::vector<int64_t> recv(send.size());
+             {
+               py::gil_scoped_release nogil;
+               g.alltoall_i64(send.data(), recv.data(), send.size() / (size_t)g.world());
+             }
+             return recv;
+           })
+      .def("publish_alloc",
+           [](ShmGroup& g, py::bytes b, int64_t size) {
+             const std::string s = b;
+             return g.publish_alloc(s.data(), s.size(), size);
+           })
+      .def("read_alloc", [](ShmGroup& g, int peer, int id) -> py::object {
+        char blob[ShmGroup::kAllocBlob];
+        int64_t size = 0;
+        if (!g.read_alloc(peer, id, blob, sizeof(blob), &size)) return py::none();
+        return py::make_tuple(py::bytes(blob, sizeof(blob)), size);
+      });
+
   m.def("set_log_level", &uda_set_log_level);
 
   // ---------------------------------------------------------------- GPU engine
@@ -737,6 +778,46 @@ PYBIND11_MODULE(_uda_native, m) {
     return std::string(ex->name()) + (send == recv ? ":ok" : ":mismatch");
   }, py::arg("device") = 0, py::arg("n") = 4096);
 
+  // Exchange backends with hand-made plans (tests): the local group runs its ranks as threads here;
+  // the IPC probe is one rank (call it from one process per rank).
+  m.def("local_exchange_probe",
+        [](int world, const std::vector<std::vector<std::vector<int64_t>>>& send,
+           const std::vector<std::vector<std::vector<int64_t>>>& recv, bool host_source, int rounds, int device) {
+          py::gil_scoped_release rel;
+          static std::atomic<int> gen{0};
+          const std::string name = "probe" + std::to_string(gen++);
+          std::vector<std::string> out(world);
+          std::vector<std::thread> ts;
+          for (int r = 0; r < world; ++r)
+            ts.emplace_back([&, r] {
+              try {
+                HIP_CHECK(hipSetDevice(device));
+                auto ex = gpu::make_local_exchange(name, r, world);
+                out[r] = gpu::exchange_probe(*ex, device, send.at(r), recv.at(r), host_source, rounds);
+              } catch (const std::exception& e) {
+                out[r] = e.what();
+              }
+            });
+          for (auto& t : ts) t.join();
+          return out;
+        },
+        py::arg("world"), py::arg("send"), py::arg("recv"), py::arg("host_source") = false, py::arg("rounds") = 1,
+        py::arg("device") = 0);
+  m.def("ipc_exchange_probe",
+        [](const std::string& name, int rank, int world, const std::vector<std::vector<int64_t>>& send,
+           const std::vector<std::vector<int64_t>>& recv, bool host_source, int rounds, int device) {
+          py::gil_scoped_release rel;
+          try {
+            HIP_CHECK(hipSetDevice(device));
+            auto ex = gpu::make_ipc_exchange(name, rank, world, device);
+            return gpu::exchange_probe(*ex, device, send, recv, host_source, rounds);
+          } catch (const std::exception& e) {
+            return std::string(e.what());
+          }
+        },
+        py::arg("name"), py::arg("rank"), py::arg("world"), py::arg("send"), py::arg("recv"),
+        py::arg("host_source") = false, py::arg("rounds") = 1, py::arg("device") = 0);
+
   py::class_<gpu::J2CSink, std::shared_ptr<gpu::J2CSink>>(m, "J2CSink")
       .def(py::init<int, int64_t>(), py::arg("reducers"), py::arg("kv_buf_bytes") = 1 << 20)
       .def_property_readonly("reducers", &gpu::J2CSink::reducers)
@@ -813,6 +894,7 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("init_comm", [](gpu::ShuffleJob& j, const std::string& uid) { j.init_comm(uid); },
            py::call_guard<py::gil_scoped_release>())
       .def("init_local", &gpu::ShuffleJob::init_local, py::call_guard<py::gil_scoped_release>())
+      .def("init_ipc", &gpu::ShuffleJob::init_ipc, py::call_guard<py::gil_scoped_release>())
       .def("generate", &gpu::ShuffleJob::generate, py::call_guard<py::gil_scoped_release>())
       .def("sample_keys",
            [](gpu::ShuffleJob& j, int64_t every) {

@@ -184,12 +184,33 @@ def test_disk_store_tier(require_gpu, tmp_path, reducers, rounds):
     assert not list(d1.iterdir()) and not list(d2.iterdir())  # files removed with the store
 
 
-def test_disk_store_refuses_local_group(require_gpu, tmp_path):
-    from uda_amd.models.terasort import TeraSortConfig, make_local_group
-    cfg = TeraSortConfig(rows_per_gpu=4000, maps_per_rank=2, rounds=2, store="disk", local_dirs=str(tmp_path),
-                         sample_every=64, **SMALL)
-    with pytest.raises(Exception, match="RCCL"):
-        make_local_group(2, cfg, group="disk2")
+@pytest.mark.parametrize("world,store,h2d_sdma", [(2, "disk", "1"), (3, "disk", "1"), (3, "host", "1"),
+                                                 (3, "host", "0")])
+def test_spill_tiers_multirank_staged(require_gpu, tmp_path, monkeypatch, world, store, h2d_sdma):
+    """Spill tiers at world > 1: every round's outgoing slices are staged into HBM (double-buffered
+    send staging, one message per peer) and every peer pulls them with the strict pairing and
+    device-memory checks of the exchange; staging runs on the staging thread (SDMA / io_uring) or,
+    with UDA_H2D_SDMA=0, as a copy kernel on the comm stream. Two steps reuse both staging parities."""
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    monkeypatch.setenv("UDA_H2D_SDMA", h2d_sdma)
+    cfg = TeraSortConfig(rows_per_gpu=30000, maps_per_rank=3, rounds=5, reducers=2, validate=True, sample_every=64,
+                         store=store, local_dirs=str(tmp_path), **SMALL)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"spill{world}{store}{h2d_sdma}")
+    readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(2)] for _ in range(world)]
+    for d in range(world):
+        jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
+    for step in range(2):
+        stats = run_collective(jobs, lambda j: j.run_step(True))
+        for d, st in enumerate(stats):
+            check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+            assert st["exchange_errors"] == 0
+            assert st["bytes_sent"] > 0 and st["bytes_h2d"] >= st["bytes_sent"]
+        if step == 0:
+            for d in range(world):
+                expect = _sorted_all(j.read_partition(m, d) for j in jobs for m in range(3))
+                assert [kv for r in readers[d] for kv in r.records] == expect
+                readers[d] = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
+                jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
 
 
 @pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}])

@@ -20,6 +20,8 @@ Data is synthetic and TeraGen-shaped (10-byte keys, 90-byte values, 104-byte IFi
 from __future__ import annotations
 
 import dataclasses
+import os
+import secrets
 import time
 
 import numpy as np
@@ -51,6 +53,7 @@ class TeraSortConfig:
     local_dirs: str = "/tmp"            # store="disk": comma-separated directories for the MOF files
     replan: bool = False                # every step recomputes the cell splits and exchanges the counts
     map_sort: bool = False              # setup: unsorted map input sorted on the device (F8 radix sort)
+    exchange: str = "ipc"               # world > 1: "ipc" (shared-memory control + hipIpc pulls) or "rccl"
 
 
 class TeraSortShuffle:
@@ -78,9 +81,15 @@ class TeraSortShuffle:
         n = native()
         t0 = time.perf_counter()
         if self.ctx.world > 1:
-            uid = n.nccl_unique_id() if self.ctx.rank == 0 else None
-            uid = self.ctx.broadcast_bytes(uid)
-            self.job.init_comm(uid)
+            if self.cfg.exchange == "ipc":
+                name = f"uda.{os.getpid()}.{secrets.token_hex(6)}".encode() if self.ctx.rank == 0 else None
+                self.job.init_ipc(self.ctx.broadcast_bytes(name).decode())
+            elif self.cfg.exchange == "rccl":
+                uid = n.nccl_unique_id() if self.ctx.rank == 0 else None
+                uid = self.ctx.broadcast_bytes(uid)
+                self.job.init_comm(uid)
+            else:
+                raise ValueError(f"unknown exchange {self.cfg.exchange!r}")
         t1 = time.perf_counter()
         self.job.generate()
         t2 = time.perf_counter()
