@@ -89,6 +89,12 @@ def parse_args(argv=None):
                     help="drive the shuffle only through the UdaBridge C ABI (uda_start/INIT/FETCH/dataFromUda) "
                          "with HBM-resident MOFs: one NetMerger handle per reduce task (1 GPU)")
     ap.add_argument("--round-mb", type=int, default=2048, help="--api: device merge round size per reduce task")
+    ap.add_argument("--mof-dir", default="",
+                    help="--api: write every map output as a file.out under this directory; the provider finds "
+                         "them through getPathUda (Hadoop-written MOFs) and serves them from its HBM store")
+    ap.add_argument("--provider-hbm-gb", type=float, default=-1.0,
+                    help="--api --mof-dir: mapred.uda.provider.hbm.bytes in GB (default: 1.25x the MOF bytes; "
+                         "0 = store off: descriptor fetches are declined and reducers fetch bytes)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -297,7 +303,12 @@ def run_api(args, ctx) -> int:
     # one provider per rank, all on one port at 127.0.0.<rank + 1> (providers of different hosts share the
     # port in Hadoop; -r of every reduce task)
     port = ctx.all_gather_object(_free_port() if rank == 0 else 0)[0] if world > 1 else 0
+    hbm_bytes = 0
+    if args.mof_dir:
+        per_rank = args.rows_per_gpu * RECORD_BYTES
+        hbm_bytes = int(per_rank * 1.25) if args.provider_hbm_gb < 0 else int(args.provider_hbm_gb * 1e9)
     b = native().ApiTeraSortBench(dict(device=device, maps=args.maps_per_gpu, reducers=R,
+                                       mof_dir=args.mof_dir, provider_hbm_bytes=hbm_bytes,
                                        records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
                                        round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
                                        transport="tcp" if world > 1 else "loopback",
@@ -315,9 +326,12 @@ def run_api(args, ctx) -> int:
     if rank == 0:
         print(f"# api setup {time.perf_counter() - t:.1f}s store={b.store_bytes/1e9:.1f}GB per rank, {world} rank(s)"
               f"{' on one GPU (rehearsal)' if args.one_gpu and world > 1 else ''}", file=sys.stderr, flush=True)
+    first_step_ms = None
     for i in range(args.warmup):
         ctx.barrier()
         st = b.step(False)
+        if first_step_ms is None:
+            first_step_ms = st["wall_ms"]  # --mof-dir: includes the provider's first-touch file loads
         if args.verbose and rank == 0:
             print(f"# warmup {i}: {json.dumps(st)}", file=sys.stderr, flush=True)
     ctx.barrier()
@@ -360,7 +374,10 @@ def run_api(args, ctx) -> int:
                 "rows_per_gpu": args.rows_per_gpu,
                 "maps_per_gpu": args.maps_per_gpu,
                 "reducers_per_gpu": R,
-                "shuffle": ("UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, MOFs in host memory fetched "
+                "shuffle": ("UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, MOF files on disk found through "
+                            "getPathUda, loaded once into the provider's HBM store and served as descriptors")
+                           if args.mof_dir else
+                           ("UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, MOFs in host memory fetched "
                             f"as bytes (mapred.uda.gpu.fetch={args.api_fetch or 'host'}), merged on the GPU")
                            if args.api_host_mofs else
                            "UdaBridge C ABI: uda_start/INIT/FETCH per reduce task, HBM-resident MOFs "
@@ -369,6 +386,9 @@ def run_api(args, ctx) -> int:
                 "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) per reduce task",
             },
             "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
+            "mof_files": bool(args.mof_dir),
+            "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
+            "provider": json.loads(b.provider_stats()),
             "close_ms": round(sum(s["close_ms"] for s in stats) / len(stats), 2),
             "buffers_per_step": int(stats[0]["buffers"]),
             "task0_stats": json.loads(stats[0]["task0_stats"]) if stats[0]["task0_stats"] else None,

@@ -88,6 +88,19 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
       so.io_threads = (int)h->host->conf_i64("mapred.uda.provider.blocked.threads.per.disk", 4);
       so.workers = (int)h->host->conf_i64("mapred.uda.provider.workers", 8);
       so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);
+      so.hbm_bytes = h->host->conf_i64("mapred.uda.provider.hbm.bytes", 0);
+      so.hbm_lease_s = h->host->conf_f64("mapred.uda.provider.hbm.lease.s", 600);
+      {
+        const std::string devs = h->host->get_conf("mapred.uda.provider.hbm.devices", "0");
+        so.hbm_devices.clear();
+        for (size_t b = 0; b <= devs.size();) {
+          const size_t e = devs.find(',', b);
+          const std::string t = devs.substr(b, e == std::string::npos ? std::string::npos : e - b);
+          if (!t.empty()) so.hbm_devices.push_back(std::atoi(t.c_str()));
+          if (e == std::string::npos) break;
+          b = e + 1;
+        }
+      }
       h->supplier = std::make_unique<uda::Supplier>(h->opt, so, h->host.get());
       h->supplier->start();
     }
@@ -108,10 +121,13 @@ int uda_do_command(uda_handle* h, const char* cmd) {
       if (!h->task) return fail_call(h, "reduce task already closed");
       h->task->handle(c);
     } else {
-      // mof_downcall_handler (MOFSupplierMain.cc:37-81): only EXIT matters
+      // mof_downcall_handler (MOFSupplierMain.cc:37-81): EXIT stops the supplier; JOB_OVER (sent by
+      // the provider plugin when an application ends) releases the job's MOFs from the HBM store
       if (c.header == uda::kExitMsg && h->supplier) {
         h->supplier->stop();
         UDA_LOG(uda::kInfo, "MOFSupplier stopped");
+      } else if (c.header == uda::kJobOverMsg && h->supplier && !c.params.empty()) {
+        h->supplier->job_over(c.params[0]);
       }
     }
   } catch (const std::exception& e) {
@@ -181,7 +197,8 @@ int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
     s = "{\"role\":\"mof_supplier\",\"requests\":" + std::to_string(h->supplier->requests()) +
         ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) +
         ",\"descriptors_served\":" + std::to_string(h->supplier->descriptors_served()) + ",\"port\":" +
-        std::to_string(h->supplier->port()) + ",\"io\":\"" + h->supplier->io_backend() + "\"}";
+        std::to_string(h->supplier->port()) + ",\"io\":\"" + h->supplier->io_backend() + "\",\"hbm_store\":" +
+        h->supplier->hbm_stats_json() + "}";
   } else {
     s = "{}";
   }

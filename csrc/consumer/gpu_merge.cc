@@ -1218,7 +1218,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     gpu::DeviceBuffer own;  // bytes fetched from a host-resident MOF
   };
   std::vector<std::unique_ptr<Part>> parts;
-  int64_t host_bytes = 0, descriptors = 0;
+  int64_t host_bytes = 0, descriptors = 0, unmapped = 0;
   gpu::PinnedBuffer chunk;
 
   // bytes of a MOF the provider does not hold in device memory: chunked fetches -> H2D
@@ -1307,10 +1307,18 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     for (size_t i = 0; i < batch.size(); ++i) {
       const FetchAck& a = acks[i];
       auto part = std::make_unique<Part>();
-      if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
-        part->dptr = gpu::resolve_device_descriptor(a.path, device);
+      std::string why;
+      const uint8_t* dp = nullptr;
+      if (a.status == 0 && gpu::is_device_descriptor(a.path) &&
+          (dp = gpu::try_resolve_device_descriptor(a.path, device, &why)) != nullptr) {
+        part->dptr = dp;
         part->part_len = a.part_len;
         ++descriptors;
+      } else if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
+        // not mappable here (another node, no IPC handle, import failure): fetch its bytes
+        UDA_LOG(kInfo, "descriptor of %s not usable (%s): fetching bytes", batch[i].map_id.c_str(), why.c_str());
+        fetch_bytes(batch[i], a.part_len, part.get());
+        ++unmapped;
       } else if (a.status == kNotDeviceResident) {
         fetch_bytes(batch[i], a.part_len, part.get());
       } else {
@@ -1335,6 +1343,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.device_descriptors = descriptors;
+    st_.unmapped_descriptors = unmapped;
     st_.host_fetched_bytes = host_bytes;
   }
 

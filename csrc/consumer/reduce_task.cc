@@ -527,8 +527,10 @@ void ReduceTask::merge_main() {
   auto t0 = std::chrono::steady_clock::now();
   try {
     const std::string gfetch = host_->get_conf("mapred.uda.gpu.fetch", "auto");  // auto | device | host
+    // a resumed attempt (LPQ checkpoint of an earlier staged attempt) merges its restored runs on the
+    // staged path: the device path has no notion of restored maps (their FETCHes are dropped)
     if (backend_ == "gpu" && codec_ == Codec::kNone && net_.online != 2 && gfetch != "host" &&
-        merge_gpu_device(gfetch == "auto")) {
+        restored_files_.empty() && merge_gpu_device(gfetch == "auto")) {
       // done: partitions merged where the provider holds them
     } else if (backend_ == "gpu") {
       merge_gpu();
@@ -802,7 +804,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
-    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors
+    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"merge_path\":\"" << s.merge_path << "\""
     << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();

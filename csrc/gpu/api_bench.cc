@@ -1,6 +1,10 @@
 // TeraSort through the C ABI with HBM-resident MOFs. See api_bench.h.
 #include "api_bench.h"
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -76,6 +80,24 @@ void log_cb(void*, const char* msg, int32_t sev) {
   if (sev <= 2) std::fprintf(stderr, "[uda api] %s\n", msg);
 }
 
+struct ProviderCtx {
+  ConfTable* conf;
+  const ApiTeraSortBench* bench;
+};
+int provider_conf_cb(void* ctx, const char* key, const char* dflt, char* out, int32_t outlen) {
+  return conf_cb(static_cast<ProviderCtx*>(ctx)->conf, key, dflt, out, outlen);
+}
+int provider_path_cb(void* ctx, const char*, const char* map_id, int32_t reduce_id, uda_index_record* out) {
+  int64_t rec[3];
+  std::string path;
+  if (!static_cast<ProviderCtx*>(ctx)->bench->resolve(map_id, reduce_id, rec, &path)) return -1;
+  out->start_offset = rec[0];
+  out->raw_length = rec[1];
+  out->part_length = rec[2];
+  std::snprintf(out->path, sizeof(out->path), "%s", path.c_str());
+  return 0;
+}
+
 ConfTable& bench_conf(const ApiBenchConfig& c) {
   static ConfTable t;
   t.kv = {{"mapred.uda.transport", c.transport},
@@ -88,6 +110,10 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
           {"mapred.uda.provider.bind.address", c.bind_addr}};
   if (c.provider_workers > 0) t.kv["mapred.uda.provider.workers"] = std::to_string(c.provider_workers);
   if (c.max_concurrent_merges >= 0) t.kv["mapred.uda.gpu.max.concurrent.merges"] = std::to_string(c.max_concurrent_merges);
+  if (c.provider_hbm_bytes > 0) {
+    t.kv["mapred.uda.provider.hbm.bytes"] = std::to_string(c.provider_hbm_bytes);
+    t.kv["mapred.uda.provider.hbm.devices"] = std::to_string(c.device);
+  }
   return t;
 }
 
@@ -106,6 +132,23 @@ ApiTeraSortBench::~ApiTeraSortBench() {
     (void)uda_do_command(h, form_cmd(kExitMsg, {}).c_str());
     uda_destroy(h);
   }
+  delete static_cast<ProviderCtx*>(provider_ctx_);
+  for (auto& kv : file_path_) ::unlink(kv.second.c_str());
+}
+
+bool ApiTeraSortBench::resolve(const std::string& map, int reduce, int64_t rec[3], std::string* path) const {
+  auto it = file_index_.find(map);
+  if (it == file_index_.end() || reduce < 0 || (size_t)(3 * reduce + 2) >= it->second.size()) return false;
+  for (int k = 0; k < 3; ++k) rec[k] = it->second[(size_t)(3 * reduce + k)];
+  *path = file_path_.at(map);
+  return true;
+}
+
+std::string ApiTeraSortBench::provider_stats() const {
+  if (!provider_) return "{}";
+  char js[4096];
+  if (uda_stats_json(static_cast<uda_handle*>(provider_), js, sizeof(js)) <= 0) return "{}";
+  return js;
 }
 
 int64_t ApiTeraSortBench::store_bytes() const { return gen_ ? gen_->store_bytes() : 0; }
@@ -138,9 +181,12 @@ void ApiTeraSortBench::setup() {
   if (cfg_.world == 1) expected_ = gen_->local_dest_records();
   // MOFSupplier handle (TaskTracker / NodeManager side)
   ConfTable& conf = bench_conf(cfg_);
+  auto* pctx = new ProviderCtx{&conf, this};
+  provider_ctx_ = pctx;
   uda_callbacks cb{};
-  cb.ctx = &conf;
-  cb.get_conf = conf_cb;
+  cb.ctx = pctx;
+  cb.get_conf = provider_conf_cb;
+  cb.get_path = provider_path_cb;
   cb.log = log_cb;
   const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
                                          "-m", "1", "-g", "/tmp", "-s", "1024"};
@@ -156,6 +202,31 @@ void ApiTeraSortBench::setup() {
     for (int r = 0; r < P; ++r) {
       const auto ir = gen_->index_record(m, r);
       index.insert(index.end(), ir.begin(), ir.end());
+    }
+    if (!cfg_.mof_dir.empty()) {  // the map task's file.out (the provider finds it through getPathUda)
+      const std::string path = cfg_.mof_dir + "/" + id + ".file.out";
+      const int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+      if (fd < 0) throw std::runtime_error("api bench: cannot create " + path + ": " + strerror(errno));
+      const int64_t len = gen_->mof_bytes(m);
+      std::vector<uint8_t> buf((size_t)std::min<int64_t>(len, 256ll << 20));
+      for (int64_t off = 0; off < len;) {
+        const int64_t n = std::min<int64_t>((int64_t)buf.size(), len - off);
+        HIP_CHECK(hipMemcpy(buf.data(), gen_->mof_device_ptr(m) + off, (size_t)n, hipMemcpyDeviceToHost));
+        for (int64_t w = 0; w < n;) {
+          const ssize_t r = ::pwrite(fd, buf.data() + w, (size_t)(n - w), off + w);
+          if (r <= 0) {
+            ::close(fd);
+            throw std::runtime_error("api bench: write to " + path + " failed");
+          }
+          w += r;
+        }
+        off += n;
+      }
+      (void)::fdatasync(fd);
+      ::close(fd);
+      file_index_[id] = index;
+      file_path_[id] = path;
+      continue;
     }
     if (cfg_.host_mofs) {  // a map output in host memory (page cache / local disk stand-in)
       host_mofs_.emplace_back((size_t)gen_->mof_bytes(m));

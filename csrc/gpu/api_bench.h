@@ -45,6 +45,11 @@ struct ApiBenchConfig {
   int provider_workers = -1;         // mapred.uda.provider.workers (-1 = default)
   int max_concurrent_merges = -1;    // mapred.uda.gpu.max.concurrent.merges (staged path; 0 = no limit, -1 = default)
   std::string transport = "loopback";
+  // Hadoop-written MOFs: each map output is written as a file under mof_dir and found by the provider
+  // through getPathUda (no registration); the provider's HBM store (provider_hbm_bytes > 0) loads a
+  // file into HBM on first touch and answers descriptor fetches from it
+  std::string mof_dir;
+  int64_t provider_hbm_bytes = 0;
 };
 
 class ApiTeraSortBench {
@@ -73,6 +78,16 @@ class ApiTeraSortBench {
   std::vector<std::string> peers_;
   std::vector<std::vector<uint8_t>> host_mofs_;  // host_mofs: the MOFs' bytes in host memory
   std::string map_id(int global_map) const;
+
+ public:
+  // getPathUda of the provider (mof_dir mode)
+  bool resolve(const std::string& map, int reduce, int64_t rec[3], std::string* path) const;
+  std::string provider_stats() const;
+
+ private:
+  std::map<std::string, std::vector<int64_t>> file_index_;  // map id -> 3 int64 per partition
+  std::map<std::string, std::string> file_path_;
+  void* provider_ctx_ = nullptr;
 };
 
 }  // namespace gpu

@@ -69,12 +69,40 @@ IpcExport ipc_export(const void* ptr) {
     return ex;
   }
   ex.base = static_cast<const uint8_t*>(base);
+  ex.size = size;
+  if (!ipc_size_ok(size)) {  // importing it would hang the reducer: peers fetch bytes instead
+    ex.refused = "allocation of " + std::to_string(size) + " bytes is in the hipIpc-hanging size range";
+    return ex;
+  }
   hipIpcMemHandle_t h;
   if (hipIpcGetMemHandle(&h, base) == hipSuccess)
     ex.handle_hex = to_hex(&h, sizeof(h));
   else
     (void)hipGetLastError();
   return ex;
+}
+
+bool ipc_size_ok(size_t bytes) { return ((uint64_t)bytes & 0xFFFFFFFFull) < (1ull << 31); }
+
+const std::string& node_id() {
+  // hostname + kernel boot id: two processes may share device memory over hipIpc only when both
+  // are equal (same machine, same boot); a container with its own hostname is treated as foreign
+  static const std::string id = [] {
+    char host[256] = {0};
+    (void)gethostname(host, sizeof(host) - 1);
+    std::string boot;
+    if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
+      char b[64] = {0};
+      if (std::fgets(b, sizeof(b), f)) boot = b;
+      std::fclose(f);
+    }
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    for (char c : std::string(host) + "|" + boot) h = (h ^ (uint8_t)c) * 1099511628211ull;
+    char out[17];
+    std::snprintf(out, sizeof(out), "%016llx", (unsigned long long)h);
+    return std::string(out);
+  }();
+  return id;
 }
 
 size_t ipc_safe_bytes(size_t bytes) {
@@ -84,42 +112,70 @@ size_t ipc_safe_bytes(size_t bytes) {
 }
 
 std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc) {
-  char head[96];
-  std::snprintf(head, sizeof(head), "hbm@%d@%d@%llx@", device, (int)getpid(),
+  char head[128];
+  std::snprintf(head, sizeof(head), "hbm@%s@%d@%d@%llx@", node_id().c_str(), device, (int)getpid(),
                 (unsigned long long)(uintptr_t)ptr);
   return std::string(head) + ipc.handle_hex + "@" + std::to_string((long long)(ptr - ipc.base));
 }
 
 bool is_device_descriptor(const std::string& s) { return s.rfind("hbm@", 0) == 0; }
 
-const uint8_t* resolve_device_descriptor(const std::string& desc, int my_device) {
+const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_device, std::string* why) {
   const auto f = split_at(desc);
-  if (f.size() != 6 || f[0] != "hbm") throw std::runtime_error("bad device descriptor '" + desc + "'");
-  const int dev = std::atoi(f[1].c_str());
-  const int pid = std::atoi(f[2].c_str());
-  const uint8_t* addr = reinterpret_cast<const uint8_t*>((uintptr_t)std::strtoull(f[3].c_str(), nullptr, 16));
-  if (pid == (int)getpid()) {
-    if (dev != my_device) {  // same process, other GPU: reads go peer-to-peer over xGMI
-      int can = 0;
-      HIP_CHECK(hipDeviceCanAccessPeer(&can, my_device, dev));
-      if (!can) throw std::runtime_error("device " + std::to_string(my_device) + " cannot access device " + f[1]);
-      const hipError_t e = hipDeviceEnablePeerAccess(dev, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(e);
-      (void)hipGetLastError();
+  if (f.size() != 7 || f[0] != "hbm") {
+    if (why) *why = "malformed device descriptor '" + desc + "'";
+    return nullptr;
+  }
+  if (f[1] != node_id()) {  // another machine (or container): its addresses and handles mean nothing here
+    if (why) *why = "descriptor from another node";
+    return nullptr;
+  }
+  const int dev = std::atoi(f[2].c_str());
+  const int pid = std::atoi(f[3].c_str());
+  const uint8_t* addr = reinterpret_cast<const uint8_t*>((uintptr_t)std::strtoull(f[4].c_str(), nullptr, 16));
+  try {
+    if (pid == (int)getpid()) {
+      if (dev != my_device) {  // same process, other GPU: reads go peer-to-peer over xGMI
+        int can = 0;
+        HIP_CHECK(hipDeviceCanAccessPeer(&can, my_device, dev));
+        if (!can) {
+          if (why) *why = "device " + std::to_string(my_device) + " cannot access device " + f[2];
+          return nullptr;
+        }
+        const hipError_t e = hipDeviceEnablePeerAccess(dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(e);
+        (void)hipGetLastError();
+      }
+      return addr;
     }
-    return addr;
+    if (f[5] == "-") {
+      if (why) *why = "provider allocation is not IPC-shareable";
+      return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_ipc_mu);
+    auto it = opened().find(f[5]);
+    if (it == opened().end()) {
+      hipIpcMemHandle_t h;
+      if (!from_hex(f[5], &h, sizeof(h))) {
+        if (why) *why = "bad IPC handle in descriptor";
+        return nullptr;
+      }
+      void* p = nullptr;
+      HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      it = opened().emplace(f[5], static_cast<uint8_t*>(p)).first;
+    }
+    return it->second + std::strtoll(f[6].c_str(), nullptr, 10);
+  } catch (const std::exception& e) {
+    if (why) *why = e.what();
+    return nullptr;
   }
-  if (f[4] == "-") throw std::runtime_error("provider allocation is not IPC-shareable: " + desc);
-  std::lock_guard<std::mutex> g(g_ipc_mu);
-  auto it = opened().find(f[4]);
-  if (it == opened().end()) {
-    hipIpcMemHandle_t h;
-    if (!from_hex(f[4], &h, sizeof(h))) throw std::runtime_error("bad IPC handle in descriptor");
-    void* p = nullptr;
-    HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-    it = opened().emplace(f[4], static_cast<uint8_t*>(p)).first;
-  }
-  return it->second + std::strtoll(f[5].c_str(), nullptr, 10);
+}
+
+const uint8_t* resolve_device_descriptor(const std::string& desc, int my_device) {
+  std::string why;
+  const uint8_t* p = try_resolve_device_descriptor(desc, my_device, &why);
+  if (!p) throw std::runtime_error("cannot map device descriptor: " + why);
+  return p;
 }
 
 void copy_device_to_host(void* dst, const void* src, int64_t bytes) {

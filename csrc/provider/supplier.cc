@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "../gpu/device_ptr.h"
+#include "../gpu/mof_cache.h"
 #include "uda/log.h"
 
 namespace uda {
@@ -14,6 +15,15 @@ Supplier::Supplier(const NetlevOptions& net, const Options& o, Host* host) : net
   AsyncIO::Options ao;
   ao.threads = o.io_threads;
   aio_ = AsyncIO::create(ao);
+  if (o.hbm_bytes > 0) {
+    gpu::MofCache::Options co;
+    co.capacity = o.hbm_bytes;
+    co.devices = o.hbm_devices;
+    co.odirect = true;
+    co.lease_s = o.hbm_lease_s;
+    hbm_ = std::make_unique<gpu::MofCache>(co);
+    UDA_LOG(kInfo, "MOFSupplier HBM store: %ld bytes over %zu GPU(s)", (long)o.hbm_bytes, o.hbm_devices.size());
+  }
 }
 
 Supplier::~Supplier() { stop(); }
@@ -44,6 +54,7 @@ void Supplier::stop() {
   for (auto& t : workers_) t.join();
   workers_.clear();
   if (aio_) aio_->drain();
+  hbm_.reset();  // after the workers: no fetch is being answered from it
   std::lock_guard<std::mutex> g(fd_mu_);
   for (auto& kv : fds_)
     if (kv.second.fd >= 0) ::close(kv.second.fd);
@@ -61,6 +72,23 @@ void Supplier::register_mof(const std::string& job, const std::string& map, cons
   }
   std::lock_guard<std::mutex> g(idx_mu_);
   mem_[job + "|" + map] = std::move(m);
+}
+
+void Supplier::job_over(const std::string& job) {
+  if (hbm_) hbm_->job_over(job);
+  std::lock_guard<std::mutex> g(idx_mu_);
+  const std::string pre = job + "|";
+  for (auto it = idx_cache_.begin(); it != idx_cache_.end();)
+    it = it->first.compare(0, pre.size(), pre) == 0 ? idx_cache_.erase(it) : std::next(it);
+}
+
+std::string Supplier::hbm_stats_json() {
+  if (!hbm_) return "{}";
+  const gpu::MofCache::Stats st = hbm_->stats();
+  return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
+         ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
+         ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
+         std::to_string(st.resident_bytes) + ",\"load_ms\":" + std::to_string(st.load_ms) + "}";
 }
 
 void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
@@ -178,7 +206,19 @@ void Supplier::process(Job& j) {
   ack.path = rec.path;
   if (j.req.buf_len == kDescriptorFetch) {
     // zero-copy fetch: the reducer reads the partition where it lives (RDMA WRITE analogue)
-    if (!mem || mem->device < 0) {
+    gpu::MofCache::Ref ref;
+    std::string why;
+    if (!mem && hbm_ && hbm_->acquire(j.req.job_id, rec.path, &ref, &why)) {
+      // a Hadoop-written MOF file, now resident in the provider's HBM store
+      if (rec.start_offset + rec.part_length > ref.len) {
+        ack.status = -4;
+        ack.error = "index beyond MOF file " + rec.path;
+      } else {
+        ack.path = gpu::make_device_descriptor(ref.device, ref.data + rec.start_offset, ref.ipc);
+        ack.sent = 0;
+        descriptors_++;
+      }
+    } else if (!mem || mem->device < 0) {
       ack.status = kNotDeviceResident;
       ack.error = "MOF is not device-resident";
     } else if (rec.start_offset + rec.part_length > mem->len) {

@@ -26,6 +26,12 @@
 #include "uda/transport.h"
 
 namespace uda {
+namespace gpu {
+class MofCache;
+}
+}  // namespace uda
+
+namespace uda {
 
 class Supplier : public DataServer {
  public:
@@ -37,6 +43,11 @@ class Supplier : public DataServer {
     std::string transport = "loopback";  // loopback | tcp
     std::string loopback_host = "*";
     std::string bind_addr;       // tcp: listen address (mapred.uda.provider.bind.address; empty = any)
+    // HBM store for file MOFs (gpu/mof_cache.h): descriptor fetches of MOFs found through getPathUda
+    // load the file into HBM once and are answered with device descriptors
+    int64_t hbm_bytes = 0;               // mapred.uda.provider.hbm.bytes (0: off)
+    std::vector<int> hbm_devices{0};     // mapred.uda.provider.hbm.devices ("0,1,...")
+    double hbm_lease_s = 600;            // mapred.uda.provider.hbm.lease.s
   };
   Supplier(const NetlevOptions& net, const Options& o, Host* host);
   ~Supplier() override;
@@ -54,6 +65,10 @@ class Supplier : public DataServer {
   int64_t requests() const { return requests_.load(); }
   int64_t bytes_served() const { return bytes_.load(); }
   int64_t descriptors_served() const { return descriptors_.load(); }
+  // JOB_OVER: the job's MOFs held in the HBM store may be freed.
+  void job_over(const std::string& job);
+  // {"loads":..,"hits":..,...} of the HBM store ("{}" when off)
+  std::string hbm_stats_json();
   const char* io_backend() const { return aio_ ? aio_->backend() : "none"; }
 
  private:
@@ -86,6 +101,7 @@ class Supplier : public DataServer {
   Host* host_;
   std::unique_ptr<AsyncIO> aio_;
   std::unique_ptr<ServerTransport> server_;
+  std::unique_ptr<gpu::MofCache> hbm_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Job> q_;

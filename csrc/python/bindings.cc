@@ -566,6 +566,21 @@ PYBIND11_MODULE(_uda_native, m) {
   // ---------------------------------------------------------------- GPU engine
   m.def("device_count", &gpu::device_count);
   m.def("ipc_safe_bytes", [](uint64_t b) { return (uint64_t)gpu::ipc_safe_bytes((size_t)b); });
+  m.def("ipc_size_ok", [](uint64_t b) { return gpu::ipc_size_ok((size_t)b); });
+  m.def("node_id", []() { return gpu::node_id(); });
+  // (address or None, reason): what a reducer does with a provider's descriptor
+  m.def("descriptor_resolve", [](const std::string& desc, int device) -> py::tuple {
+    std::string why;
+    const uint8_t* p = gpu::try_resolve_device_descriptor(desc, device, &why);
+    if (!p) return py::make_tuple(py::none(), why);
+    return py::make_tuple((uint64_t)(uintptr_t)p, why);
+  });
+  m.def("descriptor_make", [](int device, uint64_t addr, const std::string& handle_hex, uint64_t base) {
+    gpu::IpcExport ex;
+    ex.handle_hex = handle_hex;
+    ex.base = reinterpret_cast<const uint8_t*>((uintptr_t)base);
+    return gpu::make_device_descriptor(device, reinterpret_cast<const uint8_t*>((uintptr_t)addr), ex);
+  });
   // N8 device discovery: per-pair P2P reachability, link type (HSA_AMD_LINK_INFO_TYPE_*: 2 = xGMI) and
   // hop count, and the runtime's relative performance rank.
   m.def("device_topology", []() {
@@ -864,6 +879,8 @@ PYBIND11_MODULE(_uda_native, m) {
         get("fetch", c.fetch);
         get("max_concurrent_merges", c.max_concurrent_merges);
         get("provider_workers", c.provider_workers);
+        get("mof_dir", c.mof_dir);
+        get("provider_hbm_bytes", c.provider_hbm_bytes);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
@@ -882,6 +899,7 @@ PYBIND11_MODULE(_uda_native, m) {
            },
            py::arg("validate") = false)
       .def("expected_records", &gpu::ApiTeraSortBench::expected_records)
+      .def("provider_stats", &gpu::ApiTeraSortBench::provider_stats)
       .def("local_partition_records", &gpu::ApiTeraSortBench::local_partition_records)
       .def("set_expected", &gpu::ApiTeraSortBench::set_expected)
       .def("set_peers", &gpu::ApiTeraSortBench::set_peers)

@@ -13,6 +13,7 @@ package com.mellanox.hadoop.mapred;
 
 import java.io.IOException;
 import java.nio.ByteBuffer;
+import java.util.Collections;
 import java.util.Map;
 import java.util.concurrent.ConcurrentHashMap;
 
@@ -77,7 +78,11 @@ public class UdaShuffleHandler extends AuxiliaryService implements UdaBridge.Ind
 
   @Override
   public void stopApplication(ApplicationTerminationContext ctx) {
-    jobUser.remove(jobOf(ctx.getApplicationId()));
+    String job = jobOf(ctx.getApplicationId());
+    jobUser.remove(job);
+    if (supplier != null) {  // the native provider may free the job's MOFs held in its HBM store
+      UdaBridge.doCommand(UdaCmd.formCmd(UdaCmd.JOB_OVER_COMMAND, Collections.singletonList(job)));
+    }
   }
 
   @Override

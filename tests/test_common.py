@@ -139,3 +139,33 @@ def test_ipc_safe_bytes_avoids_the_hanging_size_range(native):
         assert padded >= size
         assert padded % (4 * G) < 2 * G
         assert padded - size <= 2 * G + (64 << 20)
+
+
+def test_device_descriptor_identity(native):
+    """A descriptor carries the provider's node identity (hostname + boot id): one from another node
+    or container is never mapped (the reducer fetches bytes instead); a same-process descriptor
+    resolves to its address; a descriptor without an IPC handle from another process is refused."""
+    import os
+    me = native.node_id()
+    assert len(me) == 16 and me == native.node_id()
+    d = native.descriptor_make(0, 0x7F0000001000, "-", 0x7F0000000000)
+    f = d.split("@")
+    assert f[0] == "hbm" and f[1] == me and int(f[3]) == os.getpid() and f[6] == str(0x1000)
+    addr, why = native.descriptor_resolve(d, 0)  # same process, same device: the address itself
+    assert addr == 0x7F0000001000, why
+    forged = "@".join([f[0], "0123456789abcdef"] + f[2:])  # same pid/address, other node
+    addr, why = native.descriptor_resolve(forged, 0)
+    assert addr is None and "another node" in why
+    other_pid = "@".join(f[:3] + [str(os.getpid() + 1)] + f[4:])
+    addr, why = native.descriptor_resolve(other_pid, 0)
+    assert addr is None and "not IPC-shareable" in why
+    for bad in ("hbm@1@2", "hbm@" + me + "@0@1@zz@-", "mem:job/map"):
+        assert native.descriptor_resolve(bad, 0)[0] is None
+
+
+def test_ipc_export_size_rule(native):
+    for size in (1 << 20, (1 << 31) - 1, 1 << 32, (1 << 32) + (1 << 30), 5 << 30):
+        assert native.ipc_size_ok(size), size
+    for size in (1 << 31, 3 << 30, (1 << 32) - 1, (6 << 30) + 1):
+        assert not native.ipc_size_ok(size), size
+        assert native.ipc_size_ok(native.ipc_safe_bytes(size))

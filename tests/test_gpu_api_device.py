@@ -190,3 +190,74 @@ def test_api_bench_host_mofs_gated(require_gpu, native, slots):
     assert t0["merge_path"] == "staged"
     if slots == 0:
         assert t0["gpu_gate_wait_ms"] == 0
+
+
+def _publish_files(provider, tmp_path, job, maps):
+    from uda_amd.utils.mof import write_mof
+    ids = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        path, _ = write_mof(str(tmp_path), mid, parts)
+        provider.add_mof_file(job, mid, path)  # found through getPathUda, never registered
+        ids.append(mid)
+    return ids
+
+
+@pytest.mark.parametrize("kind", ["terasort", "wordcount"])
+def test_provider_hbm_store_serves_file_mofs(require_gpu, tmp_path, kind):
+    """Hadoop-written MOF files (resolved through the getPathUda callback) are loaded once into the
+    provider's HBM store on first touch and every partition is then served as a device descriptor:
+    every reducer merges in place, output identical to the CPU merge, each file read once."""
+    p = UdaProvider(conf={"mapred.uda.provider.hbm.bytes": 1 << 30})
+    try:
+        R = 3
+        maps = (datagen.terasort(num_maps=8, reducers=R, rows_per_map=3000, seed=21) if kind == "terasort" else
+                datagen.wordcount(num_maps=8, reducers=R, words_per_map=2000, seed=21))
+        ids = _publish_files(p, tmp_path, "job_9_0100", maps)
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "auto"})
+        for r in range(R):
+            recs, st, _ = run_reduce("h", "job_9_0100", ids, r, datagen.TEXT, conf=conf, kv_buf_size=64 << 10)
+            cpu, _, _ = run_reduce("h", "job_9_0100", ids, r, datagen.TEXT, kv_buf_size=64 << 10)
+            assert recs == cpu, r
+            assert st["device_descriptors"] == 8 and st["host_fetched_bytes"] == 0, st
+            assert st["merge_path"].startswith("device")
+        hs = json.loads(p.stats())["hbm_store"]
+        assert hs["loads"] == 8 and hs["hits"] >= 8 * (R - 1) and hs["declined"] == 0, hs
+        assert hs["resident_bytes"] == sum(os.path.getsize(tmp_path / m / "file.out") for m in ids), hs
+        p.bridge.do_command(__import__("uda_amd").native().form_cmd(6, ["job_9_0100"]))  # JOB_OVER
+        hs = json.loads(p.stats())["hbm_store"]
+        assert hs["resident_bytes"] == 0 and hs["evictions"] == 8, hs
+    finally:
+        p.close()
+
+
+def test_provider_hbm_store_budget_falls_back_to_bytes(require_gpu, tmp_path):
+    """A budget that holds only some files: leased entries are never evicted under a reducer, the
+    declined MOFs are fetched as bytes, and the output is still exact."""
+    maps = datagen.terasort(num_maps=6, reducers=1, rows_per_map=4000, seed=23)
+    size = len(datagen.streams(maps)[0][0]) + 64
+    p = UdaProvider(conf={"mapred.uda.provider.hbm.bytes": 3 * size})
+    try:
+        ids = _publish_files(p, tmp_path, "job_9_0101", maps)
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device"})
+        recs, st, _ = run_reduce("h", "job_9_0101", ids, 0, datagen.TEXT, conf=conf)
+        assert recs == expected(maps, 0, datagen.TEXT)
+        hs = json.loads(p.stats())["hbm_store"]
+        assert 0 < hs["loads"] < 6 and hs["declined"] > 0 and hs["evictions"] == 0, hs
+        assert st["device_descriptors"] == hs["loads"] and st["host_fetched_bytes"] > 0, st
+    finally:
+        p.close()
+
+
+def test_bench_api_mof_files(require_gpu, tmp_path):
+    """bench.py --api --mof-dir: TeraSort with Hadoop-written MOF files through the C ABI."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--mof-dir", str(tmp_path), "--rows-per-gpu",
+           "2000000", "--maps-per-gpu", "4", "--reducers", "4", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["validated"] is True and out["mof_files"] is True
+    hs = out["provider"]["hbm_store"]
+    assert hs["loads"] == 4 and hs["declined"] == 0, hs
+    assert out["task0_stats"]["device_descriptors"] == 4
+    assert not list(tmp_path.iterdir())  # files removed with the bench

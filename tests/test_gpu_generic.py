@@ -220,6 +220,48 @@ def test_consumer_gpu_hybrid_checkpoint_resume(require_gpu, tmp_path, monkeypatc
         p.close()
 
 
+def test_checkpoint_resume_with_device_resident_mofs(require_gpu, tmp_path, monkeypatch):
+    """A resumed attempt (LPQ checkpoint of an earlier staged attempt) whose MOFs are now HBM-resident
+    must not take the device-fetch path (it would wait forever for the FETCHes the checkpoint drops,
+    or leave the restored records out): it merges the restored runs on the staged path."""
+    from uda_amd.bridge import UdaConsumer, UdaFallback
+    from uda_amd.utils.mof import read_index, write_mof
+    p = UdaProvider()
+    try:
+        maps = datagen.secondary_sort(num_maps=10, reducers=1, rows_per_map=2000, seed=9)
+        ids, files = [], []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_hdv_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts)
+            p.add_mof_file("job_hdv", mid, path)
+            ids.append(mid)
+            files.append(path)
+        d1 = tmp_path / "ld1"
+        d1.mkdir()
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.merge.bytes": 300_000,
+                "mapred.uda.gpu.spill": "disk", "mapred.uda.lpq.checkpoint": 1}
+        kw = dict(conf=conf, kv_buf_size=8192, local_dirs=(str(d1),))
+        monkeypatch.setenv("UDA_FAULT_LPQ_DONE", "2")
+        c = UdaConsumer(len(ids), "job_hdv", "attempt_job_hdv_r_000000_0", datagen.TEXT, **kw)
+        for m in ids:
+            c.fetch("h", "job_hdv", m, 0)
+        with pytest.raises(UdaFallback, match="injected"):
+            c.wait(60)
+        c.close()
+        monkeypatch.delenv("UDA_FAULT_LPQ_DONE")
+        for mid, path in zip(ids, files):  # the same map outputs, now in HBM (descriptor-servable)
+            with open(path, "rb") as f:
+                p.add_mof_device("job_hdv", mid, f.read(), read_index(path + ".index"))
+        recs, st, _ = run_reduce("h", "job_hdv", ids, 0, datagen.TEXT, timeout=90, **kw)
+        assert st["restored_lpqs"] == 2 and st["device_descriptors"] == 0, st
+        want = sorted((kv for m in maps for kv in m[0]), key=datagen.sort_key(datagen.TEXT))
+        kf = datagen.sort_key(datagen.TEXT)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+        assert sorted(recs) == sorted(want)
+    finally:
+        p.close()
+
+
 def test_consumer_gpu_device_alloc_fault_fails_once(require_gpu, tmp_path, monkeypatch):
     from uda_amd.bridge import UdaConsumer, UdaFallback
     from uda_amd.utils.mof import write_mof
