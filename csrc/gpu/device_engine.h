@@ -163,6 +163,7 @@ class DeviceMerger {
   int last_passes() const { return last_passes_; }
   bool bad_layout();  // synchronizes; true if any record was not TeraSort-shaped
   int64_t max_records() const { return max_records_; }
+  int max_runs() const { return max_runs_; }
   // Cells the single-pass K-way merge handed to its wave-level PQ so far (synchronizes).
   int kway_overflow_cells();
   bool kway_enabled() const { return kway_; }

@@ -9,7 +9,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 
 #include "device_engine.h"
@@ -44,6 +46,69 @@ struct Events {
   }
 };
 
+// Per-device pool of everything a reduce task's device merge allocates: hipFree synchronizes the
+// whole device, so allocating and freeing per task made 16 concurrent tasks stall one another at
+// every task end. Buffers only grow; a workspace whose task failed is dropped, not reused.
+struct FixedWs {
+  std::unique_ptr<DeviceMerger> merger;
+  DeviceBuffer out[2];
+  DeviceBuffer d_bases, d_nrec, d_soff, d_samp, d_bset, d_out, d_bounds, d_runs, flag;
+  hipStream_t s = nullptr;
+  hipEvent_t merged[2] = {nullptr, nullptr};
+  FixedWs() {
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (auto& e : merged) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  ~FixedWs() {
+    if (s) (void)hipStreamSynchronize(s);
+    for (auto e : merged)
+      if (e) (void)hipEventDestroy(e);
+    if (s) (void)hipStreamDestroy(s);
+  }
+  static void ensure(DeviceBuffer& b, size_t bytes) {
+    if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+  }
+};
+
+class FixedWsPool {
+ public:
+  static FixedWsPool& get() {
+    static FixedWsPool* p = new FixedWsPool;  // never destroyed: tasks may outlive static teardown
+    return *p;
+  }
+  std::unique_ptr<FixedWs> acquire(int device) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = free_[device];
+      if (!v.empty()) {
+        auto w = std::move(v.back());
+        v.pop_back();
+        return w;
+      }
+    }
+    return std::make_unique<FixedWs>();
+  }
+  void release(int device, std::unique_ptr<FixedWs> w) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& v = free_[device];
+    if (v.size() < 64) v.push_back(std::move(w));
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<int, std::vector<std::unique_ptr<FixedWs>>> free_;
+};
+
+struct WsLease {
+  int device;
+  std::unique_ptr<FixedWs> w;
+  bool clean = false;
+  explicit WsLease(int d) : device(d), w(FixedWsPool::get().acquire(d)) {}
+  ~WsLease() {
+    if (clean) FixedWsPool::get().release(device, std::move(w));
+  }
+};
+
 // Pinned ring + completion signals borrowed from the device's shared SDMA engine.
 struct Ring {
   SdmaEngine& eng;
@@ -75,7 +140,13 @@ bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
     if (r.nbytes != r.nrec * kTeraRecordBytes) return false;
     max_n = std::max(max_n, r.nrec);
   }
-  DeviceBuffer d_runs(runs.size() * sizeof(RunDesc)), flag(sizeof(int));
+  int device = 0;
+  HIP_CHECK(hipGetDevice(&device));
+  WsLease lease(device);
+  DeviceBuffer& d_runs = lease.w->d_runs;
+  DeviceBuffer& flag = lease.w->flag;
+  FixedWs::ensure(d_runs, runs.size() * sizeof(RunDesc));
+  FixedWs::ensure(flag, sizeof(int));
   HIP_CHECK(hipMemcpyAsync(d_runs.as(), runs.data(), runs.size() * sizeof(RunDesc), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemsetAsync(flag.as(), 0, sizeof(int), s));
   for (size_t b = 0; b < runs.size(); b += 65535)
@@ -83,6 +154,7 @@ bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
   int bad = 0;
   HIP_CHECK(hipMemcpyAsync(&bad, flag.as(), sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  lease.clean = true;
   return bad == 0;
 }
 
@@ -92,8 +164,9 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   HIP_CHECK(hipSetDevice(cfg.device));
   DeviceReduceStats st;
   const double t0 = now_ms();
-  Stream stream;
-  hipStream_t s = stream.s;
+  WsLease lease(cfg.device);
+  FixedWs& ws = *lease.w;
+  hipStream_t s = ws.s;
   const int K = (int)runs.size();
   if (K > 65536) throw std::runtime_error("device reduce: more than 65536 runs");
   int64_t N = 0;
@@ -111,6 +184,7 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   if (N == 0) {
     tail[0] = tail[1] = 0xFF;
     emit(tail.data(), kEofBytes);
+    lease.clean = true;
     return st;
   }
 
@@ -134,9 +208,15 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
         soff[k + 1] = soff[k] + (n > every / 2 ? (n - every / 2 + every - 1) / every : 0);
       }
       const int64_t ns = soff[K];
-      DeviceBuffer d_bases(K * sizeof(uint8_t*)), d_nrec(K * 8), d_soff((K + 1) * 8),
-          d_samp((size_t)std::max<int64_t>(ns, 1) * sizeof(Elem)), d_bset(K * sizeof(int)),
-          d_out((size_t)K * (Q + 1) * 8), d_bounds((size_t)(Q - 1) * sizeof(Elem));
+      DeviceBuffer &d_bases = ws.d_bases, &d_nrec = ws.d_nrec, &d_soff = ws.d_soff, &d_samp = ws.d_samp,
+                   &d_bset = ws.d_bset, &d_out = ws.d_out, &d_bounds = ws.d_bounds;
+      FixedWs::ensure(d_bases, K * sizeof(uint8_t*));
+      FixedWs::ensure(d_nrec, K * 8);
+      FixedWs::ensure(d_soff, (K + 1) * 8);
+      FixedWs::ensure(d_samp, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+      FixedWs::ensure(d_bset, K * sizeof(int));
+      FixedWs::ensure(d_out, (size_t)K * (Q + 1) * 8);
+      FixedWs::ensure(d_bounds, (size_t)(Q - 1) * sizeof(Elem));
       HIP_CHECK(hipMemcpyAsync(d_bases.as(), bases.data(), K * sizeof(uint8_t*), hipMemcpyHostToDevice, s));
       HIP_CHECK(hipMemcpyAsync(d_nrec.as(), nrec.data(), K * 8, hipMemcpyHostToDevice, s));
       HIP_CHECK(hipMemcpyAsync(d_soff.as(), soff.data(), (K + 1) * 8, hipMemcpyHostToDevice, s));
@@ -171,10 +251,18 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   if (trace_rounds)
     std::fprintf(stderr, "[device_reduce pid %d] planned %d runs x %d rounds, %lld records, max round %lld\n", (int)getpid(),
                  K, Q, (long long)N, (long long)max_round);
-  DeviceMerger merger(max_round, K);
-  DeviceBuffer out[2];
-  for (auto& o : out) o.alloc((size_t)std::max<int64_t>(max_round, 1) * kTeraRecordBytes);
-  Events merged;
+  if (!ws.merger || ws.merger->max_records() < max_round || ws.merger->max_runs() < K) {
+    const int64_t mr = std::max<int64_t>(max_round, ws.merger ? ws.merger->max_records() : 0);
+    const int mk = std::max(K, ws.merger ? ws.merger->max_runs() : 0);
+    ws.merger.reset();
+    ws.merger.reset(new DeviceMerger(mr, mk));
+  }
+  DeviceMerger& merger = *ws.merger;
+  DeviceBuffer* out = ws.out;
+  for (int i = 0; i < 2; ++i) FixedWs::ensure(out[i], (size_t)std::max<int64_t>(max_round, 1) * kTeraRecordBytes);
+  struct {
+    hipEvent_t* e;
+  } merged{ws.merged};
   const int S = std::max(2, cfg.pinned_slots);
   Ring ring(SdmaEngine::for_device(cfg.device), (size_t)piece * S, S);
   st.plan_ms = now_ms() - t0;
@@ -245,6 +333,8 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   }
   if (merger.bad_layout()) throw std::runtime_error("device reduce: non-TeraSort record in a FIXED10 run");
   st.records = N;
+  HIP_CHECK(hipStreamSynchronize(s));
+  lease.clean = true;
   return st;
 }
 
