@@ -89,6 +89,11 @@ def parse_args(argv=None):
                     help="drive the shuffle only through the UdaBridge C ABI (uda_start/INIT/FETCH/dataFromUda) "
                          "with HBM-resident MOFs: one NetMerger handle per reduce task (1 GPU)")
     ap.add_argument("--round-mb", type=int, default=2048, help="--api: device merge round size per reduce task")
+    ap.add_argument("--workload", choices=("terasort", "secondary"), default="terasort",
+                    help="--api: 'secondary' = BASELINE config #5: variable-length Text keys with long common "
+                         "prefixes, --skew of every map's records to reduce task 0, merged on the device in "
+                         "key-range rounds of --round-mb")
+    ap.add_argument("--skew", type=float, default=0.6, help="--api --workload secondary: share of reduce task 0")
     ap.add_argument("--mof-dir", default="",
                     help="--api: write every map output as a file.out under this directory; the provider finds "
                          "them through getPathUda (Hadoop-written MOFs) and serves them from its HBM store")
@@ -309,6 +314,7 @@ def run_api(args, ctx) -> int:
         hbm_bytes = int(per_rank * 1.25) if args.provider_hbm_gb < 0 else int(args.provider_hbm_gb * 1e9)
     b = native().ApiTeraSortBench(dict(device=device, maps=args.maps_per_gpu, reducers=R,
                                        mof_dir=args.mof_dir, provider_hbm_bytes=hbm_bytes,
+                                       workload=args.workload, skew=args.skew,
                                        records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
                                        round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
                                        transport="tcp" if world > 1 else "loopback",
@@ -348,8 +354,9 @@ def run_api(args, ctx) -> int:
         if args.verbose and rank == 0:
             print(f"# validated step: {json.dumps(vst)}", file=sys.stderr, flush=True)
     records = sum(ctx.all_gather_object(int(stats[0]["records"])))
+    nbytes = sum(ctx.all_gather_object(int(stats[0]["bytes"])))  # delivered record bytes (EOF markers included)
     ms_per_step = elapsed * 1000.0 / max(1, args.steps)
-    gbps = records * RECORD_BYTES / (ms_per_step / 1000.0) / 1e9
+    gbps = nbytes / (ms_per_step / 1000.0) / 1e9
     ctx.barrier()  # every rank's reduce tasks are done with the other ranks' providers
     if rank == 0:
         out = {
@@ -365,9 +372,16 @@ def run_api(args, ctx) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bytes",
-            "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "data": ("synthetic secondary-sort map outputs generated in HBM: 22-62 byte Text keys sharing "
+                     "5-50 byte prefixes, 0-120 byte values, "
+                     f"{args.skew:.0%} of every map's records to reduce task 0")
+                    if args.workload == "secondary" else
+                    "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),
+            "max_task_ws_gb": round(max(s["max_task_ws_bytes"] for s in stats) / 1e9, 3),
+            "max_task_rounds": int(max(s["max_task_rounds"] for s in stats)),
             "config": {
-                "model": "terasort",
+                "model": "secondary-sort" if args.workload == "secondary" else "terasort",
                 "global_batch": records,
                 "seq_len": RECORD_BYTES,
                 "parallelism": f"dp{world}",

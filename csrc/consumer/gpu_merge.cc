@@ -41,6 +41,7 @@
 #include "../gpu/device_reduce.h"
 #include "../gpu/device_engine.h"
 #include "../gpu/generic_merger.h"
+#include "../gpu/generic_rounds.h"
 #include "../gpu/sdma.h"
 #include "reduce_task.h"
 #include "uda/aio.h"
@@ -82,6 +83,7 @@ struct DeviceWorkspace {
   gpu::GenericMerger merger;
   gpu::DeviceBlockDecoder decoder;
   gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
+  gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
   ~DeviceWorkspace() {
@@ -1385,7 +1387,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     st_.merge_path = "device-fixed10";
     return true;
   }
-  // ---- any other key class: the generic merge tree, reading the partitions where they live
+  // ---- any other key class: the generic merge, reading the partitions where they live, in key-range
+  // rounds of at most mapred.uda.gpu.round.bytes of input (generic_rounds.h), so the device working
+  // set (output + ~80 B/record of merge metadata) is bounded by the round, not by the partition
   PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
@@ -1398,12 +1402,16 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     rlen.push_back(p->part_len);
     total += p->part_len;
   }
-  DeviceWorkspace::ensure(ws.out, total);
+  const int64_t round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+  const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
+  DeviceWorkspace::ensure(ws.out, rplan.max_round_bytes);
   const int64_t kv = kv_buf_size_ - kEofBytes;
   std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
   bool eof_sent = false;
+  bool last_outer = false;  // the key-range round being merged is the last one
   // merged key-range rounds go out on the copy stream while the next round merges
-  auto deliver_round = [&](const std::vector<int64_t>& cuts, int64_t, bool last) {
+  auto deliver_round = [&](const std::vector<int64_t>& cuts, int64_t, bool last_inner) {
+    const bool last = last_inner && last_outer;
     DeviceMergeOut m;
     m.cuts = cuts;
     const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
@@ -1422,10 +1430,38 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       }
     });
   };
-  gpu::GenericMergeResult r =
-      ws.merger.merge(rptr, rlen, (int)kind_, ws.out.as<uint8_t>(), total, kv, s, deliver_round);
   DeviceMergeOut m;
-  m.records = r.records;
+  for (int q = 0; q < rplan.rounds; ++q) {
+    std::vector<const uint8_t*> sp;
+    std::vector<int64_t> sl;
+    for (size_t k = 0; k < rptr.size(); ++k) {
+      const int64_t b = rplan.at((int)k, q), e = rplan.at((int)k, q + 1);
+      if (e > b) {
+        sp.push_back(rptr[k] + b);
+        sl.push_back(e - b);
+      }
+    }
+    last_outer = q + 1 == rplan.rounds;
+    if (sp.empty()) continue;
+    const auto tq = std::chrono::steady_clock::now();
+    gpu::GenericMergeResult r = ws.merger.merge(sp, sl, (int)kind_, ws.out.as<uint8_t>(), (int64_t)ws.out.size(), kv, s,
+                                                deliver_round);
+    m.records += r.records;
+    static const bool trace = std::getenv("UDA_DEVICE_REDUCE_TRACE") != nullptr;  // tools: per-round lines
+    if (trace)
+      std::fprintf(stderr, "[generic rounds] round %d/%d: %ld records, %.1f ms (d2h wait %.1f, sink %.1f ms so far)\n", q,
+                   rplan.rounds, (long)r.records,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count(), ws.d2h_ms,
+                   ws.sink_ms);
+  }
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.rpq_rounds = rplan.rounds;
+    st_.gpu_ws_bytes = (int64_t)ws.out.size() + ws.merger.workspace_bytes();
+    st_.gpu_device_ms = rplan.plan_ms;
+    st_.gpu_d2h_wait_ms = ws.d2h_ms;
+    st_.gpu_sink_ms = ws.sink_ms;
+  }
   if (!eof_sent) {
     tail[0] = tail[1] = 0xFF;
     if (sink(tail.data(), kEofBytes) != 0) throw UdaError("dataFromUda callback failed");

@@ -11,10 +11,12 @@
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <atomic>
 #include <thread>
 
 #include "device_engine.h"
 #include "j2c_sink.h"
+#include "secgen.h"
 #include "uda/cmd.h"
 #include "uda/uda_bridge.h"
 
@@ -151,7 +153,10 @@ std::string ApiTeraSortBench::provider_stats() const {
   return js;
 }
 
-int64_t ApiTeraSortBench::store_bytes() const { return gen_ ? gen_->store_bytes() : 0; }
+int64_t ApiTeraSortBench::store_bytes() const {
+  if (sec_store_) return sec_store_bytes_;
+  return gen_ ? gen_->store_bytes() : 0;
+}
 
 std::vector<int64_t> ApiTeraSortBench::local_partition_records() const {
   return gen_ ? gen_->local_dest_records() : std::vector<int64_t>();
@@ -168,6 +173,11 @@ void ApiTeraSortBench::setup() {
   if (cfg_.world > 1 && cfg_.transport != "tcp") throw std::runtime_error("api bench: world > 1 needs the tcp transport");
   // map phase stand-in: `maps` MOFs x (world * reducers) total-order partitions in this rank's HBM
   const int P = cfg_.world * cfg_.reducers;
+  if (cfg_.workload == "secondary") {
+    setup_secondary();
+    return;
+  }
+  if (cfg_.workload != "terasort") throw std::runtime_error("api bench: unknown workload " + cfg_.workload);
   ShuffleConfig sc;
   sc.device = cfg_.device;
   sc.world = P;              // partitions per MOF (no exchange is ever run on this job)
@@ -243,6 +253,54 @@ void ApiTeraSortBench::setup() {
   }
 }
 
+// Secondary-sort map outputs (secgen.h) generated straight into one HBM store and registered as
+// device MOFs: the reduce tasks take the generic-key device merge (key-range rounds).
+void ApiTeraSortBench::setup_secondary() {
+  if (cfg_.world != 1) throw std::runtime_error("api bench: the secondary workload runs with world 1");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const int P = cfg_.reducers;
+  const SecGenPlan plan = secgen_plan(cfg_.maps, P, cfg_.records_per_map, cfg_.skew, cfg_.seed);
+  sec_store_bytes_ = plan.store_bytes();
+  sec_store_.reset(new DeviceBuffer((size_t)sec_store_bytes_));
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  secgen_write(plan, sec_store_->as<uint8_t>(), s);
+  HIP_CHECK(hipStreamDestroy(s));
+  expected_.assign((size_t)P, 0);
+  for (int m = 0; m < cfg_.maps; ++m)
+    for (int q = 0; q < P; ++q) expected_[(size_t)q] += plan.nrec[(size_t)m * P + q];
+  ConfTable& conf = bench_conf(cfg_);
+  auto* pctx = new ProviderCtx{&conf, this};
+  provider_ctx_ = pctx;
+  uda_callbacks cb{};
+  cb.ctx = pctx;
+  cb.get_conf = provider_conf_cb;
+  cb.get_path = provider_path_cb;
+  cb.log = log_cb;
+  const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
+                                         "-m", "1", "-g", "/tmp", "-s", "1024"};
+  auto av = cargs(args);
+  uda_handle* h = uda_start(0, (int)av.size(), av.data(), 2, 0, &cb);
+  if (!h) throw std::runtime_error("api bench: uda_start (provider) failed");
+  provider_ = h;
+  map_ids_.clear();
+  for (int m = 0; m < cfg_.maps; ++m) {
+    const std::string id = map_id(m);
+    map_ids_.push_back(id);
+    std::vector<int64_t> index;
+    int64_t off = 0;
+    for (int q = 0; q < P; ++q) {
+      const int64_t b = plan.part_bytes[(size_t)m * P + q];
+      index.insert(index.end(), {off, b, b});
+      off += b;
+    }
+    const uint8_t* base = sec_store_->as<uint8_t>() + plan.mof_off[(size_t)m];
+    const int64_t len = plan.mof_off[(size_t)m + 1] - plan.mof_off[(size_t)m];
+    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), base, len, index.data(), P, cfg_.device) != 0)
+      throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
+  }
+}
+
 std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string* info) {
   const int R = cfg_.reducers;
   const int W = cfg_.world;
@@ -250,6 +308,27 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   if (W > 1 && (int)peers_.size() != W) throw std::runtime_error("api bench: provider addresses not set");
   J2CSink sink(R, cfg_.kv_buf_bytes);
   sink.set_check_order(validate);
+  sink.set_key_kind(1);  // Text: content order (TeraSort's fixed keys order the same either way)
+  // device-wide HBM in use, sampled through the step (the peak includes the map-output store)
+  std::atomic<bool> sampling{true};
+  std::atomic<int64_t> peak_used{0};
+  std::thread sampler([&] {
+    (void)hipSetDevice(cfg_.device);
+    while (sampling.load()) {
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+        peak_used.store(std::max<int64_t>(peak_used.load(), (int64_t)(total_b - free_b)));
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  });
+  struct SamplerGuard {
+    std::atomic<bool>& on;
+    std::thread& t;
+    ~SamplerGuard() {
+      on = false;
+      if (t.joinable()) t.join();
+    }
+  } sampler_guard{sampling, sampler};
   ConfTable& conf = bench_conf(cfg_);
   std::mutex mu;
   std::condition_variable cv;
@@ -316,13 +395,24 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   }
   const double t1 = now_ms();
   std::string paths;
+  double max_ws = 0, max_rounds = 0;
   for (int r = 0; r < R; ++r) {
     if (!handles[r]) continue;
     (void)uda_reduce_exit(handles[r]);  // joins the merge thread: its stats are final after this
     char js[4096];
-    if (r == 0 && uda_stats_json(handles[r], js, sizeof(js)) > 0) paths = js;
+    if (uda_stats_json(handles[r], js, sizeof(js)) > 0) {
+      if (r == 0) paths = js;
+      auto num = [&](const char* key) {
+        const char* q = std::strstr(js, key);
+        return q ? std::atof(q + std::strlen(key)) : 0.0;
+      };
+      max_ws = std::max(max_ws, num("\"gpu_ws_bytes\":"));
+      max_rounds = std::max(max_rounds, num("\"rpq_rounds\":"));
+    }
     uda_destroy(handles[r]);
   }
+  sampling = false;
+  if (sampler.joinable()) sampler.join();
   const double t2 = now_ms();
   for (int r = 0; r < R; ++r) {
     if (!errors[r].empty()) throw std::runtime_error("reduce task " + std::to_string(r) + ": " + errors[r]);
@@ -346,6 +436,9 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   out["records"] = recs;
   out["buffers"] = bufs;
   out["order_errors"] = validate ? oerr : -1;
+  out["peak_hbm_bytes"] = (double)peak_used.load();
+  out["max_task_ws_bytes"] = max_ws;
+  out["max_task_rounds"] = max_rounds;
   if (info) *info = paths;
   return out;
 }

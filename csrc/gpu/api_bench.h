@@ -26,6 +26,7 @@ namespace gpu {
 
 class ShuffleJob;
 class J2CSink;
+class DeviceBuffer;
 
 struct ApiBenchConfig {
   int device = 0;
@@ -50,6 +51,10 @@ struct ApiBenchConfig {
   // file into HBM on first touch and answers descriptor fetches from it
   std::string mof_dir;
   int64_t provider_hbm_bytes = 0;
+  // "terasort" or "secondary": variable-length Text keys with long common prefixes, `skew` of every
+  // map's records in reduce task 0 (BASELINE config #5; device generator secgen.h; world 1)
+  std::string workload = "terasort";
+  double skew = 0.6;
 };
 
 class ApiTeraSortBench {
@@ -77,7 +82,10 @@ class ApiTeraSortBench {
   std::vector<std::string> map_ids_;
   std::vector<std::string> peers_;
   std::vector<std::vector<uint8_t>> host_mofs_;  // host_mofs: the MOFs' bytes in host memory
+  std::unique_ptr<DeviceBuffer> sec_store_;  // secondary workload: the MOFs in HBM
+  int64_t sec_store_bytes_ = 0;
   std::string map_id(int global_map) const;
+  void setup_secondary();
 
  public:
   // getPathUda of the provider (mof_dir mode)

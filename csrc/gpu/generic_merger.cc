@@ -29,6 +29,16 @@ void GenericMerger::reserve(int64_t records, int runs) {
   cap_runs_ = std::max(runs, cap_runs_);
 }
 
+int64_t GenericMerger::workspace_bytes() const {
+  int64_t b = 0;
+  for (const DeviceBuffer* x : {&eoff_, &rounds_, &elems_a_, &elems_b_, &splits_, &sizes_, &out_off_, &scan_tmp_, &cuts_,
+                                &offsets_, &tables_, &side_, &ck_, &f1ws_})
+    b += (int64_t)x->size();
+  for (const auto& k : gk_)
+    for (const DeviceBuffer* x : {&k.tab, &k.samp, &k.sa, &k.sb, &k.bounds, &k.split, &k.hist, &k.flag}) b += (int64_t)x->size();
+  return b;
+}
+
 GenericMerger::~GenericMerger() {
   for (hipEvent_t e : round_ev_) (void)hipEventDestroy(e);
 }

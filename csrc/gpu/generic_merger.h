@@ -42,6 +42,8 @@ class GenericMerger {
 
   // runs the last merge indexed with the serial F1 walk (records longer than the parallel entry table)
   int f1_serial_runs() const { return f1_serial_runs_; }
+  // device bytes held by this merger's workspaces
+  int64_t workspace_bytes() const;
 
  private:
   int f1_serial_runs_ = 0;

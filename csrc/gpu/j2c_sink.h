@@ -57,9 +57,13 @@ class J2CSink {
       }
       if (kl < 0 || vl < 0) return fail(s, kBadFraming);
       if (p + a + b + kl + vl > len) return fail(s, kBadFraming);
-      if (order) {  // serialized key bytes ascend within a reducer
+      if (order) {  // keys ascend within a reducer (content bytes after the key class's length prefix)
         const uint8_t* k = kb + p + a + b;
-        const int kn = (int)std::min<int64_t>(kl, (int64_t)sizeof(s.last_key));
+        int64_t ko = 0;
+        if (key_kind_ == 1 && kl > 0) ko = std::min<int64_t>(kl, vint_decode_size((int)(int8_t)k[0]));  // Text
+        if (key_kind_ == 2) ko = std::min<int64_t>(kl, 4);                                              // BytesWritable
+        k += ko;
+        const int kn = (int)std::min<int64_t>(kl - ko, (int64_t)sizeof(s.last_key));
         if (s.has_last) {
           const int n = std::min(kn, s.last_len);
           const int c = std::memcmp(s.last_key, k, (size_t)n);
@@ -88,9 +92,12 @@ class J2CSink {
       s.error = kOk;
     }
   }
-  // Also check that serialized keys ascend bytewise within every reducer (the first 64 bytes). That
-  // is the key order for fixed-length keys such as TeraSort's 10-byte Text keys.
+  // Also check that keys ascend within every reducer (the first 256 bytes, see set_key_kind). Raw
+  // serialized bytes are the key order for fixed-length keys such as TeraSort's 10-byte Text keys.
   void set_check_order(bool on) { check_order_ = on; }
+  // Key class of the order check: 0 raw serialized bytes (default), 1 Text, 2 BytesWritable: the
+  // comparator's content bytes (first 256), then their length.
+  void set_key_kind(int k) { key_kind_ = k; }
   int64_t order_errors(int r) const { return st_[(size_t)r].order_errors; }
   int64_t records(int r) const { return st_[(size_t)r].records; }
   int64_t bytes(int r) const { return st_[(size_t)r].bytes; }
@@ -107,7 +114,7 @@ class J2CSink {
     int error = kOk;
     bool has_last = false;
     int last_len = 0;
-    uint8_t last_key[64];
+    uint8_t last_key[256];
   };
   static int fail(State& s, int e) {
     if (s.error == kOk) s.error = e;
@@ -115,6 +122,7 @@ class J2CSink {
   }
   int64_t kv_;
   bool check_order_ = false;
+  int key_kind_ = 0;
   std::vector<State> st_;
 };
 

@@ -881,6 +881,8 @@ PYBIND11_MODULE(_uda_native, m) {
         get("provider_workers", c.provider_workers);
         get("mof_dir", c.mof_dir);
         get("provider_hbm_bytes", c.provider_hbm_bytes);
+        get("workload", c.workload);
+        get("skew", c.skew);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())

@@ -68,6 +68,33 @@ def test_generic_keys_device_mofs(require_gpu, provider):
     assert st["merge_path"] == "device-generic"
 
 
+@pytest.mark.parametrize("gen,key_class", [("secondary_sort", datagen.TEXT), ("wordcount", datagen.TEXT),
+                                           ("bytes", datagen.BYTES)])
+@pytest.mark.parametrize("round_bytes", [64 << 10, 1 << 20])
+def test_generic_device_merge_key_range_rounds(require_gpu, provider, gen, key_class, round_bytes):
+    """Generic keys over HBM-resident MOFs merged in key-range rounds of at most round_bytes of input:
+    the rounds concatenate to the total order (duplicate-heavy keys, long common prefixes, binary
+    keys), and the device working set follows the round size, not the partition size."""
+    job = f"job_9_02{len(gen)}{round_bytes % 7}"
+    if gen == "secondary_sort":
+        maps = datagen.secondary_sort(num_maps=9, reducers=1, rows_per_map=3000, seed=41)
+    elif gen == "wordcount":
+        maps = datagen.wordcount(num_maps=9, reducers=1, words_per_map=4000, seed=41)
+    else:
+        maps = datagen.bytes_writable(num_maps=9, reducers=1, rows_per_map=2500, seed=41)
+    ids = _publish_device(provider, job, maps)
+    conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.round.bytes": round_bytes})
+    recs, st, _ = run_reduce("h", job, ids, 0, key_class, conf=conf, kv_buf_size=32 << 10)
+    cpu, _, _ = run_reduce("h", job, ids, 0, key_class, kv_buf_size=32 << 10)
+    kf = datagen.sort_key(key_class)
+    assert [kf(kv) for kv in recs] == [kf(kv) for kv in cpu] and sorted(recs) == sorted(cpu)
+    total = st["bytes_fetched"]
+    assert st["merge_path"] == "device-generic" and st["device_descriptors"] == 9
+    assert st["rpq_rounds"] >= min(4, total // round_bytes), st
+    if round_bytes == 64 << 10 and total > 2 << 20:
+        assert st["gpu_ws_bytes"] < total, st  # bounded by the round, not the partition
+
+
 def test_mixed_host_and_device_mofs(require_gpu, provider):
     """Device fetch falls back to bytes for MOFs the provider holds in host memory."""
     maps = datagen.terasort(num_maps=6, reducers=1, rows_per_map=3000, seed=5)
@@ -262,3 +289,17 @@ def test_bench_api_mof_files(require_gpu, tmp_path):
     assert hs["loads"] == 4 and hs["declined"] == 0, hs
     assert out["task0_stats"]["device_descriptors"] == 4
     assert not list(tmp_path.iterdir())  # files removed with the bench
+
+
+def test_bench_api_secondary_sort_skew(require_gpu):
+    """bench.py --api --workload secondary: config #5 through the C ABI (device-generated variable-length
+    Text MOFs, 60% of the records in reduce task 0, key-range rounds bounding the merge's HBM)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--workload", "secondary", "--rows-per-gpu",
+           "6000000", "--maps-per-gpu", "8", "--reducers", "4", "--round-mb", "64", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["validated"] is True and out["config"]["model"] == "secondary-sort"
+    assert out["task0_stats"]["merge_path"] == "device-generic"
+    assert out["max_task_rounds"] > 1 and out["max_task_ws_gb"] > 0
+    assert out["config"]["global_batch"] == 6000000

@@ -90,6 +90,20 @@ def secondary_sort(num_maps: int, reducers: int, rows_per_map: int, seed: int = 
     return _finish(maps, TEXT)
 
 
+def bytes_writable(num_maps: int, reducers: int, rows_per_map: int, seed: int = 4):
+    """BytesWritable keys (4-byte big-endian length + raw bytes, any byte values, shared prefixes)."""
+    rng = random.Random(seed)
+    maps = []
+    for _ in range(num_maps):
+        parts = [[] for _ in range(reducers)]
+        for _ in range(rows_per_map):
+            body = bytes([rng.choice((0, 1, 255))]) * rng.randint(0, 12) + bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 20)))
+            k = len(body).to_bytes(4, "big") + body
+            parts[partition_of(k, reducers)].append((k, bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 40)))))
+        maps.append(parts)
+    return _finish(maps, BYTES)
+
+
 def streams(maps) -> list[list[bytes]]:
     """Encode per-map per-reducer record lists into IFile partition streams (with EOF)."""
     return [[encode_stream(part) for part in m] for m in maps]
