@@ -79,7 +79,7 @@ struct SpillRun {
 // allocated once at the high-water mark instead of per merge (hipMalloc/hipFree of GBs costs ms and
 // hipFree synchronizes the device).
 struct DeviceWorkspace {
-  gpu::DeviceBuffer in, out, packed;
+  gpu::DeviceBuffer in, out, packed, out2;  // out2: second output of the generic key-range rounds
   gpu::GenericMerger merger;
   gpu::DeviceBlockDecoder decoder;
   gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
@@ -318,7 +318,9 @@ class DevicePool {
   }
 
  private:
-  static constexpr size_t kMaxIdle = 8;  // e.g. 4 concurrent hybrid tasks: 4 workspaces, 8 stagers
+  // 16 concurrent reduce tasks per GPU (the bench shape) must find their workspaces again: a dropped
+  // one is freed, and hipFree synchronizes the whole device under the other tasks
+  static constexpr size_t kMaxIdle = 32;
   std::mutex mu_;
   std::map<int, std::vector<std::unique_ptr<T>>> idle_;
 };
@@ -501,10 +503,15 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
 // while fn(piece k) consumes it. fn(ptr, first_cut, last_cut) gets the bytes of cuts
 // [first_cut, last_cut] (ptr = byte cuts[first_cut]).
 template <typename Fn>
-void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&& fn) {
+void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&& fn, const uint8_t* src = nullptr) {
   const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
   if (nb == 0) return;
-  if (ws.ring.size() < (size_t)(2 * kPieceBytes)) ws.ring.alloc((size_t)(2 * kPieceBytes));
+  const uint8_t* out = src ? src : ws.out.as<uint8_t>();
+  if (ws.ring.size() < (size_t)(2 * kPieceBytes)) {  // on the GPU's NUMA node, like the consumer copying out of it
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    ws.ring.alloc_on_node((size_t)(2 * kPieceBytes), gpu::device_numa_node(dev));
+  }
   for (auto& e : ws.piece_ev)
     if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // piece boundaries in cut indices
@@ -557,11 +564,10 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
     if (e - b > kPieceBytes) throw UdaError("record larger than the D2H piece");
     if (sp.eng) {
       gpu::SdmaEngine::arm(sp.sig[slot], sp.eng->parts((size_t)(e - b), 1));
-      sp.eng->copy_d2h(ws.ring.as<uint8_t>() + slot * kPieceBytes, ws.out.as<uint8_t>() + b, (size_t)(e - b),
-                       sp.sig[slot], 1);
+      sp.eng->copy_d2h(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b), sp.sig[slot], 1);
       return;
     }
-    HIP_CHECK(hipMemcpyAsync(ws.ring.as<uint8_t>() + slot * kPieceBytes, ws.out.as<uint8_t>() + b, (size_t)(e - b),
+    HIP_CHECK(hipMemcpyAsync(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(ws.piece_ev[slot], s));
   };
@@ -1403,35 +1409,109 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     total += p->part_len;
   }
   const int64_t round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+  if (total > round_bytes) {
+    // a task holding more than a round (a skewed partition) is the job's long pole: its merge kernels
+    // go first when the device is shared with the other tasks' merges
+    int lo = 0, hi = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipStreamDestroy(sg.s));
+    sg.s = nullptr;
+    HIP_CHECK(hipStreamCreateWithPriority(&sg.s, hipStreamNonBlocking, hi));
+    s = sg.s;
+  }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
+  // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
+  // dataFromUda): the consumer's work (the reduce task's bound when one task holds most of the data)
+  // never waits for the merge driver, and the merge reuses an output only after its delivery.
   DeviceWorkspace::ensure(ws.out, rplan.max_round_bytes);
+  if (rplan.rounds > 1) DeviceWorkspace::ensure(ws.out2, rplan.max_round_bytes);
+  gpu::DeviceBuffer* outs[2] = {&ws.out, rplan.rounds > 1 ? &ws.out2 : &ws.out};
   const int64_t kv = kv_buf_size_ - kEofBytes;
   std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
   bool eof_sent = false;
-  bool last_outer = false;  // the key-range round being merged is the last one
-  // merged key-range rounds go out on the copy stream while the next round merges
-  auto deliver_round = [&](const std::vector<int64_t>& cuts, int64_t, bool last_inner) {
-    const bool last = last_inner && last_outer;
-    DeviceMergeOut m;
-    m.cuts = cuts;
-    const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-    stream_out(ws, m, ws.copy_stream(), [&](const uint8_t* piece, size_t c0, size_t c1) {
-      for (size_t j = c0; j < c1; ++j) {
-        const uint8_t* p = piece + (m.cuts[j] - m.cuts[c0]);
-        int64_t len = m.cuts[j + 1] - m.cuts[j];
-        if (last && j + 1 == nb) {
-          std::memcpy(tail.data(), p, (size_t)len);
-          tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
-          p = tail.data();
-          len += kEofBytes;
-          eof_sent = true;
+  struct DJob {
+    const uint8_t* src;
+    std::vector<int64_t> cuts;
+    bool last;          // the task's final records: the EOF marker goes after them
+    bool end_of_round;  // the key-range round's output is fully handed over after this job
+  };
+  std::mutex dmu;
+  std::condition_variable dcv;
+  std::deque<DJob> djobs;
+  int delivered = 0;  // key-range rounds fully delivered
+  bool dstop = false;
+  std::string derr;
+  std::thread dthr([&] {
+    try {
+      gpu::bind_thread_to_numa(gpu::device_numa_node(device));  // the D2H ring and the consumer copies
+      HIP_CHECK(hipSetDevice(device));
+      for (;;) {
+        DJob j;
+        {
+          std::unique_lock<std::mutex> lk(dmu);
+          dcv.wait(lk, [&] { return dstop || !djobs.empty(); });
+          if (djobs.empty()) return;
+          j = std::move(djobs.front());
+          djobs.pop_front();
         }
-        if (sink(p, len) != 0) throw UdaError("dataFromUda callback failed");
+        DeviceMergeOut m;
+        m.cuts = std::move(j.cuts);
+        const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
+        stream_out(ws, m, ws.copy_stream(), [&](const uint8_t* piece, size_t c0, size_t c1) {
+          for (size_t x = c0; x < c1; ++x) {
+            const uint8_t* p = piece + (m.cuts[x] - m.cuts[c0]);
+            int64_t len = m.cuts[x + 1] - m.cuts[x];
+            if (j.last && x + 1 == nb) {
+              std::memcpy(tail.data(), p, (size_t)len);
+              tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
+              p = tail.data();
+              len += kEofBytes;
+              eof_sent = true;
+            }
+            if (sink(p, len) != 0) throw UdaError("dataFromUda callback failed");
+          }
+        }, j.src);
+        if (j.end_of_round) {
+          std::lock_guard<std::mutex> g(dmu);
+          ++delivered;
+          dcv.notify_all();
+        }
       }
-    });
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(dmu);
+      derr = e.what();
+      dstop = true;
+      dcv.notify_all();
+    }
+  });
+  struct DJoin {
+    std::thread& t;
+    std::mutex& mu;
+    std::condition_variable& cv;
+    bool& stop;
+    ~DJoin() {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+      }
+      cv.notify_all();
+      if (t.joinable()) t.join();
+    }
+  } djoin{dthr, dmu, dcv, dstop};
+  auto push = [&](DJob j) {
+    std::lock_guard<std::mutex> g(dmu);
+    if (!derr.empty()) throw UdaError("delivery failed: " + derr);
+    djobs.push_back(std::move(j));
+    dcv.notify_all();
   };
   DeviceMergeOut m;
   for (int q = 0; q < rplan.rounds; ++q) {
+    {
+      std::unique_lock<std::mutex> lk(dmu);  // outs[q & 1] held round q - 2: delivered?
+      dcv.wait(lk, [&] { return delivered >= q - 1 || !derr.empty(); });
+      if (!derr.empty()) throw UdaError("delivery failed: " + derr);
+    }
     std::vector<const uint8_t*> sp;
     std::vector<int64_t> sl;
     for (size_t k = 0; k < rptr.size(); ++k) {
@@ -1441,23 +1521,34 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         sl.push_back(e - b);
       }
     }
-    last_outer = q + 1 == rplan.rounds;
-    if (sp.empty()) continue;
+    const bool last_outer = q + 1 == rplan.rounds;
+    if (sp.empty()) {
+      push(DJob{nullptr, {}, false, true});
+      continue;
+    }
+    const uint8_t* dst = outs[q & 1]->as<uint8_t>();
     const auto tq = std::chrono::steady_clock::now();
-    gpu::GenericMergeResult r = ws.merger.merge(sp, sl, (int)kind_, ws.out.as<uint8_t>(), (int64_t)ws.out.size(), kv, s,
-                                                deliver_round);
+    gpu::GenericMergeResult r = ws.merger.merge(
+        sp, sl, (int)kind_, outs[q & 1]->as<uint8_t>(), (int64_t)outs[q & 1]->size(), kv, s,
+        [&](const std::vector<int64_t>& cuts, int64_t, bool last_inner) {
+          push(DJob{dst, cuts, last_inner && last_outer, last_inner});
+        });
     m.records += r.records;
     static const bool trace = std::getenv("UDA_DEVICE_REDUCE_TRACE") != nullptr;  // tools: per-round lines
     if (trace)
-      std::fprintf(stderr, "[generic rounds] round %d/%d: %ld records, %.1f ms (d2h wait %.1f, sink %.1f ms so far)\n", q,
-                   rplan.rounds, (long)r.records,
-                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count(), ws.d2h_ms,
-                   ws.sink_ms);
+      std::fprintf(stderr, "[generic rounds] round %d/%d: %ld records merged in %.1f ms\n", q, rplan.rounds,
+                   (long)r.records, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count());
+  }
+  {
+    std::unique_lock<std::mutex> lk(dmu);
+    dcv.wait(lk, [&] { return delivered >= rplan.rounds || !derr.empty(); });
+    if (!derr.empty()) throw UdaError("delivery failed: " + derr);
   }
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.rpq_rounds = rplan.rounds;
-    st_.gpu_ws_bytes = (int64_t)ws.out.size() + ws.merger.workspace_bytes();
+    st_.gpu_ws_bytes = (int64_t)ws.out.size() + (rplan.rounds > 1 ? (int64_t)ws.out2.size() : 0) +
+                       ws.merger.workspace_bytes();
     st_.gpu_device_ms = rplan.plan_ms;
     st_.gpu_d2h_wait_ms = ws.d2h_ms;
     st_.gpu_sink_ms = ws.sink_ms;

@@ -162,6 +162,15 @@ void PinnedBuffer::alloc(size_t bytes) {
   size_ = bytes;
 }
 
+void PinnedBuffer::alloc_on_node(size_t bytes, int node) {
+  if (ptr_) (void)hipHostFree(ptr_);
+  ptr_ = nullptr;
+  size_ = 0;
+  if (bytes == 0) return;
+  ptr_ = hip_host_alloc_on_node(bytes, node);  // hipHostMalloc under a preferred-node policy
+  size_ = bytes;
+}
+
 std::string nccl_unique_id() {
   ncclUniqueId id;
   ncclResult_t r = ncclGetUniqueId(&id);

@@ -96,6 +96,8 @@ class PinnedBuffer {
     o.size_ = 0;
   }
   void alloc(size_t bytes);
+  // pinned pages placed on NUMA node `node` (< 0: anywhere)
+  void alloc_on_node(size_t bytes, int node);
   template <typename T = uint8_t>
   T* as() const {
     return reinterpret_cast<T*>(ptr_);

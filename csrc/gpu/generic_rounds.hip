@@ -236,9 +236,16 @@ GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, c
   for (int64_t i = 0; i < ns; ++i)
     if (kl[(size_t)i] >= 0) sk.emplace_back(reinterpret_cast<const char*>(&keys[(size_t)i * kSampleKey]), (size_t)kl[(size_t)i]);
   std::sort(sk.begin(), sk.end());  // unsigned bytewise, a prefix first: the key order on content
+  // round 0 takes an eighth of a round's share: its merge is the only one not overlapped with a
+  // delivery, so the consumer starts early; rounds 1..want split the rest evenly
   std::vector<std::string> bounds;
-  for (int q = 1; q < want && !sk.empty(); ++q) {
-    const std::string& b = sk[(size_t)std::min<int64_t>((int64_t)sk.size() - 1, (int64_t)sk.size() * q / want)];
+  std::vector<double> cut;
+  const double first = 1.0 / (8.0 * want);
+  cut.push_back(first);
+  for (int q = 1; q < want; ++q) cut.push_back(first + (1.0 - first) * q / want);
+  for (double f : cut) {
+    if (sk.empty()) break;
+    const std::string& b = sk[(size_t)std::min<int64_t>((int64_t)sk.size() - 1, (int64_t)(f * (double)sk.size()))];
     if (bounds.empty() || b > bounds.back()) bounds.push_back(b);
   }
   if (bounds.empty()) return trivial();

@@ -43,6 +43,17 @@ class J2CSink {
     std::memcpy(kb, data, (size_t)len);  // dataFromUda: DirectByteBuffer -> KVBuf
     int64_t p = 0, recs = 0;
     const bool order = check_order_;
+    if (!order) {  // fast path of the walk below: both VInt headers one byte (lengths < 128)
+      while (p + 2 <= len) {
+        const int8_t k1 = (int8_t)kb[p], v1 = (int8_t)kb[p + 1];
+        if ((k1 | v1) < 0) break;  // multi-byte header or the EOF marker: general decoder
+        const int64_t next = p + 2 + k1 + v1;
+        if (next > len) return fail(s, kBadFraming);
+        s.key_bytes += k1;
+        ++recs;
+        p = next;
+      }
+    }
     while (p < len) {  // J2CQueue.next: readVInt key length, readVInt value length, skip bytes
       int64_t kl = 0, vl = 0;
       const int a = vint_decode(kb + p, (size_t)(len - p), &kl);
