@@ -84,6 +84,7 @@ struct DeviceWorkspace {
   gpu::DeviceBlockDecoder decoder;
   gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
   gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
+  gpu::DeviceBuffer frame_scratch; // device framing walk of compressed partitions (device fetch)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
   ~DeviceWorkspace() {
@@ -1229,13 +1230,30 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   int64_t host_bytes = 0, descriptors = 0, unmapped = 0;
   gpu::PinnedBuffer chunk;
 
-  // bytes of a MOF the provider does not hold in device memory: chunked fetches -> H2D
+  // bytes of a MOF the provider does not hold in device memory: chunked fetches into two pinned
+  // chunks, each chunk's H2D (async on `s`) overlapping the fetch of the next one
+  hipEvent_t chunk_ev[2] = {nullptr, nullptr};
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int i = 0; i < 2; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } chunk_ev_guard{chunk_ev};
+  gpu::PinnedBuffer chunk2;
   auto fetch_bytes = [&](const FetchParams& f, int64_t part_len, Part* part) {
     part->own.alloc((size_t)std::max<int64_t>(part_len, 16));
     part->dptr = part->own.as<uint8_t>();
     part->part_len = part_len;
     if (chunk.size() < (size_t)buffer_size_) chunk.alloc((size_t)buffer_size_);
+    if (chunk2.size() < (size_t)buffer_size_) chunk2.alloc((size_t)buffer_size_);
+    for (auto& e : chunk_ev)
+      if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    bool pending[2] = {false, false};
+    int slot = 0;
     for (int64_t off = 0; off < part_len;) {
+      uint8_t* buf = slot ? chunk2.as<uint8_t>() : chunk.as<uint8_t>();
+      if (pending[slot]) HIP_CHECK(hipEventSynchronize(chunk_ev[slot]));  // its previous H2D read it
       FetchRequest req;
       req.job_id = f.job_id;
       req.map_id = f.map_id;
@@ -1247,7 +1265,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       bool done = false;
       FetchAck got;
       fetch_begin();
-      transport_->fetch(f.host, req, chunk.as<uint8_t>(), [&](const FetchAck& a) {
+      transport_->fetch(f.host, req, buf, [&](const FetchAck& a) {
         std::lock_guard<std::mutex> g(m);
         got = a;
         done = true;
@@ -1260,10 +1278,14 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       }
       if (got.status != 0) throw UdaError("fetch of " + f.map_id + " failed: " + got.error);
       if (got.sent <= 0) throw UdaError("fetch of " + f.map_id + ": provider sent no data");
-      HIP_CHECK(hipMemcpy(part->own.as<uint8_t>() + off, chunk.as(), (size_t)got.sent, hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpyAsync(part->own.as<uint8_t>() + off, buf, (size_t)got.sent, hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipEventRecord(chunk_ev[slot], s));
+      pending[slot] = true;
       off += got.sent;
       host_bytes += got.sent;
+      slot ^= 1;
     }
+    HIP_CHECK(hipStreamSynchronize(s));
   };
 
   // ---- fetch phase: descriptors for every MOF as its FETCH arrives
@@ -1363,6 +1385,54 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     st_.bytes_delivered += len;
     return r;
   };
+  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
+                                                  device, [] { return std::make_unique<DeviceWorkspace>(); })};
+  DeviceWorkspace& ws = *ws_lease.obj;
+  ws.reset_stats();
+  // ---- compressed map outputs: F6 block decode straight from the partitions (descriptors or fetched
+  // bytes) into the workspace; the framing is walked on the device
+  if (codec_ != Codec::kNone) {
+    std::vector<const uint8_t*> cp;
+    std::vector<int64_t> cl;
+    for (const auto& p : parts) {
+      cp.push_back(p->dptr);
+      cl.push_back(p->part_len);
+    }
+    gpu::BlockPlan bp;
+    std::vector<int64_t> roff;
+    int64_t blocks = 0;
+    if (gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, s)) {
+      DeviceWorkspace::ensure(ws.in, bp.raw_total);
+      ws.decoder.decode(codec_, bp, nullptr, ws.in.as<uint8_t>(), s);
+      roff = bp.raw_offset;
+      blocks = (int64_t)bp.descs.size();
+    } else {  // framing that needs a decode (multi-chunk LZO blocks): decode on the host
+      UDA_LOG(kInfo, "device decode: framing needs a host decode (%s)", codec_name(codec_));
+      std::vector<std::vector<uint8_t>> raws;
+      roff.assign(1, 0);
+      for (size_t i = 0; i < cp.size(); ++i) {
+        std::vector<uint8_t> c((size_t)cl[i]);
+        if (cl[i] > 0) HIP_CHECK(hipMemcpy(c.data(), cp[i], (size_t)cl[i], hipMemcpyDefault));
+        BlockDecoder dec(codec_);
+        dec.feed(c.data(), c.size());
+        std::vector<uint8_t> raw, buf(1 << 20);
+        for (size_t n; (n = dec.read(buf.data(), buf.size())) > 0;) raw.insert(raw.end(), buf.begin(), buf.begin() + (long)n);
+        if (!dec.idle()) throw UdaError("truncated compressed partition");
+        roff.push_back(roff.back() + (int64_t)raw.size());
+        raws.push_back(std::move(raw));
+      }
+      DeviceWorkspace::ensure(ws.in, roff.back());
+      for (size_t i = 0; i < raws.size(); ++i)
+        if (!raws[i].empty())
+          HIP_CHECK(hipMemcpy(ws.in.as<uint8_t>() + roff[i], raws[i].data(), raws[i].size(), hipMemcpyHostToDevice));
+    }
+    for (size_t i = 0; i < parts.size(); ++i) {
+      parts[i]->dptr = ws.in.as<uint8_t>() + roff[i];
+      parts[i]->part_len = roff[i + 1] - roff[i];
+    }
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.device_decoded_blocks += blocks;
+  }
   // ---- TeraSort-shaped input: FIXED10 rounds straight over the partitions
   bool fixed = kind_ == KeyKind::kText;
   std::vector<gpu::RunDesc> runs;
@@ -1391,15 +1461,12 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
     st_.merge_path = "device-fixed10";
+    ws_lease.clean = true;
     return true;
   }
   // ---- any other key class: the generic merge, reading the partitions where they live, in key-range
   // rounds of at most mapred.uda.gpu.round.bytes of input (generic_rounds.h), so the device working
   // set (output + ~80 B/record of merge metadata) is bounded by the round, not by the partition
-  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
-                                                  device, [] { return std::make_unique<DeviceWorkspace>(); })};
-  DeviceWorkspace& ws = *ws_lease.obj;
-  ws.reset_stats();
   int64_t total = 0;
   std::vector<const uint8_t*> rptr;
   std::vector<int64_t> rlen;

@@ -529,8 +529,13 @@ void ReduceTask::merge_main() {
     const std::string gfetch = host_->get_conf("mapred.uda.gpu.fetch", "auto");  // auto | device | host
     // a resumed attempt (LPQ checkpoint of an earlier staged attempt) merges its restored runs on the
     // staged path: the device path has no notion of restored maps (their FETCHes are dropped)
-    if (backend_ == "gpu" && codec_ == Codec::kNone && net_.online != 2 && gfetch != "host" &&
-        restored_files_.empty() && merge_gpu_device(gfetch == "auto")) {
+    // compressed map outputs decode on the device straight from the descriptors (F6); hybrid-mode
+    // tasks need no LPQ spills when the partitions stay in the provider's HBM (the merge runs in
+    // key-range rounds that bound its working set), so both take the device path when the first
+    // answers are device descriptors
+    const bool dev_codec = codec_ == Codec::kNone || host_->conf_i64("mapred.uda.gpu.decompress", 1) != 0;
+    if (backend_ == "gpu" && dev_codec && gfetch != "host" && restored_files_.empty() &&
+        merge_gpu_device(gfetch == "auto")) {
       // done: partitions merged where the provider holds them
     } else if (backend_ == "gpu") {
       merge_gpu();

@@ -59,6 +59,57 @@ bool plan_block_streams(Codec codec, const std::vector<const uint8_t*>& ptrs, co
   return true;
 }
 
+bool plan_block_streams_device(Codec codec, const std::vector<const uint8_t*>& dptrs, const std::vector<int64_t>& lens,
+                               BlockPlan* plan, DeviceBuffer& scratch, hipStream_t s) {
+  const int n = (int)dptrs.size();
+  plan->descs.clear();
+  plan->raw_offset.assign(1, 0);
+  plan->raw_total = 0;
+  if (n == 0) return true;
+  // scratch: ptrs | lens | desc_first | raw_first | nblocks | raw (8 B each per stream) | status (4 B)
+  const size_t tb = (size_t)n * 52 + 64;
+  if (scratch.size() < tb) scratch.alloc(tb + tb / 2);
+  auto* d_ptrs = scratch.as<const uint8_t*>();
+  auto* d_lens = reinterpret_cast<int64_t*>(d_ptrs + n);
+  int64_t* d_dfirst = d_lens + n;
+  int64_t* d_rfirst = d_dfirst + n;
+  int64_t* d_nb = d_rfirst + n;
+  int64_t* d_raw = d_nb + n;
+  int* d_status = reinterpret_cast<int*>(d_raw + n);
+  HIP_CHECK(hipMemcpyAsync(d_ptrs, dptrs.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(d_lens, lens.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemsetAsync(d_status, 0, 4 * (size_t)n, s));
+  launch_frame_streams(d_ptrs, d_lens, n, (int)codec, nullptr, nullptr, d_nb, d_raw, nullptr, d_status, s);
+  std::vector<int64_t> nb((size_t)n), raw((size_t)n);
+  std::vector<int> st((size_t)n);
+  HIP_CHECK(hipMemcpyAsync(nb.data(), d_nb, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(raw.data(), d_raw, 8 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(st.data(), d_status, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (int i = 0; i < n; ++i)
+    if (st[(size_t)i]) return false;
+  std::vector<int64_t> dfirst((size_t)n), rfirst((size_t)n);
+  int64_t nd = 0, rt = 0;
+  for (int i = 0; i < n; ++i) {
+    dfirst[(size_t)i] = nd;
+    rfirst[(size_t)i] = rt;
+    nd += nb[(size_t)i];
+    rt += raw[(size_t)i];
+    plan->raw_offset.push_back(rt);
+  }
+  plan->raw_total = rt;
+  plan->descs.resize((size_t)nd);
+  if (nd == 0) return true;
+  DeviceBuffer d_descs((size_t)nd * sizeof(DecodeDesc));
+  HIP_CHECK(hipMemcpyAsync(d_dfirst, dfirst.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(d_rfirst, rfirst.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
+  launch_frame_streams(d_ptrs, d_lens, n, (int)codec, d_dfirst, d_rfirst, d_nb, d_raw, d_descs.as<DecodeDesc>(),
+                       d_status, s);
+  HIP_CHECK(hipMemcpyAsync(plan->descs.data(), d_descs.as(), (size_t)nd * sizeof(DecodeDesc), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return true;
+}
+
 void DeviceBlockDecoder::decode(Codec codec, const BlockPlan& plan, const uint8_t* d_in, uint8_t* d_out,
                                 hipStream_t s) {
   const int n = (int)plan.descs.size();

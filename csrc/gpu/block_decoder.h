@@ -25,9 +25,17 @@ struct BlockPlan {
 bool plan_block_streams(Codec codec, const std::vector<const uint8_t*>& ptrs, const std::vector<int64_t>& lens,
                         BlockPlan* plan);
 
+// Same plan for streams that live in device memory (HBM-resident compressed map outputs): the framing
+// is walked on the device (launch_frame_streams) and the descriptors carry absolute source
+// addresses, so decode() takes d_in = nullptr and reads every stream where it lies. false: the
+// framing needs a decode (the caller falls back to the host path). Synchronizes s.
+bool plan_block_streams_device(Codec codec, const std::vector<const uint8_t*>& dptrs, const std::vector<int64_t>& lens,
+                               BlockPlan* plan, DeviceBuffer& scratch, hipStream_t s);
+
 class DeviceBlockDecoder {
  public:
-  // d_in: device copy of the streams back to back (stream i at sum(lens[<i])); d_out: raw_total bytes.
+  // d_in: device copy of the streams back to back (stream i at sum(lens[<i])), or nullptr for a plan
+  // with absolute source addresses (plan_block_streams_device); d_out: raw_total bytes.
   // Throws UdaError on a corrupt block. Synchronizes s.
   void decode(Codec codec, const BlockPlan& plan, const uint8_t* d_in, uint8_t* d_out, hipStream_t s);
 

@@ -319,6 +319,90 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
 
 }  // namespace
 
+// Framing walk of device-resident block-compressed streams (one lane per stream, following the
+// 4-byte headers; a header read per chunk). Pass 1 (out == nullptr): blocks and raw bytes per
+// stream. Pass 2: the decode descriptors, src/src_end as absolute device addresses (decode with a
+// null input base), dst at raw_first[s] + the stream's earlier raw bytes. status[s] = 1 when the
+// framing is not resolvable without decoding (the host planner's `false`).
+__global__ void __launch_bounds__(64) frame_streams_kernel(const uint8_t* const* ptrs, const int64_t* lens, int nstreams,
+                                                           int codec, const int64_t* desc_first, const int64_t* raw_first,
+                                                           int64_t* nblocks, int64_t* raw, DecodeDesc* out, int* status) {
+  const int sidx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sidx >= nstreams) return;
+  const uint8_t* p = ptrs[sidx];
+  const int64_t n = lens[sidx];
+  int64_t i = 0, blocks = 0, rsum = 0;
+  int bad = 0;
+  while (i < n && !bad) {
+    if (i + 4 > n) {
+      bad = 1;
+      break;
+    }
+    const int64_t block_raw = (int64_t)be32(p + i);
+    i += 4;
+    if (block_raw == 0) continue;
+    const int64_t start = i;
+    int64_t left = block_raw;
+    while (left > 0) {
+      if (i + 4 > n) {
+        bad = 1;
+        break;
+      }
+      const int64_t clen = (int64_t)be32(p + i);
+      if (i + 4 + clen > n) {
+        bad = 1;
+        break;
+      }
+      int64_t produced = left;  // LZO: one chunk produces the whole block
+      if (codec == 1) {         // Snappy: the chunk's uncompressed-length varint
+        uint64_t u = 0;
+        int sh = 0, k = 0;
+        for (; k < 5 && k < clen; ++k) {
+          const uint8_t b = p[i + 4 + k];
+          u |= (uint64_t)(b & 0x7F) << sh;
+          sh += 7;
+          if (!(b & 0x80)) break;
+        }
+        if (k >= 5 || k >= clen) {
+          bad = 1;
+          break;
+        }
+        produced = (int64_t)u;
+        if (produced > left || produced == 0) {
+          bad = 1;
+          break;
+        }
+      }
+      i += 4 + clen;
+      left -= produced;
+    }
+    if (bad) break;
+    if (out) {
+      DecodeDesc d;
+      d.src = (int64_t)(uintptr_t)(p + start);
+      d.src_end = (int64_t)(uintptr_t)(p + i);
+      d.dst = raw_first[sidx] + rsum;
+      d.raw = block_raw;
+      out[desc_first[sidx] + blocks] = d;
+    }
+    ++blocks;
+    rsum += block_raw;
+  }
+  if (!out) {
+    nblocks[sidx] = blocks;
+    raw[sidx] = rsum;
+  }
+  if (bad) status[sidx] = 1;
+}
+
+void launch_frame_streams(const uint8_t* const* ptrs, const int64_t* lens, int nstreams, int codec,
+                          const int64_t* desc_first, const int64_t* raw_first, int64_t* nblocks, int64_t* raw,
+                          DecodeDesc* out, int* status, hipStream_t s) {
+  if (nstreams <= 0) return;
+  hipLaunchKernelGGL(frame_streams_kernel, dim3((unsigned)((nstreams + 63) / 64)), dim3(64), 0, s, ptrs, lens, nstreams,
+                     codec, desc_first, raw_first, nblocks, raw, out, status);
+}
+
 void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
                          hipStream_t s) {
   if (n <= 0) return;

@@ -463,6 +463,11 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
     return e ? std::atoi(e) : 1;
   }();
   kd.xcd_swizzle = xcd;
+  static const int nt = [] {
+    const char* e = std::getenv("UDA_KWAY_NT");
+    return e ? std::atoi(e) : 1;
+  }();
+  kd.nt_stores = nt;
   static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
   if (prof) {
     ensure(kw_prof_, (size_t)cell_first[G] * 5 * 8);

@@ -154,6 +154,7 @@ struct KwayDesc {
   int threads = 256;          // workgroup size: 256 or 512
   unsigned long long* prof = nullptr;  // optional [cell][5] phase timestamps (UDA_KWAY_PROF)
   int xcd_swizzle = 0;        // map consecutive cells to one XCD (workgroups are dealt round-robin over 8 XCDs)
+  int nt_stores = 1;          // F4 output with non-temporal stores (UDA_KWAY_NT=0 for plain stores)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.
@@ -237,6 +238,12 @@ struct DecodeDesc {
 // codec: 1 = Snappy, 2 = LZO1X (uda::Codec values). *status |= 1 if any block is corrupt.
 void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
                          hipStream_t s);
+// Framing walk of device-resident streams (one lane per stream). out == nullptr: per-stream block
+// counts and raw bytes; else the descriptors with absolute src addresses (decode with in = nullptr).
+// status[s] = 1: framing not resolvable without decoding (zero status first).
+void launch_frame_streams(const uint8_t* const* ptrs, const int64_t* lens, int nstreams, int codec,
+                          const int64_t* desc_first, const int64_t* raw_first, int64_t* nblocks, int64_t* raw,
+                          DecodeDesc* out, int* status, hipStream_t s);
 
 // ---------------------------------------------------------------- validation
 // Checks key order of `n` FIXED10 records at `recs` (and against *prev_key if has_prev) and

@@ -167,7 +167,7 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int 
 // lane are issued before its first store: written as load -> store pairs, the compiler must assume
 // the store may alias the next load and serializes 13 HBM round trips per 64 records.
 __device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0, const Elem* cur, int base, int valid,
-                                            uint8_t* dst) {
+                                            uint8_t* dst, bool nt) {
   constexpr int kWords = kTeraRecordBytes / 8;
   const int lane = threadIdx.x & 63;
   unsigned long long src = 0;
@@ -185,8 +185,13 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0,
       const int r = w / kWords;
       v[j] = ((const GlobalU64*)__shfl(src, r, 64))[w - r * kWords];
     }
+    if (nt) {  // the merged output is not re-read here: keep L2 for the record lines
 #pragma unroll
-    for (int j = 0; j < kWords; ++j) d[j * 64 + lane] = v[j];
+      for (int j = 0; j < kWords; ++j) __builtin_nontemporal_store(v[j], d + j * 64 + lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kWords; ++j) d[j * 64 + lane] = v[j];
+    }
     return;
   }
   const int words = valid * kWords;
@@ -392,7 +397,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   const int wave = threadIdx.x >> 6;
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
-    kw_gather64(rbase, r0, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+    kw_gather64(rbase, r0, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
   }
   if (kd.prof) {
     __builtin_amdgcn_s_waitcnt(0);

@@ -303,3 +303,58 @@ def test_bench_api_secondary_sort_skew(require_gpu):
     assert out["task0_stats"]["merge_path"] == "device-generic"
     assert out["max_task_rounds"] > 1 and out["max_task_ws_gb"] > 0
     assert out["config"]["global_batch"] == 6000000
+
+
+@pytest.mark.parametrize("codec", ["snappy", "lzo"])
+@pytest.mark.parametrize("gen", ["terasort", "secondary_sort"])
+def test_compressed_device_mofs_decode_in_place(require_gpu, provider, codec, gen):
+    """Block-compressed map outputs in the provider's HBM: the reducer walks the block framing on the
+    device, decodes (F6) straight from the descriptors and merges; every MOF is a descriptor."""
+    job = f"job_9_03{len(codec)}{len(gen)}"
+    maps = (datagen.terasort(num_maps=6, reducers=2, rows_per_map=3000, seed=51) if gen == "terasort" else
+            datagen.secondary_sort(num_maps=6, reducers=2, rows_per_map=2500, seed=51))
+    ids = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        data, index = encode_partitions(parts, codec, block_size=64 << 10)
+        provider.add_mof_device(job, mid, data, index, device=0)
+        ids.append(mid)
+    conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device"})
+    for r in range(2):
+        recs, st, _ = run_reduce("h", job, ids, r, datagen.TEXT, codec=codec, conf=conf, kv_buf_size=64 << 10)
+        want = expected(maps, r, datagen.TEXT)
+        kf = datagen.sort_key(datagen.TEXT)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want] and sorted(recs) == sorted(want)
+        assert st["device_descriptors"] == 6 and st["host_fetched_bytes"] == 0, st
+        assert st["device_decoded_blocks"] > 0 and st["merge_path"].startswith("device"), st
+
+
+def test_compressed_host_mofs_device_fetch_pipelined(require_gpu, provider):
+    """Compressed MOFs in host memory under mapred.uda.gpu.fetch=device: fetched as bytes in pipelined
+    chunks (H2D overlapping the next fetch), then decoded and merged on the device."""
+    maps = datagen.terasort(num_maps=5, reducers=1, rows_per_map=6000, seed=53)
+    ids = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_job_9_0310_m_{i:06d}_0"
+        data, index = encode_partitions(parts, "snappy", block_size=32 << 10)
+        provider.add_mof_memory("job_9_0310", mid, data, index)
+        ids.append(mid)
+    conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device"})
+    recs, st, _ = run_reduce("h", "job_9_0310", ids, 0, datagen.TEXT, codec="snappy", conf=conf, max_buf_kb=64)
+    assert recs == expected(maps, 0, datagen.TEXT)
+    assert st["device_descriptors"] == 0 and st["host_fetched_bytes"] > 0 and st["device_decoded_blocks"] > 0, st
+
+
+def test_hybrid_task_over_device_mofs_takes_device_path(require_gpu, provider, tmp_path):
+    """A hybrid-approach (LPQ/RPQ) reduce task whose map outputs are HBM-resident needs no LPQ spills:
+    it merges them in place in key-range rounds."""
+    maps = datagen.secondary_sort(num_maps=12, reducers=1, rows_per_map=2000, seed=57)
+    ids = _publish_device(provider, "job_9_0320", maps)
+    conf = dict(GPU, **{"mapred.uda.gpu.round.bytes": 256 << 10})
+    recs, st, _ = run_reduce("h", "job_9_0320", ids, 0, datagen.TEXT, conf=conf, approach=2, lpq_size=4,
+                             local_dirs=(str(tmp_path),))
+    want = expected(maps, 0, datagen.TEXT)
+    kf = datagen.sort_key(datagen.TEXT)
+    assert [kf(kv) for kv in recs] == [kf(kv) for kv in want] and sorted(recs) == sorted(want)
+    assert st["merge_path"] == "device-generic" and st["device_descriptors"] == 12 and st["lpqs"] == 0, st
+    assert st["rpq_rounds"] > 1
