@@ -463,9 +463,9 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
     return e ? std::atoi(e) : 1;
   }();
   kd.xcd_swizzle = xcd;
-  static const int nt = [] {
+  static const int nt = [] {  // non-temporal F4 stores: no measurable change (profiles/r3_kway_nt_ab.md), off
     const char* e = std::getenv("UDA_KWAY_NT");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   kd.nt_stores = nt;
   static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
