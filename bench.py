@@ -94,6 +94,9 @@ def parse_args(argv=None):
                          "prefixes, --skew of every map's records to reduce task 0, merged on the device in "
                          "key-range rounds of --round-mb")
     ap.add_argument("--skew", type=float, default=0.6, help="--api --workload secondary: share of reduce task 0")
+    ap.add_argument("--api-codec", choices=("snappy", "lzo"), default=None,
+                    help="--api: map outputs block-compressed (256 KiB blocks) and registered in HBM; reduce tasks "
+                         "decode on the device straight from the descriptors (F6)")
     ap.add_argument("--mof-dir", default="",
                     help="--api: write every map output as a file.out under this directory; the provider finds "
                          "them through getPathUda (Hadoop-written MOFs) and serves them from its HBM store")
@@ -314,7 +317,7 @@ def run_api(args, ctx) -> int:
         hbm_bytes = int(per_rank * 1.25) if args.provider_hbm_gb < 0 else int(args.provider_hbm_gb * 1e9)
     b = native().ApiTeraSortBench(dict(device=device, maps=args.maps_per_gpu, reducers=R,
                                        mof_dir=args.mof_dir, provider_hbm_bytes=hbm_bytes,
-                                       workload=args.workload, skew=args.skew,
+                                       workload=args.workload, skew=args.skew, codec=args.api_codec or "",
                                        records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
                                        round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
                                        transport="tcp" if world > 1 else "loopback",
@@ -401,6 +404,8 @@ def run_api(args, ctx) -> int:
             },
             "reduce_wall_clock_s": round(ms_per_step / 1000.0, 3),
             "mof_files": bool(args.mof_dir),
+            "codec": args.api_codec,
+            "compressed_gb": round(b.compressed_bytes / 1e9, 2) if args.api_codec else None,
             "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
             "provider": json.loads(b.provider_stats()),
             "close_ms": round(sum(s["close_ms"] for s in stats) / len(stats), 2),

@@ -17,6 +17,7 @@
 #include "device_engine.h"
 #include "j2c_sink.h"
 #include "secgen.h"
+#include "uda/codec.h"
 #include "uda/cmd.h"
 #include "uda/uda_bridge.h"
 
@@ -247,9 +248,61 @@ void ApiTeraSortBench::setup() {
         throw std::runtime_error(std::string("api bench: register_mof failed: ") + uda_last_error(h));
       continue;
     }
+    if (!cfg_.codec.empty()) continue;  // registered compressed below
     if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), gen_->mof_device_ptr(m), gen_->mof_bytes(m),
                                          index.data(), P, cfg_.device) != 0)
       throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
+  }
+  if (!cfg_.codec.empty()) compress_store();
+}
+
+// Compressed map outputs (what a job with mapred.compress.map.output writes): each partition of each
+// MOF is block-compressed on the host (one thread per MOF), the compressed MOFs are packed into one
+// HBM store and registered as device MOFs with index {offset, raw length, compressed length}.
+void ApiTeraSortBench::compress_store() {
+  const Codec c = cfg_.codec == "snappy" ? Codec::kSnappy : cfg_.codec == "lzo" ? Codec::kLzo : Codec::kNone;
+  if (c == Codec::kNone) throw std::runtime_error("api bench: unknown codec " + cfg_.codec);
+  const int P = cfg_.world * cfg_.reducers, M = cfg_.maps;
+  std::vector<std::vector<uint8_t>> comp((size_t)M);
+  std::vector<std::vector<int64_t>> idx((size_t)M);
+  std::vector<std::thread> ts;
+  std::mutex emu;
+  std::string err;
+  const int nt = std::max(1, std::min<int>(M, (int)std::thread::hardware_concurrency() / 2));
+  for (int t = 0; t < nt; ++t)
+    ts.emplace_back([&, t] {
+      try {
+        HIP_CHECK(hipSetDevice(cfg_.device));
+        std::vector<uint8_t> raw;
+        for (int m = t; m < M; m += nt) {
+          raw.resize((size_t)gen_->mof_bytes(m));
+          HIP_CHECK(hipMemcpy(raw.data(), gen_->mof_device_ptr(m), raw.size(), hipMemcpyDeviceToHost));
+          for (int r = 0; r < P; ++r) {
+            const auto ir = gen_->index_record(m, r);  // {offset, raw, part}
+            const std::vector<uint8_t> b = block_compress(c, raw.data() + ir[0], (size_t)ir[2], 256 << 10);
+            idx[(size_t)m].insert(idx[(size_t)m].end(), {(int64_t)comp[(size_t)m].size(), ir[2], (int64_t)b.size()});
+            comp[(size_t)m].insert(comp[(size_t)m].end(), b.begin(), b.end());
+          }
+        }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(emu);
+        err = e.what();
+      }
+    });
+  for (auto& t : ts) t.join();
+  if (!err.empty()) throw std::runtime_error("api bench: compressing the MOFs: " + err);
+  std::vector<int64_t> off((size_t)M + 1, 0);
+  for (int m = 0; m < M; ++m) off[(size_t)m + 1] = off[(size_t)m] + ((int64_t)comp[(size_t)m].size() + 255) / 256 * 256;
+  comp_store_.reset(new DeviceBuffer((size_t)std::max<int64_t>(off[(size_t)M], 16)));
+  uda_handle* h = static_cast<uda_handle*>(provider_);
+  for (int m = 0; m < M; ++m) {
+    uint8_t* dst = comp_store_->as<uint8_t>() + off[(size_t)m];
+    HIP_CHECK(hipMemcpy(dst, comp[(size_t)m].data(), comp[(size_t)m].size(), hipMemcpyHostToDevice));
+    const std::string id = map_id(cfg_.rank * M + m);
+    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), dst, (int64_t)comp[(size_t)m].size(),
+                                         idx[(size_t)m].data(), P, cfg_.device) != 0)
+      throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
+    comp_bytes_ += (int64_t)comp[(size_t)m].size();
   }
 }
 
@@ -372,8 +425,11 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
       const int g = cfg_.rank * R + r;  // the job's reduce task index
       char rt[96];
       std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, g);
+      const std::string codec_cls = cfg_.codec == "snappy" ? "org.apache.hadoop.io.compress.SnappyCodec"
+                                    : cfg_.codec == "lzo"  ? "com.hadoop.compression.lzo.LzoCodec"
+                                                           : "null";
       const std::vector<std::string> init = {std::to_string(W * cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
-                                             std::to_string(16 << 10), "org.apache.hadoop.io.Text", "null",
+                                             std::to_string(16 << 10), "org.apache.hadoop.io.Text", codec_cls,
                                              std::to_string(256 << 10), "0", "0"};
       if (uda_do_command(h, form_cmd(kInitMsg, init).c_str()) != 0) return fail(uda_last_error(h));
       // rotating rank order: the tasks of rank d start with rank d + 1's maps, spreading the load

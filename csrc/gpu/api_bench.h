@@ -55,6 +55,9 @@ struct ApiBenchConfig {
   // map's records in reduce task 0 (BASELINE config #5; device generator secgen.h; world 1)
   std::string workload = "terasort";
   double skew = 0.6;
+  // "snappy" / "lzo": every partition is block-compressed (256 KiB blocks) at setup and the compressed
+  // MOFs are registered in HBM; INIT announces the codec, so reduce tasks decode on the device (F6)
+  std::string codec;
 };
 
 class ApiTeraSortBench {
@@ -86,6 +89,14 @@ class ApiTeraSortBench {
   int64_t sec_store_bytes_ = 0;
   std::string map_id(int global_map) const;
   void setup_secondary();
+  void compress_store();
+  std::unique_ptr<DeviceBuffer> comp_store_;  // codec: the compressed MOFs in HBM
+  int64_t comp_bytes_ = 0;
+
+ public:
+  int64_t compressed_bytes() const { return comp_bytes_; }
+
+ private:
 
  public:
   // getPathUda of the provider (mof_dir mode)

@@ -883,6 +883,7 @@ PYBIND11_MODULE(_uda_native, m) {
         get("provider_hbm_bytes", c.provider_hbm_bytes);
         get("workload", c.workload);
         get("skew", c.skew);
+        get("codec", c.codec);
         return new gpu::ApiTeraSortBench(c);
       }))
       .def("setup", &gpu::ApiTeraSortBench::setup, py::call_guard<py::gil_scoped_release>())
@@ -902,6 +903,7 @@ PYBIND11_MODULE(_uda_native, m) {
            py::arg("validate") = false)
       .def("expected_records", &gpu::ApiTeraSortBench::expected_records)
       .def("provider_stats", &gpu::ApiTeraSortBench::provider_stats)
+      .def_property_readonly("compressed_bytes", &gpu::ApiTeraSortBench::compressed_bytes)
       .def("local_partition_records", &gpu::ApiTeraSortBench::local_partition_records)
       .def("set_expected", &gpu::ApiTeraSortBench::set_expected)
       .def("set_peers", &gpu::ApiTeraSortBench::set_peers)

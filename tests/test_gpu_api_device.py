@@ -358,3 +358,17 @@ def test_hybrid_task_over_device_mofs_takes_device_path(require_gpu, provider, t
     assert [kf(kv) for kv in recs] == [kf(kv) for kv in want] and sorted(recs) == sorted(want)
     assert st["merge_path"] == "device-generic" and st["device_descriptors"] == 12 and st["lpqs"] == 0, st
     assert st["rpq_rounds"] > 1
+
+
+@pytest.mark.parametrize("codec", ["snappy", "lzo"])
+def test_bench_api_compressed_mofs(require_gpu, codec):
+    """bench.py --api --api-codec: compressed TeraSort MOFs in HBM, decoded on the device from the
+    descriptors by every reduce task, validated."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--api-codec", codec, "--rows-per-gpu", "2000000",
+           "--maps-per-gpu", "4", "--reducers", "4", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["validated"] is True and out["codec"] == codec and 0 < out["compressed_gb"]
+    t0 = out["task0_stats"]
+    assert t0["device_descriptors"] == 4 and t0["device_decoded_blocks"] > 0, t0

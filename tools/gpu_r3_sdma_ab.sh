@@ -9,3 +9,8 @@ for v in 1 0; do
 done
 timeout -k 10 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/r3_pytest_gpu_full2.log 2>&1 || { tail -30 gpurun_out/r3_pytest_gpu_full2.log; exit 1; }
 tail -2 gpurun_out/r3_pytest_gpu_full2.log
+for c in snappy lzo; do
+  timeout -k 10 600 python -u bench.py --api --api-codec $c --rows-per-gpu 400000000 --steps 3 --warmup 1 \
+    > gpurun_out/r3_bench_api_${c}_41GB.log 2>&1 || { tail -20 gpurun_out/r3_bench_api_${c}_41GB.log; exit 1; }
+  echo "$c $(tail -1 gpurun_out/r3_bench_api_${c}_41GB.log | cut -c1-150)"
+done
