@@ -221,6 +221,10 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
 DeviceMerger::~DeviceMerger() {
   for (auto& s : slots_)
     if (s.uploaded) (void)hipEventDestroy(s.uploaded);
+  for (auto& p : pbufs_) {
+    if (p.planned) (void)hipEventDestroy(p.planned);
+    if (p.used) (void)hipEventDestroy(p.used);
+  }
 }
 
 int DeviceMerger::kway_overflow_cells() {
@@ -344,8 +348,38 @@ static void report_kway_phases(const unsigned long long* dprof, int64_t ncells, 
 // per-run cell splits -> one workgroup per cell doing F2 + F3 + F4 in LDS.
 int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
                                  hipStream_t s) {
+  const KwayPlan p = plan_kway(runs, group_first, s);
+  return run_kway(p, out, s);
+}
+
+bool DeviceMerger::kway_applicable(const std::vector<RunDesc>& runs, const std::vector<int>& group_first) const {
+  if (!kway_ || group_first.empty() || group_first.back() != (int)runs.size() || (int)runs.size() > max_runs_)
+    return false;
+  int64_t total = 0;
+  for (const auto& r : runs) total += r.nrec;
+  if (total > max_records_) return false;
+  for (size_t g = 0; g + 1 < group_first.size(); ++g)
+    if (group_first[g + 1] - group_first[g] > kKwMaxRuns) return false;
+  return true;
+}
+
+// Cell planning of one K-way merge (sample -> merge the samples per group -> splitters -> per-run
+// cell splits), enqueued on `s` into one of two plan slots. The slot's previous tiles must be done
+// reading it first (device-side wait), so planning round q+1 on a side stream overlaps the tiles of
+// round q on the compute stream.
+DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first,
+                                               hipStream_t s) {
   const int K = (int)runs.size();
   const int G = (int)group_first.size() - 1;
+  KwayPlan kp;
+  kp.pslot = next_pslot_;
+  next_pslot_ ^= 1;
+  PlanBufs& pb = pbufs_[kp.pslot];
+  if (!pb.planned) {
+    HIP_CHECK(hipEventCreateWithFlags(&pb.planned, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&pb.used, hipEventDisableTiming));
+  }
+  if (pb.used_valid) HIP_CHECK(hipStreamWaitEvent(s, pb.used, 0));
   int kmax = 1;
   for (int g = 0; g < G; ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
   const int64_t cap = kw_cap_;
@@ -381,11 +415,12 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
   auto ensure = [](DeviceBuffer& b, size_t bytes) {
     if (b.size() < bytes) b.alloc(bytes + bytes / 8);
   };
-  ensure(samp_a_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
-  ensure(samp_b_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
-  ensure(samp_runs_, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
-  ensure(kw_bounds_, (size_t)std::max<int64_t>((int64_t)G * nbmax, 1) * sizeof(Elem));
-  ensure(kw_split_, (size_t)K * per * sizeof(int64_t));
+  ensure(pb.samp_a, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(pb.samp_b, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(pb.samp_runs, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
+  ensure(pb.bounds, (size_t)std::max<int64_t>((int64_t)G * nbmax, 1) * sizeof(Elem));
+  ensure(pb.split, (size_t)K * per * sizeof(int64_t));
+  ensure(pb.splits, (size_t)(ns / kMergeTile + K + 2) * sizeof(int64_t));
 
   Slot& slot = slots_[next_slot_];
   next_slot_ = (next_slot_ + 1) % (int)slots_.size();
@@ -427,30 +462,31 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
 
   // splitters: a regular sample of every run, merged per group, every (ns_g / C_g)-th kept; the
   // per-run sample stays intact (first merge pass reads it) and brackets the split searches
-  Elem* sr = samp_runs_.as<Elem>();
-  Elem* sbuf[2] = {samp_a_.as<Elem>(), samp_b_.as<Elem>()};
+  Elem* sr = pb.samp_runs.as<Elem>();
+  Elem* sbuf[2] = {pb.samp_a.as<Elem>(), pb.samp_b.as<Elem>()};
   if (ns > 0)
     launch_sample_fixed(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec), K,
                         step, reinterpret_cast<const int64_t*>(d + o_soff), ns, sr, s);
   const Elem* merged = sr;
   int w = 0;
   for (const auto& pd : pds) {
-    launch_merge_partition(merged, pd, splits_.as<int64_t>(), s);
-    launch_merge_pass(merged, sbuf[w], pd, splits_.as<int64_t>(), s);
+    launch_merge_partition(merged, pd, pb.splits.as<int64_t>(), s);
+    launch_merge_pass(merged, sbuf[w], pd, pb.splits.as<int64_t>(), s);
     merged = sbuf[w];
     w ^= 1;
   }
   launch_pick_splitters(merged, reinterpret_cast<const int64_t*>(d + o_gs), reinterpret_cast<const int64_t*>(d + o_gc),
-                        G, (int)nbmax, kw_bounds_.as<Elem>(), s);
+                        G, (int)nbmax, pb.bounds.as<Elem>(), s);
   launch_split_sampled(reinterpret_cast<uint8_t* const*>(d + o_bases), reinterpret_cast<const int64_t*>(d + o_nrec), sr,
                        reinterpret_cast<const int64_t*>(d + o_soff), step,
-                       nbmax > 0 ? kw_bounds_.as<Elem>() : nullptr, reinterpret_cast<const int*>(d + o_bset), K,
-                       (int)nbmax, kw_split_.as<int64_t>(), s);
-  KwayDesc kd;
+                       nbmax > 0 ? pb.bounds.as<Elem>() : nullptr, reinterpret_cast<const int*>(d + o_bset), K,
+                       (int)nbmax, pb.split.as<int64_t>(), s);
+  HIP_CHECK(hipEventRecord(pb.planned, s));
+  KwayDesc& kd = kp.kd;
   kd.runs = reinterpret_cast<const RunDesc*>(d + o_runs);
   kd.group_first = reinterpret_cast<const int*>(d + o_gf);
   kd.cell_first = reinterpret_cast<const int64_t*>(d + o_cf);
-  kd.split = kw_split_.as<int64_t>();
+  kd.split = pb.split.as<int64_t>();
   kd.nbmax = (int)nbmax;
   kd.group_out = reinterpret_cast<const int64_t*>(d + o_go);
   kd.G = G;
@@ -468,16 +504,30 @@ int64_t DeviceMerger::merge_kway(const std::vector<RunDesc>& runs, const std::ve
     return e ? std::atoi(e) : 0;
   }();
   kd.nt_stores = nt;
+  kp.ncells = cell_first[G];
+  kp.total = total_records(runs);
+  return kp;
+}
+
+int64_t DeviceMerger::run_kway(const KwayPlan& kp, uint8_t* out, hipStream_t s) {
+  PlanBufs& pb = pbufs_[kp.pslot];
+  HIP_CHECK(hipStreamWaitEvent(s, pb.planned, 0));
+  KwayDesc kd = kp.kd;
   static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
   if (prof) {
-    ensure(kw_prof_, (size_t)cell_first[G] * 5 * 8);
-    HIP_CHECK(hipMemsetAsync(kw_prof_.as(), 0, (size_t)cell_first[G] * 5 * 8, s));
+    auto ensure = [](DeviceBuffer& b, size_t bytes) {
+      if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+    };
+    ensure(kw_prof_, (size_t)kp.ncells * 5 * 8);
+    HIP_CHECK(hipMemsetAsync(kw_prof_.as(), 0, (size_t)kp.ncells * 5 * 8, s));
     kd.prof = kw_prof_.as<unsigned long long>();
   }
-  launch_kway_tiles(kd, cell_first[G], out, s);
-  if (prof) report_kway_phases(kd.prof, cell_first[G], s);
+  launch_kway_tiles(kd, kp.ncells, out, s);
+  HIP_CHECK(hipEventRecord(pb.used, s));
+  pb.used_valid = true;
+  if (prof) report_kway_phases(kd.prof, kp.ncells, s);
   last_passes_ = 1;
-  return total_records(runs);
+  return kp.total;
 }
 
 // -------------------------------------------------------------------------------- ShuffleJob
@@ -506,6 +556,7 @@ ShuffleJob::ShuffleJob(const ShuffleConfig& cfg) : cfg_(cfg) {
   HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, spill ? lo_prio : hi_prio));
   HIP_CHECK(hipStreamCreateWithPriority(&s_compute_, hipStreamNonBlocking, spill ? hi_prio : lo_prio));
   HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&s_plan_, hipStreamNonBlocking));
   buf_records_ = std::max<int64_t>(1, cfg_.kv_buf_bytes / kTeraRecordBytes);
   const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
   piece_bytes_ = std::max<int64_t>(1, cfg_.d2h_piece_bytes / buf_bytes) * buf_bytes;
@@ -541,6 +592,7 @@ ShuffleJob::~ShuffleJob() {
   }
   exchange_.reset();
   if (s_copy_) (void)hipStreamDestroy(s_copy_);
+  if (s_plan_) (void)hipStreamDestroy(s_plan_);
   if (s_comm_) (void)hipStreamDestroy(s_comm_);
   if (s_compute_) (void)hipStreamDestroy(s_compute_);
 }
@@ -1439,6 +1491,49 @@ StepStats ShuffleJob::run_step(bool validate) {
     }
   } stage_guard{stage_thr, mu_, cv_, stop_};
 
+  // runs of round q, grouped by reducer: group i = cell (i, q) from every source map
+  auto build_runs = [&](int q, std::vector<RunDesc>& runs, std::vector<int>& group_first) {
+    const RoundPlan& rp = plans_[q];
+    uint8_t* rbuf = staged() ? recv_slots_[q % kSlots].as<uint8_t>() : nullptr;
+    runs.clear();
+    group_first.assign(1, 0);
+    runs.reserve((size_t)R_ * W * M);
+    for (int i = 0; i < R_; ++i) {
+      for (int s = 0; s < W; ++s)
+        for (int j = 0; j < M; ++j) {
+          const size_t x = ((size_t)s * R_ + i) * M + j;
+          RunDesc d;
+          d.nrec = rp.recv_cnt[x];
+          d.nbytes = d.nrec * kTeraRecordBytes;
+          d.offsets = nullptr;
+          if (rp.recv_off[x] >= 0)
+            d.base = rbuf + rp.recv_off[x];
+          else  // own cell, read in place from the HBM store
+            d.base = store_dev_base_ + run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+          runs.push_back(d);
+        }
+      group_first.push_back((int)runs.size());
+    }
+  };
+  // Runs read in place (HBM store, one rank): round q+1's cell planning is enqueued on the plan stream
+  // right after round q's tiles, so it runs beside them instead of between them (UDA_KWAY_LOOKAHEAD=0
+  // plans in line).
+  static const bool lookahead_env = [] {
+    const char* e = std::getenv("UDA_KWAY_LOOKAHEAD");
+    return !e || std::atoi(e) != 0;
+  }();
+  bool lookahead = false;
+  DeviceMerger::KwayPlan next_plan;
+  if (lookahead_env && !staged() && merger_->kway_enabled()) {
+    std::vector<RunDesc> r0;
+    std::vector<int> g0;
+    build_runs(0, r0, g0);
+    if (merger_->kway_applicable(r0, g0)) {
+      lookahead = true;
+      next_plan = merger_->plan_kway(r0, g0, s_plan_);
+    }
+  }
+
   for (int q = 0; q < Q_; ++q) {
     trace::Range tr_round("uda.round");
     const int slot = q % kSlots;
@@ -1484,26 +1579,9 @@ StepStats ShuffleJob::run_step(bool validate) {
       HIP_CHECK(hipEventRecord(comm_ev_[slot], s_comm_));
       HIP_CHECK(hipStreamWaitEvent(s_compute_, comm_ev_[slot], 0));
     }
-    // runs of this round, grouped by reducer: group i = cell (i, q) from every source map
     std::vector<RunDesc> runs;
-    std::vector<int> group_first{0};
-    runs.reserve((size_t)R_ * W * M);
-    for (int i = 0; i < R_; ++i) {
-      for (int s = 0; s < W; ++s)
-        for (int j = 0; j < M; ++j) {
-          const size_t x = ((size_t)s * R_ + i) * M + j;
-          RunDesc d;
-          d.nrec = rp.recv_cnt[x];
-          d.nbytes = d.nrec * kTeraRecordBytes;
-          d.offsets = nullptr;
-          if (rp.recv_off[x] >= 0)
-            d.base = rbuf + rp.recv_off[x];
-          else  // own cell, read in place from the HBM store
-            d.base = store_dev_base_ + run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
-          runs.push_back(d);
-        }
-      group_first.push_back((int)runs.size());
-    }
+    std::vector<int> group_first;
+    if (!lookahead) build_runs(q, runs, group_first);
     // output slot reuse: every D2H piece of round q-kSlots must have landed
     if (deliver && q >= kSlots) {
       const double tw = now_ms();
@@ -1512,7 +1590,16 @@ StepStats ShuffleJob::run_step(bool validate) {
     }
     HIP_CHECK(hipEventRecord(ev[4 * q + 2], s_compute_));
     uint8_t* out = out_slots_[slot].as<uint8_t>();
-    const int64_t n = merger_->merge_fixed(runs, group_first, out, s_compute_);
+    int64_t n = 0;
+    if (lookahead) {  // this round was planned while the previous one merged; plan the next one now
+      n = merger_->run_kway(next_plan, out, s_compute_);
+      if (q + 1 < Q_) {
+        build_runs(q + 1, runs, group_first);
+        next_plan = merger_->plan_kway(runs, group_first, s_plan_);
+      }
+    } else {
+      n = merger_->merge_fixed(runs, group_first, out, s_compute_);
+    }
     HIP_CHECK(hipGetLastError());
     st.merge_passes = std::max(st.merge_passes, merger_->last_passes());
     if (validate) {

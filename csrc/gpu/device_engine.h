@@ -170,6 +170,19 @@ class DeviceMerger {
   int kway_overflow_cells();
   bool kway_enabled() const { return kway_; }
 
+  // The single-pass K-way merge split in two: plan_kway enqueues a merge's cell planning on `s` into
+  // one of two plan slots, run_kway its tiles (waiting for that plan on its own stream). A caller
+  // can plan round q+1 on a side stream while round q's tiles run. kway_applicable: the runs can
+  // take this path (at most kKwMaxRuns per group, within the merger's capacity).
+  struct KwayPlan {
+    KwayDesc kd;
+    int64_t ncells = 0, total = 0;
+    int pslot = 0;
+  };
+  bool kway_applicable(const std::vector<RunDesc>& runs, const std::vector<int>& group_first) const;
+  KwayPlan plan_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, hipStream_t s);
+  int64_t run_kway(const KwayPlan& p, uint8_t* out, hipStream_t s);
+
  private:
   int64_t merge_kway(const std::vector<RunDesc>& runs, const std::vector<int>& group_first, uint8_t* out,
                      hipStream_t s);
@@ -187,7 +200,14 @@ class DeviceMerger {
   bool kway_ = true;
   int kw_cap_ = 1536;  // records per k-way cell (UDA_KWAY_CAP): 3 workgroups per CU fit LDS
   int kw_threads_ = 256;  // k-way workgroup size (UDA_KWAY_THREADS)
-  DeviceBuffer kw_prof_, samp_runs_, samp_a_, samp_b_, kw_bounds_, kw_split_, kw_overflow_;
+  DeviceBuffer kw_prof_, kw_overflow_;
+  struct PlanBufs {  // per plan slot: samples, splitters, cell splits, sample-merge scratch
+    DeviceBuffer samp_runs, samp_a, samp_b, bounds, split, splits;
+    hipEvent_t planned = nullptr, used = nullptr;
+    bool used_valid = false;
+  };
+  PlanBufs pbufs_[2];
+  int next_pslot_ = 0;
   std::vector<Slot> slots_;
   int next_slot_ = 0;
   int last_passes_ = 0;
@@ -330,6 +350,7 @@ class ShuffleJob {
   std::unique_ptr<Exchange> exchange_;
   std::unique_ptr<DiskStore> disk_;
   hipStream_t s_comm_ = nullptr, s_compute_ = nullptr, s_copy_ = nullptr;
+  hipStream_t s_plan_ = nullptr;  // K-way cell planning of the next round (runs read in place)
   DeviceBuffer store_;
   PinnedBuffer hstore_;
   uint8_t* store_base_ = nullptr;      // where run_base() points
