@@ -61,7 +61,7 @@ def parse_args(argv=None):
                     help="--api: mapred.uda.gpu.fetch of the reduce tasks (default: device, host with --api-host-mofs)")
     ap.add_argument("--api-gpu-slots", type=int, default=-1,
                     help="--api: mapred.uda.gpu.max.concurrent.merges (staged GPU merges admitted at once; 0: all; "
-                         "default: the native default, 6)")
+                         "default: 6 with --api-host-mofs, else the native default, 0 = off)")
     ap.add_argument("--api-provider-workers", type=int, default=-1,
                     help="--api: mapred.uda.provider.workers of the MOFSupplier (default 8)")
     ap.add_argument("--one-gpu", action="store_true",
@@ -322,7 +322,10 @@ def run_api(args, ctx) -> int:
                                        round_bytes=args.round_mb << 20, rank=rank, world=world, port=port,
                                        transport="tcp" if world > 1 else "loopback",
                                        bind_addr=f"127.0.0.{rank + 1}" if world > 1 else "",
-                                       host_mofs=args.api_host_mofs, max_concurrent_merges=args.api_gpu_slots,
+                                       host_mofs=args.api_host_mofs,
+                                       # the measured best for 16 tasks whose map outputs are all in (6 slots)
+                                       max_concurrent_merges=args.api_gpu_slots if args.api_gpu_slots >= 0 else
+                                       (6 if args.api_host_mofs else -1),
                                        provider_workers=args.api_provider_workers,
                                        fetch=args.api_fetch or ("host" if args.api_host_mofs else "device")))
     t = time.perf_counter()

@@ -336,8 +336,8 @@ struct PoolLease {
   }
 };
 
-// Admission of staged GPU reduce tasks per device (mapred.uda.gpu.max.concurrent.merges, default 6;
-// 0 = no limit).
+// Admission of staged GPU reduce tasks per device (mapred.uda.gpu.max.concurrent.merges, default 0 =
+// no limit).
 // Reduce tasks started together run their phases in lockstep: all fetch and copy to HBM at once (the
 // H2D direction of PCIe busy, D2H idle), then all merge, then all deliver (D2H busy, H2D idle). With
 // at most `cap` tasks admitted, in arrival order, a task's fetch and H2D overlap the merge and D2H of
@@ -613,9 +613,11 @@ void ReduceTask::merge_gpu() {
   const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
   if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
   GateLease gate;
-  // default 6: 16 concurrent host-MOF TeraSort tasks 20.8 GB/s unlimited, 31.2 / 34.3 / 32.6 with 4 / 6 / 8
-  // slots (profiles/r2_api_host_mofs_gate_sweep.md); nodes running <= 6 tasks per GPU are unaffected
-  if (const int cap = (int)host_->conf_i64("mapred.uda.gpu.max.concurrent.merges", 6); cap > 0) {
+  // Off by default: a gated task fetches nothing until all its FETCHes are in, which under reduce
+  // slow-start gives up the fetch / map-phase overlap. With every map output already there, 16
+  // concurrent host-MOF TeraSort tasks reach 20.8 GB/s unlimited and 31.2 / 34.3 / 32.6 with 4 / 6 / 8
+  // slots (profiles/r2_api_host_mofs_gate_sweep.md): set it for jobs whose reduces start after the maps.
+  if (const int cap = (int)host_->conf_i64("mapred.uda.gpu.max.concurrent.merges", 0); cap > 0) {
     const auto w0 = std::chrono::steady_clock::now();
     // A task asks for a slot only once every map has been announced (all FETCH commands in): a task
     // still waiting for map outputs (reduce slow-start) must not hold a slot, and a host that feeds the
