@@ -76,8 +76,22 @@ __device__ __forceinline__ uint32_t byte_at(const Wave& w, int64_t ip) {
   return (uint32_t)w.win[ip - w.win_base];
 }
 
+// 16 bytes per lane at any alignment: gfx950 runs in unaligned-access mode, so a packed 16-byte
+// struct compiles to one global_load/store_dwordx4 (1 KiB per wave step instead of 64 bytes).
+struct __attribute__((packed, aligned(1))) U128 {
+  uint32_t a, b, c, d;
+};
+
+// Non-overlapping copy dst[0, len) = src[0, len) by the 64 lanes.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, int64_t len, int lane) {
+  const int64_t nv = len & ~(int64_t)15;
+  for (int64_t i = (int64_t)lane * 16; i < nv; i += 64 * 16)
+    *reinterpret_cast<U128*>(dst + i) = *reinterpret_cast<const U128*>(src + i);
+  for (int64_t i = nv + lane; i < len; i += 64) dst[i] = src[i];
+}
+
 __device__ __forceinline__ void copy_literal(Wave& w, int64_t op, int64_t ip, int64_t len) {
-  for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.in[ip + i];
+  wave_copy(w.out + op, w.in + ip, len, w.lane);
 }
 
 // out[op .. op+len) = out[op-off ...] with LZ77 overlap semantics.
@@ -90,7 +104,7 @@ __device__ __forceinline__ void copy_match(Wave& w, int64_t op, int64_t off, int
     w.flushed = op;
   }
   if (off >= len) {
-    for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.out[src + i];
+    wave_copy(w.out + op, w.out + src, len, w.lane);
   } else {
     for (int64_t i = w.lane; i < len; i += 64) w.out[op + i] = w.out[src + (i % off)];
   }

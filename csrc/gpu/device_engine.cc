@@ -504,6 +504,8 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
     return e ? std::atoi(e) : 0;
   }();
   kd.nt_stores = nt;
+  const char* ip = std::getenv("UDA_KWAY_INPLACE");  // read per plan: tests flip it within one process
+  kd.inplace = ip ? std::atoi(ip) : 0;
   kp.ncells = cell_first[G];
   kp.total = total_records(runs);
   return kp;

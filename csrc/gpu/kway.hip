@@ -211,9 +211,11 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0,
 
 }  // namespace
 
-// ITEMS records per thread: the cell capacity is ITEMS * 256 and the two LDS buffers are dynamic
-// (2 * cap * 16 bytes), so smaller capacities fit more workgroups per CU.
-template <int ITEMS, int THREADS>
+// ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffers are dynamic, so
+// smaller capacities fit more workgroups per CU. INPLACE: one cap x 16-byte buffer instead of two; a
+// merge level keeps each thread's outputs in registers, waits for every thread to finish reading, then
+// writes them back in place (two barriers per level instead of one), halving the LDS per workgroup.
+template <int ITEMS, int THREADS, bool INPLACE>
 __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
   constexpr int kKwItems = ITEMS;
   constexpr int kKwThreads = THREADS;
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   constexpr int kCap = ITEMS * kKwThreads;
   extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
   Elem* bufA = kw_dyn;
-  Elem* bufB = kw_dyn + kCap;
+  Elem* bufB = INPLACE ? kw_dyn : kw_dyn + kCap;
   __shared__ int seg[kKwMaxRuns + 1];
   __shared__ int64_t beg[kKwMaxRuns];
   __shared__ const uint8_t* rbase[kKwMaxRuns];
@@ -341,6 +343,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   Elem* src = bufA;
   Elem* dst = bufB;
   const int o0 = threadIdx.x * kKwItems;
+  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // INPLACE: this thread's outputs of the current level
   for (int w = 1; w < K; w <<= 1) {
     if (o0 < n) {
       const int npairs = (K + 2 * w - 1) / (2 * w);
@@ -367,7 +370,9 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
       }
       int ia = ml, ib = d - ml;
       const int todo = min(kKwItems, n - o0);
-      for (int k = 0; k < todo; ++k) {
+#pragma unroll
+      for (int k = 0; k < kKwItems; ++k) {
+        if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
         const int o = o0 + k;
         while (o == b1) {  // next pair (empty pairs are skipped)
           ++p;
@@ -380,7 +385,12 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
           ib = 0;
         }
         const bool take_a = ib >= lb || (ia < la && kle(src[a0 + ia], src[a1 + ib]));
-        dst[o] = take_a ? src[a0 + ia] : src[a1 + ib];
+        const Elem v = take_a ? src[a0 + ia] : src[a1 + ib];
+        if (INPLACE) {
+          held_hi[k] = v.hi;
+          held_lo[k] = v.lo;
+        } else
+          dst[o] = v;
         if (take_a)
           ++ia;
         else
@@ -388,9 +398,19 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
       }
     }
     __syncthreads();
-    Elem* t = src;
-    src = dst;
-    dst = t;
+    if (INPLACE) {  // every thread has read the level: overwrite it with the merged order
+      if (o0 < n) {
+        const int todo = min(kKwItems, n - o0);
+#pragma unroll
+        for (int k = 0; k < kKwItems; ++k)
+          if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
+      }
+      __syncthreads();
+    } else {
+      Elem* t = src;
+      src = dst;
+      dst = t;
+    }
   }
   stamp(3);
   // ---- F4: records in merged order straight to the output
@@ -426,16 +446,24 @@ void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem
 int kway_cap_supported(int cap) { return cap == 2048 || cap == 1536 || cap == 1024 || cap == 512; }
 
 namespace {
+template <int ITEMS, int THREADS, bool INPLACE>
+void launch_kway_v(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
+  const size_t lds = (INPLACE ? 1 : 2) * sizeof(Elem) * (size_t)(ITEMS * THREADS);
+  static std::once_flag once;
+  std::call_once(once, [lds] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, THREADS, INPLACE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  });
+  hipLaunchKernelGGL((kway_tile_kernel<ITEMS, THREADS, INPLACE>), dim3((unsigned)ncells), dim3(THREADS), lds, s, kd,
+                     out);
+}
+
 template <int ITEMS, int THREADS>
 void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
-  const size_t lds = 2 * sizeof(Elem) * (size_t)(ITEMS * THREADS);
-  static std::once_flag once;
-  std::call_once(once, [] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, THREADS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(2 * sizeof(Elem) * ITEMS * THREADS));
-  });
-  hipLaunchKernelGGL((kway_tile_kernel<ITEMS, THREADS>), dim3((unsigned)ncells), dim3(THREADS), lds, s, kd, out);
+  if (kd.inplace)
+    launch_kway_v<ITEMS, THREADS, true>(kd, ncells, out, s);
+  else
+    launch_kway_v<ITEMS, THREADS, false>(kd, ncells, out, s);
 }
 }  // namespace
 

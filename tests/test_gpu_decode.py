@@ -1,7 +1,8 @@
 """F6 device block decode (Snappy / LZO1X) against the original bytes and the host decoders.
 
 Inputs cover incompressible data (long literals), short-period repeats (overlapping copies with
-offset < length), IFile streams, empty blocks and streams, multi-chunk Snappy blocks, and Snappy
+offset < length), long non-overlapping back-references at odd alignments (the 16-byte vector
+copies), IFile streams, empty blocks and streams, multi-chunk Snappy blocks, and Snappy
 streams from an independent encoder (pyarrow's libsnappy) when available.
 """
 import os
@@ -25,6 +26,8 @@ def _payloads():
     yield "mixed", b"".join(
         (os.urandom(rng.randint(1, 300)) if rng.random() < 0.5 else bytes([rng.randrange(256)]) * rng.randint(1, 900))
         for _ in range(600))
+    base = os.urandom(5000)  # slices of one text: long non-overlapping back-references at odd alignments
+    yield "slices", b"".join(base[o:o + n] for o, n in ((rng.randrange(4700), rng.randint(4, 300)) for _ in range(2000)))
     yield "ifile", datagen.streams(datagen.secondary_sort(3, 1, 3000, seed=2))[0][0]
     yield "tiny", b"q"
     yield "empty", b""
