@@ -283,6 +283,7 @@ def main(argv=None) -> int:
             "buffers_per_step": stats[0]["buffers"],
             "validated": validated,
             "exchange_errors": exchange_errors,
+            "ipc_fallback": getattr(job, "ipc_fallback", None),
             "reference_envelope_gbps_per_node": 5.0,
         }
         print(json.dumps(out), flush=True)

@@ -49,6 +49,7 @@
 #include "uda/compare.h"
 #include "uda/ifile.h"
 #include "uda/log.h"
+#include "uda/trace.h"
 
 namespace uda {
 
@@ -178,11 +179,12 @@ class EarlyStager {
   void copy(const uint8_t* host, uint8_t* dev, int64_t len) {
     if (len <= 0) return;
     std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(Job{host, dev, len});
+    q_.push_back(Job{host, dev, len, trace::host_enabled() ? trace::now_ns() : 0});
     cv_.notify_all();
   }
   // Every submitted copy has completed.
   void flush() {
+    const int64_t tf = trace::host_enabled() ? trace::now_ns() : 0;
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return q_.empty() && busy_ == 0; });
     lk.unlock();
@@ -196,6 +198,7 @@ class EarlyStager {
       }
     }
     if (!error_.empty()) throw UdaError("early H2D staging failed: " + error_);
+    if (tf) trace::host_event("stage_flush", bytes_, copies_, tf, trace::now_ns());
   }
   void reset() {
     flush();
@@ -215,6 +218,7 @@ class EarlyStager {
     const uint8_t* host;
     uint8_t* dev;
     int64_t len;
+    int64_t t_enq;  // trace: when the copy was queued
   };
   struct Block {
     gpu::DeviceBuffer buf;
@@ -261,6 +265,9 @@ class EarlyStager {
         if (e != hipSuccess) err = hipGetErrorString(e);
       }
       issue_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (j.t_enq) {
+        trace::host_event("stage_wait", j.len, (int64_t)(uintptr_t)j.host, j.t_enq, trace::now_ns());
+      }
       std::lock_guard<std::mutex> g(mu_);
       if (!err.empty() && error_.empty()) error_ = err;
       bytes_ += j.len;
@@ -944,6 +951,7 @@ void ReduceTask::merge_gpu() {
         // another and their H2D overlaps the rest of the fetch (all at once, they complete together)
         std::atomic<size_t> next_k{0};
         auto drain = [&](size_t k) {
+            const int64_t td = trace::host_enabled() ? trace::now_ns() : 0;
             try {
               MofFetcher& f = *ready[sub[k]];
               if (dst[k]) {
@@ -970,6 +978,7 @@ void ReduceTask::merge_gpu() {
             } catch (...) {
               errs[k] = std::current_exception();
             }
+            if (td) trace::host_event("drain", (int64_t)k, got[k].len, td, trace::now_ns());
         };
         std::vector<std::thread> ts;
         const size_t nthreads = drains > 0 ? std::min<size_t>((size_t)drains, sub.size()) : sub.size();
@@ -1010,6 +1019,7 @@ void ReduceTask::merge_gpu() {
                    fetch_ms, stager->engine(), (long long)stager->copies(), stager->bytes() / 1e6, stager->issue_ms(),
                    (long long)stage_step);
 
+    if (trace::host_enabled()) trace::host_event("fetch_phase", stage_step, drains, trace::now_ns() - (int64_t)(fetch_ms * 1e6), trace::now_ns());
     // ---- delivery of merged rounds; EOF rides in the very last buffer
     bool eof_sent = false;
     std::vector<uint8_t> tail((size_t)kv_buf_size_ + kEofBytes);
@@ -1199,6 +1209,11 @@ void ReduceTask::merge_gpu() {
     st_.gpu_sink_ms = ws.sink_ms + (ws2 ? ws2->sink_ms : 0);
     st_.fetch_ms = fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
+    if (trace::host_enabled()) {
+      trace::host_event("task", stage_step, drains,
+                        trace::now_ns() - (int64_t)((st_.merge_ms + fetch_ms) * 1e6), trace::now_ns());
+      trace::host_dump();
+    }
   } catch (...) {
     if (lpq_thr.joinable()) lpq_thr.join();  // the LPQ thread uses this frame's state
     cleanup(false);

@@ -17,6 +17,7 @@
 
 #include "uda/log.h"
 #include "uda/queues.h"
+#include "uda/trace.h"
 
 namespace uda {
 
@@ -196,7 +197,9 @@ int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off
     req.buf_len = std::min(buffer_size_, end - at);
     const int64_t want = req.buf_len;
     fetch_begin();
-    transport_->fetch(f.host, req, dst + at, [&, want, at](const FetchAck& a) {
+    const int64_t ti = trace::host_enabled() ? trace::now_ns() : 0;
+    transport_->fetch(f.host, req, dst + at, [&, want, at, ti](const FetchAck& a) {
+      if (ti) trace::host_event("fetch_req", want, (int64_t)(uintptr_t)(dst + at), ti, trace::now_ns());
       std::lock_guard<std::mutex> g(m);
       if (a.status != 0 && err.empty()) err = a.error.empty() ? "fetch failed" : a.error;
       if (a.status == 0 && a.sent != want && err.empty()) err = "short fetch";

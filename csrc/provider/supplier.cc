@@ -8,6 +8,7 @@
 #include "../gpu/device_ptr.h"
 #include "../gpu/mof_cache.h"
 #include "uda/log.h"
+#include "uda/trace.h"
 
 namespace uda {
 
@@ -250,10 +251,12 @@ void Supplier::process(Job& j) {
       j.done(ack);
       return;
     }
+    const int64_t tc = trace::host_enabled() ? trace::now_ns() : 0;
     if (mem->device >= 0)
       gpu::copy_device_to_host(j.dst, mem->data + off, len);
     else
       std::memcpy(j.dst, mem->data + off, (size_t)len);
+    if (tc) trace::host_event("serve_copy", len, (int64_t)(uintptr_t)j.dst, tc, trace::now_ns());
     bytes_ += len;
     j.done(ack);
     return;

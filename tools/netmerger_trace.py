@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Host-event trace of one NetMerger GPU task over host MOFs (2 GB secondary sort, loopback provider):
+whole-partition early staging vs piecewise staging (mapred.uda.gpu.early.h2d.step), taken apart from
+the UDA_HOST_TRACE events (csrc/common/trace.cc):
+
+  fetch_req    one transport request (issue -> completion callback)
+  serve_copy   the provider worker's memcpy into the consumer's pinned span
+  drain        one partition drained by a drain thread
+  stage_wait   an H2D staging copy: queued -> issued to the SDMA engine
+  stage_flush  the wait for every staged copy after the fetch
+  fetch_phase / task  phase brackets
+
+Prints one JSON line per variant (latency percentiles, memcpy GB/s, in-flight counts, 5 ms bins of
+bytes landed), for docs/BENCHMARKS.md's fetch-slowdown analysis.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+TRACE = os.path.abspath(os.environ.setdefault("UDA_HOST_TRACE", "/tmp/uda_host_trace.csv"))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def load(path):
+    ev = []
+    with open(path) as f:
+        for line in f:
+            k, tid, a, b, t0, t1 = line.rstrip("\n").split(",")
+            ev.append((k, int(tid), int(a), int(b), int(t0), int(t1)))
+    return ev
+
+
+def pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+
+def summarize(ev):
+    task = [e for e in ev if e[0] == "task"][-1]
+    t_start = task[4]
+    fp = [e for e in ev if e[0] == "fetch_phase"][-1]
+    out = {"task_ms": round((task[5] - task[4]) / 1e6, 1), "fetch_ms": round((fp[5] - fp[4]) / 1e6, 1)}
+    for kind in ("fetch_req", "serve_copy", "drain", "stage_wait"):
+        d = [(e[5] - e[4]) / 1e6 for e in ev if e[0] == kind]
+        out[kind] = {"n": len(d), "p50_ms": pct(d, 0.5), "p90_ms": pct(d, 0.9), "max_ms": max(d) if d else None}
+    sc = [e for e in ev if e[0] == "serve_copy"]
+    if sc:
+        gbps = [e[2] / max(e[5] - e[4], 1) for e in sc]  # bytes per ns = GB/s
+        out["serve_copy"]["p50_gbps"] = round(pct(gbps, 0.5), 2)
+        out["serve_copy"]["p10_gbps"] = round(pct(gbps, 0.1), 2)
+        out["serve_copy"]["threads"] = len({e[1] for e in sc})
+        # bytes landed per 5 ms bin, and mean memcpys in flight per bin
+        end = max(e[5] for e in sc)
+        nb = int((end - t_start) / 5e6) + 1
+        landed = [0.0] * nb
+        busy = [0.0] * nb
+        for e in sc:
+            landed[int((e[5] - t_start) / 5e6)] += e[2] / 1e6
+            t = e[4]
+            while t < e[5]:
+                b = int((t - t_start) / 5e6)
+                nxt = min(e[5], t_start + (b + 1) * 5e6)
+                busy[b] += (nxt - t) / 5e6
+                t = nxt
+        out["landed_mb_per_5ms"] = [round(x) for x in landed]
+        out["memcpys_in_flight_per_5ms"] = [round(x, 1) for x in busy]
+    sf = [e for e in ev if e[0] == "stage_flush"]
+    if sf:
+        out["stage_flush_ms"] = round((sf[-1][5] - sf[-1][4]) / 1e6, 1)
+        out["stage_copies"] = sf[-1][3]
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gb", type=float, default=2.0)
+    ap.add_argument("--maps", type=int, default=64)
+    ap.add_argument("--repeat", type=int, default=2)
+    args = ap.parse_args()
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    n = native()
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    runs = n.generate_runs("secondary", args.maps, 1, rows, 9)
+    prov = UdaProvider()
+    total = 0
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        total += len(data) - 2
+        prov.add_mof_memory("job_tr", f"attempt_tr_m_{m:06d}_0", data, index)
+    del runs
+    variants = [("warmup", {})] + [(f"{name}_{i}", conf) for i in range(args.repeat) for name, conf in (
+        ("whole", {}), ("step8m", {"mapred.uda.gpu.early.h2d.step": 8 << 20}),
+        ("step32m", {"mapred.uda.gpu.early.h2d.step": 32 << 20}))]
+    for i, (name, extra) in enumerate(variants):
+        if os.path.exists(TRACE):
+            os.unlink(TRACE)
+        conf = {"mapred.uda.merge.backend": "gpu", **extra}
+        c = UdaConsumer(args.maps, "job_tr", f"attempt_tr_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
+        t0 = time.perf_counter()
+        for m in range(args.maps):
+            c.fetch("localhost", "job_tr", f"attempt_tr_m_{m:06d}_0", 0)
+        c.wait(3600)
+        wall = time.perf_counter() - t0
+        st = c.close()
+        assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
+        res = {"variant": name, "gbps": round(total / wall / 1e9, 2), "wall_ms": round(wall * 1e3, 1),
+               "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")}}
+        if name != "warmup" and os.path.exists(TRACE):
+            res.update(summarize(load(TRACE)))
+        print(json.dumps(res), flush=True)
+    prov.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -81,6 +81,8 @@ class TeraSortShuffle:
         n = native()
         t0 = time.perf_counter()
         if self.ctx.world > 1:
+            if self.cfg.exchange == "ipc" and not self._ipc_preflight():
+                self.cfg.exchange = "rccl"  # every rank saw the same verdict (all-gathered)
             if self.cfg.exchange == "ipc":
                 name = f"uda.{os.getpid()}.{secrets.token_hex(6)}".encode() if self.ctx.rank == 0 else None
                 self.job.init_ipc(self.ctx.broadcast_bytes(name).decode())
@@ -111,6 +113,33 @@ class TeraSortShuffle:
         self.expected_records = rec[self.ctx.rank]
         self.job.set_j2c_sink(self.sink)
         self.setup_s = dict(comm_init=t1 - t0, generate=t2 - t1, plan=t3 - t2)
+
+    def _ipc_preflight(self) -> bool:
+        """Before the job commits to the IPC exchange: every rank exports a device buffer, maps every
+        peer's over hipIpc and pulls a patterned 68 KiB from each, 2 rounds (exchange_probe checks
+        every byte). All ranks all-gather the outcome, so they agree; on any failure the job falls
+        back to RCCL and says why (`ipc_fallback`). UDA_IPC_PREFLIGHT=0 skips it."""
+        self.ipc_fallback = None
+        if os.environ.get("UDA_IPC_PREFLIGHT", "1") == "0":
+            return True
+        w, r = self.ctx.world, self.ctx.rank
+        size = lambda f, t: [65536, 4096 + 104 * ((f + t) % 7)]
+        send = [size(r, p) if p != r else [] for p in range(w)]
+        recv = [size(p, r) if p != r else [] for p in range(w)]
+        name = f"udapre.{os.getpid()}.{secrets.token_hex(6)}".encode() if r == 0 else None
+        name = self.ctx.broadcast_bytes(name).decode()
+        try:
+            err = native().ipc_exchange_probe(name, r, w, send, recv, False, 2, self.device)
+        except Exception as e:  # noqa: BLE001 - reported to every rank below
+            err = f"{type(e).__name__}: {e}"
+        errs = self.ctx.all_gather_object(err)
+        bad = [f"rank {i}: {e}" for i, e in enumerate(errs) if e]
+        if bad:
+            self.ipc_fallback = "; ".join(bad)[:500]
+            if r == 0:
+                print(f"uda: IPC exchange preflight failed, using RCCL ({self.ipc_fallback})", flush=True)
+            return False
+        return True
 
     def step(self, validate: bool | None = None) -> dict:
         """One shuffle+merge+deliver pass. Every step checks what the consumers parsed (records per
