@@ -140,6 +140,10 @@ class EarlyStager {
         sdma_ = &gpu::SdmaEngine::for_device(device);
         sig_ = sdma_->make_signal();
         gpu::SdmaEngine::arm(sig_, 0);
+        for (auto& g : gsig_) {
+          g = sdma_->make_signal();
+          gpu::SdmaEngine::arm(g, 0);
+        }
       } catch (const std::exception& ex) {
         UDA_LOG(kWarn, "early staging: no SDMA engine (%s); using hipMemcpyAsync", ex.what());
         sdma_ = nullptr;
@@ -157,11 +161,15 @@ class EarlyStager {
     (void)hipStreamSynchronize(s_);
     (void)hipStreamDestroy(s_);
     if (sdma_) {
-      try {
-        gpu::SdmaEngine::wait(sig_);
-      } catch (...) {
+      std::vector<hsa_signal_t> all{sig_};
+      all.insert(all.end(), gsig_, gsig_ + kGroups);
+      for (hsa_signal_t g : all) {
+        try {
+          gpu::SdmaEngine::wait(g);
+        } catch (...) {
+        }
+        sdma_->destroy_signal(g);
       }
-      sdma_->destroy_signal(sig_);
     }
   }
   const char* engine() const { return sdma_ ? "sdma" : "hip"; }
@@ -176,11 +184,30 @@ class EarlyStager {
     std::lock_guard<std::mutex> g(mu_);
     return alloc(len);
   }
-  void copy(const uint8_t* host, uint8_t* dev, int64_t len) {
+  // group >= 0 (SDMA only): the copy also counts toward flush_group(group), so a caller can wait for
+  // one batch of copies (a progressive merge's phase) while later batches are still being queued.
+  void copy(const uint8_t* host, uint8_t* dev, int64_t len, int group = -1) {
     if (len <= 0) return;
     std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(Job{host, dev, len, trace::host_enabled() ? trace::now_ns() : 0});
+    if (group >= kGroups || (group >= 0 && !sdma_)) throw UdaError("early staging: bad copy group");
+    if (group >= 0) ++gqueued_[group];
+    q_.push_back(Job{host, dev, len, trace::host_enabled() ? trace::now_ns() : 0, group});
     cv_.notify_all();
+  }
+  static constexpr int kGroups = 16;
+  bool sdma() const { return sdma_ != nullptr; }
+  // Every copy of `group` queued so far has completed.
+  void flush_group(int group) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return gqueued_[group] == 0 || !error_.empty(); });
+    if (!error_.empty()) throw UdaError("early H2D staging failed: " + error_);
+    lk.unlock();
+    try {
+      gpu::SdmaEngine::wait(gsig_[group]);
+    } catch (const std::exception& ex) {
+      gpu::SdmaEngine::arm(gsig_[group], 0);
+      throw UdaError(std::string("early H2D staging failed: ") + ex.what());
+    }
   }
   // Every submitted copy has completed.
   void flush() {
@@ -190,11 +217,14 @@ class EarlyStager {
     lk.unlock();
     HIP_CHECK(hipStreamSynchronize(s_));
     if (sdma_) {
-      try {
-        gpu::SdmaEngine::wait(sig_);
-      } catch (const std::exception& ex) {
-        gpu::SdmaEngine::arm(sig_, 0);
-        throw UdaError(std::string("early H2D staging failed: ") + ex.what());
+      for (int g = -1; g < kGroups; ++g) {
+        hsa_signal_t sg = g < 0 ? sig_ : gsig_[g];
+        try {
+          gpu::SdmaEngine::wait(sg);
+        } catch (const std::exception& ex) {
+          gpu::SdmaEngine::arm(sg, 0);
+          throw UdaError(std::string("early H2D staging failed: ") + ex.what());
+        }
       }
     }
     if (!error_.empty()) throw UdaError("early H2D staging failed: " + error_);
@@ -219,6 +249,7 @@ class EarlyStager {
     uint8_t* dev;
     int64_t len;
     int64_t t_enq;  // trace: when the copy was queued
+    int group;
   };
   struct Block {
     gpu::DeviceBuffer buf;
@@ -253,11 +284,12 @@ class EarlyStager {
       const auto t0 = std::chrono::steady_clock::now();
       std::string err;
       if (sdma_) {
-        gpu::SdmaEngine::add(sig_, 1);
+        hsa_signal_t sg = j.group >= 0 ? gsig_[j.group] : sig_;
+        gpu::SdmaEngine::add(sg, 1);
         try {
-          sdma_->copy_h2d(j.dev, j.host, (size_t)j.len, sig_);
+          sdma_->copy_h2d(j.dev, j.host, (size_t)j.len, sg);
         } catch (const std::exception& ex) {
-          gpu::SdmaEngine::add(sig_, -1);
+          gpu::SdmaEngine::add(sg, -1);
           err = ex.what();
         }
       } else {
@@ -273,6 +305,7 @@ class EarlyStager {
       bytes_ += j.len;
       ++copies_;
       --busy_;
+      if (j.group >= 0) --gqueued_[j.group];  // issued (its signal tracks completion)
       cv_.notify_all();
     }
   }
@@ -280,6 +313,8 @@ class EarlyStager {
   hipStream_t s_ = nullptr;
   gpu::SdmaEngine* sdma_ = nullptr;
   hsa_signal_t sig_{};  // outstanding SDMA copies
+  hsa_signal_t gsig_[kGroups]{};  // outstanding copies per group
+  int64_t gqueued_[kGroups]{};    // queued, not yet issued, per group
   std::thread thr_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -691,6 +726,34 @@ void ReduceTask::merge_gpu() {
   // LPQ checkpoint (disk tier): spills[0, checkpointed) are fsynced, indexed in <path>.idx and
   // listed in the manifest; a failed attempt keeps them for the next one
   const bool ckpt = checkpoint_ && tier == "disk";
+  // Progressive merge (mapred.uda.gpu.progressive.phases = P > 1, online tasks whose whole input fits
+  // the device budget): every partition is fetched in P byte phases, all partitions' phase p before
+  // any phase p + 1, each phase staged to HBM as it lands. After phase p the key range below the least
+  // last-landed key has fully arrived in every run (plan_progressive_split), so it is merged and its
+  // output streamed back while phase p + 1 still comes in: the D2H of the output overlaps the H2D of
+  // the input on the duplex link instead of following it.
+  const int prog_phases = (int)std::min<int64_t>(EarlyStager::kGroups, host_->conf_i64("mapred.uda.gpu.progressive.phases", 0));
+  const bool prog_ok = prog_phases > 1 && stager && stager->sdma() && restored_files_.empty() && !ckpt;
+  bool prog_decided = false, progressive = false;
+  struct ProgFetch {
+    int P = 0, K = 0;
+    std::vector<std::shared_ptr<MofFetcher>> f;
+    std::vector<uint8_t*> dst, dev;
+    std::vector<int64_t> cap;
+    std::vector<std::vector<int64_t>> landed;  // [phase][run]: end of the bytes that phase fetched
+    std::vector<int> done;                     // per phase: partitions whose phase is fetched and queued to HBM
+    std::mutex mu;
+    std::condition_variable cv;
+    std::exception_ptr err;
+    std::atomic<int64_t> next{0};
+    std::vector<std::thread> threads;
+    std::chrono::steady_clock::time_point t_end;
+    ~ProgFetch() {
+      for (auto& t : threads)
+        if (t.joinable()) t.join();
+    }
+  };
+  std::unique_ptr<ProgFetch> prog;
   const std::string manifest = ckpt ? checkpoint_path() : std::string();
   size_t checkpointed = 0;
   std::vector<std::string> group_ids;  // MOFs of the current group (for the manifest)
@@ -923,6 +986,62 @@ void ReduceTask::merge_gpu() {
         }
       }
       for (auto& f : to_start) f->start();
+      if (prog_ok && !prog_decided) {
+        if (drained + (int)ready.size() < maps) continue;  // every partition's length before deciding
+        prog_decided = true;
+        int64_t tot = 0;
+        for (auto& f : ready) tot += std::max<int64_t>(f->part_len(), 0);
+        progressive = drained == 0 && tot <= budget;
+        if (progressive) {
+          prog = std::make_unique<ProgFetch>();
+          ProgFetch& pf = *prog;
+          pf.P = prog_phases;
+          pf.K = (int)ready.size();
+          pf.f = ready;
+          for (auto& f : ready) {
+            const int64_t cap = std::max<int64_t>(f->part_len(), 0);
+            pf.cap.push_back(cap);
+            pf.dst.push_back(fill_mem->alloc((size_t)std::max<int64_t>(cap, 1)));
+            pf.dev.push_back(stager->reserve(cap));
+          }
+          pf.landed.assign((size_t)pf.P, std::vector<int64_t>((size_t)pf.K, 0));
+          pf.done.assign((size_t)pf.P, 0);
+          EarlyStager* st = stager;
+          auto work = [this, &pf, st, depth] {
+            for (int64_t i; (i = pf.next++) < (int64_t)pf.P * pf.K;) {
+              const int p = (int)(i / pf.K), k = (int)(i % pf.K);
+              int64_t e = 0;
+              try {
+                MofFetcher& f = *pf.f[(size_t)k];
+                const int64_t cap = pf.cap[(size_t)k];
+                const int64_t b = cap * p / pf.P;
+                e = cap * (p + 1) / pf.P;
+                if (p == 0) {
+                  const int64_t off = f.take_first(pf.dst[(size_t)k], cap);
+                  if (off < e) fetch_direct(f.params(), pf.dst[(size_t)k], off, e, depth, nullptr, 0);
+                  e = std::max(e, off);
+                  st->copy(pf.dst[(size_t)k], pf.dev[(size_t)k], e, 0);
+                } else if (b < e) {  // (may refetch bytes the first chunk already brought: same bytes)
+                  fetch_direct(f.params(), pf.dst[(size_t)k], b, e, depth, nullptr, 0);
+                  st->copy(pf.dst[(size_t)k] + b, pf.dev[(size_t)k] + b, e - b, p);
+                }
+              } catch (...) {
+                std::lock_guard<std::mutex> g(pf.mu);
+                if (!pf.err) pf.err = std::current_exception();
+              }
+              std::lock_guard<std::mutex> g(pf.mu);
+              pf.landed[(size_t)p][(size_t)k] = e;
+              if (++pf.done[(size_t)p] == pf.K && p + 1 == pf.P) pf.t_end = std::chrono::steady_clock::now();
+              pf.cv.notify_all();
+            }
+          };
+          const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(drains > 0 ? drains : 8, pf.K));
+          for (int w = 0; w < nthreads; ++w) pf.threads.emplace_back(work);
+          drained = maps;  // the phases run on pf.threads; the merge below consumes them
+          ready.clear();
+          continue;
+        }
+      }
       // Drain arrived MOFs in parallel (each drain keeps one request in flight ahead) straight into
       // pinned spans of the group arena. Group boundaries are decided before a MOF is drained (on
       // its partition length), so a group is complete in host memory when it is merged and spilled.
@@ -1052,7 +1171,76 @@ void ReduceTask::merge_gpu() {
     const int64_t kv = kv_buf_size_ - kEofBytes;
 
     lpq_wait();  // an LPQ of the fetch phase may still be merging
-    if (spills.empty()) {
+    double prog_fetch_ms = -1;
+    if (progressive) {
+      ProgFetch& pf = *prog;
+      const int K = pf.K;
+      std::vector<int64_t> start((size_t)K, 0), land((size_t)K, 0);
+      for (int p = 0; p < pf.P; ++p) {
+        const auto tw = std::chrono::steady_clock::now();
+        {
+          std::unique_lock<std::mutex> lk(pf.mu);
+          pf.cv.wait(lk, [&] { return pf.done[(size_t)p] == K || pf.err || stop_; });
+          if (pf.err) std::rethrow_exception(pf.err);
+          if (stop_) throw UdaError("reduce task stopped during fetch");
+          for (int k = 0; k < K; ++k) land[(size_t)k] = std::max(land[(size_t)k], pf.landed[(size_t)p][(size_t)k]);
+        }
+        stager->flush_group(p);
+        ws.h2d_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
+        const bool last_phase = p + 1 == pf.P;
+        std::vector<Span> spans((size_t)K);
+        if (!last_phase) {
+          std::vector<const uint8_t*> win((size_t)K);
+          std::vector<int64_t> avail((size_t)K);
+          std::vector<char> fin((size_t)K);
+          for (int k = 0; k < K; ++k) {
+            win[(size_t)k] = pf.dev[(size_t)k] + start[(size_t)k];
+            avail[(size_t)k] = land[(size_t)k] - start[(size_t)k];
+            fin[(size_t)k] = land[(size_t)k] >= pf.cap[(size_t)k];
+          }
+          const auto tp = std::chrono::steady_clock::now();
+          const gpu::ProgressiveSplit sp = gpu::plan_progressive_split(win, avail, fin, (int)kind_, ws.rounds, s);
+          ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+          int64_t take = 0;
+          for (int k = 0; k < K; ++k) take += sp.split[(size_t)k];
+          if (take == 0) continue;  // nothing complete below the bound yet: wait for the next phase
+          for (int k = 0; k < K; ++k) {
+            spans[(size_t)k] = Span{pf.dst[(size_t)k] + start[(size_t)k], sp.split[(size_t)k],
+                                    pf.dev[(size_t)k] + start[(size_t)k]};
+            start[(size_t)k] += sp.split[(size_t)k];
+          }
+          {
+            std::lock_guard<std::mutex> g(st_mu_);
+            st_.rpq_rounds++;  // progressive phases merged
+          }
+        } else {
+          prog_fetch_ms = std::chrono::duration<double, std::milli>(pf.t_end - t0).count();
+          for (int k = 0; k < K; ++k)
+            spans[(size_t)k] = Span{pf.dst[(size_t)k] + start[(size_t)k], pf.cap[(size_t)k] - start[(size_t)k],
+                                    pf.dev[(size_t)k] + start[(size_t)k]};
+        }
+        device_merge(ws, spans, Codec::kNone, kind_, kv, s,
+                     [&](const std::vector<int64_t>& cuts, int64_t records, bool last) {
+                       DeviceMergeOut r;
+                       r.cuts = cuts;
+                       r.records = records;
+                       deliver(r, last && last_phase, ws.copy_stream(), ws);
+                     });
+      }
+      for (auto& t : pf.threads) t.join();
+      for (int k = 0; k < K; ++k) {
+        progress_count_++;
+        total_count_++;
+        {
+          std::lock_guard<std::mutex> gl(st_mu_);
+          st_.maps_fetched++;
+        }
+        if (progress_count_ == 20 || total_count_ == maps) {
+          host_->fetch_over();
+          progress_count_ = 0;
+        }
+      }
+    } else if (spills.empty()) {
       // ---- online: the whole reduce input in one device merge
       if (stager) {
         const auto tf = std::chrono::steady_clock::now();
@@ -1207,8 +1395,8 @@ void ReduceTask::merge_gpu() {
     st_.gpu_device_ms = ws.device_ms + (ws2 ? ws2->device_ms : 0);
     st_.gpu_d2h_wait_ms = ws.d2h_ms + (ws2 ? ws2->d2h_ms : 0);
     st_.gpu_sink_ms = ws.sink_ms + (ws2 ? ws2->sink_ms : 0);
-    st_.fetch_ms = fetch_ms;
-    st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
+    st_.fetch_ms = prog_fetch_ms >= 0 ? prog_fetch_ms : fetch_ms;
+    st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - st_.fetch_ms;
     if (trace::host_enabled()) {
       trace::host_event("task", stage_step, drains,
                         trace::now_ns() - (int64_t)((st_.merge_ms + fetch_ms) * 1e6), trace::now_ns());

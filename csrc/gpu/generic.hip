@@ -95,7 +95,9 @@ __device__ __forceinline__ void f1_stage(uint8_t* buf, int lane, const uint32_t 
 // Decode the record at LDS position i; returns its size, 0 for EOF, -1 for corrupt/truncated.
 // Fast path: both VInt headers are single bytes (lengths < 128, the common case); the two header
 // bytes come from two independent aligned dword reads instead of two dependent byte reads.
-__device__ __forceinline__ int64_t f1_record(const uint8_t* buf, int i, int lim, int64_t remain) {
+// partial: the run is a landed prefix of a stream still arriving; a record cut by its end (header or
+// body) ends it like the EOF marker (0), so rec_bytes is the prefix's last complete record end.
+__device__ __forceinline__ int64_t f1_record(const uint8_t* buf, int i, int lim, int64_t remain, bool partial) {
   if (i + 2 <= lim) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(buf + (i & ~3));
     const uint64_t two = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
@@ -103,31 +105,31 @@ __device__ __forceinline__ int64_t f1_record(const uint8_t* buf, int i, int lim,
     const int8_t b0 = (int8_t)(two >> sh), b1 = (int8_t)(two >> (sh + 8));
     if (b0 >= 0 && b1 >= 0) {
       const int64_t sz = 2 + (int64_t)b0 + (int64_t)b1;
-      return sz > remain ? -1 : sz;
+      return sz > remain ? (partial ? 0 : -1) : sz;
     }
   }
   int64_t kl = 0, vl = 0;
   const int a = lds_vint(buf, i, lim, &kl);
   const int b = a ? lds_vint(buf, i + a, lim, &vl) : 0;
-  if (a == 0 || b == 0) return -1;
+  if (a == 0 || b == 0) return partial && remain < 20 ? 0 : -1;  // header cut by the prefix end
   if (kl == -1 && vl == -1) return 0;
   if (kl < 0 || vl < 0) return -1;
   const int64_t sz = a + b + kl + vl;
-  return sz > remain ? -1 : sz;
+  return sz > remain ? (partial ? 0 : -1) : sz;
 }
 
 // The general decoder alone (multi-byte VInt headers, the EOF marker, a record at the run's tail):
 // reads only bytes below lim.
 template <class BP>
-__device__ __forceinline__ int64_t f1_record_slow(BP buf, int i, int lim, int64_t remain) {
+__device__ __forceinline__ int64_t f1_record_slow(BP buf, int i, int lim, int64_t remain, bool partial) {
   int64_t kl = 0, vl = 0;
   const int a = lds_vint(buf, i, lim, &kl);
   const int b = a ? lds_vint(buf, i + a, lim, &vl) : 0;
-  if (a == 0 || b == 0) return -1;
+  if (a == 0 || b == 0) return partial && remain < 20 ? 0 : -1;
   if (kl == -1 && vl == -1) return 0;
   if (kl < 0 || vl < 0) return -1;
   const int64_t sz = a + b + kl + vl;
-  return sz > remain ? -1 : sz;
+  return sz > remain ? (partial ? 0 : -1) : sz;
 }
 
 typedef __attribute__((address_space(1))) const uint8_t GlobalU8;
@@ -136,7 +138,8 @@ template <bool kProf>
 __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                            const int64_t* chunk_base, int64_t* ck_start,
                                                            int64_t* ck_count, int64_t* counts, int64_t* rec_bytes,
-                                                           int* status, uint64_t* prof, const int* run_ids) {
+                                                           int* status, uint64_t* prof, const int* run_ids,
+                                                           int partial) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kF1Chunk + 64];
   const int r = run_ids ? run_ids[blockIdx.x] : (int)blockIdx.x;
   const int lane = threadIdx.x;
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(kF1Lanes) f1_scan_kernel(uint8_t* const* bases
       int64_t here = 0;
       ck_start[cb + c] = pos;  // first record at or after c0 (or the end)
       while (pos < end) {
-        const int64_t sz = f1_record(buf, (int)(pos - c0), lim, n - pos);
+        const int64_t sz = f1_record(buf, (int)(pos - c0), lim, n - pos, partial != 0);
         if (sz <= 0) {
           if (sz < 0) st = 1;
           done = true;
@@ -237,18 +240,18 @@ constexpr int64_t kSupInvalid = -1, kSupFallback = -2;  // super codes; EOF at q
 // return 0 (global memory, where bytes past the run are not ours; the LDS stage is zero-padded).
 template <bool kGuard, class BP>
 __device__ __forceinline__ void f1_step(BP buf, int lim, int64_t nrel64, int nrel, int end_rel, int key_kind, int& pos,
-                                        int& cnt, int& code, bool& alive) {
+                                        int& cnt, int& code, bool& alive, bool partial) {
   auto rd = [&](int i) -> int { return kGuard && i >= lim ? 0 : (int)(int8_t)buf[i]; };
   const int p = alive ? pos : 0;
   const int b0 = rd(p), b1 = rd(p + 1);
   int sz = 2 + b0 + b1;
   bool fallback = false;
   if (alive && ((b0 | b1) < 0 || p + 2 > lim)) {
-    const int64_t s64 = f1_record_slow(buf, p, lim, nrel64 - p);
+    const int64_t s64 = f1_record_slow(buf, p, lim, nrel64 - p, partial);
     fallback = s64 > (int64_t)(1 << 30);
     sz = fallback ? 1 : (int)s64;
   } else if (p + sz > nrel) {
-    sz = -1;
+    sz = partial && p + sz > nrel64 ? 0 : -1;  // partial: cut by the landed prefix's end
   }
   if (key_kind == (int)KeyKind::kText && (b0 | b1) >= 0 && p + 3 <= lim)
     fallback = fallback || !(b0 >= 1 && rd(p + 2) == b0 - 1);
@@ -268,7 +271,8 @@ __device__ __forceinline__ void f1_step(BP buf, int lim, int64_t nrel64, int nre
 __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                                  const int64_t* chunk_base, const int32_t* chunk_run,
                                                                  int64_t nchunks, int32_t* fx, int32_t* fn,
-                                                                 int key_kind, int32_t* chase, int32_t* chase_n) {
+                                                                 int key_kind, int32_t* chase, int32_t* chase_n,
+                                                                 int partial) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
   __shared__ int f1_live[kF1FnWaves][3 * kF1Entries];  // surviving chains: entry, position, count
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -300,7 +304,7 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
   const int64_t nrel64 = n - c0;
   const int nrel = (int)min(nrel64, (int64_t)(1 << 30));  // records must end by here (fast path)
   auto step = [&](int& pos, int& cnt, int& code, bool& alive) {
-    f1_step<false>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive);
+    f1_step<false>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive, partial != 0);
   };
   int32_t* x = fx + c * kF1Entries;
   int32_t* m = fn + c * kF1Entries;
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
 __global__ void __launch_bounds__(256) f1_chase_kernel(uint8_t* const* bases, const int64_t* nbytes,
                                                        const int64_t* chunk_base, const int32_t* chunk_run,
                                                        int64_t nchunks, const int32_t* chase, const int32_t* chase_n,
-                                                       int32_t* fx, int32_t* fn, int key_kind) {
+                                                       int32_t* fx, int32_t* fn, int key_kind, int partial) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t c = t / kF1Chase;
   const int i = (int)(t % kF1Chase);
@@ -396,7 +400,7 @@ __global__ void __launch_bounds__(256) f1_chase_kernel(uint8_t* const* bases, co
   const int e = in[0];
   int pos = in[1], cnt = in[2], code = pos;
   bool alive = true;
-  while (alive) f1_step<true>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive);
+  while (alive) f1_step<true>(buf, lim, nrel64, nrel, end_rel, key_kind, pos, cnt, code, alive, partial != 0);
   fx[c * kF1Entries + e] = code;
   fn[c * kF1Entries + e] = cnt;
 }
@@ -833,14 +837,14 @@ void launch_max_i64(const int64_t* v, int64_t n, unsigned long long* out, hipStr
 
 void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                     int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
-                    hipStream_t s, uint64_t* prof, const int* run_ids) {
+                    hipStream_t s, uint64_t* prof, const int* run_ids, bool partial) {
   if (nruns <= 0) return;
   if (prof)
     hipLaunchKernelGGL(f1_scan_kernel<true>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes, chunk_base,
-                       ck_start, ck_count, counts, rec_bytes, status, prof, run_ids);
+                       ck_start, ck_count, counts, rec_bytes, status, prof, run_ids, (int)partial);
   else
     hipLaunchKernelGGL(f1_scan_kernel<false>, dim3((unsigned)nruns), dim3(kF1Lanes), 0, s, bases, nbytes,
-                       chunk_base, ck_start, ck_count, counts, rec_bytes, status, prof, run_ids);
+                       chunk_base, ck_start, ck_count, counts, rec_bytes, status, prof, run_ids, (int)partial);
 }
 
 size_t f1_parallel_workspace(int64_t nchunks, int64_t nsup) {
@@ -852,7 +856,7 @@ int64_t f1_super_chunks() { return kF1Super; }
 void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                         const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
                         int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
-                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind) {
+                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind, bool partial) {
   if (nruns <= 0) return;
   uint8_t* w = static_cast<uint8_t*>(workspace);
   int32_t* fx = reinterpret_cast<int32_t*>(w);
@@ -865,10 +869,11 @@ void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns,
   int32_t* chase_n = chase + nchunks * kF1Chase * 3;
   if (nchunks > 0) {
     hipLaunchKernelGGL(f1_fn_kernel, dim3((unsigned)((nchunks + kF1FnWaves - 1) / kF1FnWaves)), dim3(64 * kF1FnWaves),
-                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn, key_kind, chase, chase_n);
+                       0, s, bases, nbytes, chunk_base, chunk_run, nchunks, fx, fn, key_kind, chase, chase_n,
+                       (int)partial);
     const int64_t lanes = nchunks * kF1Chase;
     hipLaunchKernelGGL(f1_chase_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, bases, nbytes,
-                       chunk_base, chunk_run, nchunks, chase, chase_n, fx, fn, key_kind);
+                       chunk_base, chunk_run, nchunks, chase, chase_n, fx, fn, key_kind, (int)partial);
     hipLaunchKernelGGL(f1_super_kernel, dim3((unsigned)((nsup + 3) / 4)), dim3(256), 0, s, nbytes, chunk_base,
                        sup_base, sup_run, nsup, fx, fn, sx, sn);
     (void)hipMemsetAsync(sup_entry, 0xFF, (size_t)nsup * 8, s);

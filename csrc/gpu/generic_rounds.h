@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "device_engine.h"
@@ -43,6 +44,25 @@ struct GenericRoundsWs {
 // Synchronizes `s`.
 GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
                                       int kind, int64_t round_bytes, GenericRoundsWs& ws, hipStream_t s);
+
+// Progressive merging of runs that are still arriving (a reduce task whose partitions land over PCIe
+// while the merged output goes back the other way). windows[k]: device bytes of run k not merged yet,
+// avail[k] of them landed; final_run[k]: the window holds the rest of run k. F1 over the landed
+// prefixes (a record cut by the prefix end is not counted) gives each window's complete records; the
+// bound is the least key among the last complete records of the non-final windows (every record
+// below it has landed in every run); split[k] = the first record of window k not below the bound, so
+// merging [0, split[k]) of every window emits a key range no later record can precede. No bound when
+// every window is final (split = complete); all splits 0 when a non-final window has no complete
+// record yet.
+struct ProgressiveSplit {
+  std::vector<int64_t> complete, split;
+  bool bounded = false;
+  std::string bound;
+  double ms = 0;
+};
+ProgressiveSplit plan_progressive_split(const std::vector<const uint8_t*>& windows, const std::vector<int64_t>& avail,
+                                        const std::vector<char>& final_run, int kind, GenericRoundsWs& ws,
+                                        hipStream_t s);
 
 }  // namespace gpu
 }  // namespace uda

@@ -120,6 +120,40 @@ __global__ void __launch_bounds__(64) gr_split_kernel(uint8_t* const* bases, con
   out[(int64_t)r * (nb + 2) + 1 + bi] = pos < end ? pos : end;
 }
 
+// Key of the last complete record of each run (up to kSampleKey content bytes; klen -1 if the run has
+// none): the last chunk in which a record starts below rec_bytes, then a walk to the last start.
+__global__ void __launch_bounds__(64) gr_lastkey_kernel(uint8_t* const* bases, const int64_t* rec_bytes,
+                                                        const int64_t* chunk_base, const int64_t* ck_start,
+                                                        const int64_t* ck_count, int nruns, int kind,
+                                                        int64_t chunk_bytes, uint8_t* keys, int32_t* klen) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nruns) return;
+  klen[r] = -1;
+  const int64_t rb = rec_bytes[r];
+  if (rb <= 0) return;
+  const int64_t lo = chunk_base[r];
+  int64_t c = lo + (rb - 1) / chunk_bytes;
+  if (c >= chunk_base[r + 1]) c = chunk_base[r + 1] - 1;
+  while (c >= lo && (ck_count[c] == 0 || ck_start[c] >= rb)) --c;
+  if (c < lo) return;
+  const uint8_t* p = bases[r];
+  int64_t pos = ck_start[c], last = pos;
+  while (pos < rb) {
+    int len = 0;
+    int64_t size = 0;
+    (void)rec_key(p + pos, rb - pos, kind, &len, &size);
+    if (size <= 0) break;
+    last = pos;
+    pos += size;
+  }
+  int len = 0;
+  int64_t size = 0;
+  const uint8_t* k = rec_key(p + last, rb - last, kind, &len, &size);
+  const int n = len < kSampleKey ? len : kSampleKey;
+  for (int j = 0; j < n; ++j) keys[(int64_t)r * kSampleKey + j] = k[j];
+  klen[r] = n;
+}
+
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -127,33 +161,32 @@ double now_ms() {
 void ensure(DeviceBuffer& b, size_t bytes) {
   if (b.size() < bytes) b.alloc(bytes + bytes / 8 + 256);
 }
-}  // namespace
+struct F1Dev {
+  int64_t nchunks = 0;
+  std::vector<int64_t> chunk_base;
+  std::vector<int32_t> chunk_run;
+  uint8_t** d_bases = nullptr;
+  int64_t *d_nbytes = nullptr, *d_counts = nullptr, *d_recb = nullptr, *d_cbase = nullptr;
+  int64_t *d_ckstart = nullptr, *d_ckcount = nullptr;
+  int* d_status = nullptr;
+};
 
-GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
-                                      int kind, int64_t round_bytes, GenericRoundsWs& ws, hipStream_t s) {
-  const double t0 = now_ms();
-  GenericRoundsPlan plan;
+// F1 pass 1 over the runs (chunk checkpoints, record bytes per run) in the planner's workspace.
+// partial: runs are landed prefixes (a record cut by the end is not counted). Synchronizes `s`;
+// throws on a corrupt run.
+F1Dev f1_checkpoints(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes, int kind,
+                     bool partial, GenericRoundsWs& ws, hipStream_t s) {
+  F1Dev f;
   const int K = (int)runs.size();
-  int64_t total = 0;
-  for (int64_t b : run_bytes) total += b;
-  const int want = (int)std::max<int64_t>(1, (total + std::max<int64_t>(round_bytes, 1) - 1) / std::max<int64_t>(round_bytes, 1));
-  auto trivial = [&] {
-    plan.rounds = 1;
-    plan.pos.assign((size_t)K * 2, 0);
-    for (int k = 0; k < K; ++k) plan.pos[(size_t)k * 2 + 1] = run_bytes[k];
-    plan.max_round_bytes = total;
-    plan.plan_ms = now_ms() - t0;
-    return plan;
-  };
-  if (want <= 1 || K == 0) return trivial();
-
-  // ---- F1 checkpoints of the whole runs (pass 1 only)
   const int64_t CH = f1_chunk_bytes();
-  std::vector<int64_t> chunk_base(K + 1, 0);
+  std::vector<int64_t>& chunk_base = f.chunk_base;
+  chunk_base.assign(K + 1, 0);
   for (int k = 0; k < K; ++k) chunk_base[k + 1] = chunk_base[k] + (run_bytes[k] + CH - 1) / CH;
   const int64_t nchunks = chunk_base[K];
-  if (nchunks == 0) return trivial();
-  std::vector<int32_t> chunk_run((size_t)nchunks);
+  f.nchunks = nchunks;
+  if (nchunks == 0) return f;
+  std::vector<int32_t>& chunk_run = f.chunk_run;
+  chunk_run.resize((size_t)nchunks);
   for (int k = 0; k < K; ++k)
     for (int64_t c = chunk_base[k]; c < chunk_base[k + 1]; ++c) chunk_run[(size_t)c] = k;
   const int64_t SC = f1_super_chunks();
@@ -189,7 +222,7 @@ GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, c
   HIP_CHECK(hipMemcpyAsync(d_supbase, sup_base.data(), 8 * (size_t)(K + 1), hipMemcpyHostToDevice, s));
   if (nsup > 0) HIP_CHECK(hipMemcpyAsync(d_suprun, sup_run.data(), 4 * (size_t)nsup, hipMemcpyHostToDevice, s));
   launch_f1_parallel(d_bases, d_nbytes, K, d_cbase, d_crun, nchunks, d_supbase, d_suprun, nsup, d_fws, d_ckstart,
-                     d_ckcount, d_counts, d_recb, d_status, s, kind);
+                     d_ckcount, d_counts, d_recb, d_status, s, kind, partial);
   std::vector<int> status(K);
   HIP_CHECK(hipMemcpyAsync(status.data(), d_status, 4 * (size_t)K, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -200,12 +233,49 @@ GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, c
     DeviceBuffer d_redo(redo.size() * 4);
     HIP_CHECK(hipMemcpyAsync(d_redo.as(), redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
     launch_f1_scan(d_bases, d_nbytes, (int)redo.size(), d_cbase, d_ckstart, d_ckcount, d_counts, d_recb, d_status, s,
-                   nullptr, d_redo.as<int>());
+                   nullptr, d_redo.as<int>(), partial);
     HIP_CHECK(hipMemcpyAsync(status.data(), d_status, 4 * (size_t)K, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
   }
   for (int k = 0; k < K; ++k)
     if (status[k] != 0) throw std::runtime_error("round planning: corrupt or truncated IFile run " + std::to_string(k));
+  f.d_bases = d_bases;
+  f.d_nbytes = d_nbytes;
+  f.d_counts = d_counts;
+  f.d_recb = d_recb;
+  f.d_status = d_status;
+  f.d_cbase = d_cbase;
+  f.d_ckstart = d_ckstart;
+  f.d_ckcount = d_ckcount;
+  return f;
+}
+}  // namespace
+
+GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, const std::vector<int64_t>& run_bytes,
+                                      int kind, int64_t round_bytes, GenericRoundsWs& ws, hipStream_t s) {
+  const double t0 = now_ms();
+  GenericRoundsPlan plan;
+  const int K = (int)runs.size();
+  int64_t total = 0;
+  for (int64_t b : run_bytes) total += b;
+  const int want = (int)std::max<int64_t>(1, (total + std::max<int64_t>(round_bytes, 1) - 1) / std::max<int64_t>(round_bytes, 1));
+  auto trivial = [&] {
+    plan.rounds = 1;
+    plan.pos.assign((size_t)K * 2, 0);
+    for (int k = 0; k < K; ++k) plan.pos[(size_t)k * 2 + 1] = run_bytes[k];
+    plan.max_round_bytes = total;
+    plan.plan_ms = now_ms() - t0;
+    return plan;
+  };
+  if (want <= 1 || K == 0) return trivial();
+
+  // ---- F1 checkpoints of the whole runs (pass 1 only)
+  F1Dev f = f1_checkpoints(runs, run_bytes, kind, false, ws, s);
+  const int64_t nchunks = f.nchunks;
+  if (nchunks == 0) return trivial();
+  const std::vector<int32_t>& chunk_run = f.chunk_run;
+  uint8_t** d_bases = f.d_bases;
+  int64_t *d_recb = f.d_recb, *d_cbase = f.d_cbase, *d_ckstart = f.d_ckstart, *d_ckcount = f.d_ckcount;
 
   // ---- sample chunk-leading keys (chunks spread evenly over all input bytes)
   const int64_t ns = std::min<int64_t>(nchunks, (int64_t)want * kSamplesPerRound);
@@ -284,6 +354,76 @@ GenericRoundsPlan plan_generic_rounds(const std::vector<const uint8_t*>& runs, c
   }
   plan.plan_ms = now_ms() - t0;
   return plan;
+}
+
+ProgressiveSplit plan_progressive_split(const std::vector<const uint8_t*>& windows, const std::vector<int64_t>& avail,
+                                        const std::vector<char>& final_run, int kind, GenericRoundsWs& ws,
+                                        hipStream_t s) {
+  const double t0 = now_ms();
+  ProgressiveSplit ps;
+  const int K = (int)windows.size();
+  ps.complete.assign(K, 0);
+  ps.split.assign(K, 0);
+  F1Dev f = f1_checkpoints(windows, avail, kind, true, ws, s);
+  if (f.nchunks == 0) {
+    ps.ms = now_ms() - t0;
+    return ps;
+  }
+  HIP_CHECK(hipMemcpyAsync(ps.complete.data(), f.d_recb, 8 * (size_t)K, hipMemcpyDeviceToHost, s));
+  ensure(ws.samp, (size_t)K * (4 + kSampleKey) + 256);
+  auto* d_kl = ws.samp.as<int32_t>();
+  auto* d_keys = reinterpret_cast<uint8_t*>(d_kl + K + 16);
+  hipLaunchKernelGGL(gr_lastkey_kernel, dim3((unsigned)((K + 63) / 64)), dim3(64), 0, s, f.d_bases, f.d_recb, f.d_cbase,
+                     f.d_ckstart, f.d_ckcount, K, kind, f1_chunk_bytes(), d_keys, d_kl);
+  HIP_CHECK(hipGetLastError());
+  std::vector<int32_t> kl((size_t)K);
+  std::vector<uint8_t> keys((size_t)K * kSampleKey);
+  HIP_CHECK(hipMemcpyAsync(kl.data(), d_kl, 4 * (size_t)K, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(keys.data(), d_keys, keys.size(), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  // bound: the least last-complete key over the windows that do not reach their run's end; every
+  // record below it has landed (a run's later records are >= its last landed key >= the bound)
+  bool have = false, all_final = true;
+  std::string bound;
+  for (int k = 0; k < K; ++k) {
+    if (final_run[(size_t)k]) continue;
+    all_final = false;
+    if (kl[(size_t)k] < 0) {  // nothing complete landed yet in this window: no record is safe to merge
+      ps.ms = now_ms() - t0;
+      return ps;
+    }
+    std::string key(reinterpret_cast<const char*>(&keys[(size_t)k * kSampleKey]), (size_t)kl[(size_t)k]);
+    if (!have || key < bound) bound = std::move(key);
+    have = true;
+  }
+  if (all_final) {  // the rest of every run: no bound
+    ps.split = ps.complete;
+    ps.bounded = false;
+    ps.ms = now_ms() - t0;
+    return ps;
+  }
+  ps.bounded = true;
+  ps.bound = bound;
+  const int32_t boff[2] = {0, (int32_t)bound.size()};
+  ensure(ws.bounds, bound.size() + 8 + 64);
+  auto* d_boff = ws.bounds.as<int32_t>();
+  auto* d_bb = reinterpret_cast<uint8_t*>(d_boff + 2);
+  HIP_CHECK(hipMemcpyAsync(d_boff, boff, 8, hipMemcpyHostToDevice, s));
+  if (!bound.empty()) HIP_CHECK(hipMemcpyAsync(d_bb, bound.data(), bound.size(), hipMemcpyHostToDevice, s));
+  ensure(ws.out, 8 * (size_t)K * 3);
+  hipLaunchKernelGGL(gr_split_kernel, dim3((unsigned)((K + 63) / 64)), dim3(64), 0, s, f.d_bases, f.d_recb, f.d_cbase,
+                     f.d_ckstart, f.d_ckcount, K, kind, d_bb, d_boff, 1, ws.out.as<int64_t>());
+  HIP_CHECK(hipGetLastError());
+  std::vector<int64_t> pos((size_t)K * 3);
+  HIP_CHECK(hipMemcpyAsync(pos.data(), ws.out.as(), 8 * pos.size(), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (int k = 0; k < K; ++k) {
+    const int64_t v = pos[(size_t)k * 3 + 1];
+    if (v < 0 || v > ps.complete[(size_t)k]) throw std::runtime_error("progressive split out of range in run " + std::to_string(k));
+    ps.split[(size_t)k] = v;
+  }
+  ps.ms = now_ms() - t0;
+  return ps;
 }
 
 }  // namespace gpu

@@ -173,10 +173,12 @@ void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem
 // F1 pass 1 (one wave per run): chunk checkpoints ck_start/ck_count for the chunks of run r at
 // [chunk_base[r], chunk_base[r+1]) (chunks of f1_chunk_bytes()), records per run, record bytes
 // before the EOF marker, status != 0 on a corrupt/truncated stream. prof: diagnostic cycle split.
+// partial: every run is the landed prefix of a stream still arriving; a record cut by its end ends
+// the run like the EOF marker, so rec_bytes is the end of its last complete record.
 int64_t f1_chunk_bytes();
 void launch_f1_scan(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                     int64_t* ck_start, int64_t* ck_count, int64_t* counts, int64_t* rec_bytes, int* status,
-                    hipStream_t s, uint64_t* prof = nullptr, const int* run_ids = nullptr);
+                    hipStream_t s, uint64_t* prof = nullptr, const int* run_ids = nullptr, bool partial = false);
 // F1 pass 1, parallel form: same outputs as launch_f1_scan from per-chunk transfer functions
 // composed per superchunk (f1_super_chunks() chunks) and per run. sup_base[r]..sup_base[r+1] are
 // run r's superchunks, sup_run their run. status[r] == 2: the run needs the serial scan.
@@ -185,7 +187,7 @@ int64_t f1_super_chunks();
 void launch_f1_parallel(uint8_t* const* bases, const int64_t* nbytes, int nruns, const int64_t* chunk_base,
                         const int32_t* chunk_run, int64_t nchunks, const int64_t* sup_base, const int32_t* sup_run,
                         int64_t nsup, void* workspace, int64_t* ck_start, int64_t* ck_count, int64_t* counts,
-                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind = -1);
+                        int64_t* rec_bytes, int* status, hipStream_t s, int key_kind = -1, bool partial = false);
 // F1 pass 2 (one wave per chunk): record offsets; ck_ord = exclusive scan of ck_count (global
 // record ordinal of each chunk's first record), elem_off = first ordinal of each run (nruns+1),
 // chunk_run[c] = run of chunk c. offsets[r] has counts[r]+1 entries (last = record bytes).

@@ -147,6 +147,41 @@ def test_consumer_gpu_fetch_drains_and_piecewise_staging(require_gpu, drains, st
         p.close()
 
 
+@pytest.mark.parametrize("phases,drains,maps,kind", [(2, 3, 9, "text"), (3, 1, 9, "text"), (7, 3, 9, "text"),
+                                                     (4, 8, 20, "bytes"), (5, 3, 3, "text")])
+def test_consumer_gpu_progressive_phases(require_gpu, phases, drains, maps, kind):
+    """mapred.uda.gpu.progressive.phases: partitions fetched in byte phases (all partitions' phase p
+    first), each phase's key range below the least last-landed key merged and delivered while later
+    phases arrive. The stream must equal the CPU merge's, with records cut by a phase end (partial F1)
+    carried into the next phase, and partitions of very different sizes (skewed reducers)."""
+    from uda_amd.utils.mof import encode_partitions
+    p = UdaProvider()
+    try:
+        if kind == "text":
+            mp = datagen.secondary_sort(num_maps=maps, reducers=2, rows_per_map=1500, seed=13 + phases)
+            key_class = datagen.TEXT
+        else:
+            mp = datagen.bytes_writable(num_maps=maps, reducers=2, rows_per_map=900, seed=3)
+            key_class = datagen.BYTES
+        ids = []
+        for i, parts in enumerate(datagen.streams(mp)):
+            mid = f"attempt_p_m_{i:06d}_0"
+            data, index = encode_partitions(parts)
+            p.add_mof_memory("job_p", mid, data, index)
+            ids.append(mid)
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": drains,
+                "mapred.uda.gpu.progressive.phases": phases}
+        recs_gpu, st, _ = run_reduce("h", "job_p", ids, 0, key_class, conf=conf, max_buf_kb=16, min_buf_kb=16,
+                                     kv_buf_size=8192)
+        recs_cpu, _, _ = run_reduce("h", "job_p", ids, 0, key_class, max_buf_kb=16, min_buf_kb=16, kv_buf_size=8192)
+        assert st["backend"] == "gpu" and st["maps_fetched"] == maps
+        assert [k for k, _ in recs_gpu] == [k for k, _ in recs_cpu]
+        assert sorted(recs_gpu) == sorted(recs_cpu)
+        assert st["rpq_rounds"] >= 1  # at least one phase merged before the last one
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("tier,codec", [("host", None), ("disk", None), ("disk", "snappy")])
 def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
     """Reduce input larger than the device budget: LPQ merges on the GPU spill to host DRAM or to

@@ -1,9 +1,10 @@
 #!/bin/bash
-# In-place k-way A/B + W=2 spill tiers (tools/gpu_r3_inplace.sh), vectorized F6 decode: tests, compressed
-# C-ABI benches, kernel-trace profile of the Snappy run.
+# Progressive NetMerger phases (tests + trace), vectorized F6 decode (tests + compressed C-ABI benches),
+# in-place k-way A/B (tools/gpu_r3_inplace.sh).
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+bash tools/gpu_r3_prog.sh || exit 1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_decode.py \
   tests/test_gpu_api_device.py -k "decode or codec or compress or snappy or lzo" > gpurun_out/r3_decode_tests.log 2>&1 \
   || { tail -30 gpurun_out/r3_decode_tests.log; exit 1; }
@@ -14,7 +15,3 @@ for c in snappy lzo; do
   echo "$c $(tail -1 gpurun_out/r3_bench_api_${c}_41GB_vec.log | cut -c1-150)"
 done
 bash tools/gpu_r3_inplace.sh || exit 1
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lzo -o lzo -- python3 bench.py --api --api-codec lzo \
-  --rows-per-gpu 400000000 --steps 2 --warmup 1 > gpurun_out/r3_prof_lzo.log 2>&1 || { tail -20 gpurun_out/r3_prof_lzo.log; exit 1; }
-find gpurun_out/prof_lzo -name "*kernel_stats.csv" | head -1 | xargs head -12 | cut -c1-200

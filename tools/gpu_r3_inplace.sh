@@ -7,18 +7,10 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_terasort.py \
   -k "kway" > gpurun_out/r3_inplace_tests.log 2>&1 || { tail -30 gpurun_out/r3_inplace_tests.log; exit 1; }
 tail -1 gpurun_out/r3_inplace_tests.log
-for cfg in "0 1536" "1 1536" "1 2048" "1 1024" "0 1536" "1 1536"; do
+for cfg in "0 1536" "1 1536" "1 2048" "1 1024" "1 1536"; do
   set -- $cfg
   log=gpurun_out/r3_kway_inplace$1_cap$2.log
   UDA_KWAY_INPLACE=$1 UDA_KWAY_CAP=$2 timeout -k 10 300 python -u bench.py --device-only --steps 5 --warmup 1 --no-validate \
     > $log 2>&1 || { tail -20 $log; exit 1; }
   echo "inplace=$1 cap=$2 $(tail -1 $log | cut -c1-140)"
-done
-# W > 1 spill tiers: 2 real processes on GPU 0 over the IPC exchange, staging on the SDMA thread
-for st in host disk; do
-  rows=200000000; [ $st = disk ] && rows=100000000
-  log=gpurun_out/r3_bench_ipc2_store_$st.log
-  timeout -k 10 600 python -u bench.py --gpus 2 --one-gpu --exchange ipc --store $st --rows-per-gpu $rows --steps 3 --warmup 1 \
-    > $log 2>&1 || { tail -20 $log; exit 1; }
-  echo "store=$st $(tail -1 $log | cut -c1-200)"
 done

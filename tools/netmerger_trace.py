@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host-event trace of one NetMerger GPU task over host MOFs (2 GB secondary sort, loopback provider):
-whole-partition early staging vs piecewise staging (mapred.uda.gpu.early.h2d.step), taken apart from
-the UDA_HOST_TRACE events (csrc/common/trace.cc):
+whole-partition early staging vs piecewise staging (mapred.uda.gpu.early.h2d.step) vs progressive
+phases (mapred.uda.gpu.progressive.phases), taken apart from the UDA_HOST_TRACE events
+(csrc/common/trace.cc):
 
   fetch_req    one transport request (issue -> completion callback)
   serve_copy   the provider worker's memcpy into the consumer's pinned span
@@ -82,6 +83,8 @@ def main() -> int:
     ap.add_argument("--gb", type=float, default=2.0)
     ap.add_argument("--maps", type=int, default=64)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--variants", default="whole,step8m,step32m",
+                    help="comma list of whole, step8m, step32m, prog2, prog4, prog8, prog16")
     args = ap.parse_args()
     from uda_amd import native
     from uda_amd.bridge import UdaConsumer, UdaProvider
@@ -97,9 +100,12 @@ def main() -> int:
         total += len(data) - 2
         prov.add_mof_memory("job_tr", f"attempt_tr_m_{m:06d}_0", data, index)
     del runs
-    variants = [("warmup", {})] + [(f"{name}_{i}", conf) for i in range(args.repeat) for name, conf in (
-        ("whole", {}), ("step8m", {"mapred.uda.gpu.early.h2d.step": 8 << 20}),
-        ("step32m", {"mapred.uda.gpu.early.h2d.step": 32 << 20}))]
+    named = {"whole": {}, "step8m": {"mapred.uda.gpu.early.h2d.step": 8 << 20},
+             "step32m": {"mapred.uda.gpu.early.h2d.step": 32 << 20}}
+    for ph in (2, 4, 8, 16):
+        named[f"prog{ph}"] = {"mapred.uda.gpu.progressive.phases": ph}
+    variants = [("warmup", {})] + [(f"{name}_{i}", named[name]) for i in range(args.repeat)
+                                   for name in args.variants.split(",")]
     for i, (name, extra) in enumerate(variants):
         if os.path.exists(TRACE):
             os.unlink(TRACE)
@@ -113,7 +119,9 @@ def main() -> int:
         st = c.close()
         assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
         res = {"variant": name, "gbps": round(total / wall / 1e9, 2), "wall_ms": round(wall * 1e3, 1),
-               "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")}}
+               "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")},
+               "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
+               "progressive_rounds": st.get("rpq_rounds")}
         if name != "warmup" and os.path.exists(TRACE):
             res.update(summarize(load(TRACE)))
         print(json.dumps(res), flush=True)
