@@ -1597,6 +1597,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   // ---- compressed map outputs: F6 block decode straight from the partitions (descriptors or fetched
   // bytes) into the workspace; the framing is walked on the device
   if (codec_ != Codec::kNone) {
+    const auto td = std::chrono::steady_clock::now();
     std::vector<const uint8_t*> cp;
     std::vector<int64_t> cl;
     for (const auto& p : parts) {
@@ -1635,8 +1636,10 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       parts[i]->dptr = ws.in.as<uint8_t>() + roff[i];
       parts[i]->part_len = roff[i + 1] - roff[i];
     }
+    HIP_CHECK(hipStreamSynchronize(s));  // (the merge below syncs it anyway): decode time on its own
     std::lock_guard<std::mutex> g(st_mu_);
     st_.device_decoded_blocks += blocks;
+    st_.gpu_decode_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
   }
   // ---- TeraSort-shaped input: FIXED10 rounds straight over the partitions
   bool fixed = kind_ == KeyKind::kText;

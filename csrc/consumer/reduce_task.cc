@@ -810,7 +810,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
-    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
     << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"merge_path\":\"" << s.merge_path << "\""

@@ -51,6 +51,7 @@ struct ReduceStats {
   // GPU backend phase split: H2D staging, device decode+merge, waits on D2H pieces, host consumers
   // (dataFromUda / spill writes) of the pinned pieces
   double gpu_h2d_ms = 0, gpu_device_ms = 0, gpu_d2h_wait_ms = 0, gpu_sink_ms = 0;
+  double gpu_decode_ms = 0;  // device fetch, compressed partitions: framing walk + F6 decode (stream synced)
   double gpu_gate_wait_ms = 0;  // waiting for a GPU merge slot (mapred.uda.gpu.max.concurrent.merges)
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
   int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;

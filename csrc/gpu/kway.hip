@@ -370,6 +370,9 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
       }
       int ia = ml, ib = d - ml;
       const int todo = min(kKwItems, n - o0);
+      // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
+      // to the cell so a run's end never reads past the buffer
+      Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
 #pragma unroll
       for (int k = 0; k < kKwItems; ++k) {
         if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
@@ -383,18 +386,25 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
           lb = b1 - a1;
           ia = 0;
           ib = 0;
+          va = src[min(a0, n - 1)];
+          vb = src[min(a1, n - 1)];
         }
-        const bool take_a = ib >= lb || (ia < la && kle(src[a0 + ia], src[a1 + ib]));
-        const Elem v = take_a ? src[a0 + ia] : src[a1 + ib];
+        const bool take_a = ib >= lb || (ia < la && kle(va, vb));
+        Elem v;  // field-wise select: a select of the two structs becomes a scratch slot + indexed load
+        v.hi = take_a ? va.hi : vb.hi;
+        v.lo = take_a ? va.lo : vb.lo;
         if (INPLACE) {
           held_hi[k] = v.hi;
           held_lo[k] = v.lo;
         } else
           dst[o] = v;
-        if (take_a)
+        if (take_a) {
           ++ia;
-        else
+          va = src[min(a0 + ia, n - 1)];
+        } else {
           ++ib;
+          vb = src[min(a1 + ib, n - 1)];
+        }
       }
     }
     __syncthreads();
