@@ -383,7 +383,10 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   int kmax = 1;
   for (int g = 0; g < G; ++g) kmax = std::max(kmax, group_first[g + 1] - group_first[g]);
   const int64_t cap = kw_cap_;
-  int64_t T = cap / 2;  // target records per cell
+  // target records per cell: cap * fill %; the rest of the capacity is the sampling slack (K * step)
+  const char* fe = std::getenv("UDA_KWAY_FILL");  // read per plan: tests flip it within one process
+  const int fill = fe ? std::min(90, std::max(10, std::atoi(fe))) : 50;
+  int64_t T = cap * fill / 100;
   if (const char* e = std::getenv("UDA_KWAY_TARGET")) T = std::max<int64_t>(1, std::atoll(e));  // tests: force the PQ path
   const int64_t step = std::max<int64_t>(1, (cap - std::min<int64_t>(T, cap)) / (kmax + 2));  // cell <= T + K*step
   std::vector<int64_t> soff(K + 1, 0), nrec(K);
@@ -506,6 +509,8 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   kd.nt_stores = nt;
   const char* ip = std::getenv("UDA_KWAY_INPLACE");  // read per plan: tests flip it within one process
   kd.inplace = ip ? std::atoi(ip) : 0;
+  const char* sp = std::getenv("UDA_KWAY_SPREAD");
+  kd.spread = sp ? std::atoi(sp) : 0;
   kp.ncells = cell_first[G];
   kp.total = total_records(runs);
   return kp;

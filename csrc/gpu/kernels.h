@@ -156,6 +156,7 @@ struct KwayDesc {
   int xcd_swizzle = 0;        // map consecutive cells to one XCD (workgroups are dealt round-robin over 8 XCDs)
   int nt_stores = 0;          // F4 output with non-temporal stores (UDA_KWAY_NT=1)
   int inplace = 0;            // one LDS buffer, merge levels written back in place (UDA_KWAY_INPLACE)
+  int spread = 0;             // F3 outputs per thread = ceil(n / threads) instead of ITEMS (UDA_KWAY_SPREAD)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

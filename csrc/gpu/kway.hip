@@ -342,7 +342,10 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   // ---- F3: pairwise merge levels inside LDS
   Elem* src = bufA;
   Elem* dst = bufB;
-  const int o0 = threadIdx.x * kKwItems;
+  // outputs per thread: the full ITEMS, or (spread) n spread evenly over the workgroup, so a cell
+  // filled to half its capacity keeps every thread busy with half as long a merge chain
+  const int ipt = kd.spread ? (n + kKwThreads - 1) / kKwThreads : kKwItems;
+  const int o0 = threadIdx.x * ipt;
   uint64_t held_hi[kKwItems], held_lo[kKwItems];  // INPLACE: this thread's outputs of the current level
   for (int w = 1; w < K; w <<= 1) {
     if (o0 < n) {
@@ -369,7 +372,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
           mh = mid;
       }
       int ia = ml, ib = d - ml;
-      const int todo = min(kKwItems, n - o0);
+      const int todo = min(ipt, n - o0);
       // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
       // to the cell so a run's end never reads past the buffer
       Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
@@ -410,7 +413,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
     __syncthreads();
     if (INPLACE) {  // every thread has read the level: overwrite it with the merged order
       if (o0 < n) {
-        const int todo = min(kKwItems, n - o0);
+        const int todo = min(ipt, n - o0);
 #pragma unroll
         for (int k = 0; k < kKwItems; ++k)
           if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
