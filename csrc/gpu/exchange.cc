@@ -229,6 +229,7 @@ struct Group {
   int arrived = 0;
   uint64_t generation = 0;
   bool aborted = false;
+  bool failed = false;  // a rank's exchange failed after the entry barrier (see LocalExchange::exchange)
   std::vector<const std::vector<std::vector<Span>>*> sends;  // per rank, valid between barriers
   std::vector<const int64_t*> counts;
   // per rank: event recorded after its receive copies of exchange seq (parity seq & 1), and the
@@ -314,6 +315,11 @@ class LocalExchange : public Exchange {
     g.sends[rank_] = &send;
     HIP_CHECK(hipEventRecord(g.ready_ev[rank_], s));
     g.barrier();
+    // Between the two barriers the peers read this rank's send list and enqueue copies from its
+    // memory, so a rank that fails here must not return (and free either) before they are done: it
+    // marks the group failed and still meets the exit barrier; then every rank drains its copies,
+    // meets once more and throws.
+    std::string err;
     try {
       for (int k = 1; k < world_; ++k) {
         const int from = (rank_ - k + world_) % world_;
@@ -336,11 +342,26 @@ class LocalExchange : public Exchange {
         g.done_seq[rank_] = seq + 1;
       }
       g.cv.notify_all();
-    } catch (...) {
-      g.abort();
-      throw;
+    } catch (const std::exception& e) {
+      err = e.what();
+      std::lock_guard<std::mutex> gl(g.mu);
+      g.failed = true;
     }
     g.barrier();  // peers' send lists are no longer read
+    bool failed;
+    {
+      std::lock_guard<std::mutex> gl(g.mu);
+      failed = g.failed;
+    }
+    if (failed) {
+      (void)hipStreamSynchronize(s);  // copies reading the peers' memory have landed
+      try {
+        g.barrier();
+      } catch (const std::exception&) {  // a peer passed it first and marked the group aborted
+      }
+      g.abort();  // the group is unusable from here on
+      throw std::runtime_error(err.empty() ? "local exchange group aborted by another rank" : err);
+    }
   }
 
   // The peers read this rank's send slices on their own streams: wait for their copies' events.
