@@ -385,7 +385,7 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   const int64_t cap = kw_cap_;
   // target records per cell: cap * fill %; the rest of the capacity is the sampling slack (K * step)
   const char* fe = std::getenv("UDA_KWAY_FILL");  // read per plan: tests flip it within one process
-  const int fill = fe ? std::min(90, std::max(10, std::atoi(fe))) : 50;
+  const int fill = fe ? std::min(90, std::max(10, std::atoi(fe))) : 65;  // profiles/r3_kway_occupancy.md
   int64_t T = cap * fill / 100;
   if (const char* e = std::getenv("UDA_KWAY_TARGET")) T = std::max<int64_t>(1, std::atoll(e));  // tests: force the PQ path
   const int64_t step = std::max<int64_t>(1, (cap - std::min<int64_t>(T, cap)) / (kmax + 2));  // cell <= T + K*step
@@ -508,9 +508,11 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   }();
   kd.nt_stores = nt;
   const char* ip = std::getenv("UDA_KWAY_INPLACE");  // read per plan: tests flip it within one process
-  kd.inplace = ip ? std::atoi(ip) : 0;
+  // defaults from the device-only sweep (profiles/r3_kway_occupancy.md): one LDS buffer (more
+  // workgroups per CU) and the F3 outputs spread over all threads, +18.5 % over two buffers
+  kd.inplace = ip ? std::atoi(ip) : 1;
   const char* sp = std::getenv("UDA_KWAY_SPREAD");
-  kd.spread = sp ? std::atoi(sp) : 0;
+  kd.spread = sp ? std::atoi(sp) : 1;
   kp.ncells = cell_first[G];
   kp.total = total_records(runs);
   return kp;

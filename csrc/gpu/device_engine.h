@@ -198,7 +198,7 @@ class DeviceMerger {
   DeviceBuffer flag_;
   // single-pass K-way merge (kway.hip): samples (ping-pong), splitters, cell split table, overflow
   bool kway_ = true;
-  int kw_cap_ = 1536;  // records per k-way cell (UDA_KWAY_CAP): 3 workgroups per CU fit LDS
+  int kw_cap_ = 2048;  // records per k-way cell (UDA_KWAY_CAP); in-place LDS merge: 4 workgroups per CU
   int kw_threads_ = 256;  // k-way workgroup size (UDA_KWAY_THREADS)
   DeviceBuffer kw_prof_, kw_overflow_;
   struct PlanBufs {  // per plan slot: samples, splitters, cell splits, sample-merge scratch

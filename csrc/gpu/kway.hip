@@ -10,10 +10,12 @@
 //    each run gives the cell slices. With s = (cap - T) / (K + 2) a cell holds at most
 //    T + K*s <= cap records (T = target), so it always fits LDS; output offsets are the sums of the
 //    lower bounds, no scan needed.
-//  * One workgroup per cell (256 threads; cap = 1536 records by default, 512..2048 selectable):
-//    the slices' keys are loaded once from the records into LDS as 16-byte elements (F2), the K
-//    sorted slices are merged pairwise inside LDS (log2 K levels, merge path per thread, ping-pong
-//    between two cap x 16-byte buffers: no HBM traffic between levels), and the records are
+//  * One workgroup per cell (256 threads; cap = 2048 records by default, 512..2048 selectable,
+//    cells planned to 65 % of it): the slices' keys are loaded once from the records into LDS as
+//    16-byte elements (F2), the K sorted slices are merged pairwise inside LDS (log2 K levels, merge
+//    path per thread over ceil(n / 256) outputs; by default every level is written back in place
+//    into one cap x 16-byte buffer, two barriers per level, so 4 workgroups fit a CU; no HBM
+//    traffic between levels), and the records are
 //    gathered straight to the output (F4): one wave per 64 output records, 13 consecutive 8-byte
 //    words per record, 512-byte coalesced stores. HBM traffic per record: its key line, then one
 //    record read and one record write.
@@ -21,8 +23,9 @@
 //    so every phase keeps its loads in flight together: F2 issues all of a thread's key loads
 //    before the first LDS write, F4 all 13 word loads of a lane before its first store (with no
 //    per-lane guards on full waves, which would split the stores into blocks that each drain
-//    vmcnt). 1536-record cells fit 3 workgroups per CU (51 KiB LDS each, 91 VGPRs); per-phase
-//    timings come from UDA_KWAY_PROF (profiles/r2_kway_tuning.md).
+//    vmcnt). Round 2 ran 1536-record cells in two buffers (3 workgroups per CU, 51 KiB LDS each,
+//    92 VGPRs); round 3's in-place levels and bigger, fuller cells are +18.5 % (device-only sweep,
+//    profiles/r3_kway_occupancy.md). Per-phase timings come from UDA_KWAY_PROF.
 //  * A cell that would not fit LDS (only possible with massively duplicated keys) is merged by a
 //    wave-level priority queue: lanes own runs, a wave argmin picks the next record each step.
 #include "kernels.h"

@@ -58,6 +58,7 @@ def summarize(ev):
         out["serve_copy"]["threads"] = len({e[1] for e in sc})
         # bytes landed per 5 ms bin, and mean memcpys in flight per bin
         end = max(e[5] for e in sc)
+        t_start = min(t_start, min(e[4] for e in sc))  # copies may start before the task bracket opens
         nb = int((end - t_start) / 5e6) + 1
         landed = [0.0] * nb
         busy = [0.0] * nb
