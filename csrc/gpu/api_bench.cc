@@ -8,6 +8,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -116,6 +117,19 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
   if (c.provider_hbm_bytes > 0) {
     t.kv["mapred.uda.provider.hbm.bytes"] = std::to_string(c.provider_hbm_bytes);
     t.kv["mapred.uda.provider.hbm.devices"] = std::to_string(c.device);
+  }
+  // A/B runs: UDA_API_CONF="key=value,key=value" adds or overrides job configuration keys
+  if (const char* extra = std::getenv("UDA_API_CONF")) {
+    std::string all(extra);
+    size_t b = 0;
+    while (b < all.size()) {
+      size_t e = all.find(',', b);
+      if (e == std::string::npos) e = all.size();
+      const std::string kv = all.substr(b, e - b);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos && eq > 0) t.kv[kv.substr(0, eq)] = kv.substr(eq + 1);
+      b = e + 1;
+    }
   }
   return t;
 }

@@ -172,7 +172,10 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int 
 __device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0, const Elem* cur, int base, int valid,
                                             uint8_t* dst, bool nt) {
   constexpr int kWords = kTeraRecordBytes / 8;
-  const int lane = threadIdx.x & 63;
+  // opaque per call: otherwise the per-word lane constants (record index, word offset) of all 13
+  // words are hoisted out of the caller's loop and held in ~39 VGPRs, which caps the SIMD at 5 waves
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
   unsigned long long src = 0;
   if (lane < valid) {
     const Elem e = cur[base + lane];
