@@ -207,7 +207,7 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   if (const char* e = std::getenv("UDA_KWAY")) kway_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("UDA_KWAY_CAP")) kw_cap_ = std::atoi(e);
   if (const char* e = std::getenv("UDA_KWAY_THREADS")) kw_threads_ = std::atoi(e) == 512 ? 512 : 256;
-  if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536 or 2048");
+  if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536, 1792 or 2048");
   kw_overflow_.alloc(sizeof(int));
   HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
   slots_.resize(4);
@@ -497,6 +497,7 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   kd.bad_layout = flag_.as<int>();
   kd.cap = (int)cap;
   kd.threads = kw_threads_;
+  kd.kmax = kmax;
   static const int xcd = [] {
     const char* e = std::getenv("UDA_KWAY_XCD");  // default on: +0.5 % device-only (profiles/r2_kway_xcd_ab.md)
     return e ? std::atoi(e) : 1;

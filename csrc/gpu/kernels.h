@@ -139,7 +139,7 @@ void launch_gk_round_bounds(const int64_t* split, int K, int64_t C, const int64_
 
 // ---------------------------------------------------------------- single-pass K-way merge (F2+F3+F4)
 constexpr int kKwCap = 2048;       // records per cell (LDS capacity of one workgroup)
-constexpr int kKwMaxRuns = 128;    // runs per group on the single-pass path
+constexpr int kKwMaxRuns = 256;    // runs per group on the single-pass path (8 GPUs x 32 maps)
 struct KwayDesc {
   const RunDesc* runs;        // every run of the round, grouped by reducer
   const int* group_first;     // G+1
@@ -157,6 +157,7 @@ struct KwayDesc {
   int nt_stores = 0;          // F4 output with non-temporal stores (UDA_KWAY_NT=1)
   int inplace = 0;            // one LDS buffer, merge levels written back in place (UDA_KWAY_INPLACE)
   int spread = 0;             // F3 outputs per thread = ceil(n / threads) instead of ITEMS (UDA_KWAY_SPREAD)
+  int kmax = kKwMaxRuns;      // most runs in one group of this plan (sizes the per-slice LDS tables)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

@@ -132,9 +132,10 @@ __global__ void __launch_bounds__(256) split_sampled_kernel(uint8_t* const* base
   out[t] = a;
 }
 
-// Exclusive scan of the K slice lengths into seg[0..K] and the sum of the slice starts (wave 0).
-__device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int ncell, int r0, int K, int* seg,
-                                          int64_t* beg, int64_t* start_sum) {
+// Wave 0: exclusive scan of the K slice lengths into seg[0..K], each slice's first record into
+// sbase[k], and the sum of the slice starts (the cell's first output record within its group).
+__device__ __forceinline__ void kw_slices(const KwayDesc& kd, int c, int ncell, int r0, int K, int* seg,
+                                          const uint8_t** sbase, int64_t* start_sum) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   const int per = kd.nbmax + 2;
@@ -148,7 +149,7 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int 
       const int r = r0 + k;
       const int64_t b = c == 0 ? 0 : kd.split[(int64_t)r * per + c];
       const int64_t e = (c + 1 == ncell) ? kd.runs[r].nrec : kd.split[(int64_t)r * per + c + 1];
-      beg[k] = b;
+      sbase[k] = kd.runs[r].base + b * kTeraRecordBytes;
       len = (int)(e - b);
       bsum += (unsigned long long)b;
     }
@@ -169,7 +170,7 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int g, int c, int 
 // 13 x 8-byte words per record, one wave per 64 consecutive output records. All 13 loads of a
 // lane are issued before its first store: written as load -> store pairs, the compiler must assume
 // the store may alias the next load and serializes 13 HBM round trips per 64 records.
-__device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0, const Elem* cur, int base, int valid,
+__device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const Elem* cur, int base, int valid,
                                             uint8_t* dst, bool nt) {
   constexpr int kWords = kTeraRecordBytes / 8;
   // opaque per call: otherwise the per-word lane constants (record index, word offset) of all 13
@@ -180,7 +181,7 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* rbase, int r0,
   if (lane < valid) {
     const Elem e = cur[base + lane];
     const int run = (int)((e.lo >> 32) & 0xFFFF);
-    src = (unsigned long long)(rbase[run - r0] + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes);
+    src = (unsigned long long)(sbase[run] + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes);
   }
   uint64_t* d = reinterpret_cast<uint64_t*>(dst);
   uint64_t v[kWords];
@@ -230,9 +231,10 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
   Elem* bufA = kw_dyn;
   Elem* bufB = INPLACE ? kw_dyn : kw_dyn + kCap;
-  __shared__ int seg[kKwMaxRuns + 1];
-  __shared__ int64_t beg[kKwMaxRuns];
-  __shared__ const uint8_t* rbase[kKwMaxRuns];
+  // per-slice tables behind the element buffer(s), sized by the plan's largest group (kd.kmax): a
+  // 32-run round needs 388 bytes here, not the 2.5 KiB a static kKwMaxRuns table would pin
+  const uint8_t** sbase = reinterpret_cast<const uint8_t**>(kw_dyn + (INPLACE ? 1 : 2) * kCap);  // slice starts
+  int* seg = reinterpret_cast<int*>(sbase + kd.kmax);  // [K + 1] slice offsets within the cell
   __shared__ int64_t s_start;
   // The dispatcher deals workgroups round-robin over the 8 XCDs (each with its own L2); with the
   // swizzle, XCD x takes a contiguous block of cells, so neighbouring cells of a group (adjacent
@@ -259,28 +261,34 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   const int c = (int)(b - kd.cell_first[g]);
   const int ncell = (int)(kd.cell_first[g + 1] - kd.cell_first[g]);
   const int r0 = kd.group_first[g], K = kd.group_first[g + 1] - r0;
-  kw_slices(kd, g, c, ncell, r0, K, seg, beg, &s_start);
-  for (int k = threadIdx.x; k < K; k += kKwThreads) rbase[k] = kd.runs[r0 + k].base;
+  kw_slices(kd, c, ncell, r0, K, seg, sbase, &s_start);
   __syncthreads();
   stamp(1);
   const int n = seg[K];
   uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
   if (n > kCap) {  // uniform across the block
     if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
-    // wave-level priority queue: lanes own runs; each step a wave argmin picks the next record
+    // wave-level priority queue: lane l owns slices l, l + 64, ... (K <= 256: four per lane, their
+    // remaining counts and taken counts in registers); each step a wave argmin picks the next record
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
     constexpr int kWords = kTeraRecordBytes / 8;
-    // positions: beg[k] advances in place; ends from the slice table
+    constexpr int kPer = kKwMaxRuns / 64;
+    int left[kPer], taken[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = lane + 64 * j;
+      left[j] = k < K ? seg[k + 1] - seg[k] : 0;
+      taken[j] = 0;
+    }
     for (int64_t i = 0; i < n; ++i) {
       Elem best{~0ull, ~0ull};
       int bk = -1;
-      for (int k = lane; k < K; k += 64) {
-        const int64_t p = beg[k];
-        const int64_t end = (c + 1 == ncell) ? kd.runs[r0 + k].nrec
-                                              : kd.split[(int64_t)(r0 + k) * (kd.nbmax + 2) + c + 1];
-        if (p < end) {
-          const Elem e = load_key_elem(kd.runs[r0 + k].base + p * kTeraRecordBytes, r0 + k, p, kd.bad_layout);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int k = lane + 64 * j;
+        if (left[j] > 0) {
+          const Elem e = load_key_elem(sbase[k] + (int64_t)taken[j] * kTeraRecordBytes, k, taken[j], kd.bad_layout);
           if (bk < 0 || kle(e, best)) {
             best = e;
             bk = k;
@@ -298,12 +306,18 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
           bk = ok;
         }
       }
-      const int run = (int)((best.lo >> 32) & 0xFFFF);
       const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(kd.runs[run].base + pos * kTeraRecordBytes);
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(sbase[bk] + pos * kTeraRecordBytes);
       uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
       if (lane < kWords) dst[lane] = src[lane];
-      if (lane == 0) beg[bk] = pos + 1;
+      if (lane == (bk & 63)) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if ((bk >> 6) == j) {
+            ++taken[j];
+            --left[j];
+          }
+      }
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
     }
@@ -312,8 +326,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   // ---- F2: keys of every slice into LDS (all of a thread's key loads in flight at once)
   if (n > 0) {
     uint64_t w0[kKwItems], w1[kKwItems];
-    int slv[kKwItems];
-    int64_t posv[kKwItems];
+    int slv[kKwItems], posv[kKwItems];  // slice, record within the slice
 #pragma unroll
     for (int k = 0; k < kKwItems; ++k) {
       // items past n re-read item n - 1: unguarded loads stay in one block and all stay in flight
@@ -327,11 +340,11 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
           sh = mid;
       }
       slv[k] = sl;
-      posv[k] = beg[sl] + (i - seg[sl]);
+      posv[k] = i - seg[sl];
     }
 #pragma unroll
     for (int k = 0; k < kKwItems; ++k) {
-      const GlobalU64* rec = gptr(rbase[slv[k]] + posv[k] * kTeraRecordBytes);
+      const GlobalU64* rec = gptr(sbase[slv[k]] + (int64_t)posv[k] * kTeraRecordBytes);
       w0[k] = rec[0];
       w1[k] = rec[1];
     }
@@ -339,7 +352,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
 #pragma unroll
     for (int k = 0; k < kKwItems; ++k) {
       const int i = threadIdx.x + k * kKwThreads;
-      if (i < n) bufA[i] = key_elem(w0[k], w1[k], r0 + slv[k], posv[k], bad);
+      if (i < n) bufA[i] = key_elem(w0[k], w1[k], slv[k], posv[k], bad);  // ties: (slice, position) order
     }
     if (bad) *kd.bad_layout = 1;
   }
@@ -436,7 +449,7 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   const int wave = threadIdx.x >> 6;
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
-    kw_gather64(rbase, r0, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
+    kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
   }
   if (kd.prof) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -462,16 +475,19 @@ void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem
                      samples, soff, every, bounds, run_bound_set, nruns, nb, out);
 }
 
-int kway_cap_supported(int cap) { return cap == 2048 || cap == 1536 || cap == 1024 || cap == 512; }
+int kway_cap_supported(int cap) { return cap == 2048 || cap == 1792 || cap == 1536 || cap == 1024 || cap == 512; }
 
 namespace {
 template <int ITEMS, int THREADS, bool INPLACE>
 void launch_kway_v(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
-  const size_t lds = (INPLACE ? 1 : 2) * sizeof(Elem) * (size_t)(ITEMS * THREADS);
+  const size_t elems = (INPLACE ? 1 : 2) * sizeof(Elem) * (size_t)(ITEMS * THREADS);
+  auto tables = [](int k) { return (size_t)k * sizeof(void*) + (size_t)(k + 1) * sizeof(int); };
+  if (kd.kmax < 1 || kd.kmax > kKwMaxRuns) throw std::runtime_error("kway: bad runs per group " + std::to_string(kd.kmax));
+  const size_t lds = (elems + tables(kd.kmax) + 15) & ~(size_t)15;
   static std::once_flag once;
-  std::call_once(once, [lds] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
+  std::call_once(once, [elems, tables] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, THREADS, INPLACE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(elems + tables(kKwMaxRuns) + 16));
   });
   hipLaunchKernelGGL((kway_tile_kernel<ITEMS, THREADS, INPLACE>), dim3((unsigned)ncells), dim3(THREADS), lds, s, kd,
                      out);
@@ -491,6 +507,10 @@ void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStre
   const bool wide = kd.threads == 512;
   switch (kd.cap) {
     case 2048: wide ? launch_kway<4, 512>(kd, ncells, out, s) : launch_kway<8, 256>(kd, ncells, out, s); break;
+    case 1792:  // 256 threads only: 28.4 KiB in place, 5 workgroups per CU
+      if (wide) throw std::runtime_error("kway: cell capacity 1792 needs 256-thread workgroups");
+      launch_kway<7, 256>(kd, ncells, out, s);
+      break;
     case 1536: wide ? launch_kway<3, 512>(kd, ncells, out, s) : launch_kway<6, 256>(kd, ncells, out, s); break;
     case 1024: wide ? launch_kway<2, 512>(kd, ncells, out, s) : launch_kway<4, 256>(kd, ncells, out, s); break;
     case 512: wide ? launch_kway<1, 512>(kd, ncells, out, s) : launch_kway<2, 256>(kd, ncells, out, s); break;

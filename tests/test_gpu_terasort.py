@@ -240,6 +240,28 @@ def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
         assert st2["merge_passes"] == 3  # ceil(log2(6)) pairwise passes
 
 
+@pytest.mark.parametrize("env", [{}, {"UDA_KWAY_TARGET": "100000"}, {"UDA_KWAY_CAP": "1792"}])
+def test_kway_many_runs_per_group(require_gpu, monkeypatch, env):
+    """200 runs per group (an 8-GPU round has 8 x 32 = 256): the single-pass merge sizes its per-slice
+    LDS tables by the plan's largest group and must order records like the pairwise tree, on the LDS
+    path, on the wave-PQ path (UDA_KWAY_TARGET above the capacity) and at the 1792-record capacity."""
+    ref_env = {"UDA_KWAY": "0"}
+    out = []
+    for e in (ref_env, env):
+        for k in ("UDA_KWAY", "UDA_KWAY_TARGET", "UDA_KWAY_CAP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in e.items():
+            monkeypatch.setenv(k, v)
+        j = _job(200 * 300, 200, 2, reducers=2, **SMALL)
+        readers = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
+        j.use_python_sink(lambda r, b, rd=readers: rd[r].feed(b), with_reducer=True)
+        st = j.step()
+        j.check(st)
+        out.append([r.records for r in readers])
+        assert st["merge_passes"] == (8 if e is ref_env else 1)
+    assert out[0] == out[1]
+
+
 @pytest.mark.parametrize("world,store", [(1, "hbm"), (1, "host"), (2, "hbm")])
 def test_replan_every_step(require_gpu, world, store):
     """replan=True: each step recomputes the cell splits from the map outputs (and, for world>1,
