@@ -498,6 +498,8 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   kd.cap = (int)cap;
   kd.threads = kw_threads_;
   kd.kmax = kmax;
+  const char* f4 = std::getenv("UDA_KWAY_F4");
+  kd.f4_lane = f4 && std::string(f4) == "lane";
   static const int xcd = [] {
     const char* e = std::getenv("UDA_KWAY_XCD");  // default on: +0.5 % device-only (profiles/r2_kway_xcd_ab.md)
     return e ? std::atoi(e) : 1;

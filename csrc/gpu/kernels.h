@@ -158,6 +158,7 @@ struct KwayDesc {
   int inplace = 0;            // one LDS buffer, merge levels written back in place (UDA_KWAY_INPLACE)
   int spread = 0;             // F3 outputs per thread = ceil(n / threads) instead of ITEMS (UDA_KWAY_SPREAD)
   int kmax = kKwMaxRuns;      // most runs in one group of this plan (sizes the per-slice LDS tables)
+  int f4_lane = 0;            // F4 copies one whole record per lane (UDA_KWAY_F4=lane)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

@@ -216,6 +216,30 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const E
   }
 }
 
+// F4 alternative (UDA_KWAY_F4=lane): lane l copies output record base + l whole, as six 16-byte
+// pieces and one 8-byte piece with immediate offsets from one address (no per-word cross-lane
+// address shuffles, no per-word index arithmetic); stores are 16 bytes at a 104-byte stride.
+__device__ __forceinline__ void kw_copy_lane(const uint8_t* const* sbase, const Elem* cur, int base, int valid,
+                                             uint8_t* dst) {
+  typedef unsigned int U4 __attribute__((ext_vector_type(4), aligned(4)));
+  typedef unsigned int U2 __attribute__((ext_vector_type(2), aligned(4)));
+  typedef __attribute__((address_space(1))) const U4 GU4;
+  typedef __attribute__((address_space(1))) const U2 GU2;
+  const int lane = threadIdx.x & 63;
+  if (lane >= valid) return;
+  const Elem e = cur[base + lane];
+  const uint8_t* src = sbase[(int)((e.lo >> 32) & 0xFFFF)] + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes;
+  GU4* s4 = (GU4*)(uintptr_t)src;
+  U4 v[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) v[j] = s4[j];
+  const U2 t = *(GU2*)(uintptr_t)(src + 96);
+  uint8_t* d = dst + (int64_t)lane * kTeraRecordBytes;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) reinterpret_cast<U4*>(d)[j] = v[j];
+  *reinterpret_cast<U2*>(d + 96) = t;
+}
+
 }  // namespace
 
 // ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffers are dynamic, so
@@ -449,7 +473,10 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   const int wave = threadIdx.x >> 6;
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
-    kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
+    if (kd.f4_lane)
+      kw_copy_lane(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+    else
+      kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
   }
   if (kd.prof) {
     __builtin_amdgcn_s_waitcnt(0);

@@ -216,7 +216,8 @@ def test_spill_tiers_multirank_staged(require_gpu, tmp_path, monkeypatch, world,
 @pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}, {"UDA_KWAY_INPLACE": "1"},
                                  {"UDA_KWAY_INPLACE": "0"}, {"UDA_KWAY_INPLACE": "1", "UDA_KWAY_CAP": "2048"},
                                  {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"},
-                                 {"UDA_KWAY_SPREAD": "1", "UDA_KWAY_INPLACE": "1"}, {"UDA_KWAY_SPREAD": "1"}])
+                                 {"UDA_KWAY_SPREAD": "1", "UDA_KWAY_INPLACE": "1"}, {"UDA_KWAY_SPREAD": "1"},
+                                 {"UDA_KWAY_F4": "lane"}, {"UDA_KWAY_F4": "lane", "UDA_KWAY_THREADS": "512"}])
 def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
     """The single-pass K-way merge (default) and the pairwise merge-path tree (UDA_KWAY=0) order
     records identically; UDA_KWAY_TARGET above the LDS capacity routes every cell through the
