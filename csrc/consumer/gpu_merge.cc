@@ -386,9 +386,11 @@ struct PoolLease {
 // the tasks ahead of it, so both PCIe directions stay busy. Tasks wait in FIFO order of arrival.
 class DeviceGate {
  public:
-  static DeviceGate& get() {
-    static DeviceGate* g = new DeviceGate;  // never destroyed: reduce tasks may outlive static teardown
-    return *g;
+  // gate 0: staged GPU merges (mapred.uda.gpu.max.concurrent.merges); gate 1: device block decodes
+  // of compressed descriptor tasks (mapred.uda.gpu.decode.slots)
+  static DeviceGate& get(int which = 0) {
+    static DeviceGate* g[2] = {new DeviceGate, new DeviceGate};  // never destroyed: tasks may outlive static teardown
+    return *g[which & 1];
   }
   // false if `stopped` became true while waiting
   template <class Stop>
@@ -431,8 +433,9 @@ class DeviceGate {
 
 struct GateLease {
   int device = -1;
+  int which = 0;
   ~GateLease() {
-    if (device >= 0) DeviceGate::get().release(device);
+    if (device >= 0) DeviceGate::get(which).release(device);
   }
 };
 
@@ -1598,6 +1601,17 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   // bytes) into the workspace; the framing is walked on the device
   if (codec_ != Codec::kNone) {
     const auto td = std::chrono::steady_clock::now();
+    // Decodes of concurrent tasks take turns (FIFO, mapred.uda.gpu.decode.slots at once, default 1;
+    // 0 = no limit): a decode fills the device by itself, so running them in turn costs no decode
+    // throughput, and the first tasks reach their merge and D2H delivery while later ones still
+    // decode. All at once, every task finished decoding together and PCIe idled until then.
+    GateLease dgate;
+    dgate.which = 1;
+    if (const int slots = (int)host_->conf_i64("mapred.uda.gpu.decode.slots", 1); slots > 0) {
+      if (!DeviceGate::get(1).acquire(device, slots, [&] { return stop_.load(); }))
+        throw UdaError("reduce task stopped while waiting for a device decode slot");
+      dgate.device = device;
+    }
     std::vector<const uint8_t*> cp;
     std::vector<int64_t> cl;
     for (const auto& p : parts) {
