@@ -244,7 +244,9 @@ def netmerger(args) -> dict:
         # process that exceeds it inside a 100 ms period is stalled until the next one
         out[name + "_cpu_s"] = round(r1.ru_utime + r1.ru_stime - r0.ru_utime - r0.ru_stime, 3)
         st = c.close()
-        assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
+        print(f"# {name}: {wall * 1e3:.1f} ms, delivered {st['bytes_delivered'] - 2} of {total} "
+              f"path={st.get('merge_path')}", file=sys.stderr, flush=True)
+        assert st["bytes_delivered"] - 2 == total, (name, st)
         out[name + "_gbps"] = round(total / wall / 1e9, 3)
         out[name + "_merge_ms"] = round(st["merge_ms"], 1)
         out[name + "_fetch_ms"] = round(st["fetch_ms"], 1)

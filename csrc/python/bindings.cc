@@ -358,6 +358,26 @@ PYBIND11_MODULE(_uda_native, m) {
       .def_readonly("framing_errors", &StreamValidator::framing_errors)
       .def_readonly("checksum", &StreamValidator::checksum)
       .def_readonly("eof", &StreamValidator::eof);
+  // True iff the whole-record buffer's last record is the EOF marker (-1, -1): walks the VInt framing
+  // from the buffer's start (a dataFromUda buffer begins on a record boundary), so record bytes that
+  // happen to end in 0xFF 0xFF are not taken for the marker. -1 on broken framing.
+  m.def("buffer_ends_with_eof", [](py::buffer b) {
+    py::buffer_info bi = b.request();
+    const uint8_t* p = static_cast<const uint8_t*>(bi.ptr);
+    const int64_t n = (int64_t)(bi.size * bi.itemsize);
+    int64_t off = 0;
+    while (off < n) {
+      int64_t kl = 0, vl = 0;
+      const int a = vint_decode(p + off, (size_t)(n - off), &kl);
+      if (a <= 0) return -1;
+      const int c = vint_decode(p + off + a, (size_t)(n - off - a), &vl);
+      if (c <= 0) return -1;
+      if (kl == -1 && vl == -1) return off + a + c == n ? 1 : -1;
+      if (kl < 0 || vl < 0 || off + a + c + kl + vl > n) return -1;
+      off += a + c + kl + vl;
+    }
+    return 0;
+  });
   m.def("ifile_checksum", [](py::buffer b) {
     py::buffer_info bi = b.request();
     int64_t recs = 0, bytes = 0;

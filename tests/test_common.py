@@ -169,3 +169,19 @@ def test_ipc_export_size_rule(native):
     for size in (1 << 31, 3 << 30, (1 << 32) - 1, (6 << 30) + 1):
         assert not native.ipc_size_ok(size), size
         assert native.ipc_size_ok(native.ipc_safe_bytes(size))
+
+
+def test_buffer_ends_with_eof_walks_the_framing():
+    """The keep_records=False consumer finishes on the EOF marker, found by walking the VInt framing:
+    a record whose value ends in 0xFF 0xFF must not pass for the marker (it once ended a 2 GB task
+    early, 582 MB in)."""
+    from uda_amd import native
+    from uda_amd.utils.ifile import encode_record, encode_stream, text
+    n = native()
+    tricky = encode_record(text(b"k1"), b"abc\xff\xff") + encode_record(text(b"k2"), b"\x00\xff\xff")
+    assert tricky.endswith(b"\xff\xff")
+    assert n.buffer_ends_with_eof(tricky) == 0
+    assert n.buffer_ends_with_eof(tricky + b"\xff\xff") == 1
+    assert n.buffer_ends_with_eof(b"\xff\xff") == 1
+    assert n.buffer_ends_with_eof(encode_stream([(text(b"a"), b"\xff\xff")])) == 1
+    assert n.buffer_ends_with_eof(tricky[:-1]) == -1  # a cut record is broken framing

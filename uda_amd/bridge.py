@@ -143,7 +143,8 @@ class UdaConsumer:
             self.reader.feed(buf)
             if self.reader.eof:
                 self._done.set()
-        elif len(buf) >= 2 and bytes(buf[-2:]) == b"\xff\xff":
+        elif len(buf) >= 2 and bytes(buf[-2:]) == b"\xff\xff" and native().buffer_ends_with_eof(buf) == 1:
+            # (a record's own bytes may end in 0xFF 0xFF: only a walk of the framing tells the marker)
             self._done.set()
         return 0
 
