@@ -431,6 +431,17 @@ class DeviceGate {
   std::map<int, Dev> devs_;
 };
 
+// Staged GPU merges running per device (the progressive-phase default asks whether a task is alone).
+std::atomic<int>& staged_merges(int device) {
+  static std::atomic<int> n[64];
+  return n[device & 63];
+}
+struct StagedCount {
+  int device;
+  explicit StagedCount(int d) : device(d) { staged_merges(device).fetch_add(1); }
+  ~StagedCount() { staged_merges(device).fetch_sub(1); }
+};
+
 struct GateLease {
   int device = -1;
   int which = 0;
@@ -735,7 +746,13 @@ void ReduceTask::merge_gpu() {
   // last-landed key has fully arrived in every run (plan_progressive_split), so it is merged and its
   // output streamed back while phase p + 1 still comes in: the D2H of the output overlaps the H2D of
   // the input on the duplex link instead of following it.
-  const int prog_phases = (int)std::min<int64_t>(EarlyStager::kGroups, host_->conf_i64("mapred.uda.gpu.progressive.phases", 0));
+  // Default (-1): 4 phases when the task is the only staged GPU merge on its device when it decides
+  // (a lone task: 22 -> 26.3-26.8 GB/s on the 2 GB secondary sort); concurrent tasks already overlap
+  // each other's H2D and D2H and gain nothing (profiles/r3_api_host_mofs_progressive_ab.txt).
+  const int64_t prog_conf = host_->conf_i64("mapred.uda.gpu.progressive.phases", -1);
+  const int prog_phases = (int)std::min<int64_t>(EarlyStager::kGroups, prog_conf < 0 ? 4 : prog_conf);
+  const bool prog_auto = prog_conf < 0;
+  StagedCount staged_count(device);
   const bool prog_ok = prog_phases > 1 && stager && stager->sdma() && restored_files_.empty() && !ckpt;
   bool prog_decided = false, progressive = false;
   struct ProgFetch {
@@ -994,7 +1011,7 @@ void ReduceTask::merge_gpu() {
         prog_decided = true;
         int64_t tot = 0;
         for (auto& f : ready) tot += std::max<int64_t>(f->part_len(), 0);
-        progressive = drained == 0 && tot <= budget;
+        progressive = drained == 0 && tot <= budget && (!prog_auto || staged_merges(device).load() == 1);
         if (progressive) {
           prog = std::make_unique<ProgFetch>();
           ProgFetch& pf = *prog;

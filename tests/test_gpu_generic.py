@@ -148,7 +148,7 @@ def test_consumer_gpu_fetch_drains_and_piecewise_staging(require_gpu, drains, st
 
 
 @pytest.mark.parametrize("phases,drains,maps,kind", [(2, 3, 9, "text"), (3, 1, 9, "text"), (7, 3, 9, "text"),
-                                                     (4, 8, 20, "bytes"), (5, 3, 3, "text")])
+                                                     (4, 8, 20, "bytes"), (5, 3, 3, "text"), (None, 3, 9, "text")])
 def test_consumer_gpu_progressive_phases(require_gpu, phases, drains, maps, kind):
     """mapred.uda.gpu.progressive.phases: partitions fetched in byte phases (all partitions' phase p
     first), each phase's key range below the least last-landed key merged and delivered while later
@@ -158,7 +158,7 @@ def test_consumer_gpu_progressive_phases(require_gpu, phases, drains, maps, kind
     p = UdaProvider()
     try:
         if kind == "text":
-            mp = datagen.secondary_sort(num_maps=maps, reducers=2, rows_per_map=1500, seed=13 + phases)
+            mp = datagen.secondary_sort(num_maps=maps, reducers=2, rows_per_map=1500, seed=13 + (phases or 0))
             key_class = datagen.TEXT
         else:
             mp = datagen.bytes_writable(num_maps=maps, reducers=2, rows_per_map=900, seed=3)
@@ -169,8 +169,9 @@ def test_consumer_gpu_progressive_phases(require_gpu, phases, drains, maps, kind
             data, index = encode_partitions(parts)
             p.add_mof_memory("job_p", mid, data, index)
             ids.append(mid)
-        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": drains,
-                "mapred.uda.gpu.progressive.phases": phases}
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch.drains": drains}
+        if phases is not None:  # None: the default, progressive when the task is alone on its device
+            conf["mapred.uda.gpu.progressive.phases"] = phases
         recs_gpu, st, _ = run_reduce("h", "job_p", ids, 0, key_class, conf=conf, max_buf_kb=16, min_buf_kb=16,
                                      kv_buf_size=8192)
         recs_cpu, _, _ = run_reduce("h", "job_p", ids, 0, key_class, max_buf_kb=16, min_buf_kb=16, kv_buf_size=8192)
