@@ -800,8 +800,14 @@ void ReduceTask::merge_gpu() {
   // one group at a time, while the fetch fills the next group (the reference's fetcher running ahead
   // of the LPQ merges, MergeManager.cc:202-288).
   auto merge_spill = [&](std::vector<Span> jg, std::vector<std::string> ids, EarlyStager* st) {
+    const int64_t tl = trace::host_enabled() ? trace::now_ns() : 0;
     if (st) st->flush();
+    const int64_t tm = tl ? trace::now_ns() : 0;
     DeviceMergeOut m = device_merge(ws, jg, stage_codec, kind_, kSampleSpacing, s);
+    if (tl) {
+      trace::host_event("lpq_flush", (int64_t)jg.size(), 0, tl, tm);
+      trace::host_event("lpq_merge", m.bytes, (int64_t)jg.size(), tm, trace::now_ns());
+    }
     count_decoded(m.decoded_blocks);
     if (st) st->reset();  // the merge read the staged copies; recycle their HBM
     SpillRun run;
@@ -822,9 +828,11 @@ void ReduceTask::merge_gpu() {
     std::atomic<int64_t> err{0};
     if (!disk) {
       const auto td = std::chrono::steady_clock::now();
+      const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
       if (m.bytes > 0)
         HIP_CHECK(hipMemcpyAsync(run.mem, ws.out.as<uint8_t>(), (size_t)m.bytes, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
+      if (tt) trace::host_event("lpq_d2h", m.bytes, 0, tt, trace::now_ns());
       ws.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
       for (size_t j = 0; j + 1 < m.cuts.size(); ++j) {
         run.cut.push_back(m.cuts[j]);

@@ -47,7 +47,7 @@ def summarize(ev):
     t_start = task[4]
     fp = [e for e in ev if e[0] == "fetch_phase"][-1]
     out = {"task_ms": round((task[5] - task[4]) / 1e6, 1), "fetch_ms": round((fp[5] - fp[4]) / 1e6, 1)}
-    for kind in ("fetch_req", "serve_copy", "drain", "stage_wait"):
+    for kind in ("fetch_req", "serve_copy", "drain", "stage_wait", "lpq_flush", "lpq_merge", "lpq_d2h"):
         d = [(e[5] - e[4]) / 1e6 for e in ev if e[0] == kind]
         out[kind] = {"n": len(d), "p50_ms": pct(d, 0.5), "p90_ms": pct(d, 0.9), "max_ms": max(d) if d else None}
     sc = [e for e in ev if e[0] == "serve_copy"]
@@ -72,6 +72,11 @@ def summarize(ev):
                 t = nxt
         out["landed_mb_per_5ms"] = [round(x) for x in landed]
         out["memcpys_in_flight_per_5ms"] = [round(x, 1) for x in busy]
+    for kind in ("lpq_flush", "lpq_merge", "lpq_d2h"):  # hybrid: LPQ spans relative to the task start
+        sp = [e for e in ev if e[0] == kind]
+        if sp:
+            out[kind]["sum_ms"] = round(sum(e[5] - e[4] for e in sp) / 1e6, 1)
+            out[kind]["spans_ms"] = [(round((e[4] - t_start) / 1e6, 1), round((e[5] - t_start) / 1e6, 1)) for e in sp]
     sf = [e for e in ev if e[0] == "stage_flush"]
     if sf:
         out["stage_flush_ms"] = round((sf[-1][5] - sf[-1][4]) / 1e6, 1)
@@ -105,6 +110,8 @@ def main() -> int:
              "step32m": {"mapred.uda.gpu.early.h2d.step": 32 << 20}}
     for ph in (2, 4, 8, 16):
         named[f"prog{ph}"] = {"mapred.uda.gpu.progressive.phases": ph}
+    named["whole"] = {"mapred.uda.gpu.progressive.phases": 0}
+    named["hybrid"] = {"mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6), "mapred.uda.gpu.spill": "host"}
     variants = [("warmup", {})] + [(f"{name}_{i}", named[name]) for i in range(args.repeat)
                                    for name in args.variants.split(",")]
     for i, (name, extra) in enumerate(variants):
@@ -120,6 +127,7 @@ def main() -> int:
         st = c.close()
         assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
         res = {"variant": name, "gbps": round(total / wall / 1e9, 2), "wall_ms": round(wall * 1e3, 1),
+               "lpqs": st.get("lpqs"), "spill_bytes": st.get("spill_bytes"),
                "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")},
                "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
                "progressive_rounds": st.get("rpq_rounds")}
