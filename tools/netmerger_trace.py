@@ -84,6 +84,19 @@ def summarize(ev):
     return out
 
 
+def cpu_throttle():
+    """(nr_throttled, throttled_usec) of this cgroup (v2 cpu.stat), or None: the GPU boxes run commands
+    under a CPU quota, and a task whose threads exceed it inside a period stalls until the next one."""
+    for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"):
+        try:
+            kv = dict(line.split() for line in open(path))
+        except OSError:
+            continue
+        usec = int(kv["throttled_usec"]) if "throttled_usec" in kv else int(kv.get("throttled_time", 0)) // 1000
+        return int(kv.get("nr_throttled", 0)), usec
+    return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=2.0)
@@ -119,6 +132,7 @@ def main() -> int:
             os.unlink(TRACE)
         conf = {"mapred.uda.merge.backend": "gpu", **extra}
         c = UdaConsumer(args.maps, "job_tr", f"attempt_tr_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
+        thr0 = cpu_throttle()
         t0 = time.perf_counter()
         for m in range(args.maps):
             c.fetch("localhost", "job_tr", f"attempt_tr_m_{m:06d}_0", 0)
@@ -131,6 +145,9 @@ def main() -> int:
                "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")},
                "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
                "progressive_rounds": st.get("rpq_rounds")}
+        thr1 = cpu_throttle()
+        if thr0 and thr1:
+            res["cpu_throttled"] = {"periods": thr1[0] - thr0[0], "ms": round((thr1[1] - thr0[1]) / 1e3, 1)}
         if name != "warmup" and os.path.exists(TRACE):
             res.update(summarize(load(TRACE)))
         print(json.dumps(res), flush=True)
