@@ -87,8 +87,17 @@ struct DeviceWorkspace {
   gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
   gpu::DeviceBuffer frame_scratch; // device framing walk of compressed partitions (device fetch)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
+  hsa_signal_t h2d_sig{};    // SDMA H2D of pinned spans (device_merge, pinned_src)
+  bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
   ~DeviceWorkspace() {
+    if (h2d_sig.handle) {
+      try {
+        gpu::SdmaEngine::wait(h2d_sig);
+      } catch (...) {
+      }
+      (void)hsa_signal_destroy(h2d_sig);
+    }
     for (auto e : piece_ev)
       if (e) (void)hipEventDestroy(e);
     if (cs) (void)hipStreamDestroy(cs);
@@ -452,8 +461,11 @@ struct GateLease {
 
 // on_round: deliver the merged output in key-range rounds while the device merges the next one
 // (GenericMerger::merge); time spent in it is not counted as device time.
+// pinned_src: the host spans are pinned (spill arenas): their H2D goes to an SDMA engine (not the
+// delivery engine) instead of a blit kernel whose host reads would slow the merge kernels beside it.
 DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_runs, Codec codec, KeyKind kind,
-                            int64_t spacing, hipStream_t s, const gpu::GenericMerger::RoundFn& on_round = nullptr) {
+                            int64_t spacing, hipStream_t s, const gpu::GenericMerger::RoundFn& on_round = nullptr,
+                            bool pinned_src = false) {
   double round_ms = 0;
   gpu::GenericMerger::RoundFn timed;
   if (on_round)
@@ -526,8 +538,26 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   std::vector<const uint8_t*> runs;
   std::vector<int64_t> bytes;
   int64_t off = 0;
+  gpu::SdmaEngine* h2d = nullptr;
+  if (pinned_src && host_raw.empty() && ws.h2d_sdma_ok) {
+    try {
+      int dev = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      h2d = &gpu::SdmaEngine::for_device(dev);
+      if (!ws.h2d_sig.handle) ws.h2d_sig = h2d->make_signal();
+      gpu::SdmaEngine::arm(ws.h2d_sig, 0);
+    } catch (const std::exception&) {
+      h2d = nullptr;
+      ws.h2d_sdma_ok = false;
+    }
+  }
   for (size_t i = 0; i < ptrs.size(); ++i) {
-    if (lens[i] > 0) HIP_CHECK(hipMemcpyAsync(stage + off, ptrs[i], (size_t)lens[i], hipMemcpyHostToDevice, s));
+    if (lens[i] > 0 && h2d) {
+      gpu::SdmaEngine::add(ws.h2d_sig, 1);
+      h2d->copy_h2d(stage + off, ptrs[i], (size_t)lens[i], ws.h2d_sig);
+    } else if (lens[i] > 0) {
+      HIP_CHECK(hipMemcpyAsync(stage + off, ptrs[i], (size_t)lens[i], hipMemcpyHostToDevice, s));
+    }
     if (decode_on_device) {
       runs.push_back(in.as<uint8_t>() + plan.raw_offset[i]);
       bytes.push_back(plan.raw_offset[i + 1] - plan.raw_offset[i]);
@@ -537,6 +567,7 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
     }
     off += lens[i];
   }
+  if (h2d) gpu::SdmaEngine::wait(ws.h2d_sig);
   HIP_CHECK(hipStreamSynchronize(s));
   auto t1 = std::chrono::steady_clock::now();
   ws.h2d_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -1396,7 +1427,12 @@ void ReduceTask::merge_gpu() {
             views.push_back(Span{p, e - b});
           }
         }
-        return device_merge(*wsv[q & 1], views, Codec::kNone, kind_, kv, sv[q & 1]);  // views: host spans
+        // views: pinned host spans (spill arena or slice arena): SDMA H2D (UDA_RPQ_H2D_SDMA=0: blit)
+        static const bool sdma_h2d = [] {
+          const char* e = std::getenv("UDA_RPQ_H2D_SDMA");
+          return !e || std::atoi(e) != 0;
+        }();
+        return device_merge(*wsv[q & 1], views, Codec::kNone, kind_, kv, sv[q & 1], nullptr, sdma_h2d);
       };
       std::future<DeviceMergeOut> next = std::async(std::launch::async, prep, 0);
       for (int q = 0; q < rounds; ++q) {
