@@ -87,7 +87,7 @@ struct DeviceWorkspace {
   gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
   gpu::DeviceBuffer frame_scratch; // device framing walk of compressed partitions (device fetch)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
-  hsa_signal_t h2d_sig{};    // SDMA H2D of pinned spans (device_merge, pinned_src)
+  hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
   ~DeviceWorkspace() {
@@ -860,8 +860,28 @@ void ReduceTask::merge_gpu() {
     if (!disk) {
       const auto td = std::chrono::steady_clock::now();
       const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
-      if (m.bytes > 0)
+      // on the SDMA delivery engine (idle until the RPQ rounds deliver), not a blit kernel on the CUs
+      // the next LPQ merge needs; device_merge returned with `s` drained (UDA_LPQ_D2H_SDMA=0: blit)
+      static const bool sdma_d2h = [] {
+        const char* e = std::getenv("UDA_LPQ_D2H_SDMA");
+        return !e || std::atoi(e) != 0;
+      }();
+      gpu::SdmaEngine* eng = nullptr;
+      if (sdma_d2h && m.bytes > 0) {
+        try {
+          eng = &gpu::SdmaEngine::for_device(device);
+        } catch (const std::exception&) {
+          eng = nullptr;
+        }
+      }
+      if (eng) {
+        if (!ws.h2d_sig.handle) ws.h2d_sig = eng->make_signal();
+        gpu::SdmaEngine::arm(ws.h2d_sig, eng->parts((size_t)m.bytes, 1));
+        eng->copy_d2h(run.mem, ws.out.as<uint8_t>(), (size_t)m.bytes, ws.h2d_sig, 1);
+        gpu::SdmaEngine::wait(ws.h2d_sig);
+      } else if (m.bytes > 0) {
         HIP_CHECK(hipMemcpyAsync(run.mem, ws.out.as<uint8_t>(), (size_t)m.bytes, hipMemcpyDeviceToHost, s));
+      }
       HIP_CHECK(hipStreamSynchronize(s));
       if (tt) trace::host_event("lpq_d2h", m.bytes, 0, tt, trace::now_ns());
       ws.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
