@@ -54,10 +54,18 @@ void DeviceBuffer::alloc(size_t bytes) {
   if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
   // Blocks another process may map over hipIpc (our descriptor fetch, RCCL's peer registration of
   // send/receive buffers) must stay out of the size range that hangs the importer (device_ptr.h).
+  const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
   HIP_CHECK(hipMalloc(&ptr_, ipc_safe_bytes(bytes)));
+  if (tt) trace::host_event("device_alloc", (int64_t)bytes, 0, tt, trace::now_ns());
   size_ = bytes;
 }
 void DeviceBuffer::reset() {
+  if (ptr_ && trace::host_enabled()) {
+    const int64_t tt = trace::now_ns();
+    (void)hipFree(ptr_);
+    trace::host_event("device_free", (int64_t)size_, 0, tt, trace::now_ns());
+    ptr_ = nullptr;
+  }
   if (ptr_) (void)hipFree(ptr_);
   ptr_ = nullptr;
   size_ = 0;
@@ -85,7 +93,10 @@ PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
   Block b;
   b.size = (min_bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
   void* p = nullptr;
-  if (hipHostMalloc(&p, b.size, hipHostMallocDefault) != hipSuccess) {
+  const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
+  const hipError_t he = hipHostMalloc(&p, b.size, hipHostMallocDefault);
+  if (tt) trace::host_event("pinned_alloc", (int64_t)b.size, (int64_t)min_bytes, tt, trace::now_ns());
+  if (he != hipSuccess) {
     // trim the cache and retry once
     std::multimap<size_t, uint8_t*> drop;
     {
