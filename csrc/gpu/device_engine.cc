@@ -91,7 +91,10 @@ PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
     }
   }
   Block b;
-  b.size = (min_bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+  // 2 MiB granules; blocks above 64 MiB in 32 MiB granules, so the next task's slightly different
+  // sizes (LPQ spills, partitions) find the cached block instead of pinning a new one (tens of ms)
+  const size_t gran = min_bytes > ((size_t)64 << 20) ? ((size_t)32 << 20) : ((size_t)2 << 20);
+  b.size = (min_bytes + gran - 1) & ~(gran - 1);
   void* p = nullptr;
   const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
   const hipError_t he = hipHostMalloc(&p, b.size, hipHostMallocDefault);
