@@ -230,7 +230,10 @@ def netmerger(args) -> dict:
                                       "mapred.uda.gpu.spill": "host"}),
                 ("gpu_hybrid", {"mapred.uda.merge.backend": "gpu",
                                 "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
-                                "mapred.uda.gpu.spill": "host"})]
+                                "mapred.uda.gpu.spill": "host"}),
+                ("gpu_hybrid_lpq", {"mapred.uda.merge.backend": "gpu",
+                                    "mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6),
+                                    "mapred.uda.gpu.spill": "host", "mapred.uda.gpu.hybrid.direct": 0})]
     for i, (name, conf) in enumerate(variants):
         c = UdaConsumer(args.maps, "job_nm", f"attempt_nm_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
         r0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -252,6 +255,8 @@ def netmerger(args) -> dict:
         out[name + "_fetch_ms"] = round(st["fetch_ms"], 1)
         if name.startswith("gpu"):
             out[name + "_phases_ms"] = {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")}
+        if name.startswith("gpu_hybrid"):
+            out[name + "_direct"] = st.get("hybrid_direct")
         if name == "gpu_hybrid":
             out["hybrid_lpqs"] = st["lpqs"]
             out["hybrid_rpq_rounds"] = st["rpq_rounds"]

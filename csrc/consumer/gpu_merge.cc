@@ -687,6 +687,29 @@ int cmp_key(KeyKind kind, const std::string& a, const std::string& b) {
                      reinterpret_cast<const uint8_t*>(b.data()), (int)b.size());
 }
 
+// Direct RPQ (see merge_gpu): a fetched partition, already a sorted run in pinned DRAM, becomes an RPQ
+// input as it is: the record boundary at or after every `spacing` bytes and its key, by one walk of
+// the VInt headers. bytes = the records (an EOF marker ends the walk and is left out).
+SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
+  SpillRun run;
+  run.mem = p;
+  int64_t off = 0, next_cut = 0;
+  while (off < len) {
+    RecordView rv;
+    const Parse ps = ifile_parse(p + off, (size_t)(len - off), &rv);
+    if (ps == Parse::kEof) break;
+    if (ps != Parse::kRecord) throw UdaError("hybrid index: bad record in a fetched partition");
+    if (off >= next_cut) {
+      run.cut.push_back(off);
+      run.key.emplace_back(reinterpret_cast<const char*>(rv.key), (size_t)rv.klen);
+      next_cut = off + spacing;
+    }
+    off += rv.size();
+  }
+  run.bytes = off;
+  return run;
+}
+
 }  // namespace
 
 void ReduceTask::merge_gpu() {
@@ -996,6 +1019,56 @@ void ReduceTask::merge_gpu() {
       }
     });
   };
+  // Direct RPQ (mapred.uda.gpu.hybrid.direct, default on, DRAM tier, uncompressed partitions, at most
+  // mapred.uda.gpu.hybrid.direct.max.runs maps): once the input outgrows the device budget, the
+  // fetched partitions stay where the fetch put them (pinned DRAM, already sorted runs) and are indexed
+  // by the drain threads; the RPQ key-range rounds then merge slices of all of them. The reference's
+  // LPQ level (MergeManager.cc:202-288) bounds a CPU heap's fan-in and spills to disk; on this tier it
+  // would only re-sort bytes already in DRAM, at two extra PCIe crossings (LPQ H2D + spill D2H), while
+  // the device K-way merge takes hundreds of runs per round. The disk tier keeps the LPQ level.
+  const bool direct_ok = tier == "host" && codec_ == Codec::kNone && restored_files_.empty() && !ckpt &&
+                         host_->conf_i64("mapred.uda.gpu.hybrid.direct", 1) != 0 &&
+                         maps <= host_->conf_i64("mapred.uda.gpu.hybrid.direct.max.runs", 1024);
+  bool direct = false;
+  std::vector<SpillRun> direct_runs;  // one per fetched partition, in `group` order
+  auto index_spans = [&](const std::vector<Span>& spans, size_t first, std::vector<SpillRun>* out) {
+    const size_t n = spans.size() - first;
+    out->resize(n);
+    std::atomic<size_t> nk{0};
+    std::vector<std::exception_ptr> errs(n);
+    std::vector<std::thread> ts;
+    const size_t nt = std::min<size_t>(n, (size_t)std::max<int64_t>(1, drains > 0 ? drains : 8));
+    for (size_t w = 0; w < nt; ++w)
+      ts.emplace_back([&] {
+        for (size_t k; (k = nk++) < n;) try {
+            (*out)[k] = index_host_run(const_cast<uint8_t*>(spans[first + k].p), spans[first + k].len, kSampleSpacing);
+          } catch (...) {
+            errs[k] = std::current_exception();
+          }
+      });
+    for (auto& t : ts) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  };
+  // The group overflowed the budget: an LPQ merge, or the switch to direct RPQ (partitions drained so
+  // far are indexed here, later ones by their drain threads; early staging to HBM stops).
+  auto overflow = [&] {
+    if (!direct_ok) {
+      spill_group();
+      return;
+    }
+    if (direct) return;
+    direct = true;
+    if (stager) {
+      stager->reset();  // the partitions' HBM copies are not used: RPQ rounds copy their slices
+      stager = nullptr;
+    }
+    std::vector<SpillRun> idx;
+    index_spans(group, 0, &idx);
+    for (auto& r : idx) direct_runs.push_back(std::move(r));
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.hybrid_direct = 1;
+  };
   // resume: restored LPQ spills (data + sparse index) of a failed attempt
   if (ckpt && restored_files_.empty()) ::unlink(manifest.c_str());
   for (const std::string& path : restored_files_) {
@@ -1130,14 +1203,16 @@ void ReduceTask::merge_gpu() {
         while (next < ready.size()) {
           const int64_t pl = std::max<int64_t>(ready[next]->part_len(), 0);
           const int64_t est = pl * (codec_ != Codec::kNone ? 3 : 1);  // decoded size estimate
-          if ((!group.empty() || !sub.empty()) && group_raw + est > budget) break;
+          if (!direct && (!group.empty() || !sub.empty()) && group_raw + est > budget) break;
           sub.push_back(next++);
           group_raw += est;
         }
-        if (sub.empty()) {  // the group is full: merge and spill it, then admit the MOF
-          spill_group();
+        if (sub.empty()) {  // the group is full: merge and spill it (or go direct), then admit the MOF
+          overflow();
           continue;
         }
+        const bool index_now = direct;  // direct RPQ: each drain thread indexes its partition
+        std::vector<SpillRun> sub_idx(index_now ? sub.size() : 0);
         std::vector<Span> got(sub.size());
         std::vector<std::vector<uint8_t>> host_decoded(sub.size());
         std::vector<uint8_t*> dst(sub.size(), nullptr);
@@ -1168,6 +1243,7 @@ void ReduceTask::merge_gpu() {
                 }
                 if (dev && stage_step <= 0) stager->copy(dst[k], dev, off);
                 got[k] = Span{dst[k], off, dev};
+                if (index_now) sub_idx[k] = index_host_run(dst[k], off, kSampleSpacing);
               } else {  // host decode: decoded length unknown up front
                 std::vector<uint8_t> buf((size_t)buffer_size_);
                 for (int64_t n; (n = f.pull(buf.data(), (int64_t)buf.size())) > 0;)
@@ -1194,6 +1270,7 @@ void ReduceTask::merge_gpu() {
             got[k] = Span{p, (int64_t)host_decoded[k].size()};
           }
           group.push_back(got[k]);
+          if (index_now) direct_runs.push_back(std::move(sub_idx[k]));
           if (ckpt) group_ids.push_back(ready[sub[k]]->params().map_id);
           drained++;
           progress_count_++;
@@ -1207,7 +1284,7 @@ void ReduceTask::merge_gpu() {
             progress_count_ = 0;
           }
         }
-        if (next < ready.size()) spill_group();  // the next MOF did not fit this group
+        if (next < ready.size()) overflow();  // the next MOF did not fit this group
       }
       ready.clear();
     }
@@ -1319,7 +1396,7 @@ void ReduceTask::merge_gpu() {
           progress_count_ = 0;
         }
       }
-    } else if (spills.empty()) {
+    } else if (spills.empty() && !direct) {
       // ---- online: the whole reduce input in one device merge
       if (stager) {
         const auto tf = std::chrono::steady_clock::now();
@@ -1336,9 +1413,13 @@ void ReduceTask::merge_gpu() {
                                       });
       count_decoded(m.decoded_blocks);
     } else {
-      // ---- hybrid: last LPQ, then RPQ rounds over the spilled runs
-      spill_group();
-      lpq_wait();
+      // ---- hybrid: last LPQ, then RPQ rounds over the spilled runs (direct: over the partitions)
+      if (direct) {
+        spills = std::move(direct_runs);
+      } else {
+        spill_group();
+        lpq_wait();
+      }
       const int R = (int)spills.size();
       struct Sample {
         int run;
@@ -1397,12 +1478,17 @@ void ReduceTask::merge_gpu() {
         if (lo < 0) return 0;
         const int64_t b = run.cut[(size_t)lo];
         const int64_t e = (size_t)lo + 1 < run.cut.size() ? run.cut[(size_t)lo + 1] : run.bytes;
-        std::vector<uint8_t> win((size_t)(e - b));
-        read_run(run, b, e - b, win.data());
+        std::vector<uint8_t> win;
+        const uint8_t* w = run.mem ? run.mem + b : nullptr;  // DRAM runs are scanned in place
+        if (!w) {
+          win.resize((size_t)(e - b));
+          read_run(run, b, e - b, win.data());
+          w = win.data();
+        }
         int64_t p = 0;
         while (b + p < e) {
           RecordView rv;
-          if (ifile_parse(win.data() + p, (size_t)(e - b - p), &rv) != Parse::kRecord)
+          if (ifile_parse(w + p, (size_t)(e - b - p), &rv) != Parse::kRecord)
             throw UdaError("spill scan: bad record");
           if (key_compare(kind_, rv.key, rv.klen, reinterpret_cast<const uint8_t*>(k.data()), (int)k.size()) >= 0)
             break;
@@ -1411,10 +1497,30 @@ void ReduceTask::merge_gpu() {
         return b + p;
       };
       std::vector<std::vector<int64_t>> bnd((size_t)R);
-      for (int r = 0; r < R; ++r) {
+      auto run_bounds = [&](int r) {
         bnd[(size_t)r].push_back(0);
         for (auto& k : split) bnd[(size_t)r].push_back(boundary(spills[(size_t)r], k));
         bnd[(size_t)r].push_back(spills[(size_t)r].bytes);
+      };
+      bool all_mem = true;
+      for (const SpillRun& run : spills) all_mem = all_mem && run.fd < 0;
+      if (all_mem && R > 1) {  // in-place scans of DRAM runs, spread over threads (files share one AsyncIO)
+        std::atomic<int> nr{0};
+        std::vector<std::exception_ptr> errs((size_t)R);
+        std::vector<std::thread> ts;
+        for (int w = 0; w < std::min(R, 8); ++w)
+          ts.emplace_back([&] {
+            for (int r; (r = nr++) < R;) try {
+                run_bounds(r);
+              } catch (...) {
+                errs[(size_t)r] = std::current_exception();
+              }
+          });
+        for (auto& t : ts) t.join();
+        for (auto& e : errs)
+          if (e) std::rethrow_exception(e);
+      } else {
+        for (int r = 0; r < R; ++r) run_bounds(r);
       }
       const int rounds = (int)split.size() + 1;
       {

@@ -56,16 +56,10 @@ struct TaskHost {
   std::string failure;
   bool finished = false;
 };
+// dataFromUda: the KVBuf copy; the task's walker thread walks it and reports EOF (set_on_eof)
 int data_cb(void* ctx, const void* buf, int32_t len) {
   auto* t = static_cast<TaskHost*>(ctx);
-  const int r = t->sink->consume(t->reducer, static_cast<const uint8_t*>(buf), len);
-  if (r == 0 && t->sink->eof(t->reducer)) {
-    std::lock_guard<std::mutex> g(*t->mu);
-    t->finished = true;
-    ++*t->done;
-    t->cv->notify_all();
-  }
-  return r;
+  return t->sink->consume(t->reducer, static_cast<const uint8_t*>(buf), len);
 }
 void failure_cb(void* ctx, const char* reason) {
   auto* t = static_cast<TaskHost*>(ctx);
@@ -373,7 +367,20 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   const int W = cfg_.world;
   if ((int)expected_.size() != R) throw std::runtime_error("api bench: expected record counts not set");
   if (W > 1 && (int)peers_.size() != W) throw std::runtime_error("api bench: provider addresses not set");
+  std::mutex mu;
+  std::condition_variable cv;
+  int done = 0;
+  std::vector<TaskHost> hosts(R);  // before the sink: its reduce-task threads report EOF into them
   J2CSink sink(R, cfg_.kv_buf_bytes);
+  sink.set_on_eof([&hosts](int r) {  // the reduce task's thread walked its EOF marker
+    TaskHost& t = hosts[(size_t)r];
+    std::lock_guard<std::mutex> g(*t.mu);
+    if (!t.finished) {
+      t.finished = true;
+      ++*t.done;
+    }
+    t.cv->notify_all();
+  });
   sink.set_check_order(validate);
   sink.set_key_kind(1);  // Text: content order (TeraSort's fixed keys order the same either way)
   // device-wide HBM in use, sampled through the step (the peak includes the map-output store)
@@ -397,10 +404,6 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
     }
   } sampler_guard{sampling, sampler};
   ConfTable& conf = bench_conf(cfg_);
-  std::mutex mu;
-  std::condition_variable cv;
-  int done = 0;
-  std::vector<TaskHost> hosts(R);
   std::vector<uda_handle*> handles(R, nullptr);
   std::vector<std::string> errors(R);
   const double t0 = now_ms();
@@ -481,6 +484,7 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
     }
     uda_destroy(handles[r]);
   }
+  sink.flush();  // every delivered KVBuf walked
   sampling = false;
   if (sampler.joinable()) sampler.join();
   const double t2 = now_ms();

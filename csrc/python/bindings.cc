@@ -854,8 +854,14 @@ PYBIND11_MODULE(_uda_native, m) {
         py::arg("host_source") = false, py::arg("rounds") = 1, py::arg("device") = 0);
 
   py::class_<gpu::J2CSink, std::shared_ptr<gpu::J2CSink>>(m, "J2CSink")
-      .def(py::init<int, int64_t>(), py::arg("reducers"), py::arg("kv_buf_bytes") = 1 << 20)
+      .def(py::init([](int r, int64_t kv, py::object threaded) {
+             return std::make_shared<gpu::J2CSink>(r, kv, threaded.is_none() ? gpu::J2CSink::default_threaded()
+                                                                               : threaded.cast<bool>());
+           }),
+           py::arg("reducers"), py::arg("kv_buf_bytes") = 1 << 20, py::arg("threaded") = py::none())
       .def_property_readonly("reducers", &gpu::J2CSink::reducers)
+      .def_property_readonly("threaded", &gpu::J2CSink::threaded)
+      .def("flush", &gpu::J2CSink::flush, py::call_guard<py::gil_scoped_release>())
       .def("records", &gpu::J2CSink::records)
       .def("bytes", &gpu::J2CSink::bytes)
       .def("buffers", &gpu::J2CSink::buffers)
@@ -863,7 +869,7 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("error", &gpu::J2CSink::error)
       .def("order_errors", &gpu::J2CSink::order_errors)
       .def("set_check_order", &gpu::J2CSink::set_check_order)
-      .def("reset", &gpu::J2CSink::reset)
+      .def("reset", &gpu::J2CSink::reset, py::call_guard<py::gil_scoped_release>())
       // one dataFromUda buffer for reducer r (returns the sink's status code, 0 = ok); reps > 1
       // consumes the same buffer again (micro-benchmarks; EOF buffers only once)
       .def("consume", [](gpu::J2CSink& s, int r, py::buffer b, int reps) {

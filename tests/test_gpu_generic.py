@@ -183,10 +183,13 @@ def test_consumer_gpu_progressive_phases(require_gpu, phases, drains, maps, kind
         p.close()
 
 
-@pytest.mark.parametrize("tier,codec", [("host", None), ("disk", None), ("disk", "snappy")])
-def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
+@pytest.mark.parametrize("tier,codec,direct", [("host", None, 1), ("host", None, 0), ("disk", None, 1),
+                                               ("disk", "snappy", 1)])
+def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec, direct):
     """Reduce input larger than the device budget: LPQ merges on the GPU spill to host DRAM or to
-    the local dirs (AsyncIO), then RPQ key-range rounds merge the spilled runs on the GPU."""
+    the local dirs (AsyncIO), then RPQ key-range rounds merge the spilled runs on the GPU. On the
+    DRAM tier the default is the direct RPQ: no LPQ level, the rounds merge slices of the fetched
+    partitions where the fetch put them (mapred.uda.gpu.hybrid.direct=0 keeps the LPQ level)."""
     from uda_amd.utils.mof import write_mof
     p = UdaProvider()
     try:
@@ -200,10 +203,13 @@ def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec):
         d1 = tmp_path / "ld1"
         d1.mkdir()
         conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.merge.bytes": 300_000,
-                "mapred.uda.gpu.spill": tier}
+                "mapred.uda.gpu.spill": tier, "mapred.uda.gpu.hybrid.direct": direct}
         recs, st, c = run_reduce("h", f"job_h{tier}{codec}", ids, 0, datagen.TEXT, codec=codec, conf=conf,
                                  kv_buf_size=8192, local_dirs=(str(d1),))
-        assert st["lpqs"] >= 4 and st["rpq_rounds"] >= 3, st
+        if tier == "host" and direct:
+            assert st["hybrid_direct"] == 1 and st["lpqs"] == 0 and st["rpq_rounds"] >= 3, st
+        else:
+            assert st["hybrid_direct"] == 0 and st["lpqs"] >= 4 and st["rpq_rounds"] >= 3, st
         want = sorted((kv for m in maps for kv in m[0]), key=datagen.sort_key(datagen.TEXT))
         kf = datagen.sort_key(datagen.TEXT)
         assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]

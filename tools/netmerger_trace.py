@@ -126,6 +126,7 @@ def main() -> int:
         named[f"prog{ph}"] = {"mapred.uda.gpu.progressive.phases": ph}
     named["whole"] = {"mapred.uda.gpu.progressive.phases": 0}
     named["hybrid"] = {"mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6), "mapred.uda.gpu.spill": "host"}
+    named["hybrid_lpq"] = {**named["hybrid"], "mapred.uda.gpu.hybrid.direct": 0}
     variants = [("warmup", {})] + [(f"{name}_{i}", named[name]) for i in range(args.repeat)
                                    for name in args.variants.split(",")]
     for i, (name, extra) in enumerate(variants):
@@ -145,7 +146,7 @@ def main() -> int:
                "lpqs": st.get("lpqs"), "spill_bytes": st.get("spill_bytes"),
                "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")},
                "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
-               "progressive_rounds": st.get("rpq_rounds")}
+               "progressive_rounds": st.get("rpq_rounds"), "hybrid_direct": st.get("hybrid_direct")}
         thr1 = cpu_throttle()
         if thr0 and thr1:
             res["cpu_throttled"] = {"periods": thr1[0] - thr0[0], "ms": round((thr1[1] - thr0[1]) / 1e3, 1)}

@@ -148,6 +148,7 @@ class TeraSortShuffle:
             self.sink.reset()
         st = self.job.run_step(self.cfg.validate if validate is None else validate)
         if self.sink is not None and self.cfg.deliver_host:
+            self.sink.flush()  # the reduce tasks' threads walked every delivered KVBuf
             st["consumer_records"] = [self.sink.records(i) for i in range(self.cfg.reducers)]
             st["consumer_errors"] = [self.sink.error(i) for i in range(self.cfg.reducers)]
             st["consumer_eof"] = [self.sink.eof(i) for i in range(self.cfg.reducers)]
