@@ -571,6 +571,8 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   HIP_CHECK(hipStreamSynchronize(s));
   auto t1 = std::chrono::steady_clock::now();
   ws.h2d_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  const int64_t tm = trace::host_enabled() ? trace::now_ns() : 0;
+  if (tm) trace::host_event("dm_h2d", staged, (int64_t)ptrs.size(), tm - (int64_t)((t1 - t0).count()), tm);
   DeviceMergeOut res;
   if (decode_on_device) {
     ws.decoder.decode(codec, plan, ws.packed.as<uint8_t>(), in.as<uint8_t>(), s);
@@ -580,6 +582,7 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   gpu::GenericMergeResult r = ws.merger.merge(runs, bytes, (int)kind, out.as<uint8_t>(), total, spacing, s, timed);
   HIP_CHECK(hipStreamSynchronize(s));
   ws.device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count() - round_ms;
+  if (tm) trace::host_event("dm_merge", total, (int64_t)ptrs.size(), tm, trace::now_ns());
   res.bytes = r.bytes;
   res.cuts = std::move(r.cuts);
   res.records = r.records;
@@ -691,10 +694,20 @@ int cmp_key(KeyKind kind, const std::string& a, const std::string& b) {
 // input as it is: the record boundary at or after every `spacing` bytes and its key, by one walk of
 // the VInt headers. bytes = the records (an EOF marker ends the walk and is left out).
 SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
+  const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
   SpillRun run;
   run.mem = p;
   int64_t off = 0, next_cut = 0;
   while (off < len) {
+    // between cuts: skip records with one-byte VInt headers (lengths < 128) without parsing them
+    while (off < next_cut && off + 2 <= len) {
+      const int8_t k1 = (int8_t)p[off], v1 = (int8_t)p[off + 1];
+      if ((k1 | v1) < 0) break;  // multi-byte header or the EOF marker: the parser below
+      const int64_t nx = off + 2 + k1 + v1;
+      if (nx > len) break;  // truncated: the parser below reports it
+      off = nx;
+    }
+    if (off >= len) break;
     RecordView rv;
     const Parse ps = ifile_parse(p + off, (size_t)(len - off), &rv);
     if (ps == Parse::kEof) break;
@@ -707,6 +720,7 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
     off += rv.size();
   }
   run.bytes = off;
+  if (tt) trace::host_event("index", len, (int64_t)run.cut.size(), tt, trace::now_ns());
   return run;
 }
 
@@ -760,8 +774,9 @@ void ReduceTask::merge_gpu() {
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
-  PoolLease<DeviceWorkspace> ws2_lease{device, nullptr};  // second workspace of the pipelined RPQ rounds
+  PoolLease<DeviceWorkspace> ws2_lease{device, nullptr}, ws3_lease{device, nullptr};  // pipelined RPQ rounds
   DeviceWorkspace* ws2 = nullptr;
+  DeviceWorkspace* ws3 = nullptr;
   // uncompressed partitions go to HBM as soon as each one is complete (overlapping the fetch)
   // Two stagers: the group being fetched is staged by `stager` while the LPQ thread merges the
   // previous group out of `job_stager`'s arena; spill_group swaps them.
@@ -1527,21 +1542,28 @@ void ReduceTask::merge_gpu() {
         std::lock_guard<std::mutex> g(st_mu_);
         st_.rpq_rounds = rounds;
       }
-      // RPQ rounds, pipelined over two workspaces: round q + 1's slices are read, copied to HBM and
-      // merged on a helper thread (workspace and stream of parity q + 1) while round q is delivered.
+      // RPQ rounds: each round's slices are read, copied to HBM and merged on a helper thread (its own
+      // workspace and stream) while earlier rounds are delivered.
       ws2_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
       ws2 = ws2_lease.obj.get();
       ws2->reset_stats();
-      StreamGuard sg2;
+      // Three workspaces, two rounds prepared ahead: round q + 2's slices cross PCIe (SDMA H2D) while
+      // round q + 1 merges and round q is delivered (D2H), so the rounds cost max(H2D, merge, D2H)
+      // each instead of H2D + merge.
+      ws3_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
+      ws3 = ws3_lease.obj.get();
+      ws3->reset_stats();
+      StreamGuard sg2, sg3;
       HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
-      DeviceWorkspace* wsv[2] = {&ws, ws2};
-      hipStream_t sv[2] = {s, sg2.s};
-      gpu::PinnedArena slice_mem[2];
+      HIP_CHECK(hipStreamCreateWithFlags(&sg3.s, hipStreamNonBlocking));
+      DeviceWorkspace* wsv[3] = {&ws, ws2, ws3};
+      hipStream_t sv[3] = {s, sg2.s, sg3.s};
+      gpu::PinnedArena slice_mem[3];
       auto prep = [&](int q) {
         if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
         std::vector<Span> views;
-        gpu::PinnedArena& sm = slice_mem[q & 1];
-        sm.release_all();  // round q - 2's slices: copied to HBM before its merge returned
+        gpu::PinnedArena& sm = slice_mem[q % 3];
+        sm.release_all();  // round q - 3's slices: copied to HBM before its merge returned
         for (int r = 0; r < R; ++r) {
           const SpillRun& run = spills[(size_t)r];
           const int64_t b = bnd[(size_t)r][(size_t)q], e = bnd[(size_t)r][(size_t)q + 1];
@@ -1558,13 +1580,17 @@ void ReduceTask::merge_gpu() {
           const char* e = std::getenv("UDA_RPQ_H2D_SDMA");
           return !e || std::atoi(e) != 0;
         }();
-        return device_merge(*wsv[q & 1], views, Codec::kNone, kind_, kv, sv[q & 1], nullptr, sdma_h2d);
+        return device_merge(*wsv[q % 3], views, Codec::kNone, kind_, kv, sv[q % 3], nullptr, sdma_h2d);
       };
-      std::future<DeviceMergeOut> next = std::async(std::launch::async, prep, 0);
+      std::vector<std::future<DeviceMergeOut>> next((size_t)rounds);
+      for (int q = 0; q < std::min(rounds, 2); ++q) next[(size_t)q] = std::async(std::launch::async, prep, q);
       for (int q = 0; q < rounds; ++q) {
-        DeviceMergeOut m = next.get();
-        if (q + 1 < rounds) next = std::async(std::launch::async, prep, q + 1);
-        deliver(m, q + 1 == rounds, sv[q & 1], *wsv[q & 1]);
+        DeviceMergeOut m = next[(size_t)q].get();
+        // workspace (q + 2) % 3 delivered round q - 1 before this iteration
+        if (q + 2 < rounds) next[(size_t)q + 2] = std::async(std::launch::async, prep, q + 2);
+        const int64_t td = trace::host_enabled() ? trace::now_ns() : 0;
+        deliver(m, q + 1 == rounds, sv[q % 3], *wsv[q % 3]);
+        if (td) trace::host_event("rpq_deliver", m.bytes, q, td, trace::now_ns());
       }
     }
     if (!eof_sent) {  // empty final round (or empty input): EOF alone
@@ -1578,13 +1604,14 @@ void ReduceTask::merge_gpu() {
     HIP_CHECK(hipStreamSynchronize(s));
     ws_lease.clean = true;
     ws2_lease.clean = true;
+    ws3_lease.clean = true;
     stager_lease.clean = true;
     stager_lease2.clean = true;
     std::lock_guard<std::mutex> g(st_mu_);
-    st_.gpu_h2d_ms = ws.h2d_ms + (ws2 ? ws2->h2d_ms : 0);
-    st_.gpu_device_ms = ws.device_ms + (ws2 ? ws2->device_ms : 0);
-    st_.gpu_d2h_wait_ms = ws.d2h_ms + (ws2 ? ws2->d2h_ms : 0);
-    st_.gpu_sink_ms = ws.sink_ms + (ws2 ? ws2->sink_ms : 0);
+    st_.gpu_h2d_ms = ws.h2d_ms + (ws2 ? ws2->h2d_ms : 0) + (ws3 ? ws3->h2d_ms : 0);
+    st_.gpu_device_ms = ws.device_ms + (ws2 ? ws2->device_ms : 0) + (ws3 ? ws3->device_ms : 0);
+    st_.gpu_d2h_wait_ms = ws.d2h_ms + (ws2 ? ws2->d2h_ms : 0) + (ws3 ? ws3->d2h_ms : 0);
+    st_.gpu_sink_ms = ws.sink_ms + (ws2 ? ws2->sink_ms : 0) + (ws3 ? ws3->sink_ms : 0);
     st_.fetch_ms = prog_fetch_ms >= 0 ? prog_fetch_ms : fetch_ms;
     st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - st_.fetch_ms;
     if (trace::host_enabled()) {

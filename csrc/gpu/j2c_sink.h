@@ -33,10 +33,13 @@ class J2CSink {
  public:
   enum Error : int { kOk = 0, kTooLong = 1, kBadFraming = 2, kAfterEof = 3 };
 
-  // UDA_J2C_THREADS=0: inline walks by default (A/B of the threading model)
+  // Default inline; UDA_J2C_THREADS=1 walks on the reduce task's own thread. Measured on MI355X boxes
+  // (profiles/r3_j2c_threads_ab.md): the copy out of the SDMA-written ring, not the walk, bounds a
+  // task (~25 GB/s per thread), so the split gains 9 % on the skewed config #5 task and loses on a
+  // single out-of-cache stream (the walker reads the KVBuf from the copying core's cache).
   static bool default_threaded() {
     const char* e = std::getenv("UDA_J2C_THREADS");
-    return !e || std::atoi(e) != 0;
+    return e && std::atoi(e) != 0;
   }
   J2CSink(int reducers, int64_t kv_buf_bytes, bool threaded = default_threaded())
       : kv_(kv_buf_bytes), threaded_(threaded) {

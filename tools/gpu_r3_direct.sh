@@ -1,6 +1,6 @@
 #!/bin/bash
 # Direct RPQ vs the LPQ level on the DRAM tier (2 GB secondary sort, one task, budget = input / 6):
-# hybrid tests, host-event traces of both, and a GenericMerger phase profile of the LPQ variant.
+# hybrid/consumer tests, then host-event traces of both (index, per-round H2D / merge / delivery spans).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_generic.py \
@@ -13,7 +13,8 @@ import json
 for line in open('gpurun_out/r3_direct_ab.jsonl'):
     d = json.loads(line)
     print(d['variant'], d['gbps'], d['wall_ms'], 'fetch', d.get('fetch_ms'), 'direct', d.get('hybrid_direct'), 'lpqs', d.get('lpqs'), 'rounds', d.get('progressive_rounds'), d['phases_ms'])
+    for k in ('index', 'dm_h2d', 'dm_merge', 'rpq_deliver'):
+        v = d.get(k)
+        if v and v.get('n'):
+            print('   ', k, {kk: vv for kk, vv in v.items() if kk != 'spans_ms'}, (v.get('spans_ms') or [])[:14])
 "
-UDA_GM_PROFILE=1 timeout -k 10 200 python -u tools/netmerger_trace.py --variants hybrid_lpq --repeat 1 \
-  > gpurun_out/r3_lpq_gmprof.jsonl 2> gpurun_out/r3_lpq_gmprof.err || { tail -20 gpurun_out/r3_lpq_gmprof.err; exit 1; }
-grep -c . gpurun_out/r3_lpq_gmprof.err
