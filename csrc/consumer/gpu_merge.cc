@@ -1045,7 +1045,7 @@ void ReduceTask::merge_gpu() {
                          host_->conf_i64("mapred.uda.gpu.hybrid.direct", 1) != 0 &&
                          maps <= host_->conf_i64("mapred.uda.gpu.hybrid.direct.max.runs", 1024);
   bool direct = false;
-  std::vector<SpillRun> direct_runs;  // one per fetched partition, in `group` order
+  std::vector<SpillRun> direct_runs;  // one per partition drained after the switch, in `group` order
   auto index_spans = [&](const std::vector<Span>& spans, size_t first, std::vector<SpillRun>* out) {
     const size_t n = spans.size() - first;
     out->resize(n);
@@ -1065,6 +1065,7 @@ void ReduceTask::merge_gpu() {
     for (auto& e : errs)
       if (e) std::rethrow_exception(e);
   };
+  std::future<std::vector<SpillRun>> direct_head;  // partitions drained before the switch, indexed meanwhile
   // The group overflowed the budget: an LPQ merge, or the switch to direct RPQ (partitions drained so
   // far are indexed here, later ones by their drain threads; early staging to HBM stops).
   auto overflow = [&] {
@@ -1078,9 +1079,12 @@ void ReduceTask::merge_gpu() {
       stager->reset();  // the partitions' HBM copies are not used: RPQ rounds copy their slices
       stager = nullptr;
     }
-    std::vector<SpillRun> idx;
-    index_spans(group, 0, &idx);
-    for (auto& r : idx) direct_runs.push_back(std::move(r));
+    // indexed beside the fetch (which goes on filling `group`; the spans indexed here are a copy)
+    direct_head = std::async(std::launch::async, [&index_spans, head = group] {
+      std::vector<SpillRun> idx;
+      index_spans(head, 0, &idx);
+      return idx;
+    });
     std::lock_guard<std::mutex> g(st_mu_);
     st_.hybrid_direct = 1;
   };
@@ -1430,7 +1434,8 @@ void ReduceTask::merge_gpu() {
     } else {
       // ---- hybrid: last LPQ, then RPQ rounds over the spilled runs (direct: over the partitions)
       if (direct) {
-        spills = std::move(direct_runs);
+        spills = direct_head.get();
+        for (auto& r : direct_runs) spills.push_back(std::move(r));
       } else {
         spill_group();
         lpq_wait();

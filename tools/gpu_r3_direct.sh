@@ -13,6 +13,7 @@ import json
 for line in open('gpurun_out/r3_direct_ab.jsonl'):
     d = json.loads(line)
     print(d['variant'], d['gbps'], d['wall_ms'], 'fetch', d.get('fetch_ms'), 'direct', d.get('hybrid_direct'), 'lpqs', d.get('lpqs'), 'rounds', d.get('progressive_rounds'), d['phases_ms'])
+    print('    vm', d.get('vm_deltas'))
     for k in ('index', 'dm_h2d', 'dm_merge', 'rpq_deliver'):
         v = d.get(k)
         if v and v.get('n'):

@@ -98,6 +98,29 @@ def cpu_throttle():
     return None
 
 
+VMSTAT_KEYS = ("numa_hint_faults", "numa_hint_faults_local", "numa_pages_migrated", "pgmigrate_success",
+               "compact_stall", "thp_fault_alloc", "thp_collapse_alloc", "pgmajfault", "pgfault", "tlb_remote_flush")
+
+
+def vm_counters():
+    """System-wide /proc/vmstat counters that can stall a process for tens of ms (NUMA hinting faults,
+    compaction, THP) and this process's minor/major faults."""
+    out = {}
+    try:
+        for line in open("/proc/vmstat"):
+            k, v = line.split()
+            if k in VMSTAT_KEYS:
+                out[k] = int(v)
+    except OSError:
+        pass
+    try:
+        f = open("/proc/self/stat").read().rsplit(")", 1)[1].split()
+        out["self_minflt"], out["self_majflt"] = int(f[7]), int(f[9])
+    except (OSError, IndexError, ValueError):
+        pass
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=2.0)
@@ -106,6 +129,12 @@ def main() -> int:
     ap.add_argument("--variants", default="whole,step8m,step32m",
                     help="comma list of whole, step8m, step32m, prog2, prog4, prog8, prog16")
     args = ap.parse_args()
+    for f in ("/proc/sys/kernel/numa_balancing", "/sys/kernel/mm/transparent_hugepage/enabled",
+              "/sys/kernel/mm/transparent_hugepage/defrag"):
+        try:
+            print(f"# {f}: {open(f).read().strip()}", file=sys.stderr, flush=True)
+        except OSError:
+            pass
     from uda_amd import native
     from uda_amd.bridge import UdaConsumer, UdaProvider
     from uda_amd.utils.datagen import TEXT
@@ -135,6 +164,7 @@ def main() -> int:
         conf = {"mapred.uda.merge.backend": "gpu", **extra}
         c = UdaConsumer(args.maps, "job_tr", f"attempt_tr_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
         thr0 = cpu_throttle()
+        vm0 = vm_counters()
         t0 = time.perf_counter()
         for m in range(args.maps):
             c.fetch("localhost", "job_tr", f"attempt_tr_m_{m:06d}_0", 0)
@@ -148,6 +178,8 @@ def main() -> int:
                "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
                "progressive_rounds": st.get("rpq_rounds"), "hybrid_direct": st.get("hybrid_direct")}
         thr1 = cpu_throttle()
+        vm1 = vm_counters()
+        res["vm_deltas"] = {k: vm1[k] - vm0[k] for k in vm1 if k in vm0 and vm1[k] != vm0[k]}
         if thr0 and thr1:
             res["cpu_throttled"] = {"periods": thr1[0] - thr0[0], "ms": round((thr1[1] - thr0[1]) / 1e3, 1)}
         if name != "warmup" and os.path.exists(TRACE):
