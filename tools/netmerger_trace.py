@@ -121,11 +121,49 @@ def vm_counters():
     return out
 
 
+class WchanSampler:
+    """Every ~2 ms, the scheduler state and kernel wait channel of every thread of this process
+    (/proc/self/task/*/stat, wchan): where threads sit while a task stalls. Samples of running
+    threads and of the usual idle waits (futex, poll, sleep) are only counted."""
+    IDLE = ("futex", "do_epoll_wait", "hrtimer_nanosleep", "do_sys_poll", "do_select", "pipe_read",
+            "unix_stream_read", "inet_csk_accept", "0")
+
+    def __init__(self):
+        import threading
+        self.samples = []
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        t0 = time.perf_counter()
+        while not self.stop.is_set():
+            now = round((time.perf_counter() - t0) * 1e3, 1)
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    st = open(f"/proc/self/task/{tid}/stat").read()
+                    comm = st[st.index("(") + 1:st.rindex(")")]
+                    state = st[st.rindex(")") + 2]
+                    wchan = open(f"/proc/self/task/{tid}/wchan").read().strip()
+                except (OSError, ValueError):
+                    continue
+                if state == "R" or any(wchan.startswith(i) for i in self.IDLE):
+                    continue
+                self.samples.append((now, comm, state, wchan))
+            time.sleep(0.002)
+
+    def summary(self):
+        from collections import Counter
+        c = Counter((w, st) for _, _, st, w in self.samples)
+        return {"busy_waits": [[w, st, n] for (w, st), n in c.most_common(12)],
+                "first": self.samples[:20]}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=2.0)
     ap.add_argument("--maps", type=int, default=64)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--wchan", action="store_true", help="sample every thread's kernel wait channel")
     ap.add_argument("--variants", default="whole,step8m,step32m",
                     help="comma list of whole, step8m, step32m, prog2, prog4, prog8, prog16")
     args = ap.parse_args()
@@ -165,12 +203,18 @@ def main() -> int:
         c = UdaConsumer(args.maps, "job_tr", f"attempt_tr_r_{i:06d}_0", TEXT, conf=conf, keep_records=False)
         thr0 = cpu_throttle()
         vm0 = vm_counters()
+        ws = WchanSampler() if args.wchan else None
+        if ws:
+            ws.t.start()
         t0 = time.perf_counter()
         for m in range(args.maps):
             c.fetch("localhost", "job_tr", f"attempt_tr_m_{m:06d}_0", 0)
         c.wait(3600)
         wall = time.perf_counter() - t0
         st = c.close()
+        if ws:
+            ws.stop.set()
+            ws.t.join()
         assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
         res = {"variant": name, "gbps": round(total / wall / 1e9, 2), "wall_ms": round(wall * 1e3, 1),
                "lpqs": st.get("lpqs"), "spill_bytes": st.get("spill_bytes"),
@@ -179,6 +223,8 @@ def main() -> int:
                "progressive_rounds": st.get("rpq_rounds"), "hybrid_direct": st.get("hybrid_direct")}
         thr1 = cpu_throttle()
         vm1 = vm_counters()
+        if ws:
+            res["wchan"] = ws.summary()
         res["vm_deltas"] = {k: vm1[k] - vm0[k] for k in vm1 if k in vm0 and vm1[k] != vm0[k]}
         if thr0 and thr1:
             res["cpu_throttled"] = {"periods": thr1[0] - thr0[0], "ms": round((thr1[1] - thr0[1]) / 1e3, 1)}
