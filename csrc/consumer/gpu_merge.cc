@@ -85,7 +85,7 @@ struct DeviceWorkspace {
   gpu::DeviceBlockDecoder decoder;
   gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
   gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
-  gpu::DeviceBuffer frame_scratch; // device framing walk of compressed partitions (device fetch)
+  gpu::DeviceBuffer frame_scratch, frame_descs; // device framing walk of compressed partitions (device fetch)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
@@ -1840,7 +1840,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     gpu::BlockPlan bp;
     std::vector<int64_t> roff;
     int64_t blocks = 0;
-    if (gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, s)) {
+    if (gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, ws.frame_descs, s)) {
       DeviceWorkspace::ensure(ws.in, bp.raw_total);
       ws.decoder.decode(codec_, bp, nullptr, ws.in.as<uint8_t>(), s);
       roff = bp.raw_offset;

@@ -60,7 +60,7 @@ bool plan_block_streams(Codec codec, const std::vector<const uint8_t*>& ptrs, co
 }
 
 bool plan_block_streams_device(Codec codec, const std::vector<const uint8_t*>& dptrs, const std::vector<int64_t>& lens,
-                               BlockPlan* plan, DeviceBuffer& scratch, hipStream_t s) {
+                               BlockPlan* plan, DeviceBuffer& scratch, DeviceBuffer& desc_scratch, hipStream_t s) {
   const int n = (int)dptrs.size();
   plan->descs.clear();
   plan->raw_offset.assign(1, 0);
@@ -100,7 +100,9 @@ bool plan_block_streams_device(Codec codec, const std::vector<const uint8_t*>& d
   plan->raw_total = rt;
   plan->descs.resize((size_t)nd);
   if (nd == 0) return true;
-  DeviceBuffer d_descs((size_t)nd * sizeof(DecodeDesc));
+  // the caller's buffer, kept across tasks: a per-call DeviceBuffer cost a device-synchronizing hipFree
+  if (desc_scratch.size() < (size_t)nd * sizeof(DecodeDesc)) desc_scratch.alloc((size_t)nd * sizeof(DecodeDesc) * 3 / 2);
+  DeviceBuffer& d_descs = desc_scratch;
   HIP_CHECK(hipMemcpyAsync(d_dfirst, dfirst.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(d_rfirst, rfirst.data(), 8 * (size_t)n, hipMemcpyHostToDevice, s));
   launch_frame_streams(d_ptrs, d_lens, n, (int)codec, d_dfirst, d_rfirst, d_nb, d_raw, d_descs.as<DecodeDesc>(),

@@ -30,7 +30,7 @@ bool plan_block_streams(Codec codec, const std::vector<const uint8_t*>& ptrs, co
 // addresses, so decode() takes d_in = nullptr and reads every stream where it lies. false: the
 // framing needs a decode (the caller falls back to the host path). Synchronizes s.
 bool plan_block_streams_device(Codec codec, const std::vector<const uint8_t*>& dptrs, const std::vector<int64_t>& lens,
-                               BlockPlan* plan, DeviceBuffer& scratch, hipStream_t s);
+                               BlockPlan* plan, DeviceBuffer& scratch, DeviceBuffer& desc_scratch, hipStream_t s);
 
 class DeviceBlockDecoder {
  public:

@@ -172,7 +172,9 @@ void PinnedBuffer::alloc(size_t bytes) {
   ptr_ = nullptr;
   size_ = 0;
   if (bytes == 0) return;
+  const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
   HIP_CHECK(hipHostMalloc(&ptr_, bytes, hipHostMallocDefault));
+  if (tt) trace::host_event("pinned_buf_alloc", (int64_t)bytes, -1, tt, trace::now_ns());
   size_ = bytes;
 }
 
@@ -181,7 +183,9 @@ void PinnedBuffer::alloc_on_node(size_t bytes, int node) {
   ptr_ = nullptr;
   size_ = 0;
   if (bytes == 0) return;
+  const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
   ptr_ = hip_host_alloc_on_node(bytes, node);  // hipHostMalloc under a preferred-node policy
+  if (tt) trace::host_event("pinned_buf_alloc", (int64_t)bytes, node, tt, trace::now_ns());
   size_ = bytes;
 }
 

@@ -14,6 +14,34 @@
 namespace uda {
 namespace gpu {
 
+namespace {
+// All passes' tables (pairs, then tile prefix, per pass) in one upload into a buffer the merger keeps:
+// a DeviceBuffer per pass meant a hipMalloc and a device-synchronizing hipFree per pass of every merge,
+// which stalled the work of concurrent merges (pipelined RPQ rounds, other reduce tasks).
+std::vector<PassDesc> upload_passes(const std::vector<MergePassPlan>& plans, DeviceBuffer& buf, hipStream_t s) {
+  std::vector<int64_t> all;
+  std::vector<size_t> at;
+  for (const MergePassPlan& mp : plans) {
+    at.push_back(all.size());
+    all.insert(all.end(), mp.pairs.begin(), mp.pairs.end());
+    all.insert(all.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
+  }
+  std::vector<PassDesc> out;
+  if (plans.empty()) return out;
+  if (buf.size() < all.size() * 8) buf.alloc(all.size() * 8 + all.size() * 2 + 256);
+  HIP_CHECK(hipMemcpyAsync(buf.as(), all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+  for (size_t i = 0; i < plans.size(); ++i) {
+    PassDesc pd;
+    pd.pairs = buf.as<int64_t>() + at[i];
+    pd.tile_prefix = pd.pairs + plans[i].pairs.size();
+    pd.npairs = plans[i].npairs;
+    pd.ntiles = plans[i].ntiles;
+    out.push_back(pd);
+  }
+  return out;
+}
+}  // namespace
+
 void GenericMerger::reserve(int64_t records, int runs) {
   if (records <= cap_records_ && runs <= cap_runs_) return;
   records = std::max<int64_t>(records, 1);
@@ -81,7 +109,6 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
   int64_t* d_soff = b.tab.as<int64_t>();
   HIP_CHECK(hipMemcpyAsync(d_soff, soff.data(), 8 * (K + 1), hipMemcpyHostToDevice, s));
   const Elem* m = b.samp.as<Elem>();
-  std::vector<DeviceBuffer> pass_tabs;
   if (ns > 0) {
     launch_gk_sample(in, d_off, d_soff, K, step, ns, b.samp.as<Elem>(), s);
     bool done = false;
@@ -94,16 +121,7 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
     if (!done) {
       Elem* sbuf[2] = {b.sa.as<Elem>(), b.sb.as<Elem>()};
       int w = 0;
-      for (const MergePassPlan& mp : plan_merge_passes(soff, {0, K}, kGenericMergeTile)) {
-        std::vector<int64_t> tab(mp.pairs);
-        tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
-        pass_tabs.emplace_back(tab.size() * 8);
-        HIP_CHECK(hipMemcpyAsync(pass_tabs.back().as(), tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
-        PassDesc pd;
-        pd.pairs = pass_tabs.back().as<int64_t>();
-        pd.tile_prefix = pass_tabs.back().as<int64_t>() + mp.pairs.size();
-        pd.npairs = mp.npairs;
-        pd.ntiles = mp.ntiles;
+      for (const PassDesc& pd : upload_passes(plan_merge_passes(soff, {0, K}, kGenericMergeTile), b.passtab, s)) {
         launch_merge_partition_generic(m, pd, splits_.as<int64_t>(), ctx, s);
         launch_merge_pass_generic(m, sbuf[w], pd, splits_.as<int64_t>(), ctx, s);
         m = sbuf[w];
@@ -291,19 +309,6 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
   phase("f2_normalize");
   // ---- F3: single-pass K-way merge (generic_kway.hip) when K allows, else the pairwise tree;
   // per-pass descriptors are small host tables uploaded per pass
-  std::vector<DeviceBuffer> pass_tabs;
-  auto upload_pass = [&](const MergePassPlan& mp) {
-    std::vector<int64_t> tab(mp.pairs);
-    tab.insert(tab.end(), mp.tile_prefix.begin(), mp.tile_prefix.end());
-    pass_tabs.emplace_back(tab.size() * 8);
-    HIP_CHECK(hipMemcpyAsync(pass_tabs.back().as(), tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
-    PassDesc pd;
-    pd.pairs = pass_tabs.back().as<int64_t>();
-    pd.tile_prefix = pass_tabs.back().as<int64_t>() + mp.pairs.size();
-    pd.npairs = mp.npairs;
-    pd.ntiles = mp.ntiles;
-    return pd;
-  };
   const char* gk_env = std::getenv("UDA_GKWAY");  // 0: pairwise tree only (A/B and tests)
   const bool gk_on = !(gk_env && *gk_env && std::atoi(gk_env) == 0);
   const bool gk = gk_on && K >= 2 && K <= kGkMaxRuns;
@@ -407,9 +412,9 @@ GenericMergeResult GenericMerger::merge(const std::vector<const uint8_t*>& runs,
         UDA_LOG(kWarn, "generic k-way: a cell above capacity, falling back to the pairwise merge");
       }
     }
-    for (const MergePassPlan& mp : merged ? std::vector<MergePassPlan>{}
-                                          : plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile)) {
-      const PassDesc pd = upload_pass(mp);
+    for (const PassDesc& pd : merged ? std::vector<PassDesc>{}
+                                     : upload_passes(plan_merge_passes(eoff, {0, (int)eoff.size() - 1}, kGenericMergeTile),
+                                                     passtab_, s)) {
       launch_merge_partition_generic(cur, pd, splits_.as<int64_t>(), ctx, s);
       launch_merge_pass_generic(cur, nxt, pd, splits_.as<int64_t>(), ctx, s);
       std::swap(cur, nxt);

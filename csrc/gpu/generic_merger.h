@@ -48,14 +48,14 @@ class GenericMerger {
  private:
   int f1_serial_runs_ = 0;
   void reserve(int64_t records, int runs);
-  DeviceBuffer eoff_, rounds_;
+  DeviceBuffer eoff_, rounds_, passtab_;  // passtab_: pairwise-tree pass tables (no hipMalloc/hipFree per merge)
   PinnedBuffer cuts_host_;
   std::vector<hipEvent_t> round_ev_;
   DeviceBuffer elems_a_, elems_b_, splits_, sizes_, out_off_, scan_tmp_, cuts_, offsets_, tables_, side_, ck_, f1ws_;
   // single-pass K-way (generic_kway.hip), per recursion level: sample offsets, per-run samples,
   // merged samples (ping-pong), splitters, per-run cell splits, sample histogram, overflow flag
   struct KwayBuffers {
-    DeviceBuffer tab, samp, sa, sb, bounds, split, hist, flag;
+    DeviceBuffer tab, samp, sa, sb, bounds, split, hist, flag, passtab;
   };
   std::vector<KwayBuffers> gk_;
   static constexpr int64_t kGkRecurseSamples = 1 << 18;  // larger samples are merged by a K-way level

@@ -48,7 +48,7 @@ def summarize(ev):
     fp = [e for e in ev if e[0] == "fetch_phase"][-1]
     out = {"task_ms": round((task[5] - task[4]) / 1e6, 1), "fetch_ms": round((fp[5] - fp[4]) / 1e6, 1)}
     for kind in ("fetch_req", "serve_copy", "drain", "index", "dm_h2d", "dm_merge", "rpq_deliver", "stage_wait", "lpq_flush", "lpq_merge", "lpq_d2h", "pinned_alloc",
-                 "device_alloc", "device_free"):
+                 "pinned_buf_alloc", "device_alloc", "device_free"):
         d = [(e[5] - e[4]) / 1e6 for e in ev if e[0] == kind]
         out[kind] = {"n": len(d), "p50_ms": pct(d, 0.5), "p90_ms": pct(d, 0.9), "max_ms": max(d) if d else None}
     sc = [e for e in ev if e[0] == "serve_copy"]
@@ -73,7 +73,7 @@ def summarize(ev):
                 t = nxt
         out["landed_mb_per_5ms"] = [round(x) for x in landed]
         out["memcpys_in_flight_per_5ms"] = [round(x, 1) for x in busy]
-    for kind in ("index", "dm_h2d", "dm_merge", "rpq_deliver", "lpq_flush", "lpq_merge", "lpq_d2h", "pinned_alloc", "device_alloc", "device_free"):  # spans vs task start
+    for kind in ("index", "dm_h2d", "dm_merge", "rpq_deliver", "lpq_flush", "lpq_merge", "lpq_d2h", "pinned_alloc", "pinned_buf_alloc", "device_alloc", "device_free"):  # spans vs task start
         sp = [e for e in ev if e[0] == kind]
         if sp:
             out[kind]["sum_ms"] = round(sum(e[5] - e[4] for e in sp) / 1e6, 1)
