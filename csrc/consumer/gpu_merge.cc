@@ -1052,7 +1052,8 @@ void ReduceTask::merge_gpu() {
     std::atomic<size_t> nk{0};
     std::vector<std::exception_ptr> errs(n);
     std::vector<std::thread> ts;
-    const size_t nt = std::min<size_t>(n, (size_t)std::max<int64_t>(1, drains > 0 ? drains : 8));
+    // half the drain threads: this runs beside them (and the provider's) under the task's CPU share
+    const size_t nt = std::min<size_t>(n, (size_t)std::max<int64_t>(1, (drains > 0 ? drains : 8) / 2));
     for (size_t w = 0; w < nt; ++w)
       ts.emplace_back([&] {
         for (size_t k; (k = nk++) < n;) try {
