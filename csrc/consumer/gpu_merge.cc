@@ -726,7 +726,68 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
 
 }  // namespace
 
+// Every reduce task of a Hadoop job usually runs in a fresh JVM (YarnChild), so what a warm process
+// keeps in its pools (HIP context, code objects, pinned rings and arenas, workspaces) a task would build
+// on its critical path: a 2 GB task went 27 -> 3.9 GB/s cold (profiles/r3_netmerger2.json). INIT comes
+// while most maps still run (reduce slow-start), so the task builds them then. Best effort: any failure
+// leaves the merge to build what it needs as before.
+void ReduceTask::prewarm_gpu() {
+  const auto t0 = std::chrono::steady_clock::now();
+  try {
+    if (gpu::device_count() <= 0) return;
+    const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+    if (hipSetDevice(device) != hipSuccess) return;
+    try {
+      (void)gpu::SdmaEngine::for_device(device);
+    } catch (const std::exception&) {
+    }
+    // once per process: the context and the library's code objects (loaded at the first kernel
+    // launch); later prewarms must not hipFree (it synchronizes the device under running tasks)
+    static std::once_flag code_once;
+    std::call_once(code_once, [] {
+      gpu::DeviceBuffer tmp(64);
+      HIP_CHECK(hipMemsetAsync(tmp.as(), 0, 64, nullptr));
+      gpu::launch_max_i32(tmp.as<int32_t>(), 1, reinterpret_cast<unsigned int*>(tmp.as<uint8_t>() + 32), nullptr);
+      HIP_CHECK(hipStreamSynchronize(nullptr));
+    });
+    // a workspace with its pinned D2H ring (NUMA-local), and an early stager, into the device pools
+    {
+      PoolLease<DeviceWorkspace> wl{device, DevicePool<DeviceWorkspace>::get().acquire(
+                                                device, [] { return std::make_unique<DeviceWorkspace>(); })};
+      if (wl.obj->ring.size() < (size_t)(2 * kPieceBytes))
+        wl.obj->ring.alloc_on_node((size_t)(2 * kPieceBytes), gpu::device_numa_node(device));
+      wl.clean = true;
+    }
+    if (host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0) {
+      PoolLease<EarlyStager> sl{device, DevicePool<EarlyStager>::get().acquire(
+                                            device, [device] { return std::make_unique<EarlyStager>(device); })};
+      sl.clean = true;
+    }
+    // pinned blocks for the fetch arena, kept in the pool's cache for this task's partitions (not for
+    // tasks that only fetch device descriptors)
+    const bool staged = host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device";
+    const int64_t pin = staged ? host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 256) << 20 : 0;
+    std::vector<gpu::PinnedPool::Block> blocks;
+    for (int64_t b = 0; b < pin && !stop_; b += (int64_t)gpu::PinnedArena::kBlock)
+      blocks.push_back(gpu::PinnedPool::instance().acquire(gpu::PinnedArena::kBlock));
+    for (auto& b : blocks) gpu::PinnedPool::instance().release(b);
+  } catch (const std::exception& e) {
+    UDA_LOG(kWarn, "GPU prewarm: %s", e.what());
+  }
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.gpu_prewarm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void ReduceTask::join_prewarm() {
+  if (!prewarm_thr_.joinable()) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  prewarm_thr_.join();
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.gpu_prewarm_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 void ReduceTask::merge_gpu() {
+  join_prewarm();
   if (gpu::device_count() <= 0) throw UdaError("mapred.uda.merge.backend=gpu but no HIP device is visible");
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -1641,6 +1702,7 @@ void ReduceTask::merge_gpu() {
 // Reference: start_fetch_req / RDMA WRITE into the reducer buffer (src/DataNet/RDMAClient.cc:559-600,
 // src/DataNet/RDMAServer.cc:537-631) and merge_online (src/Merger/MergeManager.cc:184-193).
 bool ReduceTask::merge_gpu_device(bool probe) {
+  join_prewarm();
   if (gpu::device_count() <= 0) throw UdaError("mapred.uda.merge.backend=gpu but no HIP device is visible");
   auto t0 = std::chrono::steady_clock::now();
   const int maps = init_.num_maps;

@@ -398,6 +398,8 @@ void ReduceTask::on_init(const InitParams& p) {
   // CPU: the hybrid (approach 2) LPQ files; GPU: the disk-tier LPQ spills of the GPU hybrid merge
   checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && (backend_ == "gpu" || net_.online == 2);
   if (checkpoint_) load_checkpoint();
+  if (backend_ == "gpu" && host_->conf_i64("mapred.uda.gpu.prewarm", 1) != 0)
+    prewarm_thr_ = std::thread([this] { prewarm_gpu(); });
   merge_thr_ = std::thread([this] { merge_main(); });
 }
 
@@ -507,6 +509,7 @@ void ReduceTask::exit() {
   stop_ = true;
   cv_.notify_all();
   if (merge_thr_.joinable()) merge_thr_.join();
+  if (prewarm_thr_.joinable()) prewarm_thr_.join();
   if (transport_) transport_->close();
   // completions of requests still in flight (a provider worker may be serving one) touch this task
   std::unique_lock<std::mutex> lk(inflight_mu_);
@@ -810,7 +813,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"hybrid_direct\":" << s.hybrid_direct << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
-    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
     << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"merge_path\":\"" << s.merge_path << "\""

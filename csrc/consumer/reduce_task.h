@@ -54,6 +54,8 @@ struct ReduceStats {
   double gpu_h2d_ms = 0, gpu_device_ms = 0, gpu_d2h_wait_ms = 0, gpu_sink_ms = 0;
   double gpu_decode_ms = 0;  // device fetch, compressed partitions: framing walk + F6 decode (stream synced)
   double gpu_gate_wait_ms = 0;  // waiting for a GPU merge slot (mapred.uda.gpu.max.concurrent.merges)
+  double gpu_prewarm_ms = -1;   // INIT-time GPU prewarm (mapred.uda.gpu.prewarm); -1: not run
+  double gpu_prewarm_wait_ms = 0;  // the merge waiting for the prewarm to finish
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
   int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;
   int64_t restored_lpqs = 0, restored_maps = 0;  // hybrid resume from an LPQ checkpoint
@@ -98,6 +100,11 @@ class ReduceTask {
   // Device fetch (descriptors, merge in place). probe: return false before consuming anything if the
   // first MOFs are not device-resident (the caller then runs merge_gpu()).
   bool merge_gpu_device(bool probe);
+  // GPU backend: started at INIT on prewarm_thr_ (mapred.uda.gpu.prewarm): HIP context, SDMA engine,
+  // code objects, a pooled workspace with its pinned D2H ring and early stager, pinned fetch-arena
+  // blocks, all while the FETCHes are still to come (reduce slow-start). The merge joins it first.
+  void prewarm_gpu();
+  void join_prewarm();
   // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
   void fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids = nullptr);
   // LPQ checkpoint (mapred.uda.lpq.checkpoint): completed LPQ spill files survive a failed attempt,
@@ -140,6 +147,7 @@ class ReduceTask {
   std::atomic<bool> exiting_{false};  // exit() from the host (not a failure)
   std::atomic<bool> finished_{false};
   std::thread merge_thr_;
+  std::thread prewarm_thr_;
   bool inited_ = false;
   int next_index_ = 0;
 
