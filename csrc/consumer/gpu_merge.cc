@@ -34,6 +34,7 @@
 #include <fstream>
 #include <future>
 #include <random>
+#include <set>
 #include <thread>
 
 #include "../gpu/block_decoder.h"
@@ -90,6 +91,9 @@ struct DeviceWorkspace {
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
+  // D2H link gate of this task's deliveries (see D2HLinkGate); slots 0: ungated
+  int gate_device = 0, gate_slots = 0;
+  int64_t gate_left = 0;  // bytes this task still has to deliver (its priority)
   ~DeviceWorkspace() {
     if (h2d_sig.handle) {
       try {
@@ -102,7 +106,15 @@ struct DeviceWorkspace {
       if (e) (void)hipEventDestroy(e);
     if (cs) (void)hipStreamDestroy(cs);
   }
-  void reset_stats() { h2d_ms = device_ms = d2h_ms = sink_ms = 0; }
+  void reset_stats() {
+    h2d_ms = device_ms = d2h_ms = sink_ms = 0;
+    gate_slots = 0;
+  }
+  void gate(int device, int slots, int64_t left) {
+    gate_device = device;
+    gate_slots = slots;
+    gate_left = left;
+  }
   // D2H stream of streamed deliveries (the merge stream is busy with the next round)
   hipStream_t copy_stream() {
     if (!cs) HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
@@ -589,6 +601,46 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   return res;
 }
 
+// D2H pieces in flight per device (mapred.uda.gpu.d2h.slots). Concurrent copies share the PCIe link
+// about evenly, so with every task's delivery in flight at once the task with the most to deliver (a
+// skewed reducer, whose single consumer thread bounds the job) gets 1/16 of the link and its consumer
+// starves while the small tasks finish. With a few slots, a free slot goes to the waiting task with the
+// most bytes left (longest delivery first): that task streams at its consumer's rate from the start
+// and the others share the rest of the link.
+constexpr int kD2HSlotsDefault = 2;
+
+class D2HLinkGate {
+ public:
+  static D2HLinkGate& get() {
+    static D2HLinkGate* g = new D2HLinkGate;  // never destroyed: tasks may outlive static teardown
+    return *g;
+  }
+  void acquire(int device, int slots, int64_t left) {
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev& d = devs_[device];
+    const auto me = d.waiting.emplace(-left, d.next++).first;  // ordered: most bytes left first, then FIFO
+    cv_.wait(lk, [&] { return d.used < slots && d.waiting.begin() == me; });
+    d.waiting.erase(me);
+    ++d.used;
+    cv_.notify_all();
+  }
+  void release(int device) {
+    std::lock_guard<std::mutex> g(mu_);
+    --devs_[device].used;
+    cv_.notify_all();
+  }
+
+ private:
+  struct Dev {
+    int used = 0;
+    uint64_t next = 0;
+    std::set<std::pair<int64_t, uint64_t>> waiting;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int, Dev> devs_;
+};
+
 // Stream the merged output of `m` (in ws.out) to the host in pieces of up to kPieceBytes that end on
 // record boundaries (the cuts), double-buffered through pinned memory: the D2H of piece k+1 runs
 // while fn(piece k) consumes it. fn(ptr, first_cut, last_cut) gets the bytes of cuts
@@ -649,10 +701,27 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
     }
     if (sp.eng) HIP_CHECK(hipStreamSynchronize(s));
   }
+  // gated deliveries hold a slot from the piece's enqueue until its copy has landed
+  struct GateHold {
+    DeviceWorkspace& w;
+    bool held = false;
+    void take() {
+      if (w.gate_slots > 0) {
+        D2HLinkGate::get().acquire(w.gate_device, w.gate_slots, w.gate_left);
+        held = true;
+      }
+    }
+    void drop() {
+      if (held) D2HLinkGate::get().release(w.gate_device);
+      held = false;
+    }
+    ~GateHold() { drop(); }
+  } gh{ws};
   auto enqueue = [&](size_t piece) {
     const int slot = (int)(piece & 1);
     const int64_t b = m.cuts[pb[piece]], e = m.cuts[pb[piece + 1]];
     if (e - b > kPieceBytes) throw UdaError("record larger than the D2H piece");
+    gh.take();
     if (sp.eng) {
       gpu::SdmaEngine::arm(sp.sig[slot], sp.eng->parts((size_t)(e - b), 1));
       sp.eng->copy_d2h(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b), sp.sig[slot], 1);
@@ -671,6 +740,8 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
       gpu::SdmaEngine::wait(sp.sig[slot]);
     else
       HIP_CHECK(hipEventSynchronize(ws.piece_ev[slot]));
+    gh.drop();
+    ws.gate_left -= m.cuts[pb[piece + 1]] - m.cuts[pb[piece]];
     auto t1 = std::chrono::steady_clock::now();
     ws.d2h_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (piece + 1 < np) enqueue(piece + 1);
@@ -1406,6 +1477,13 @@ void ReduceTask::merge_gpu() {
       st_.records += m.records;
     };
     const int64_t kv = kv_buf_size_ - kEofBytes;
+    const int d2h_slots = (int)host_->conf_i64("mapred.uda.gpu.d2h.slots", kD2HSlotsDefault);
+    int64_t task_bytes = 0;
+    for (const Span& sp : group) task_bytes += sp.len;
+    if (prog)
+      for (int64_t c : prog->cap) task_bytes += c;
+    for (const SpillRun& r : spills) task_bytes += r.bytes;
+    ws.gate(device, d2h_slots, task_bytes);
 
     lpq_wait();  // an LPQ of the fetch phase may still be merging
     double prog_fetch_ms = -1;
@@ -1614,12 +1692,14 @@ void ReduceTask::merge_gpu() {
       ws2_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
       ws2 = ws2_lease.obj.get();
       ws2->reset_stats();
+      ws2->gate(device, d2h_slots, task_bytes);
       // Three workspaces, two rounds prepared ahead: round q + 2's slices cross PCIe (SDMA H2D) while
       // round q + 1 merges and round q is delivered (D2H), so the rounds cost max(H2D, merge, D2H)
       // each instead of H2D + merge.
       ws3_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
       ws3 = ws3_lease.obj.get();
       ws3->reset_stats();
+      ws3->gate(device, d2h_slots, task_bytes);
       StreamGuard sg2, sg3;
       HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
       HIP_CHECK(hipStreamCreateWithFlags(&sg3.s, hipStreamNonBlocking));
@@ -1992,6 +2072,11 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     s = sg.s;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
+  {
+    int64_t left = 0;
+    for (int64_t l : rlen) left += l;
+    ws.gate(device, (int)host_->conf_i64("mapred.uda.gpu.d2h.slots", kD2HSlotsDefault), left);
+  }
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
   // dataFromUda): the consumer's work (the reduce task's bound when one task holds most of the data)
   // never waits for the merge driver, and the merge reuses an output only after its delivery.
