@@ -440,6 +440,9 @@ class DeviceGate {
     --devs_[device].used;
     cv_.notify_all();
   }
+  // host function enqueued behind a gated copy: frees the slot the moment the copy has landed (not when
+  // the task comes back for it after consuming the previous piece)
+  static void release_cb(void* device) { get().release((int)(intptr_t)device); }
 
  private:
   struct Dev {
@@ -607,7 +610,9 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
 // starves while the small tasks finish. With a few slots, a free slot goes to the waiting task with the
 // most bytes left (longest delivery first): that task streams at its consumer's rate from the start
 // and the others share the rest of the link.
-constexpr int kD2HSlotsDefault = 2;
+// off by default: with the slot freed as the copy lands, config #5 gained 4 % and 16 uniform staged tasks
+// lost 3 % (both within box noise; profiles/r3_d2h_gate_ab.md)
+constexpr int kD2HSlotsDefault = 0;
 
 class D2HLinkGate {
  public:
@@ -629,6 +634,9 @@ class D2HLinkGate {
     --devs_[device].used;
     cv_.notify_all();
   }
+  // host function enqueued behind a gated copy: frees the slot the moment the copy has landed (not when
+  // the task comes back for it after consuming the previous piece)
+  static void release_cb(void* device) { get().release((int)(intptr_t)device); }
 
  private:
   struct Dev {
@@ -730,6 +738,10 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
     HIP_CHECK(hipMemcpyAsync(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(ws.piece_ev[slot], s));
+    if (gh.held) {
+      HIP_CHECK(hipLaunchHostFunc(s, &D2HLinkGate::release_cb, (void*)(intptr_t)ws.gate_device));
+      gh.held = false;  // the stream releases it
+    }
   };
   const size_t np = pb.size() - 1;
   enqueue(0);
@@ -837,7 +849,7 @@ void ReduceTask::prewarm_gpu() {
     // pinned blocks for the fetch arena, kept in the pool's cache for this task's partitions (not for
     // tasks that only fetch device descriptors)
     const bool staged = host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device";
-    const int64_t pin = staged ? host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 256) << 20 : 0;
+    const int64_t pin = staged ? host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 1024) << 20 : 0;
     std::vector<gpu::PinnedPool::Block> blocks;
     for (int64_t b = 0; b < pin && !stop_; b += (int64_t)gpu::PinnedArena::kBlock)
       blocks.push_back(gpu::PinnedPool::instance().acquire(gpu::PinnedArena::kBlock));

@@ -44,12 +44,19 @@ def child(args) -> int:
     st = c.close()
     prov.close()
     assert st["bytes_delivered"] - 2 == total, (st["bytes_delivered"], total)
+    trace = {}
+    tr = os.environ.get("UDA_HOST_TRACE")
+    if tr and os.path.exists(tr):  # host-event breakdown of the task (tools/netmerger_trace.py)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import netmerger_trace
+        trace = netmerger_trace.summarize(netmerger_trace.load(tr))
+        os.unlink(tr)
     print(json.dumps({"prewarm": args.prewarm, "gap_s": args.gap, "gb": round(total / 1e9, 3),
                       "gbps": round(total / wall / 1e9, 2), "wall_ms": round(wall * 1e3, 1),
                       "fetch_ms": round(st["fetch_ms"], 1), "merge_ms": round(st["merge_ms"], 1),
                       "prewarm_ms": round(st.get("gpu_prewarm_ms", -1), 1),
                       "prewarm_wait_ms": round(st.get("gpu_prewarm_wait_ms", 0), 1),
-                      "merge_path": st.get("merge_path")}), flush=True)
+                      "merge_path": st.get("merge_path"), **({"trace": trace} if trace else {})}), flush=True)
     return 0
 
 
