@@ -71,9 +71,7 @@ void DeviceBuffer::reset() {
   size_ = 0;
 }
 
-PinnedBuffer::~PinnedBuffer() {
-  if (ptr_) (void)hipHostFree(ptr_);
-}
+PinnedBuffer::~PinnedBuffer() { pinned_host_free(ptr_); }
 PinnedPool& PinnedPool::instance() {
   static PinnedPool* pool = new PinnedPool();  // leaked on purpose: outlives every user at exit
   return *pool;
@@ -97,9 +95,9 @@ PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
   b.size = (min_bytes + gran - 1) & ~(gran - 1);
   void* p = nullptr;
   const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
-  const hipError_t he = hipHostMalloc(&p, b.size, hipHostMallocDefault);
-  if (tt) trace::host_event("pinned_alloc", (int64_t)b.size, (int64_t)min_bytes, tt, trace::now_ns());
-  if (he != hipSuccess) {
+  try {
+    p = pinned_host_alloc(b.size);
+  } catch (const std::exception&) {
     // trim the cache and retry once
     std::multimap<size_t, uint8_t*> drop;
     {
@@ -107,10 +105,14 @@ PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
       drop.swap(free_);
       cached_ = 0;
     }
-    for (auto& kv : drop) (void)hipHostFree(kv.second);
-    if (hipHostMalloc(&p, b.size, hipHostMallocDefault) != hipSuccess)
+    for (auto& kv : drop) pinned_host_free(kv.second);
+    try {
+      p = pinned_host_alloc(b.size);
+    } catch (const std::exception&) {
       throw std::runtime_error("pinned host allocation of " + std::to_string(b.size) + " bytes failed");
+    }
   }
+  if (tt) trace::host_event("pinned_alloc", (int64_t)b.size, (int64_t)min_bytes, tt, trace::now_ns());
   b.p = static_cast<uint8_t*>(p);
   return b;
 }
@@ -119,7 +121,7 @@ void PinnedPool::release(Block b) {
   if (!b.p) return;
   std::lock_guard<std::mutex> g(mu_);
   if (cached_ + b.size > cap_) {
-    (void)hipHostFree(b.p);
+    pinned_host_free(b.p);
     return;
   }
   free_.emplace(b.size, b.p);
@@ -168,23 +170,23 @@ void PinnedArena::release_all() {
 }
 
 void PinnedBuffer::alloc(size_t bytes) {
-  if (ptr_) (void)hipHostFree(ptr_);
+  pinned_host_free(ptr_);
   ptr_ = nullptr;
   size_ = 0;
   if (bytes == 0) return;
   const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
-  HIP_CHECK(hipHostMalloc(&ptr_, bytes, hipHostMallocDefault));
+  ptr_ = pinned_host_alloc(bytes);
   if (tt) trace::host_event("pinned_buf_alloc", (int64_t)bytes, -1, tt, trace::now_ns());
   size_ = bytes;
 }
 
 void PinnedBuffer::alloc_on_node(size_t bytes, int node) {
-  if (ptr_) (void)hipHostFree(ptr_);
+  pinned_host_free(ptr_);
   ptr_ = nullptr;
   size_ = 0;
   if (bytes == 0) return;
   const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
-  ptr_ = hip_host_alloc_on_node(bytes, node);  // hipHostMalloc under a preferred-node policy
+  ptr_ = pinned_host_alloc(bytes, node);  // preferred-node pages, registered (sdma.h)
   if (tt) trace::host_event("pinned_buf_alloc", (int64_t)bytes, node, tt, trace::now_ns());
   size_ = bytes;
 }
@@ -613,7 +615,7 @@ ShuffleJob::~ShuffleJob() {
   for (auto e : comm_ev_) (void)hipEventDestroy(e);
   for (auto e : sent_ev_) (void)hipEventDestroy(e);
   for (auto e : piece_ev_) (void)hipEventDestroy(e);
-  if (!sdma_ && ring_) (void)hipHostFree(ring_);
+  if (!sdma_ && ring_) pinned_host_free(ring_);
   if (sdma_) {
     for (auto sg : piece_sig_) sdma_->destroy_signal(sg);
     sdma_->free_host(ring_);

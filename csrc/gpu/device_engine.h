@@ -84,7 +84,7 @@ class DeviceBuffer {
   size_t size_ = 0;
 };
 
-// Owning pinned host allocation (hipHostMalloc).
+// Owning pinned host allocation (pinned_host_alloc).
 class PinnedBuffer {
  public:
   PinnedBuffer() = default;
@@ -109,7 +109,7 @@ class PinnedBuffer {
   size_t size_ = 0;
 };
 
-// Process-wide cache of pinned host blocks (hipHostMalloc). The GPU consumer stages fetched
+// Process-wide cache of pinned host blocks (pinned_host_alloc). The GPU consumer stages fetched
 // partitions and spill slices in them: page-locking / page-faulting and unmapping GBs per reduce
 // task costs more than the merge itself, and a pinned source turns H2D into a direct DMA.
 class PinnedPool {

@@ -53,7 +53,7 @@ DiskStore::~DiskStore() {
     if (pending_[i]) (void)hipEventSynchronize(ev_[i]);
     (void)hipEventDestroy(ev_[i]);
   }
-  if (ring_) (void)hipHostFree(ring_);
+  if (ring_) pinned_host_free(ring_);
   for (size_t f = 0; f < fds_.size(); ++f) {
     if (fds_[f] >= 0) ::close(fds_[f]);
     ::unlink(paths_[f].c_str());

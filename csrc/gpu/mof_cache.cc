@@ -46,7 +46,7 @@ MofCache::~MofCache() {
   for (auto e : ev_) (void)hipEventDestroy(e);
   for (auto s : streams_)
     if (s) (void)hipStreamDestroy(s);
-  if (ring_) (void)hipHostFree(ring_);
+  if (ring_) pinned_host_free(ring_);
 }
 
 void MofCache::free_entry(Entry* e) {

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -13,6 +14,10 @@
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
 
 #include "uda/log.h"
 
@@ -138,7 +143,14 @@ void bind_thread_to_numa(int node) {
   if (n > 0) (void)sched_setaffinity(0, sizeof(want), &want);
 }
 
-void* hip_host_alloc_on_node(size_t bytes, int node) {
+namespace {
+std::mutex g_pin_mu;
+std::unordered_map<void*, std::pair<void*, size_t>>& pinned_maps() {  // aligned ptr -> (mapping, length)
+  static auto* m = new std::unordered_map<void*, std::pair<void*, size_t>>();
+  return *m;
+}
+
+void* hip_host_malloc_on_node(size_t bytes, int node) {
   void* p = nullptr;
   if (node < 0 || node >= 64) {
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) throw std::runtime_error("hipHostMalloc failed");
@@ -152,6 +164,83 @@ void* hip_host_alloc_on_node(size_t bytes, int node) {
   if (e != hipSuccess) throw std::runtime_error("hipHostMalloc (NUMA node " + std::to_string(node) + ") failed");
   return p;
 }
+
+// mmap + hugepage advice + parallel first touch + hipHostRegister; nullptr if any step fails
+void* register_fresh_pages(size_t bytes, int node) {
+  constexpr size_t kHuge = (size_t)2 << 20;
+  const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+  const size_t maplen = len + kHuge;  // room to align the start to a huge page
+  void* m = mmap(nullptr, maplen, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return nullptr;
+  uint8_t* a = reinterpret_cast<uint8_t*>(((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+  (void)madvise(a, len, MADV_HUGEPAGE);
+  (void)madvise(m, maplen, MADV_DONTFORK);  // a forked child must not copy (or share) pinned pages
+  if (node >= 0 && node < 64) {
+    const unsigned long mask = 1ul << node;
+    constexpr int kMpolPreferred = 1;
+    (void)syscall(SYS_mbind, a, len, kMpolPreferred, &mask, sizeof(mask) * 8, 0);
+  }
+  // first touch: the kernel zeroes the pages in the touching threads, not inside the registration
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>(8, len / ((size_t)32 << 20)));
+  const size_t per = (len / nt + kHuge - 1) & ~(kHuge - 1);
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nt; ++t)
+    ts.emplace_back([=] {
+      const size_t b = (size_t)t * per;
+      if (b >= len) return;
+      const size_t n = std::min(per, len - b);
+      for (size_t o = 0; o < n; o += 4096) a[b + o] = 0;
+    });
+  for (auto& t : ts) t.join();
+  if (hipHostRegister(a, len, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(m, maplen);
+    return nullptr;
+  }
+  void* d = nullptr;  // copies and kernels use the host address: it must be the device address too
+  if (hipHostGetDevicePointer(&d, a, 0) != hipSuccess || d != a) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(a);
+    munmap(m, maplen);
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(g_pin_mu);
+  pinned_maps()[a] = {m, maplen};
+  return a;
+}
+}  // namespace
+
+void* pinned_host_alloc(size_t bytes, int node) {
+  static const bool reg = [] {
+    const char* e = std::getenv("UDA_PINNED_REGISTER");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (bytes == 0) bytes = 1;
+  if (reg)
+    if (void* p = register_fresh_pages(bytes, node)) return p;
+  return hip_host_malloc_on_node(bytes, node);
+}
+
+void pinned_host_free(void* p) {
+  if (!p) return;
+  std::pair<void*, size_t> m{nullptr, 0};
+  {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = pinned_maps().find(p);
+    if (it != pinned_maps().end()) {
+      m = it->second;
+      pinned_maps().erase(it);
+    }
+  }
+  if (m.first) {
+    (void)hipHostUnregister(p);
+    munmap(m.first, m.second);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
+void* hip_host_alloc_on_node(size_t bytes, int node) { return pinned_host_alloc(bytes, node); }
 
 std::string numa_residency(const void* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);

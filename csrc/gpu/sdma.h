@@ -81,8 +81,15 @@ class SdmaEngine {
 // CPUs of that node (no-op when unknown). Used for the delivery/consumer threads.
 int device_numa_node(int device);
 void bind_thread_to_numa(int node);
-// Pinned host allocation placed on NUMA node `node` (hipHostMalloc under a preferred-node memory
-// policy, hipHostMallocNumaUser); plain hipHostMalloc when node < 0. Free with hipHostFree.
+// Pinned host memory, preferably on NUMA node `node` (< 0: anywhere). Pages are created by the
+// caller's threads, not under the runtime's registration: mmap, MADV_HUGEPAGE, first touch from up to
+// 8 threads, then hipHostRegister (8 x 256 MiB: ~30 ms, against ~400 ms of hipHostMalloc, which zeroes
+// and pins 4 KiB pages one allocation at a time; tools/probes/pinned_alloc_probe.cc). Falls back to
+// hipHostMalloc (UDA_PINNED_REGISTER=0, or if the registered range is not mapped at the same device
+// address). Free with pinned_host_free.
+void* pinned_host_alloc(size_t bytes, int node = -1);
+void pinned_host_free(void* p);
+// The same, kept for its callers (placement on `node`).
 void* hip_host_alloc_on_node(size_t bytes, int node);
 // Where the pages of the mapping containing `p` live, from /proc/self/numa_maps: "N1=100%" style
 // summary (or "unknown").
