@@ -828,10 +828,12 @@ void ReduceTask::prewarm_gpu() {
     // launch); later prewarms must not hipFree (it synchronizes the device under running tasks)
     static std::once_flag code_once;
     std::call_once(code_once, [] {
-      gpu::DeviceBuffer tmp(64);
-      HIP_CHECK(hipMemsetAsync(tmp.as(), 0, 64, nullptr));
-      gpu::launch_max_i32(tmp.as<int32_t>(), 1, reinterpret_cast<unsigned int*>(tmp.as<uint8_t>() + 32), nullptr);
+      uint8_t* tmp = nullptr;  // raw hipMalloc: the prewarm is not the merge (fault injection hits the merge)
+      HIP_CHECK(hipMalloc(&tmp, 64));
+      HIP_CHECK(hipMemsetAsync(tmp, 0, 64, nullptr));
+      gpu::launch_max_i32(reinterpret_cast<int32_t*>(tmp), 1, reinterpret_cast<unsigned int*>(tmp + 32), nullptr);
       HIP_CHECK(hipStreamSynchronize(nullptr));
+      HIP_CHECK(hipFree(tmp));
     });
     // a workspace with its pinned D2H ring (NUMA-local), and an early stager, into the device pools
     {

@@ -318,7 +318,7 @@ def test_consumer_gpu_device_alloc_fault_fails_once(require_gpu, tmp_path, monke
             ids.append(mid)
         monkeypatch.setenv("UDA_FAULT_DEVICE_ALLOC", "1")
         c = UdaConsumer(len(ids), "job_fa", "attempt_job_fa_r_000000_0", datagen.TEXT,
-                        conf={"mapred.uda.merge.backend": "gpu"})
+                        conf={"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.prewarm": 0})
         for m in ids:
             c.fetch("h", "job_fa", m, 0)
         with pytest.raises(UdaFallback, match="injected"):
