@@ -814,11 +814,11 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
 // on its critical path: a 2 GB task went 27 -> 3.9 GB/s cold (profiles/r3_netmerger2.json). INIT comes
 // while most maps still run (reduce slow-start), so the task builds them then. Best effort: any failure
 // leaves the merge to build what it needs as before.
-void ReduceTask::prewarm_gpu() {
+void ReduceTask::prewarm_gpu(PrewarmConf pc) {
   const auto t0 = std::chrono::steady_clock::now();
   try {
     if (gpu::device_count() <= 0) return;
-    const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+    const int device = pc.device;
     if (hipSetDevice(device) != hipSuccess) return;
     try {
       (void)gpu::SdmaEngine::for_device(device);
@@ -843,15 +843,14 @@ void ReduceTask::prewarm_gpu() {
         wl.obj->ring.alloc_on_node((size_t)(2 * kPieceBytes), gpu::device_numa_node(device));
       wl.clean = true;
     }
-    if (host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0) {
+    if (pc.early_h2d) {
       PoolLease<EarlyStager> sl{device, DevicePool<EarlyStager>::get().acquire(
                                             device, [device] { return std::make_unique<EarlyStager>(device); })};
       sl.clean = true;
     }
     // pinned blocks for the fetch arena, kept in the pool's cache for this task's partitions (not for
     // tasks that only fetch device descriptors)
-    const bool staged = host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device";
-    const int64_t pin = staged ? host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 1024) << 20 : 0;
+    const int64_t pin = pc.pinned_bytes;
     std::vector<gpu::PinnedPool::Block> blocks;
     for (int64_t b = 0; b < pin && !stop_; b += (int64_t)gpu::PinnedArena::kBlock)
       blocks.push_back(gpu::PinnedPool::instance().acquire(gpu::PinnedArena::kBlock));

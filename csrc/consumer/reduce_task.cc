@@ -398,8 +398,15 @@ void ReduceTask::on_init(const InitParams& p) {
   // CPU: the hybrid (approach 2) LPQ files; GPU: the disk-tier LPQ spills of the GPU hybrid merge
   checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && (backend_ == "gpu" || net_.online == 2);
   if (checkpoint_) load_checkpoint();
-  if (backend_ == "gpu" && host_->conf_i64("mapred.uda.gpu.prewarm", 1) != 0)
-    prewarm_thr_ = std::thread([this] { prewarm_gpu(); });
+  if (backend_ == "gpu" && host_->conf_i64("mapred.uda.gpu.prewarm", 1) != 0) {
+    PrewarmConf pc;
+    pc.device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+    pc.early_h2d = host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0;
+    // pinned fetch-arena blocks, not for tasks that only fetch device descriptors
+    if (host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device")
+      pc.pinned_bytes = host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 1024) << 20;
+    prewarm_thr_ = std::thread([this, pc] { prewarm_gpu(pc); });
+  }
   merge_thr_ = std::thread([this] { merge_main(); });
 }
 

@@ -103,7 +103,12 @@ class ReduceTask {
   // GPU backend: started at INIT on prewarm_thr_ (mapred.uda.gpu.prewarm): HIP context, SDMA engine,
   // code objects, a pooled workspace with its pinned D2H ring and early stager, pinned fetch-arena
   // blocks, all while the FETCHes are still to come (reduce slow-start). The merge joins it first.
-  void prewarm_gpu();
+  struct PrewarmConf {  // read on the INIT thread (the host's get_conf may be bound to it)
+    int device = 0;
+    bool early_h2d = true;
+    int64_t pinned_bytes = 0;
+  };
+  void prewarm_gpu(PrewarmConf pc);
   void join_prewarm();
   // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
   void fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids = nullptr);
