@@ -357,3 +357,39 @@ def test_generic_kway_recursive_sample_merge(require_gpu, monkeypatch, recurse):
     assert ops.last_stats["passes"] == 1
     c, _ = ops.merge_runs(runs, datagen.TEXT, "cpu")
     assert g == c
+
+
+@pytest.mark.parametrize("conf_extra", [
+    {"mapred.uda.gpu.d2h.slots": 1},                                   # every delivery piece through the gate
+    {"mapred.uda.gpu.prewarm": 1, "mapred.uda.gpu.prewarm.pinned.mb": 64},
+    {"mapred.uda.gpu.prewarm": 0, "mapred.uda.gpu.progressive.phases": 0},
+    {"mapred.uda.gpu.merge.bytes": 200_000, "mapred.uda.gpu.spill": "host", "mapred.uda.gpu.d2h.slots": 1},
+])
+def test_consumer_gpu_gate_and_prewarm(require_gpu, conf_extra):
+    """The D2H link gate (slots freed by a stream host function as each piece lands) and the INIT-time
+    prewarm change when work happens, never what is delivered: the stream equals the CPU merge's,
+    including a direct-RPQ hybrid task whose rounds all go through a one-slot gate."""
+    from uda_amd.utils.mof import encode_partitions
+    p = UdaProvider()
+    try:
+        mp = datagen.secondary_sort(num_maps=10, reducers=2, rows_per_map=1500, seed=21)
+        ids = []
+        for i, parts in enumerate(datagen.streams(mp)):
+            mid = f"attempt_g_m_{i:06d}_0"
+            data, index = encode_partitions(parts)
+            p.add_mof_memory("job_g2", mid, data, index)
+            ids.append(mid)
+        conf = {"mapred.uda.merge.backend": "gpu", **conf_extra}
+        recs_gpu, st, _ = run_reduce("h", "job_g2", ids, 0, datagen.TEXT, conf=conf, max_buf_kb=16, min_buf_kb=16,
+                                     kv_buf_size=8192)
+        recs_cpu, _, _ = run_reduce("h", "job_g2", ids, 0, datagen.TEXT, max_buf_kb=16, min_buf_kb=16,
+                                    kv_buf_size=8192)
+        assert st["backend"] == "gpu" and st["maps_fetched"] == len(ids)
+        assert [k for k, _ in recs_gpu] == [k for k, _ in recs_cpu]
+        assert sorted(recs_gpu) == sorted(recs_cpu)
+        if conf_extra.get("mapred.uda.gpu.prewarm") == 1:
+            assert st["gpu_prewarm_ms"] >= 0, st
+        if "mapred.uda.gpu.merge.bytes" in conf_extra:
+            assert st["hybrid_direct"] == 1 and st["rpq_rounds"] >= 2, st
+    finally:
+        p.close()
