@@ -827,12 +827,17 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
     // once per process: the context and the library's code objects (loaded at the first kernel
     // launch); later prewarms must not hipFree (it synchronizes the device under running tasks)
     static std::once_flag code_once;
-    std::call_once(code_once, [] {
+    std::call_once(code_once, [device] {
       uint8_t* tmp = nullptr;  // raw hipMalloc: the prewarm is not the merge (fault injection hits the merge)
-      HIP_CHECK(hipMalloc(&tmp, 64));
+      HIP_CHECK(hipMalloc(&tmp, 4096));
       HIP_CHECK(hipMemsetAsync(tmp, 0, 64, nullptr));
       gpu::launch_max_i32(reinterpret_cast<int32_t*>(tmp), 1, reinterpret_cast<unsigned int*>(tmp + 32), nullptr);
       HIP_CHECK(hipStreamSynchronize(nullptr));
+      try {  // the SDMA engines' queues (staging H2D, delivery D2H)
+        gpu::SdmaEngine::for_device(device).warm(tmp);
+      } catch (const std::exception& e) {
+        UDA_LOG(kWarn, "GPU prewarm: SDMA warm-up: %s", e.what());
+      }
       HIP_CHECK(hipFree(tmp));
     });
     // a workspace with its pinned D2H ring (NUMA-local), and an early stager, into the device pools

@@ -336,6 +336,25 @@ SdmaEngine::SdmaEngine(int device) {
   UDA_LOG(kInfo, "SDMA delivery: device %d numa %d engines mask 0x%x preferred 0x%x", device, numa_node_, mask, pref);
 }
 
+void SdmaEngine::warm(void* dev_scratch) {
+  void* host = pinned_host_alloc(4096);
+  hsa_signal_t sig = make_signal();
+  try {
+    arm(sig, 1);
+    copy_h2d(dev_scratch, host, 4096, sig);
+    wait(sig);
+    arm(sig, parts(4096, 1));
+    copy_d2h(host, dev_scratch, 4096, sig, 1);
+    wait(sig);
+  } catch (...) {
+    destroy_signal(sig);
+    pinned_host_free(host);
+    throw;
+  }
+  destroy_signal(sig);
+  pinned_host_free(host);
+}
+
 SdmaEngine::~SdmaEngine() {
   if (hsa_inited_) (void)hsa_shut_down();
 }

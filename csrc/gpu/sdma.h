@@ -61,6 +61,10 @@ class SdmaEngine {
   // Block until the signal reaches 0; throws on a copy error (negative value).
   static void wait(hsa_signal_t s);
 
+  // One small copy in each direction on the engines this class uses: the runtime creates an engine's
+  // queue at its first copy (a cold reduce task's first staging copies waited ~150 ms behind it), so a
+  // prewarm can take that cost before the task's data arrives. Synchronous; `dev_scratch` >= 4 KiB.
+  void warm(void* dev_scratch);
   int numa_node() const { return numa_node_; }
   int engines() const { return (int)engine_ids_.size(); }
   std::string describe() const;
