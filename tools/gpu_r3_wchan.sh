@@ -12,6 +12,7 @@ for line in open('gpurun_out/r3_wchan.jsonl'):
     print(d['variant'], d['gbps'], 'fetch_req_max', (d.get('fetch_req') or {}).get('max_ms'), 'landed', d.get('landed_mb_per_5ms'))
     w = d.get('wchan') or {}
     print('   ', w.get('busy_waits'))
+    print('    futex', w.get('contended_futex'))
     for k in ('pinned_alloc', 'pinned_buf_alloc', 'device_alloc', 'device_free'):
         v = d.get(k) or {}
         if v.get('n'):

@@ -131,6 +131,7 @@ class WchanSampler:
     def __init__(self):
         import threading
         self.samples = []
+        self.futex = []  # (ms, thread name, futex word address)
         self.stop = threading.Event()
         self.t = threading.Thread(target=self.run, daemon=True)
 
@@ -146,6 +147,14 @@ class WchanSampler:
                     wchan = open(f"/proc/self/task/{tid}/wchan").read().strip()
                 except (OSError, ValueError):
                     continue
+                if wchan.startswith("futex"):  # which lock: the futex word's address (syscall arg 1)
+                    try:
+                        sc = open(f"/proc/self/task/{tid}/syscall").read().split()
+                        if sc and sc[0] == "202":
+                            self.futex.append((now, comm, int(sc[1], 16)))
+                    except (OSError, ValueError, IndexError):
+                        pass
+                    continue
                 if state == "R" or any(wchan.startswith(i) for i in self.IDLE):
                     continue
                 self.samples.append((now, comm, state, wchan))
@@ -154,7 +163,31 @@ class WchanSampler:
     def summary(self):
         from collections import Counter
         c = Counter((w, st) for _, _, st, w in self.samples)
+        maps = []
+        try:
+            for line in open("/proc/self/maps"):
+                f = line.split()
+                lo, hi = (int(x, 16) for x in f[0].split("-"))
+                maps.append((lo, hi, f[5] if len(f) > 5 else "[anon]"))
+        except OSError:
+            pass
+        def where(a):
+            for lo, hi, name in maps:
+                if lo <= a < hi:
+                    return f"{name}+0x{a - lo:x}"
+            return "?"
+        # futex words waited on by several threads in the same sample: contended locks
+        per_t = {}
+        for t, comm, a in self.futex:
+            per_t.setdefault((t, a), set()).add(comm)
+        contended = Counter()
+        names = {}
+        for (t, a), comms in per_t.items():
+            if len(comms) >= 3:
+                contended[a] += 1
+                names.setdefault(a, set()).update(comms)
         return {"busy_waits": [[w, st, n] for (w, st), n in c.most_common(12)],
+                "contended_futex": [[hex(a), where(a), n, sorted(names[a])[:6]] for a, n in contended.most_common(6)],
                 "first": self.samples[:20]}
 
 
