@@ -227,6 +227,8 @@ def main() -> int:
     named["whole"] = {"mapred.uda.gpu.progressive.phases": 0}
     named["hybrid"] = {"mapred.uda.gpu.merge.bytes": max(1 << 20, total // 6), "mapred.uda.gpu.spill": "host"}
     named["hybrid_lpq"] = {**named["hybrid"], "mapred.uda.gpu.hybrid.direct": 0}
+    named["whole_nopw"] = {**named["whole"], "mapred.uda.gpu.prewarm": 0}
+    named["prog4_nopw"] = {"mapred.uda.gpu.progressive.phases": 4, "mapred.uda.gpu.prewarm": 0}
     variants = [("warmup", {})] + [(f"{name}_{i}", named[name]) for i in range(args.repeat)
                                    for name in args.variants.split(",")]
     for i, (name, extra) in enumerate(variants):
@@ -253,7 +255,8 @@ def main() -> int:
                "lpqs": st.get("lpqs"), "spill_bytes": st.get("spill_bytes"),
                "phases_ms": {k: round(st["gpu_" + k + "_ms"], 1) for k in ("h2d", "device", "d2h_wait", "sink")},
                "fetch_ms_stat": round(st["fetch_ms"], 1), "merge_ms_stat": round(st["merge_ms"], 1),
-               "progressive_rounds": st.get("rpq_rounds"), "hybrid_direct": st.get("hybrid_direct")}
+               "progressive_rounds": st.get("rpq_rounds"), "hybrid_direct": st.get("hybrid_direct"),
+               "prewarm_ms": st.get("gpu_prewarm_ms"), "prewarm_wait_ms": st.get("gpu_prewarm_wait_ms")}
         thr1 = cpu_throttle()
         vm1 = vm_counters()
         if ws:
