@@ -7,13 +7,15 @@
 //
 // Hybrid (input larger than the budget, mapred.uda.gpu.merge.bytes): the reference's two-level
 // merge (merge_hybrid, src/Merger/MergeManager.cc:195-290) re-planned for a device:
-//   LPQ  MOFs are grouped as they arrive; each group is merged on the GPU and spilled to the host
-//        tier (DRAM) or to the local dirs through AsyncIO (io_uring), with a sparse index: the
-//        key at every record boundary the merge placed <= 256 KiB apart.
-//   RPQ  instead of a streaming heap over the spilled runs, the key space is cut into rounds from
-//        the sparse indices (splitters every ~budget bytes); for each round the matching byte
-//        range of every spilled run is loaded and merged on the GPU in one go. Records equal to a
-//        splitter all fall in the later round, in every run, so ties keep run order.
+//   LPQ  (disk tier, or mapred.uda.gpu.hybrid.direct=0) MOFs are grouped as they arrive; each group
+//        is merged on the GPU and spilled to the local dirs through AsyncIO (io_uring) or to DRAM,
+//        with a sparse index: the key at every record boundary the merge placed <= 256 KiB apart.
+//        DRAM tier by default: no LPQ level; the fetched partitions are the runs, indexed the same
+//        way by the drain threads (direct RPQ, see merge_gpu).
+//   RPQ  instead of a streaming heap over the runs, the key space is cut into rounds from the
+//        sparse indices (splitters every ~budget/2 bytes); for each round the matching byte range
+//        of every run is copied to HBM and merged on the GPU in one go. Records equal to a splitter
+//        all fall in the later round, in every run, so ties keep run order.
 // Reference counterpart of the online path: merge_online (MergeManager.cc:184-193).
 #include <fcntl.h>
 #include <sys/stat.h>
