@@ -758,9 +758,13 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
     ws.gate_left -= m.cuts[pb[piece + 1]] - m.cuts[pb[piece]];
     auto t1 = std::chrono::steady_clock::now();
     ws.d2h_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const int64_t tp = trace::host_enabled() ? trace::now_ns() : 0;
+    if (tp) trace::host_event("so_wait", (int64_t)(uintptr_t)&ws, 0, tp - (int64_t)(t1 - t0).count(), tp);
     if (piece + 1 < np) enqueue(piece + 1);
     fn(ws.ring.as<uint8_t>() + slot * kPieceBytes, pb[piece], pb[piece + 1]);
     ws.sink_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    if (tp) trace::host_event("so_sink", (int64_t)(uintptr_t)&ws, m.cuts[pb[piece + 1]] - m.cuts[pb[piece]], tp,
+                              trace::now_ns());
   }
 }
 
@@ -2125,11 +2129,13 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       for (;;) {
         DJob j;
         {
+          const int64_t ti = trace::host_enabled() ? trace::now_ns() : 0;
           std::unique_lock<std::mutex> lk(dmu);
           dcv.wait(lk, [&] { return dstop || !djobs.empty(); });
           if (djobs.empty()) return;
           j = std::move(djobs.front());
           djobs.pop_front();
+          if (ti) trace::host_event("gr_idle", (int64_t)(uintptr_t)&ws, 0, ti, trace::now_ns());
         }
         DeviceMergeOut m;
         m.cuts = std::move(j.cuts);
@@ -2184,9 +2190,11 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   DeviceMergeOut m;
   for (int q = 0; q < rplan.rounds; ++q) {
     {
+      const int64_t tw = trace::host_enabled() ? trace::now_ns() : 0;
       std::unique_lock<std::mutex> lk(dmu);  // outs[q & 1] held round q - 2: delivered?
       dcv.wait(lk, [&] { return delivered >= q - 1 || !derr.empty(); });
       if (!derr.empty()) throw UdaError("delivery failed: " + derr);
+      if (tw) trace::host_event("gr_slot_wait", (int64_t)(uintptr_t)&ws, q, tw, trace::now_ns());
     }
     std::vector<const uint8_t*> sp;
     std::vector<int64_t> sl;
@@ -2210,6 +2218,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
           push(DJob{dst, cuts, last_inner && last_outer, last_inner});
         });
     m.records += r.records;
+    if (trace::host_enabled())
+      trace::host_event("gr_merge", (int64_t)(uintptr_t)&ws, q,
+                        trace::now_ns() - (int64_t)(std::chrono::steady_clock::now() - tq).count(), trace::now_ns());
     static const bool trace = std::getenv("UDA_DEVICE_REDUCE_TRACE") != nullptr;  // tools: per-round lines
     if (trace)
       std::fprintf(stderr, "[generic rounds] round %d/%d: %ld records merged in %.1f ms\n", q, rplan.rounds,
