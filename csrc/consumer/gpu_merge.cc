@@ -618,9 +618,10 @@ constexpr int kD2HSlotsDefault = 0;
 
 class D2HLinkGate {
  public:
-  static D2HLinkGate& get() {
-    static D2HLinkGate* g = new D2HLinkGate;  // never destroyed: tasks may outlive static teardown
-    return *g;
+  // 0: D2H pieces; 1: generic device merges of descriptor tasks (mapred.uda.gpu.merge.slots)
+  static D2HLinkGate& get(int which = 0) {
+    static D2HLinkGate* g[2] = {new D2HLinkGate, new D2HLinkGate};  // never destroyed: tasks may outlive static teardown
+    return *g[which & 1];
   }
   void acquire(int device, int slots, int64_t left) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -2101,6 +2102,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     for (int64_t l : rlen) left += l;
     ws.gate(device, (int)host_->conf_i64("mapred.uda.gpu.d2h.slots", kD2HSlotsDefault), left);
   }
+  const int merge_slots = (int)host_->conf_i64("mapred.uda.gpu.merge.slots", 0);
+  int64_t merge_left = 0;
+  for (int64_t l : rlen) merge_left += l;
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
   // dataFromUda): the consumer's work (the reduce task's bound when one task holds most of the data)
   // never waits for the merge driver, and the merge reuses an output only after its delivery.
@@ -2211,6 +2215,20 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       continue;
     }
     const uint8_t* dst = outs[q & 1]->as<uint8_t>();
+    // merge turns (mapred.uda.gpu.merge.slots > 0): at most that many tasks' rounds merge at once,
+    // the next turn to the task with the most input left, so a skewed task's next round does not queue
+    // behind every other task's first merge while its consumer idles
+    struct Turn {
+      int device = -1;
+      ~Turn() {
+        if (device >= 0) D2HLinkGate::get(1).release(device);
+      }
+    } turn;
+    if (merge_slots > 0) {
+      D2HLinkGate::get(1).acquire(device, merge_slots, merge_left);
+      turn.device = device;
+    }
+    for (int64_t l : sl) merge_left -= l;
     const auto tq = std::chrono::steady_clock::now();
     gpu::GenericMergeResult r = ws.merger.merge(
         sp, sl, (int)kind_, outs[q & 1]->as<uint8_t>(), (int64_t)outs[q & 1]->size(), kv, s,
