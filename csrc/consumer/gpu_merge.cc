@@ -1809,6 +1809,10 @@ void ReduceTask::merge_gpu() {
 bool ReduceTask::merge_gpu_device(bool probe) {
   join_prewarm();
   if (gpu::device_count() <= 0) throw UdaError("mapred.uda.merge.backend=gpu but no HIP device is visible");
+  // The task's device memory mostly comes from pooled workspaces sized by earlier tasks, so a
+  // DeviceBuffer allocation may never happen in this task: the injected device-allocation failure
+  // (UDA_FAULT_DEVICE_ALLOC) also counts the task taking its workspaces.
+  if (fault_hit("DEVICE_ALLOC")) throw UdaError("injected device allocation failure (GPU merge workspaces)");
   auto t0 = std::chrono::steady_clock::now();
   const int maps = init_.num_maps;
   const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
