@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../consumer/reduce_task.h"
+#include "../gpu/hbm_ledger.h"
 #include "../provider/supplier.h"
 #include "uda/cmd.h"
 #include "uda/host.h"
@@ -90,8 +91,16 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
       so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);
       so.hbm_bytes = h->host->conf_i64("mapred.uda.provider.hbm.bytes", 0);
       so.hbm_lease_s = h->host->conf_f64("mapred.uda.provider.hbm.lease.s", 600);
-      {
-        const std::string devs = h->host->get_conf("mapred.uda.provider.hbm.devices", "0");
+      if (so.hbm_bytes > 0) {
+        // default: stripe the store over every GPU the provider sees, so a node's reduce tasks (placed
+        // over all GPUs, mapred.uda.gpu.device=auto) find their map outputs spread the same way
+        std::string devs = h->host->get_conf("mapred.uda.provider.hbm.devices", "all");
+        if (devs == "all") {
+          devs.clear();
+          const int n = (int)uda::gpu::visible_device_keys().size();
+          for (int d = 0; d < n; ++d) devs += (d ? "," : "") + std::to_string(d);
+          if (devs.empty()) devs = "0";
+        }
         so.hbm_devices.clear();
         for (size_t b = 0; b <= devs.size();) {
           const size_t e = devs.find(',', b);

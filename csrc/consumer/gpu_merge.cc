@@ -45,6 +45,7 @@
 #include "../gpu/device_engine.h"
 #include "../gpu/generic_merger.h"
 #include "../gpu/generic_rounds.h"
+#include "../gpu/hbm_ledger.h"
 #include "../gpu/sdma.h"
 #include "reduce_task.h"
 #include "uda/aio.h"
@@ -126,6 +127,10 @@ struct DeviceWorkspace {
   static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
     bytes = std::max<int64_t>(bytes, 16);
     if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
+  }
+  int64_t device_bytes() const {
+    return (int64_t)(in.held() + out.held() + packed.held() + out2.held() + frame_scratch.held() + frame_descs.held()) +
+           merger.workspace_bytes();
   }
 };
 
@@ -265,6 +270,12 @@ class EarlyStager {
   double issue_ms() const { return issue_ms_; }
   int64_t copies() const { return copies_; }
   int64_t bytes() const { return bytes_; }
+  int64_t device_bytes() {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t n = 0;
+    for (const auto& b : blocks_) n += (int64_t)b.buf.held();
+    return n;
+  }
 
  private:
   struct Job {
@@ -361,7 +372,13 @@ template <class T>
 class DevicePool {
  public:
   static DevicePool& get() {
-    static DevicePool* p = new DevicePool;  // never destroyed: HIP may be torn down first at exit
+    static DevicePool* p = [] {
+      auto* q = new DevicePool;  // never destroyed: HIP may be torn down first at exit
+      // idle objects hold HBM: the device's byte budget trims them (largest first) under pressure
+      gpu::HbmLedger::get().add_pool({[q](int d, int64_t want) { return q->trim(d, want); },
+                                      [q](int d) { return q->idle(d); }});
+      return q;
+    }();
     return *p;
   }
   template <class Make>
@@ -382,10 +399,40 @@ class DevicePool {
     auto& v = idle_[device];
     if (v.size() < kMaxIdle) v.push_back(std::move(o));
   }
+  int64_t trim(int device, int64_t want) {
+    std::vector<std::unique_ptr<T>> drop;
+    int64_t got = 0;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = idle_[device];
+      std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a->device_bytes() < b->device_bytes(); });
+      while (!v.empty() && got < want) {
+        got += v.back()->device_bytes();
+        drop.push_back(std::move(v.back()));
+        v.pop_back();
+      }
+    }
+    if (!drop.empty()) {
+      int cur = 0;
+      HIP_CHECK(hipGetDevice(&cur));
+      HIP_CHECK(hipSetDevice(device));
+      drop.clear();
+      HIP_CHECK(hipSetDevice(cur));
+    }
+    return got;
+  }
+  int64_t idle(int device) {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t n = 0;
+    for (auto& o : idle_[device]) n += o->device_bytes();
+    return n;
+  }
 
  private:
+  // Idle objects are bounded in bytes by the device's HBM budget (trimmed under pressure); the count
+  // bound only limits the host memory they pin (a workspace's D2H ring is 128 MiB of pinned DRAM).
   // 16 concurrent reduce tasks per GPU (the bench shape) must find their workspaces again: a dropped
-  // one is freed, and hipFree synchronizes the whole device under the other tasks
+  // one is freed, and hipFree synchronizes the whole device under the other tasks.
   static constexpr size_t kMaxIdle = 32;
   std::mutex mu_;
   std::map<int, std::vector<std::unique_ptr<T>>> idle_;
@@ -824,8 +871,9 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
 void ReduceTask::prewarm_gpu(PrewarmConf pc) {
   const auto t0 = std::chrono::steady_clock::now();
   try {
+    std::call_once(placed_, [this] { place_on_gpu(); });
     if (gpu::device_count() <= 0) return;
-    const int device = pc.device;
+    const int device = device_;
     if (hipSetDevice(device) != hipSuccess) return;
     try {
       (void)gpu::SdmaEngine::for_device(device);
@@ -875,9 +923,14 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
 }
 
 void ReduceTask::join_prewarm() {
-  if (!prewarm_thr_.joinable()) return;
+  // placed by the prewarm; without one (or if it failed there) here, where a failure fails the task
+  if (!prewarm_thr_.joinable()) {
+    std::call_once(placed_, [this] { place_on_gpu(); });
+    return;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   prewarm_thr_.join();
+  std::call_once(placed_, [this] { place_on_gpu(); });
   std::lock_guard<std::mutex> g(st_mu_);
   st_.gpu_prewarm_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -891,7 +944,7 @@ void ReduceTask::merge_gpu() {
   }
   auto t0 = std::chrono::steady_clock::now();
   const int maps = init_.num_maps;
-  const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+  const int device = device_;
   if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
   GateLease gate;
   // Off by default: a gated task fetches nothing until all its FETCHes are in, which under reduce
@@ -1815,7 +1868,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   if (fault_hit("DEVICE_ALLOC")) throw UdaError("injected device allocation failure (GPU merge workspaces)");
   auto t0 = std::chrono::steady_clock::now();
   const int maps = init_.num_maps;
-  const int device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
+  const int device = device_;
   HIP_CHECK(hipSetDevice(device));
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
@@ -1988,10 +2041,44 @@ bool ReduceTask::merge_gpu_device(bool probe) {
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
+  // HBM admission (gpu/hbm_ledger.h): the task's device working set -- decoded partitions, the
+  // key-range round's output slots and merge tables -- is reserved before it is allocated, under the
+  // device's byte budget shared with the provider's store and every other task on the node. A round
+  // that could never fit is halved until it does; a task that fits later waits (FIFO) for it.
+  gpu::HbmLedger& ledger = gpu::HbmLedger::get();
+  std::unique_ptr<gpu::HbmLedger::Reservation> hbm_res;
+  int64_t round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+  auto admit = [&](int64_t fixed, const std::function<int64_t(int64_t)>& round_ws) {
+    const int64_t hr = ledger.headroom(device);
+    while (round_bytes > (64ll << 20) && fixed + round_ws(round_bytes) > hr) round_bytes /= 2;
+    hbm_res = ledger.reserve(device, std::max<int64_t>(0, fixed + round_ws(round_bytes)), [&] { return stop_.load(); });
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.hbm_wait_ms += hbm_res->wait_ms();
+    st_.hbm_reserved = hbm_res->granted();
+    st_.round_bytes = round_bytes;
+  };
   // ---- compressed map outputs: F6 block decode straight from the partitions (descriptors or fetched
   // bytes) into the workspace; the framing is walked on the device
   if (codec_ != Codec::kNone) {
     const auto td = std::chrono::steady_clock::now();
+    std::vector<const uint8_t*> cp;
+    std::vector<int64_t> cl;
+    for (const auto& p : parts) {
+      cp.push_back(p->dptr);
+      cl.push_back(p->part_len);
+    }
+    gpu::BlockPlan bp;
+    std::vector<int64_t> roff;
+    int64_t blocks = 0;
+    const bool dev_frames = gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, ws.frame_descs, s);
+    if (dev_frames) {
+      // decode output and the merge's rounds at once: a task holding its decoded partitions must
+      // not then wait for merge memory behind tasks doing the same
+      const int64_t raw = bp.raw_total;
+      admit(std::max<int64_t>(0, raw + raw / 8 - (int64_t)ws.in.held()), [&](int64_t rb) {
+        return gpu::fixed_round_ws_bytes(std::min(rb, raw), (int)parts.size());
+      });
+    }
     // Decodes of concurrent tasks take turns (FIFO, mapred.uda.gpu.decode.slots at once, default 1;
     // 0 = no limit): a decode fills the device by itself, so running them in turn costs no decode
     // throughput, and the first tasks reach their merge and D2H delivery while later ones still
@@ -2003,16 +2090,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         throw UdaError("reduce task stopped while waiting for a device decode slot");
       dgate.device = device;
     }
-    std::vector<const uint8_t*> cp;
-    std::vector<int64_t> cl;
-    for (const auto& p : parts) {
-      cp.push_back(p->dptr);
-      cl.push_back(p->part_len);
-    }
-    gpu::BlockPlan bp;
-    std::vector<int64_t> roff;
-    int64_t blocks = 0;
-    if (gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, ws.frame_descs, s)) {
+    if (dev_frames) {
       DeviceWorkspace::ensure(ws.in, bp.raw_total);
       ws.decoder.decode(codec_, bp, nullptr, ws.in.as<uint8_t>(), s);
       roff = bp.raw_offset;
@@ -2063,9 +2141,15 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     gpu::DeviceReduceConfig cfg;
     cfg.device = device;
     cfg.kv_buf_bytes = kv_buf_size_;
-    cfg.round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+    cfg.round_bytes = round_bytes;
+    cfg.stop = [&] { return stop_.load(); };
     gpu::DeviceReduceStats ds = gpu::device_reduce_fixed(cfg, runs, sink);
     std::lock_guard<std::mutex> g(st_mu_);
+    if (!hbm_res) {
+      st_.hbm_wait_ms += ds.hbm_wait_ms;
+      st_.hbm_reserved = ds.hbm_reserved;
+    }
+    st_.round_bytes = ds.round_bytes;
     st_.records = ds.records;
     st_.rpq_rounds = ds.rounds;
     st_.gpu_device_ms = ds.plan_ms + ds.merge_wait_ms;
@@ -2088,7 +2172,15 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     rlen.push_back(p->part_len);
     total += p->part_len;
   }
-  const int64_t round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+  // working set of a generic round of rb input bytes: two output slots + ~88 B of merge metadata per
+  // record (records of >= 64 B) over what the pooled workspace already holds
+  if (!hbm_res) {
+    const int64_t have = (int64_t)(ws.out.held() + ws.out2.held()) + ws.merger.workspace_bytes();
+    admit(0, [&](int64_t rb) {
+      const int64_t b = std::min(rb, total);
+      return std::max<int64_t>(0, (int64_t)(2.25 * (double)b + 1.4 * (double)b) - have);
+    });
+  }
   if (total > round_bytes) {
     // a task holding more than a round (a skewed partition) is the job's long pole: its merge kernels
     // go first when the device is shared with the other tasks' merges
@@ -2234,11 +2326,16 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     }
     for (int64_t l : sl) merge_left -= l;
     const auto tq = std::chrono::steady_clock::now();
+    bool round_closed = false;
     gpu::GenericMergeResult r = ws.merger.merge(
         sp, sl, (int)kind_, outs[q & 1]->as<uint8_t>(), (int64_t)outs[q & 1]->size(), kv, s,
         [&](const std::vector<int64_t>& cuts, int64_t, bool last_inner) {
           push(DJob{dst, cuts, last_inner && last_outer, last_inner});
+          round_closed = round_closed || last_inner;
         });
+    // slices holding only EOF markers: the merge saw no records and never called back, but the
+    // delivery thread still has to count this round as handed over
+    if (!round_closed) push(DJob{nullptr, {}, false, true});
     m.records += r.records;
     if (trace::host_enabled())
       trace::host_event("gr_merge", (int64_t)(uintptr_t)&ws, q,

@@ -15,7 +15,9 @@
 #include <random>
 #include <sstream>
 
+#include "../gpu/hbm_ledger.h"
 #include "uda/log.h"
+#include "uda/node_registry.h"
 #include "uda/queues.h"
 #include "uda/trace.h"
 
@@ -398,9 +400,12 @@ void ReduceTask::on_init(const InitParams& p) {
   // CPU: the hybrid (approach 2) LPQ files; GPU: the disk-tier LPQ spills of the GPU hybrid merge
   checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && (backend_ == "gpu" || net_.online == 2);
   if (checkpoint_) load_checkpoint();
+  if (backend_ == "gpu") {
+    device_conf_ = host_->get_conf("mapred.uda.gpu.device", "auto");
+    hbm_budget_conf_ = std::atof(host_->get_conf("mapred.uda.gpu.hbm.budget", "0").c_str());
+  }
   if (backend_ == "gpu" && host_->conf_i64("mapred.uda.gpu.prewarm", 1) != 0) {
     PrewarmConf pc;
-    pc.device = (int)host_->conf_i64("mapred.uda.gpu.device", 0);
     pc.early_h2d = host_->conf_i64("mapred.uda.gpu.early.h2d", 1) != 0;
     // pinned fetch-arena blocks, not for tasks that only fetch device descriptors
     if (host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device")
@@ -408,6 +413,32 @@ void ReduceTask::on_init(const InitParams& p) {
     prewarm_thr_ = std::thread([this, pc] { prewarm_gpu(pc); });
   }
   merge_thr_ = std::thread([this] { merge_main(); });
+}
+
+void ReduceTask::place_on_gpu() {
+  const std::string& conf = device_conf_;
+  const std::vector<std::string> keys = gpu::visible_device_keys();
+  if (keys.empty()) {
+    device_ = 0;  // merge_gpu reports "no HIP device" when the task gets there
+    return;
+  }
+  NodeRegistry* reg = NodeRegistry::instance();
+  if (conf != "auto" && !conf.empty()) {
+    device_ = std::atoi(conf.c_str());
+    if (device_ < 0 || device_ >= (int)keys.size())
+      throw UdaError("mapred.uda.gpu.device=" + conf + " but " + std::to_string(keys.size()) + " GPU(s) are visible");
+    if (reg) registry_slot_ = reg->add_task(keys[(size_t)device_], init_.reduce_task_id);
+  } else if (reg) {
+    const NodeRegistry::Placement pl = reg->place_task(keys, init_.reduce_task_id);
+    device_ = pl.index;
+    registry_slot_ = pl.slot;
+  } else {
+    device_ = 0;
+  }
+  // per-device HBM budget: bytes, or a fraction of the device's HBM (default 0.92)
+  gpu::HbmLedger::get().configure(device_, hbm_budget_conf_);
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.gpu_device = device_;
 }
 
 // attempt_<jt>_<job>_m_<task>_<n> -> attempt_<jt>_<job>_m_<task> (the map task, any attempt)
@@ -522,6 +553,11 @@ void ReduceTask::exit() {
   std::unique_lock<std::mutex> lk(inflight_mu_);
   if (!inflight_cv_.wait_for(lk, std::chrono::seconds(120), [&] { return inflight_ == 0; }))
     UDA_LOG(kError, "reduce task exit: %ld fetch completions still outstanding", (long)inflight_);
+  lk.unlock();
+  if (registry_slot_ >= 0) {
+    if (NodeRegistry* reg = NodeRegistry::instance()) reg->release(registry_slot_);
+    registry_slot_ = -1;
+  }
 }
 
 void ReduceTask::fetch_begin() {
@@ -823,7 +859,8 @@ std::string ReduceTask::stats_json() const {
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
     << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
-    << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"merge_path\":\"" << s.merge_path << "\""
+    << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms
+    << ",\"hbm_reserved\":" << s.hbm_reserved << ",\"round_bytes\":" << s.round_bytes << ",\"gpu_device\":" << s.gpu_device << ",\"merge_path\":\"" << s.merge_path << "\""
     << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();
 }

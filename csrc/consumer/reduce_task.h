@@ -54,6 +54,10 @@ struct ReduceStats {
   double gpu_h2d_ms = 0, gpu_device_ms = 0, gpu_d2h_wait_ms = 0, gpu_sink_ms = 0;
   double gpu_decode_ms = 0;  // device fetch, compressed partitions: framing walk + F6 decode (stream synced)
   double gpu_gate_wait_ms = 0;  // waiting for a GPU merge slot (mapred.uda.gpu.max.concurrent.merges)
+  double hbm_wait_ms = 0;       // waiting for the device working set under the HBM budget
+  int64_t hbm_reserved = 0;     // bytes of that reservation
+  int64_t round_bytes = 0;      // device fetch: key-range round size used (halved to fit the budget)
+  int gpu_device = -1;          // HIP device the task ran on (mapred.uda.gpu.device, auto = placed)
   double gpu_prewarm_ms = -1;   // INIT-time GPU prewarm (mapred.uda.gpu.prewarm); -1: not run
   double gpu_prewarm_wait_ms = 0;  // the merge waiting for the prewarm to finish
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
@@ -104,12 +108,22 @@ class ReduceTask {
   // code objects, a pooled workspace with its pinned D2H ring and early stager, pinned fetch-arena
   // blocks, all while the FETCHes are still to come (reduce slow-start). The merge joins it first.
   struct PrewarmConf {  // read on the INIT thread (the host's get_conf may be bound to it)
-    int device = 0;
     bool early_h2d = true;
     int64_t pinned_bytes = 0;
   };
   void prewarm_gpu(PrewarmConf pc);
   void join_prewarm();
+  // GPU backend: the task's HIP device. mapred.uda.gpu.device = an index pins it; "auto" (default)
+  // takes the visible GPU with the fewest live reduce tasks on the node (uda/node_registry.h), so a
+  // node's reduce task processes spread over its GPUs. Registered until the task ends.
+  // Runs once, on the prewarm thread (or the merge thread without prewarm): HIP's first call can
+  // take a while in a fresh process and INIT must not wait for it.
+  void place_on_gpu();
+  std::once_flag placed_;
+  std::string device_conf_ = "auto";   // read on the INIT thread
+  double hbm_budget_conf_ = 0;
+  int device_ = 0;
+  int registry_slot_ = -1;
   // Fetch `n` MOFs into `q` (reference merge_do_fetching_phase).
   void fetch_phase(MergeQueue* q, int n, std::vector<std::string>* map_ids = nullptr);
   // LPQ checkpoint (mapred.uda.lpq.checkpoint): completed LPQ spill files survive a failed attempt,

@@ -301,7 +301,7 @@ void ApiTeraSortBench::compress_store() {
   if (!err.empty()) throw std::runtime_error("api bench: compressing the MOFs: " + err);
   std::vector<int64_t> off((size_t)M + 1, 0);
   for (int m = 0; m < M; ++m) off[(size_t)m + 1] = off[(size_t)m] + ((int64_t)comp[(size_t)m].size() + 255) / 256 * 256;
-  comp_store_.reset(new DeviceBuffer((size_t)std::max<int64_t>(off[(size_t)M], 16)));
+  comp_store_.reset(new DeviceBuffer((size_t)std::max<int64_t>(off[(size_t)M], 16), /*resident=*/true));
   uda_handle* h = static_cast<uda_handle*>(provider_);
   for (int m = 0; m < M; ++m) {
     uint8_t* dst = comp_store_->as<uint8_t>() + off[(size_t)m];
@@ -322,7 +322,7 @@ void ApiTeraSortBench::setup_secondary() {
   const int P = cfg_.reducers;
   const SecGenPlan plan = secgen_plan(cfg_.maps, P, cfg_.records_per_map, cfg_.skew, cfg_.seed);
   sec_store_bytes_ = plan.store_bytes();
-  sec_store_.reset(new DeviceBuffer((size_t)sec_store_bytes_));
+  sec_store_.reset(new DeviceBuffer((size_t)sec_store_bytes_, /*resident=*/true));
   hipStream_t s;
   HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   secgen_write(plan, sec_store_->as<uint8_t>(), s);

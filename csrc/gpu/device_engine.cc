@@ -1,6 +1,7 @@
 // Device shuffle/merge engine implementation. See device_engine.h for the design.
 #include "device_engine.h"
 #include "device_ptr.h"
+#include "hbm_ledger.h"
 #include "merge_plan.h"
 #include "sdma.h"
 #include "uda/fault.h"
@@ -48,16 +49,28 @@ void hip_check(hipError_t e, const char* what, const char* file, int line) {
 
 // ------------------------------------------------------------------------------------ buffers
 DeviceBuffer::~DeviceBuffer() { reset(); }
-void DeviceBuffer::alloc(size_t bytes) {
+void DeviceBuffer::alloc(size_t bytes, bool resident) {
   reset();
   if (bytes == 0) return;
   if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
   // Blocks another process may map over hipIpc (our descriptor fetch, RCCL's peer registration of
   // send/receive buffers) must stay out of the size range that hangs the importer (device_ptr.h).
+  const size_t held = ipc_safe_bytes(bytes);
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HbmLedger::get().on_alloc(dev, (int64_t)held, resident);
   const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
-  HIP_CHECK(hipMalloc(&ptr_, ipc_safe_bytes(bytes)));
+  const hipError_t e = hipMalloc(&ptr_, held);
+  if (e != hipSuccess) {
+    ptr_ = nullptr;
+    HbmLedger::get().on_free(dev, (int64_t)held, resident);
+    HIP_CHECK(e);
+  }
   if (tt) trace::host_event("device_alloc", (int64_t)bytes, 0, tt, trace::now_ns());
   size_ = bytes;
+  held_ = held;
+  dev_ = dev;
+  resident_ = resident;
 }
 void DeviceBuffer::reset() {
   if (ptr_ && trace::host_enabled()) {
@@ -67,8 +80,9 @@ void DeviceBuffer::reset() {
     ptr_ = nullptr;
   }
   if (ptr_) (void)hipFree(ptr_);
+  if (held_) HbmLedger::get().on_free(dev_, (int64_t)held_, resident_);
   ptr_ = nullptr;
-  size_ = 0;
+  size_ = held_ = 0;
 }
 
 PinnedBuffer::~PinnedBuffer() { pinned_host_free(ptr_); }
@@ -210,11 +224,8 @@ int device_count() {
 //   RunDesc runs[K] | int64 elem_off[K+1] | uint8_t* bases[K] | per pass: pairs[3P], tile_prefix[P+1]
 DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
     : max_records_(max_records), max_runs_(max_runs) {
-  elems_a_.alloc((size_t)std::max<int64_t>(max_records, 1) * sizeof(Elem));
-  elems_b_.alloc((size_t)std::max<int64_t>(max_records, 1) * sizeof(Elem));
-  // tiles per pass <= records/2048 + pairs; splits buffer sized for one pass
-  const int64_t max_tiles = max_records / kMergeTile + max_runs + 2;
-  splits_.alloc((size_t)max_tiles * sizeof(int64_t));
+  // the merge-tree buffers (2 x 16 B per record) are allocated on the tree path's first use: the
+  // single-pass K-way merge, which takes every group of <= kKwMaxRuns runs, never touches them
   flag_.alloc(sizeof(int));
   HIP_CHECK(hipMemset(flag_.as(), 0, sizeof(int)));
   int passes = 1;
@@ -236,6 +247,16 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
     s.dev.alloc(slot_bytes_);
     HIP_CHECK(hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming));
   }
+}
+
+int64_t DeviceMerger::device_bytes() const {
+  int64_t n = (int64_t)(elems_a_.held() + elems_b_.held() + splits_.held() + flag_.held() + kw_prof_.held() +
+                        kw_overflow_.held());
+  for (const auto& p : pbufs_)
+    n += (int64_t)(p.samp_runs.held() + p.samp_a.held() + p.samp_b.held() + p.bounds.held() + p.split.held() +
+                   p.splits.held());
+  for (const auto& s : slots_) n += (int64_t)s.dev.held();
+  return n;
 }
 
 DeviceMerger::~DeviceMerger() {
@@ -277,6 +298,13 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
     if (kmax <= kKwMaxRuns) return merge_kway(runs, group_first, out, s);
   }
 
+  if (!elems_a_.size()) {
+    elems_a_.alloc((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
+    elems_b_.alloc((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
+    // tiles per pass <= records/2048 + pairs; splits buffer sized for one pass
+    const int64_t max_tiles = max_records_ / kMergeTile + max_runs_ + 2;
+    splits_.alloc((size_t)max_tiles * sizeof(int64_t));
+  }
   Slot& slot = slots_[next_slot_];
   next_slot_ = (next_slot_ + 1) % (int)slots_.size();
   if (slot.used) HIP_CHECK(hipEventSynchronize(slot.uploaded));
@@ -692,7 +720,7 @@ void ShuffleJob::generate() {
     HIP_CHECK(hipHostGetDevicePointer(&dp, store_base_, 0));
     store_dev_base_ = reinterpret_cast<uint8_t*>(dp);
   } else {
-    store_.alloc((size_t)store_bytes_);  // padded for hipIpc export by DeviceBuffer::alloc
+    store_.alloc((size_t)store_bytes_, /*resident=*/true);  // padded for hipIpc export by DeviceBuffer::alloc
     store_base_ = store_dev_base_ = store_.as<uint8_t>();
   }
 

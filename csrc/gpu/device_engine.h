@@ -49,39 +49,49 @@ namespace gpu {
 void hip_check(hipError_t e, const char* what, const char* file, int line);
 #define HIP_CHECK(x) ::uda::gpu::hip_check((x), #x, __FILE__, __LINE__)
 
-// Owning device allocation.
+// Owning device allocation. Every allocation and free is accounted in the device's HBM ledger
+// (hbm_ledger.h); `resident` marks data that stays (a map-output store), not a task's working set.
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;
-  explicit DeviceBuffer(size_t bytes) { alloc(bytes); }
+  explicit DeviceBuffer(size_t bytes, bool resident = false) { alloc(bytes, resident); }
   ~DeviceBuffer();
   DeviceBuffer(const DeviceBuffer&) = delete;
   DeviceBuffer& operator=(const DeviceBuffer&) = delete;
-  DeviceBuffer(DeviceBuffer&& o) noexcept : ptr_(o.ptr_), size_(o.size_) {
-    o.ptr_ = nullptr;
-    o.size_ = 0;
-  }
+  DeviceBuffer(DeviceBuffer&& o) noexcept { take(o); }
   DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
     if (this != &o) {
       reset();
-      ptr_ = o.ptr_;
-      size_ = o.size_;
-      o.ptr_ = nullptr;
-      o.size_ = 0;
+      take(o);
     }
     return *this;
   }
-  void alloc(size_t bytes);
+  void alloc(size_t bytes, bool resident = false);
   void reset();
   template <typename T = uint8_t>
   T* as() const {
     return reinterpret_cast<T*>(ptr_);
   }
   size_t size() const { return size_; }
+  // bytes held in HBM (the allocation may be padded for hipIpc export)
+  size_t held() const { return held_; }
+  int device() const { return dev_; }
 
  private:
+  void take(DeviceBuffer& o) {
+    ptr_ = o.ptr_;
+    size_ = o.size_;
+    held_ = o.held_;
+    dev_ = o.dev_;
+    resident_ = o.resident_;
+    o.ptr_ = nullptr;
+    o.size_ = o.held_ = 0;
+  }
   void* ptr_ = nullptr;
   size_t size_ = 0;
+  size_t held_ = 0;
+  int dev_ = -1;
+  bool resident_ = false;
 };
 
 // Owning pinned host allocation (pinned_host_alloc).
@@ -166,6 +176,8 @@ class DeviceMerger {
   bool bad_layout();  // synchronizes; true if any record was not TeraSort-shaped
   int64_t max_records() const { return max_records_; }
   int max_runs() const { return max_runs_; }
+  // HBM held by this merger's buffers
+  int64_t device_bytes() const;
   // Cells the single-pass K-way merge handed to its wave-level PQ so far (synchronizes).
   int kway_overflow_cells();
   bool kway_enabled() const { return kway_; }

@@ -15,7 +15,9 @@
 #include <stdexcept>
 
 #include "device_engine.h"
+#include "hbm_ledger.h"
 #include "sdma.h"
+#include "uda/error.h"
 #include "uda/trace.h"
 #include "uda/vint.h"
 
@@ -68,13 +70,54 @@ struct FixedWs {
   static void ensure(DeviceBuffer& b, size_t bytes) {
     if (b.size() < bytes) b.alloc(bytes + bytes / 8);
   }
+  int64_t device_bytes() const {
+    int64_t n = merger ? merger->device_bytes() : 0;
+    for (const DeviceBuffer* b : {&out[0], &out[1], &d_bases, &d_nrec, &d_soff, &d_samp, &d_bset, &d_out, &d_bounds,
+                                  &d_runs, &flag})
+      n += (int64_t)b->held();
+    return n;
+  }
 };
 
 class FixedWsPool {
  public:
   static FixedWsPool& get() {
-    static FixedWsPool* p = new FixedWsPool;  // never destroyed: tasks may outlive static teardown
+    static FixedWsPool* p = [] {
+      auto* q = new FixedWsPool;  // never destroyed: tasks may outlive static teardown
+      HbmLedger::get().add_pool({[q](int d, int64_t want) { return q->trim(d, want); },
+                                 [q](int d) { return q->idle(d); }});
+      return q;
+    }();
     return *p;
+  }
+  // free idle workspaces of `device`, largest first, until `want` bytes are freed
+  int64_t trim(int device, int64_t want) {
+    std::vector<std::unique_ptr<FixedWs>> drop;
+    int64_t got = 0;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = free_[device];
+      std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a->device_bytes() < b->device_bytes(); });
+      while (!v.empty() && got < want) {
+        got += v.back()->device_bytes();
+        drop.push_back(std::move(v.back()));
+        v.pop_back();
+      }
+    }
+    if (!drop.empty()) {
+      int cur = 0;
+      HIP_CHECK(hipGetDevice(&cur));
+      HIP_CHECK(hipSetDevice(device));
+      drop.clear();
+      HIP_CHECK(hipSetDevice(cur));
+    }
+    return got;
+  }
+  int64_t idle(int device) {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t n = 0;
+    for (const auto& w : free_[device]) n += w->device_bytes();
+    return n;
   }
   std::unique_ptr<FixedWs> acquire(int device) {
     {
@@ -133,6 +176,13 @@ struct Ring {
 };
 }  // namespace
 
+int64_t fixed_round_ws_bytes(int64_t round_bytes, int runs) {
+  // two output slots grown 1/8 past a round that may run ~10 % over the mean, plus the merger's
+  // per-round plan tables (cell splits, samples: ~2 % of the round) and its upload slots
+  const double slot = (double)round_bytes * 1.1 * 1.125;
+  return (int64_t)(2 * slot + 0.02 * (double)round_bytes) + (int64_t)runs * 4096 + (16ll << 20);
+}
+
 bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
   if (runs.empty()) return true;
   int64_t max_n = 0;
@@ -188,8 +238,24 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
     return st;
   }
 
+  // ---- HBM admission: the round size must fit the budget next to everything else on the node
+  HbmLedger& led = HbmLedger::get();
+  int64_t round_bytes = std::max<int64_t>(cfg.round_bytes, kTeraRecordBytes);
+  const bool caller_reserved = led.bound() != nullptr && led.bound()->device() == cfg.device;
+  std::unique_ptr<HbmLedger::Reservation> res;
+  if (!caller_reserved) {
+    auto need = [&](int64_t rb) {
+      return std::max<int64_t>(0, fixed_round_ws_bytes(std::min(rb, N * kTeraRecordBytes), K) - ws.device_bytes());
+    };
+    const int64_t hr = led.headroom(cfg.device);
+    while (round_bytes > (64ll << 20) && need(round_bytes) > hr) round_bytes /= 2;
+    res = led.reserve(cfg.device, need(round_bytes), cfg.stop);
+    st.hbm_wait_ms = res->wait_ms();
+    st.hbm_reserved = res->granted();
+  }
+  st.round_bytes = round_bytes;
   // ---- round plan: key sample -> Q-1 bounds -> per-run split positions
-  const int Q = (int)std::max<int64_t>(1, (N * kTeraRecordBytes + cfg.round_bytes - 1) / cfg.round_bytes);
+  const int Q = (int)std::max<int64_t>(1, (N * kTeraRecordBytes + round_bytes - 1) / round_bytes);
   std::vector<int64_t> pos((size_t)K * (Q + 1), 0);
   {
     std::vector<uint8_t*> bases(K);

@@ -29,7 +29,11 @@ struct DeviceReduceConfig {
   int64_t piece_bytes = 64ll << 20;   // D2H granule
   int pinned_slots = 4;
   int64_t sample_every = 4096;        // one key sampled per this many records for the round bounds
-};
+  // HBM admission (hbm_ledger.h): the task's round working set is reserved before its merge; a
+  // round that could never fit the budget is halved until it does. A reservation already bound to
+  // the calling thread (a caller that reserved for decode + merge at once) is drawn from instead.
+  std::function<bool()> stop;         // gives up waiting for HBM when true
+}; 
 
 struct DeviceReduceStats {
   int64_t records = 0;
@@ -38,7 +42,14 @@ struct DeviceReduceStats {
   int rounds = 0;
   int merge_passes = 0;
   double plan_ms = 0, merge_wait_ms = 0, d2h_wait_ms = 0, sink_ms = 0;
+  double hbm_wait_ms = 0;      // waiting for the HBM reservation
+  int64_t hbm_reserved = 0;    // bytes reserved for the round working set
+  int64_t round_bytes = 0;     // round size used (after any shrink to fit the budget)
 };
+
+// HBM a FIXED10 round working set of `round_bytes` merged bytes needs (two output slots and the
+// merger's per-round tables), for admission.
+int64_t fixed_round_ws_bytes(int64_t round_bytes, int runs);
 
 // True if every run holds whole TeraSort-shaped records (VInt 11, VInt 91, Text 10 + 90 bytes).
 // Synchronizes `s`.

@@ -23,6 +23,12 @@ class ProtocolError : public UdaError {
   using UdaError::UdaError;
 };
 
+// A device working set that does not fit the HBM budget (mapred.uda.gpu.hbm.budget) now, or ever.
+class HbmBudgetError : public UdaError {
+ public:
+  using UdaError::UdaError;
+};
+
 // A one-shot failure latch: the first report wins and triggers the hook; later ones are counted.
 class FailureLatch {
  public:

@@ -34,6 +34,8 @@
 #include "uda/log.h"
 #include "uda/vint.h"
 #include "uda/shm_group.h"
+#include "uda/node_registry.h"
+#include "../gpu/hbm_ledger.h"
 #include <atomic>
 #include <thread>
 
@@ -580,6 +582,115 @@ PYBIND11_MODULE(_uda_native, m) {
         if (!g.read_alloc(peer, id, blob, sizeof(blob), &size)) return py::none();
         return py::make_tuple(py::bytes(blob, sizeof(blob)), size);
       });
+
+  // node-local registry of reduce tasks / HBM bytes per GPU (CPU-testable, no HIP)
+  py::class_<NodeRegistry>(m, "NodeRegistry")
+      .def(py::init<const std::string&>(), py::arg("name") = std::string())
+      .def_property_readonly("name", &NodeRegistry::name)
+      .def("place_task",
+           [](NodeRegistry& r, const std::vector<std::string>& keys, const std::string& tag) {
+             const NodeRegistry::Placement p = r.place_task(keys, tag);
+             return py::make_tuple(p.index, p.slot);
+           })
+      .def("add_task", &NodeRegistry::add_task)
+      .def("release", &NodeRegistry::release)
+      .def("set_bytes", &NodeRegistry::set_bytes, py::arg("key"), py::arg("bytes"), py::arg("resident") = 0)
+      .def("usage",
+           [](NodeRegistry& r, const std::string& key) {
+             const NodeRegistry::Use u = r.usage(key);
+             py::dict d;
+             d["tasks"] = u.tasks;
+             d["bytes"] = u.bytes;
+             d["resident"] = u.resident;
+             return d;
+           })
+      .def_property_readonly("reclaimed", &NodeRegistry::reclaimed)
+      .def("unlink", &NodeRegistry::unlink);
+  m.def("process_running", &process_running, py::arg("pid"), py::arg("start") = 0);
+  m.def("process_start_ticks", &process_start_ticks);
+  // HBM budget ledger on fake devices (no HIP): tests of admission, trimming and the node-wide total
+  m.def("hbm_fake_device", [](int d, int64_t total, const std::string& key) {
+    gpu::HbmLedger::get().set_fake_device(d, total, key);
+  });
+  m.def("hbm_configure", [](int d, double conf) { gpu::HbmLedger::get().configure(d, conf); });
+  m.def("hbm_alloc", [](int d, int64_t b, bool resident) { gpu::HbmLedger::get().on_alloc(d, b, resident); },
+        py::arg("device"), py::arg("bytes"), py::arg("resident") = false);
+  m.def("hbm_free", [](int d, int64_t b, bool resident) { gpu::HbmLedger::get().on_free(d, b, resident); },
+        py::arg("device"), py::arg("bytes"), py::arg("resident") = false);
+  m.def("hbm_headroom", [](int d) { return gpu::HbmLedger::get().headroom(d); });
+  m.def("hbm_stats", [](int d) {
+    const gpu::HbmLedger::Stats s = gpu::HbmLedger::get().stats(d);
+    py::dict o;
+    o["budget"] = s.budget;
+    o["used"] = s.used;
+    o["reserved"] = s.reserved;
+    o["peak"] = s.peak;
+    o["resident"] = s.resident;
+    o["node_bytes"] = s.node_bytes;
+    o["trimmed"] = s.trimmed;
+    o["over"] = s.over;
+    o["waits"] = s.waits;
+    o["wait_ms"] = s.wait_ms;
+    return o;
+  });
+  // an idle pool of fake objects: trimmed by the ledger under pressure (returns the pool's id)
+  m.def("hbm_fake_pool", [](int d, std::vector<int64_t> sizes) {
+    auto objs = std::make_shared<std::vector<int64_t>>(std::move(sizes));
+    auto mu = std::make_shared<std::mutex>();
+    for (int64_t b : *objs) gpu::HbmLedger::get().on_alloc(d, b);
+    gpu::HbmLedger::get().add_pool(
+        {[objs, mu, d](int dev, int64_t want) -> int64_t {
+           if (dev != d) return 0;
+           std::vector<int64_t> drop;
+           {
+             std::lock_guard<std::mutex> g(*mu);
+             std::sort(objs->begin(), objs->end());
+             int64_t got = 0;
+             while (!objs->empty() && got < want) {
+               got += objs->back();
+               drop.push_back(objs->back());
+               objs->pop_back();
+             }
+           }
+           int64_t freed = 0;
+           for (int64_t b : drop) {
+             gpu::HbmLedger::get().on_free(d, b);
+             freed += b;
+           }
+           return freed;
+         },
+         [objs, mu, d](int dev) -> int64_t {
+           if (dev != d) return 0;
+           std::lock_guard<std::mutex> g(*mu);
+           int64_t n = 0;
+           for (int64_t b : *objs) n += b;
+           return n;
+         }});
+  });
+  struct PyReservation {
+    std::unique_ptr<gpu::HbmLedger::Reservation> r;
+  };
+  py::class_<PyReservation, std::shared_ptr<PyReservation>>(m, "HbmReservation")
+      .def_property_readonly("granted", [](PyReservation& p) { return p.r ? p.r->granted() : 0; })
+      .def_property_readonly("wait_ms", [](PyReservation& p) { return p.r ? p.r->wait_ms() : 0.0; })
+      .def("alloc", [](PyReservation& p, int64_t b) {  // an allocation drawing from the reservation
+        if (!p.r) throw std::runtime_error("reservation released");
+        auto scope = p.r->bind();
+        gpu::HbmLedger::get().on_alloc(p.r->device(), b);
+      })
+      .def("release", [](PyReservation& p) { p.r.reset(); });
+  m.def("hbm_reserve",
+        [](int d, int64_t bytes, double timeout_s) {
+          auto p = std::make_shared<PyReservation>();
+          {
+            py::gil_scoped_release nogil;
+            p->r = gpu::HbmLedger::get().reserve(d, bytes, nullptr, timeout_s);
+            // the Python thread is not where the allocations happen: unbind (alloc() binds per call)
+            p->r->unbind();
+          }
+          return p;
+        },
+        py::arg("device"), py::arg("bytes"), py::arg("timeout_s") = 30.0);
 
   m.def("set_log_level", &uda_set_log_level);
 

@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""One parametrized GPU-box runner (replaces the per-experiment gpurun shell recipes).
+
+    gpurun --timeout 1100 -- 'python3 tools/gpu_run.py --tag r4 pytest smoke bench api41'
+    gpurun -- 'python3 tools/gpu_run.py --tag ab --cmd "sec48x=400=python -u bench.py --api ..." sec48'
+
+Every step runs under its own time limit in its own process group, stdout goes to
+gpurun_out/<tag>_<name>.log and stderr to .err. The runner prints one summary line per step (the
+JSON line a bench prints: value, validated, plus --keys) and stops at the first failing step: after
+a fault, an abort, a crash or a time limit nothing else may use the GPU in that call.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PY = "python3 -u"
+
+# name -> (seconds, command). Commands run from the repo root through bash.
+RECIPES: dict[str, tuple[int, str]] = {
+    "pytest": (900, f"{PY} -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread"),
+    "smoke": (300, f"{PY} -c 'import __graft_entry__ as g; g.smoke()'"),
+    "bench": (400, f"{PY} bench.py --steps 3 --warmup 1"),
+    "device_only": (300, f"{PY} bench.py --device-only --steps 3 --warmup 1"),
+    "api41": (400, f"{PY} bench.py --api --rows-per-gpu 400000000 --steps 3 --warmup 1"),
+    "api130": (500, f"{PY} bench.py --api --steps 3 --warmup 1"),
+    "api_files41": (600, f"{PY} bench.py --api --mof-dir /tmp/uda_mofs --rows-per-gpu 400000000 --steps 2 --warmup 0"),
+    "api2_one_gpu": (500, f"{PY} bench.py --api --gpus 2 --one-gpu --rows-per-gpu 400000000 --steps 3 --warmup 1"),
+    "api4_one_gpu": (500, f"{PY} bench.py --api --gpus 4 --one-gpu --rows-per-gpu 200000000 --steps 3 --warmup 1"),
+    "sec48": (400, f"{PY} bench.py --api --workload secondary --rows-per-gpu 470000000 --steps 3 --warmup 1"),
+    "sec100": (600, f"{PY} bench.py --api --workload secondary --rows-per-gpu 970000000 --steps 2 --warmup 1"),
+    "sec2_one_gpu": (600, f"{PY} bench.py --api --workload secondary --gpus 2 --one-gpu --rows-per-gpu 235000000 --steps 3 --warmup 1"),
+    "snappy41": (400, f"{PY} bench.py --api --api-codec snappy --rows-per-gpu 400000000 --steps 3 --warmup 1"),
+    "snappy130": (600, f"{PY} bench.py --api --api-codec snappy --steps 2 --warmup 1"),
+    "lzo41": (400, f"{PY} bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 3 --warmup 1"),
+    "ipc2": (400, f"{PY} bench.py --gpus 2 --one-gpu --exchange ipc --rows-per-gpu 300000000 --steps 3 --warmup 1"),
+    "ipc4": (400, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --rows-per-gpu 150000000 --steps 3 --warmup 1"),
+    "ipc8": (600, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
+    "ipc4_host": (600, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --store host --rows-per-gpu 100000000 --steps 2 --warmup 1"),
+    "node": (600, f"{PY} bench.py --api --node --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
+    "netmerger": (400, f"{PY} benchmarks/run_configs.py netmerger --gb 2 --maps 64 --reducers 1"),
+    "prof_bench": (500, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- "
+                        "python3 bench.py --steps 3 --warmup 1"),
+    "prof_device_only": (400, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_device_only -o run -- "
+                              "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+}
+
+# PMC passes over one short device-only step: each pass stays within the per-block counter limits
+PMC_PROG = "python3 bench.py --device-only --rows-per-gpu 100000000 --steps 1 --warmup 0 --no-validate"
+PMC_PASSES = [
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAVE_CYCLES",
+    "FETCH_SIZE",
+    "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum",
+]
+for i, counters in enumerate(PMC_PASSES):
+    RECIPES[f"pmc{i + 1}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/pmc{i + 1} -o run -- {PMC_PROG}")
+
+
+def summarize(path: str, keys: list[str]) -> str:
+    line = None
+    try:
+        with open(path, errors="replace") as f:
+            for ln in f:
+                ln = ln.strip()
+                if ln.startswith("{") and ln.endswith("}"):
+                    line = ln
+    except OSError:
+        return ""
+    if line is None:
+        return ""
+    try:
+        d = json.loads(line)
+    except ValueError:
+        return line[:200]
+    out = {k: d.get(k) for k in ["value", "validated", "ms_per_step", *keys] if k in d}
+    return json.dumps(out)
+
+
+def run_step(tag: str, name: str, seconds: int, cmd: str, keys: list[str]) -> int:
+    os.makedirs(OUT, exist_ok=True)
+    log = os.path.join(OUT, f"{tag}_{name}.log")
+    err = os.path.join(OUT, f"{tag}_{name}.err")
+    env = dict(os.environ, PYTHONUNBUFFERED="1", TMPDIR="/tmp")
+    t0 = time.time()
+    print(f"== {name} ({seconds}s): {cmd}", flush=True)
+    with open(log, "w") as fo, open(err, "w") as fe:
+        p = subprocess.Popen(["bash", "-c", cmd], cwd=ROOT, stdout=fo, stderr=fe, env=env, start_new_session=True)
+        try:
+            rc = p.wait(timeout=seconds)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGTERM)
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+            rc = 124
+    dt = time.time() - t0
+    s = summarize(log, keys)
+    print(f"   rc={rc} {dt:.0f}s {s}", flush=True)
+    if rc != 0:
+        for path in (log, err):
+            try:
+                with open(path, errors="replace") as f:
+                    tail = f.readlines()[-25:]
+                print(f"   --- tail {os.path.basename(path)}", *tail, sep="   ", flush=True)
+            except OSError:
+                pass
+    return rc
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("steps", nargs="*", help="recipe names, in order: " + " ".join(RECIPES))
+    ap.add_argument("--tag", default="run", help="log file prefix under gpurun_out/")
+    ap.add_argument("--cmd", action="append", default=[], help="ad-hoc step NAME=SECONDS=COMMAND")
+    ap.add_argument("--keys", default="", help="extra JSON keys to print from each step's last JSON line")
+    ap.add_argument("--list", action="store_true")
+    a = ap.parse_args()
+    recipes = dict(RECIPES)
+    for c in a.cmd:
+        name, secs, cmd = c.split("=", 2)
+        recipes[name] = (int(secs), cmd)
+    if a.list:
+        for k, (t, c) in recipes.items():
+            print(f"{k:18s} {t:4d}s  {c}")
+        return 0
+    keys = [k for k in a.keys.split(",") if k]
+    for name in a.steps:
+        if name not in recipes:
+            print(f"unknown step {name}", file=sys.stderr)
+            return 2
+        t, cmd = recipes[name]
+        rc = run_step(a.tag, name, t, cmd, keys)
+        if rc != 0:
+            return rc
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
