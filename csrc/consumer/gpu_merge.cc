@@ -863,6 +863,38 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
 
 }  // namespace
 
+void ReduceTask::release_descriptors(const std::set<std::string>& hosts, const std::string& holder) {
+  if (hosts.empty() || !transport_) return;
+  struct Wait {  // outlives this call if a provider answers late
+    std::mutex m;
+    std::condition_variable c;
+    size_t left = 0;
+  };
+  auto w = std::make_shared<Wait>();
+  w->left = hosts.size();
+  for (const auto& h : hosts) {
+    FetchRequest req;
+    req.job_id = init_.job_id;
+    req.map_id = "*";
+    req.reduce_id = 0;
+    req.buf_len = kDescriptorRelease;
+    req.holder = holder;
+    fetch_begin();
+    transport_->fetch(h, req, nullptr, [this, w](const FetchAck&) {
+      {
+        std::lock_guard<std::mutex> g(w->m);
+        --w->left;
+        w->c.notify_all();
+      }
+      fetch_end();
+    });
+  }
+  std::unique_lock<std::mutex> lk(w->m);
+  // a provider that does not answer keeps the references until its backstop drops them
+  if (!w->c.wait_for(lk, std::chrono::seconds(10), [&] { return w->left == 0; }))
+    throw UdaError("descriptor release not acknowledged by " + std::to_string(w->left) + " provider(s)");
+}
+
 // Every reduce task of a Hadoop job usually runs in a fresh JVM (YarnChild), so what a warm process
 // keeps in its pools (HIP context, code objects, pinned rings and arenas, workspaces) a task would build
 // on its critical path: a 2 GB task went 27 -> 3.9 GB/s cold (profiles/r3_netmerger2.json). INIT comes
@@ -1873,6 +1905,26 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
+  // Descriptors are references the providers keep for this task (gpu/mof_cache.h): released when the
+  // task is done with them -- its merge finished, or it failed -- after the device has stopped
+  // reading the partitions (the merge stream is synchronized first).
+  const std::string holder = gpu::reducer_holder_id(init_.reduce_task_id);
+  struct DescRelease {
+    ReduceTask* t;
+    StreamGuard& sg;
+    const std::string& holder;
+    std::vector<std::string> descs;
+    std::set<std::string> hosts;
+    ~DescRelease() {
+      if (sg.s) (void)hipStreamSynchronize(sg.s);
+      for (const auto& d : descs) gpu::release_device_descriptor(d);
+      try {
+        t->release_descriptors(hosts, holder);
+      } catch (const std::exception& e) {
+        UDA_LOG(kWarn, "releasing descriptors: %s", e.what());
+      }
+    }
+  } desc_release{this, sg, holder, {}, {}};
   struct Part {
     const uint8_t* dptr = nullptr;
     int64_t part_len = 0;
@@ -1963,6 +2015,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       req.map_id = batch[i].map_id;
       req.reduce_id = batch[i].reduce_id;
       req.buf_len = kDescriptorFetch;
+      req.holder = holder;
+      desc_release.hosts.insert(batch[i].host);
       fetch_begin();
       transport_->fetch(batch[i].host, req, nullptr, [&, i](const FetchAck& a) {
         std::lock_guard<std::mutex> g(m);
@@ -1995,6 +2049,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
           (dp = gpu::try_resolve_device_descriptor(a.path, device, &why)) != nullptr) {
         part->dptr = dp;
         part->part_len = a.part_len;
+        desc_release.descs.push_back(a.path);
         ++descriptors;
       } else if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
         // not mappable here (another node, no IPC handle, import failure): fetch its bytes

@@ -104,6 +104,8 @@ class ReduceTask {
   // Device fetch (descriptors, merge in place). probe: return false before consuming anything if the
   // first MOFs are not device-resident (the caller then runs merge_gpu()).
   bool merge_gpu_device(bool probe);
+  // Tell every provider in `hosts` that `holder` (this task) is done with its descriptors.
+  void release_descriptors(const std::set<std::string>& hosts, const std::string& holder);
   // GPU backend: started at INIT on prewarm_thr_ (mapred.uda.gpu.prewarm): HIP context, SDMA engine,
   // code objects, a pooled workspace with its pinned D2H ring and early stager, pinned fetch-arena
   // blocks, all while the FETCHes are still to come (reduce slow-start). The merge joins it first.

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "device_engine.h"
+#include "uda/node_registry.h"
 
 namespace uda {
 namespace gpu {
@@ -50,10 +51,17 @@ std::vector<std::string> split_at(const std::string& s) {
   }
 }
 
-// Process-wide map of opened IPC handles (a handle is opened once per process).
+// Process-wide map of opened IPC handles (a handle is opened once per process). Registered stores
+// stay mapped for the process's life; leased ones (a provider HBM store entry) are counted per
+// resolved descriptor and closed when the last one is released.
+struct Mapping {
+  uint8_t* base = nullptr;
+  int leased_refs = 0;
+  bool leased = false;
+};
 std::mutex g_ipc_mu;
-std::map<std::string, uint8_t*>& opened() {
-  static auto* m = new std::map<std::string, uint8_t*>();  // mappings live until process exit
+std::map<std::string, Mapping>& opened() {
+  static auto* m = new std::map<std::string, Mapping>();
   return *m;
 }
 }  // namespace
@@ -111,18 +119,41 @@ size_t ipc_safe_bytes(size_t bytes) {
   return bytes + ((1ull << 32) - r) + (64ull << 20);  // remainder 64 MiB
 }
 
-std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc) {
+std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc, bool leased) {
   char head[128];
   std::snprintf(head, sizeof(head), "hbm@%s@%d@%d@%llx@", node_id().c_str(), device, (int)getpid(),
                 (unsigned long long)(uintptr_t)ptr);
-  return std::string(head) + ipc.handle_hex + "@" + std::to_string((long long)(ptr - ipc.base));
+  return std::string(head) + ipc.handle_hex + "@" + std::to_string((long long)(ptr - ipc.base)) + (leased ? "@L" : "");
+}
+
+std::string reducer_holder_id(const std::string& task) {
+  const int pid = (int)getpid();
+  return node_id() + ":" + std::to_string(pid) + ":" + std::to_string((unsigned long long)process_start_ticks(pid)) +
+         ":" + task;
+}
+
+int open_ipc_mappings() {
+  std::lock_guard<std::mutex> g(g_ipc_mu);
+  return (int)opened().size();
+}
+
+void release_device_descriptor(const std::string& desc) {
+  const auto f = split_at(desc);
+  if (f.size() != 8 || f[7] != "L" || f[5] == "-" || std::atoi(f[3].c_str()) == (int)getpid()) return;
+  std::lock_guard<std::mutex> g(g_ipc_mu);
+  auto it = opened().find(f[5]);
+  if (it == opened().end() || !it->second.leased) return;
+  if (--it->second.leased_refs > 0) return;
+  (void)hipIpcCloseMemHandle(it->second.base);
+  (void)hipGetLastError();
+  opened().erase(it);
 }
 
 bool is_device_descriptor(const std::string& s) { return s.rfind("hbm@", 0) == 0; }
 
 const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_device, std::string* why) {
   const auto f = split_at(desc);
-  if (f.size() != 7 || f[0] != "hbm") {
+  if ((f.size() != 7 && !(f.size() == 8 && f[7] == "L")) || f[0] != "hbm") {
     if (why) *why = "malformed device descriptor '" + desc + "'";
     return nullptr;
   }
@@ -152,6 +183,7 @@ const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_dev
       if (why) *why = "provider allocation is not IPC-shareable";
       return nullptr;
     }
+    const bool leased = f.size() == 8;
     std::lock_guard<std::mutex> g(g_ipc_mu);
     auto it = opened().find(f[5]);
     if (it == opened().end()) {
@@ -162,9 +194,13 @@ const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_dev
       }
       void* p = nullptr;
       HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      it = opened().emplace(f[5], static_cast<uint8_t*>(p)).first;
+      Mapping mp;
+      mp.base = static_cast<uint8_t*>(p);
+      mp.leased = leased;
+      it = opened().emplace(f[5], mp).first;
     }
-    return it->second + std::strtoll(f[6].c_str(), nullptr, 10);
+    if (leased) it->second.leased_refs++;
+    return it->second.base + std::strtoll(f[6].c_str(), nullptr, 10);
   } catch (const std::exception& e) {
     if (why) *why = e.what();
     return nullptr;

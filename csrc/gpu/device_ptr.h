@@ -36,7 +36,10 @@ bool ipc_size_ok(size_t bytes);
 const std::string& node_id();
 size_t ipc_safe_bytes(size_t bytes);
 
-std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc);
+// leased: the provider frees the allocation once every holder released it (its HBM store), so a
+// reducer in another process closes its IPC mapping when it releases its last descriptor into it;
+// registered MOFs (not leased) stay mapped for the process's life.
+std::string make_device_descriptor(int device, const uint8_t* ptr, const IpcExport& ipc, bool leased = false);
 bool is_device_descriptor(const std::string& s);
 // Device address (usable on `my_device`) of a descriptor, or nullptr (reason in *why) when it cannot
 // be used here: another node, no IPC handle, peer access impossible, import failure. Callers then
@@ -44,6 +47,14 @@ bool is_device_descriptor(const std::string& s);
 const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_device, std::string* why);
 // Same, throwing instead of returning nullptr.
 const uint8_t* resolve_device_descriptor(const std::string& desc, int my_device);
+// A resolved leased descriptor is done with: its IPC mapping is closed when no other descriptor of
+// this process uses it.
+void release_device_descriptor(const std::string& desc);
+// Identity of a reducer that holds descriptors ("<node>:<pid>:<start ticks>:<task>"): the provider
+// keeps what it hands out until this holder releases it, or its process is gone.
+std::string reducer_holder_id(const std::string& task);
+// IPC mappings this process holds open (tests).
+int open_ipc_mappings();
 // Copy device memory at `src` (any device) to host `dst`.
 void copy_device_to_host(void* dst, const void* src, int64_t bytes);
 

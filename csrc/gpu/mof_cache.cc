@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -15,6 +16,7 @@
 #include "sdma.h"
 #include "uda/aio.h"
 #include "uda/log.h"
+#include "uda/node_registry.h"
 
 namespace uda {
 namespace gpu {
@@ -24,7 +26,44 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 int64_t align_io(int64_t v) { return (v + kAioAlignment - 1) / kAioAlignment * kAioAlignment; }
+
+// holder id "<node>:<pid>:<start ticks>:<task>" (reducer_holder_id in device_ptr.h)
+bool holder_alive(const std::string& h, double last, double now, double lease_s) {
+  const size_t a = h.find(':');
+  const size_t b = a == std::string::npos ? a : h.find(':', a + 1);
+  const size_t c = b == std::string::npos ? b : h.find(':', b + 1);
+  if (c == std::string::npos) return now - last < lease_s;  // not ours to check: lease only
+  if (h.compare(0, a, node_id()) != 0) return now - last < lease_s;  // another node
+  const int pid = std::atoi(h.substr(a + 1, b - a - 1).c_str());
+  const uint64_t start = std::strtoull(h.substr(b + 1, c - b - 1).c_str(), nullptr, 10);
+  return process_running(pid, start);
+}
 }  // namespace
+
+struct MofCache::Loader {
+  enum State { kFree = 0, kReading = 1, kCopying = 2 };
+  struct Slot {
+    State state = kFree;
+    std::shared_ptr<Entry> e;
+    int64_t off = 0, len = 0, result = 0;
+    bool read_done = false;
+    hsa_signal_t sig{};
+    hipEvent_t ev = nullptr;
+  };
+  int device = 0;
+  std::thread thr;
+  std::condition_variable cv;  // with MofCache::mu_
+  bool stop = false;
+  std::deque<std::shared_ptr<Entry>> pending;  // to allocate + open
+  std::deque<std::shared_ptr<Entry>> active;   // unread bytes left, read in turn
+  std::vector<Slot> slots;
+  std::unique_ptr<AsyncIO> aio;
+  uint8_t* ring = nullptr;
+  SdmaEngine* sdma = nullptr;
+  hipStream_t stream = nullptr;
+  bool ready = false;
+  std::string setup_error;
+};
 
 MofCache::MofCache(const Options& o) : opt_(o) {
   opt_.chunk_bytes = align_io(std::max<int64_t>(opt_.chunk_bytes, 1 << 20));
@@ -35,65 +74,123 @@ MofCache::MofCache(const Options& o) : opt_(o) {
 }
 
 MofCache::~MofCache() {
+  std::vector<std::unique_ptr<Loader>> ls;
   {
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& kv : entries_)
-      if (!kv.second->loading) free_entry(kv.second.get());
-    entries_.clear();
+    for (auto& kv : loaders_) {
+      kv.second->stop = true;
+      kv.second->cv.notify_all();
+    }
   }
-  std::lock_guard<std::mutex> g(load_mu_);
-  if (aio_) aio_->drain();
-  for (auto e : ev_) (void)hipEventDestroy(e);
-  for (auto s : streams_)
-    if (s) (void)hipStreamDestroy(s);
-  if (ring_) pinned_host_free(ring_);
+  for (auto& kv : loaders_)
+    if (kv.second->thr.joinable()) kv.second->thr.join();
+  std::lock_guard<std::mutex> g(mu_);
+  entries_.clear();
+  loaders_.clear();
 }
 
-void MofCache::free_entry(Entry* e) {
-  if (e->dptr) (void)hipFree(e->dptr);
-  e->dptr = nullptr;
+MofCache::Ref MofCache::ref_of(const Entry& e) const {
+  Ref r;
+  r.data = e.dptr;
+  r.len = e.len;
+  r.device = e.device;
+  r.ipc = e.ipc;
+  return r;
+}
+
+bool MofCache::evictable(Entry& e, double now) {
+  if (e.loading) return false;
+  for (auto it = e.holders.begin(); it != e.holders.end();) {
+    if (holder_alive(it->first, it->second.second, now, opt_.lease_s)) {
+      ++it;
+    } else {
+      UDA_LOG(kInfo, "provider HBM store: holder %s of %s is gone; its references dropped", it->first.c_str(),
+              e.path.c_str());
+      st_.holders_reaped++;
+      it = e.holders.erase(it);
+    }
+  }
+  return e.job_done || e.holders.empty();
+}
+
+void MofCache::erase_entry(const std::string& path) {
+  auto it = entries_.find(path);
+  if (it == entries_.end()) return;
+  used_[it->second->device] -= std::max<int64_t>(it->second->len, 1);
+  entries_.erase(it);  // the HBM goes when the last in-flight chunk of it is done
 }
 
 bool MofCache::make_room(int device, int64_t bytes, double now) {
   if (bytes > per_device_) return false;
   while (used_[device] + bytes > per_device_) {
-    std::map<std::string, std::shared_ptr<Entry>>::iterator victim = entries_.end();
-    for (auto it = entries_.begin(); it != entries_.end(); ++it) {
-      Entry& e = *it->second;
-      if (e.device != device || e.loading) continue;
-      if (!e.job_done && now - e.last_served < opt_.lease_s) continue;  // a reducer may still read it
-      if (victim == entries_.end() || e.last_served < victim->second->last_served) victim = it;
+    // finished jobs first, then unreferenced entries, least recently served first
+    std::shared_ptr<Entry> victim;
+    for (auto& kv : entries_) {
+      Entry& e = *kv.second;
+      if (e.device != device || !evictable(e, now)) continue;
+      if (!victim || (e.job_done && !victim->job_done) ||
+          (e.job_done == victim->job_done && e.last_served < victim->last_served))
+        victim = kv.second;
     }
-    if (victim == entries_.end()) return false;
-    UDA_LOG(kDebug, "provider HBM store: evicting %s (%ld bytes)", victim->first.c_str(), (long)victim->second->len);
-    used_[device] -= victim->second->len;
-    free_entry(victim->second.get());
-    entries_.erase(victim);
+    if (!victim) return false;
+    UDA_LOG(kDebug, "provider HBM store: evicting %s (%ld bytes)", victim->path.c_str(), (long)victim->len);
+    erase_entry(victim->path);
     st_.evictions++;
   }
   return true;
 }
 
-bool MofCache::acquire(const std::string& job, const std::string& path, Ref* out, std::string* why) {
+void MofCache::collect_ready(Entry& e, std::vector<Fire>* fire) {
+  for (auto it = e.waiters.begin(); it != e.waiters.end();) {
+    if (it->need_end <= e.landed) {
+      fire->push_back(Fire{std::move(it->ready), true, ref_of(e), std::string()});
+      it = e.waiters.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+void MofCache::fail_entry(Entry& e, const std::string& why, std::vector<Fire>* fire) {
+  if (e.failed) return;
+  e.failed = true;
+  e.loading = false;
+  e.error = why;
+  UDA_LOG(kWarn, "provider HBM store: loading %s failed: %s", e.path.c_str(), why.c_str());
+  for (auto& w : e.waiters) fire->push_back(Fire{std::move(w.ready), false, Ref(), why});
+  e.waiters.clear();
+  st_.declined++;
+  if (e.fd >= 0 && e.reads_in_flight == 0) {
+    ::close(e.fd);
+    e.fd = -1;
+  }
+  auto it = entries_.find(e.path);
+  if (it != entries_.end() && it->second.get() == &e) erase_entry(e.path);
+}
+
+bool MofCache::acquire_async(const std::string& job, const std::string& path, const std::string& holder,
+                             int64_t need_end, Ready ready, std::string* why) {
   if (!enabled()) {
     if (why) *why = "provider HBM store disabled";
     return false;
   }
   std::unique_lock<std::mutex> lk(mu_);
-  for (;;) {
-    auto it = entries_.find(path);
-    if (it == entries_.end()) break;
+  const double now = now_s();
+  auto it = entries_.find(path);
+  if (it != entries_.end()) {
     std::shared_ptr<Entry> e = it->second;
-    if (e->loading) {
-      cv_.wait(lk);
-      continue;
-    }
-    e->last_served = now_s();
+    e->last_served = now;
+    auto& h = e->holders[holder];
+    h.first++;
+    h.second = now;
     st_.hits++;
-    out->data = static_cast<const uint8_t*>(e->dptr);
-    out->len = e->len;
-    out->device = e->device;
-    out->ipc = e->ipc;
+    if (e->landed >= need_end || !e->loading) {
+      const Ref r = ref_of(*e);
+      lk.unlock();
+      ready(true, r, std::string());
+    } else {
+      e->waiters.push_back(Waiter{need_end, std::move(ready)});
+    }
     return true;
   }
   struct stat sb;
@@ -106,142 +203,88 @@ bool MofCache::acquire(const std::string& job, const std::string& path, Ref* out
   int device = opt_.devices[0];
   for (int d : opt_.devices)
     if (per_device_ - used_[d] > per_device_ - used_[device]) device = d;
-  if (!make_room(device, std::max<int64_t>(len, 1), now_s())) {
-    if (why) *why = "provider HBM budget exhausted (all resident MOFs leased)";
+  if (!make_room(device, std::max<int64_t>(len, 1), now)) {
+    if (why) *why = "provider HBM budget exhausted (every resident MOF is held by a reducer)";
     st_.declined++;
     return false;
   }
   auto e = std::make_shared<Entry>();
   e->job = job;
+  e->path = path;
   e->device = device;
   e->len = len;
+  e->last_served = e->t_start = now;
+  e->holders[holder] = {1, now};
+  e->waiters.push_back(Waiter{need_end, std::move(ready)});
   used_[device] += std::max<int64_t>(len, 1);
   entries_[path] = e;
-  lk.unlock();
-  const double t0 = now_s();
-  try {
-    load(path, e.get());
-  } catch (const std::exception& ex) {
-    lk.lock();
-    used_[device] -= std::max<int64_t>(len, 1);
-    free_entry(e.get());
-    entries_.erase(path);
-    st_.declined++;
-    cv_.notify_all();
-    if (why) *why = ex.what();
-    UDA_LOG(kWarn, "provider HBM store: loading %s failed: %s", path.c_str(), ex.what());
-    return false;
+  std::unique_ptr<Loader>& L = loaders_[device];
+  if (!L) {
+    L.reset(new Loader);
+    L->device = device;
+    Loader* lp = L.get();
+    L->thr = std::thread([this, lp] { loader_main(lp); });
   }
-  lk.lock();
-  e->loading = false;
-  e->last_served = now_s();
-  st_.loads++;
-  st_.bytes_loaded += len;
-  st_.load_ms += (now_s() - t0) * 1000.0;
-  cv_.notify_all();
-  out->data = static_cast<const uint8_t*>(e->dptr);
-  out->len = e->len;
-  out->device = e->device;
-  out->ipc = e->ipc;
+  L->pending.push_back(e);
+  L->cv.notify_all();
   return true;
 }
 
-// Whole file -> HBM: reads of chunk_bytes (O_DIRECT, 4 KiB aligned) into the pinned ring with up to
-// `chunks` in flight; each landed chunk is copied H2D on the device's stream, and its ring slot is
-// reused once that copy finished.
-void MofCache::load(const std::string& path, Entry* e) {
-  std::lock_guard<std::mutex> g(load_mu_);
-  const int dev_index = (int)(std::find(opt_.devices.begin(), opt_.devices.end(), e->device) - opt_.devices.begin());
-  HIP_CHECK(hipSetDevice(e->device));
-  if (!aio_) {
-    AsyncIO::Options ao;
-    ao.threads = 4;
-    ao.queue_depth = 2 * opt_.chunks;
-    aio_ = AsyncIO::create(ao);
-    ring_ = static_cast<uint8_t*>(
-        hip_host_alloc_on_node((size_t)(opt_.chunk_bytes * opt_.chunks), device_numa_node(opt_.devices[0])));
-    ev_.resize((size_t)opt_.chunks, nullptr);
-    for (auto& ev : ev_) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    streams_.assign(opt_.devices.size(), nullptr);
-  }
-  if (!streams_[(size_t)dev_index]) HIP_CHECK(hipStreamCreateWithFlags(&streams_[(size_t)dev_index], hipStreamNonBlocking));
-  hipStream_t s = streams_[(size_t)dev_index];
-  HIP_CHECK(hipMalloc(&e->dptr, ipc_safe_bytes((size_t)std::max<int64_t>(e->len, 1))));
-  e->ipc = ipc_export(e->dptr);
-  bool direct = opt_.odirect;
-  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
-  if (fd < 0 && direct) {
-    direct = false;
-    fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
-  }
-  if (fd < 0) throw std::runtime_error("cannot open " + path + ": " + strerror(errno));
-  struct FdGuard {
-    int fd;
-    ~FdGuard() { ::close(fd); }
-  } fg{fd};
-  const int64_t C = opt_.chunk_bytes, n = (e->len + C - 1) / C;
-  const int K = opt_.chunks;
-  std::vector<int64_t> result((size_t)n, 0);
-  std::vector<char> done((size_t)n, 0);
-  std::vector<char> pending((size_t)K, 0);
+bool MofCache::acquire(const std::string& job, const std::string& path, const std::string& holder, Ref* out,
+                       std::string* why) {
   std::mutex m;
   std::condition_variable c;
-  int64_t next_submit = 0, next_finish = 0;
-  try {
-    while (next_finish < n) {
-      while (next_submit < n && next_submit - next_finish < K) {
-        const int slot = (int)(next_submit % K);
-        if (pending[(size_t)slot]) {  // the slot's previous H2D must have read it
-          HIP_CHECK(hipEventSynchronize(ev_[(size_t)slot]));
-          pending[(size_t)slot] = 0;
-        }
-        const int64_t off = next_submit * C;
-        const int64_t want = std::min(C, e->len - off);
-        const int64_t i = next_submit;
-        aio_->read(fd, off, direct ? align_io(want) : want, ring_ + (int64_t)slot * C, [&, i](int64_t r) {
-          std::lock_guard<std::mutex> lg(m);
-          result[(size_t)i] = r;
-          done[(size_t)i] = 1;
-          c.notify_all();
-        });
-        ++next_submit;
-      }
-      {
-        std::unique_lock<std::mutex> lk(m);
-        c.wait(lk, [&] { return done[(size_t)next_finish] != 0; });
-      }
-      const int64_t off = next_finish * C;
-      const int64_t want = std::min(C, e->len - off);
-      if (result[(size_t)next_finish] < want)
-        throw std::runtime_error("short read from " + path + " at " + std::to_string(off));
-      const int slot = (int)(next_finish % K);
-      HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(e->dptr) + off, ring_ + (int64_t)slot * C, (size_t)want,
-                               hipMemcpyHostToDevice, s));
-      HIP_CHECK(hipEventRecord(ev_[(size_t)slot], s));
-      pending[(size_t)slot] = 1;
-      ++next_finish;
-    }
-    HIP_CHECK(hipStreamSynchronize(s));
-  } catch (...) {
-    aio_->drain();  // no read may land in the ring after we leave
-    (void)hipStreamSynchronize(s);
-    throw;
+  bool done = false, ok = false;
+  std::string err;
+  if (!acquire_async(job, path, holder, INT64_MAX / 2, [&](bool k, const Ref& r, const std::string& w) {
+        std::lock_guard<std::mutex> g(m);
+        ok = k;
+        if (k) *out = r;
+        err = w;
+        done = true;
+        c.notify_all();
+      }, why))
+    return false;
+  std::unique_lock<std::mutex> lk(m);
+  c.wait(lk, [&] { return done; });
+  if (!ok && why) *why = err;
+  return ok;
+}
+
+void MofCache::release(const std::string& path, const std::string& holder) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = entries_.find(path);
+  if (it == entries_.end()) return;
+  auto h = it->second->holders.find(holder);
+  if (h == it->second->holders.end()) return;
+  st_.releases++;
+  if (--h->second.first <= 0) it->second->holders.erase(h);
+}
+
+void MofCache::release_holder(const std::string& job, const std::string& holder) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& kv : entries_) {
+    Entry& e = *kv.second;
+    if (e.job != job) continue;
+    auto h = e.holders.find(holder);
+    if (h == e.holders.end()) continue;
+    st_.releases += h->second.first;
+    e.holders.erase(h);
   }
 }
 
 void MofCache::job_over(const std::string& job) {
   std::lock_guard<std::mutex> g(mu_);
-  for (auto it = entries_.begin(); it != entries_.end();) {
-    Entry& e = *it->second;
-    if (e.job == job && !e.loading) {
-      used_[e.device] -= std::max<int64_t>(e.len, 1);
-      free_entry(&e);
-      st_.evictions++;
-      it = entries_.erase(it);
-    } else {
-      if (e.job == job) e.job_done = true;
-      ++it;
-    }
+  std::vector<std::string> drop;
+  for (auto& kv : entries_) {
+    Entry& e = *kv.second;
+    if (e.job != job) continue;
+    e.job_done = true;
+    if (!e.loading) drop.push_back(kv.first);
+  }
+  for (const auto& p : drop) {
+    erase_entry(p);
+    st_.evictions++;
   }
 }
 
@@ -250,7 +293,244 @@ MofCache::Stats MofCache::stats() {
   Stats s = st_;
   s.resident_bytes = 0;
   for (auto& kv : used_) s.resident_bytes += kv.second;
+  s.holders = 0;
+  for (auto& kv : entries_)
+    for (auto& h : kv.second->holders) s.holders += h.second.first;
+  if (busy_loaders_ > 0) s.load_wall_ms += (now_s() - busy_since_) * 1000.0;
   return s;
+}
+
+// One loader per GPU: allocation + open of new entries, O_DIRECT chunk reads round-robin over the
+// files being loaded, SDMA H2D of every landed chunk, and the readiness of each file's prefix.
+void MofCache::loader_main(Loader* L) {
+  const int C_slots = opt_.chunks;
+  const int64_t C = opt_.chunk_bytes;
+  std::vector<Fire> fire;
+  try {
+    const int node = device_numa_node(L->device);
+    bind_thread_to_numa(node);
+    HIP_CHECK(hipSetDevice(L->device));
+    AsyncIO::Options ao;
+    ao.threads = 2;
+    ao.queue_depth = 2 * C_slots;
+    L->aio = AsyncIO::create(ao);
+    L->ring = static_cast<uint8_t*>(pinned_host_alloc((size_t)(C * C_slots), node));
+    try {
+      L->sdma = &SdmaEngine::for_device(L->device);
+    } catch (const std::exception& ex) {
+      UDA_LOG(kWarn, "provider HBM store: no SDMA engine on device %d (%s); hipMemcpyAsync", L->device, ex.what());
+      L->sdma = nullptr;
+    }
+    L->slots.resize((size_t)C_slots);
+    for (auto& s : L->slots) {
+      if (L->sdma) {
+        s.sig = L->sdma->make_signal();
+        SdmaEngine::arm(s.sig, 0);
+      } else {
+        HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      }
+    }
+    if (!L->sdma) HIP_CHECK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+    L->ready = true;
+  } catch (const std::exception& ex) {
+    L->setup_error = ex.what();
+  }
+
+  std::unique_lock<std::mutex> lk(mu_);
+  bool was_busy = false;
+  for (;;) {
+    if (L->stop) {  // the store is going away: nothing new starts, loads in progress fail
+      for (auto& e : L->pending) fail_entry(*e, "provider HBM store stopped", &fire);
+      for (auto& e : L->active) fail_entry(*e, "provider HBM store stopped", &fire);
+      L->pending.clear();
+      L->active.clear();
+    }
+    // ---- new entries: HBM allocation (resident in the HBM budget) and the file, outside the lock
+    while (!L->pending.empty()) {
+      std::shared_ptr<Entry> e = L->pending.front();
+      L->pending.pop_front();
+      std::string err = L->setup_error;
+      std::unique_ptr<DeviceBuffer> mem;
+      int fd = -1;
+      bool direct = opt_.odirect;
+      IpcExport ipc;
+      lk.unlock();
+      if (err.empty()) {
+        try {
+          mem.reset(new DeviceBuffer((size_t)std::max<int64_t>(e->len, 1), /*resident=*/true));
+          ipc = ipc_export(mem->as<uint8_t>());
+          fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
+          if (fd < 0 && direct) {
+            direct = false;
+            fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC);
+          }
+          if (fd < 0) err = "cannot open " + e->path + ": " + strerror(errno);
+        } catch (const std::exception& ex) {
+          err = ex.what();
+        }
+      }
+      lk.lock();
+      if (!err.empty() || e->failed) {
+        if (fd >= 0) ::close(fd);
+        fail_entry(*e, err.empty() ? e->error : err, &fire);
+        continue;
+      }
+      e->mem = std::move(mem);
+      e->dptr = e->mem->as<uint8_t>();
+      e->ipc = ipc;
+      e->fd = fd;
+      e->direct = direct;
+      if (e->len == 0) {
+        e->loading = false;
+        collect_ready(*e, &fire);
+      } else {
+        L->active.push_back(e);
+      }
+    }
+    // ---- landed reads: issue their H2D copies
+    for (int i = 0; i < C_slots; ++i) {
+      Loader::Slot& s = L->slots[(size_t)i];
+      if (s.state != Loader::kReading || !s.read_done) continue;
+      Entry& e = *s.e;
+      if (e.failed || s.result < s.len) {
+        if (!e.failed) fail_entry(e, "short read from " + e.path + " at " + std::to_string(s.off), &fire);
+        if (--e.reads_in_flight == 0 && e.fd >= 0 && e.failed) {
+          ::close(e.fd);
+          e.fd = -1;
+        }
+        s = Loader::Slot{Loader::kFree, nullptr, 0, 0, 0, false, s.sig, s.ev};
+        continue;
+      }
+      try {
+        if (L->sdma) {
+          SdmaEngine::arm(s.sig, 1);
+          L->sdma->copy_h2d(const_cast<uint8_t*>(e.dptr) + s.off, L->ring + (int64_t)i * C, (size_t)s.len, s.sig);
+        } else {
+          HIP_CHECK(hipMemcpyAsync(const_cast<uint8_t*>(e.dptr) + s.off, L->ring + (int64_t)i * C, (size_t)s.len,
+                                   hipMemcpyHostToDevice, L->stream));
+          HIP_CHECK(hipEventRecord(s.ev, L->stream));
+        }
+        s.state = Loader::kCopying;
+      } catch (const std::exception& ex) {
+        fail_entry(e, ex.what(), &fire);
+        --e.reads_in_flight;
+        s = Loader::Slot{Loader::kFree, nullptr, 0, 0, 0, false, s.sig, s.ev};
+      }
+    }
+    // ---- finished copies: the file's landed prefix grows; waiters whose partition is in are answered
+    bool copying = false;
+    for (int i = 0; i < C_slots; ++i) {
+      Loader::Slot& s = L->slots[(size_t)i];
+      if (s.state != Loader::kCopying) continue;
+      bool done = false, bad = false;
+      if (L->sdma) {
+        const hsa_signal_value_t v = hsa_signal_load_scacquire(s.sig);
+        done = v <= 0;
+        bad = v < 0;
+      } else {
+        const hipError_t q = hipEventQuery(s.ev);
+        done = q != hipErrorNotReady;
+        bad = done && q != hipSuccess;
+      }
+      if (!done) {
+        copying = true;
+        continue;
+      }
+      std::shared_ptr<Entry> ep = s.e;
+      Entry& e = *ep;
+      --e.reads_in_flight;
+      if (bad) {
+        fail_entry(e, "H2D copy of " + e.path + " failed", &fire);
+        if (L->sdma) SdmaEngine::arm(s.sig, 0);
+      } else if (!e.failed) {
+        e.done_chunks[s.off] = s.len;
+        for (auto it = e.done_chunks.begin(); it != e.done_chunks.end() && it->first == e.landed;
+             it = e.done_chunks.erase(it))
+          e.landed += it->second;
+        collect_ready(e, &fire);
+        if (e.landed >= e.len) {
+          e.loading = false;
+          st_.loads++;
+          st_.bytes_loaded += e.len;
+          st_.load_ms += (now_s() - e.t_start) * 1000.0;
+          collect_ready(e, &fire);
+        }
+      }
+      if ((e.failed || !e.loading) && e.reads_in_flight == 0 && e.fd >= 0) {
+        ::close(e.fd);
+        e.fd = -1;
+      }
+      if (e.job_done && !e.loading && !e.failed) {  // JOB_OVER came while it was loading
+        erase_entry(e.path);
+        st_.evictions++;
+      }
+      s = Loader::Slot{Loader::kFree, nullptr, 0, 0, 0, false, s.sig, s.ev};
+    }
+    // ---- free slots: the next chunk of each file being loaded, in turn
+    struct Submit {
+      int slot, fd;
+      int64_t off, len;
+    };
+    std::vector<Submit> subs;
+    for (int i = 0; i < C_slots && !L->active.empty(); ++i) {
+      Loader::Slot& s = L->slots[(size_t)i];
+      if (s.state != Loader::kFree) continue;
+      std::shared_ptr<Entry> e;
+      while (!L->active.empty() && !e) {
+        e = L->active.front();
+        L->active.pop_front();
+        if (e->failed || e->next_read >= e->len) e.reset();
+      }
+      if (!e) break;
+      const int64_t off = e->next_read, want = std::min(C, e->len - off);
+      e->next_read += want;
+      e->reads_in_flight++;
+      if (e->next_read < e->len) L->active.push_back(e);
+      s.state = Loader::kReading;
+      s.e = e;
+      s.off = off;
+      s.len = want;
+      s.read_done = false;
+      s.result = 0;
+      subs.push_back(Submit{i, e->fd, off, e->direct ? align_io(want) : want});
+    }
+    const bool busy = !L->active.empty() || !subs.empty() || copying ||
+                      std::any_of(L->slots.begin(), L->slots.end(), [](const Loader::Slot& s) { return s.state != 0; });
+    if (busy != was_busy) {  // wall time with any loader busy
+      if (busy && busy_loaders_++ == 0) busy_since_ = now_s();
+      if (!busy && --busy_loaders_ == 0) st_.load_wall_ms += (now_s() - busy_since_) * 1000.0;
+      was_busy = busy;
+    }
+    if (!subs.empty() || !fire.empty()) {
+      lk.unlock();
+      for (const Submit& sb : subs) {
+        Loader::Slot* sp = &L->slots[(size_t)sb.slot];
+        L->aio->read(sb.fd, sb.off, sb.len, L->ring + (int64_t)sb.slot * C, [this, L, sp](int64_t r) {
+          std::lock_guard<std::mutex> g(mu_);
+          sp->result = r;
+          sp->read_done = true;
+          L->cv.notify_all();
+        });
+      }
+      for (Fire& f : fire) f.ready(f.ok, f.ref, f.why);
+      fire.clear();
+      lk.lock();
+      continue;
+    }
+    if (L->stop && !busy && L->pending.empty()) break;
+    if (copying)
+      L->cv.wait_for(lk, std::chrono::microseconds(200));  // SDMA completions are polled
+    else if (L->pending.empty())
+      L->cv.wait_for(lk, std::chrono::milliseconds(50));
+  }
+  lk.unlock();
+  if (L->aio) L->aio->drain();
+  for (auto& s : L->slots) {
+    if (L->sdma && s.sig.handle) L->sdma->destroy_signal(s.sig);
+    if (s.ev) (void)hipEventDestroy(s.ev);
+  }
+  if (L->stream) (void)hipStreamDestroy(L->stream);
+  if (L->ring) pinned_host_free(L->ring);
 }
 
 }  // namespace gpu

@@ -2,30 +2,42 @@
 //
 // Reference: the DataEngine resolves (job, map, reduce) through getPathUda on first touch and then
 // reads the partition chunk by chunk from the MOF file with O_DIRECT AIO for every request
-// (src/MOFServer/IndexInfo.cc:238-274 process_shuffle_request, :304-335 aio_read_chunk_data).
+// (src/MOFServer/IndexInfo.cc:238-274 process_shuffle_request, :304-335 aio_read_chunk_data); its
+// fd cache is refcounted by in-flight reads (:195-233) and a chunk is released only when the SEND
+// that used it completed (:276-301, src/DataNet/RDMAServer.cc:200-213).
 //
-// MI355X design: on the first descriptor fetch that touches a MOF file, the whole file is read once
-// (io_uring O_DIRECT into a NUMA-local pinned chunk ring, a window of reads in flight) and copied
-// into an HBM allocation of its own (hipMemcpyAsync per chunk, i.e. the SDMA engines), exportable
-// over hipIpc. Every later fetch of any of its partitions is answered with a device descriptor, so
-// reducers on the node merge the partitions where they lie (xGMI reads from another GPU) and the
-// file is read from disk once instead of once per reducer. MOFs are striped over the configured
-// GPUs (the one with the most free budget takes the next file).
+// MI355X design: the first descriptor fetch that touches a MOF file makes it resident in HBM (an
+// allocation of its own, exportable over hipIpc); every fetch of any of its partitions is answered
+// with a device descriptor, so reducers on the node merge the partitions where they lie (xGMI
+// reads from another GPU) and the file is read from disk once instead of once per reducer.
 //
-// Lifetime: a reducer may read a served partition long after the descriptor went out (there is no
-// release message in the protocol), so an entry is evictable only when its job ended (JOB_OVER from
-// the provider plugin) or when it has not been served for `lease_s` seconds. When the budget is
-// exhausted and nothing is evictable, acquire() declines and the provider answers "not device
-// resident": the reducer falls back to byte fetches from the file (never a wrong answer).
+// Loading: one loader thread per GPU, each with its own io_uring reads (O_DIRECT, 4 KiB aligned)
+// into a pinned chunk ring on that GPU's NUMA node and SDMA H2D copies. A loader reads the chunks of
+// every file it is loading in turn, so all files of a job advance together; since a MOF holds its
+// partitions in order, partition r of every file lands at about the same time and reduce task r
+// can start as soon as its partitions are in (a fetch is answered once the bytes up to the end of
+// its partition have landed, not the whole file).
+//
+// Lifetime: a descriptor handed out is a reference, held by the reducer that fetched it (holder id:
+// node, pid, process start time, task) until it releases it -- when its merge has consumed the
+// partitions, or when the task ends or fails. An entry with holders is never evicted, whatever the
+// budget pressure; entries of finished jobs (JOB_OVER) go first, then unreferenced ones by LRU.
+// Backstop for reducers that die without releasing: a holder on this node whose process is gone is
+// dropped; a holder on another node that has not fetched from the entry for `lease_s` is dropped.
+// When the budget is exhausted and nothing is evictable, the fetch is declined ("not device
+// resident") and the reducer fetches the partition's bytes instead: never a wrong answer.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "device_ptr.h"
@@ -34,15 +46,17 @@ namespace uda {
 class AsyncIO;
 namespace gpu {
 
+class DeviceBuffer;
+
 class MofCache {
  public:
   struct Options {
     int64_t capacity = 0;           // HBM bytes over all devices (mapred.uda.provider.hbm.bytes); 0 = off
     std::vector<int> devices{0};    // GPUs the MOFs are striped over (mapred.uda.provider.hbm.devices)
     int64_t chunk_bytes = 16 << 20;  // disk read granule
-    int chunks = 8;                  // reads in flight
+    int chunks = 16;                 // reads + copies in flight per loader
     bool odirect = true;
-    double lease_s = 600;            // an entry served within this many seconds is never evicted
+    double lease_s = 600;            // a holder on another node idle this long is presumed dead
   };
   struct Ref {
     const uint8_t* data = nullptr;  // device address of the file's first byte
@@ -52,8 +66,12 @@ class MofCache {
   };
   struct Stats {
     int64_t loads = 0, hits = 0, declined = 0, evictions = 0, bytes_loaded = 0, resident_bytes = 0;
-    double load_ms = 0;
+    int64_t holders = 0, holders_reaped = 0, releases = 0;
+    double load_ms = 0;       // summed per-file load time
+    double load_wall_ms = 0;  // time any load was in progress (loads overlap)
   };
+  // ok: the bytes [0, need_end) are in HBM (ref valid); else why says what failed.
+  using Ready = std::function<void(bool ok, const Ref& ref, const std::string& why)>;
 
   explicit MofCache(const Options& o);
   ~MofCache();
@@ -61,41 +79,69 @@ class MofCache {
   MofCache& operator=(const MofCache&) = delete;
 
   bool enabled() const { return opt_.capacity > 0 && !opt_.devices.empty(); }
-  // Device copy of the MOF file `path` of job `job` (loaded on first touch; concurrent callers of a
-  // file being loaded wait for it). false (reason in *why) when it cannot be cached now.
-  bool acquire(const std::string& job, const std::string& path, Ref* out, std::string* why);
-  // The job is over: its MOFs may be evicted at once.
+  // Take `holder`'s reference on the MOF file `path` of job `job` (loading it on first touch) and
+  // call ready() once its first need_end bytes are resident: inline if they already are, else from
+  // a loader thread. false (reason in *why; ready never called) when it cannot be cached now.
+  bool acquire_async(const std::string& job, const std::string& path, const std::string& holder, int64_t need_end,
+                     Ready ready, std::string* why);
+  // Blocking form (tests): the whole file.
+  bool acquire(const std::string& job, const std::string& path, const std::string& holder, Ref* out, std::string* why);
+  // Drop one of holder's references on `path` / all of holder's references on job's MOFs.
+  void release(const std::string& path, const std::string& holder);
+  void release_holder(const std::string& job, const std::string& holder);
+  // The job is over: its MOFs may be evicted at once, whoever still holds them.
   void job_over(const std::string& job);
   Stats stats();
 
  private:
+  struct Waiter {
+    int64_t need_end;
+    Ready ready;
+  };
   struct Entry {
-    std::string job;
+    std::string job, path;
     int device = -1;
     int64_t len = 0;
-    void* dptr = nullptr;
+    std::unique_ptr<DeviceBuffer> mem;
+    const uint8_t* dptr = nullptr;
     IpcExport ipc;
     bool loading = true, failed = false, job_done = false;
     std::string error;
-    double last_served = 0;
+    double last_served = 0, t_start = 0;
+    std::map<std::string, std::pair<int, double>> holders;  // holder -> (references, last fetch time)
+    std::vector<Waiter> waiters;
+    // loader state
+    int fd = -1;
+    bool direct = false;
+    int64_t next_read = 0, landed = 0;
+    std::map<int64_t, int64_t> done_chunks;  // landed beyond `landed`: offset -> length
+    int reads_in_flight = 0;
   };
-  void load(const std::string& path, Entry* e);  // fills e (device chosen by the caller), throws
-  bool make_room(int device, int64_t bytes, double now);  // under mu_: evict until `bytes` fit
-  void free_entry(Entry* e);
+  struct Loader;
+  struct Fire {
+    Ready ready;
+    bool ok;
+    Ref ref;
+    std::string why;
+  };
+
+  bool make_room(int device, int64_t bytes, double now);  // mu_ held: evict until `bytes` fit
+  bool evictable(Entry& e, double now);                   // mu_ held (reaps dead holders)
+  void erase_entry(const std::string& path);              // mu_ held
+  Ref ref_of(const Entry& e) const;
+  void loader_main(Loader* L);
+  void fail_entry(Entry& e, const std::string& why, std::vector<Fire>* fire);  // mu_ held
+  void collect_ready(Entry& e, std::vector<Fire>* fire);                      // mu_ held
 
   Options opt_;
   int64_t per_device_ = 0;
   std::mutex mu_;
-  std::condition_variable cv_;
   std::map<std::string, std::shared_ptr<Entry>> entries_;  // by path
   std::map<int, int64_t> used_;                             // device -> bytes resident or loading
+  std::map<int, std::unique_ptr<Loader>> loaders_;          // by device
   Stats st_;
-  // loader state (one load at a time: the disk / PCIe link is the bound, not the CPU)
-  std::mutex load_mu_;
-  std::unique_ptr<AsyncIO> aio_;
-  uint8_t* ring_ = nullptr;
-  std::vector<hipEvent_t> ev_;
-  std::vector<hipStream_t> streams_;  // per device index
+  int busy_loaders_ = 0;
+  double busy_since_ = 0;
 };
 
 }  // namespace gpu

@@ -30,6 +30,9 @@ struct FetchRequest {
   int64_t raw_len = -1;
   int64_t part_len = -1;
   std::string path;
+  // descriptor fetch / release: the reducer holding the descriptor (gpu::reducer_holder_id); carried
+  // in the RTS path field on the wire
+  std::string holder;
 };
 
 struct FetchAck {
@@ -47,6 +50,10 @@ constexpr int kMofPathMax = 600;       // NETLEV_MOF_PATH_MAX_SIZE (NetlevComm.h
 // address in FetchAck.path (see csrc/gpu/device_ptr.h) and sends no bytes; a MOF that is not
 // device-resident answers kNotDeviceResident and the reducer fetches bytes instead.
 constexpr int64_t kDescriptorFetch = -1;
+// FetchRequest.buf_len of a descriptor release: the holder is done with the descriptor of
+// (job, map, reduce), or with every descriptor of the job when map_id is "*". The provider may then
+// free the partition's HBM copy (see csrc/gpu/mof_cache.h).
+constexpr int64_t kDescriptorRelease = -2;
 constexpr int kNotDeviceResident = -12;
 constexpr int kFetchReqMax = 800;      // NETLEV_FETCH_REQSIZE (NetlevComm.h:30)
 

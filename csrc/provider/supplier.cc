@@ -87,6 +87,10 @@ std::string Supplier::hbm_stats_json() {
   if (!hbm_) return "{}";
   const gpu::MofCache::Stats st = hbm_->stats();
   return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
+         ",\"holders\":" + std::to_string(st.holders) + ",\"releases\":" + std::to_string(st.releases) +
+         ",\"holders_reaped\":" + std::to_string(st.holders_reaped) + ",\"load_wall_ms\":" +
+         std::to_string(st.load_wall_ms) + ",\"load_gbps\":" +
+         std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
          ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
          ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
          std::to_string(st.resident_bytes) + ",\"load_ms\":" + std::to_string(st.load_ms) + "}";
@@ -189,6 +193,20 @@ void Supplier::process(Job& j) {
   IndexRec rec;
   const MemMof* mem = nullptr;
   FetchAck ack;
+  if (j.req.buf_len == kDescriptorRelease) {
+    // the reducer is done with descriptors it fetched (chunk release on SEND completion,
+    // src/MOFServer/IndexInfo.cc:276-301): the store may free the MOFs nobody holds any more
+    if (hbm_) {
+      if (j.req.map_id == "*") {
+        hbm_->release_holder(j.req.job_id, j.req.holder);
+      } else if (resolve(j.req, &rec, &mem) && !mem) {
+        hbm_->release(rec.path, j.req.holder);
+      }
+    }
+    releases_++;
+    j.done(ack);
+    return;
+  }
   if (!resolve(j.req, &rec, &mem)) {
     ack.status = -2;
     ack.error = "cannot resolve MOF " + j.req.job_id + "/" + j.req.map_id + "/" + std::to_string(j.req.reduce_id);
@@ -207,19 +225,32 @@ void Supplier::process(Job& j) {
   ack.path = rec.path;
   if (j.req.buf_len == kDescriptorFetch) {
     // zero-copy fetch: the reducer reads the partition where it lives (RDMA WRITE analogue)
-    gpu::MofCache::Ref ref;
     std::string why;
-    if (!mem && hbm_ && hbm_->acquire(j.req.job_id, rec.path, &ref, &why)) {
-      // a Hadoop-written MOF file, now resident in the provider's HBM store
-      if (rec.start_offset + rec.part_length > ref.len) {
-        ack.status = -4;
-        ack.error = "index beyond MOF file " + rec.path;
-      } else {
-        ack.path = gpu::make_device_descriptor(ref.device, ref.data + rec.start_offset, ref.ipc);
-        ack.sent = 0;
-        descriptors_++;
-      }
-    } else if (!mem || mem->device < 0) {
+    if (!mem && hbm_) {
+      // a Hadoop-written MOF file, made resident in the provider's HBM store: answered once the file
+      // has landed up to the end of this partition (the loader fills files in turn)
+      const int64_t need = rec.start_offset + rec.part_length;
+      auto done = j.done;
+      const bool taken = hbm_->acquire_async(
+          j.req.job_id, rec.path, j.req.holder, need,
+          [this, ack, done, rec, need](bool ok, const gpu::MofCache::Ref& ref, const std::string& w) mutable {
+            if (!ok) {
+              ack.status = kNotDeviceResident;  // the reducer fetches the bytes instead
+              ack.error = "provider HBM store: " + w;
+            } else if (need > ref.len) {
+              ack.status = -4;
+              ack.error = "index beyond MOF file " + rec.path;
+            } else {
+              ack.path = gpu::make_device_descriptor(ref.device, ref.data + rec.start_offset, ref.ipc, /*leased=*/true);
+              ack.sent = 0;
+              descriptors_++;
+            }
+            done(ack);
+          },
+          &why);
+      if (taken) return;
+    }
+    if (!mem || mem->device < 0) {
       ack.status = kNotDeviceResident;
       ack.error = "MOF is not device-resident";
     } else if (rec.start_offset + rec.part_length > mem->len) {

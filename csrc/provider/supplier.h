@@ -47,7 +47,8 @@ class Supplier : public DataServer {
     // load the file into HBM once and are answered with device descriptors
     int64_t hbm_bytes = 0;               // mapred.uda.provider.hbm.bytes (0: off)
     std::vector<int> hbm_devices{0};     // mapred.uda.provider.hbm.devices ("0,1,...")
-    double hbm_lease_s = 600;            // mapred.uda.provider.hbm.lease.s
+    double hbm_lease_s = 600;            // mapred.uda.provider.hbm.lease.s: a holder on another node idle
+                                         // this long is presumed dead (same-node holders: process liveness)
   };
   Supplier(const NetlevOptions& net, const Options& o, Host* host);
   ~Supplier() override;
@@ -113,7 +114,7 @@ class Supplier : public DataServer {
   std::mutex fd_mu_;
   std::unordered_map<std::string, OpenFile> fds_;
   uint64_t fd_clock_ = 0;
-  std::atomic<int64_t> requests_{0}, bytes_{0}, descriptors_{0};
+  std::atomic<int64_t> requests_{0}, bytes_{0}, descriptors_{0}, releases_{0};
 };
 
 }  // namespace uda

@@ -18,6 +18,7 @@
 #include "block_decoder.h"
 #include "device_engine.h"
 #include "device_ptr.h"
+#include "mof_cache.h"
 #include "exchange.h"
 #include "api_bench.h"
 #include "generic_merger.h"
@@ -695,6 +696,54 @@ PYBIND11_MODULE(_uda_native, m) {
   m.def("set_log_level", &uda_set_log_level);
 
   // ---------------------------------------------------------------- GPU engine
+  // the provider's HBM store of MOF files on its own (gpu/mof_cache.h): loads, holders, eviction
+  py::class_<gpu::MofCache>(m, "MofStore")
+      .def(py::init([](int64_t capacity, std::vector<int> devices, double lease_s, int64_t chunk_bytes) {
+             gpu::MofCache::Options o;
+             o.capacity = capacity;
+             o.devices = devices;
+             o.lease_s = lease_s;
+             o.chunk_bytes = chunk_bytes;
+             return new gpu::MofCache(o);
+           }),
+           py::arg("capacity"), py::arg("devices") = std::vector<int>{0}, py::arg("lease_s") = 600.0,
+           py::arg("chunk_bytes") = 16 << 20)
+      .def("acquire",
+           [](gpu::MofCache& c, const std::string& job, const std::string& path, const std::string& holder) {
+             gpu::MofCache::Ref r;
+             std::string why;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = c.acquire(job, path, holder, &r, &why);
+             }
+             return py::make_tuple(ok, why, (uint64_t)(uintptr_t)r.data, r.len, r.device);
+           })
+      .def("release", &gpu::MofCache::release)
+      .def("release_holder", &gpu::MofCache::release_holder)
+      .def("job_over", &gpu::MofCache::job_over)
+      .def("stats", [](gpu::MofCache& c) {
+        const gpu::MofCache::Stats s = c.stats();
+        py::dict d;
+        d["loads"] = s.loads;
+        d["hits"] = s.hits;
+        d["declined"] = s.declined;
+        d["evictions"] = s.evictions;
+        d["bytes_loaded"] = s.bytes_loaded;
+        d["resident_bytes"] = s.resident_bytes;
+        d["holders"] = s.holders;
+        d["holders_reaped"] = s.holders_reaped;
+        d["releases"] = s.releases;
+        return d;
+      });
+  m.def("reducer_holder_id", &gpu::reducer_holder_id);
+  m.def("open_ipc_mappings", &gpu::open_ipc_mappings);
+  m.def("device_read", [](uint64_t addr, int64_t len) {  // device bytes back to the host (tests)
+    std::string out((size_t)len, '\0');
+    if (len > 0) HIP_CHECK(hipMemcpy(out.data(), reinterpret_cast<const void*>((uintptr_t)addr), (size_t)len,
+                                     hipMemcpyDeviceToHost));
+    return py::bytes(out);
+  });
   m.def("device_count", &gpu::device_count);
   m.def("ipc_safe_bytes", [](uint64_t b) { return (uint64_t)gpu::ipc_safe_bytes((size_t)b); });
   m.def("ipc_size_ok", [](uint64_t b) { return gpu::ipc_size_ok((size_t)b); });

@@ -32,7 +32,9 @@ std::string format_rts(const FetchRequest& r, uint64_t remote_addr, uint64_t req
   return r.job_id + ":" + r.map_id + ":" + std::to_string(r.fetched) + ":" + std::to_string(r.reduce_id) +
          ":" + std::to_string(remote_addr) + ":" + std::to_string(req_ptr) + ":" +
          std::to_string(r.buf_len) + ":" + std::to_string(r.mof_offset) + ":" +
-         (r.path.empty() ? std::string("?") : r.path) + ":" + std::to_string(r.raw_len) + ":" +
+         (r.buf_len < 0 ? (r.holder.empty() ? std::string("?") : r.holder)
+                        : (r.path.empty() ? std::string("?") : r.path)) +
+         ":" + std::to_string(r.raw_len) + ":" +
          std::to_string(r.part_len);
 }
 
@@ -51,6 +53,10 @@ bool parse_rts(const std::string& s, FetchRequest* r, uint64_t* remote_addr, uin
   std::string path = f[8];
   for (size_t i = 9; i + 2 < f.size(); ++i) path += ":" + f[i];
   r->path = (path == "?") ? std::string() : path;
+  if (r->buf_len < 0) {  // descriptor fetch / release: the path field is the holder
+    r->holder = r->path;
+    r->path.clear();
+  }
   r->raw_len = to_i64(f[f.size() - 2]);
   r->part_len = to_i64(f[f.size() - 1]);
   return true;

@@ -1,0 +1,132 @@
+"""GPU: lifetime of the provider's HBM store of MOF files (csrc/gpu/mof_cache.h).
+
+A descriptor handed to a reducer is a reference the reducer holds until it releases it: an entry
+with a live holder is never evicted, however long ago it was served and however full the budget;
+a released, finished-job, or dead holder's entry is evictable. Reducers release their descriptors
+when their merge is done (a release message on the fetch transport), so a job's store drains.
+
+Reference: chunks are freed only when the SEND that used them completed, and the fd cache is
+refcounted by in-flight reads (src/DataNet/RDMAServer.cc:200-213, src/MOFServer/IndexInfo.cc:195-233,
+276-301)."""
+import json
+import os
+import time
+
+import pytest
+
+from uda_amd.bridge import UdaProvider, run_reduce
+from uda_amd.utils import datagen
+from uda_amd.utils.mof import encode_partitions
+
+pytestmark = pytest.mark.gpu
+GPU = {"mapred.uda.merge.backend": "gpu"}
+MB = 1 << 20
+
+
+def _files(tmp_path, n, size):
+    paths = []
+    for i in range(n):
+        p = tmp_path / f"mof{i}.out"
+        p.write_bytes(os.urandom(size))
+        paths.append(str(p))
+    return paths
+
+
+def test_held_entry_outlives_its_lease_under_budget_pressure(require_gpu, native, tmp_path):
+    size = 24 * MB + 4096 * 3  # not a multiple of the chunk: a short last read
+    f = _files(tmp_path, 3, size)
+    store = native.MofStore(capacity=2 * size + MB, devices=[0], lease_s=0.5, chunk_bytes=4 * MB)
+    me = native.reducer_holder_id("attempt_r_000000_0")  # this process: alive
+    ok, why, a0, n0, _ = store.acquire("job", f[0], me)
+    assert ok and n0 == size, why
+    assert native.device_read(a0, size) == open(f[0], "rb").read()  # every chunk landed in order
+    ok, _, _, _, _ = store.acquire("job", f[1], me)
+    assert ok
+    time.sleep(1.2)  # past the lease: a held entry stays anyway
+    ok, why, _, _, _ = store.acquire("job", f[2], "other-reducer")
+    assert not ok and "held" in why, why
+    st = store.stats()
+    assert st["evictions"] == 0 and st["holders"] == 2 and st["declined"] == 1, st
+    assert native.device_read(a0, 4096) == open(f[0], "rb").read(4096)  # still resident and intact
+    store.release(f[0], me)
+    ok, why, a2, _, _ = store.acquire("job", f[2], "other-reducer")
+    assert ok, why
+    assert native.device_read(a2, size) == open(f[2], "rb").read()
+    st = store.stats()
+    assert st["evictions"] == 1 and st["releases"] == 1 and st["loads"] == 3, st
+
+
+def test_dead_or_foreign_holders_are_dropped(require_gpu, native, tmp_path):
+    size = 8 * MB
+    f = _files(tmp_path, 3, size)
+    store = native.MofStore(capacity=2 * size + MB, devices=[0], lease_s=0.5)
+    dead = f"{native.node_id()}:999999:1:attempt_r_1"  # this node, a process that is gone
+    foreign = "0123456789abcdef:4242:7:attempt_r_2"  # another node: only its lease protects it
+    assert store.acquire("job", f[0], dead)[0]
+    assert store.acquire("job", f[1], foreign)[0]
+    # the foreign holder fetched just now: its entry stays; the dead holder's entry goes
+    ok, why, _, _, _ = store.acquire("job", f[2], "x")
+    assert ok, why
+    st = store.stats()
+    assert st["evictions"] == 1 and st["holders_reaped"] == 1, st
+    time.sleep(1.0)  # the foreign holder's lease runs out
+    store.release(f[2], "x")
+    ok, why, _, _, _ = store.acquire("job", f[0], "y")
+    assert ok, why
+    assert store.stats()["holders_reaped"] == 2
+
+
+def test_reduce_tasks_release_their_descriptors(require_gpu, tmp_path):
+    """A job's reduce tasks fetch descriptors of Hadoop-written MOFs and release them when merged:
+    afterwards nothing is held, and another job can take the HBM without waiting for JOB_OVER."""
+    from uda_amd.utils.mof import write_mof
+    maps = datagen.terasort(num_maps=4, reducers=2, rows_per_map=3000, seed=31)
+    size = sum(len(b) for b in datagen.streams(maps)[0]) + 4096
+    p = UdaProvider(conf={"mapred.uda.provider.hbm.bytes": 5 * size})
+    try:
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_job_9_0200_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts)
+            p.add_mof_file("job_9_0200", mid, path)
+            ids.append(mid)
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device"})
+        for r in range(2):
+            recs, st, _ = run_reduce("h", "job_9_0200", ids, r, datagen.TEXT, conf=conf)
+            assert len(recs) == sum(len(m[r]) for m in maps)
+            assert st["device_descriptors"] == 4, st
+        hs = json.loads(p.stats())["hbm_store"]
+        assert hs["holders"] == 0 and hs["releases"] >= 8 and hs["loads"] == 4, hs
+        # a second job's MOFs fit only by evicting the first job's (released, job still running)
+        ids2 = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_job_9_0201_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path / "j2"), mid, parts)
+            p.add_mof_file("job_9_0201", mid, path)
+            ids2.append(mid)
+        recs, st, _ = run_reduce("h", "job_9_0201", ids2, 0, datagen.TEXT, conf=conf)
+        assert st["device_descriptors"] == 4 and st["host_fetched_bytes"] == 0, st
+        hs = json.loads(p.stats())["hbm_store"]
+        assert hs["evictions"] >= 3 and hs["declined"] == 0, hs
+    finally:
+        p.close()
+
+
+def test_empty_partitions_on_the_generic_device_path(require_gpu):
+    """Every partition holds only its EOF marker (BytesWritable keys: the generic merge, not FIXED10):
+    the task must end with an EOF-only delivery instead of waiting for a round that never merges."""
+    p = UdaProvider()
+    try:
+        ids = []
+        for i in range(5):
+            mid = f"attempt_job_9_0202_m_{i:06d}_0"
+            data, index = encode_partitions([[], []], None)
+            p.add_mof_device("job_9_0202", mid, data, index, device=0)
+            ids.append(mid)
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.round.bytes": 1 << 20})
+        t0 = time.time()
+        recs, st, _ = run_reduce("h", "job_9_0202", ids, 1, datagen.BYTES, conf=conf)
+        assert recs == [] and st["records"] == 0 and st["merge_path"] == "device-generic", st
+        assert time.time() - t0 < 60
+    finally:
+        p.close()
