@@ -1423,6 +1423,10 @@ void ReduceTask::merge_gpu() {
           EarlyStager* st = stager;
           auto work = [this, &pf, st, depth] {
             for (int64_t i; (i = pf.next++) < (int64_t)pf.P * pf.K;) {
+              {
+                std::lock_guard<std::mutex> g(pf.mu);
+                if (stop_ || pf.err) break;  // a stopped or failed task fetches no further phases
+              }
               const int p = (int)(i / pf.K), k = (int)(i % pf.K);
               int64_t e = 0;
               try {
@@ -1605,7 +1609,10 @@ void ReduceTask::merge_gpu() {
         const auto tw = std::chrono::steady_clock::now();
         {
           std::unique_lock<std::mutex> lk(pf.mu);
-          pf.cv.wait(lk, [&] { return pf.done[(size_t)p] == K || pf.err || stop_; });
+          // exit() sets stop_ without notifying pf.cv: wake up to look
+          while (!pf.cv.wait_for(lk, std::chrono::milliseconds(50),
+                                 [&] { return pf.done[(size_t)p] == K || pf.err || stop_; })) {
+          }
           if (pf.err) std::rethrow_exception(pf.err);
           if (stop_) throw UdaError("reduce task stopped during fetch");
           for (int k = 0; k < K; ++k) land[(size_t)k] = std::max(land[(size_t)k], pf.landed[(size_t)p][(size_t)k]);

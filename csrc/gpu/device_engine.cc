@@ -73,6 +73,7 @@ void DeviceBuffer::alloc(size_t bytes, bool resident) {
   resident_ = resident;
 }
 void DeviceBuffer::reset() {
+  if (ptr_) note_device_free(ptr_);  // an exporter's cached IPC identity of this address is stale now
   if (ptr_ && trace::host_enabled()) {
     const int64_t tt = trace::now_ns();
     (void)hipFree(ptr_);

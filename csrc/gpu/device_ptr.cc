@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -212,6 +213,29 @@ const uint8_t* resolve_device_descriptor(const std::string& desc, int my_device)
   const uint8_t* p = try_resolve_device_descriptor(desc, my_device, &why);
   if (!p) throw std::runtime_error("cannot map device descriptor: " + why);
   return p;
+}
+
+namespace {
+std::mutex g_free_mu;
+std::atomic<uint64_t> g_free_epoch{0};
+std::map<uintptr_t, uint64_t>& freed_bases() {
+  static auto* m = new std::map<uintptr_t, uint64_t>();  // base -> epoch of its last free
+  return *m;
+}
+}  // namespace
+
+uint64_t alloc_epoch() { return g_free_epoch.load(std::memory_order_acquire); }
+
+void note_device_free(const void* base) {
+  std::lock_guard<std::mutex> g(g_free_mu);
+  freed_bases()[(uintptr_t)base] = g_free_epoch.fetch_add(1, std::memory_order_acq_rel) + 1;
+}
+
+bool freed_since(const void* base, uint64_t epoch) {
+  if (g_free_epoch.load(std::memory_order_acquire) == epoch) return false;  // nothing freed at all
+  std::lock_guard<std::mutex> g(g_free_mu);
+  auto it = freed_bases().find((uintptr_t)base);
+  return it != freed_bases().end() && it->second > epoch;
 }
 
 void copy_device_to_host(void* dst, const void* src, int64_t bytes) {

@@ -55,6 +55,13 @@ void release_device_descriptor(const std::string& desc);
 std::string reducer_holder_id(const std::string& task);
 // IPC mappings this process holds open (tests).
 int open_ipc_mappings();
+// Device allocations freed by this process, by base address: an exporter that cached an allocation's
+// IPC identity (IpcExchange) checks it before reusing the entry, since a new allocation can get the
+// same address. alloc_epoch() numbers the frees; freed_since(base, e) is true if `base` was freed
+// after epoch e.
+uint64_t alloc_epoch();
+void note_device_free(const void* base);
+bool freed_since(const void* base, uint64_t epoch);
 // Copy device memory at `src` (any device) to host `dst`.
 void copy_device_to_host(void* dst, const void* src, int64_t bytes);
 

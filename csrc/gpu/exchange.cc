@@ -1,4 +1,5 @@
 #include "exchange.h"
+#include "device_ptr.h"
 
 #include <rccl/rccl.h>
 
@@ -309,8 +310,15 @@ class LocalExchange : public Exchange {
   void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
                 hipStream_t s) override {
     Group& g = *group_;
-    if ((int)send.size() != world_ || (int)recv.size() != world_) throw std::runtime_error("exchange: bad peer lists");
-    if (!send[rank_].empty() || !recv[rank_].empty()) throw std::runtime_error("exchange: self slices");
+    // a rank that throws before the barrier must wake its peers (Group::barrier has no timeout)
+    if ((int)send.size() != world_ || (int)recv.size() != world_) {
+      g.abort();
+      throw std::runtime_error("exchange: bad peer lists");
+    }
+    if (!send[rank_].empty() || !recv[rank_].empty()) {
+      g.abort();
+      throw std::runtime_error("exchange: self slices");
+    }
     const int64_t seq = seq_++;
     g.sends[rank_] = &send;
     HIP_CHECK(hipEventRecord(g.ready_ev[rank_], s));
@@ -446,11 +454,11 @@ class IpcExchange : public Exchange {
 
   void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
                 hipStream_t s) override {
-    if ((int)send.size() != world_ || (int)recv.size() != world_) throw std::runtime_error("exchange: bad peer lists");
-    if (!send[rank_].empty() || !recv[rank_].empty()) throw std::runtime_error("exchange: self slices");
     const int64_t k = seq_++;
     const int par = (int)(k & 1);
     try {
+      if ((int)send.size() != world_ || (int)recv.size() != world_) throw std::runtime_error("exchange: bad peer lists");
+      if (!send[rank_].empty() || !recv[rank_].empty()) throw std::runtime_error("exchange: self slices");
       // The peers pull with their own streams: what this rank's stream still has to write into the
       // send slices (staging copies enqueued before this call) must land before the outbox says so.
       bool sends = false;
@@ -551,9 +559,13 @@ class IpcExchange : public Exchange {
     auto it = exported_.upper_bound(a);
     if (it != exported_.begin()) {
       --it;
-      if (a >= it->first && a + (uintptr_t)bytes <= it->first + (uintptr_t)it->second.first) {
-        *off = (int64_t)(a - it->first);
-        return it->second.second;
+      if (a >= it->first && a + (uintptr_t)bytes <= it->first + (uintptr_t)it->second.size) {
+        if (!freed_since(reinterpret_cast<const void*>(it->first), it->second.epoch)) {
+          *off = (int64_t)(a - it->first);
+          return it->second.id;
+        }
+        // freed and allocated again at the same address: a new export (peers map the new handle)
+        exported_.erase(it);
       }
     }
     check_device_memory(p, "send");
@@ -570,9 +582,10 @@ class IpcExchange : public Exchange {
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     if (a + (uintptr_t)bytes > b + size) throw std::runtime_error("exchange: send slice crosses its allocation's end");
     hipIpcMemHandle_t h;
+    const uint64_t epoch = alloc_epoch();
     HIP_CHECK(hipIpcGetMemHandle(&h, base));
     const int id = grp_.publish_alloc(&h, sizeof(h), (int64_t)size);
-    exported_[b] = {size, id};
+    exported_[b] = Exported{size, id, epoch};
     *off = (int64_t)(a - b);
     return id;
   }
@@ -657,7 +670,12 @@ class IpcExchange : public Exchange {
   ShmGroup grp_;
   int64_t seq_ = 0;
   int64_t bytes_pulled_ = 0;
-  std::map<uintptr_t, std::pair<size_t, int>> exported_;         // base -> (size, id)
+  struct Exported {
+    size_t size;
+    int id;
+    uint64_t epoch;  // alloc_epoch() at export: a later free of the base invalidates the entry
+  };
+  std::map<uintptr_t, Exported> exported_;  // by base
   std::map<std::pair<int, int>, std::pair<void*, int64_t>> mapped_;  // (peer, id) -> (mapping, size)
   std::mutex mu_;
   std::condition_variable cv_;
@@ -682,7 +700,8 @@ class IpcExchange : public Exchange {
 void Exchange::wait(hipStream_t s) { HIP_CHECK(hipStreamSynchronize(s)); }
 
 std::string exchange_probe(Exchange& ex, int device, const std::vector<std::vector<int64_t>>& send_sizes,
-                           const std::vector<std::vector<int64_t>>& recv_sizes, bool host_source, int rounds) {
+                           const std::vector<std::vector<int64_t>>& recv_sizes, bool host_source, int rounds,
+                           int64_t export_bytes) {
   const int W = ex.world(), me = ex.rank();
   auto pattern = [](int from, int to, size_t i, int round) { return (uint8_t)((from * 31 + to * 7 + i * 3 + round) & 0xFF); };
   try {
@@ -696,11 +715,18 @@ std::string exchange_probe(Exchange& ex, int device, const std::vector<std::vect
     DeviceBuffer dsend, drecv((size_t)std::max<int64_t>(rb, 16));
     PinnedBuffer hsend;
     uint8_t* sbase;
+    // export_bytes > the slices: one allocation of that size (a map-output store is one multi-GB
+    // export) with the slices spread over it, the last ending at its end, so peers map and read
+    // beyond 4 GiB of it as the shuffle rounds will
+    const int64_t alloc_bytes = std::max<int64_t>(std::max<int64_t>(sb, 16), host_source ? 0 : export_bytes);
+    int64_t nslices = 0;
+    for (auto& v : send_sizes) nslices += (int64_t)v.size();
+    const int64_t gap = nslices > 0 ? ((alloc_bytes - sb) / nslices) & ~(int64_t)255 : 0;
     if (host_source) {
       hsend.alloc((size_t)std::max<int64_t>(sb, 16));
       sbase = hsend.as<uint8_t>();
     } else {
-      dsend.alloc((size_t)std::max<int64_t>(sb, 16));
+      dsend.alloc((size_t)alloc_bytes);
       sbase = dsend.as<uint8_t>();
     }
     hipStream_t st;
@@ -716,6 +742,7 @@ std::string exchange_probe(Exchange& ex, int device, const std::vector<std::vect
       int64_t off = 0;
       for (int p = 0; p < W; ++p)
         for (size_t i = 0; i < send_sizes[p].size(); ++i) {
+          off += gap;
           HIP_CHECK(hipMemsetAsync(sbase + off, pattern(me, p, i, round), (size_t)send_sizes[p][i], st));
           send[p].push_back(Span{sbase + off, send_sizes[p][i]});
           off += send_sizes[p][i];

@@ -90,8 +90,11 @@ std::unique_ptr<Exchange> make_ipc_exchange(const std::string& name, int rank, i
 // Test probe: `rounds` exchanges of synthetic slices (send_sizes[p] / recv_sizes[p]: slice sizes to /
 // from peer p), every received byte checked. Returns "" or the error (pairing, memory-kind, data).
 // host_source: the send slices live in pinned host memory (must be refused).
+// export_bytes: the send slices are spread over one device allocation of this size (a store-sized
+// export: the peers map it and read beyond 4 GiB of it).
 std::string exchange_probe(Exchange& ex, int device, const std::vector<std::vector<int64_t>>& send_sizes,
-                           const std::vector<std::vector<int64_t>>& recv_sizes, bool host_source, int rounds);
+                           const std::vector<std::vector<int64_t>>& recv_sizes, bool host_source, int rounds,
+                           int64_t export_bytes = 0);
 
 }  // namespace gpu
 }  // namespace uda

@@ -1000,18 +1000,19 @@ PYBIND11_MODULE(_uda_native, m) {
         py::arg("device") = 0);
   m.def("ipc_exchange_probe",
         [](const std::string& name, int rank, int world, const std::vector<std::vector<int64_t>>& send,
-           const std::vector<std::vector<int64_t>>& recv, bool host_source, int rounds, int device) {
+           const std::vector<std::vector<int64_t>>& recv, bool host_source, int rounds, int device,
+           int64_t export_bytes) {
           py::gil_scoped_release rel;
           try {
             HIP_CHECK(hipSetDevice(device));
             auto ex = gpu::make_ipc_exchange(name, rank, world, device);
-            return gpu::exchange_probe(*ex, device, send, recv, host_source, rounds);
+            return gpu::exchange_probe(*ex, device, send, recv, host_source, rounds, export_bytes);
           } catch (const std::exception& e) {
             return std::string(e.what());
           }
         },
         py::arg("name"), py::arg("rank"), py::arg("world"), py::arg("send"), py::arg("recv"),
-        py::arg("host_source") = false, py::arg("rounds") = 1, py::arg("device") = 0);
+        py::arg("host_source") = false, py::arg("rounds") = 1, py::arg("device") = 0, py::arg("export_bytes") = 0);
 
   py::class_<gpu::J2CSink, std::shared_ptr<gpu::J2CSink>>(m, "J2CSink")
       .def(py::init([](int r, int64_t kv, py::object threaded) {

@@ -60,16 +60,16 @@ def test_local_exchange_refuses_host_source(require_gpu, native):
     assert any("not device memory" in e for e in errs), errs
 
 
-def _ipc_rank(name, rank, world, send, recv, host_source, rounds, q):
+def _ipc_rank(name, rank, world, send, recv, host_source, rounds, export, q):
     import uda_amd
-    q.put((rank, uda_amd.native().ipc_exchange_probe(name, rank, world, send, recv, host_source, rounds, 0)))
+    q.put((rank, uda_amd.native().ipc_exchange_probe(name, rank, world, send, recv, host_source, rounds, 0, export)))
 
 
-def _run_ipc(world, send, recv, host_source=False, rounds=1):
+def _run_ipc(world, send, recv, host_source=False, rounds=1, export=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     name = f"udaprobe.{os.getpid()}.{secrets.token_hex(4)}"
-    ps = [ctx.Process(target=_ipc_rank, args=(name, r, world, send[r], recv[r], host_source, rounds, q))
+    ps = [ctx.Process(target=_ipc_rank, args=(name, r, world, send[r], recv[r], host_source, rounds, export, q))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -87,6 +87,15 @@ def _run_ipc(world, send, recv, host_source=False, rounds=1):
 def test_ipc_exchange_matched_processes(require_gpu):
     send, recv = _plan(3, _sizes)
     assert _run_ipc(3, send, recv, rounds=4) == [""] * 3
+
+
+def test_ipc_preflight_shape_over_a_store_sized_export(require_gpu):
+    """The job's preflight shape: each rank exports one allocation larger than 4 GiB (padded out of
+    the hipIpc-hanging size range) with production-size slices spread up to its end; the peers map
+    it and pull every slice with the batched copy kernel, every byte checked."""
+    slice_bytes = (2 << 20) // 104 * 104
+    send, recv = _plan(2, lambda f, t: [slice_bytes + 104 * i for i in range(16)])
+    assert _run_ipc(2, send, recv, rounds=2, export=(4 << 30) + (256 << 20)) == [""] * 2
 
 
 def test_ipc_exchange_refuses_mismatch_and_host_source(require_gpu):

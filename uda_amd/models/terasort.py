@@ -82,7 +82,10 @@ class TeraSortShuffle:
         t0 = time.perf_counter()
         if self.ctx.world > 1:
             if self.cfg.exchange == "ipc" and not self._ipc_preflight():
-                self.cfg.exchange = "rccl"  # every rank saw the same verdict (all-gathered)
+                # every rank saw the same verdict (all-gathered). No silent switch to another backend:
+                # RCCL runs only when asked for (--exchange rccl)
+                raise RuntimeError(f"IPC exchange preflight failed ({self.ipc_fallback}); the job stops here. "
+                                   "Fix the cause, or run with --exchange rccl to use RCCL instead")
             if self.cfg.exchange == "ipc":
                 name = f"uda.{os.getpid()}.{secrets.token_hex(6)}".encode() if self.ctx.rank == 0 else None
                 self.job.init_ipc(self.ctx.broadcast_bytes(name).decode())
@@ -115,21 +118,28 @@ class TeraSortShuffle:
         self.setup_s = dict(comm_init=t1 - t0, generate=t2 - t1, plan=t3 - t2)
 
     def _ipc_preflight(self) -> bool:
-        """Before the job commits to the IPC exchange: every rank exports a device buffer, maps every
-        peer's over hipIpc and pulls a patterned 68 KiB from each, 2 rounds (exchange_probe checks
-        every byte). All ranks all-gather the outcome, so they agree; on any failure the job falls
-        back to RCCL and says why (`ipc_fallback`). UDA_IPC_PREFLIGHT=0 skips it."""
+        """Before the job commits to the IPC exchange, the shuffle's own pattern on a small scale: every
+        rank exports one device allocation larger than 4 GiB (a map-output store is one multi-GB export,
+        padded by ipc_safe_bytes) holding 16 slices per peer of the production slice size spread up to
+        its end, every peer maps it over hipIpc and pulls its slices with the batched copy kernel, 2
+        rounds, every byte checked (exchange_probe). All ranks all-gather the outcome, so they agree;
+        on failure the job stops with the reason (`ipc_fallback`). UDA_IPC_PREFLIGHT=0 skips it."""
         self.ipc_fallback = None
         if os.environ.get("UDA_IPC_PREFLIGHT", "1") == "0":
             return True
-        w, r = self.ctx.world, self.ctx.rank
-        size = lambda f, t: [65536, 4096 + 104 * ((f + t) % 7)]
+        w, r, c = self.ctx.world, self.ctx.rank, self.cfg
+        # a round's slice: one map output's cell for one reducer (store / (maps x world x reducers x rounds))
+        store = c.rows_per_gpu * RECORD_BYTES
+        slice_bytes = store // max(1, c.maps_per_rank * w * c.reducers * c.rounds)
+        slice_bytes = int(min(64 << 20, max(4096, slice_bytes))) // 104 * 104
+        size = lambda f, t: [slice_bytes + 104 * ((f + t + i) % 7) for i in range(16)]  # noqa: E731
         send = [size(r, p) if p != r else [] for p in range(w)]
         recv = [size(p, r) if p != r else [] for p in range(w)]
+        export = int(os.environ.get("UDA_IPC_PREFLIGHT_EXPORT", str((4 << 30) + (256 << 20))))
         name = f"udapre.{os.getpid()}.{secrets.token_hex(6)}".encode() if r == 0 else None
         name = self.ctx.broadcast_bytes(name).decode()
         try:
-            err = native().ipc_exchange_probe(name, r, w, send, recv, False, 2, self.device)
+            err = native().ipc_exchange_probe(name, r, w, send, recv, False, 2, self.device, export)
         except Exception as e:  # noqa: BLE001 - reported to every rank below
             err = f"{type(e).__name__}: {e}"
         errs = self.ctx.all_gather_object(err)
@@ -137,7 +147,7 @@ class TeraSortShuffle:
         if bad:
             self.ipc_fallback = "; ".join(bad)[:500]
             if r == 0:
-                print(f"uda: IPC exchange preflight failed, using RCCL ({self.ipc_fallback})", flush=True)
+                print(f"uda: IPC exchange preflight failed ({self.ipc_fallback})", flush=True)
             return False
         return True
 
