@@ -103,6 +103,17 @@ def parse_args(argv=None):
     ap.add_argument("--provider-hbm-gb", type=float, default=-1.0,
                     help="--api --mof-dir: mapred.uda.provider.hbm.bytes in GB (default: 1.25x the MOF bytes; "
                          "0 = store off: descriptor fetches are declined and reducers fetch bytes)")
+    ap.add_argument("--node", action="store_true",
+                    help="--api: the node shape: this process is the node's MOFSupplier (map outputs in its HBM, TCP) "
+                         "and every step is a wave of --reducers reduce tasks, each a fresh process "
+                         "(uda_amd/bin/uda_reduce_task: uda_start, INIT, FETCHes, dataFromUda into a J2C consumer), "
+                         "as YARN runs one JVM per reduce task; value includes the processes' start")
+    ap.add_argument("--node-gap", type=float, default=0.0,
+                    help="--node: seconds between a wave's INITs and its FETCHes (reduce slow-start: the tasks start "
+                         "while the maps still run); 0 = the tasks start when every map output is there")
+    ap.add_argument("--node-slots", type=int, default=15,
+                    help="--node: reduce task processes running at once (YARN containers of the node); the one-GPU "
+                         "box allows 16 GPU processes, the provider is one of them")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -165,6 +176,9 @@ def main(argv=None) -> int:
     if ctx.world != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
         return 2
+    if args.api and args.node:
+        torch.cuda.set_device(0)
+        return run_node(args, ctx)
     if args.api:
         torch.cuda.set_device(0 if args.one_gpu else ctx.local_rank)
         return run_api(args, ctx)
@@ -296,6 +310,143 @@ def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
         so.bind(("127.0.0.1", 0))
         return so.getsockname()[1]
+
+
+def run_node(args, ctx) -> int:
+    """The node shape of a Hadoop job on one GPU: this process is the node's MOFSupplier (the NodeManager
+    aux service, MOFSupplierMain.cc:87-143) with the maps' outputs in its HBM, served over TCP; a step is
+    a wave of reduce tasks, each started as a fresh process (UdaBridge.cc:187-263, NetMergerMain.cc:44-77:
+    one NetMerger per ReduceTask JVM) that INITs, FETCHes its partition of every map as device
+    descriptors (the provider's HBM mapped over hipIpc), merges on the GPU and walks every delivered
+    buffer. value = record bytes delivered / wall time of the wave, process starts included."""
+    import statistics
+    import subprocess as sp
+
+    from uda_amd import native
+    if ctx.world != 1:
+        print("bench: --node runs one provider process per node (--gpus 1)", file=sys.stderr)
+        return 2
+    exe = os.path.join(ROOT, "uda_amd", "bin", "uda_reduce_task")
+    if not os.access(exe, os.X_OK):
+        print(f"bench: {exe} is missing; build with python tools/build.py", file=sys.stderr)
+        return 2
+    R = args.reducers
+    port = _free_port()
+    b = native().ApiTeraSortBench(dict(device=0, maps=args.maps_per_gpu, reducers=R, workload=args.workload,
+                                       skew=args.skew, codec=args.api_codec or "",
+                                       records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
+                                       round_bytes=args.round_mb << 20, rank=0, world=1, port=port,
+                                       transport="tcp", bind_addr="127.0.0.1", fetch="device",
+                                       provider_workers=args.api_provider_workers))
+    t = time.perf_counter()
+    b.setup()
+    cmds = [b.task_commands(r) for r in range(R)]
+    expected = b.expected_records()
+    print(f"# node setup {time.perf_counter() - t:.1f}s store={b.store_bytes / 1e9:.1f}GB provider port {port}, "
+          f"{R} reduce task processes per wave, {args.node_slots} at once", file=sys.stderr, flush=True)
+    conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch": "device", "mapred.uda.transport": "tcp",
+            "mapred.uda.gpu.device": "auto", "mapred.uda.gpu.round.bytes": str(args.round_mb << 20)}
+    for kv in filter(None, os.environ.get("UDA_API_CONF", "").split(",")):
+        k, _, v = kv.partition("=")
+        conf[k] = v
+    start = ["-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
+    errlog = open(os.path.join(ROOT, "gpurun_out" if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp",
+                               "node_tasks.err"), "a")
+
+    def wave(validate: bool) -> dict:
+        t0 = time.perf_counter()
+        todo, running, out = list(range(R)), {}, {}
+        t_fetch = None
+
+        def launch(r):
+            argv = [exe]
+            for k, v in conf.items():
+                argv += ["-D", f"{k}={v}"]
+            argv += ["--expect", str(expected[r])] + (["--check-order"] if validate else []) + ["--"] + start
+            p = sp.Popen(argv, stdin=sp.PIPE, stdout=sp.PIPE, stderr=errlog, text=True, cwd=ROOT)
+            p.stdin.write(cmds[r][0] + "\n")  # INIT: the task starts (prewarm) while maps may still run
+            p.stdin.flush()
+            return p
+
+        def fetch(p, r):
+            p.stdin.write("\n".join(cmds[r][1:]) + "\n")
+            p.stdin.close()
+
+        while todo or running:
+            while todo and len(running) < args.node_slots:
+                r = todo.pop(0)
+                running[r] = launch(r)
+                if t_fetch is not None:  # a later container: its maps are long done
+                    fetch(running[r], r)
+            if t_fetch is None:
+                time.sleep(args.node_gap)
+                t_fetch = time.perf_counter()
+                for r, p in running.items():
+                    fetch(p, r)
+            for r, p in list(running.items()):
+                if p.poll() is not None:
+                    line = p.stdout.read().strip().splitlines()
+                    res = json.loads(line[-1]) if line else {"error": "no output"}
+                    if p.returncode != 0 or res.get("error"):
+                        raise RuntimeError(f"reduce task {r} (pid {p.pid}) failed rc={p.returncode}: {res.get('error')}")
+                    out[r] = res
+                    del running[r]
+            time.sleep(0.002)
+        t1 = time.perf_counter()
+        nbytes = sum(o["bytes"] for o in out.values())
+        med = lambda k: round(statistics.median(o[k] for o in out.values()), 1)  # noqa: E731
+        return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "bytes": nbytes,
+                "records": sum(o["records"] for o in out.values()),
+                "order_errors": sum(o["order_errors"] for o in out.values()),
+                "task_ms_median": {k: med(k) for k in ("exec_to_main_ms", "start_ms", "init_ms",
+                                                       "fetch_to_first_data_ms", "fetch_to_eof_ms", "exit_ms")},
+                "task0": out[0]["task"]}
+
+    for i in range(args.warmup):
+        st = wave(False)
+        if args.verbose:
+            print(f"# warmup {i}: {json.dumps(st)}", file=sys.stderr, flush=True)
+    stats = [wave(False) for _ in range(args.steps)]
+    validated = None
+    if not args.no_validate:
+        vst = wave(True)
+        validated = vst["order_errors"] == 0
+    ms = sum(s["wall_ms"] for s in stats) / len(stats)
+    fetch_ms = sum(s["from_fetch_ms"] for s in stats) / len(stats)
+    nbytes = stats[0]["bytes"]
+    out = {
+        "metric": "TeraSort shuffle+merge GB/s whole-node",
+        "value": round(nbytes / ms / 1e6, 3),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "ranks": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bytes",
+        "data": "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)"
+                if args.workload == "terasort" else f"synthetic secondary-sort map outputs, {args.skew:.0%} skew",
+        "config": {"model": "terasort" if args.workload == "terasort" else "secondary-sort",
+                   "global_batch": int(stats[0]["records"]), "seq_len": 104, "parallelism": "dp1",
+                   "rows_per_gpu": args.rows_per_gpu, "maps_per_gpu": args.maps_per_gpu, "reducers_per_gpu": R,
+                   "shuffle": "node shape: one MOFSupplier process (map outputs in its HBM, TCP control) + one fresh "
+                              "process per reduce task (uda_reduce_task: INIT/FETCH/dataFromUda), descriptors "
+                              "mapped over hipIpc",
+                   "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
+        "node": {"slots": args.node_slots, "gap_s": args.node_gap,
+                 "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
+                 "task_ms_median": stats[-1]["task_ms_median"]},
+        "task0_stats": json.loads(stats[-1]["task0"]) if stats[-1]["task0"] else None,
+        "provider": json.loads(b.provider_stats()),
+        "validated": validated,
+        "reference_envelope_gbps_per_node": 5.0,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    return 0
 
 
 def run_api(args, ctx) -> int:

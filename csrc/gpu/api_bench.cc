@@ -362,6 +362,39 @@ void ApiTeraSortBench::setup_secondary() {
   }
 }
 
+std::vector<std::string> ApiTeraSortBench::task_commands(int r) const {
+  const int R = cfg_.reducers, W = cfg_.world;
+  const int g = cfg_.rank * R + r;  // the job's reduce task index
+  char rt[96];
+  std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, g);
+  const std::string codec_cls = cfg_.codec == "snappy" ? "org.apache.hadoop.io.compress.SnappyCodec"
+                                : cfg_.codec == "lzo"  ? "com.hadoop.compression.lzo.LzoCodec"
+                                                       : "null";
+  std::vector<std::string> out;
+  const std::vector<std::string> init = {std::to_string(W * cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
+                                         std::to_string(16 << 10), "org.apache.hadoop.io.Text", codec_cls,
+                                         std::to_string(256 << 10), "0", "0"};
+  out.push_back(form_cmd(kInitMsg, init));
+  // rotating rank order: the tasks of rank d start with rank d + 1's maps, spreading the load
+  for (int k = 0; k < W; ++k) {
+    const int p = (cfg_.rank + 1 + k) % W;
+    const std::string host = W == 1 ? (cfg_.transport == "tcp" ? "127.0.0.1" : "localhost") : peers_[(size_t)p];
+    for (int m = 0; m < cfg_.maps; ++m) {
+      const std::vector<std::string> f = {host, cfg_.job, map_id(p * cfg_.maps + m), std::to_string(g)};
+      out.push_back(form_cmd(kFetchMsg, f));
+    }
+  }
+  return out;
+}
+
+int ApiTeraSortBench::provider_port() const {
+  if (!provider_) return -1;
+  char js[4096];
+  if (uda_stats_json(static_cast<uda_handle*>(provider_), js, sizeof(js)) <= 0) return -1;
+  const char* q = std::strstr(js, "\"port\":");
+  return q ? std::atoi(q + 7) : -1;
+}
+
 std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string* info) {
   const int R = cfg_.reducers;
   const int W = cfg_.world;
@@ -439,25 +472,8 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
         cv.notify_all();
       };
       if (!h) return fail("uda_start failed");
-      const int g = cfg_.rank * R + r;  // the job's reduce task index
-      char rt[96];
-      std::snprintf(rt, sizeof(rt), "attempt_%s_r_%06d_0", cfg_.job.c_str() + 4, g);
-      const std::string codec_cls = cfg_.codec == "snappy" ? "org.apache.hadoop.io.compress.SnappyCodec"
-                                    : cfg_.codec == "lzo"  ? "com.hadoop.compression.lzo.LzoCodec"
-                                                           : "null";
-      const std::vector<std::string> init = {std::to_string(W * cfg_.maps), cfg_.job, rt, "0", std::to_string(1 << 20),
-                                             std::to_string(16 << 10), "org.apache.hadoop.io.Text", codec_cls,
-                                             std::to_string(256 << 10), "0", "0"};
-      if (uda_do_command(h, form_cmd(kInitMsg, init).c_str()) != 0) return fail(uda_last_error(h));
-      // rotating rank order: the tasks of rank d start with rank d + 1's maps, spreading the load
-      for (int k = 0; k < W; ++k) {
-        const int p = (cfg_.rank + 1 + k) % W;
-        const std::string host = W == 1 ? "localhost" : peers_[(size_t)p];
-        for (int m = 0; m < cfg_.maps; ++m) {
-          const std::vector<std::string> f = {host, cfg_.job, map_id(p * cfg_.maps + m), std::to_string(g)};
-          if (uda_do_command(h, form_cmd(kFetchMsg, f).c_str()) != 0) return fail(uda_last_error(h));
-        }
-      }
+      for (const std::string& c : task_commands(r))
+        if (uda_do_command(h, c.c_str()) != 0) return fail(uda_last_error(h));
     });
   }
   for (auto& t : ts) t.join();

@@ -76,6 +76,12 @@ class ApiTeraSortBench {
   std::vector<int64_t> local_partition_records() const;
   void set_expected(const std::vector<int64_t>& e) { expected_ = e; }
   void set_peers(const std::vector<std::string>& hosts) { peers_ = hosts; }
+  // The commands reduce task r's host sends (its ReduceTask JVM): INIT, then one FETCH per map, in
+  // the order step() issues them. Node mode (bench.py --api --node) feeds them to reduce task
+  // processes of their own (uda_reduce_task).
+  std::vector<std::string> task_commands(int r) const;
+  // TCP port the MOFSupplier listens on (transport tcp), else -1.
+  int provider_port() const;
 
  private:
   ApiBenchConfig cfg_;

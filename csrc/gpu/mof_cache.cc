@@ -142,7 +142,7 @@ bool MofCache::make_room(int device, int64_t bytes, double now) {
 
 void MofCache::collect_ready(Entry& e, std::vector<Fire>* fire) {
   for (auto it = e.waiters.begin(); it != e.waiters.end();) {
-    if (it->need_end <= e.landed) {
+    if (it->need_end <= e.landed || !e.loading) {  // (a whole-file waiter asks past the end)
       fire->push_back(Fire{std::move(it->ready), true, ref_of(e), std::string()});
       it = e.waiters.erase(it);
     } else {

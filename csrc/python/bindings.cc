@@ -1094,6 +1094,8 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("local_partition_records", &gpu::ApiTeraSortBench::local_partition_records)
       .def("set_expected", &gpu::ApiTeraSortBench::set_expected)
       .def("set_peers", &gpu::ApiTeraSortBench::set_peers)
+      .def("task_commands", &gpu::ApiTeraSortBench::task_commands)
+      .def("provider_port", &gpu::ApiTeraSortBench::provider_port)
       .def_property_readonly("store_bytes", &gpu::ApiTeraSortBench::store_bytes);
 
   py::class_<gpu::ShuffleJob>(m, "ShuffleJob")

@@ -1,0 +1,63 @@
+"""CPU tier: uda_reduce_task, one reduce task in a process of its own (as Hadoop runs each reduce task
+in its own JVM), against a MOFSupplier in another process over the TCP transport: INIT and FETCH
+commands on stdin, the merged stream walked by the J2C consumer, one JSON line out.
+
+Reference: UdaBridge startNative / doCommandNative (src/UdaBridge.cc:187-295), NetMergerMain
+(src/Merger/NetMergerMain.cc:44-77), J2CQueue (plugins/shared/.../UdaPlugin.java:456-538)."""
+import json
+import os
+import socket
+import subprocess
+
+import pytest
+
+from uda_amd.bridge import FETCH, INIT, UdaProvider
+from uda_amd.utils import datagen
+from uda_amd.utils.mof import encode_partitions
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "uda_amd", "bin", "uda_reduce_task")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _task(native, port, job, ids, r, expect, backend="cpu", order=False):
+    argv = [EXE, "-D", "mapred.uda.transport=tcp", "-D", f"mapred.uda.merge.backend={backend}",
+            "--expect", str(expect), "--kv-buf", str(64 << 10)] + (["--check-order"] if order else [])
+    argv += ["--", "-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
+    init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_{r:06d}_0", "0", str(1 << 20),
+                                  str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0", "0"])
+    lines = [init] + [native.form_cmd(FETCH, ["127.0.0.1", job, m, str(r)]) for m in ids]
+    p = subprocess.run(argv, input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=120)
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    return p.returncode, out
+
+
+@pytest.mark.skipif(not os.access(EXE, os.X_OK), reason="uda_reduce_task not built")
+def test_reduce_task_processes_against_a_provider_process(native):
+    port = _port()
+    prov = UdaProvider(transport="tcp", data_port=port, conf={"mapred.uda.provider.bind.address": "127.0.0.1"})
+    try:
+        job = "job_7_0001"
+        maps = datagen.terasort(num_maps=5, reducers=2, rows_per_map=2000, seed=77)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_{job}_m_{i:06d}_0"
+            data, index = encode_partitions(parts, None)
+            prov.add_mof_memory(job, mid, data, index)
+            ids.append(mid)
+        for r in range(2):
+            want = sum(len(m[r]) for m in maps)
+            rc, out = _task(native, port, job, ids, r, want, order=True)
+            assert rc == 0 and out["error"] == "", out
+            assert out["records"] == want and out["order_errors"] == 0
+            assert out["task"]["maps_fetched"] == 5 and out["task"]["backend"] == "cpu"
+            assert out["fetch_to_eof_ms"] >= 0 and out["exec_to_end_ms"] >= out["fetch_to_eof_ms"]
+        rc, out = _task(native, port, job, ids, 0, 1)  # wrong expectation: the process says so
+        assert rc == 1 and "expected 1" in out["error"], out
+    finally:
+        prov.close()

@@ -34,14 +34,25 @@ def sources() -> tuple[list[str], list[str]]:
     return lib, mod
 
 
-def installed_outputs() -> tuple[str, str]:
-    ext = sysconfig.get_config_var("EXT_SUFFIX")
-    return (os.path.join(ROOT, "uda_amd", "lib", "libuda.so"), os.path.join(ROOT, "uda_amd", "_uda_native" + ext))
+def app_sources() -> list[str]:
+    """Executables: csrc/apps/<name>_main.cc -> uda_amd/bin/uda_<name>, linked against libuda.so."""
+    return sorted(glob.glob(os.path.join(ROOT, "csrc", "apps", "*_main.cc")))
 
 
-def staged_outputs(build_dir: str) -> tuple[str, str]:
+def app_name(src: str) -> str:
+    return "uda_" + os.path.basename(src)[: -len("_main.cc")]
+
+
+def installed_outputs() -> list[str]:
     ext = sysconfig.get_config_var("EXT_SUFFIX")
-    return os.path.join(build_dir, "lib", "libuda.so"), os.path.join(build_dir, "_uda_native" + ext)
+    return ([os.path.join(ROOT, "uda_amd", "lib", "libuda.so"), os.path.join(ROOT, "uda_amd", "_uda_native" + ext)] +
+            [os.path.join(ROOT, "uda_amd", "bin", app_name(s)) for s in app_sources()])
+
+
+def staged_outputs(build_dir: str) -> list[str]:
+    ext = sysconfig.get_config_var("EXT_SUFFIX")
+    return ([os.path.join(build_dir, "lib", "libuda.so"), os.path.join(build_dir, "_uda_native" + ext)] +
+            [os.path.join(build_dir, "bin", app_name(s)) for s in app_sources()])
 
 
 def install(build_dir: str) -> None:
@@ -69,7 +80,7 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
     py_inc = f"-I{pybind11.get_include()} -I{sysconfig.get_paths()['include']}"
     # link inside the flavour's build dir; install() copies into uda_amd/ (ninja alone would keep
     # a stale in-tree .so written by another flavour, its mtime being newer than our objects)
-    lib_out, mod_out = staged_outputs(build_dir)
+    lib_out, mod_out = staged_outputs(build_dir)[:2]
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     lines = [
         "ninja_required_version = 1.5",
@@ -87,6 +98,9 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
         f"  description = LINK $out",
         f"rule pymod\n  command = $hipcc -shared -fPIC{host_san} $in -o $out -L{os.path.dirname(lib_out)} "
         f"-luda -Wl,-rpath,'$$ORIGIN/lib' -L{ROCM}/lib -lamdhip64\n  description = LINK $out",
+        f"rule app\n  command = $hipcc{host_san} $in -o $out -L{os.path.dirname(lib_out)} "
+        f"-luda -Wl,-rpath,'$$ORIGIN/../lib' -L{ROCM}/lib -lamdhip64 -lpthread -Wl,-rpath,{ROCM}/lib\n"
+        f"  description = LINK $out",
     ]
     objs = []
     for s in lib_srcs:
@@ -103,7 +117,15 @@ def write_ninja(build_dir: str, debug: bool, sanitize: str | None) -> str:
         mobjs.append(o)
     lines.append(f"build {lib_out}: solib {' '.join(objs)}")
     lines.append(f"build {mod_out}: pymod {' '.join(mobjs)} | {lib_out}")
-    lines.append(f"default {mod_out}")
+    apps = []
+    for s, out in zip(app_sources(), staged_outputs(build_dir)[2:]):
+        rel = os.path.relpath(s, os.path.join(ROOT, "csrc"))
+        o = os.path.join(build_dir, rel + ".o")
+        lines.append(f"build {o}: cxx {s}")
+        lines.append(f"build {out}: app {o} | {lib_out}")
+        apps.append(out)
+    os.makedirs(os.path.join(build_dir, "bin"), exist_ok=True)
+    lines.append(f"default {mod_out} {' '.join(apps)}")
     path = os.path.join(build_dir, "build.ninja")
     os.makedirs(build_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib_out), exist_ok=True)

@@ -25,7 +25,7 @@ PY = "python3 -u"
 
 # name -> (seconds, command). Commands run from the repo root through bash.
 RECIPES: dict[str, tuple[int, str]] = {
-    "pytest": (900, f"{PY} -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread"),
+    "pytest": (900, f"{PY} -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread"),
     "smoke": (300, f"{PY} -c 'import __graft_entry__ as g; g.smoke()'"),
     "bench": (400, f"{PY} bench.py --steps 3 --warmup 1"),
     "device_only": (300, f"{PY} bench.py --device-only --steps 3 --warmup 1"),
@@ -44,7 +44,10 @@ RECIPES: dict[str, tuple[int, str]] = {
     "ipc4": (400, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --rows-per-gpu 150000000 --steps 3 --warmup 1"),
     "ipc8": (600, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
     "ipc4_host": (600, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --store host --rows-per-gpu 100000000 --steps 2 --warmup 1"),
-    "node": (600, f"{PY} bench.py --api --node --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "node": (600, f"{PY} bench.py --api --node --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "node130": (700, f"{PY} bench.py --api --node --reducers 15 --steps 2 --warmup 1"),
+    "node_gap": (600, f"{PY} bench.py --api --node --reducers 15 --node-gap 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
     "netmerger": (400, f"{PY} benchmarks/run_configs.py netmerger --gb 2 --maps 64 --reducers 1"),
     "prof_bench": (500, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- "
