@@ -238,7 +238,6 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   slot_bytes_ += (size_t)max_runs * (sizeof(RunDesc) + 4 * sizeof(int64_t) + 2 * sizeof(int)) + 64 * 16;
   if (const char* e = std::getenv("UDA_KWAY")) kway_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("UDA_KWAY_CAP")) kw_cap_ = std::atoi(e);
-  if (const char* e = std::getenv("UDA_KWAY_THREADS")) kw_threads_ = std::atoi(e) == 512 ? 512 : 256;
   if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536, 1792 or 2048");
   kw_overflow_.alloc(sizeof(int));
   HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
@@ -545,26 +544,7 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   kd.overflow = kw_overflow_.as<int>();
   kd.bad_layout = flag_.as<int>();
   kd.cap = (int)cap;
-  kd.threads = kw_threads_;
   kd.kmax = kmax;
-  const char* f4 = std::getenv("UDA_KWAY_F4");
-  kd.f4_lane = f4 && std::string(f4) == "lane";
-  static const int xcd = [] {
-    const char* e = std::getenv("UDA_KWAY_XCD");  // default on: +0.5 % device-only (profiles/r2_kway_xcd_ab.md)
-    return e ? std::atoi(e) : 1;
-  }();
-  kd.xcd_swizzle = xcd;
-  static const int nt = [] {  // non-temporal F4 stores: no measurable change (profiles/r3_kway_nt_ab.md), off
-    const char* e = std::getenv("UDA_KWAY_NT");
-    return e ? std::atoi(e) : 0;
-  }();
-  kd.nt_stores = nt;
-  const char* ip = std::getenv("UDA_KWAY_INPLACE");  // read per plan: tests flip it within one process
-  // defaults from the device-only sweep (profiles/r3_kway_occupancy.md): one LDS buffer (more
-  // workgroups per CU) and the F3 outputs spread over all threads, +18.5 % over two buffers
-  kd.inplace = ip ? std::atoi(ip) : 1;
-  const char* sp = std::getenv("UDA_KWAY_SPREAD");
-  kd.spread = sp ? std::atoi(sp) : 1;
   kp.ncells = cell_first[G];
   kp.total = total_records(runs);
   return kp;
@@ -1577,15 +1557,11 @@ StepStats ShuffleJob::run_step(bool validate) {
     }
   };
   // Runs read in place (HBM store, one rank): round q+1's cell planning is enqueued on the plan stream
-  // right after round q's tiles, so it runs beside them instead of between them (UDA_KWAY_LOOKAHEAD=0
-  // plans in line).
-  static const bool lookahead_env = [] {
-    const char* e = std::getenv("UDA_KWAY_LOOKAHEAD");
-    return !e || std::atoi(e) != 0;
-  }();
+  // right after round q's tiles, so it runs beside them instead of between them (+1.7 % device-only,
+  // profiles/r3_kway_lookahead_ab.md).
   bool lookahead = false;
   DeviceMerger::KwayPlan next_plan;
-  if (lookahead_env && !staged() && merger_->kway_enabled()) {
+  if (!staged() && merger_->kway_enabled()) {
     std::vector<RunDesc> r0;
     std::vector<int> g0;
     build_runs(0, r0, g0);

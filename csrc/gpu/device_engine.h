@@ -211,7 +211,6 @@ class DeviceMerger {
   // single-pass K-way merge (kway.hip): samples (ping-pong), splitters, cell split table, overflow
   bool kway_ = true;
   int kw_cap_ = 2048;  // records per k-way cell (UDA_KWAY_CAP); in-place LDS merge: 4 workgroups per CU
-  int kw_threads_ = 256;  // k-way workgroup size (UDA_KWAY_THREADS)
   DeviceBuffer kw_prof_, kw_overflow_;
   struct PlanBufs {  // per plan slot: samples, splitters, cell splits, sample-merge scratch
     DeviceBuffer samp_runs, samp_a, samp_b, bounds, split, splits;

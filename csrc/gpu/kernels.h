@@ -151,14 +151,8 @@ struct KwayDesc {
   int* overflow;              // cells merged by the wave-level PQ (did not fit LDS)
   int* bad_layout;            // set if a record is not TeraSort-shaped
   int cap = kKwCap;           // records per cell on the LDS path (kway_cap_supported)
-  int threads = 256;          // workgroup size: 256 or 512
   unsigned long long* prof = nullptr;  // optional [cell][5] phase timestamps (UDA_KWAY_PROF)
-  int xcd_swizzle = 0;        // map consecutive cells to one XCD (workgroups are dealt round-robin over 8 XCDs)
-  int nt_stores = 0;          // F4 output with non-temporal stores (UDA_KWAY_NT=1)
-  int inplace = 0;            // one LDS buffer, merge levels written back in place (UDA_KWAY_INPLACE)
-  int spread = 0;             // F3 outputs per thread = ceil(n / threads) instead of ITEMS (UDA_KWAY_SPREAD)
   int kmax = kKwMaxRuns;      // most runs in one group of this plan (sizes the per-slice LDS tables)
-  int f4_lane = 0;            // F4 copies one whole record per lane (UDA_KWAY_F4=lane)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

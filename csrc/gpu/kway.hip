@@ -169,9 +169,11 @@ __device__ __forceinline__ void kw_slices(const KwayDesc& kd, int c, int ncell, 
 
 // 13 x 8-byte words per record, one wave per 64 consecutive output records. All 13 loads of a
 // lane are issued before its first store: written as load -> store pairs, the compiler must assume
-// the store may alias the next load and serializes 13 HBM round trips per 64 records.
+// the store may alias the next load and serializes 13 HBM round trips per 64 records. (Measured and
+// dropped: non-temporal stores, and one whole record per lane as 16-byte pieces; both within noise,
+// profiles/r3_kway_nt_ab.md, profiles/r3_kway_occupancy.md.)
 __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const Elem* cur, int base, int valid,
-                                            uint8_t* dst, bool nt) {
+                                            uint8_t* dst) {
   constexpr int kWords = kTeraRecordBytes / 8;
   // opaque per call: otherwise the per-word lane constants (record index, word offset) of all 13
   // words are hoisted out of the caller's loop and held in ~39 VGPRs, which caps the SIMD at 5 waves
@@ -192,13 +194,8 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const E
       const int r = w / kWords;
       v[j] = ((const GlobalU64*)__shfl(src, r, 64))[w - r * kWords];
     }
-    if (nt) {  // the merged output is not re-read here: keep L2 for the record lines
 #pragma unroll
-      for (int j = 0; j < kWords; ++j) __builtin_nontemporal_store(v[j], d + j * 64 + lane);
-    } else {
-#pragma unroll
-      for (int j = 0; j < kWords; ++j) d[j * 64 + lane] = v[j];
-    }
+    for (int j = 0; j < kWords; ++j) d[j * 64 + lane] = v[j];
     return;
   }
   const int words = valid * kWords;
@@ -216,55 +213,30 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const E
   }
 }
 
-// F4 alternative (UDA_KWAY_F4=lane): lane l copies output record base + l whole, as six 16-byte
-// pieces and one 8-byte piece with immediate offsets from one address (no per-word cross-lane
-// address shuffles, no per-word index arithmetic); stores are 16 bytes at a 104-byte stride.
-__device__ __forceinline__ void kw_copy_lane(const uint8_t* const* sbase, const Elem* cur, int base, int valid,
-                                             uint8_t* dst) {
-  typedef unsigned int U4 __attribute__((ext_vector_type(4), aligned(4)));
-  typedef unsigned int U2 __attribute__((ext_vector_type(2), aligned(4)));
-  typedef __attribute__((address_space(1))) const U4 GU4;
-  typedef __attribute__((address_space(1))) const U2 GU2;
-  const int lane = threadIdx.x & 63;
-  if (lane >= valid) return;
-  const Elem e = cur[base + lane];
-  const uint8_t* src = sbase[(int)((e.lo >> 32) & 0xFFFF)] + (int64_t)(e.lo & 0xFFFFFFFFull) * kTeraRecordBytes;
-  GU4* s4 = (GU4*)(uintptr_t)src;
-  U4 v[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) v[j] = s4[j];
-  const U2 t = *(GU2*)(uintptr_t)(src + 96);
-  uint8_t* d = dst + (int64_t)lane * kTeraRecordBytes;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) reinterpret_cast<U4*>(d)[j] = v[j];
-  *reinterpret_cast<U2*>(d + 96) = t;
-}
-
 }  // namespace
 
-// ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffers are dynamic, so
-// smaller capacities fit more workgroups per CU. INPLACE: one cap x 16-byte buffer instead of two; a
-// merge level keeps each thread's outputs in registers, waits for every thread to finish reading, then
-// writes them back in place (two barriers per level instead of one), halving the LDS per workgroup.
-template <int ITEMS, int THREADS, bool INPLACE>
-__global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
+// ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffer is dynamic, so
+// smaller capacities fit more workgroups per CU. One cap x 16-byte buffer: a merge level keeps each
+// thread's outputs in registers, waits for every thread to finish reading, then writes them back in
+// place (two barriers per level), half the LDS of ping-pong buffers (+18.5 %, r3_kway_occupancy.md).
+template <int ITEMS>
+__global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
   constexpr int kKwItems = ITEMS;
-  constexpr int kKwThreads = THREADS;
-  constexpr int kKwWaves = THREADS / 64;
+  constexpr int kKwThreads = 256;
+  constexpr int kKwWaves = kKwThreads / 64;
   constexpr int kCap = ITEMS * kKwThreads;
   extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
   Elem* bufA = kw_dyn;
-  Elem* bufB = INPLACE ? kw_dyn : kw_dyn + kCap;
-  // per-slice tables behind the element buffer(s), sized by the plan's largest group (kd.kmax): a
+  // per-slice tables behind the element buffer, sized by the plan's largest group (kd.kmax): a
   // 32-run round needs 388 bytes here, not the 2.5 KiB a static kKwMaxRuns table would pin
-  const uint8_t** sbase = reinterpret_cast<const uint8_t**>(kw_dyn + (INPLACE ? 1 : 2) * kCap);  // slice starts
+  const uint8_t** sbase = reinterpret_cast<const uint8_t**>(kw_dyn + kCap);  // slice starts
   int* seg = reinterpret_cast<int*>(sbase + kd.kmax);  // [K + 1] slice offsets within the cell
   __shared__ int64_t s_start;
   // The dispatcher deals workgroups round-robin over the 8 XCDs (each with its own L2); with the
   // swizzle, XCD x takes a contiguous block of cells, so neighbouring cells of a group (adjacent
   // slices of the same runs, sharing the boundary record lines) meet in one L2.
   int64_t b = blockIdx.x;
-  if (kd.xcd_swizzle) {
+  {
     const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
     b = x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
   }
@@ -384,12 +356,11 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
   stamp(2);
   // ---- F3: pairwise merge levels inside LDS
   Elem* src = bufA;
-  Elem* dst = bufB;
-  // outputs per thread: the full ITEMS, or (spread) n spread evenly over the workgroup, so a cell
-  // filled to half its capacity keeps every thread busy with half as long a merge chain
-  const int ipt = kd.spread ? (n + kKwThreads - 1) / kKwThreads : kKwItems;
+  // outputs per thread: n spread evenly over the workgroup, so a cell filled to 65 % of its capacity
+  // keeps every thread busy with a 65 % long merge chain
+  const int ipt = (n + kKwThreads - 1) / kKwThreads;
   const int o0 = threadIdx.x * ipt;
-  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // INPLACE: this thread's outputs of the current level
+  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // this thread's outputs of the current level
   for (int w = 1; w < K; w <<= 1) {
     if (o0 < n) {
       const int npairs = (K + 2 * w - 1) / (2 * w);
@@ -439,11 +410,8 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
         Elem v;  // field-wise select: a select of the two structs becomes a scratch slot + indexed load
         v.hi = take_a ? va.hi : vb.hi;
         v.lo = take_a ? va.lo : vb.lo;
-        if (INPLACE) {
-          held_hi[k] = v.hi;
-          held_lo[k] = v.lo;
-        } else
-          dst[o] = v;
+        held_hi[k] = v.hi;
+        held_lo[k] = v.lo;
         if (take_a) {
           ++ia;
           va = src[min(a0 + ia, n - 1)];
@@ -454,29 +422,21 @@ __global__ void __launch_bounds__(THREADS) kway_tile_kernel(KwayDesc kd, uint8_t
       }
     }
     __syncthreads();
-    if (INPLACE) {  // every thread has read the level: overwrite it with the merged order
-      if (o0 < n) {
-        const int todo = min(ipt, n - o0);
+    // every thread has read the level: overwrite it with the merged order
+    if (o0 < n) {
+      const int todo = min(ipt, n - o0);
 #pragma unroll
-        for (int k = 0; k < kKwItems; ++k)
-          if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
-      }
-      __syncthreads();
-    } else {
-      Elem* t = src;
-      src = dst;
-      dst = t;
+      for (int k = 0; k < kKwItems; ++k)
+        if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
     }
+    __syncthreads();
   }
   stamp(3);
   // ---- F4: records in merged order straight to the output
   const int wave = threadIdx.x >> 6;
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
-    if (kd.f4_lane)
-      kw_copy_lane(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
-    else
-      kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes, kd.nt_stores != 0);
+    kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
   }
   if (kd.prof) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -505,42 +465,29 @@ void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem
 int kway_cap_supported(int cap) { return cap == 2048 || cap == 1792 || cap == 1536 || cap == 1024 || cap == 512; }
 
 namespace {
-template <int ITEMS, int THREADS, bool INPLACE>
-void launch_kway_v(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
-  const size_t elems = (INPLACE ? 1 : 2) * sizeof(Elem) * (size_t)(ITEMS * THREADS);
+template <int ITEMS>
+void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
+  const size_t elems = sizeof(Elem) * (size_t)(ITEMS * 256);
   auto tables = [](int k) { return (size_t)k * sizeof(void*) + (size_t)(k + 1) * sizeof(int); };
   if (kd.kmax < 1 || kd.kmax > kKwMaxRuns) throw std::runtime_error("kway: bad runs per group " + std::to_string(kd.kmax));
   const size_t lds = (elems + tables(kd.kmax) + 15) & ~(size_t)15;
   static std::once_flag once;
   std::call_once(once, [elems, tables] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, THREADS, INPLACE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(elems + tables(kKwMaxRuns) + 16));
   });
-  hipLaunchKernelGGL((kway_tile_kernel<ITEMS, THREADS, INPLACE>), dim3((unsigned)ncells), dim3(THREADS), lds, s, kd,
-                     out);
-}
-
-template <int ITEMS, int THREADS>
-void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
-  if (kd.inplace)
-    launch_kway_v<ITEMS, THREADS, true>(kd, ncells, out, s);
-  else
-    launch_kway_v<ITEMS, THREADS, false>(kd, ncells, out, s);
+  hipLaunchKernelGGL((kway_tile_kernel<ITEMS>), dim3((unsigned)ncells), dim3(256), lds, s, kd, out);
 }
 }  // namespace
 
 void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
   if (ncells <= 0) return;
-  const bool wide = kd.threads == 512;
   switch (kd.cap) {
-    case 2048: wide ? launch_kway<4, 512>(kd, ncells, out, s) : launch_kway<8, 256>(kd, ncells, out, s); break;
-    case 1792:  // 256 threads only: 28.4 KiB in place, 5 workgroups per CU
-      if (wide) throw std::runtime_error("kway: cell capacity 1792 needs 256-thread workgroups");
-      launch_kway<7, 256>(kd, ncells, out, s);
-      break;
-    case 1536: wide ? launch_kway<3, 512>(kd, ncells, out, s) : launch_kway<6, 256>(kd, ncells, out, s); break;
-    case 1024: wide ? launch_kway<2, 512>(kd, ncells, out, s) : launch_kway<4, 256>(kd, ncells, out, s); break;
-    case 512: wide ? launch_kway<1, 512>(kd, ncells, out, s) : launch_kway<2, 256>(kd, ncells, out, s); break;
+    case 2048: launch_kway<8>(kd, ncells, out, s); break;
+    case 1792: launch_kway<7>(kd, ncells, out, s); break;  // 28.4 KiB, 5 workgroups per CU
+    case 1536: launch_kway<6>(kd, ncells, out, s); break;
+    case 1024: launch_kway<4>(kd, ncells, out, s); break;
+    case 512: launch_kway<2>(kd, ncells, out, s); break;
     default: throw std::runtime_error("kway: unsupported cell capacity " + std::to_string(kd.cap));
   }
 }

@@ -213,16 +213,12 @@ def test_spill_tiers_multirank_staged(require_gpu, tmp_path, monkeypatch, world,
                 jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
 
 
-@pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}, {"UDA_KWAY_INPLACE": "1"},
-                                 {"UDA_KWAY_INPLACE": "0"}, {"UDA_KWAY_INPLACE": "1", "UDA_KWAY_CAP": "2048"},
-                                 {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"},
-                                 {"UDA_KWAY_SPREAD": "1", "UDA_KWAY_INPLACE": "1"}, {"UDA_KWAY_SPREAD": "1"},
-                                 {"UDA_KWAY_F4": "lane"}, {"UDA_KWAY_F4": "lane", "UDA_KWAY_THREADS": "512"}])
+@pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}, {"UDA_KWAY_CAP": "1536"},
+                                 {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"}, {"UDA_KWAY_CAP": "1024"}])
 def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
     """The single-pass K-way merge (default) and the pairwise merge-path tree (UDA_KWAY=0) order
     records identically; UDA_KWAY_TARGET above the LDS capacity routes every cell through the
-    wave-level priority queue, which must give the same stream; so must the in-place LDS merge
-    (UDA_KWAY_INPLACE, one buffer per workgroup) and the two-buffer one."""
+    wave-level priority queue, which must give the same stream; so must every cell capacity."""
     ref = _job(60000, 6, 2, reducers=2, **SMALL)
     readers = [J2CQueueReader(max_len=64 << 10) for _ in range(2)]
     ref.use_python_sink(lambda r, b: readers[r].feed(b), with_reducer=True)
