@@ -94,9 +94,6 @@ struct DeviceWorkspace {
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
-  // D2H link gate of this task's deliveries (see D2HLinkGate); slots 0: ungated
-  int gate_device = 0, gate_slots = 0;
-  int64_t gate_left = 0;  // bytes this task still has to deliver (its priority)
   ~DeviceWorkspace() {
     if (h2d_sig.handle) {
       try {
@@ -109,15 +106,7 @@ struct DeviceWorkspace {
       if (e) (void)hipEventDestroy(e);
     if (cs) (void)hipStreamDestroy(cs);
   }
-  void reset_stats() {
-    h2d_ms = device_ms = d2h_ms = sink_ms = 0;
-    gate_slots = 0;
-  }
-  void gate(int device, int slots, int64_t left) {
-    gate_device = device;
-    gate_slots = slots;
-    gate_left = left;
-  }
+  void reset_stats() { h2d_ms = device_ms = d2h_ms = sink_ms = 0; }
   // D2H stream of streamed deliveries (the merge stream is busy with the next round)
   hipStream_t copy_stream() {
     if (!cs) HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
@@ -653,52 +642,6 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   return res;
 }
 
-// D2H pieces in flight per device (mapred.uda.gpu.d2h.slots). Concurrent copies share the PCIe link
-// about evenly, so with every task's delivery in flight at once the task with the most to deliver (a
-// skewed reducer, whose single consumer thread bounds the job) gets 1/16 of the link and its consumer
-// starves while the small tasks finish. With a few slots, a free slot goes to the waiting task with the
-// most bytes left (longest delivery first): that task streams at its consumer's rate from the start
-// and the others share the rest of the link.
-// off by default: with the slot freed as the copy lands, config #5 gained 4 % and 16 uniform staged tasks
-// lost 3 % (both within box noise; profiles/r3_d2h_gate_ab.md)
-constexpr int kD2HSlotsDefault = 0;
-
-class D2HLinkGate {
- public:
-  // 0: D2H pieces; 1: generic device merges of descriptor tasks (mapred.uda.gpu.merge.slots)
-  static D2HLinkGate& get(int which = 0) {
-    static D2HLinkGate* g[2] = {new D2HLinkGate, new D2HLinkGate};  // never destroyed: tasks may outlive static teardown
-    return *g[which & 1];
-  }
-  void acquire(int device, int slots, int64_t left) {
-    std::unique_lock<std::mutex> lk(mu_);
-    Dev& d = devs_[device];
-    const auto me = d.waiting.emplace(-left, d.next++).first;  // ordered: most bytes left first, then FIFO
-    cv_.wait(lk, [&] { return d.used < slots && d.waiting.begin() == me; });
-    d.waiting.erase(me);
-    ++d.used;
-    cv_.notify_all();
-  }
-  void release(int device) {
-    std::lock_guard<std::mutex> g(mu_);
-    --devs_[device].used;
-    cv_.notify_all();
-  }
-  // host function enqueued behind a gated copy: frees the slot the moment the copy has landed (not when
-  // the task comes back for it after consuming the previous piece)
-  static void release_cb(void* device) { get().release((int)(intptr_t)device); }
-
- private:
-  struct Dev {
-    int used = 0;
-    uint64_t next = 0;
-    std::set<std::pair<int64_t, uint64_t>> waiting;
-  };
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::map<int, Dev> devs_;
-};
-
 // Stream the merged output of `m` (in ws.out) to the host in pieces of up to kPieceBytes that end on
 // record boundaries (the cuts), double-buffered through pinned memory: the D2H of piece k+1 runs
 // while fn(piece k) consumes it. fn(ptr, first_cut, last_cut) gets the bytes of cuts
@@ -724,86 +667,20 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
     while (k < nb && m.cuts[k + 1] - start <= kPieceBytes) ++k;
     pb.push_back(k);
   }
-  // UDA_NM_D2H_SDMA=1: D2H on the SDMA delivery engine instead of hipMemcpyAsync (a blit kernel on the
-  // CUs). SDMA copies are not stream-ordered, so the round's output is complete once `s` has drained.
-  // Off by default: 16 concurrent host-MOF tasks gain ~10 % (33.2 vs 30.0 GB/s) but a single task lost
-  // its round overlap in some runs (11.6-22.7 vs 22.6-23.4 GB/s; profiles/r2_nm_d2h_sdma_ab.md).
-  static const bool use_sdma = [] {
-    const char* e = std::getenv("UDA_NM_D2H_SDMA");
-    return e && std::atoi(e) != 0;
-  }();
-  struct SdmaPieces {
-    gpu::SdmaEngine* eng = nullptr;
-    hsa_signal_t sig[2]{};
-    ~SdmaPieces() {
-      if (!eng) return;
-      for (auto& g : sig) {  // copies still in flight (fn threw) land before the ring is reused
-        try {
-          gpu::SdmaEngine::wait(g);
-        } catch (...) {
-        }
-        eng->destroy_signal(g);
-      }
-    }
-  } sp;
-  if (use_sdma) {
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    try {
-      gpu::SdmaEngine& e = gpu::SdmaEngine::for_device(dev);
-      sp.sig[0] = e.make_signal();
-      sp.sig[1] = e.make_signal();
-      sp.eng = &e;
-    } catch (const std::exception&) {
-      sp.eng = nullptr;
-    }
-    if (sp.eng) HIP_CHECK(hipStreamSynchronize(s));
-  }
-  // gated deliveries hold a slot from the piece's enqueue until its copy has landed
-  struct GateHold {
-    DeviceWorkspace& w;
-    bool held = false;
-    void take() {
-      if (w.gate_slots > 0) {
-        D2HLinkGate::get().acquire(w.gate_device, w.gate_slots, w.gate_left);
-        held = true;
-      }
-    }
-    void drop() {
-      if (held) D2HLinkGate::get().release(w.gate_device);
-      held = false;
-    }
-    ~GateHold() { drop(); }
-  } gh{ws};
   auto enqueue = [&](size_t piece) {
     const int slot = (int)(piece & 1);
     const int64_t b = m.cuts[pb[piece]], e = m.cuts[pb[piece + 1]];
     if (e - b > kPieceBytes) throw UdaError("record larger than the D2H piece");
-    gh.take();
-    if (sp.eng) {
-      gpu::SdmaEngine::arm(sp.sig[slot], sp.eng->parts((size_t)(e - b), 1));
-      sp.eng->copy_d2h(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b), sp.sig[slot], 1);
-      return;
-    }
     HIP_CHECK(hipMemcpyAsync(ws.ring.as<uint8_t>() + slot * kPieceBytes, out + b, (size_t)(e - b),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(ws.piece_ev[slot], s));
-    if (gh.held) {
-      HIP_CHECK(hipLaunchHostFunc(s, &D2HLinkGate::release_cb, (void*)(intptr_t)ws.gate_device));
-      gh.held = false;  // the stream releases it
-    }
   };
   const size_t np = pb.size() - 1;
   enqueue(0);
   for (size_t piece = 0; piece < np; ++piece) {
     const int slot = (int)(piece & 1);
     auto t0 = std::chrono::steady_clock::now();
-    if (sp.eng)
-      gpu::SdmaEngine::wait(sp.sig[slot]);
-    else
-      HIP_CHECK(hipEventSynchronize(ws.piece_ev[slot]));
-    gh.drop();
-    ws.gate_left -= m.cuts[pb[piece + 1]] - m.cuts[pb[piece]];
+    HIP_CHECK(hipEventSynchronize(ws.piece_ev[slot]));
     auto t1 = std::chrono::steady_clock::now();
     ws.d2h_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     const int64_t tp = trace::host_enabled() ? trace::now_ns() : 0;
@@ -1141,13 +1018,9 @@ void ReduceTask::merge_gpu() {
       const auto td = std::chrono::steady_clock::now();
       const int64_t tt = trace::host_enabled() ? trace::now_ns() : 0;
       // on the SDMA delivery engine (idle until the RPQ rounds deliver), not a blit kernel on the CUs
-      // the next LPQ merge needs; device_merge returned with `s` drained (UDA_LPQ_D2H_SDMA=0: blit)
-      static const bool sdma_d2h = [] {
-        const char* e = std::getenv("UDA_LPQ_D2H_SDMA");
-        return !e || std::atoi(e) != 0;
-      }();
+      // the next LPQ merge needs; device_merge returned with `s` drained
       gpu::SdmaEngine* eng = nullptr;
-      if (sdma_d2h && m.bytes > 0) {
+      if (m.bytes > 0) {
         try {
           eng = &gpu::SdmaEngine::for_device(device);
         } catch (const std::exception&) {
@@ -1591,13 +1464,6 @@ void ReduceTask::merge_gpu() {
       st_.records += m.records;
     };
     const int64_t kv = kv_buf_size_ - kEofBytes;
-    const int d2h_slots = (int)host_->conf_i64("mapred.uda.gpu.d2h.slots", kD2HSlotsDefault);
-    int64_t task_bytes = 0;
-    for (const Span& sp : group) task_bytes += sp.len;
-    if (prog)
-      for (int64_t c : prog->cap) task_bytes += c;
-    for (const SpillRun& r : spills) task_bytes += r.bytes;
-    ws.gate(device, d2h_slots, task_bytes);
 
     lpq_wait();  // an LPQ of the fetch phase may still be merging
     double prog_fetch_ms = -1;
@@ -1809,14 +1675,12 @@ void ReduceTask::merge_gpu() {
       ws2_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
       ws2 = ws2_lease.obj.get();
       ws2->reset_stats();
-      ws2->gate(device, d2h_slots, task_bytes);
       // Three workspaces, two rounds prepared ahead: round q + 2's slices cross PCIe (SDMA H2D) while
       // round q + 1 merges and round q is delivered (D2H), so the rounds cost max(H2D, merge, D2H)
       // each instead of H2D + merge.
       ws3_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
       ws3 = ws3_lease.obj.get();
       ws3->reset_stats();
-      ws3->gate(device, d2h_slots, task_bytes);
       StreamGuard sg2, sg3;
       HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
       HIP_CHECK(hipStreamCreateWithFlags(&sg3.s, hipStreamNonBlocking));
@@ -1839,12 +1703,8 @@ void ReduceTask::merge_gpu() {
             views.push_back(Span{p, e - b});
           }
         }
-        // views: pinned host spans (spill arena or slice arena): SDMA H2D (UDA_RPQ_H2D_SDMA=0: blit)
-        static const bool sdma_h2d = [] {
-          const char* e = std::getenv("UDA_RPQ_H2D_SDMA");
-          return !e || std::atoi(e) != 0;
-        }();
-        return device_merge(*wsv[q % 3], views, Codec::kNone, kind_, kv, sv[q % 3], nullptr, sdma_h2d);
+        // views: pinned host spans (spill arena or slice arena): SDMA H2D, not a blit kernel
+        return device_merge(*wsv[q % 3], views, Codec::kNone, kind_, kv, sv[q % 3], nullptr, true);
       };
       std::vector<std::future<DeviceMergeOut>> next((size_t)rounds);
       for (int q = 0; q < std::min(rounds, 2); ++q) next[(size_t)q] = std::async(std::launch::async, prep, q);
@@ -2255,14 +2115,6 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     s = sg.s;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
-  {
-    int64_t left = 0;
-    for (int64_t l : rlen) left += l;
-    ws.gate(device, (int)host_->conf_i64("mapred.uda.gpu.d2h.slots", kD2HSlotsDefault), left);
-  }
-  const int merge_slots = (int)host_->conf_i64("mapred.uda.gpu.merge.slots", 0);
-  int64_t merge_left = 0;
-  for (int64_t l : rlen) merge_left += l;
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
   // dataFromUda): the consumer's work (the reduce task's bound when one task holds most of the data)
   // never waits for the merge driver, and the merge reuses an output only after its delivery.
@@ -2373,20 +2225,6 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       continue;
     }
     const uint8_t* dst = outs[q & 1]->as<uint8_t>();
-    // merge turns (mapred.uda.gpu.merge.slots > 0): at most that many tasks' rounds merge at once,
-    // the next turn to the task with the most input left, so a skewed task's next round does not queue
-    // behind every other task's first merge while its consumer idles
-    struct Turn {
-      int device = -1;
-      ~Turn() {
-        if (device >= 0) D2HLinkGate::get(1).release(device);
-      }
-    } turn;
-    if (merge_slots > 0) {
-      D2HLinkGate::get(1).acquire(device, merge_slots, merge_left);
-      turn.device = device;
-    }
-    for (int64_t l : sl) merge_left -= l;
     const auto tq = std::chrono::steady_clock::now();
     bool round_closed = false;
     gpu::GenericMergeResult r = ws.merger.merge(

@@ -424,7 +424,6 @@ class IpcExchange : public Exchange {
         grp_(name, rank, world, (size_t)256 << 10, 16 + (size_t)8 * world + kMaxEntries * sizeof(Entry),
              env_timeout()) {
     HIP_CHECK(hipSetDevice(device_));
-    if (const char* c = std::getenv("UDA_IPC_COPY")) kernel_copy_ = std::string(c) != "memcpy";
     descs_.resize(4);
     for (auto& d : descs_) HIP_CHECK(hipEventCreateWithFlags(&d.uploaded, hipEventDisableTiming));
     progress_ = std::thread([this] { progress_loop(); });
@@ -446,7 +445,7 @@ class IpcExchange : public Exchange {
   }
   int rank() const override { return rank_; }
   int world() const override { return world_; }
-  std::string name() const override { return kernel_copy_ ? "ipc" : "ipc-memcpy"; }
+  std::string name() const override { return "ipc"; }
 
   void alltoall_i64(const int64_t* send, int64_t* recv, size_t n, hipStream_t) override {
     grp_.alltoall_i64(send, recv, n);
@@ -501,11 +500,7 @@ class IpcExchange : public Exchange {
         check_pairing(from, rank_, sizes, recv[from]);
         for (int i = 0; i < c; ++i) {
           const uint8_t* src = peer_ptr(from, pe[i].alloc, pe[i].off, pe[i].bytes);
-          if (kernel_copy_)
-            copies.push_back(CopyDesc{src, const_cast<uint8_t*>(recv[from][i].ptr), pe[i].bytes});
-          else
-            HIP_CHECK(hipMemcpyAsync(const_cast<uint8_t*>(recv[from][i].ptr), src, (size_t)pe[i].bytes,
-                                     hipMemcpyDeviceToDevice, s));
+          copies.push_back(CopyDesc{src, const_cast<uint8_t*>(recv[from][i].ptr), pe[i].bytes});
           max_bytes = std::max(max_bytes, pe[i].bytes);
           bytes_pulled_ += pe[i].bytes;
         }
@@ -682,7 +677,6 @@ class IpcExchange : public Exchange {
   std::deque<std::pair<int64_t, hipEvent_t>> pending_;
   std::vector<hipEvent_t> free_ev_;
   bool stop_ = false;
-  bool kernel_copy_ = true;  // UDA_IPC_COPY=memcpy: one hipMemcpyAsync per slice instead
   struct DescSlot {
     PinnedBuffer host;
     DeviceBuffer dev;

@@ -707,33 +707,6 @@ __device__ __forceinline__ void copy_small(const uint8_t* s, uint8_t* d, int L) 
   }
 }
 
-__global__ void __launch_bounds__(256) gather_var_kernel(GenericKeyCtx ctx, const Elem* elems, int64_t n,
-                                                         const int64_t* out_off, uint8_t* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t g = elems[i].lo & 0xFFFFFFFFFFFFull;
-  const uint8_t* src = ctx.recptr[g];
-  const int L = ctx.reclen[g];
-  uint8_t* dst = out + out_off[i];
-  if (L < 16) {
-    copy_small(src, dst, L);
-    return;
-  }
-  for (int base = 0; base < L; base += 128) {
-    u32x4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int off = min(base + 16 * k, L - 16);
-      v[k] = *reinterpret_cast<const u32x4_u*>(src + off);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int off = min(base + 16 * k, L - 16);
-      *reinterpret_cast<u32x4_u*>(dst + off) = v[k];
-    }
-  }
-}
-
 // F4 with kGatherLanes lanes per record: the lanes of a group copy 16-byte pieces of one record, so a
 // wave's load touches 64 / kGatherLanes records (two or three cache lines each) instead of 64, and
 // consecutive groups write consecutive output records. Pieces past the record end are clamped to its
@@ -926,12 +899,7 @@ void launch_exclusive_scan(const int64_t* in, int64_t* out, int64_t n, int64_t* 
 void launch_gather_var(GenericKeyCtx ctx, const Elem* elems, int64_t n, const int64_t* out_off, uint8_t* out,
                        hipStream_t s) {
   if (n <= 0) return;
-  const char* e = std::getenv("UDA_GATHER_LANE");  // 1: the lane-per-record gather (A/B measurement)
-  if (e && std::atoi(e) != 0) {
-    hipLaunchKernelGGL(gather_var_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ctx, elems, n, out_off,
-                       out);
-    return;
-  }
+  // 8 lanes per record (one record per lane measured 0.8 ms slower on the 2 GB secondary sort)
   hipLaunchKernelGGL(gather_var_grp_kernel<8>, dim3((unsigned)((n * 8 + 255) / 256)), dim3(256), 0, s, ctx, elems, n,
                      out_off, out);
 }

@@ -360,15 +360,13 @@ def test_generic_kway_recursive_sample_merge(require_gpu, monkeypatch, recurse):
 
 
 @pytest.mark.parametrize("conf_extra", [
-    {"mapred.uda.gpu.d2h.slots": 1},                                   # every delivery piece through the gate
     {"mapred.uda.gpu.prewarm": 1, "mapred.uda.gpu.prewarm.pinned.mb": 64},
     {"mapred.uda.gpu.prewarm": 0, "mapred.uda.gpu.progressive.phases": 0},
-    {"mapred.uda.gpu.merge.bytes": 200_000, "mapred.uda.gpu.spill": "host", "mapred.uda.gpu.d2h.slots": 1},
+    {"mapred.uda.gpu.merge.bytes": 200_000, "mapred.uda.gpu.spill": "host"},
 ])
 def test_consumer_gpu_gate_and_prewarm(require_gpu, conf_extra):
-    """The D2H link gate (slots freed by a stream host function as each piece lands) and the INIT-time
-    prewarm change when work happens, never what is delivered: the stream equals the CPU merge's,
-    including a direct-RPQ hybrid task whose rounds all go through a one-slot gate."""
+    """The INIT-time prewarm and the phase / hybrid choices change when work happens, never what is
+    delivered: the stream equals the CPU merge's, including a direct-RPQ hybrid task."""
     from uda_amd.utils.mof import encode_partitions
     p = UdaProvider()
     try:
