@@ -535,7 +535,7 @@ def run_api(args, ctx) -> int:
             "dtype": "bytes",
             "data": ("synthetic secondary-sort map outputs generated in HBM: 22-62 byte Text keys sharing "
                      "5-50 byte prefixes, 0-120 byte values, "
-                     f"{args.skew:.0%} of every map's records to reduce task 0")
+                     f"{args.skew:.0%} of every map's records to reduce task 0" + (" of every rank" if world > 1 else ""))
                     if args.workload == "secondary" else
                     "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
             "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),

@@ -168,6 +168,7 @@ int64_t ApiTeraSortBench::store_bytes() const {
 }
 
 std::vector<int64_t> ApiTeraSortBench::local_partition_records() const {
+  if (cfg_.workload == "secondary") return sec_part_records_;
   return gen_ ? gen_->local_dest_records() : std::vector<int64_t>();
 }
 
@@ -317,19 +318,21 @@ void ApiTeraSortBench::compress_store() {
 // Secondary-sort map outputs (secgen.h) generated straight into one HBM store and registered as
 // device MOFs: the reduce tasks take the generic-key device merge (key-range rounds).
 void ApiTeraSortBench::setup_secondary() {
-  if (cfg_.world != 1) throw std::runtime_error("api bench: the secondary workload runs with world 1");
   HIP_CHECK(hipSetDevice(cfg_.device));
-  const int P = cfg_.reducers;
-  const SecGenPlan plan = secgen_plan(cfg_.maps, P, cfg_.records_per_map, cfg_.skew, cfg_.seed);
+  // partitions of every rank's maps: world x reducers; reduce task 0 of every rank is the hot one
+  const int P = cfg_.world * cfg_.reducers;
+  const SecGenPlan plan = secgen_plan(cfg_.maps, P, cfg_.records_per_map, cfg_.skew,
+                                      cfg_.seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)cfg_.rank), cfg_.reducers);
   sec_store_bytes_ = plan.store_bytes();
   sec_store_.reset(new DeviceBuffer((size_t)sec_store_bytes_, /*resident=*/true));
   hipStream_t s;
   HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   secgen_write(plan, sec_store_->as<uint8_t>(), s);
   HIP_CHECK(hipStreamDestroy(s));
-  expected_.assign((size_t)P, 0);
+  sec_part_records_.assign((size_t)P, 0);
   for (int m = 0; m < cfg_.maps; ++m)
-    for (int q = 0; q < P; ++q) expected_[(size_t)q] += plan.nrec[(size_t)m * P + q];
+    for (int q = 0; q < P; ++q) sec_part_records_[(size_t)q] += plan.nrec[(size_t)m * P + q];
+  if (cfg_.world == 1) expected_ = sec_part_records_;
   ConfTable& conf = bench_conf(cfg_);
   auto* pctx = new ProviderCtx{&conf, this};
   provider_ctx_ = pctx;
@@ -346,7 +349,7 @@ void ApiTeraSortBench::setup_secondary() {
   provider_ = h;
   map_ids_.clear();
   for (int m = 0; m < cfg_.maps; ++m) {
-    const std::string id = map_id(m);
+    const std::string id = map_id(cfg_.rank * cfg_.maps + m);
     map_ids_.push_back(id);
     std::vector<int64_t> index;
     int64_t off = 0;

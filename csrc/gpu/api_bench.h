@@ -52,7 +52,7 @@ struct ApiBenchConfig {
   std::string mof_dir;
   int64_t provider_hbm_bytes = 0;
   // "terasort" or "secondary": variable-length Text keys with long common prefixes, `skew` of every
-  // map's records in reduce task 0 (BASELINE config #5; device generator secgen.h; world 1)
+  // map's records in reduce task 0 of every rank (BASELINE config #5; device generator secgen.h)
   std::string workload = "terasort";
   double skew = 0.6;
   // "snappy" / "lzo": every partition is block-compressed (256 KiB blocks) at setup and the compressed
@@ -93,6 +93,7 @@ class ApiTeraSortBench {
   std::vector<std::vector<uint8_t>> host_mofs_;  // host_mofs: the MOFs' bytes in host memory
   std::unique_ptr<DeviceBuffer> sec_store_;  // secondary workload: the MOFs in HBM
   int64_t sec_store_bytes_ = 0;
+  std::vector<int64_t> sec_part_records_;  // secondary workload: this rank's maps' records per partition
   std::string map_id(int global_map) const;
   void setup_secondary();
   void compress_store();

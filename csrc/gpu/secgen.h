@@ -1,5 +1,5 @@
 // Device generator of secondary-sort map outputs (variable-length Text keys with long common
-// prefixes, `skew` of every map's records in partition 0). See secgen.hip.
+// prefixes, `skew` of every map's records in the hot partitions). See secgen.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,8 +19,12 @@ struct SecGenPlan {
   int64_t store_bytes() const { return mof_off.empty() ? 0 : mof_off.back(); }
 };
 
-// Record counts and exact byte sizes (computed on the current device).
-SecGenPlan secgen_plan(int maps, int partitions, int64_t records_per_map, double skew, uint64_t seed);
+// Record counts and exact byte sizes (computed on the current device). Hot partitions: every
+// `hot_every`-th (0, hot_every, 2 * hot_every, ...; hot_every <= 0: partition 0 only) shares `skew` of
+// every map's records evenly, the other partitions share the rest (a multi-GPU job: reduce task 0 of
+// every GPU is the skewed one).
+SecGenPlan secgen_plan(int maps, int partitions, int64_t records_per_map, double skew, uint64_t seed,
+                       int hot_every = 0);
 // Write every MOF into `store` (device, store_bytes() bytes). Synchronizes `s`.
 void secgen_write(const SecGenPlan& p, uint8_t* store, hipStream_t s);
 

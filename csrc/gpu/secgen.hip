@@ -118,22 +118,32 @@ __global__ void secgen_eof_kernel(const int64_t* eof_at, int nruns, uint8_t* bas
 }
 }  // namespace
 
-SecGenPlan secgen_plan(int maps, int partitions, int64_t records_per_map, double skew, uint64_t seed) {
+SecGenPlan secgen_plan(int maps, int partitions, int64_t records_per_map, double skew, uint64_t seed,
+                       int hot_every) {
   SecGenPlan p;
   p.maps = maps;
   p.partitions = partitions;
   p.seed = seed;
   p.nrec.assign((size_t)maps * partitions, 0);
+  if (hot_every <= 0 || hot_every > partitions) hot_every = partitions;
+  const int nhot = (partitions + hot_every - 1) / hot_every, ncold = partitions - nhot;
   for (int m = 0; m < maps; ++m) {
     int64_t* n = &p.nrec[(size_t)m * partitions];
-    if (partitions == 1) {
-      n[0] = records_per_map;
+    if (ncold == 0) {  // every partition hot (one partition): an even split
+      for (int q = 0; q < partitions; ++q) n[q] = records_per_map / partitions + (q < records_per_map % partitions);
       continue;
     }
     const int64_t hot = (int64_t)((double)records_per_map * skew);
     const int64_t rest = records_per_map - hot;
-    n[0] = hot;
-    for (int q = 1; q < partitions; ++q) n[q] = rest / (partitions - 1) + (q - 1 < rest % (partitions - 1) ? 1 : 0);
+    for (int q = 0, h = 0, c = 0; q < partitions; ++q) {
+      if (q % hot_every == 0) {
+        n[q] = hot / nhot + (h < hot % nhot ? 1 : 0);
+        ++h;
+      } else {
+        n[q] = rest / ncold + (c < rest % ncold ? 1 : 0);
+        ++c;
+      }
+    }
   }
   // per-run byte sizes on the device (records + EOF)
   const int R = maps * partitions;
