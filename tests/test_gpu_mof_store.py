@@ -118,9 +118,9 @@ def test_empty_partitions_on_the_generic_device_path(require_gpu):
     p = UdaProvider()
     try:
         ids = []
-        for i in range(5):
+        for i, parts in enumerate(datagen.streams([[[], []] for _ in range(5)])):  # EOF markers only
             mid = f"attempt_job_9_0202_m_{i:06d}_0"
-            data, index = encode_partitions([[], []], None)
+            data, index = encode_partitions(parts, None)
             p.add_mof_device("job_9_0202", mid, data, index, device=0)
             ids.append(mid)
         conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.round.bytes": 1 << 20})
