@@ -263,6 +263,9 @@ void ApiTeraSortBench::setup() {
       throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
   }
   if (!cfg_.codec.empty()) compress_store();
+  // the generated store served only as the map side's output: the compressed copy (codec) or the
+  // MOF files (mof_dir) are what the provider serves, so its HBM goes back to the reduce tasks
+  if (!cfg_.codec.empty() || !cfg_.mof_dir.empty() || cfg_.host_mofs) gen_->release_store();
 }
 
 // Compressed map outputs (what a job with mapred.compress.map.output writes): each partition of each

@@ -314,6 +314,12 @@ class ShuffleJob {
   double map_sort_ms() const { return map_sort_ms_; }  // cfg.map_sort: device time of the map-side sorts
   // Device address / size of MOF m in the partition store (host address for the host tier).
   const uint8_t* mof_device_ptr(int m) const { return store_dev_base_ + mof_off_.at(m); }
+  // Drop the HBM store once its bytes live elsewhere (the API bench's compressed copy or MOF files);
+  // the plan's metadata (index records, expected counts) stays valid, steps do not.
+  void release_store() {
+    store_.reset();
+    store_base_ = store_dev_base_ = nullptr;
+  }
   int64_t mof_bytes(int m) const { return mof_off_.at(m + 1) - mof_off_.at(m); }
   int64_t max_round_records() const { return max_round_records_; }
   int comm_ranks() const { return exchange_ ? exchange_->comm_ranks() : 1; }
