@@ -269,32 +269,46 @@ void ApiTeraSortBench::setup() {
 }
 
 // Compressed map outputs (what a job with mapred.compress.map.output writes): each partition of each
-// MOF is block-compressed on the host (one thread per MOF), the compressed MOFs are packed into one
-// HBM store and registered as device MOFs with index {offset, raw length, compressed length}.
+// MOF is block-compressed on the host and the compressed MOFs are packed into one HBM store,
+// registered as device MOFs with index {offset, raw length, compressed length}. Sized for the
+// flagship scale (130 GB per GPU): the raw MOFs go to host memory once and leave HBM, each MOF is
+// compressed partition by partition into its own host region (compressed data never outgrows the
+// raw bytes it replaces; checked), and only then is the compressed store allocated -- raw and
+// compressed copies never share HBM, and the host holds one copy plus a partition per thread.
 void ApiTeraSortBench::compress_store() {
   const Codec c = cfg_.codec == "snappy" ? Codec::kSnappy : cfg_.codec == "lzo" ? Codec::kLzo : Codec::kNone;
   if (c == Codec::kNone) throw std::runtime_error("api bench: unknown codec " + cfg_.codec);
   const int P = cfg_.world * cfg_.reducers, M = cfg_.maps;
-  std::vector<std::vector<uint8_t>> comp((size_t)M);
+  std::vector<int64_t> raw_off((size_t)M + 1, 0);
+  for (int m = 0; m < M; ++m) raw_off[(size_t)m + 1] = raw_off[(size_t)m] + gen_->mof_bytes(m);
+  std::unique_ptr<uint8_t[]> host_mem(new uint8_t[(size_t)std::max<int64_t>(raw_off[(size_t)M], 1)]);  // no zero fill
+  uint8_t* host = host_mem.get();
+  for (int m = 0; m < M; ++m)
+    HIP_CHECK(hipMemcpy(host + raw_off[(size_t)m], gen_->mof_device_ptr(m), (size_t)gen_->mof_bytes(m),
+                        hipMemcpyDeviceToHost));
+  gen_->release_store();
+  std::vector<int64_t> comp_len((size_t)M, 0);
   std::vector<std::vector<int64_t>> idx((size_t)M);
   std::vector<std::thread> ts;
   std::mutex emu;
   std::string err;
-  const int nt = std::max(1, std::min<int>(M, (int)std::thread::hardware_concurrency() / 2));
+  const int nt = std::max(1, std::min<int>({M, 16, (int)std::thread::hardware_concurrency()}));
   for (int t = 0; t < nt; ++t)
     ts.emplace_back([&, t] {
       try {
-        HIP_CHECK(hipSetDevice(cfg_.device));
-        std::vector<uint8_t> raw;
         for (int m = t; m < M; m += nt) {
-          raw.resize((size_t)gen_->mof_bytes(m));
-          HIP_CHECK(hipMemcpy(raw.data(), gen_->mof_device_ptr(m), raw.size(), hipMemcpyDeviceToHost));
+          uint8_t* mof = host + raw_off[(size_t)m];
+          int64_t at = 0;  // compressed bytes written back into the MOF's own region
           for (int r = 0; r < P; ++r) {
             const auto ir = gen_->index_record(m, r);  // {offset, raw, part}
-            const std::vector<uint8_t> b = block_compress(c, raw.data() + ir[0], (size_t)ir[2], 256 << 10);
-            idx[(size_t)m].insert(idx[(size_t)m].end(), {(int64_t)comp[(size_t)m].size(), ir[2], (int64_t)b.size()});
-            comp[(size_t)m].insert(comp[(size_t)m].end(), b.begin(), b.end());
+            const std::vector<uint8_t> b = block_compress(c, mof + ir[0], (size_t)ir[2], 256 << 10);
+            if (at + (int64_t)b.size() > ir[0] + ir[2])
+              throw std::runtime_error("compressed partition outgrew its raw bytes (incompressible input)");
+            std::memmove(mof + at, b.data(), b.size());
+            idx[(size_t)m].insert(idx[(size_t)m].end(), {at, ir[2], (int64_t)b.size()});
+            at += (int64_t)b.size();
           }
+          comp_len[(size_t)m] = at;
         }
       } catch (const std::exception& e) {
         std::lock_guard<std::mutex> g(emu);
@@ -304,17 +318,17 @@ void ApiTeraSortBench::compress_store() {
   for (auto& t : ts) t.join();
   if (!err.empty()) throw std::runtime_error("api bench: compressing the MOFs: " + err);
   std::vector<int64_t> off((size_t)M + 1, 0);
-  for (int m = 0; m < M; ++m) off[(size_t)m + 1] = off[(size_t)m] + ((int64_t)comp[(size_t)m].size() + 255) / 256 * 256;
+  for (int m = 0; m < M; ++m) off[(size_t)m + 1] = off[(size_t)m] + (comp_len[(size_t)m] + 255) / 256 * 256;
   comp_store_.reset(new DeviceBuffer((size_t)std::max<int64_t>(off[(size_t)M], 16), /*resident=*/true));
   uda_handle* h = static_cast<uda_handle*>(provider_);
   for (int m = 0; m < M; ++m) {
     uint8_t* dst = comp_store_->as<uint8_t>() + off[(size_t)m];
-    HIP_CHECK(hipMemcpy(dst, comp[(size_t)m].data(), comp[(size_t)m].size(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dst, host + raw_off[(size_t)m], (size_t)comp_len[(size_t)m], hipMemcpyHostToDevice));
     const std::string id = map_id(cfg_.rank * M + m);
-    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), dst, (int64_t)comp[(size_t)m].size(),
+    if (uda_provider_register_mof_device(h, cfg_.job.c_str(), id.c_str(), dst, comp_len[(size_t)m],
                                          idx[(size_t)m].data(), P, cfg_.device) != 0)
       throw std::runtime_error(std::string("api bench: register_mof_device failed: ") + uda_last_error(h));
-    comp_bytes_ += (int64_t)comp[(size_t)m].size();
+    comp_bytes_ += comp_len[(size_t)m];
   }
 }
 
