@@ -472,10 +472,16 @@ void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s
   if (kd.kmax < 1 || kd.kmax > kKwMaxRuns) throw std::runtime_error("kway: bad runs per group " + std::to_string(kd.kmax));
   const size_t lds = (elems + tables(kd.kmax) + 15) & ~(size_t)15;
   static std::once_flag once;
+  static hipError_t attr = hipSuccess;
   std::call_once(once, [elems, tables] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(elems + tables(kKwMaxRuns) + 16));
+    attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(elems + tables(kKwMaxRuns) + 16));
+    // some runtimes refuse the attribute for template kernels: harmless while a launch stays within the
+    // default, and the error must not linger for the next hipGetLastError
+    if (attr != hipSuccess) (void)hipGetLastError();
   });
+  if (attr != hipSuccess && lds > (64u << 10))
+    throw std::runtime_error(std::string("kway: cannot raise the LDS limit: ") + hipGetErrorString(attr));
   hipLaunchKernelGGL((kway_tile_kernel<ITEMS>), dim3((unsigned)ncells), dim3(256), lds, s, kd, out);
 }
 }  // namespace
