@@ -1769,6 +1769,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   const int maps = init_.num_maps;
   const int device = device_;
   HIP_CHECK(hipSetDevice(device));
+  HIP_PENDING("the device fetch");
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
@@ -1921,6 +1922,10 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       } else if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
         // not mappable here (another node, no IPC handle, import failure): fetch its bytes
         UDA_LOG(kInfo, "descriptor of %s not usable (%s): fetching bytes", batch[i].map_id.c_str(), why.c_str());
+        if (unmapped == 0) {
+          std::lock_guard<std::mutex> g(st_mu_);
+          st_.unmapped_reason = why;
+        }
         fetch_bytes(batch[i], a.part_len, part.get());
         ++unmapped;
       } else if (a.status == kNotDeviceResident) {
@@ -1944,6 +1949,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     }
   }
   const double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  HIP_PENDING("the end of the descriptor fetch");
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.device_descriptors = descriptors;
@@ -1963,6 +1969,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
+  HIP_PENDING("the merge workspace");
   // HBM admission (gpu/hbm_ledger.h): the task's device working set -- decoded partitions, the
   // key-range round's output slots and merge tables -- is reserved before it is allocated, under the
   // device's byte budget shared with the provider's store and every other task on the node. A round

@@ -28,6 +28,15 @@ constexpr int kProgressReportLimit = 20;  // PROGRESS_REPORT_LIMIT (MergeManager
 constexpr int kExtraBuffers = 10;         // EXTRA_RDMA_BUFFERS (reducer.cc:50)
 constexpr int kMinParallelLpqs = 3;       // MIN_PARALLEL_LPQS (MergeManager.h:125)
 
+std::string json_escape(const std::string& in) {
+  std::string o;
+  for (char c : in) {
+    if (c == '"' || c == '\\') o += '\\';
+    o += (unsigned char)c < 0x20 ? ' ' : c;
+  }
+  return o;
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -858,7 +867,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
-    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
+    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"unmapped_reason\":\"" << json_escape(s.unmapped_reason) << "\"" << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms
     << ",\"hbm_reserved\":" << s.hbm_reserved << ",\"round_bytes\":" << s.round_bytes << ",\"gpu_device\":" << s.gpu_device << ",\"merge_path\":\"" << s.merge_path << "\""
     << ",\"finished\":" << (finished_ ? "true" : "false") << "}";

@@ -65,6 +65,7 @@ struct ReduceStats {
   int64_t restored_lpqs = 0, restored_maps = 0;  // hybrid resume from an LPQ checkpoint
   int64_t device_descriptors = 0;     // GPU device fetch: partitions merged in the provider's HBM
   int64_t unmapped_descriptors = 0;   // descriptors not mappable here (other node, no handle): bytes fetched
+  std::string unmapped_reason;        // why the first of them could not be mapped
   int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
   std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)
   std::string backend;

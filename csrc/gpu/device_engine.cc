@@ -563,7 +563,9 @@ int64_t DeviceMerger::run_kway(const KwayPlan& kp, uint8_t* out, hipStream_t s) 
     HIP_CHECK(hipMemsetAsync(kw_prof_.as(), 0, (size_t)kp.ncells * 5 * 8, s));
     kd.prof = kw_prof_.as<unsigned long long>();
   }
+  HIP_CHECK(hipGetLastError());  // nothing pending from the plan's launches
   launch_kway_tiles(kd, kp.ncells, out, s);
+  HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(pb.used, s));
   pb.used_valid = true;
   if (prof) report_kway_phases(kd.prof, kp.ncells, s);

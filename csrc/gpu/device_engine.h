@@ -48,6 +48,9 @@ namespace gpu {
 
 void hip_check(hipError_t e, const char* what, const char* file, int line);
 #define HIP_CHECK(x) ::uda::gpu::hip_check((x), #x, __FILE__, __LINE__)
+// Throw if an earlier call on this thread left an error behind (kernel launches report theirs only
+// through hipGetLastError): names the stretch of code it came from.
+#define HIP_PENDING(where) ::uda::gpu::hip_check(hipGetLastError(), "a call before " where, __FILE__, __LINE__)
 
 // Owning device allocation. Every allocation and free is accounted in the device's HBM ledger
 // (hbm_ledger.h); `resident` marks data that stays (a map-output store), not a task's working set.

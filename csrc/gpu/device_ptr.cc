@@ -203,6 +203,7 @@ const uint8_t* try_resolve_device_descriptor(const std::string& desc, int my_dev
     if (leased) it->second.leased_refs++;
     return it->second.base + std::strtoll(f[6].c_str(), nullptr, 10);
   } catch (const std::exception& e) {
+    (void)hipGetLastError();  // the caller falls back to bytes: the failed import must not linger
     if (why) *why = e.what();
     return nullptr;
   }

@@ -201,6 +201,7 @@ bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
   HIP_CHECK(hipMemsetAsync(flag.as(), 0, sizeof(int), s));
   for (size_t b = 0; b < runs.size(); b += 65535)
     launch_check_fixed(d_runs.as<RunDesc>() + b, (int)std::min<size_t>(65535, runs.size() - b), max_n, flag.as<int>(), s);
+  HIP_CHECK(hipGetLastError());  // the launch itself
   int bad = 0;
   HIP_CHECK(hipMemcpyAsync(&bad, flag.as(), sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -212,6 +213,8 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
                                       const std::function<int(const uint8_t*, int64_t)>& sink) {
   trace::Range tr("uda.device_reduce");
   HIP_CHECK(hipSetDevice(cfg.device));
+  if (const hipError_t pending = hipGetLastError(); pending != hipSuccess)  // a failure before this call
+    throw std::runtime_error(std::string("device reduce: HIP error pending on entry: ") + hipGetErrorString(pending));
   DeviceReduceStats st;
   const double t0 = now_ms();
   WsLease lease(cfg.device);
@@ -291,6 +294,7 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
       if (ns > 0) {
         launch_sample_fixed(d_bases.as<uint8_t*>(), d_nrec.as<int64_t>(), K, every, d_soff.as<int64_t>(), ns,
                             d_samp.as<Elem>(), s);
+        HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(samp.data(), d_samp.as(), (size_t)ns * sizeof(Elem), hipMemcpyDeviceToHost, s));
       }
       HIP_CHECK(hipStreamSynchronize(s));
@@ -301,6 +305,7 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
       HIP_CHECK(hipMemcpyAsync(d_bounds.as(), bounds.data(), (size_t)(Q - 1) * sizeof(Elem), hipMemcpyHostToDevice, s));
       launch_split_fixed(d_bases.as<uint8_t*>(), d_nrec.as<int64_t>(), d_bounds.as<Elem>(), d_bset.as<int>(), K, Q - 1,
                          d_out.as<int64_t>(), s);
+      HIP_CHECK(hipGetLastError());
       HIP_CHECK(hipMemcpyAsync(pos.data(), d_out.as(), pos.size() * 8, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
     }
