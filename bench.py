@@ -176,8 +176,7 @@ def main(argv=None) -> int:
     if ctx.world != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
         return 2
-    if args.api and args.node:
-        torch.cuda.set_device(0)
+    if args.api and args.node:  # every GPU call in native processes (this one only orchestrates)
         return run_node(args, ctx)
     if args.api:
         torch.cuda.set_device(0 if args.one_gpu else ctx.local_rank)
@@ -313,45 +312,64 @@ def _free_port() -> int:
 
 
 def run_node(args, ctx) -> int:
-    """The node shape of a Hadoop job on one GPU: this process is the node's MOFSupplier (the NodeManager
-    aux service, MOFSupplierMain.cc:87-143) with the maps' outputs in its HBM, served over TCP; a step is
-    a wave of reduce tasks, each started as a fresh process (UdaBridge.cc:187-263, NetMergerMain.cc:44-77:
-    one NetMerger per ReduceTask JVM) that INITs, FETCHes its partition of every map as device
-    descriptors (the provider's HBM mapped over hipIpc), merges on the GPU and walks every delivered
-    buffer. value = record bytes delivered / wall time of the wave, process starts included."""
+    """The node shape of a Hadoop job on one GPU: the node's MOFSupplier is a process of its own
+    (uda_amd/bin/uda_mof_supplier, the NodeManager aux service, MOFSupplierMain.cc:87-143) holding the
+    maps' outputs in its HBM and serving them over TCP; a step is a wave of reduce tasks, each started
+    as a fresh process (uda_amd/bin/uda_reduce_task; UdaBridge.cc:187-263, NetMergerMain.cc:44-77: one
+    NetMerger per ReduceTask JVM) that INITs, FETCHes its partition of every map as device descriptors
+    (the supplier's HBM mapped over hipIpc), merges on the GPU and walks every delivered buffer. This
+    process only orchestrates (no GPU call), so every process on the GPU uses the system HIP runtime,
+    as on a Hadoop node. value = record bytes delivered / wall time of the wave, process starts included."""
     import statistics
     import subprocess as sp
 
-    from uda_amd import native
     if ctx.world != 1:
-        print("bench: --node runs one provider process per node (--gpus 1)", file=sys.stderr)
+        print("bench: --node runs one supplier process per node (--gpus 1)", file=sys.stderr)
         return 2
-    exe = os.path.join(ROOT, "uda_amd", "bin", "uda_reduce_task")
-    if not os.access(exe, os.X_OK):
-        print(f"bench: {exe} is missing; build with python tools/build.py", file=sys.stderr)
-        return 2
+    bindir = os.path.join(ROOT, "uda_amd", "bin")
+    exe, sup = os.path.join(bindir, "uda_reduce_task"), os.path.join(bindir, "uda_mof_supplier")
+    for x in (exe, sup):
+        if not os.access(x, os.X_OK):
+            print(f"bench: {x} is missing; build with python tools/build.py", file=sys.stderr)
+            return 2
     R = args.reducers
-    port = _free_port()
-    b = native().ApiTeraSortBench(dict(device=0, maps=args.maps_per_gpu, reducers=R, workload=args.workload,
-                                       skew=args.skew, codec=args.api_codec or "",
-                                       records_per_map=max(1, args.rows_per_gpu // args.maps_per_gpu),
-                                       round_bytes=args.round_mb << 20, rank=0, world=1, port=port,
-                                       transport="tcp", bind_addr="127.0.0.1", fetch="device",
-                                       provider_workers=args.api_provider_workers))
+    logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+    errlog = open(os.path.join(logdir, "node_tasks.err"), "a")
+    supplier = sp.Popen([sup, "device=0", f"maps={args.maps_per_gpu}", f"reducers={R}",
+                         f"records_per_map={max(1, args.rows_per_gpu // args.maps_per_gpu)}",
+                         f"round_bytes={args.round_mb << 20}", f"workload={args.workload}", f"skew={args.skew}",
+                         f"codec={args.api_codec or ''}", f"port={_free_port()}", "bind=127.0.0.1",
+                         f"workers={args.api_provider_workers}"],
+                        stdin=sp.PIPE, stdout=sp.PIPE, stderr=errlog, text=True, cwd=ROOT)
+    try:
+        return _node_waves(args, supplier, exe, errlog, statistics, sp)
+    finally:
+        if supplier.poll() is None:
+            try:
+                supplier.stdin.write("exit\n")
+                supplier.stdin.flush()
+                supplier.wait(60)
+            except (OSError, sp.TimeoutExpired):
+                supplier.kill()
+                supplier.wait()
+
+
+def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
     t = time.perf_counter()
-    b.setup()
-    cmds = [b.task_commands(r) for r in range(R)]
-    expected = b.expected_records()
-    print(f"# node setup {time.perf_counter() - t:.1f}s store={b.store_bytes / 1e9:.1f}GB provider port {port}, "
-          f"{R} reduce task processes per wave, {args.node_slots} at once", file=sys.stderr, flush=True)
+    first = supplier.stdout.readline()
+    info = json.loads(first) if first.strip() else {"error": f"supplier exited rc={supplier.poll()}"}
+    if "error" in info:
+        raise RuntimeError(f"MOF supplier failed: {info['error']}")
+    R, port, cmds, expected = args.reducers, info["port"], info["commands"], info["expected"]
+    print(f"# node setup {time.perf_counter() - t:.1f}s store={info['store_bytes'] / 1e9:.1f}GB supplier pid "
+          f"{supplier.pid} port {port}, {R} reduce task processes per wave, {args.node_slots} at once",
+          file=sys.stderr, flush=True)
     conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch": "device", "mapred.uda.transport": "tcp",
             "mapred.uda.gpu.device": "auto", "mapred.uda.gpu.round.bytes": str(args.round_mb << 20)}
     for kv in filter(None, os.environ.get("UDA_API_CONF", "").split(",")):
         k, _, v = kv.partition("=")
         conf[k] = v
     start = ["-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
-    errlog = open(os.path.join(ROOT, "gpurun_out" if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp",
-                               "node_tasks.err"), "a")
 
     def wave(validate: bool) -> dict:
         t0 = time.perf_counter()
@@ -393,10 +411,9 @@ def run_node(args, ctx) -> int:
                     del running[r]
             time.sleep(0.002)
         t1 = time.perf_counter()
-        nbytes = sum(o["bytes"] for o in out.values())
         med = lambda k: round(statistics.median(o[k] for o in out.values()), 1)  # noqa: E731
-        return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "bytes": nbytes,
-                "records": sum(o["records"] for o in out.values()),
+        return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3,
+                "bytes": sum(o["bytes"] for o in out.values()), "records": sum(o["records"] for o in out.values()),
                 "order_errors": sum(o["order_errors"] for o in out.values()),
                 "task_ms_median": {k: med(k) for k in ("exec_to_main_ms", "start_ms", "init_ms",
                                                        "fetch_to_first_data_ms", "fetch_to_eof_ms", "exit_ms")},
@@ -409,8 +426,10 @@ def run_node(args, ctx) -> int:
     stats = [wave(False) for _ in range(args.steps)]
     validated = None
     if not args.no_validate:
-        vst = wave(True)
-        validated = vst["order_errors"] == 0
+        validated = wave(True)["order_errors"] == 0
+    supplier.stdin.write("stats\n")
+    supplier.stdin.flush()
+    provider = json.loads(supplier.stdout.readline())
     ms = sum(s["wall_ms"] for s in stats) / len(stats)
     fetch_ms = sum(s["from_fetch_ms"] for s in stats) / len(stats)
     nbytes = stats[0]["bytes"]
@@ -432,20 +451,19 @@ def run_node(args, ctx) -> int:
         "config": {"model": "terasort" if args.workload == "terasort" else "secondary-sort",
                    "global_batch": int(stats[0]["records"]), "seq_len": 104, "parallelism": "dp1",
                    "rows_per_gpu": args.rows_per_gpu, "maps_per_gpu": args.maps_per_gpu, "reducers_per_gpu": R,
-                   "shuffle": "node shape: one MOFSupplier process (map outputs in its HBM, TCP control) + one fresh "
-                              "process per reduce task (uda_reduce_task: INIT/FETCH/dataFromUda), descriptors "
-                              "mapped over hipIpc",
+                   "shuffle": "node shape: one MOFSupplier process (uda_mof_supplier: map outputs in its HBM, TCP "
+                              "control) + one fresh process per reduce task (uda_reduce_task: INIT/FETCH/"
+                              "dataFromUda), descriptors mapped over hipIpc",
                    "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
         "node": {"slots": args.node_slots, "gap_s": args.node_gap,
                  "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
                  "task_ms_median": stats[-1]["task_ms_median"]},
-        "task0_stats": json.loads(stats[-1]["task0"]) if stats[-1]["task0"] else None,
-        "provider": json.loads(b.provider_stats()),
+        "task0_stats": stats[-1]["task0"],
+        "provider": provider,
         "validated": validated,
         "reference_envelope_gbps_per_node": 5.0,
     }
     print(json.dumps(out), flush=True)
-    ctx.close()
     return 0
 
 
