@@ -779,15 +779,27 @@ void ReduceTask::release_descriptors(const std::set<std::string>& hosts, const s
 // leaves the merge to build what it needs as before.
 void ReduceTask::prewarm_gpu(PrewarmConf pc) {
   const auto t0 = std::chrono::steady_clock::now();
+  auto tp = t0;
+  std::string phases;
+  auto lap = [&](const char* name) {
+    const auto t = std::chrono::steady_clock::now();
+    char b[48];
+    std::snprintf(b, sizeof(b), "%s%s=%.1f", phases.empty() ? "" : " ", name,
+                  std::chrono::duration<double, std::milli>(t - tp).count());
+    phases += b;
+    tp = t;
+  };
   try {
     std::call_once(placed_, [this] { place_on_gpu(); });
     if (gpu::device_count() <= 0) return;
     const int device = device_;
     if (hipSetDevice(device) != hipSuccess) return;
+    lap("hip");
     try {
       (void)gpu::SdmaEngine::for_device(device);
     } catch (const std::exception&) {
     }
+    lap("sdma");
     // once per process: the context and the library's code objects (loaded at the first kernel
     // launch); later prewarms must not hipFree (it synchronizes the device under running tasks)
     static std::once_flag code_once;
@@ -804,6 +816,7 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
       }
       HIP_CHECK(hipFree(tmp));
     });
+    lap("code");
     // a workspace with its pinned D2H ring (NUMA-local), and an early stager, into the device pools
     {
       PoolLease<DeviceWorkspace> wl{device, DevicePool<DeviceWorkspace>::get().acquire(
@@ -817,6 +830,17 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
                                             device, [device] { return std::make_unique<EarlyStager>(device); })};
       sl.clean = true;
     }
+    lap("ws");
+    // TeraSort-shaped tasks merge through device_reduce_fixed: its pooled workspace, merger and SDMA
+    // delivery ring
+    {
+      gpu::DeviceReduceConfig cfg;
+      cfg.device = device;
+      cfg.kv_buf_bytes = kv_buf_size_;
+      cfg.round_bytes = pc.round_bytes;
+      gpu::prewarm_device_reduce(cfg, std::max(1, pc.maps));
+    }
+    lap("fixed10");
     // pinned blocks for the fetch arena, kept in the pool's cache for this task's partitions (not for
     // tasks that only fetch device descriptors)
     const int64_t pin = pc.pinned_bytes;
@@ -824,11 +848,13 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
     for (int64_t b = 0; b < pin && !stop_; b += (int64_t)gpu::PinnedArena::kBlock)
       blocks.push_back(gpu::PinnedPool::instance().acquire(gpu::PinnedArena::kBlock));
     for (auto& b : blocks) gpu::PinnedPool::instance().release(b);
+    lap("pinned");
   } catch (const std::exception& e) {
     UDA_LOG(kWarn, "GPU prewarm: %s", e.what());
   }
   std::lock_guard<std::mutex> g(st_mu_);
   st_.gpu_prewarm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  st_.gpu_prewarm_phases = phases;
 }
 
 void ReduceTask::join_prewarm() {
@@ -1913,8 +1939,13 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       auto part = std::make_unique<Part>();
       std::string why;
       const uint8_t* dp = nullptr;
-      if (a.status == 0 && gpu::is_device_descriptor(a.path) &&
-          (dp = gpu::try_resolve_device_descriptor(a.path, device, &why)) != nullptr) {
+      const auto tm = std::chrono::steady_clock::now();
+      if (a.status == 0 && gpu::is_device_descriptor(a.path)) {
+        dp = gpu::try_resolve_device_descriptor(a.path, device, &why);
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.descriptor_map_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tm).count();
+      }
+      if (dp != nullptr) {
         part->dptr = dp;
         part->part_len = a.part_len;
         desc_release.descs.push_back(a.path);
@@ -1961,6 +1992,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     if (stop_) throw UdaError("reduce task stopped during merge");
     const int r = host_->data_from_uda(p, (int32_t)len);
     std::lock_guard<std::mutex> g(st_mu_);
+    if (st_.buffers == 0)
+      st_.first_data_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     st_.buffers++;
     st_.bytes_delivered += len;
     return r;

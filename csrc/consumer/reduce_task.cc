@@ -419,6 +419,8 @@ void ReduceTask::on_init(const InitParams& p) {
     // pinned fetch-arena blocks, not for tasks that only fetch device descriptors
     if (host_->get_conf("mapred.uda.gpu.fetch", "auto") != "device")
       pc.pinned_bytes = host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 1024) << 20;
+    pc.round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
+    pc.maps = p.num_maps;
     prewarm_thr_ = std::thread([this, pc] { prewarm_gpu(pc); });
   }
   merge_thr_ = std::thread([this] { merge_main(); });
@@ -865,9 +867,9 @@ std::string ReduceTask::stats_json() const {
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"hybrid_direct\":" << s.hybrid_direct << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
-    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"gpu_prewarm_phases\":\"" << s.gpu_prewarm_phases << "\"" << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
-    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"unmapped_reason\":\"" << json_escape(s.unmapped_reason) << "\"" << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
+    << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"unmapped_reason\":\"" << json_escape(s.unmapped_reason) << "\"" << ",\"descriptor_map_ms\":" << s.descriptor_map_ms << ",\"first_data_ms\":" << s.first_data_ms << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms
     << ",\"hbm_reserved\":" << s.hbm_reserved << ",\"round_bytes\":" << s.round_bytes << ",\"gpu_device\":" << s.gpu_device << ",\"merge_path\":\"" << s.merge_path << "\""
     << ",\"finished\":" << (finished_ ? "true" : "false") << "}";

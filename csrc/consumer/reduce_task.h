@@ -60,12 +60,15 @@ struct ReduceStats {
   int gpu_device = -1;          // HIP device the task ran on (mapred.uda.gpu.device, auto = placed)
   double gpu_prewarm_ms = -1;   // INIT-time GPU prewarm (mapred.uda.gpu.prewarm); -1: not run
   double gpu_prewarm_wait_ms = 0;  // the merge waiting for the prewarm to finish
+  std::string gpu_prewarm_phases;  // ms per prewarm phase: hip init, sdma, code, workspaces, fixed10, pinned
   // per-MOF buffer pair split when compressed (reducer.cc:463-491): fetch side / uncompressed side
   int64_t fetch_buf_bytes = 0, uncomp_buf_bytes = 0;
   int64_t restored_lpqs = 0, restored_maps = 0;  // hybrid resume from an LPQ checkpoint
   int64_t device_descriptors = 0;     // GPU device fetch: partitions merged in the provider's HBM
   int64_t unmapped_descriptors = 0;   // descriptors not mappable here (other node, no handle): bytes fetched
   std::string unmapped_reason;        // why the first of them could not be mapped
+  double descriptor_map_ms = 0;       // resolving descriptors (hipIpcOpenMemHandle of another process's HBM)
+  double first_data_ms = -1;          // device fetch: from the merge's start to the first dataFromUda
   int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
   std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)
   std::string backend;
@@ -113,6 +116,8 @@ class ReduceTask {
   struct PrewarmConf {  // read on the INIT thread (the host's get_conf may be bound to it)
     bool early_h2d = true;
     int64_t pinned_bytes = 0;
+    int64_t round_bytes = 2ll << 30;
+    int maps = 0;
   };
   void prewarm_gpu(PrewarmConf pc);
   void join_prewarm();

@@ -183,6 +183,22 @@ int64_t fixed_round_ws_bytes(int64_t round_bytes, int runs) {
   return (int64_t)(2 * slot + 0.02 * (double)round_bytes) + (int64_t)runs * 4096 + (16ll << 20);
 }
 
+void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs) {
+  HIP_CHECK(hipSetDevice(cfg.device));
+  WsLease lease(cfg.device);
+  FixedWs& ws = *lease.w;
+  const int64_t rec = std::max<int64_t>(1, cfg.round_bytes / kTeraRecordBytes);
+  const int64_t mr = rec + rec / 8;  // rounds run a little over their mean
+  if (!ws.merger || ws.merger->max_records() < mr || ws.merger->max_runs() < runs) ws.merger.reset(new DeviceMerger(mr, runs));
+  const int64_t buf_bytes = std::max<int64_t>(1, cfg.kv_buf_bytes / kTeraRecordBytes) * kTeraRecordBytes;
+  const int64_t piece = std::max<int64_t>(1, cfg.piece_bytes / buf_bytes) * buf_bytes;
+  const int S = std::max(2, cfg.pinned_slots);
+  {
+    Ring ring(SdmaEngine::for_device(cfg.device), (size_t)piece * S, S);  // back to the engine's cache
+  }
+  lease.clean = true;
+}
+
 bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
   if (runs.empty()) return true;
   int64_t max_n = 0;

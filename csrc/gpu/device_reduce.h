@@ -47,6 +47,12 @@ struct DeviceReduceStats {
   int64_t round_bytes = 0;     // round size used (after any shrink to fit the budget)
 };
 
+// Build what a FIXED10 task's first round would otherwise build on its critical path (a fresh reduce
+// task process: Hadoop runs every reduce task in its own JVM): a pooled workspace with its stream,
+// a merger sized for `runs` runs and rounds of `round_bytes` (its upload slots and plan tables; the
+// round's output slots stay for the HBM admission), and the delivery ring in the SDMA engine's cache.
+void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs);
+
 // HBM a FIXED10 round working set of `round_bytes` merged bytes needs (two output slots and the
 // merger's per-round tables), for admission.
 int64_t fixed_round_ws_bytes(int64_t round_bytes, int runs);

@@ -52,9 +52,12 @@ struct MofCache::Loader {
   };
   int device = 0;
   std::thread thr;
+  std::thread opener;          // allocates HBM and opens the file of new entries (never stalls the reads)
   std::condition_variable cv;  // with MofCache::mu_
+  std::condition_variable ocv; // opener: new pending entries (with MofCache::mu_)
   bool stop = false;
-  std::deque<std::shared_ptr<Entry>> pending;  // to allocate + open
+  std::deque<std::shared_ptr<Entry>> pending;  // to allocate + open (opener thread)
+  int opening = 0;                             // taken by the opener, not yet active
   std::deque<std::shared_ptr<Entry>> active;   // unread bytes left, read in turn
   std::vector<Slot> slots;
   std::unique_ptr<AsyncIO> aio;
@@ -82,8 +85,11 @@ MofCache::~MofCache() {
       kv.second->cv.notify_all();
     }
   }
-  for (auto& kv : loaders_)
+  for (auto& kv : loaders_) {
+    kv.second->ocv.notify_all();
+    if (kv.second->opener.joinable()) kv.second->opener.join();
     if (kv.second->thr.joinable()) kv.second->thr.join();
+  }
   std::lock_guard<std::mutex> g(mu_);
   entries_.clear();
   loaders_.clear();
@@ -224,9 +230,10 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
     L->device = device;
     Loader* lp = L.get();
     L->thr = std::thread([this, lp] { loader_main(lp); });
+    L->opener = std::thread([this, lp] { opener_main(lp); });
   }
   L->pending.push_back(e);
-  L->cv.notify_all();
+  L->ocv.notify_all();
   return true;
 }
 
@@ -300,8 +307,72 @@ MofCache::Stats MofCache::stats() {
   return s;
 }
 
-// One loader per GPU: allocation + open of new entries, O_DIRECT chunk reads round-robin over the
-// files being loaded, SDMA H2D of every landed chunk, and the readiness of each file's prefix.
+// A loader's opener thread: HBM allocation (resident in the HBM budget), IPC export and the file of
+// every new entry, so the reads of files already open never wait behind them (a 1.3 GB hipMalloc +
+// export takes milliseconds; 32 of them serialized in the read loop cost the first step a second).
+void MofCache::opener_main(Loader* L) {
+  (void)hipSetDevice(L->device);
+  std::vector<Fire> fire;
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    L->ocv.wait(lk, [&] { return L->stop || !L->pending.empty(); });
+    if (L->pending.empty()) return;  // stopped and drained
+    std::shared_ptr<Entry> e = L->pending.front();
+    L->pending.pop_front();
+    ++L->opening;
+    std::string err = L->stop ? "provider HBM store stopped" : "";
+    std::unique_ptr<DeviceBuffer> mem;
+    int fd = -1;
+    bool direct = opt_.odirect;
+    IpcExport ipc;
+    lk.unlock();
+    const double t0 = now_s();
+    if (err.empty()) {
+      try {
+        mem.reset(new DeviceBuffer((size_t)std::max<int64_t>(e->len, 1), /*resident=*/true));
+        ipc = ipc_export(mem->as<uint8_t>());
+        fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
+        if (fd < 0 && direct) {
+          direct = false;
+          fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC);
+        }
+        if (fd < 0) err = "cannot open " + e->path + ": " + strerror(errno);
+      } catch (const std::exception& ex) {
+        err = ex.what();
+      }
+    }
+    const double dt = now_s() - t0;
+    lk.lock();
+    --L->opening;
+    st_.open_ms += dt * 1000.0;
+    if (!err.empty() || e->failed) {
+      if (fd >= 0) ::close(fd);
+      fail_entry(*e, err.empty() ? e->error : err, &fire);
+    } else {
+      e->mem = std::move(mem);
+      e->dptr = e->mem->as<uint8_t>();
+      e->ipc = ipc;
+      e->fd = fd;
+      e->direct = direct;
+      if (e->len == 0) {
+        e->loading = false;
+        collect_ready(*e, &fire);
+      } else {
+        L->active.push_back(e);
+      }
+      L->cv.notify_all();
+    }
+    if (!fire.empty()) {
+      lk.unlock();
+      for (Fire& f : fire) f.ready(f.ok, f.ref, f.why);
+      fire.clear();
+      lk.lock();
+    }
+  }
+}
+
+// One loader per GPU: O_DIRECT chunk reads round-robin over the files being loaded, SDMA H2D of every
+// landed chunk, and the readiness of each file's prefix.
 void MofCache::loader_main(Loader* L) {
   const int C_slots = opt_.chunks;
   const int64_t C = opt_.chunk_bytes;
@@ -340,52 +411,8 @@ void MofCache::loader_main(Loader* L) {
   bool was_busy = false;
   for (;;) {
     if (L->stop) {  // the store is going away: nothing new starts, loads in progress fail
-      for (auto& e : L->pending) fail_entry(*e, "provider HBM store stopped", &fire);
       for (auto& e : L->active) fail_entry(*e, "provider HBM store stopped", &fire);
-      L->pending.clear();
       L->active.clear();
-    }
-    // ---- new entries: HBM allocation (resident in the HBM budget) and the file, outside the lock
-    while (!L->pending.empty()) {
-      std::shared_ptr<Entry> e = L->pending.front();
-      L->pending.pop_front();
-      std::string err = L->setup_error;
-      std::unique_ptr<DeviceBuffer> mem;
-      int fd = -1;
-      bool direct = opt_.odirect;
-      IpcExport ipc;
-      lk.unlock();
-      if (err.empty()) {
-        try {
-          mem.reset(new DeviceBuffer((size_t)std::max<int64_t>(e->len, 1), /*resident=*/true));
-          ipc = ipc_export(mem->as<uint8_t>());
-          fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
-          if (fd < 0 && direct) {
-            direct = false;
-            fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC);
-          }
-          if (fd < 0) err = "cannot open " + e->path + ": " + strerror(errno);
-        } catch (const std::exception& ex) {
-          err = ex.what();
-        }
-      }
-      lk.lock();
-      if (!err.empty() || e->failed) {
-        if (fd >= 0) ::close(fd);
-        fail_entry(*e, err.empty() ? e->error : err, &fire);
-        continue;
-      }
-      e->mem = std::move(mem);
-      e->dptr = e->mem->as<uint8_t>();
-      e->ipc = ipc;
-      e->fd = fd;
-      e->direct = direct;
-      if (e->len == 0) {
-        e->loading = false;
-        collect_ready(*e, &fire);
-      } else {
-        L->active.push_back(e);
-      }
     }
     // ---- landed reads: issue their H2D copies
     for (int i = 0; i < C_slots; ++i) {
@@ -517,10 +544,10 @@ void MofCache::loader_main(Loader* L) {
       lk.lock();
       continue;
     }
-    if (L->stop && !busy && L->pending.empty()) break;
+    if (L->stop && !busy && L->pending.empty() && L->opening == 0) break;
     if (copying)
       L->cv.wait_for(lk, std::chrono::microseconds(200));  // SDMA completions are polled
-    else if (L->pending.empty())
+    else
       L->cv.wait_for(lk, std::chrono::milliseconds(50));
   }
   lk.unlock();

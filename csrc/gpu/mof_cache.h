@@ -69,6 +69,7 @@ class MofCache {
     int64_t holders = 0, holders_reaped = 0, releases = 0;
     double load_ms = 0;       // summed per-file load time
     double load_wall_ms = 0;  // time any load was in progress (loads overlap)
+    double open_ms = 0;       // summed HBM allocation + IPC export + open of new entries
   };
   // ok: the bytes [0, need_end) are in HBM (ref valid); else why says what failed.
   using Ready = std::function<void(bool ok, const Ref& ref, const std::string& why)>;
@@ -130,6 +131,7 @@ class MofCache {
   void erase_entry(const std::string& path);              // mu_ held
   Ref ref_of(const Entry& e) const;
   void loader_main(Loader* L);
+  void opener_main(Loader* L);
   void fail_entry(Entry& e, const std::string& why, std::vector<Fire>* fire);  // mu_ held
   void collect_ready(Entry& e, std::vector<Fire>* fire);                      // mu_ held
 

@@ -89,7 +89,7 @@ std::string Supplier::hbm_stats_json() {
   return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
          ",\"holders\":" + std::to_string(st.holders) + ",\"releases\":" + std::to_string(st.releases) +
          ",\"holders_reaped\":" + std::to_string(st.holders_reaped) + ",\"load_wall_ms\":" +
-         std::to_string(st.load_wall_ms) + ",\"load_gbps\":" +
+         std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) + ",\"load_gbps\":" +
          std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
          ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
          ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
