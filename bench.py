@@ -412,7 +412,17 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
             time.sleep(0.002)
         t1 = time.perf_counter()
         med = lambda k: round(statistics.median(o[k] for o in out.values()), 1)  # noqa: E731
-        return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3,
+        # per task, ms after the wave's first exec (CLOCK_BOOTTIME, the tasks' own clock): exec, first
+        # FETCH, first dataFromUda, EOF walked, process end
+        t_base = min(o["t_exec_boot_ms"] for o in out.values())
+        timeline = []
+        for r in sorted(out):
+            o = out[r]
+            ff = o["t_exec_boot_ms"] + o["first_fetch_ms"]
+            eof = o["t_end_boot_ms"] - o["exit_ms"]
+            timeline.append([round(x - t_base) for x in (o["t_exec_boot_ms"], ff, ff + o["fetch_to_first_data_ms"],
+                                                         eof, o["t_end_boot_ms"])])
+        return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "timeline": timeline,
                 "bytes": sum(o["bytes"] for o in out.values()), "records": sum(o["records"] for o in out.values()),
                 "order_errors": sum(o["order_errors"] for o in out.values()),
                 "task_ms_median": {k: med(k) for k in ("exec_to_main_ms", "start_ms", "init_ms",
@@ -457,7 +467,9 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
                    "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
         "node": {"slots": args.node_slots, "gap_s": args.node_gap,
                  "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
-                 "task_ms_median": stats[-1]["task_ms_median"]},
+                 "task_ms_median": stats[-1]["task_ms_median"],
+                 "timeline_ms": {"columns": ["exec", "first_fetch", "first_data", "eof", "end"],
+                                 "tasks": stats[-1]["timeline"]}},
         "task0_stats": stats[-1]["task0"],
         "provider": provider,
         "validated": validated,
