@@ -111,6 +111,10 @@ def parse_args(argv=None):
     ap.add_argument("--node-gap", type=float, default=0.0,
                     help="--node: seconds between a wave's INITs and its FETCHes (reduce slow-start: the tasks start "
                          "while the maps still run); 0 = the tasks start when every map output is there")
+    ap.add_argument("--node-service", action="store_true",
+                    help="--node: the supplier process is also the node's merge service (every reduce task process "
+                         "is a thin client whose NetMerger runs in the service: one GPU context, warm pools and "
+                         "the HBM store in one process; mapred.uda.gpu.merge.service)")
     ap.add_argument("--node-slots", type=int, default=15,
                     help="--node: reduce task processes running at once (YARN containers of the node); the one-GPU "
                          "box allows 16 GPU processes, the provider is one of them")
@@ -335,7 +339,8 @@ def run_node(args, ctx) -> int:
     R = args.reducers
     logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
     errlog = open(os.path.join(logdir, "node_tasks.err"), "a")
-    supplier = sp.Popen([sup, "device=0", f"maps={args.maps_per_gpu}", f"reducers={R}",
+    args.service_path = f"/tmp/uda-merge-{os.getpid()}.sock" if args.node_service else ""
+    supplier = sp.Popen([sup, "device=0", f"service={args.service_path}", f"maps={args.maps_per_gpu}", f"reducers={R}",
                          f"records_per_map={max(1, args.rows_per_gpu // args.maps_per_gpu)}",
                          f"round_bytes={args.round_mb << 20}", f"workload={args.workload}", f"skew={args.skew}",
                          f"codec={args.api_codec or ''}", f"port={_free_port()}", "bind=127.0.0.1",
@@ -366,6 +371,8 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
           file=sys.stderr, flush=True)
     conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch": "device", "mapred.uda.transport": "tcp",
             "mapred.uda.gpu.device": "auto", "mapred.uda.gpu.round.bytes": str(args.round_mb << 20)}
+    if args.service_path:
+        conf["mapred.uda.gpu.merge.service"] = args.service_path
     for kv in filter(None, os.environ.get("UDA_API_CONF", "").split(",")):
         k, _, v = kv.partition("=")
         conf[k] = v
@@ -463,9 +470,11 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
                    "rows_per_gpu": args.rows_per_gpu, "maps_per_gpu": args.maps_per_gpu, "reducers_per_gpu": R,
                    "shuffle": "node shape: one MOFSupplier process (uda_mof_supplier: map outputs in its HBM, TCP "
                               "control) + one fresh process per reduce task (uda_reduce_task: INIT/FETCH/"
-                              "dataFromUda), descriptors mapped over hipIpc",
+                              "dataFromUda), " + ("NetMergers hosted by the supplier's merge service, merged "
+                                                  "buffers read in place from its shared pinned rings"
+                                                  if args.service_path else "descriptors mapped over hipIpc"),
                    "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
-        "node": {"slots": args.node_slots, "gap_s": args.node_gap,
+        "node": {"slots": args.node_slots, "gap_s": args.node_gap, "merge_service": bool(args.service_path),
                  "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
                  "task_ms_median": stats[-1]["task_ms_median"],
                  "timeline_ms": {"columns": ["exec", "first_fetch", "first_data", "eof", "end"],

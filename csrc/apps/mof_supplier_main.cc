@@ -4,7 +4,10 @@
 // reduce task processes (uda_reduce_task) merge the partitions where they lie.
 //
 //   uda_mof_supplier key=value...     (device, maps, reducers, records_per_map, round_bytes, workload,
-//                                      skew, codec, port, bind, workers, seed)
+//                                      skew, codec, port, bind, workers, seed, service)
+//
+// service=<socket path>: the process is also the node's merge service (merge_service.h): reduce task
+// processes started with mapred.uda.gpu.merge.service=<path> run their NetMerger in here.
 //
 // After setup it prints one JSON line: the port, the store size, every reduce task's expected record
 // count and its command strings (INIT + FETCHes, as its ReduceTask JVM would send them). Then it
@@ -14,9 +17,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
+#include <memory>
 #include <string>
 
 #include "api_bench.h"
+#include "service/merge_service.h"
 
 namespace {
 std::string js(const std::string& s) {
@@ -34,6 +39,7 @@ int main(int argc, char** argv) {
   c.transport = "tcp";
   c.bind_addr = "127.0.0.1";
   c.fetch = "device";
+  std::string service;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     const size_t eq = a.find('=');
@@ -54,12 +60,15 @@ int main(int argc, char** argv) {
     else if (k == "bind") c.bind_addr = v;
     else if (k == "workers") c.provider_workers = std::atoi(v.c_str());
     else if (k == "seed") c.seed = std::strtoull(v.c_str(), nullptr, 0);
+    else if (k == "service") service = v;
     else {
       std::fprintf(stderr, "uda_mof_supplier: unknown key %s\n", k.c_str());
       return 2;
     }
   }
   try {
+    std::unique_ptr<uda::MergeService> svc;  // first: the pinned rings allocated after it are shareable
+    if (!service.empty()) svc = std::make_unique<uda::MergeService>(service);
     uda::gpu::ApiTeraSortBench b(c);
     b.setup();
     std::string out = "{\"port\":" + std::to_string(b.provider_port()) + ",\"store_bytes\":" +
@@ -79,7 +88,12 @@ int main(int argc, char** argv) {
     for (std::string line; std::getline(std::cin, line);) {
       if (line == "exit") break;
       if (line == "stats") {
-        std::printf("%s\n", b.provider_stats().c_str());
+        std::string st = b.provider_stats();
+        if (svc && !st.empty() && st.back() == '}')
+          st = st.substr(0, st.size() - 1) + ",\"merge_service\":{\"sessions\":" + std::to_string(svc->sessions()) +
+               ",\"zero_copy_buffers\":" + std::to_string(svc->zero_copy_buffers()) +
+               ",\"bounced_buffers\":" + std::to_string(svc->bounced_buffers()) + "}}";
+        std::printf("%s\n", st.c_str());
         std::fflush(stdout);
       }
     }

@@ -11,6 +11,7 @@
 #include "../consumer/reduce_task.h"
 #include "../gpu/hbm_ledger.h"
 #include "../provider/supplier.h"
+#include "../service/merge_service.h"
 #include "uda/cmd.h"
 #include "uda/host.h"
 #include "uda/log.h"
@@ -23,6 +24,8 @@ struct uda_handle {
   std::unique_ptr<uda::Host> host;
   std::unique_ptr<uda::Supplier> supplier;
   std::unique_ptr<uda::ReduceTask> task;
+  std::unique_ptr<uda::RemoteReduceTask> remote;  // NetMerger hosted by the node's merge service
+  std::unique_ptr<uda::MergeService> service;     // provider: hosts the node's NetMergers
   std::string last_error;
   std::mutex mu;
 };
@@ -80,7 +83,18 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
   UDA_LOG(uda::kInfo, "UDA: The version is %s role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
   try {
     if (h->is_merger) {
-      h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());
+      // a node merge service hosts the NetMerger where the GPU context, the pools and the provider's
+      // HBM store already live (merge_service.h); without one, the task merges in this process
+      const std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "");
+      if (!svc.empty()) {
+        try {
+          h->remote = std::make_unique<uda::RemoteReduceTask>(svc, args, h->host.get());
+          UDA_LOG(uda::kInfo, "NetMerger hosted by the merge service at %s", svc.c_str());
+        } catch (const std::exception& e) {
+          UDA_LOG(uda::kWarn, "merge service unavailable (%s): merging in this process", e.what());
+        }
+      }
+      if (!h->remote) h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());
     } else {
       uda::Supplier::Options so;
       so.transport = h->host->get_conf("mapred.uda.transport", "loopback");
@@ -110,6 +124,9 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
           b = e + 1;
         }
       }
+      // before the supplier allocates its pinned rings, so they are shareable with the service's clients
+      const std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "");
+      if (!svc.empty()) h->service = std::make_unique<uda::MergeService>(svc);
       h->supplier = std::make_unique<uda::Supplier>(h->opt, so, h->host.get());
       h->supplier->start();
     }
@@ -127,12 +144,17 @@ int uda_do_command(uda_handle* h, const char* cmd) {
   if (!uda::parse_cmd(cmd ? cmd : "", &c)) return fail_call(h, "C++ could not parse Hadoop command");
   try {
     if (h->is_merger) {
+      if (h->remote) {
+        h->remote->handle(cmd);
+        return 0;
+      }
       if (!h->task) return fail_call(h, "reduce task already closed");
       h->task->handle(c);
     } else {
       // mof_downcall_handler (MOFSupplierMain.cc:37-81): EXIT stops the supplier; JOB_OVER (sent by
       // the provider plugin when an application ends) releases the job's MOFs from the HBM store
       if (c.header == uda::kExitMsg && h->supplier) {
+        h->service.reset();
         h->supplier->stop();
         UDA_LOG(uda::kInfo, "MOFSupplier stopped");
       } else if (c.header == uda::kJobOverMsg && h->supplier && !c.params.empty()) {
@@ -153,6 +175,8 @@ int uda_reduce_exit(uda_handle* h) {
       h->task->exit();
       UDA_LOG(uda::kInfo, "reduce task closed: %s", h->task->stats_json().c_str());
     }
+    if (h->remote) h->remote->exit();
+    h->service.reset();
     if (h->supplier) h->supplier->stop();
   } catch (const std::exception& e) {
     return fail_call(h, e.what());
@@ -165,8 +189,11 @@ void uda_destroy(uda_handle* h) {
   {
     std::lock_guard<std::mutex> g(h->mu);
     if (h->task) h->task->exit();
+    if (h->remote) h->remote->exit();
+    h->service.reset();
     if (h->supplier) h->supplier->stop();
     h->task.reset();
+    h->remote.reset();
     h->supplier.reset();
   }
   delete h;
@@ -202,6 +229,8 @@ int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
   std::string s;
   if (h->task) {
     s = h->task->stats_json();
+  } else if (h->remote) {
+    s = h->remote->stats_json();
   } else if (h->supplier) {
     s = "{\"role\":\"mof_supplier\",\"requests\":" + std::to_string(h->supplier->requests()) +
         ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) +

@@ -16,6 +16,8 @@
 #include <stdexcept>
 #include <mutex>
 #include <thread>
+#include <atomic>
+#include <map>
 #include <unordered_map>
 #include <vector>
 
@@ -165,14 +167,39 @@ void* hip_host_malloc_on_node(size_t bytes, int node) {
   return p;
 }
 
-// mmap + hugepage advice + parallel first touch + hipHostRegister; nullptr if any step fails
+struct SharedRegion {
+  size_t len;
+  int fd;
+  uint64_t id;
+};
+std::atomic<bool> g_shareable{false};
+std::atomic<uint64_t> g_next_share_id{1};
+std::map<uintptr_t, SharedRegion>& shared_regions() {  // aligned start -> region (under g_pin_mu)
+  static auto* m = new std::map<uintptr_t, SharedRegion>();
+  return *m;
+}
+
+// mmap + hugepage advice + parallel first touch + hipHostRegister; nullptr if any step fails. In
+// shareable mode the pages are a memfd mapped shared at the aligned start (the rest of the
+// reservation stays an inaccessible anonymous mapping).
 void* register_fresh_pages(size_t bytes, int node) {
   constexpr size_t kHuge = (size_t)2 << 20;
   const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
   const size_t maplen = len + kHuge;  // room to align the start to a huge page
-  void* m = mmap(nullptr, maplen, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  const bool share = g_shareable.load();
+  void* m = mmap(nullptr, maplen, share ? PROT_NONE : PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (m == MAP_FAILED) return nullptr;
   uint8_t* a = reinterpret_cast<uint8_t*>(((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+  int fd = -1;
+  if (share) {
+    fd = (int)syscall(SYS_memfd_create, "uda-pinned", 1u /* MFD_CLOEXEC */);
+    if (fd < 0 || ftruncate(fd, (off_t)len) != 0 ||
+        mmap(a, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fd, 0) == MAP_FAILED) {
+      if (fd >= 0) close(fd);
+      munmap(m, maplen);
+      return nullptr;
+    }
+  }
   (void)madvise(a, len, MADV_HUGEPAGE);
   (void)madvise(m, maplen, MADV_DONTFORK);  // a forked child must not copy (or share) pinned pages
   if (node >= 0 && node < 64) {
@@ -192,20 +219,24 @@ void* register_fresh_pages(size_t bytes, int node) {
       for (size_t o = 0; o < n; o += 4096) a[b + o] = 0;
     });
   for (auto& t : ts) t.join();
-  if (hipHostRegister(a, len, hipHostRegisterPortable) != hipSuccess) {
-    (void)hipGetLastError();
+  auto undo = [&] {
+    if (fd >= 0) close(fd);
     munmap(m, maplen);
     return nullptr;
+  };
+  if (hipHostRegister(a, len, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return undo();
   }
   void* d = nullptr;  // copies and kernels use the host address: it must be the device address too
   if (hipHostGetDevicePointer(&d, a, 0) != hipSuccess || d != a) {
     (void)hipGetLastError();
     (void)hipHostUnregister(a);
-    munmap(m, maplen);
-    return nullptr;
+    return undo();
   }
   std::lock_guard<std::mutex> g(g_pin_mu);
   pinned_maps()[a] = {m, maplen};
+  if (fd >= 0) shared_regions()[(uintptr_t)a] = SharedRegion{len, fd, g_next_share_id.fetch_add(1)};
   return a;
 }
 }  // namespace
@@ -231,6 +262,11 @@ void pinned_host_free(void* p) {
       m = it->second;
       pinned_maps().erase(it);
     }
+    auto sr = shared_regions().find((uintptr_t)p);
+    if (sr != shared_regions().end()) {
+      close(sr->second.fd);  // clients keep their own mappings of the pages until they unmap
+      shared_regions().erase(sr);
+    }
   }
   if (m.first) {
     (void)hipHostUnregister(p);
@@ -241,6 +277,23 @@ void pinned_host_free(void* p) {
 }
 
 void* hip_host_alloc_on_node(size_t bytes, int node) { return pinned_host_alloc(bytes, node); }
+
+void set_pinned_shareable(bool on) { g_shareable.store(on); }
+
+bool pinned_share_of(const void* p, size_t len, PinnedShare* out) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> g(g_pin_mu);
+  auto& m = shared_regions();
+  auto it = m.upper_bound(a);
+  if (it == m.begin()) return false;
+  --it;
+  if (a + len > it->first + it->second.len) return false;
+  out->fd = it->second.fd;
+  out->id = it->second.id;
+  out->offset = a - it->first;
+  out->region_bytes = it->second.len;
+  return true;
+}
 
 std::string numa_residency(const void* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);

@@ -95,6 +95,18 @@ void* pinned_host_alloc(size_t bytes, int node = -1);
 void pinned_host_free(void* p);
 // The same, kept for its callers (placement on `node`).
 void* hip_host_alloc_on_node(size_t bytes, int node);
+// Node merge service (csrc/service/merge_service.h): pinned host memory allocated after
+// set_pinned_shareable(true) lives in memfd-backed shared mappings, so a client process can map the
+// delivery rings the service's SDMA engine writes and read the merged buffers in place.
+// pinned_share_of finds the shareable region holding [p, p + len): its memfd (owned by the region,
+// valid while the region is allocated), a process-unique id, the region's size and p's offset in it.
+struct PinnedShare {
+  int fd = -1;
+  uint64_t id = 0;
+  size_t offset = 0, region_bytes = 0;
+};
+void set_pinned_shareable(bool on);
+bool pinned_share_of(const void* p, size_t len, PinnedShare* out);
 // Where the pages of the mapping containing `p` live, from /proc/self/numa_maps: "N1=100%" style
 // summary (or "unknown").
 std::string numa_residency(const void* p);

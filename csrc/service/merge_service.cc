@@ -1,0 +1,622 @@
+// Node merge service and its client. See merge_service.h.
+#include "merge_service.h"
+
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <set>
+
+#include "../consumer/reduce_task.h"
+#include "../gpu/sdma.h"
+#include "uda/cmd.h"
+#include "uda/error.h"
+#include "uda/log.h"
+
+namespace uda {
+
+namespace {
+
+// ---- framing: u32 type, u32 payload length, payload; an fd may ride along (SCM_RIGHTS)
+enum Msg : uint32_t {
+  kHello = 1,      // c->s: startNative argv, '\0'-separated
+  kCmd = 2,        // c->s: command string
+  kConfReply = 3,  // c->s: u32 request id, value
+  kAck = 4,        // c->s: i32 dataFromUda status
+  kExit = 5,       // c->s: reduce task close
+  kReady = 10,     // s->c: task started
+  kRefused = 11,     // s->c: HELLO refused (reason)
+  kConfReq = 12,   // s->c: u32 request id, key '\0' default
+  kRegion = 13,    // s->c: u64 id, u64 bytes + the memfd
+  kData = 14,      // s->c: u64 region id, u64 offset, u32 length
+  kFetchOver = 15, // s->c
+  kFail = 16,      // s->c: reason (failureInUda)
+  kCmdResult = 17, // s->c: i32 status, error text
+  kStats = 18,     // s->c: stats JSON (reply to EXIT)
+};
+
+constexpr uint32_t kMaxPayload = 64u << 20;
+
+bool write_all(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n > 0) {
+    const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    c += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+bool send_msg(int sock, uint32_t type, const std::string& payload, int pass_fd = -1) {
+  uint32_t hdr[2] = {type, (uint32_t)payload.size()};
+  if (pass_fd < 0) {
+    std::string buf(reinterpret_cast<const char*>(hdr), sizeof(hdr));
+    buf += payload;
+    return write_all(sock, buf.data(), buf.size());
+  }
+  msghdr mh{};
+  iovec iov{hdr, sizeof(hdr)};
+  mh.msg_iov = &iov;
+  mh.msg_iovlen = 1;
+  alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(int))];
+  std::memset(cbuf, 0, sizeof(cbuf));
+  mh.msg_control = cbuf;
+  mh.msg_controllen = sizeof(cbuf);
+  cmsghdr* cm = CMSG_FIRSTHDR(&mh);
+  cm->cmsg_level = SOL_SOCKET;
+  cm->cmsg_type = SCM_RIGHTS;
+  cm->cmsg_len = CMSG_LEN(sizeof(int));
+  std::memcpy(CMSG_DATA(cm), &pass_fd, sizeof(int));
+  ssize_t w;
+  do {
+    w = ::sendmsg(sock, &mh, MSG_NOSIGNAL);
+  } while (w < 0 && errno == EINTR);
+  if (w <= 0) return false;
+  if ((size_t)w < sizeof(hdr) && !write_all(sock, reinterpret_cast<char*>(hdr) + w, sizeof(hdr) - (size_t)w))
+    return false;
+  return write_all(sock, payload.data(), payload.size());
+}
+
+// false on EOF or error. *fd_out gets a passed descriptor (-1 if none).
+bool recv_msg(int sock, uint32_t* type, std::string* payload, int* fd_out) {
+  uint32_t hdr[2];
+  size_t got = 0;
+  *fd_out = -1;
+  while (got < sizeof(hdr)) {
+    msghdr mh{};
+    iovec iov{reinterpret_cast<char*>(hdr) + got, sizeof(hdr) - got};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(int))];
+    mh.msg_control = cbuf;
+    mh.msg_controllen = sizeof(cbuf);
+    const ssize_t r = ::recvmsg(sock, &mh, MSG_CMSG_CLOEXEC);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
+      if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(fd_out, CMSG_DATA(cm), sizeof(int));
+    got += (size_t)r;
+  }
+  *type = hdr[0];
+  if (hdr[1] > kMaxPayload) return false;
+  payload->resize(hdr[1]);
+  got = 0;
+  while (got < hdr[1]) {
+    const ssize_t r = ::recv(sock, &(*payload)[got], hdr[1] - got, 0);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    got += (size_t)r;
+  }
+  return true;
+}
+
+template <typename T>
+void put(std::string& s, T v) {
+  s.append(reinterpret_cast<const char*>(&v), sizeof(T));
+}
+template <typename T>
+T get(const std::string& s, size_t at) {
+  T v{};
+  if (at + sizeof(T) <= s.size()) std::memcpy(&v, s.data() + at, sizeof(T));
+  return v;
+}
+
+sockaddr_un unix_addr(const std::string& path) {
+  sockaddr_un a{};
+  a.sun_family = AF_UNIX;
+  if (path.size() >= sizeof(a.sun_path)) throw UdaError("merge service socket path too long: " + path);
+  std::memcpy(a.sun_path, path.c_str(), path.size() + 1);
+  return a;
+}
+
+}  // namespace
+
+// ============================================================================ service side
+
+struct MergeService::Session : std::enable_shared_from_this<MergeService::Session> {
+  MergeService* svc;
+  int sock;
+  std::mutex send_mu;
+  // replies from the client, by kind
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint32_t, std::string> conf_replies;
+  uint32_t next_conf = 1;
+  std::deque<int32_t> acks;
+  bool closed = false;  // the client went away
+  // commands run on their own thread: INIT pulls configuration, which the reader thread answers
+  std::deque<std::string> cmds;
+  bool exit_requested = false;
+  std::set<uint64_t> regions_sent;
+  // bounce buffer for merged bytes outside shareable pinned memory (EOF tails, host-path buffers)
+  int bounce_fd = -1;
+  uint8_t* bounce = nullptr;
+  size_t bounce_bytes = 0;
+  uint64_t bounce_id = 0;
+  std::unique_ptr<Host> host;
+  std::unique_ptr<ReduceTask> task;
+  std::thread reader, runner;
+
+  Session(MergeService* s, int fd) : svc(s), sock(fd) {}
+  ~Session() {
+    if (bounce) munmap(bounce, bounce_bytes);
+    if (bounce_fd >= 0) close(bounce_fd);
+    if (sock >= 0) close(sock);
+  }
+
+  bool send(uint32_t type, const std::string& p, int fd = -1) {
+    std::lock_guard<std::mutex> g(send_mu);
+    return send_msg(sock, type, p, fd);
+  }
+
+  // ---- host callbacks of the task (called on the task's threads)
+  static int data_cb(void* ctx, const void* buf, int32_t len) { return static_cast<Session*>(ctx)->deliver(buf, len); }
+  static int conf_cb(void* ctx, const char* key, const char* dflt, char* out, int32_t outlen) {
+    const std::string v = static_cast<Session*>(ctx)->conf(key ? key : "", dflt ? dflt : "");
+    const int32_t n = (int32_t)std::min<size_t>(v.size(), (size_t)std::max(0, outlen - 1));
+    std::memcpy(out, v.data(), (size_t)n);
+    out[n] = 0;
+    return n;
+  }
+  static void fetch_over_cb(void* ctx) { static_cast<Session*>(ctx)->send(kFetchOver, ""); }
+  static void failure_cb(void* ctx, const char* reason) {
+    static_cast<Session*>(ctx)->send(kFail, reason && *reason ? reason : "merge service task failure");
+  }
+
+  std::string conf(const std::string& key, const std::string& dflt) {
+    uint32_t id;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (closed) return dflt;
+      id = next_conf++;
+    }
+    std::string p;
+    put<uint32_t>(p, id);
+    p += key;
+    p.push_back('\0');
+    p += dflt;
+    if (!send(kConfReq, p)) return dflt;
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return closed || conf_replies.count(id); });
+    if (!conf_replies.count(id)) return dflt;
+    std::string v = std::move(conf_replies[id]);
+    conf_replies.erase(id);
+    return v;
+  }
+
+  int deliver(const void* buf, int32_t len) {
+    gpu::PinnedShare ps;
+    uint64_t id;
+    size_t off;
+    if (len > 0 && gpu::pinned_share_of(buf, (size_t)len, &ps)) {
+      if (!regions_sent.count(ps.id)) {  // one delivery thread per task: no race on the set
+        std::string r;
+        put<uint64_t>(r, ps.id);
+        put<uint64_t>(r, ps.region_bytes);
+        if (!send(kRegion, r, ps.fd)) return -1;
+        regions_sent.insert(ps.id);
+      }
+      id = ps.id;
+      off = ps.offset;
+      svc->zero_copy_.fetch_add(1);
+    } else {
+      if ((size_t)len > bounce_bytes && !grow_bounce((size_t)len)) return -1;
+      std::memcpy(bounce, buf, (size_t)len);
+      id = bounce_id;
+      off = 0;
+      svc->bounced_.fetch_add(1);
+    }
+    std::string d;
+    put<uint64_t>(d, id);
+    put<uint64_t>(d, off);
+    put<uint32_t>(d, (uint32_t)len);
+    if (!send(kData, d)) return -1;
+    // the buffer is reused once dataFromUda returns: wait for the client to have consumed it
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return closed || !acks.empty(); });
+    if (acks.empty()) return -1;
+    const int32_t st = acks.front();
+    acks.pop_front();
+    return st;
+  }
+
+  bool grow_bounce(size_t need) {
+    if (bounce) munmap(bounce, bounce_bytes);
+    if (bounce_fd >= 0) close(bounce_fd);
+    bounce = nullptr;
+    bounce_bytes = 0;
+    bounce_fd = (int)memfd_create("uda-bounce", MFD_CLOEXEC);
+    const size_t sz = (need + 4095) & ~(size_t)4095;
+    if (bounce_fd < 0 || ftruncate(bounce_fd, (off_t)sz) != 0) return false;
+    void* p = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_SHARED, bounce_fd, 0);
+    if (p == MAP_FAILED) return false;
+    bounce = static_cast<uint8_t*>(p);
+    bounce_bytes = sz;
+    bounce_id = (1ull << 63) | svc->bounced_.load();  // never a pinned region id; a new id per growth
+    std::string r;
+    put<uint64_t>(r, bounce_id);
+    put<uint64_t>(r, sz);
+    return send(kRegion, r, bounce_fd);
+  }
+
+  void start(const std::vector<std::string>& args) {
+    uda_callbacks cb{};
+    cb.ctx = this;
+    cb.data_from_uda = data_cb;
+    cb.get_conf = conf_cb;
+    cb.fetch_over = fetch_over_cb;
+    cb.failure = failure_cb;
+    host = std::make_unique<Host>(&cb);
+    NetlevOptions opt;
+    std::string err;
+    if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
+    task = std::make_unique<ReduceTask>(opt, host.get());
+  }
+
+  void run_commands() {
+    for (;;) {
+      std::string c;
+      bool ex;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return closed || exit_requested || !cmds.empty(); });
+        if (!cmds.empty()) {
+          c = std::move(cmds.front());
+          cmds.pop_front();
+          ex = false;
+        } else {
+          ex = true;
+        }
+      }
+      if (ex) break;
+      int32_t st = 0;
+      std::string why;
+      HadoopCmd hc;
+      if (!parse_cmd(c, &hc)) {
+        st = -1;
+        why = "C++ could not parse Hadoop command";
+      } else {
+        try {
+          task->handle(hc);
+        } catch (const std::exception& e) {
+          st = -1;
+          why = e.what();
+        }
+      }
+      std::string r;
+      put<int32_t>(r, st);
+      r += why;
+      send(kCmdResult, r);
+    }
+    // EXIT (or the client is gone): stop and join the task, then report its stats
+    std::string stats = "{}";
+    try {
+      task->exit();
+      stats = task->stats_json();
+    } catch (const std::exception& e) {
+      UDA_LOG(kWarn, "merge service: task exit: %s", e.what());
+    }
+    bool gone;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      gone = closed;
+    }
+    if (!gone) send(kStats, stats);
+  }
+
+  void read_loop() {
+    for (;;) {
+      uint32_t t;
+      std::string p;
+      int fd;
+      if (!recv_msg(sock, &t, &p, &fd)) break;
+      if (fd >= 0) close(fd);
+      std::lock_guard<std::mutex> g(mu);
+      if (t == kCmd) {
+        cmds.push_back(std::move(p));
+      } else if (t == kConfReply) {
+        conf_replies[get<uint32_t>(p, 0)] = p.size() > 4 ? p.substr(4) : std::string();
+      } else if (t == kAck) {
+        acks.push_back(get<int32_t>(p, 0));
+      } else if (t == kExit) {
+        exit_requested = true;
+      }
+      cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(mu);
+    closed = true;
+    cv.notify_all();
+  }
+};
+
+MergeService::MergeService(const std::string& path) : path_(path) {
+  gpu::set_pinned_shareable(true);
+  listen_fd_ = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (listen_fd_ < 0) throw UdaError(std::string("merge service: socket: ") + strerror(errno));
+  ::unlink(path.c_str());
+  sockaddr_un a = unix_addr(path);
+  const mode_t old = ::umask(0077);  // the node's tasks run as the service's user
+  const int rc = ::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a));
+  ::umask(old);
+  if (rc != 0 || ::listen(listen_fd_, 256) != 0) {
+    const std::string e = strerror(errno);
+    close(listen_fd_);
+    throw UdaError("merge service: cannot listen on " + path + ": " + e);
+  }
+  acceptor_ = std::thread([this] { accept_main(); });
+  UDA_LOG(kInfo, "merge service listening on %s", path.c_str());
+}
+
+MergeService::~MergeService() {
+  stop_ = true;
+  ::shutdown(listen_fd_, SHUT_RDWR);
+  if (acceptor_.joinable()) acceptor_.join();
+  close(listen_fd_);
+  ::unlink(path_.c_str());
+  std::vector<std::shared_ptr<Session>> live;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    live.swap(live_);
+  }
+  for (auto& s : live) {
+    ::shutdown(s->sock, SHUT_RDWR);  // the reader sees EOF: the runner stops the task
+    if (s->reader.joinable()) s->reader.join();
+    if (s->runner.joinable()) s->runner.join();
+  }
+}
+
+void MergeService::accept_main() {
+  while (!stop_) {
+    pollfd pf{listen_fd_, POLLIN, 0};
+    const int pr = ::poll(&pf, 1, 200);
+    {  // reap finished sessions
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto it = live_.begin(); it != live_.end();) {
+        Session& s = **it;
+        bool done;
+        {
+          std::lock_guard<std::mutex> sg(s.mu);
+          done = s.closed;
+        }
+        if (done) {
+          if (s.reader.joinable()) s.reader.join();
+          if (s.runner.joinable()) s.runner.join();
+          it = live_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    if (pr <= 0 || !(pf.revents & POLLIN)) continue;
+    const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) continue;
+    auto s = std::make_shared<Session>(this, fd);
+    uint32_t t;
+    std::string p;
+    int pfd;
+    if (!recv_msg(fd, &t, &p, &pfd) || t != kHello) {
+      if (pfd >= 0) close(pfd);
+      continue;  // ~Session closes the socket
+    }
+    std::vector<std::string> args;
+    for (size_t b = 0; b < p.size();) {
+      const size_t e = p.find('\0', b);
+      args.push_back(p.substr(b, e == std::string::npos ? std::string::npos : e - b));
+      if (e == std::string::npos) break;
+      b = e + 1;
+    }
+    // the reader must run before the task starts: ReduceTask's constructor pulls configuration
+    s->reader = std::thread([s] { s->read_loop(); });
+    try {
+      s->start(args);
+    } catch (const std::exception& e) {
+      s->send(kRefused, e.what());
+      ::shutdown(fd, SHUT_RDWR);
+      s->reader.join();
+      continue;
+    }
+    s->send(kReady, "");
+    s->runner = std::thread([s] { s->run_commands(); });
+    ++sessions_;
+    std::lock_guard<std::mutex> g(mu_);
+    live_.push_back(s);
+  }
+}
+
+// ============================================================================ client side
+
+struct RemoteReduceTask::Impl {
+  Host* host;
+  int sock = -1;
+  std::thread reader;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int32_t, std::string>> results;
+  bool have_stats = false, closed = false, exited = false;
+  std::string stats = "{}";
+  std::map<uint64_t, std::pair<uint8_t*, size_t>> regions;  // id -> our mapping
+
+  ~Impl() {
+    if (sock >= 0) ::shutdown(sock, SHUT_RDWR);
+    if (reader.joinable()) reader.join();
+    if (sock >= 0) close(sock);
+    for (auto& kv : regions) munmap(kv.second.first, kv.second.second);
+  }
+
+  void read_loop() {
+    for (;;) {
+      uint32_t t;
+      std::string p;
+      int fd;
+      if (!recv_msg(sock, &t, &p, &fd)) break;
+      if (t == kRegion) {
+        const uint64_t id = get<uint64_t>(p, 0), bytes = get<uint64_t>(p, 8);
+        if (fd >= 0) {
+          void* m = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
+          close(fd);
+          if (m != MAP_FAILED) {
+            auto old = regions.find(id);
+            if (old != regions.end()) munmap(old->second.first, old->second.second);
+            regions[id] = {static_cast<uint8_t*>(m), (size_t)bytes};
+          }
+        }
+      } else if (t == kData) {
+        if (fd >= 0) close(fd);
+        const uint64_t id = get<uint64_t>(p, 0), off = get<uint64_t>(p, 8);
+        const uint32_t len = get<uint32_t>(p, 16);
+        int32_t st = -1;
+        auto it = regions.find(id);
+        if (it != regions.end() && off + len <= it->second.second)
+          st = host->data_from_uda(it->second.first + off, (int32_t)len);
+        else
+          host->fail("merge service sent a buffer outside its shared regions");
+        std::string a;
+        put<int32_t>(a, st);
+        std::lock_guard<std::mutex> g(send_mu);
+        if (!send_msg(sock, kAck, a)) break;
+      } else if (t == kConfReq) {
+        if (fd >= 0) close(fd);
+        const uint32_t id = get<uint32_t>(p, 0);
+        const std::string kd = p.size() > 4 ? p.substr(4) : std::string();
+        const size_t z = kd.find('\0');
+        const std::string key = kd.substr(0, z), dflt = z == std::string::npos ? "" : kd.substr(z + 1);
+        std::string r;
+        put<uint32_t>(r, id);
+        r += host->get_conf(key, dflt);
+        std::lock_guard<std::mutex> g(send_mu);
+        if (!send_msg(sock, kConfReply, r)) break;
+      } else {
+        if (fd >= 0) close(fd);
+        if (t == kFetchOver) {
+          host->fetch_over();
+        } else if (t == kFail) {
+          host->fail(p);
+        } else {
+          std::lock_guard<std::mutex> g(mu);
+          if (t == kCmdResult) {
+            results.emplace_back(get<int32_t>(p, 0), p.size() > 4 ? p.substr(4) : std::string());
+          } else if (t == kStats) {
+            stats = p;
+            have_stats = true;
+          } else if (t == kReady) {
+            results.emplace_back(0, std::string());
+          } else if (t == kRefused) {
+            results.emplace_back(-1, p);
+          }
+          cv.notify_all();
+        }
+      }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    const bool unexpected = !exited;
+    closed = true;
+    cv.notify_all();
+    if (unexpected) host->fail("merge service connection lost");
+  }
+
+  std::pair<int32_t, std::string> wait_result() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return closed || !results.empty(); });
+    if (results.empty()) return {-1, "merge service connection lost"};
+    auto r = std::move(results.front());
+    results.pop_front();
+    return r;
+  }
+
+  bool send(uint32_t t, const std::string& p) {
+    std::lock_guard<std::mutex> g(send_mu);
+    return send_msg(sock, t, p);
+  }
+  std::mutex send_mu;
+};
+
+RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<std::string>& args, Host* host)
+    : impl_(new Impl) {
+  impl_->host = host;
+  impl_->sock = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (impl_->sock < 0) throw UdaError(std::string("merge service client: socket: ") + strerror(errno));
+  sockaddr_un a = unix_addr(path);
+  if (::connect(impl_->sock, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
+    throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
+  std::string hello;
+  for (size_t i = 0; i < args.size(); ++i) {
+    if (i) hello.push_back('\0');
+    hello += args[i];
+  }
+  if (!send_msg(impl_->sock, kHello, hello)) throw UdaError("merge service " + path + ": HELLO failed");
+  Impl* im = impl_.get();
+  impl_->reader = std::thread([im] { im->read_loop(); });
+  const auto r = impl_->wait_result();
+  if (r.first != 0) {
+    {
+      std::lock_guard<std::mutex> g(impl_->mu);
+      impl_->exited = true;  // a refused start is an error of this call, not a task failure
+    }
+    throw UdaError("merge service refused the task: " + r.second);
+  }
+}
+
+RemoteReduceTask::~RemoteReduceTask() {
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    impl_->exited = true;
+  }
+  impl_.reset();
+}
+
+void RemoteReduceTask::handle(const std::string& cmd) {
+  if (!impl_->send(kCmd, cmd)) throw UdaError("merge service connection lost");
+  const auto r = impl_->wait_result();
+  if (r.first != 0) throw UdaError(r.second);
+}
+
+void RemoteReduceTask::exit() {
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    if (impl_->exited) return;
+    impl_->exited = true;
+  }
+  if (!impl_->send(kExit, "")) return;
+  std::unique_lock<std::mutex> lk(impl_->mu);
+  impl_->cv.wait_for(lk, std::chrono::seconds(120), [&] { return impl_->have_stats || impl_->closed; });
+}
+
+std::string RemoteReduceTask::stats_json() {
+  std::lock_guard<std::mutex> g(impl_->mu);
+  if (impl_->have_stats && impl_->stats.size() > 1 && impl_->stats.back() == '}')
+    return impl_->stats.substr(0, impl_->stats.size() - 1) + ",\"merge_service\":true}";
+  return impl_->stats;
+}
+
+}  // namespace uda

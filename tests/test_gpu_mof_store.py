@@ -132,14 +132,17 @@ def test_empty_partitions_on_the_generic_device_path(require_gpu):
         p.close()
 
 
-def test_bench_node_shape_small(require_gpu):
-    """bench.py --api --node: the provider in this process, every reduce task a fresh uda_reduce_task
-    process mapping the provider's HBM over hipIpc (validated wave, descriptors only)."""
+@pytest.mark.parametrize("service", [False, True])
+def test_bench_node_shape_small(require_gpu, service):
+    """bench.py --api --node: the provider in its own process, every reduce task a fresh uda_reduce_task
+    process mapping the provider's HBM over hipIpc (validated wave, descriptors only); with
+    --node-service the NetMergers run in the provider process and the task processes read the merged
+    buffers in place from its shared pinned rings (zero-copy)."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--api", "--node", "--reducers", "3", "--rows-per-gpu",
-           "3000000", "--maps-per-gpu", "6", "--steps", "1", "--warmup", "1"]
+           "3000000", "--maps-per-gpu", "6", "--steps", "1", "--warmup", "1"] + (["--node-service"] if service else [])
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -147,3 +150,7 @@ def test_bench_node_shape_small(require_gpu):
     t0 = out["task0_stats"]
     assert t0["device_descriptors"] == 6 and t0["host_fetched_bytes"] == 0 and t0["gpu_device"] == 0, t0
     assert out["node"]["task_ms_median"]["fetch_to_eof_ms"] > 0
+    if service:
+        ms = out["provider"]["merge_service"]
+        assert t0.get("merge_service") is True and ms["sessions"] >= 6, ms
+        assert ms["zero_copy_buffers"] > ms["bounced_buffers"], ms

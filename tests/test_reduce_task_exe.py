@@ -25,8 +25,8 @@ def _port():
         return s.getsockname()[1]
 
 
-def _task(native, port, job, ids, r, expect, backend="cpu", order=False):
-    argv = [EXE, "-D", "mapred.uda.transport=tcp", "-D", f"mapred.uda.merge.backend={backend}",
+def _task(native, port, job, ids, r, expect, backend="cpu", order=False, extra=()):
+    argv = [EXE, "-D", "mapred.uda.transport=tcp", "-D", f"mapred.uda.merge.backend={backend}", *extra,
             "--expect", str(expect), "--kv-buf", str(64 << 10)] + (["--check-order"] if order else [])
     argv += ["--", "-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
     init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_{r:06d}_0", "0", str(1 << 20),
@@ -59,5 +59,75 @@ def test_reduce_task_processes_against_a_provider_process(native):
             assert out["fetch_to_eof_ms"] >= 0 and out["exec_to_end_ms"] >= out["fetch_to_eof_ms"]
         rc, out = _task(native, port, job, ids, 0, 1)  # wrong expectation: the process says so
         assert rc == 1 and "expected 1" in out["error"], out
+    finally:
+        prov.close()
+
+
+def _service_provider(tmp_path, port):
+    path = str(tmp_path / "merge.sock")
+    prov = UdaProvider(transport="tcp", data_port=port, conf={"mapred.uda.provider.bind.address": "127.0.0.1",
+                                                              "mapred.uda.gpu.merge.service": path})
+    job = "job_8_0001"
+    maps = datagen.terasort(num_maps=4, reducers=3, rows_per_map=1500, seed=78)
+    ids = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        data, index = encode_partitions(parts, None)
+        prov.add_mof_memory(job, mid, data, index)
+        ids.append(mid)
+    return prov, path, job, maps, ids
+
+
+@pytest.mark.skipif(not os.access(EXE, os.X_OK), reason="uda_reduce_task not built")
+def test_reduce_tasks_hosted_by_the_merge_service(native, tmp_path):
+    """mapred.uda.gpu.merge.service: the reduce task processes are thin clients; their NetMergers run in
+    the provider's process (commands, configuration pulls, dataFromUda and the stats cross a Unix
+    socket). Three tasks at once, each must deliver its partition in order."""
+    import concurrent.futures as cf
+    port = _port()
+    prov, path, job, maps, ids = _service_provider(tmp_path, port)
+    try:
+        def run(r):
+            want = sum(len(m[r]) for m in maps)
+            return want, _task(native, port, job, ids, r, want, order=True, extra=["-D", f"mapred.uda.gpu.merge.service={path}"])
+        with cf.ThreadPoolExecutor(3) as ex:
+            outs = list(ex.map(run, range(3)))
+        for want, (rc, out) in outs:
+            assert rc == 0 and out["error"] == "", out
+            assert out["records"] == want and out["order_errors"] == 0
+            assert out["task"].get("merge_service") is True and out["task"]["maps_fetched"] == 4
+    finally:
+        prov.close()
+
+
+@pytest.mark.skipif(not os.access(EXE, os.X_OK), reason="uda_reduce_task not built")
+def test_merge_service_survives_a_dead_client_and_reports_failures(native, tmp_path):
+    """A client killed mid-task leaves the service serving the next task; a task whose FETCH names a map
+    the provider does not have fails in its own process (failureInUda), as an in-process task would;
+    an unreachable service means the task merges in its own process."""
+    port = _port()
+    prov, path, job, maps, ids = _service_provider(tmp_path, port)
+    try:
+        argv = [EXE, "-D", "mapred.uda.transport=tcp", "-D", "mapred.uda.merge.backend=cpu",
+                "-D", f"mapred.uda.gpu.merge.service={path}", "--", "-w", "256", "-r", str(port), "-a", "1", "-m",
+                "1", "-g", "/tmp", "-s", "1024"]
+        init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_000001_0", "0", str(1 << 20),
+                                      str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0", "0"])
+        p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        p.stdin.write(init + "\n")
+        p.stdin.flush()
+        import time
+        time.sleep(0.5)
+        p.kill()
+        p.wait()
+        want = sum(len(m[1]) for m in maps)
+        rc, out = _task(native, port, job, ids, 1, want, order=True, extra=["-D", f"mapred.uda.gpu.merge.service={path}"])
+        assert rc == 0 and out["records"] == want and out["task"].get("merge_service") is True, out
+        rc, out = _task(native, port, job, ids[:3] + [f"attempt_{job}_m_000099_0"], 2, 1,
+                        extra=["-D", f"mapred.uda.gpu.merge.service={path}"])
+        assert rc == 1 and out["error"], out
+        rc, out = _task(native, port, job, ids, 0, sum(len(m[0]) for m in maps),
+                        extra=["-D", f"mapred.uda.gpu.merge.service={tmp_path}/none.sock"])
+        assert rc == 0 and "merge_service" not in out["task"], out
     finally:
         prov.close()

@@ -28,7 +28,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 def sources() -> tuple[list[str], list[str]]:
     lib = []
     for pat in ("common/*.cc", "engine/*.cc", "provider/*.cc", "consumer/*.cc", "transport/*.cc",
-                "io/*.cc", "codec/*.cc", "gpu/*.cc", "gpu/*.hip", "bridge/*.cc"):
+                "io/*.cc", "codec/*.cc", "gpu/*.cc", "gpu/*.hip", "service/*.cc", "bridge/*.cc"):
         lib += sorted(glob.glob(os.path.join(ROOT, "csrc", pat)))
     mod = sorted(glob.glob(os.path.join(ROOT, "csrc", "python", "*.cc")))
     return lib, mod
