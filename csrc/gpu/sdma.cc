@@ -442,6 +442,17 @@ void SdmaEngine::release_ring(void* p, size_t bytes) {
 
 void* SdmaEngine::alloc_host(size_t bytes) {
   void* p = nullptr;
+  if (g_shareable.load()) {
+    // merge service: delivery rings its clients map (memfd-backed, registered; sdma.h)
+    try {
+      p = pinned_host_alloc(bytes, numa_node_);
+      PinnedShare ps;
+      if (pinned_share_of(p, 1, &ps)) return p;
+      pinned_host_free(p);  // registration of the shared pages failed: the host pool, not shareable
+    } catch (const std::exception&) {
+    }
+    p = nullptr;
+  }
   hsa_check(hsa_amd_memory_pool_allocate(host_pool_, bytes, 0, &p), "host pool allocate");
   hsa_status_t s = hsa_amd_agents_allow_access(1, &gpu_, nullptr, p);
   if (s != HSA_STATUS_SUCCESS) {
@@ -452,7 +463,12 @@ void* SdmaEngine::alloc_host(size_t bytes) {
 }
 
 void SdmaEngine::free_host(void* p) {
-  if (p) (void)hsa_amd_memory_pool_free(p);
+  if (!p) return;
+  PinnedShare ps;
+  if (pinned_share_of(p, 1, &ps))
+    pinned_host_free(p);
+  else
+    (void)hsa_amd_memory_pool_free(p);
 }
 
 hsa_signal_t SdmaEngine::make_signal() {

@@ -6,6 +6,7 @@
 #include <sys/mman.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/time.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -166,6 +167,8 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   uint64_t bounce_id = 0;
   std::unique_ptr<Host> host;
   std::unique_ptr<ReduceTask> task;
+  std::vector<std::string> args;  // startNative arguments (HELLO)
+  std::atomic<bool> finished{false};  // the runner has returned: the session can be reaped
   std::thread reader, runner;
 
   Session(MergeService* s, int fd) : svc(s), sock(fd) {}
@@ -282,6 +285,23 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     std::string err;
     if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
     task = std::make_unique<ReduceTask>(opt, host.get());
+  }
+
+  // The task's whole life on one thread: start (its constructor pulls configuration, which the reader
+  // thread answers), the commands in order, and the stop on EXIT or when the client went away.
+  void run() {
+    try {
+      start(args);
+    } catch (const std::exception& e) {
+      send(kRefused, e.what());
+      ::shutdown(sock, SHUT_RDWR);
+      finished = true;
+      return;
+    }
+    send(kReady, "");
+    svc->sessions_.fetch_add(1);
+    run_commands();
+    finished = true;
   }
 
   void run_commands() {
@@ -407,7 +427,7 @@ void MergeService::accept_main() {
         bool done;
         {
           std::lock_guard<std::mutex> sg(s.mu);
-          done = s.closed;
+          done = s.closed && s.finished.load();  // joins below return at once
         }
         if (done) {
           if (s.reader.joinable()) s.reader.join();
@@ -422,6 +442,8 @@ void MergeService::accept_main() {
     const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) continue;
     auto s = std::make_shared<Session>(this, fd);
+    timeval hello_wait{10, 0};
+    (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &hello_wait, sizeof(hello_wait));
     uint32_t t;
     std::string p;
     int pfd;
@@ -429,26 +451,16 @@ void MergeService::accept_main() {
       if (pfd >= 0) close(pfd);
       continue;  // ~Session closes the socket
     }
-    std::vector<std::string> args;
     for (size_t b = 0; b < p.size();) {
       const size_t e = p.find('\0', b);
-      args.push_back(p.substr(b, e == std::string::npos ? std::string::npos : e - b));
+      s->args.push_back(p.substr(b, e == std::string::npos ? std::string::npos : e - b));
       if (e == std::string::npos) break;
       b = e + 1;
     }
-    // the reader must run before the task starts: ReduceTask's constructor pulls configuration
+    timeval none{0, 0};
+    (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
     s->reader = std::thread([s] { s->read_loop(); });
-    try {
-      s->start(args);
-    } catch (const std::exception& e) {
-      s->send(kRefused, e.what());
-      ::shutdown(fd, SHUT_RDWR);
-      s->reader.join();
-      continue;
-    }
-    s->send(kReady, "");
-    s->runner = std::thread([s] { s->run_commands(); });
-    ++sessions_;
+    s->runner = std::thread([s] { s->run(); });
     std::lock_guard<std::mutex> g(mu_);
     live_.push_back(s);
   }

@@ -60,6 +60,74 @@ def child(args) -> int:
     return 0
 
 
+def node(args) -> int:
+    """The node shape of a cold reduce task: this process is the node's MOFSupplier (host MOFs, TCP, long
+    lived and warm, as the NodeManager aux service is), and every trial starts a fresh uda_reduce_task
+    process (its ReduceTask JVM): INIT, the slow-start gap, then the FETCHes; the task reports FETCH ->
+    EOF. With the merge service the task's NetMerger runs in this process (warm GPU context and pools)
+    and the task process only reads the merged buffers in place; without it the task merges in its own
+    process (prewarm during the gap)."""
+    import socket
+    import time
+    from uda_amd import native
+    from uda_amd.bridge import FETCH, INIT, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    n = native()
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "uda_amd", "bin", "uda_reduce_task")
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    runs = n.generate_runs("secondary", args.maps, 1, rows, 9)
+    mofs = []
+    for m, parts in enumerate(runs):
+        data, index = encode_partitions(parts)
+        mofs.append((f"attempt_cold_m_{m:06d}_0", data, index, n.ifile_checksum(parts[0])[0]))
+    del runs
+    total = sum(len(d) - 2 for _, d, _, _ in mofs)
+    expect = sum(c for _, _, _, c in mofs)
+    for svc in (1, 0):
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        path = f"/tmp/uda-cold-{os.getpid()}.sock"
+        conf = {"mapred.uda.provider.bind.address": "127.0.0.1"}
+        if svc:
+            conf["mapred.uda.gpu.merge.service"] = path
+        prov = UdaProvider(transport="tcp", data_port=port, conf=conf)
+        try:
+            for mid, data, index, _ in mofs:
+                prov.add_mof_memory("job_cold", mid, data, index)
+            for t in range(args.repeat + 1):  # trial 0 warms the service's pools (a node's first task)
+                argv = [exe, "-D", "mapred.uda.transport=tcp", "-D", f"mapred.uda.merge.backend={args.backend}",
+                        "-D", f"mapred.uda.gpu.prewarm={args.prewarm}", "--expect", str(expect), "--check-order"]
+                if svc:
+                    argv += ["-D", f"mapred.uda.gpu.merge.service={path}"]
+                argv += ["--", "-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
+                init = n.form_cmd(INIT, [str(args.maps), "job_cold", "attempt_cold_r_000000_0", "0", str(1 << 20),
+                                         str(16 << 10), TEXT, "null", str(256 << 10), "0", "0"])
+                p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+                p.stdin.write(init + "\n")
+                p.stdin.flush()
+                time.sleep(args.gap)
+                p.stdin.write("\n".join(n.form_cmd(FETCH, ["127.0.0.1", "job_cold", mid, "0"]) for mid, _, _, _ in mofs) + "\n")
+                p.stdin.close()
+                out = p.stdout.read()
+                p.wait(timeout=300)
+                res = json.loads(out.strip().splitlines()[-1])
+                if p.returncode != 0 or res.get("error"):
+                    print(json.dumps({"error": res.get("error"), "rc": p.returncode}), flush=True)
+                    return 1
+                st = res["task"]
+                print(json.dumps({"mode": "node", "merge_service": bool(svc), "trial": t, "gap_s": args.gap,
+                                  "gb": round(total / 1e9, 3), "gbps": round(total / res["fetch_to_eof_ms"] / 1e6, 2),
+                                  "fetch_to_eof_ms": res["fetch_to_eof_ms"], "exec_to_end_ms": res["exec_to_end_ms"],
+                                  "fetch_ms": round(st.get("fetch_ms", -1), 1), "merge_ms": round(st.get("merge_ms", -1), 1),
+                                  "prewarm_wait_ms": round(st.get("gpu_prewarm_wait_ms", 0), 1),
+                                  "merge_path": st.get("merge_path")}), flush=True)
+        finally:
+            prov.close()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=2.0)
@@ -68,9 +136,14 @@ def main() -> int:
     ap.add_argument("--prewarm", type=int, default=1)
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--backend", default="gpu", help="--node: mapred.uda.merge.backend of the tasks")
+    ap.add_argument("--node", action="store_true",
+                    help="provider (and merge service) in this process, each task a fresh uda_reduce_task process")
     args = ap.parse_args()
     if args.child:
         return child(args)
+    if args.node:
+        return node(args)
     for _ in range(args.repeat):
         for pw in (1, 0):
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--gb", str(args.gb),

@@ -49,6 +49,9 @@ RECIPES: dict[str, tuple[int, str]] = {
     "node_gap": (600, f"{PY} bench.py --api --node --reducers 15 --node-gap 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
+    "coldnode": (400, f"{PY} tools/cold_task_bench.py --node --repeat 3"),
+    "nodesvc": (400, f"{PY} bench.py --api --node --node-service --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodesvc130": (500, f"{PY} bench.py --api --node --node-service --reducers 15 --steps 2 --warmup 1"),
     "netmerger": (400, f"{PY} benchmarks/run_configs.py netmerger --gb 2 --maps 64 --reducers 1"),
     "prof_bench": (500, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- "
                         "python3 bench.py --steps 3 --warmup 1"),
