@@ -30,8 +30,6 @@
 //    wave-level priority queue: lanes own runs, a wave argmin picks the next record each step.
 #include "kernels.h"
 
-#include <algorithm>
-#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -215,256 +213,13 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const E
   }
 }
 
-// One pairwise merge level: outputs o0 .. o0 + todo - 1 of level w (pairs of w-slice segments) into
-// held[], read from the level in src (n elements in the cell, reads clamped to it).
-template <int ITEMS>
-__device__ __forceinline__ void kw_merge_level(const Elem* src, const int* seg, int K, int w, int n, int o0, int todo,
-                                               uint64_t* held_hi, uint64_t* held_lo) {
-  const int npairs = (K + 2 * w - 1) / (2 * w);
-  // pair p covers segments [2pw, 2pw + 2w): find the pair holding output o0
-  int pl = 0, ph = npairs;
-  while (ph - pl > 1) {
-    const int mid = (pl + ph) >> 1;
-    if (seg[min(2 * mid * w, K)] <= o0)
-      pl = mid;
-    else
-      ph = mid;
-  }
-  int p = pl;
-  int a0 = seg[min(2 * p * w, K)], a1 = seg[min((2 * p + 1) * w, K)], b1 = seg[min((2 * p + 2) * w, K)];
-  // merge path at diagonal o0 - a0 within the pair
-  int d = o0 - a0, la = a1 - a0, lb = b1 - a1;
-  int ml = d > lb ? d - lb : 0, mh = d < la ? d : la;
-  while (ml < mh) {
-    const int mid = (ml + mh) >> 1;
-    if (kle(src[a0 + mid], src[a1 + d - 1 - mid]))
-      ml = mid + 1;
-    else
-      mh = mid;
-  }
-  int ia = ml, ib = d - ml;
-  // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
-  // to the cell so a run's end never reads past the buffer
-  Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
-    const int o = o0 + k;
-    while (o == b1) {  // next pair (empty pairs are skipped)
-      ++p;
-      a0 = b1;
-      a1 = seg[min((2 * p + 1) * w, K)];
-      b1 = seg[min((2 * p + 2) * w, K)];
-      la = a1 - a0;
-      lb = b1 - a1;
-      ia = 0;
-      ib = 0;
-      va = src[min(a0, n - 1)];
-      vb = src[min(a1, n - 1)];
-    }
-    const bool take_a = ib >= lb || (ia < la && kle(va, vb));
-    Elem v;  // field-wise select: a select of the two structs becomes a scratch slot + indexed load
-    v.hi = take_a ? va.hi : vb.hi;
-    v.lo = take_a ? va.lo : vb.lo;
-    held_hi[k] = v.hi;
-    held_lo[k] = v.lo;
-    if (take_a) {
-      ++ia;
-      va = src[min(a0 + ia, n - 1)];
-    } else {
-      ++ib;
-      vb = src[min(a1 + ib, n - 1)];
-    }
-  }
-}
-
-// Which group and cell of the group output cell b is.
-__device__ __forceinline__ void kw_locate(const KwayDesc& kd, int64_t b, int& g, int& c, int& ncell, int& r0, int& K) {
-  int lo = 0, hi = kd.G;  // cell_first[lo] <= b < cell_first[lo + 1]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (kd.cell_first[mid] <= b)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  g = lo;
-  c = (int)(b - kd.cell_first[g]);
-  ncell = (int)(kd.cell_first[g + 1] - kd.cell_first[g]);
-  r0 = kd.group_first[g];
-  K = kd.group_first[g + 1] - r0;
-}
-
-// F2, first half: issue every key load of the cell's n <= cap records (items past n re-read item
-// n - 1, so the loads stay unguarded and all in flight); sp = slice << 16 | record within the slice.
-template <int ITEMS>
-__device__ __forceinline__ void kw_keys_issue(const uint8_t* const* sbase, const int* seg, int K, int n, uint64_t* w0,
-                                              uint64_t* w1, int* sp) {
-  if (n <= 0) return;
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int i = min((int)threadIdx.x + k * 256, n - 1);
-    int sl = 0, sh = K;  // seg[sl] <= i < seg[sl + 1]
-    while (sh - sl > 1) {
-      const int mid = (sl + sh) >> 1;
-      if (seg[mid] <= i)
-        sl = mid;
-      else
-        sh = mid;
-    }
-    sp[k] = (sl << 16) | (i - seg[sl]);
-  }
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const GlobalU64* rec = gptr(sbase[sp[k] >> 16] + (int64_t)(sp[k] & 0xFFFF) * kTeraRecordBytes);
-    w0[k] = rec[0];
-    w1[k] = rec[1];
-  }
-}
-
-// F2, second half: the landed keys into LDS as merge elements (ties: slice, then position).
-template <int ITEMS>
-__device__ __forceinline__ void kw_keys_write(Elem* buf, int n, const uint64_t* w0, const uint64_t* w1, const int* sp,
-                                              int* bad_layout) {
-  int bad = 0;
-#pragma unroll
-  for (int k = 0; k < ITEMS; ++k) {
-    const int i = threadIdx.x + k * 256;
-    if (i < n) buf[i] = key_elem(w0[k], w1[k], sp[k] >> 16, sp[k] & 0xFFFF, bad);
-  }
-  if (bad) *bad_layout = 1;
-}
-
-// A cell that does not fit LDS (massively duplicated keys), merged by wave 0 alone as a wave-level
-// priority queue: lane l owns slices l, l + 64, ... (K <= 256: four per lane, their remaining and
-// taken counts in registers); each step a wave argmin picks the next record.
-__device__ void kw_pq(const KwayDesc& kd, const uint8_t* const* sbase, const int* seg, int K, int n, uint8_t* obase) {
-  const int lane = threadIdx.x;
-  constexpr int kWords = kTeraRecordBytes / 8;
-  constexpr int kPer = kKwMaxRuns / 64;
-  int left[kPer], taken[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = lane + 64 * j;
-    left[j] = k < K ? seg[k + 1] - seg[k] : 0;
-    taken[j] = 0;
-  }
-  for (int64_t i = 0; i < n; ++i) {
-    Elem best{~0ull, ~0ull};
-    int bk = -1;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int k = lane + 64 * j;
-      if (left[j] > 0) {
-        const Elem e = load_key_elem(sbase[k] + (int64_t)taken[j] * kTeraRecordBytes, k, taken[j], kd.bad_layout);
-        if (bk < 0 || kle(e, best)) {
-          best = e;
-          bk = k;
-        }
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const uint64_t oh = __shfl_xor(best.hi, off, 64), ol = __shfl_xor(best.lo, off, 64);
-      const int ok = __shfl_xor(bk, off, 64);
-      const bool take = ok >= 0 && (bk < 0 || oh < best.hi || (oh == best.hi && ol < best.lo));
-      if (take) {
-        best.hi = oh;
-        best.lo = ol;
-        bk = ok;
-      }
-    }
-    const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(sbase[bk] + pos * kTeraRecordBytes);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
-    if (lane < kWords) dst[lane] = src[lane];
-    if (lane == (bk & 63)) {
-#pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        if ((bk >> 6) == j) {
-          ++taken[j];
-          --left[j];
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// F3: the K sorted slices of the cell (seg[0..K] offsets, n elements in src) merged pairwise in
-// place: log2(K) levels, each thread's outputs of a level held in registers until every thread has
-// read the level.
-template <int ITEMS, bool WAVEF3>
-__device__ __forceinline__ void kw_f3(Elem* src, const int* seg, int K, int n) {
-  constexpr int kKwItems = ITEMS;
-  constexpr int kKwThreads = 256;
-  constexpr int kKwWaves = kKwThreads / 64;
-  // outputs per thread: n spread evenly over the workgroup, so a cell filled to 65 % of its capacity
-  // keeps every thread busy with a 65 % long merge chain
-  const int ipt = (n + kKwThreads - 1) / kKwThreads;
-  const int o0 = threadIdx.x * ipt;
-  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // this thread's outputs of the current level
-  int w0 = 1;
-  if (WAVEF3) {
-    // The low levels merge inside groups of Kq consecutive slices (Kq a power of two, one group per
-    // wave): a wave's lanes run in lockstep and its LDS operations complete in order, so those levels
-    // need no workgroup barrier. Only if every group fits the held registers (uniform decision).
-    int Kq = 1;
-    while (Kq * kKwWaves < K) Kq <<= 1;
-    bool fits = Kq > 1;
-#pragma unroll
-    for (int g2 = 0; g2 < kKwWaves; ++g2) fits = fits && seg[min((g2 + 1) * Kq, K)] - seg[min(g2 * Kq, K)] <= 64 * kKwItems;
-    if (fits) {
-      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-      const int e0 = seg[min(wv * Kq, K)], e1 = seg[min((wv + 1) * Kq, K)];
-      const int ipw = (e1 - e0 + 63) / 64, ow = e0 + lane * ipw;
-      const int todo = ow < e1 ? min(ipw, e1 - ow) : 0;
-      for (int w = 1; w < Kq; w <<= 1) {
-        if (todo > 0) kw_merge_level<kKwItems>(src, seg, K, w, n, ow, todo, held_hi, held_lo);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int k = 0; k < kKwItems; ++k)
-          if (k < todo) src[ow + k] = Elem{held_hi[k], held_lo[k]};
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      __syncthreads();
-      w0 = Kq;
-    }
-  }
-  for (int w = w0; w < K; w <<= 1) {
-    if (o0 < n) kw_merge_level<kKwItems>(src, seg, K, w, n, o0, min(ipt, n - o0), held_hi, held_lo);
-    __syncthreads();
-    // every thread has read the level: overwrite it with the merged order
-    if (o0 < n) {
-      const int todo = min(ipt, n - o0);
-#pragma unroll
-      for (int k = 0; k < kKwItems; ++k)
-        if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
-    }
-    __syncthreads();
-  }
-}
-
-// F4: records in merged order straight to the output, one wave per 64 output records
-__device__ __forceinline__ void kw_f4(const uint8_t* const* sbase, const Elem* src, int n, uint8_t* obase) {
-  const int wave = threadIdx.x >> 6;
-  for (int base = wave * 64; base < n; base += 4 * 64) {
-    const int valid = min(64, n - base);
-    kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
-  }
-}
-
 }  // namespace
 
 // ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffer is dynamic, so
 // smaller capacities fit more workgroups per CU. One cap x 16-byte buffer: a merge level keeps each
 // thread's outputs in registers, waits for every thread to finish reading, then writes them back in
 // place (two barriers per level), half the LDS of ping-pong buffers (+18.5 %, r3_kway_occupancy.md).
-template <int ITEMS, bool WAVEF3>
+template <int ITEMS>
 __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* out) {
   constexpr int kKwItems = ITEMS;
   constexpr int kKwThreads = 256;
@@ -509,8 +264,59 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
   uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
   if (n > kCap) {  // uniform across the block
     if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
+    // wave-level priority queue: lane l owns slices l, l + 64, ... (K <= 256: four per lane, their
+    // remaining counts and taken counts in registers); each step a wave argmin picks the next record
     if (threadIdx.x >= 64) return;
-    kw_pq(kd, sbase, seg, K, n, obase);
+    const int lane = threadIdx.x;
+    constexpr int kWords = kTeraRecordBytes / 8;
+    constexpr int kPer = kKwMaxRuns / 64;
+    int left[kPer], taken[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = lane + 64 * j;
+      left[j] = k < K ? seg[k + 1] - seg[k] : 0;
+      taken[j] = 0;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      Elem best{~0ull, ~0ull};
+      int bk = -1;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int k = lane + 64 * j;
+        if (left[j] > 0) {
+          const Elem e = load_key_elem(sbase[k] + (int64_t)taken[j] * kTeraRecordBytes, k, taken[j], kd.bad_layout);
+          if (bk < 0 || kle(e, best)) {
+            best = e;
+            bk = k;
+          }
+        }
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t oh = __shfl_xor(best.hi, off, 64), ol = __shfl_xor(best.lo, off, 64);
+        const int ok = __shfl_xor(bk, off, 64);
+        const bool take = ok >= 0 && (bk < 0 || oh < best.hi || (oh == best.hi && ol < best.lo));
+        if (take) {
+          best.hi = oh;
+          best.lo = ol;
+          bk = ok;
+        }
+      }
+      const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(sbase[bk] + pos * kTeraRecordBytes);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
+      if (lane < kWords) dst[lane] = src[lane];
+      if (lane == (bk & 63)) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if ((bk >> 6) == j) {
+            ++taken[j];
+            --left[j];
+          }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+    }
     return;
   }
   // ---- F2: keys of every slice into LDS (all of a thread's key loads in flight at once)
@@ -550,83 +356,92 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
   stamp(2);
   // ---- F3: pairwise merge levels inside LDS
   Elem* src = bufA;
-  kw_f3<ITEMS, WAVEF3>(src, seg, K, n);
+  // outputs per thread: n spread evenly over the workgroup, so a cell filled to 65 % of its capacity
+  // keeps every thread busy with a 65 % long merge chain
+  const int ipt = (n + kKwThreads - 1) / kKwThreads;
+  const int o0 = threadIdx.x * ipt;
+  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // this thread's outputs of the current level
+  for (int w = 1; w < K; w <<= 1) {
+    if (o0 < n) {
+      const int npairs = (K + 2 * w - 1) / (2 * w);
+      // pair p covers segments [2pw, 2pw + 2w): find the pair holding output o0
+      int pl = 0, ph = npairs;
+      while (ph - pl > 1) {
+        const int mid = (pl + ph) >> 1;
+        if (seg[min(2 * mid * w, K)] <= o0)
+          pl = mid;
+        else
+          ph = mid;
+      }
+      int p = pl;
+      int a0 = seg[min(2 * p * w, K)], a1 = seg[min((2 * p + 1) * w, K)], b1 = seg[min((2 * p + 2) * w, K)];
+      // merge path at diagonal o0 - a0 within the pair
+      int d = o0 - a0, la = a1 - a0, lb = b1 - a1;
+      int ml = d > lb ? d - lb : 0, mh = d < la ? d : la;
+      while (ml < mh) {
+        const int mid = (ml + mh) >> 1;
+        if (kle(src[a0 + mid], src[a1 + d - 1 - mid]))
+          ml = mid + 1;
+        else
+          mh = mid;
+      }
+      int ia = ml, ib = d - ml;
+      const int todo = min(ipt, n - o0);
+      // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
+      // to the cell so a run's end never reads past the buffer
+      Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
+#pragma unroll
+      for (int k = 0; k < kKwItems; ++k) {
+        if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
+        const int o = o0 + k;
+        while (o == b1) {  // next pair (empty pairs are skipped)
+          ++p;
+          a0 = b1;
+          a1 = seg[min((2 * p + 1) * w, K)];
+          b1 = seg[min((2 * p + 2) * w, K)];
+          la = a1 - a0;
+          lb = b1 - a1;
+          ia = 0;
+          ib = 0;
+          va = src[min(a0, n - 1)];
+          vb = src[min(a1, n - 1)];
+        }
+        const bool take_a = ib >= lb || (ia < la && kle(va, vb));
+        Elem v;  // field-wise select: a select of the two structs becomes a scratch slot + indexed load
+        v.hi = take_a ? va.hi : vb.hi;
+        v.lo = take_a ? va.lo : vb.lo;
+        held_hi[k] = v.hi;
+        held_lo[k] = v.lo;
+        if (take_a) {
+          ++ia;
+          va = src[min(a0 + ia, n - 1)];
+        } else {
+          ++ib;
+          vb = src[min(a1 + ib, n - 1)];
+        }
+      }
+    }
+    __syncthreads();
+    // every thread has read the level: overwrite it with the merged order
+    if (o0 < n) {
+      const int todo = min(ipt, n - o0);
+#pragma unroll
+      for (int k = 0; k < kKwItems; ++k)
+        if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
+    }
+    __syncthreads();
+  }
   stamp(3);
   // ---- F4: records in merged order straight to the output
-  kw_f4(sbase, src, n, obase);
+  const int wave = threadIdx.x >> 6;
+  for (int base = wave * 64; base < n; base += kKwWaves * 64) {
+    const int valid = min(64, n - base);
+    kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
+  }
   if (kd.prof) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     stamp(4);
-  }
-}
-
-// Persistent, software-pipelined form of kway_tile_kernel: each workgroup merges a sequence of cells
-// and issues the next cell's key loads (F2) before merging the current one, so they land while F3
-// runs in LDS (no global traffic) and F4 gathers. The one-cell kernel exposes F2's full HBM latency
-// per cell (a third of a cell's life, UDA_KWAY_PROF: F2 13 / F3 14 / F4 17 us). Costs a second set of
-// per-slice tables in LDS and the prefetched keys' registers.
-template <int ITEMS, bool WAVEF3>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) kway_pipe_kernel(KwayDesc kd, uint8_t* out, int64_t ncells) {
-  constexpr int kCap = ITEMS * 256;
-  extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
-  Elem* buf = kw_dyn;
-  // two sets of per-slice tables: the cell being merged, and the next one whose keys are in flight
-  char* tb = reinterpret_cast<char*>(kw_dyn + kCap);
-  const size_t ts = (size_t)kd.kmax * sizeof(void*) + (size_t)((kd.kmax + 2) & ~1) * sizeof(int);
-  const uint8_t** sb[2];
-  int* sg[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    sb[t] = reinterpret_cast<const uint8_t**>(tb + t * ts);
-    sg[t] = reinterpret_cast<int*>(sb[t] + kd.kmax);
-  }
-  __shared__ int64_t s_start[2];
-  // XCD x (blockIdx.x % 8: the dispatcher deals workgroups round-robin over the XCDs, each with its own
-  // L2) owns a contiguous block of cells, which its workgroups take in turn: neighbouring cells (adjacent
-  // slices of the same runs) are merged at about the same time in one L2.
-  const int64_t x = blockIdx.x % 8, W = gridDim.x;
-  const int64_t wx = W / 8 + (x < W % 8 ? 1 : 0), slot = blockIdx.x / 8;
-  const int64_t q = ncells / 8, rem = ncells % 8;
-  const int64_t lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
-  const int64_t hi = lo + q + (x < rem ? 1 : 0);
-  int64_t cell = lo + slot;
-  if (cell >= hi) return;  // uniform: the whole workgroup has no cell
-  int g, c, ncell, r0, K;
-  kw_locate(kd, cell, g, c, ncell, r0, K);
-  kw_slices(kd, c, ncell, r0, K, sg[0], sb[0], &s_start[0]);
-  __syncthreads();
-  int n = sg[0][K];
-  uint64_t w0[ITEMS], w1[ITEMS];
-  int sp[ITEMS];
-  if (n <= kCap) kw_keys_issue<ITEMS>(sb[0], sg[0], K, n, w0, w1, sp);
-  for (int t = 0;; t ^= 1) {
-    if (n <= kCap) kw_keys_write<ITEMS>(buf, n, w0, w1, sp, kd.bad_layout);
-    const int64_t next = cell + wx;
-    const bool more = next < hi;  // uniform
-    int gn = 0, Kn = 0;
-    if (more) {
-      int cn, ncn, r0n;
-      kw_locate(kd, next, gn, cn, ncn, r0n, Kn);
-      kw_slices(kd, cn, ncn, r0n, Kn, sg[t ^ 1], sb[t ^ 1], &s_start[t ^ 1]);
-    }
-    __syncthreads();  // this cell's keys in LDS, the next cell's tables published
-    const int nn = more ? sg[t ^ 1][Kn] : 0;
-    if (more && nn <= kCap) kw_keys_issue<ITEMS>(sb[t ^ 1], sg[t ^ 1], Kn, nn, w0, w1, sp);
-    uint8_t* obase = out + (kd.group_out[g] + s_start[t]) * kTeraRecordBytes;
-    if (n > kCap) {  // uniform
-      if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
-      if (threadIdx.x < 64) kw_pq(kd, sb[t], sg[t], K, n, obase);
-    } else {
-      kw_f3<ITEMS, WAVEF3>(buf, sg[t], K, n);
-      kw_f4(sb[t], buf, n, obase);
-    }
-    if (!more) break;
-    __syncthreads();  // buf and table set t are free for the next cell
-    cell = next;
-    g = gn;
-    K = Kn;
-    n = nn;
   }
 }
 
@@ -650,72 +465,37 @@ void launch_split_sampled(uint8_t* const* bases, const int64_t* nrec, const Elem
 int kway_cap_supported(int cap) { return cap == 2048 || cap == 1792 || cap == 1536 || cap == 1024 || cap == 512; }
 
 namespace {
-template <int ITEMS, bool WAVEF3>
-void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s, bool pipe) {
+template <int ITEMS>
+void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
   const size_t elems = sizeof(Elem) * (size_t)(ITEMS * 256);
   auto tables = [](int k) { return (size_t)k * sizeof(void*) + (size_t)(k + 1) * sizeof(int); };
-  auto tables2 = [](int k) { return 2 * ((size_t)k * sizeof(void*) + (size_t)((k + 2) & ~1) * sizeof(int)); };
   if (kd.kmax < 1 || kd.kmax > kKwMaxRuns) throw std::runtime_error("kway: bad runs per group " + std::to_string(kd.kmax));
-  const void* fn = pipe ? reinterpret_cast<const void*>(kway_pipe_kernel<ITEMS, WAVEF3>)
-                        : reinterpret_cast<const void*>(kway_tile_kernel<ITEMS, WAVEF3>);
-  const size_t lds = (elems + (pipe ? tables2(kd.kmax) : tables(kd.kmax)) + 15) & ~(size_t)15;
-  static std::once_flag once[2];
-  static hipError_t attr[2] = {hipSuccess, hipSuccess};
-  static int resident[2] = {0, 0};  // workgroups per CU at the largest table size (pipe grid)
-  const int v = pipe ? 1 : 0;
-  std::call_once(once[v], [&] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
-    const size_t max_lds = elems + (pipe ? tables2(kKwMaxRuns) : tables(kKwMaxRuns)) + 16;
-    attr[v] = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
+  const size_t lds = (elems + tables(kd.kmax) + 15) & ~(size_t)15;
+  static std::once_flag once;
+  static hipError_t attr = hipSuccess;
+  std::call_once(once, [elems, tables] {  // dynamic LDS above the 64 KiB default (gfx950 has 160 KiB per CU)
+    attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kway_tile_kernel<ITEMS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(elems + tables(kKwMaxRuns) + 16));
     // some runtimes refuse the attribute for template kernels: harmless while a launch stays within the
     // default, and the error must not linger for the next hipGetLastError
-    if (attr[v] != hipSuccess) (void)hipGetLastError();
-    if (pipe) {
-      int per_cu = 0, dev = 0, cus = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, elems + tables2(32)) != hipSuccess ||
-          hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-        (void)hipGetLastError();
-        per_cu = 4;
-        cus = 256;
-      }
-      resident[v] = std::max(1, per_cu) * std::max(1, cus);
-    }
+    if (attr != hipSuccess) (void)hipGetLastError();
   });
-  if (attr[v] != hipSuccess && lds > (64u << 10))
-    throw std::runtime_error(std::string("kway: cannot raise the LDS limit: ") + hipGetErrorString(attr[v]));
-  if (pipe) {
-    const int64_t grid = std::min<int64_t>(ncells, resident[v]);
-    hipLaunchKernelGGL((kway_pipe_kernel<ITEMS, WAVEF3>), dim3((unsigned)grid), dim3(256), lds, s, kd, out, ncells);
-  } else {
-    hipLaunchKernelGGL((kway_tile_kernel<ITEMS, WAVEF3>), dim3((unsigned)ncells), dim3(256), lds, s, kd, out);
-  }
-}
-
-template <bool WAVEF3>
-void launch_kway_cap(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s, bool pipe) {
-  switch (kd.cap) {
-    case 2048: launch_kway<8, WAVEF3>(kd, ncells, out, s, pipe); break;
-    case 1792: launch_kway<7, WAVEF3>(kd, ncells, out, s, pipe); break;  // 28.4 KiB, 5 workgroups per CU
-    case 1536: launch_kway<6, WAVEF3>(kd, ncells, out, s, pipe); break;
-    case 1024: launch_kway<4, WAVEF3>(kd, ncells, out, s, pipe); break;
-    case 512: launch_kway<2, WAVEF3>(kd, ncells, out, s, pipe); break;
-    default: throw std::runtime_error("kway: unsupported cell capacity " + std::to_string(kd.cap));
-  }
-}
-
-bool env_flag(const char* name) {  // read per launch: tests flip these within one process
-  const char* e = std::getenv(name);
-  return e && std::atoi(e) != 0;
+  if (attr != hipSuccess && lds > (64u << 10))
+    throw std::runtime_error(std::string("kway: cannot raise the LDS limit: ") + hipGetErrorString(attr));
+  hipLaunchKernelGGL((kway_tile_kernel<ITEMS>), dim3((unsigned)ncells), dim3(256), lds, s, kd, out);
 }
 }  // namespace
 
 void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
   if (ncells <= 0) return;
-  const bool pipe = env_flag("UDA_KWAY_PIPE") && kd.prof == nullptr;  // phase stamps: one-cell kernel
-  if (env_flag("UDA_KWAY_WAVEF3"))
-    launch_kway_cap<true>(kd, ncells, out, s, pipe);
-  else
-    launch_kway_cap<false>(kd, ncells, out, s, pipe);
+  switch (kd.cap) {
+    case 2048: launch_kway<8>(kd, ncells, out, s); break;
+    case 1792: launch_kway<7>(kd, ncells, out, s); break;  // 28.4 KiB, 5 workgroups per CU
+    case 1536: launch_kway<6>(kd, ncells, out, s); break;
+    case 1024: launch_kway<4>(kd, ncells, out, s); break;
+    case 512: launch_kway<2>(kd, ncells, out, s); break;
+    default: throw std::runtime_error("kway: unsupported cell capacity " + std::to_string(kd.cap));
+  }
 }
 
 }  // namespace gpu

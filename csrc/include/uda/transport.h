@@ -103,6 +103,9 @@ std::unique_ptr<ServerTransport> make_loopback_server(const std::string& host);
 // the same port at different addresses, as providers on different hosts do.
 std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr = std::string());
 std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits);
+// A process hosting both a provider and reduce tasks (the node merge service): TCP fetches that name a
+// provider of this process (a local address and its port) are served in process, zero-copy.
+void set_tcp_local_bypass(bool on);
 
 // Fault injection for tests (env UDA_FAULT_FETCH=<n>: the n-th fetch fails; see uda/fault.h).
 bool fault_should_fail_fetch();

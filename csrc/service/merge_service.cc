@@ -22,6 +22,7 @@
 #include "uda/cmd.h"
 #include "uda/error.h"
 #include "uda/log.h"
+#include "uda/transport.h"
 
 namespace uda {
 
@@ -382,6 +383,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
 
 MergeService::MergeService(const std::string& path) : path_(path) {
   gpu::set_pinned_shareable(true);
+  set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider without a socket
   listen_fd_ = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (listen_fd_ < 0) throw UdaError(std::string("merge service: socket: ") + strerror(errno));
   ::unlink(path.c_str());

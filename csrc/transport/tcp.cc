@@ -6,6 +6,7 @@
 // RDMAServer.cc:537-631 folded into one frame). Credits: at most `credits` requests in flight per
 // connection (wqes_per_conn); the client connects with up to 5 tries (RECONNECT_TRIES).
 #include <arpa/inet.h>
+#include <ifaddrs.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -66,6 +67,33 @@ bool write_full(int fd, const void* p, size_t n) {
   return true;
 }
 
+// Providers of this process by (IPv4 listen address, 0 = any; port). A process that hosts both a
+// provider and reduce tasks (the node merge service, set_tcp_local_bypass) serves its tasks' fetches of
+// that provider in process: the provider writes straight into the fetch buffer, as on the loopback
+// transport, instead of moving every byte through a TCP socket pair.
+std::mutex g_local_mu;
+std::map<std::pair<uint32_t, int>, DataServer*>& local_servers() {
+  static auto* m = new std::map<std::pair<uint32_t, int>, DataServer*>();
+  return *m;
+}
+std::atomic<bool> g_local_bypass{false};
+
+bool local_ipv4(uint32_t ip_be) {
+  if ((ntohl(ip_be) >> 24) == 127) return true;
+  static const std::vector<uint32_t> mine = [] {
+    std::vector<uint32_t> v;
+    ifaddrs* ifa = nullptr;
+    if (getifaddrs(&ifa) == 0) {
+      for (ifaddrs* i = ifa; i; i = i->ifa_next)
+        if (i->ifa_addr && i->ifa_addr->sa_family == AF_INET)
+          v.push_back(reinterpret_cast<sockaddr_in*>(i->ifa_addr)->sin_addr.s_addr);
+      freeifaddrs(ifa);
+    }
+    return v;
+  }();
+  return std::find(mine.begin(), mine.end(), ip_be) != mine.end();
+}
+
 void tune(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
@@ -100,12 +128,22 @@ class TcpServer : public ServerTransport {
     socklen_t len = sizeof(a);
     getsockname(lfd_, (sockaddr*)&a, &len);
     port_ = ntohs(a.sin_port);
+    local_key_ = {a.sin_addr.s_addr, port_};
+    {
+      std::lock_guard<std::mutex> g(g_local_mu);
+      local_servers()[local_key_] = s;
+    }
     running_ = true;
     acceptor_ = std::thread([this] { accept_loop(); });
   }
 
   void stop() override {
     if (!running_.exchange(false)) return;
+    {
+      std::lock_guard<std::mutex> g(g_local_mu);
+      auto it = local_servers().find(local_key_);
+      if (it != local_servers().end() && it->second == server_) local_servers().erase(it);
+    }
     ::shutdown(lfd_, SHUT_RDWR);
     ::close(lfd_);
     if (acceptor_.joinable()) acceptor_.join();
@@ -189,6 +227,7 @@ class TcpServer : public ServerTransport {
 
   int port_;
   std::string bind_addr_;
+  std::pair<uint32_t, int> local_key_{0, 0};
   int credits_;
   int lfd_ = -1;
   std::atomic<bool> running_{false};
@@ -206,6 +245,19 @@ class TcpClient : public ClientTransport {
   ~TcpClient() override { close(); }
 
   void fetch(const std::string& host, const FetchRequest& req, uint8_t* dst, FetchDone done) override {
+    if (g_local_bypass.load()) {
+      if (DataServer* s = local_server(host)) {
+        if (fault_should_fail_fetch()) {
+          FetchAck a;
+          a.status = -5;
+          a.error = "injected fetch failure";
+          done(a);
+          return;
+        }
+        s->serve(req, dst, std::move(done));
+        return;
+      }
+    }
     std::shared_ptr<Conn> c;
     try {
       c = connect(host);
@@ -274,6 +326,41 @@ class TcpClient : public ClientTransport {
     bool dead = false;
     std::thread reader;
   };
+
+  // The provider of this process that `host_spec` names, if any (resolved once per host).
+  DataServer* local_server(const std::string& host_spec) {
+    std::pair<uint32_t, int> key{0, -1};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = resolved_.find(host_spec);
+      if (it != resolved_.end()) key = it->second;
+    }
+    if (key.second < 0) {
+      std::string host = host_spec;
+      int port = port_;
+      const auto colon = host_spec.rfind(':');
+      if (colon != std::string::npos) {
+        host = host_spec.substr(0, colon);
+        port = std::atoi(host_spec.c_str() + colon + 1);
+      }
+      addrinfo hints{}, *res = nullptr;
+      hints.ai_family = AF_INET;
+      hints.ai_socktype = SOCK_STREAM;
+      uint32_t ip = 0xFFFFFFFFu;  // unresolvable: never local
+      if (getaddrinfo(host.c_str(), nullptr, &hints, &res) == 0 && res) {
+        ip = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr.s_addr;
+        freeaddrinfo(res);
+      }
+      key = {ip, port};
+      std::lock_guard<std::mutex> g(mu_);
+      resolved_[host_spec] = key;
+    }
+    if (key.first == 0xFFFFFFFFu || !local_ipv4(key.first)) return nullptr;
+    std::lock_guard<std::mutex> g(g_local_mu);
+    auto it = local_servers().find(key);  // a provider listening on exactly that address
+    if (it == local_servers().end()) it = local_servers().find({0u, key.second});  // or on any
+    return it == local_servers().end() ? nullptr : it->second;
+  }
 
   std::shared_ptr<Conn> connect(const std::string& host_spec) {
     std::lock_guard<std::mutex> g(mu_);
@@ -363,8 +450,11 @@ class TcpClient : public ClientTransport {
   std::atomic<uint64_t> next_id_{1};
   std::mutex mu_;
   std::unordered_map<std::string, std::shared_ptr<Conn>> conns_;
+  std::unordered_map<std::string, std::pair<uint32_t, int>> resolved_;  // host spec -> (IPv4, port)
 };
 }  // namespace
+
+void set_tcp_local_bypass(bool on) { g_local_bypass.store(on); }
 
 std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr) {
   return std::make_unique<TcpServer>(port, credits > 0 ? credits : 256, bind_addr);
