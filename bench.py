@@ -111,10 +111,11 @@ def parse_args(argv=None):
     ap.add_argument("--node-gap", type=float, default=0.0,
                     help="--node: seconds between a wave's INITs and its FETCHes (reduce slow-start: the tasks start "
                          "while the maps still run); 0 = the tasks start when every map output is there")
-    ap.add_argument("--node-service", action="store_true",
+    ap.add_argument("--node-service", action=argparse.BooleanOptionalAction, default=True,
                     help="--node: the supplier process is also the node's merge service (every reduce task process "
                          "is a thin client whose NetMerger runs in the service: one GPU context, warm pools and "
-                         "the HBM store in one process; mapred.uda.gpu.merge.service)")
+                         "the HBM store in one process; mapred.uda.gpu.merge.service; the recommended deployment). "
+                         "--no-node-service: every task merges in its own fresh process")
     ap.add_argument("--node-slots", type=int, default=15,
                     help="--node: reduce task processes running at once (YARN containers of the node); the one-GPU "
                          "box allows 16 GPU processes, the provider is one of them")

@@ -142,7 +142,7 @@ def test_bench_node_shape_small(require_gpu, service):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--api", "--node", "--reducers", "3", "--rows-per-gpu",
-           "3000000", "--maps-per-gpu", "6", "--steps", "1", "--warmup", "1"] + (["--node-service"] if service else [])
+           "3000000", "--maps-per-gpu", "6", "--steps", "1", "--warmup", "1", "--node-service" if service else "--no-node-service"]
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])

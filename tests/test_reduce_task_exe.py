@@ -131,3 +131,27 @@ def test_merge_service_survives_a_dead_client_and_reports_failures(native, tmp_p
         assert rc == 0 and "merge_service" not in out["task"], out
     finally:
         prov.close()
+
+
+@pytest.mark.skipif(not os.access(EXE, os.X_OK), reason="uda_reduce_task not built")
+def test_task_fails_cleanly_when_the_merge_service_goes_away(native, tmp_path):
+    """The service's process ends while a hosted task waits for its remaining FETCHes: the task
+    process reports the failure (failureInUda -> Hadoop's vanilla shuffle) and exits instead of hanging."""
+    import time
+    port = _port()
+    prov, path, job, maps, ids = _service_provider(tmp_path, port)
+    try:
+        argv = [EXE, "-D", "mapred.uda.transport=tcp", "-D", "mapred.uda.merge.backend=cpu",
+                "-D", f"mapred.uda.gpu.merge.service={path}", "--", "-w", "256", "-r", str(port), "-a", "1", "-m",
+                "1", "-g", "/tmp", "-s", "1024"]
+        init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_000000_0", "0", str(1 << 20),
+                                      str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0", "0"])
+        p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        p.stdin.write(init + "\n" + native.form_cmd(FETCH, ["127.0.0.1", job, ids[0], "0"]) + "\n")
+        p.stdin.flush()
+        time.sleep(0.5)
+    finally:
+        prov.close()  # stops the merge service with the supplier
+    out, _ = p.communicate(timeout=60)
+    res = json.loads(out.strip().splitlines()[-1])
+    assert p.returncode == 1 and "merge service" in res["error"], res

@@ -44,8 +44,8 @@ RECIPES: dict[str, tuple[int, str]] = {
     "ipc4": (400, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --rows-per-gpu 150000000 --steps 3 --warmup 1"),
     "ipc8": (600, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
     "ipc4_host": (600, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --store host --rows-per-gpu 100000000 --steps 2 --warmup 1"),
-    "node": (600, f"{PY} bench.py --api --node --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
-    "node130": (700, f"{PY} bench.py --api --node --reducers 15 --steps 2 --warmup 1"),
+    "node": (600, f"{PY} bench.py --api --node --no-node-service --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "node130": (700, f"{PY} bench.py --api --node --no-node-service --reducers 15 --steps 2 --warmup 1"),
     "node_gap": (600, f"{PY} bench.py --api --node --reducers 15 --node-gap 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
