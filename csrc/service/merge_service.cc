@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <random>
 #include <set>
 
 #include "../consumer/reduce_task.h"
@@ -28,13 +29,17 @@ namespace uda {
 
 namespace {
 
-// ---- framing: u32 type, u32 payload length, payload; an fd may ride along (SCM_RIGHTS)
+// ---- framing: u32 type, u32 payload length, payload; an fd may ride along (SCM_RIGHTS). A task uses
+// two connections: the control one (HELLO with a session token, commands, configuration, stats, failures)
+// and a data one (REGION / DATA from the service, ACK back), so a merged buffer's hand-over costs one
+// wake-up on each side instead of a hop through the control reader.
 enum Msg : uint32_t {
   kHello = 1,      // c->s: startNative argv, '\0'-separated
   kCmd = 2,        // c->s: command string
   kConfReply = 3,  // c->s: u32 request id, value
   kAck = 4,        // c->s: i32 dataFromUda status
   kExit = 5,       // c->s: reduce task close
+  kDataHello = 6,  // c->s, on the task's second (data) connection: u64 session token
   kReady = 10,     // s->c: task started
   kRefused = 11,     // s->c: HELLO refused (reason)
   kConfReq = 12,   // s->c: u32 request id, key '\0' default
@@ -155,12 +160,13 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   std::condition_variable cv;
   std::map<uint32_t, std::string> conf_replies;
   uint32_t next_conf = 1;
-  std::deque<int32_t> acks;
   bool closed = false;  // the client went away
   // commands run on their own thread: INIT pulls configuration, which the reader thread answers
   std::deque<std::string> cmds;
   bool exit_requested = false;
   std::set<uint64_t> regions_sent;
+  uint64_t token = 0;
+  int dsock = -1;  // the data connection (attached by the acceptor; used by the delivering thread only)
   // bounce buffer for merged bytes outside shareable pinned memory (EOF tails, host-path buffers)
   int bounce_fd = -1;
   uint8_t* bounce = nullptr;
@@ -177,6 +183,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     if (bounce) munmap(bounce, bounce_bytes);
     if (bounce_fd >= 0) close(bounce_fd);
     if (sock >= 0) close(sock);
+    if (dsock >= 0) close(dsock);
   }
 
   bool send(uint32_t type, const std::string& p, int fd = -1) {
@@ -220,6 +227,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   }
 
   int deliver(const void* buf, int32_t len) {
+    if (dsock < 0 && !data_channel()) return -1;
     gpu::PinnedShare ps;
     uint64_t id;
     size_t off;
@@ -228,7 +236,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
         std::string r;
         put<uint64_t>(r, ps.id);
         put<uint64_t>(r, ps.region_bytes);
-        if (!send(kRegion, r, ps.fd)) return -1;
+        if (!send_msg(dsock, kRegion, r, ps.fd)) return -1;
         regions_sent.insert(ps.id);
       }
       id = ps.id;
@@ -245,14 +253,22 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     put<uint64_t>(d, id);
     put<uint64_t>(d, off);
     put<uint32_t>(d, (uint32_t)len);
-    if (!send(kData, d)) return -1;
+    if (!send_msg(dsock, kData, d)) return -1;
     // the buffer is reused once dataFromUda returns: wait for the client to have consumed it
+    uint32_t t;
+    std::string a;
+    int fd;
+    if (!recv_msg(dsock, &t, &a, &fd) || t != kAck) {
+      if (fd >= 0) close(fd);
+      return -1;
+    }
+    return get<int32_t>(a, 0);
+  }
+
+  bool data_channel() {  // the client attaches it right after HELLO
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return closed || !acks.empty(); });
-    if (acks.empty()) return -1;
-    const int32_t st = acks.front();
-    acks.pop_front();
-    return st;
+    cv.wait_for(lk, std::chrono::seconds(30), [&] { return closed || dsock >= 0; });
+    return dsock >= 0;
   }
 
   bool grow_bounce(size_t need) {
@@ -271,7 +287,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     std::string r;
     put<uint64_t>(r, bounce_id);
     put<uint64_t>(r, sz);
-    return send(kRegion, r, bounce_fd);
+    return send_msg(dsock, kRegion, r, bounce_fd);
   }
 
   void start(const std::vector<std::string>& args) {
@@ -368,8 +384,6 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
         cmds.push_back(std::move(p));
       } else if (t == kConfReply) {
         conf_replies[get<uint32_t>(p, 0)] = p.size() > 4 ? p.substr(4) : std::string();
-      } else if (t == kAck) {
-        acks.push_back(get<int32_t>(p, 0));
       } else if (t == kExit) {
         exit_requested = true;
       }
@@ -377,6 +391,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     }
     std::lock_guard<std::mutex> g(mu);
     closed = true;
+    if (dsock >= 0) ::shutdown(dsock, SHUT_RDWR);  // a delivery waiting for an ACK returns
     cv.notify_all();
   }
 };
@@ -449,10 +464,32 @@ void MergeService::accept_main() {
     uint32_t t;
     std::string p;
     int pfd;
-    if (!recv_msg(fd, &t, &p, &pfd) || t != kHello) {
+    if (!recv_msg(fd, &t, &p, &pfd) || (t != kHello && t != kDataHello) || p.size() < 8) {
       if (pfd >= 0) close(pfd);
       continue;  // ~Session closes the socket
     }
+    const uint64_t token = get<uint64_t>(p, 0);
+    if (t == kDataHello) {  // a task's data connection: attach it to its session
+      timeval none{0, 0};
+      (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+      std::shared_ptr<Session> owner;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto& x : live_)
+          if (x->token == token) owner = x;
+      }
+      if (owner) {
+        std::lock_guard<std::mutex> g(owner->mu);
+        if (owner->dsock < 0 && !owner->closed) {
+          owner->dsock = s->sock;
+          s->sock = -1;  // now the owner's
+          owner->cv.notify_all();
+        }
+      }
+      continue;
+    }
+    s->token = token;
+    p.erase(0, 8);
     for (size_t b = 0; b < p.size();) {
       const size_t e = p.find('\0', b);
       s->args.push_back(p.substr(b, e == std::string::npos ? std::string::npos : e - b));
@@ -472,8 +509,8 @@ void MergeService::accept_main() {
 
 struct RemoteReduceTask::Impl {
   Host* host;
-  int sock = -1;
-  std::thread reader;
+  int sock = -1, dsock = -1;
+  std::thread reader, data_reader;
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::pair<int32_t, std::string>> results;
@@ -483,17 +520,27 @@ struct RemoteReduceTask::Impl {
 
   ~Impl() {
     if (sock >= 0) ::shutdown(sock, SHUT_RDWR);
+    if (dsock >= 0) ::shutdown(dsock, SHUT_RDWR);
     if (reader.joinable()) reader.join();
+    if (data_reader.joinable()) data_reader.join();
     if (sock >= 0) close(sock);
+    if (dsock >= 0) close(dsock);
     for (auto& kv : regions) munmap(kv.second.first, kv.second.second);
   }
 
-  void read_loop() {
+  // The data connection: REGION (a shared mapping to add) and DATA (a merged buffer in one of them)
+  // from the service, in order; each DATA is handed to dataFromUda in place, then acknowledged. Waits
+  // briefly with a spin first: the next buffer usually follows the ACK within microseconds.
+  void data_loop() {
     for (;;) {
+      pollfd pf{dsock, POLLIN, 0};
+      const auto t0 = std::chrono::steady_clock::now();
+      while (::poll(&pf, 1, 0) == 0 && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(30)) {
+      }
       uint32_t t;
       std::string p;
       int fd;
-      if (!recv_msg(sock, &t, &p, &fd)) break;
+      if (!recv_msg(dsock, &t, &p, &fd)) return;
       if (t == kRegion) {
         const uint64_t id = get<uint64_t>(p, 0), bytes = get<uint64_t>(p, 8);
         if (fd >= 0) {
@@ -517,9 +564,20 @@ struct RemoteReduceTask::Impl {
           host->fail("merge service sent a buffer outside its shared regions");
         std::string a;
         put<int32_t>(a, st);
-        std::lock_guard<std::mutex> g(send_mu);
-        if (!send_msg(sock, kAck, a)) break;
-      } else if (t == kConfReq) {
+        if (!send_msg(dsock, kAck, a)) return;
+      } else if (fd >= 0) {
+        close(fd);
+      }
+    }
+  }
+
+  void read_loop() {
+    for (;;) {
+      uint32_t t;
+      std::string p;
+      int fd;
+      if (!recv_msg(sock, &t, &p, &fd)) break;
+      if (t == kConfReq) {
         if (fd >= 0) close(fd);
         const uint32_t id = get<uint32_t>(p, 0);
         const std::string kd = p.size() > 4 ? p.substr(4) : std::string();
@@ -583,13 +641,26 @@ RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<st
   sockaddr_un a = unix_addr(path);
   if (::connect(impl_->sock, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
     throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
+  uint64_t token = 0;
+  {
+    std::random_device rd;
+    token = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 20);
+  }
   std::string hello;
+  put<uint64_t>(hello, token);
   for (size_t i = 0; i < args.size(); ++i) {
     if (i) hello.push_back('\0');
     hello += args[i];
   }
   if (!send_msg(impl_->sock, kHello, hello)) throw UdaError("merge service " + path + ": HELLO failed");
+  impl_->dsock = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  std::string dh;
+  put<uint64_t>(dh, token);
+  if (impl_->dsock < 0 || ::connect(impl_->dsock, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 ||
+      !send_msg(impl_->dsock, kDataHello, dh))
+    throw UdaError("merge service " + path + ": data connection failed");
   Impl* im = impl_.get();
+  impl_->data_reader = std::thread([im] { im->data_loop(); });
   impl_->reader = std::thread([im] { im->read_loop(); });
   const auto r = impl_->wait_result();
   if (r.first != 0) {
