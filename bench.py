@@ -579,6 +579,8 @@ def run_api(args, ctx) -> int:
                     if args.workload == "secondary" else
                     "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
             "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),
+            "hbm_budget_gb": round(stats[-1].get("hbm_budget_bytes", 0) / 1e9, 2),
+            "hbm_budget_waits": int(stats[-1].get("hbm_budget_waits", 0)),
             "max_task_ws_gb": round(max(s["max_task_ws_bytes"] for s in stats) / 1e9, 3),
             "max_task_rounds": int(max(s["max_task_rounds"] for s in stats)),
             "config": {

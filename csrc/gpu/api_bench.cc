@@ -1,5 +1,6 @@
 // TeraSort through the C ABI with HBM-resident MOFs. See api_bench.h.
 #include "api_bench.h"
+#include "hbm_ledger.h"
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -547,6 +548,12 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   out["buffers"] = bufs;
   out["order_errors"] = validate ? oerr : -1;
   out["peak_hbm_bytes"] = (double)peak_used.load();
+  {
+    const HbmLedger::Stats ls = HbmLedger::get().stats(cfg_.device);
+    out["hbm_budget_bytes"] = (double)ls.budget;
+    out["hbm_ledger_peak_bytes"] = (double)ls.peak;
+    out["hbm_budget_waits"] = (double)ls.waits;
+  }
   out["max_task_ws_bytes"] = max_ws;
   out["max_task_rounds"] = max_rounds;
   if (info) *info = paths;

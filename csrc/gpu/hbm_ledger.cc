@@ -70,6 +70,7 @@ void HbmLedger::set_fake_device(int device, int64_t total_bytes, const std::stri
   std::lock_guard<std::mutex> g(mu_);
   Dev& d = devs_[device];
   d.init = true;
+  d.fake = true;
   d.key = key;
   d.total = total_bytes;
   d.budget = (int64_t)((double)total_bytes * kDefaultFraction);
@@ -121,6 +122,25 @@ int64_t HbmLedger::others_resident(Dev& d) {
   } catch (const std::exception&) {
     return 0;
   }
+}
+
+int64_t HbmLedger::device_used(int device, Dev& d) {
+  if (d.fake) return 0;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  size_t free_b = 0, total_b = 0;
+  const bool ok = (cur == device || hipSetDevice(device) == hipSuccess) && hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+  if (cur != device) (void)hipSetDevice(cur);
+  if (!ok) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  const int64_t u = (int64_t)(total_b - free_b);
+  d.device_peak = std::max(d.device_peak, u);
+  return u;
 }
 
 void HbmLedger::add_pool(Pool p) {
@@ -238,7 +258,10 @@ std::unique_ptr<HbmLedger::Reservation> HbmLedger::reserve(int device, int64_t b
   };
   for (;;) {
     if (d.queue.front() == me) {
-      const int64_t over = others(d) + d.used + d.reserved + bytes - d.budget;
+      // the ledger's own accounting, and what the device itself reports in use (the HIP runtime's and
+      // any untracked allocations count against the budget too) plus the reservations not yet allocated
+      const int64_t over = std::max(others(d) + d.used + d.reserved + bytes - d.budget,
+                                    device_used(device, d) + d.reserved + bytes - d.budget);
       if (over <= 0) break;
       lk.unlock();
       const int64_t freed = trim_pools(device, over);
@@ -310,6 +333,7 @@ HbmLedger::Stats HbmLedger::stats(int device) {
   s.node_bytes = others(d) + d.used + d.reserved;
   s.trimmed = d.trimmed;
   s.over = d.over;
+  s.device_peak = d.device_peak;
   s.waits = d.waits;
   s.wait_ms = d.wait_ms;
   return s;

@@ -100,6 +100,7 @@ class HbmLedger {
 
   struct Stats {
     int64_t budget = 0, used = 0, reserved = 0, peak = 0, resident = 0, node_bytes = 0, trimmed = 0, over = 0;
+    int64_t device_peak = 0;  // device-reported HBM in use, highest seen at a reservation
     int64_t waits = 0;
     double wait_ms = 0;
   };
@@ -113,7 +114,9 @@ class HbmLedger {
     bool init = false;
     std::string key;  // node-registry key (PCI bus id)
     int64_t total = 0, budget = 0;
+    bool fake = false;  // set_fake_device: no HIP device behind it
     int64_t used = 0, reserved = 0, peak = 0, resident = 0, trimmed = 0, over = 0, waits = 0;
+    int64_t device_peak = 0;  // HBM in use on the device (hipMemGetInfo) seen at reservations
     double wait_ms = 0;
     uint64_t next_ticket = 0;
     std::deque<uint64_t> queue;  // reservations waiting, FIFO
@@ -122,6 +125,7 @@ class HbmLedger {
   void publish(Dev& d);  // mu_ held: this process's bytes into the node registry
   int64_t others(Dev& d);  // mu_ held: bytes the node's other processes hold
   int64_t others_resident(Dev& d);  // mu_ held: resident bytes of the node's other processes
+  int64_t device_used(int device, Dev& d);  // HBM in use on the device, tracked or not (0 if unknown)
   int64_t trim_pools(int device, int64_t want);  // mu_ NOT held
   int64_t idle_bytes(int device);                // mu_ NOT held
 
