@@ -544,7 +544,10 @@ struct RemoteReduceTask::Impl {
       if (t == kRegion) {
         const uint64_t id = get<uint64_t>(p, 0), bytes = get<uint64_t>(p, 8);
         if (fd >= 0) {
-          void* m = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
+          // populated up front: faulting the pages in one at a time as the buffers arrive costs a
+          // minor fault per 4 KiB (shared memory pages are small unless the host enables THP for shmem)
+          void* m = mmap(nullptr, bytes, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, 0);
+          if (m != MAP_FAILED) (void)madvise(m, bytes, MADV_HUGEPAGE);
           close(fd);
           if (m != MAP_FAILED) {
             auto old = regions.find(id);

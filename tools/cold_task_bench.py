@@ -84,7 +84,8 @@ def node(args) -> int:
     del runs
     total = sum(len(d) - 2 for _, d, _, _ in mofs)
     expect = sum(c for _, _, _, c in mofs)
-    for svc in (1, 0):
+    child_env = {k: v for k, v in os.environ.items() if k != "UDA_HOST_TRACE"}  # the trace is this process's
+    for svc in ((1,) if args.service_only else (1, 0)):
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
             port = so.getsockname()[1]
@@ -104,7 +105,7 @@ def node(args) -> int:
                 argv += ["--", "-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
                 init = n.form_cmd(INIT, [str(args.maps), "job_cold", "attempt_cold_r_000000_0", "0", str(1 << 20),
                                          str(16 << 10), TEXT, "null", str(256 << 10), "0", "0"])
-                p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+                p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=child_env)
                 p.stdin.write(init + "\n")
                 p.stdin.flush()
                 time.sleep(args.gap)
@@ -122,6 +123,9 @@ def node(args) -> int:
                                   "fetch_to_eof_ms": res["fetch_to_eof_ms"], "exec_to_end_ms": res["exec_to_end_ms"],
                                   "fetch_ms": round(st.get("fetch_ms", -1), 1), "merge_ms": round(st.get("merge_ms", -1), 1),
                                   "prewarm_wait_ms": round(st.get("gpu_prewarm_wait_ms", 0), 1),
+                                  "fetch_to_first_data_ms": res["fetch_to_first_data_ms"],
+                                  **{k: round(st.get(k, -1), 1) for k in ("gpu_h2d_ms", "gpu_device_ms", "gpu_d2h_wait_ms",
+                                                                           "gpu_sink_ms")},
                                   "merge_path": st.get("merge_path")}), flush=True)
         finally:
             prov.close()
@@ -137,6 +141,7 @@ def main() -> int:
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--backend", default="gpu", help="--node: mapred.uda.merge.backend of the tasks")
+    ap.add_argument("--service-only", action="store_true", help="--node: only the merge-service trials")
     ap.add_argument("--node", action="store_true",
                     help="provider (and merge service) in this process, each task a fresh uda_reduce_task process")
     args = ap.parse_args()
