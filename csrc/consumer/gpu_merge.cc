@@ -383,6 +383,29 @@ class DevicePool {
     }
     return make();
   }
+  // The idle object that fits a task needing about `want` device bytes: the smallest one holding at
+  // least that much, else the largest. Handing a skewed task a small workspace makes it grow (and
+  // hipFree the old buffers, which synchronizes the device under every other task) while a large
+  // one sits idle or goes to a small task.
+  template <class Make>
+  std::unique_ptr<T> acquire_fit(int device, int64_t want, Make&& make) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = idle_[device];
+      if (!v.empty()) {
+        size_t best = 0;
+        for (size_t i = 1; i < v.size(); ++i) {
+          const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
+          const bool b_fits = b >= want, c_fits = c >= want;
+          if (c_fits ? (!b_fits || c < b) : (!b_fits && c > b)) best = i;
+        }
+        std::unique_ptr<T> o = std::move(v[best]);
+        v.erase(v.begin() + (long)best);
+        return o;
+      }
+    }
+    return make();
+  }
   void release(int device, std::unique_ptr<T> o) {
     std::lock_guard<std::mutex> g(mu_);
     auto& v = idle_[device];
@@ -1998,8 +2021,11 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     st_.bytes_delivered += len;
     return r;
   };
-  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
-                                                  device, [] { return std::make_unique<DeviceWorkspace>(); })};
+  int64_t in_bytes = 0;
+  for (const auto& p : parts) in_bytes += p->part_len;
+  const int64_t want_ws = (int64_t)(3.65 * (double)std::min<int64_t>(in_bytes, host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30)));
+  PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire_fit(
+                                                  device, want_ws, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
   HIP_PENDING("the merge workspace");

@@ -119,13 +119,21 @@ class FixedWsPool {
     for (const auto& w : free_[device]) n += w->device_bytes();
     return n;
   }
-  std::unique_ptr<FixedWs> acquire(int device) {
+  // the smallest idle workspace holding `want` bytes, else the largest (want < 0: any)
+  std::unique_ptr<FixedWs> acquire(int device, int64_t want = -1) {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto& v = free_[device];
       if (!v.empty()) {
-        auto w = std::move(v.back());
-        v.pop_back();
+        size_t best = v.size() - 1;
+        if (want >= 0)
+          for (size_t i = 0; i < v.size(); ++i) {
+            const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
+            const bool b_fits = b >= want, c_fits = c >= want;
+            if (c_fits ? (!b_fits || c < b) : (!b_fits && c > b)) best = i;
+          }
+        auto w = std::move(v[best]);
+        v.erase(v.begin() + (long)best);
         return w;
       }
     }
@@ -146,7 +154,7 @@ struct WsLease {
   int device;
   std::unique_ptr<FixedWs> w;
   bool clean = false;
-  explicit WsLease(int d) : device(d), w(FixedWsPool::get().acquire(d)) {}
+  explicit WsLease(int d, int64_t want = -1) : device(d), w(FixedWsPool::get().acquire(d, want)) {}
   ~WsLease() {
     if (clean) FixedWsPool::get().release(device, std::move(w));
   }
@@ -233,13 +241,13 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
     throw std::runtime_error(std::string("device reduce: HIP error pending on entry: ") + hipGetErrorString(pending));
   DeviceReduceStats st;
   const double t0 = now_ms();
-  WsLease lease(cfg.device);
-  FixedWs& ws = *lease.w;
-  hipStream_t s = ws.s;
   const int K = (int)runs.size();
   if (K > 65536) throw std::runtime_error("device reduce: more than 65536 runs");
   int64_t N = 0;
   for (const auto& r : runs) N += r.nrec;
+  WsLease lease(cfg.device, fixed_round_ws_bytes(std::min<int64_t>(cfg.round_bytes, N * kTeraRecordBytes), K));
+  FixedWs& ws = *lease.w;
+  hipStream_t s = ws.s;
   const int64_t buf_records = std::max<int64_t>(1, cfg.kv_buf_bytes / kTeraRecordBytes);
   const int64_t buf_bytes = buf_records * kTeraRecordBytes;
   const int64_t piece = std::max<int64_t>(1, cfg.piece_bytes / buf_bytes) * buf_bytes;
