@@ -139,6 +139,16 @@ T get(const std::string& s, size_t at) {
   return v;
 }
 
+// Wait up to `us` for `fd` to become readable by polling it, before the caller's blocking read: a
+// merged buffer's hand-over is a request/reply in tens of microseconds, less than two scheduler
+// wake-ups cost on a loaded node.
+void spin_readable(int fd, int us) {
+  pollfd pf{fd, POLLIN, 0};
+  const auto t0 = std::chrono::steady_clock::now();
+  while (::poll(&pf, 1, 0) == 0 && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(us)) {
+  }
+}
+
 sockaddr_un unix_addr(const std::string& path) {
   sockaddr_un a{};
   a.sun_family = AF_UNIX;
@@ -258,6 +268,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     uint32_t t;
     std::string a;
     int fd;
+    spin_readable(dsock, 200);  // the client copies a 1 MiB buffer in ~30-40 us
     if (!recv_msg(dsock, &t, &a, &fd) || t != kAck) {
       if (fd >= 0) close(fd);
       return -1;
@@ -533,10 +544,7 @@ struct RemoteReduceTask::Impl {
   // briefly with a spin first: the next buffer usually follows the ACK within microseconds.
   void data_loop() {
     for (;;) {
-      pollfd pf{dsock, POLLIN, 0};
-      const auto t0 = std::chrono::steady_clock::now();
-      while (::poll(&pf, 1, 0) == 0 && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(30)) {
-      }
+      spin_readable(dsock, 100);
       uint32_t t;
       std::string p;
       int fd;
