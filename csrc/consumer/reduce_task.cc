@@ -297,7 +297,7 @@ void ReduceTask::handle(const HadoopCmd& cmd) {
             UDA_LOG(kDebug, "fetch of %s skipped: restored from the LPQ checkpoint", f.map_id.c_str());
             break;
           }
-          const std::string had = it->second;  // discard_checkpoint() clears the map
+          const std::string had = it->second;
           discard_checkpoint();
           throw UdaError("map task re-executed since the LPQ checkpoint (" + had + " -> " + f.map_id +
                          "): checkpoint discarded, the next attempt starts clean");
@@ -461,16 +461,15 @@ std::string map_task_of(const std::string& attempt) {
   return attempt;
 }
 
-// The manifest and every LPQ file it lists are removed; nothing of the failed attempt is reused.
+// The manifest and every LPQ file it lists are removed; nothing of the failed attempt is reused. The
+// in-memory lists stay as they are: this runs on the host's command thread while the merge thread may
+// be reading them, and the task is failing anyway (the next attempt starts from the missing manifest).
 void ReduceTask::discard_checkpoint() {
   for (const auto& f : restored_files_) {
     ::unlink(f.c_str());
     ::unlink((f + ".idx").c_str());
   }
   ::unlink(checkpoint_path().c_str());
-  restored_files_.clear();
-  restored_maps_.clear();
-  restored_tasks_.clear();
 }
 
 std::string ReduceTask::checkpoint_path() const {

@@ -703,9 +703,16 @@ void RemoteReduceTask::exit() {
     if (impl_->exited) return;
     impl_->exited = true;
   }
-  if (!impl_->send(kExit, "")) return;
-  std::unique_lock<std::mutex> lk(impl_->mu);
-  impl_->cv.wait_for(lk, std::chrono::seconds(120), [&] { return impl_->have_stats || impl_->closed; });
+  if (impl_->send(kExit, "")) {
+    std::unique_lock<std::mutex> lk(impl_->mu);
+    impl_->cv.wait_for(lk, std::chrono::seconds(120), [&] { return impl_->have_stats || impl_->closed; });
+  }
+  // the session is over: nothing more comes on either connection, so the readers go now (the JVM
+  // keeps a closed reduce task's handle until it is collected)
+  ::shutdown(impl_->sock, SHUT_RDWR);
+  ::shutdown(impl_->dsock, SHUT_RDWR);
+  if (impl_->reader.joinable()) impl_->reader.join();
+  if (impl_->data_reader.joinable()) impl_->data_reader.join();
 }
 
 std::string RemoteReduceTask::stats_json() {
