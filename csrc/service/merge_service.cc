@@ -176,7 +176,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   bool exit_requested = false;
   std::set<uint64_t> regions_sent;
   uint64_t token = 0;
-  int dsock = -1;  // the data connection (attached by the acceptor; used by the delivering thread only)
+  std::atomic<int> dsock{-1};  // the data connection (attached by the acceptor, used by the delivering thread)
   // bounce buffer for merged bytes outside shareable pinned memory (EOF tails, host-path buffers)
   int bounce_fd = -1;
   uint8_t* bounce = nullptr;
@@ -193,7 +193,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     if (bounce) munmap(bounce, bounce_bytes);
     if (bounce_fd >= 0) close(bounce_fd);
     if (sock >= 0) close(sock);
-    if (dsock >= 0) close(dsock);
+    if (dsock.load() >= 0) close(dsock.load());
   }
 
   bool send(uint32_t type, const std::string& p, int fd = -1) {
@@ -278,8 +278,8 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
 
   bool data_channel() {  // the client attaches it right after HELLO
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait_for(lk, std::chrono::seconds(30), [&] { return closed || dsock >= 0; });
-    return dsock >= 0;
+    cv.wait_for(lk, std::chrono::seconds(30), [&] { return closed || dsock.load() >= 0; });
+    return dsock.load() >= 0;
   }
 
   bool grow_bounce(size_t need) {
@@ -402,7 +402,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     }
     std::lock_guard<std::mutex> g(mu);
     closed = true;
-    if (dsock >= 0) ::shutdown(dsock, SHUT_RDWR);  // a delivery waiting for an ACK returns
+    if (dsock.load() >= 0) ::shutdown(dsock.load(), SHUT_RDWR);  // a delivery waiting for an ACK returns
     cv.notify_all();
   }
 };
@@ -491,8 +491,8 @@ void MergeService::accept_main() {
       }
       if (owner) {
         std::lock_guard<std::mutex> g(owner->mu);
-        if (owner->dsock < 0 && !owner->closed) {
-          owner->dsock = s->sock;
+        if (owner->dsock.load() < 0 && !owner->closed) {
+          owner->dsock.store(s->sock);
           s->sock = -1;  // now the owner's
           owner->cv.notify_all();
         }
