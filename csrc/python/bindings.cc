@@ -632,6 +632,7 @@ PYBIND11_MODULE(_uda_native, m) {
     o["over"] = s.over;
     o["waits"] = s.waits;
     o["wait_ms"] = s.wait_ms;
+    o["device_peak"] = s.device_peak;
     return o;
   });
   // an idle pool of fake objects: trimmed by the ledger under pressure (returns the pool's id)

@@ -154,3 +154,27 @@ def test_bench_node_shape_small(require_gpu, service):
         ms = out["provider"]["merge_service"]
         assert t0.get("merge_service") is True and ms["sessions"] >= 6, ms
         assert ms["zero_copy_buffers"] > ms["bounced_buffers"], ms
+
+
+def test_hbm_budget_counts_untracked_device_memory(require_gpu, native):
+    """A reservation is checked against what the device reports in use, not only the ledger's own
+    allocations: HBM taken outside the ledger (here a torch tensor) leaves less room under the budget."""
+    import torch
+    d = 0
+    native.hbm_stats(d)  # initializes the device's ledger entry
+    free, total = torch.cuda.mem_get_info(d)
+    used = total - free
+    try:
+        native.hbm_configure(d, float(used + (6 << 30)))  # budget: what is in use now + 6 GiB
+        r = native.hbm_reserve(d, 2 << 30, 10.0)  # fits
+        del r
+        blob = torch.empty(5 << 30, dtype=torch.uint8, device=f"cuda:{d}")  # untracked 5 GiB
+        with pytest.raises(Exception, match="HBM"):
+            native.hbm_reserve(d, 2 << 30, 1.0)  # 5 + 2 > 6 GiB: waits, then gives up
+        del blob
+        torch.cuda.empty_cache()
+        r = native.hbm_reserve(d, 2 << 30, 10.0)  # room again once the untracked memory is gone
+        del r
+        assert native.hbm_stats(d)["device_peak"] >= used + (5 << 30)
+    finally:
+        native.hbm_configure(d, 0.0)  # back to the default fraction
