@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <poll.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/time.h>
@@ -408,6 +409,13 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
 };
 
 MergeService::MergeService(const std::string& path) : path_(path) {
+  // every shareable pinned allocation keeps its memfd open for the clients that will map it: allow
+  // the process as many descriptors as the host lets it have
+  rlimit nl{};
+  if (getrlimit(RLIMIT_NOFILE, &nl) == 0 && nl.rlim_cur < nl.rlim_max) {
+    nl.rlim_cur = nl.rlim_max;
+    (void)setrlimit(RLIMIT_NOFILE, &nl);
+  }
   gpu::set_pinned_shareable(true);
   set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider without a socket
   listen_fd_ = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
