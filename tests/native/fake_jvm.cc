@@ -68,6 +68,7 @@ struct Jvm {
   std::string out;
   bool eof = false;
   std::atomic<int> fetch_over{0}, buffers{0}, failures{0}, logs{0}, unattached_calls{0}, non_direct{0};
+  std::atomic<int> hosted{0};  // log lines saying the NetMerger runs in the merge service
   std::atomic<int> attaches{0}, detaches{0}, bad_slot{0};
   std::atomic<long> live_local{0};
   Obj bridge_cls{kClass, "com/mellanox/hadoop/mapred/UdaBridge"};
@@ -189,6 +190,8 @@ void call_void(Table*, Obj*, void* mid, const jvalue* a) {
     }
     case 5:
       J.logs++;
+      if (a && a[0].l && static_cast<Obj*>(a[0].l)->str.find("hosted by the merge service") != std::string::npos)
+        J.hosted++;
       break;
     case 6: {
       std::lock_guard<std::mutex> lk(J.mu);
@@ -298,6 +301,7 @@ int main(int argc, char** argv) {
   install();
   t_attached = true;  // this is the "Java main thread"
   std::vector<std::string> prov_args, cons_args, cmds, bad_cmds;
+  int log_level = 3;
   std::string exit_cmd, out_path;
   {
     std::ifstream in(argv[2]);
@@ -315,6 +319,7 @@ int main(int argc, char** argv) {
       else if (tag == "bad") bad_cmds.push_back(rest);
       else if (tag == "exit") exit_cmd = rest;
       else if (tag == "out") out_path = rest;
+      else if (tag == "loglevel") log_level = std::atoi(rest.c_str());
       else if (tag == "conf") {
         std::istringstream cs(rest);
         std::string k, v;
@@ -355,12 +360,12 @@ int main(int argc, char** argv) {
   }
   Table* env = &g_env;
   const jint ver = on_load(&g_vm, nullptr);
-  set_log(env, &J.bridge_cls, 3);
+  set_log(env, &J.bridge_cls, log_level);
   int exceptions = 0, unexpected_exceptions = 0;
   std::string first_exception;
-  jint rc = start(env, &J.bridge_cls, 0, string_array(prov_args), 3, 0);
+  jint rc = start(env, &J.bridge_cls, 0, string_array(prov_args), log_level, 0);
   if (!t_exception.empty()) unexpected_exceptions++, first_exception = t_exception, t_exception.clear();
-  rc |= start(env, &J.bridge_cls, 1, string_array(cons_args), 3, 0);
+  rc |= start(env, &J.bridge_cls, 1, string_array(cons_args), log_level, 0);
   if (!t_exception.empty()) unexpected_exceptions++, first_exception = t_exception, t_exception.clear();
   for (auto& b : bad_cmds) {
     do_cmd(env, &J.bridge_cls, new Obj{kString, b});
@@ -392,10 +397,10 @@ int main(int argc, char** argv) {
   printf("{\"onload_version\":%d,\"start_rc\":%d,\"finished\":%s,\"fetch_over\":%d,\"buffers\":%d,\"bytes\":%zu,"
          "\"failures\":%d,\"logs\":%d,\"bad_cmd_exceptions\":%d,\"unexpected_exceptions\":%d,\"attaches\":%d,"
          "\"detaches\":%d,\"unattached_calls\":%d,\"non_direct\":%d,\"bad_slot\":%d,\"live_local_refs\":%ld,"
-         "\"first_exception\":\"%s\"}\n",
+         "\"hosted\":%d,\"first_exception\":\"%s\"}\n",
          ver, rc, finished ? "true" : "false", J.fetch_over.load(), J.buffers.load(), J.out.size(), J.failures.load(),
          J.logs.load(), exceptions, unexpected_exceptions, J.attaches.load(), J.detaches.load(),
-         J.unattached_calls.load(), J.non_direct.load(), J.bad_slot.load(), J.live_local.load(),
+         J.unattached_calls.load(), J.non_direct.load(), J.bad_slot.load(), J.live_local.load(), J.hosted.load(),
          first_exception.c_str());
   fflush(stdout);
   // libuda's worker threads are joined by reduce exit / EXIT; leave the library loaded (as a JVM does)

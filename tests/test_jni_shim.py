@@ -32,12 +32,15 @@ def fake_jvm(tmp_path_factory, native):  # `native` makes sure the build is pres
     return exe
 
 
-def _manifest(native, path, mofs, maps, job, reduce_id, extra_fetch=(), codec=None, kv_buf=64 << 10):
+def _manifest(native, path, mofs, maps, job, reduce_id, extra_fetch=(), codec=None, kv_buf=64 << 10, service=None):
     lines = [
         "conf mapred.uda.transport loopback",
         "conf mapred.uda.loopback.host *",
         f"conf mapred.uda.kv.buf.size {kv_buf}",
     ]
+    if service:  # the provider hosts the merge service and the NetMerger is its client
+        lines.append(f"conf mapred.uda.gpu.merge.service {service}")
+        lines.append("loglevel 4")  # info: the start logs where the NetMerger runs
     for a in ["-w", "256", "-r", "9011", "-m", "1", "-g", "/tmp", "-s", "1024"]:
         lines.append(f"parg {a}")
     for a in ["-w", "256", "-r", "9011", "-a", "1", "-m", "1", "-g", "/tmp", "-s", "64"]:
@@ -63,8 +66,10 @@ def _run(fake_jvm, manifest):
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("codec", [None, "snappy"])
-def test_jni_reduce_through_fake_jvm(native, fake_jvm, tmp_path, codec):
+@pytest.mark.parametrize("codec,service", [(None, False), ("snappy", False), (None, True)])
+def test_jni_reduce_through_fake_jvm(native, fake_jvm, tmp_path, codec, service):
+    """With the merge service, dataFromUda / fetchOverMessage come from the client's socket threads:
+    the shim must attach them like any other native thread."""
     maps = datagen.secondary_sort(num_maps=9, reducers=2, rows_per_map=400, seed=31)
     job = "job_jni_" + (codec or "raw")
     mofs = {}
@@ -72,7 +77,7 @@ def test_jni_reduce_through_fake_jvm(native, fake_jvm, tmp_path, codec):
         mid = f"attempt_{job}_m_{i:06d}_0"
         mofs[mid] = write_mof(str(tmp_path), mid, parts, codec=codec)
     m = str(tmp_path / "manifest.txt")
-    _manifest(native, m, mofs, maps, job, 1, codec=codec)
+    _manifest(native, m, mofs, maps, job, 1, codec=codec, service=str(tmp_path / "svc.sock") if service else None)
     st = _run(fake_jvm, m)
     assert st["onload_version"] == 0x00010004
     assert st["start_rc"] == 0 and st["finished"] and st["failures"] == 0
@@ -82,6 +87,7 @@ def test_jni_reduce_through_fake_jvm(native, fake_jvm, tmp_path, codec):
     assert st["live_local_refs"] == 0
     assert st["attaches"] >= 1 and st["detaches"] == st["attaches"]
     assert st["fetch_over"] >= 1 and st["buffers"] >= 2
+    assert st["hosted"] == (1 if service else 0), st
     got = decode_stream(open(m + ".out", "rb").read())
     want = sorted((kv for mp in maps for kv in mp[1]), key=datagen.sort_key(datagen.TEXT))
     kf = datagen.sort_key(datagen.TEXT)
