@@ -383,10 +383,10 @@ class DevicePool {
     }
     return make();
   }
-  // The idle object that fits a task needing about `want` device bytes: the smallest one holding at
-  // least that much, else the largest. Handing a skewed task a small workspace makes it grow (and
-  // hipFree the old buffers, which synchronizes the device under every other task) while a large
-  // one sits idle or goes to a small task.
+  // The idle object closest in size to what a task needs (about `want` device bytes; ties go to the
+  // larger). Handing a skewed task a small workspace makes it grow (and hipFree the old buffers, which
+  // synchronizes the device under every other task) while a large one sits idle or goes to a small
+  // task; a small task taking the largest one does the same to the next skewed task.
   template <class Make>
   std::unique_ptr<T> acquire_fit(int device, int64_t want, Make&& make) {
     {
@@ -396,8 +396,8 @@ class DevicePool {
         size_t best = 0;
         for (size_t i = 1; i < v.size(); ++i) {
           const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
-          const bool b_fits = b >= want, c_fits = c >= want;
-          if (c_fits ? (!b_fits || c < b) : (!b_fits && c > b)) best = i;
+          const int64_t db = b > want ? b - want : want - b, dc = c > want ? c - want : want - c;
+          if (dc < db || (dc == db && c > b)) best = i;
         }
         std::unique_ptr<T> o = std::move(v[best]);
         v.erase(v.begin() + (long)best);

@@ -119,7 +119,7 @@ class FixedWsPool {
     for (const auto& w : free_[device]) n += w->device_bytes();
     return n;
   }
-  // the smallest idle workspace holding `want` bytes, else the largest (want < 0: any)
+  // the idle workspace closest in size to `want` bytes, ties to the larger (want < 0: any)
   std::unique_ptr<FixedWs> acquire(int device, int64_t want = -1) {
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -129,8 +129,8 @@ class FixedWsPool {
         if (want >= 0)
           for (size_t i = 0; i < v.size(); ++i) {
             const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
-            const bool b_fits = b >= want, c_fits = c >= want;
-            if (c_fits ? (!b_fits || c < b) : (!b_fits && c > b)) best = i;
+            const int64_t db = b > want ? b - want : want - b, dc = c > want ? c - want : want - c;
+            if (dc < db || (dc == db && c > b)) best = i;
           }
         auto w = std::move(v[best]);
         v.erase(v.begin() + (long)best);
