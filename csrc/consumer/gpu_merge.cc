@@ -84,6 +84,7 @@ struct SpillRun {
 // allocated once at the high-water mark instead of per merge (hipMalloc/hipFree of GBs costs ms and
 // hipFree synchronizes the device).
 struct DeviceWorkspace {
+  int64_t pool_key = 0;  // input bytes of the task that last used it (DevicePool::acquire_fit)
   gpu::DeviceBuffer in, out, packed, out2;  // out2: second output of the generic key-range rounds
   gpu::GenericMerger merger;
   gpu::DeviceBlockDecoder decoder;
@@ -383,28 +384,33 @@ class DevicePool {
     }
     return make();
   }
-  // The idle object closest in size to what a task needs (about `want` device bytes; ties go to the
-  // larger). Handing a skewed task a small workspace makes it grow (and hipFree the old buffers, which
-  // synchronizes the device under every other task) while a large one sits idle or goes to a small
-  // task; a small task taking the largest one does the same to the next skewed task.
+  // The idle object last used by the task most like this one: the closest pool_key (the input bytes of
+  // the task that used it; ties to the larger object), then tagged with `key`. The jobs of a wave repeat
+  // their shapes, so a skewed task gets back the workspace it grew before. Handing it a small one makes
+  // it grow again (and hipFree the old buffers, which synchronizes the device under every other task),
+  // and what its size promises is no guide: tasks of any input size beyond one round size their
+  // workspaces to the round (config #5, 100 GB: 16.6 GB/s last-in, 20-30 by size, see BENCHMARKS.md).
   template <class Make>
-  std::unique_ptr<T> acquire_fit(int device, int64_t want, Make&& make) {
+  std::unique_ptr<T> acquire_fit(int device, int64_t key, Make&& make) {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto& v = idle_[device];
       if (!v.empty()) {
         size_t best = 0;
         for (size_t i = 1; i < v.size(); ++i) {
-          const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
-          const int64_t db = b > want ? b - want : want - b, dc = c > want ? c - want : want - c;
-          if (dc < db || (dc == db && c > b)) best = i;
+          const int64_t b = v[best]->pool_key, c = v[i]->pool_key;
+          const int64_t db = b > key ? b - key : key - b, dc = c > key ? c - key : key - c;
+          if (dc < db || (dc == db && v[i]->device_bytes() > v[best]->device_bytes())) best = i;
         }
         std::unique_ptr<T> o = std::move(v[best]);
         v.erase(v.begin() + (long)best);
+        o->pool_key = key;
         return o;
       }
     }
-    return make();
+    std::unique_ptr<T> o = make();
+    o->pool_key = key;
+    return o;
   }
   void release(int device, std::unique_ptr<T> o) {
     std::lock_guard<std::mutex> g(mu_);
@@ -2023,9 +2029,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   };
   int64_t in_bytes = 0;
   for (const auto& p : parts) in_bytes += p->part_len;
-  const int64_t want_ws = (int64_t)(3.65 * (double)std::min<int64_t>(in_bytes, host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30)));
   PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire_fit(
-                                                  device, want_ws, [] { return std::make_unique<DeviceWorkspace>(); })};
+                                                  device, in_bytes, [] { return std::make_unique<DeviceWorkspace>(); })};
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
   HIP_PENDING("the merge workspace");

@@ -52,6 +52,7 @@ struct Events {
 // whole device, so allocating and freeing per task made 16 concurrent tasks stall one another at
 // every task end. Buffers only grow; a workspace whose task failed is dropped, not reused.
 struct FixedWs {
+  int64_t pool_key = 0;  // input bytes of the task that last used it (FixedWsPool::acquire)
   std::unique_ptr<DeviceMerger> merger;
   DeviceBuffer out[2];
   DeviceBuffer d_bases, d_nrec, d_soff, d_samp, d_bset, d_out, d_bounds, d_runs, flag;
@@ -119,25 +120,29 @@ class FixedWsPool {
     for (const auto& w : free_[device]) n += w->device_bytes();
     return n;
   }
-  // the idle workspace closest in size to `want` bytes, ties to the larger (want < 0: any)
-  std::unique_ptr<FixedWs> acquire(int device, int64_t want = -1) {
+  // the idle workspace last used by the task most like this one (closest pool_key = input bytes; ties
+  // to the larger; key < 0: any), as DevicePool::acquire_fit in gpu_merge.cc
+  std::unique_ptr<FixedWs> acquire(int device, int64_t key = -1) {
     {
       std::lock_guard<std::mutex> g(mu_);
       auto& v = free_[device];
       if (!v.empty()) {
         size_t best = v.size() - 1;
-        if (want >= 0)
+        if (key >= 0)
           for (size_t i = 0; i < v.size(); ++i) {
-            const int64_t b = v[best]->device_bytes(), c = v[i]->device_bytes();
-            const int64_t db = b > want ? b - want : want - b, dc = c > want ? c - want : want - c;
-            if (dc < db || (dc == db && c > b)) best = i;
+            const int64_t b = v[best]->pool_key, c = v[i]->pool_key;
+            const int64_t db = b > key ? b - key : key - b, dc = c > key ? c - key : key - c;
+            if (dc < db || (dc == db && v[i]->device_bytes() > v[best]->device_bytes())) best = i;
           }
         auto w = std::move(v[best]);
         v.erase(v.begin() + (long)best);
+        if (key >= 0) w->pool_key = key;
         return w;
       }
     }
-    return std::make_unique<FixedWs>();
+    auto w = std::make_unique<FixedWs>();
+    if (key >= 0) w->pool_key = key;
+    return w;
   }
   void release(int device, std::unique_ptr<FixedWs> w) {
     std::lock_guard<std::mutex> g(mu_);
@@ -154,7 +159,7 @@ struct WsLease {
   int device;
   std::unique_ptr<FixedWs> w;
   bool clean = false;
-  explicit WsLease(int d, int64_t want = -1) : device(d), w(FixedWsPool::get().acquire(d, want)) {}
+  explicit WsLease(int d, int64_t key = -1) : device(d), w(FixedWsPool::get().acquire(d, key)) {}
   ~WsLease() {
     if (clean) FixedWsPool::get().release(device, std::move(w));
   }
@@ -245,7 +250,7 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   if (K > 65536) throw std::runtime_error("device reduce: more than 65536 runs");
   int64_t N = 0;
   for (const auto& r : runs) N += r.nrec;
-  WsLease lease(cfg.device, fixed_round_ws_bytes(std::min<int64_t>(cfg.round_bytes, N * kTeraRecordBytes), K));
+  WsLease lease(cfg.device, N * kTeraRecordBytes);
   FixedWs& ws = *lease.w;
   hipStream_t s = ws.s;
   const int64_t buf_records = std::max<int64_t>(1, cfg.kv_buf_bytes / kTeraRecordBytes);
