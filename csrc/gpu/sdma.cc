@@ -171,6 +171,7 @@ struct SharedRegion {
   size_t len;
   int fd;
   uint64_t id;
+  int node;  // NUMA node the pages were bound to (-1: any)
 };
 std::atomic<bool> g_shareable{false};
 std::atomic<uint64_t> g_next_share_id{1};
@@ -236,7 +237,8 @@ void* register_fresh_pages(size_t bytes, int node) {
   }
   std::lock_guard<std::mutex> g(g_pin_mu);
   pinned_maps()[a] = {m, maplen};
-  if (fd >= 0) shared_regions()[(uintptr_t)a] = SharedRegion{len, fd, g_next_share_id.fetch_add(1)};
+  if (fd >= 0)
+    shared_regions()[(uintptr_t)a] = SharedRegion{len, fd, g_next_share_id.fetch_add(1), node >= 0 && node < 64 ? node : -1};
   return a;
 }
 }  // namespace
@@ -292,6 +294,7 @@ bool pinned_share_of(const void* p, size_t len, PinnedShare* out) {
   out->id = it->second.id;
   out->offset = a - it->first;
   out->region_bytes = it->second.len;
+  out->numa_node = it->second.node;
   return true;
 }
 

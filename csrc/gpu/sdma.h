@@ -104,6 +104,7 @@ struct PinnedShare {
   int fd = -1;
   uint64_t id = 0;
   size_t offset = 0, region_bytes = 0;
+  int numa_node = -1;  // where the pages live (-1: unknown)
 };
 void set_pinned_shareable(bool on);
 bool pinned_share_of(const void* p, size_t len, PinnedShare* out);

@@ -44,7 +44,7 @@ enum Msg : uint32_t {
   kReady = 10,     // s->c: task started
   kRefused = 11,     // s->c: HELLO refused (reason)
   kConfReq = 12,   // s->c: u32 request id, key '\0' default
-  kRegion = 13,    // s->c: u64 id, u64 bytes + the memfd
+  kRegion = 13,    // s->c: u64 id, u64 bytes, i32 NUMA node + the memfd
   kData = 14,      // s->c: u64 region id, u64 offset, u32 length
   kFetchOver = 15, // s->c
   kFail = 16,      // s->c: reason (failureInUda)
@@ -247,6 +247,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
         std::string r;
         put<uint64_t>(r, ps.id);
         put<uint64_t>(r, ps.region_bytes);
+        put<int32_t>(r, ps.numa_node);
         if (!send_msg(dsock, kRegion, r, ps.fd)) return -1;
         regions_sent.insert(ps.id);
       }
@@ -299,6 +300,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     std::string r;
     put<uint64_t>(r, bounce_id);
     put<uint64_t>(r, sz);
+    put<int32_t>(r, -1);
     return send_msg(dsock, kRegion, r, bounce_fd);
   }
 
@@ -529,6 +531,7 @@ void MergeService::accept_main() {
 struct RemoteReduceTask::Impl {
   Host* host;
   int sock = -1, dsock = -1;
+  int bound_node = -1;  // NUMA node the data thread is bound to (the delivery rings' node)
   std::thread reader, data_reader;
   std::mutex mu;
   std::condition_variable cv;
@@ -559,6 +562,13 @@ struct RemoteReduceTask::Impl {
       if (!recv_msg(dsock, &t, &p, &fd)) return;
       if (t == kRegion) {
         const uint64_t id = get<uint64_t>(p, 0), bytes = get<uint64_t>(p, 8);
+        const int node = p.size() >= 20 ? get<int32_t>(p, 16) : -1;
+        if (node >= 0 && node != bound_node) {
+          // dataFromUda copies out of these pages: run where they live, as the in-process delivery
+          // thread does (gpu_merge.cc binds it to the GPU's node)
+          gpu::bind_thread_to_numa(node);
+          bound_node = node;
+        }
         if (fd >= 0) {
           // populated up front: faulting the pages in one at a time as the buffers arrive costs a
           // minor fault per 4 KiB (shared memory pages are small unless the host enables THP for shmem)
