@@ -406,19 +406,20 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
           va = src[min(a0, n - 1)];
           vb = src[min(a1, n - 1)];
         }
-        const bool take_a = ib >= lb || (ia < la && kle(va, vb));
-        Elem v;  // field-wise select: a select of the two structs becomes a scratch slot + indexed load
-        v.hi = take_a ? va.hi : vb.hi;
-        v.lo = take_a ? va.lo : vb.lo;
-        held_hi[k] = v.hi;
-        held_lo[k] = v.lo;
-        if (take_a) {
-          ++ia;
-          va = src[min(a0 + ia, n - 1)];
-        } else {
-          ++ib;
-          vb = src[min(a1 + ib, n - 1)];
-        }
+        // straight-line step: bitwise conditions, the advancing side's next index selected, one
+        // ds_read_b128 for the whole wave (as two exec-masked reads behind branches: same speed, more
+        // LDS instructions; profiles/r4_kway_one_read_ab.md). Field-wise selects: a select of the two
+        // structs becomes a scratch slot + indexed load.
+        const bool take_a = (ib >= lb) | ((ia < la) & kle(va, vb));
+        held_hi[k] = take_a ? va.hi : vb.hi;
+        held_lo[k] = take_a ? va.lo : vb.lo;
+        ia += take_a ? 1 : 0;
+        ib += take_a ? 0 : 1;
+        const Elem nv = src[min(take_a ? a0 + ia : a1 + ib, n - 1)];
+        va.hi = take_a ? nv.hi : va.hi;
+        va.lo = take_a ? nv.lo : va.lo;
+        vb.hi = take_a ? vb.hi : nv.hi;
+        vb.lo = take_a ? vb.lo : nv.lo;
       }
     }
     __syncthreads();
