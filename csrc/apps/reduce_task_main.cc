@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
     }
   }
   host.conf["mapred.uda.kv.buf.size"] = std::to_string(kv_buf);
-  uda::gpu::J2CSink sink(1, kv_buf, false);
+  uda::gpu::J2CSink sink(1, kv_buf);  // UDA_J2C_THREADS=1: copy on the delivering thread, walk on this one
   sink.set_check_order(check_order);
   sink.set_key_kind(1);
   sink.set_on_eof([&host](int) {
