@@ -477,6 +477,7 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
                    "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
         "node": {"slots": args.node_slots, "gap_s": args.node_gap, "merge_service": bool(args.service_path),
                  "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
+                 "step_ms": [round(st["wall_ms"], 1) for st in stats],
                  "task_ms_median": stats[-1]["task_ms_median"],
                  "timeline_ms": {"columns": ["exec", "first_fetch", "first_data", "eof", "end"],
                                  "tasks": stats[-1]["timeline"]}},
@@ -606,6 +607,7 @@ def run_api(args, ctx) -> int:
             "mof_files": bool(args.mof_dir),
             "codec": args.api_codec,
             "compressed_gb": round(b.compressed_bytes / 1e9, 2) if args.api_codec else None,
+            "step_ms": [round(float(s["wall_ms"]), 1) for s in stats],  # this rank's timed steps
             "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
             # --mof-dir: the first step includes every MOF file's load into the provider's HBM store (a
             # job loads each MOF once): this is the rate a job sees
