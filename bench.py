@@ -608,6 +608,9 @@ def run_api(args, ctx) -> int:
             "codec": args.api_codec,
             "compressed_gb": round(b.compressed_bytes / 1e9, 2) if args.api_codec else None,
             "step_ms": [round(float(s["wall_ms"]), 1) for s in stats],  # this rank's timed steps
+            "step_hbm_wait_ms": [[round(float(s.get("hbm_wait_ms_sum", 0)), 1), round(float(s.get("hbm_wait_ms_max", 0)), 1)]
+                                 for s in stats],  # [sum over the tasks, slowest task]
+            "step_task_ms_max": [round(float(s.get("task_total_ms_max", 0)), 1) for s in stats],
             "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
             # --mof-dir: the first step includes every MOF file's load into the provider's HBM store (a
             # job loads each MOF once): this is the rate a job sees

@@ -505,7 +505,7 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   }
   const double t1 = now_ms();
   std::string paths;
-  double max_ws = 0, max_rounds = 0;
+  double max_ws = 0, max_rounds = 0, hbm_wait_sum = 0, hbm_wait_max = 0, task_total_max = 0;
   for (int r = 0; r < R; ++r) {
     if (!handles[r]) continue;
     (void)uda_reduce_exit(handles[r]);  // joins the merge thread: its stats are final after this
@@ -518,6 +518,10 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
       };
       max_ws = std::max(max_ws, num("\"gpu_ws_bytes\":"));
       max_rounds = std::max(max_rounds, num("\"rpq_rounds\":"));
+      const double wait = num("\"hbm_wait_ms\":"), total = num("\"total_ms\":");
+      hbm_wait_sum += wait;
+      hbm_wait_max = std::max(hbm_wait_max, wait);
+      task_total_max = std::max(task_total_max, total);
     }
     uda_destroy(handles[r]);
   }
@@ -556,6 +560,9 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   }
   out["max_task_ws_bytes"] = max_ws;
   out["max_task_rounds"] = max_rounds;
+  out["hbm_wait_ms_sum"] = hbm_wait_sum;  // the tasks' budget waits this step
+  out["hbm_wait_ms_max"] = hbm_wait_max;
+  out["task_total_ms_max"] = task_total_max;
   if (info) *info = paths;
   return out;
 }
