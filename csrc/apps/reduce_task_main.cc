@@ -13,7 +13,8 @@
 // line (consumer counts, the phases of the process's life, the task's own stats). Exit code 0 only if
 // the task delivered every expected record with intact framing (and key order, --check-order).
 // UDA_J2C_THREADS=1 runs the consumer as the plugin does: dataFromUda copies into the KVBuf on the
-// delivering thread, the walk runs on the main thread (default: both inline on the delivering thread).
+// delivering thread, the walk runs on a walker thread of its own, the reducer's thread in the plugin
+// (default: both inline on the delivering thread).
 #include <time.h>
 #include <unistd.h>
 
