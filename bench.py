@@ -174,6 +174,7 @@ def main(argv=None) -> int:
 
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
+    from uda_amd import native
     from uda_amd.models.terasort import RECORD_BYTES, TeraSortConfig, TeraSortShuffle
     from uda_amd.parallel.dist import init_from_env
 
@@ -302,6 +303,7 @@ def main(argv=None) -> int:
             "validated": validated,
             "exchange_errors": exchange_errors,
             "ipc_fallback": getattr(job, "ipc_fallback", None),
+            "hbm_over_budget_bytes": int(native().hbm_stats(device)["over"]),
             "reference_envelope_gbps_per_node": 5.0,
         }
         print(json.dumps(out), flush=True)
@@ -582,6 +584,8 @@ def run_api(args, ctx) -> int:
             "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),
             "hbm_budget_gb": round(stats[-1].get("hbm_budget_bytes", 0) / 1e9, 2),
             "hbm_budget_waits": int(stats[-1].get("hbm_budget_waits", 0)),
+            # bytes allocated outside a reservation while the device was over its budget (0 = the budget held)
+            "hbm_over_budget_bytes": int(stats[-1].get("hbm_over_budget_bytes", 0)),
             "max_task_ws_gb": round(max(s["max_task_ws_bytes"] for s in stats) / 1e9, 3),
             "max_task_rounds": int(max(s["max_task_rounds"] for s in stats)),
             "config": {

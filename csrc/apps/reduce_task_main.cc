@@ -163,8 +163,7 @@ int main(int argc, char** argv) {
   }
   const double t_eof = boot_ms();
   (void)uda_reduce_exit(h);
-  char js[4096] = "{}";
-  (void)uda_stats_json(h, js, sizeof(js));
+  const std::string js = uda_stats_string(h);  // any size (free-text fields can make it long)
   uda_destroy(h);
   sink.flush();
   const double t_end = boot_ms();
@@ -182,7 +181,7 @@ int main(int argc, char** argv) {
       (long long)sink.order_errors(0), json_escape(err).c_str(), t_main - t_exec, t_started - t_main,
       t_init > 0 ? t_init - t_started : -1.0, t_first_fetch > 0 ? t_first_fetch - t_exec : -1.0,
       t_first_fetch > 0 && host.t_first_data > 0 ? host.t_first_data - t_first_fetch : -1.0,
-      t_first_fetch > 0 ? t_eof - t_first_fetch : -1.0, t_end - t_eof, t_end - t_exec, t_exec, t_end, js);
+      t_first_fetch > 0 ? t_eof - t_first_fetch : -1.0, t_end - t_eof, t_end - t_exec, t_exec, t_end, js.c_str());
   std::fflush(stdout);
   (void)t_last_cmd;
   return err.empty() ? 0 : 1;

@@ -243,7 +243,7 @@ int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
   const int32_t n = (int32_t)std::min<size_t>(s.size(), (size_t)outlen - 1);
   std::memcpy(out, s.data(), (size_t)n);
   out[n] = 0;
-  return n;
+  return (int)std::min<size_t>(s.size(), (size_t)INT32_MAX);  // the whole length: the caller may retry larger
 }
 
 }  // extern "C"

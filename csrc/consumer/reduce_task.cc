@@ -28,9 +28,10 @@ constexpr int kProgressReportLimit = 20;  // PROGRESS_REPORT_LIMIT (MergeManager
 constexpr int kExtraBuffers = 10;         // EXTRA_RDMA_BUFFERS (reducer.cc:50)
 constexpr int kMinParallelLpqs = 3;       // MIN_PARALLEL_LPQS (MergeManager.h:125)
 
-std::string json_escape(const std::string& in) {
+// free text in the stats (error reasons): escaped and capped, so the object stays one short JSON line
+std::string json_escape(const std::string& in, size_t cap = 512) {
   std::string o;
-  for (char c : in) {
+  for (char c : in.size() > cap ? in.substr(0, cap) : in) {
     if (c == '"' || c == '\\') o += '\\';
     o += (unsigned char)c < 0x20 ? ' ' : c;
   }
@@ -866,7 +867,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
     << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"hybrid_direct\":" << s.hybrid_direct << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
-    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"gpu_prewarm_phases\":\"" << s.gpu_prewarm_phases << "\"" << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
+    << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"gpu_prewarm_phases\":\"" << json_escape(s.gpu_prewarm_phases) << "\"" << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
     << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"unmapped_reason\":\"" << json_escape(s.unmapped_reason) << "\"" << ",\"descriptor_map_ms\":" << s.descriptor_map_ms << ",\"first_data_ms\":" << s.first_data_ms << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
     << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms

@@ -158,9 +158,7 @@ bool ApiTeraSortBench::resolve(const std::string& map, int reduce, int64_t rec[3
 
 std::string ApiTeraSortBench::provider_stats() const {
   if (!provider_) return "{}";
-  char js[4096];
-  if (uda_stats_json(static_cast<uda_handle*>(provider_), js, sizeof(js)) <= 0) return "{}";
-  return js;
+  return uda_stats_string(static_cast<uda_handle*>(provider_));
 }
 
 int64_t ApiTeraSortBench::store_bytes() const {
@@ -410,8 +408,8 @@ std::vector<std::string> ApiTeraSortBench::task_commands(int r) const {
 
 int ApiTeraSortBench::provider_port() const {
   if (!provider_) return -1;
-  char js[4096];
-  if (uda_stats_json(static_cast<uda_handle*>(provider_), js, sizeof(js)) <= 0) return -1;
+  const std::string st = uda_stats_string(static_cast<uda_handle*>(provider_));
+  const char* js = st.c_str();
   const char* q = std::strstr(js, "\"port\":");
   return q ? std::atoi(q + 7) : -1;
 }
@@ -509,9 +507,10 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   for (int r = 0; r < R; ++r) {
     if (!handles[r]) continue;
     (void)uda_reduce_exit(handles[r]);  // joins the merge thread: its stats are final after this
-    char js[4096];
-    if (uda_stats_json(handles[r], js, sizeof(js)) > 0) {
-      if (r == 0) paths = js;
+    const std::string st = uda_stats_string(handles[r]);
+    const char* js = st.c_str();
+    if (st.size() > 2) {
+      if (r == 0) paths = st;
       auto num = [&](const char* key) {
         const char* q = std::strstr(js, key);
         return q ? std::atof(q + std::strlen(key)) : 0.0;
@@ -557,6 +556,7 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
     out["hbm_budget_bytes"] = (double)ls.budget;
     out["hbm_ledger_peak_bytes"] = (double)ls.peak;
     out["hbm_budget_waits"] = (double)ls.waits;
+    out["hbm_over_budget_bytes"] = (double)ls.over;  // allocations outside a reservation past the budget
   }
   out["max_task_ws_bytes"] = max_ws;
   out["max_task_rounds"] = max_rounds;

@@ -102,6 +102,19 @@ class RcclExchange : public Exchange {
 
   void exchange(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
                 hipStream_t s) override {
+    if (aborted_) throw std::runtime_error("RCCL communicator was aborted after an earlier failure");
+    // A rank that gives up here never enters this round's group, while its peers already inside it
+    // wait for its sends until the timeout: every failure before or inside the group aborts the
+    // communicator (the peers' async-error polling then sees it) instead of only throwing.
+    try {
+      exchange_group(send, recv, s);
+    } catch (const std::exception& e) {
+      fail(std::string("RCCL exchange: ") + e.what());
+    }
+  }
+
+  void exchange_group(const std::vector<std::vector<Span>>& send, const std::vector<std::vector<Span>>& recv,
+                      hipStream_t s) {
     if ((int)send.size() != world_ || (int)recv.size() != world_) throw std::runtime_error("exchange: bad peer lists");
     if (!send[rank_].empty() || !recv[rank_].empty()) throw std::runtime_error("exchange: self slices");
     std::vector<Span> one_send(world_, Span{nullptr, 0}), one_recv(world_, Span{nullptr, 0});

@@ -76,6 +76,11 @@ void HbmLedger::set_fake_device(int device, int64_t total_bytes, const std::stri
   d.budget = (int64_t)((double)total_bytes * kDefaultFraction);
 }
 
+void HbmLedger::set_fake_untracked(int device, int64_t bytes) {
+  std::lock_guard<std::mutex> g(mu_);
+  devs_[device].fake_untracked = bytes;
+}
+
 void HbmLedger::configure(int device, double conf) {
   std::lock_guard<std::mutex> g(mu_);
   Dev& d = dev(device);
@@ -125,7 +130,7 @@ int64_t HbmLedger::others_resident(Dev& d) {
 }
 
 int64_t HbmLedger::device_used(int device, Dev& d) {
-  if (d.fake) return 0;
+  if (d.fake) return d.fake_untracked > 0 ? d.fake_untracked + others(d) + d.used : 0;
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess) {
     (void)hipGetLastError();
@@ -231,8 +236,19 @@ int64_t HbmLedger::used(int device) {
 int64_t HbmLedger::headroom(int device) {
   std::lock_guard<std::mutex> g(mu_);
   Dev& d = dev(device);
-  // what stays whatever the tasks do: MOF stores of every process on the node
-  return d.budget - others_resident(d) - d.resident;
+  // what stays whatever the tasks do: MOF stores of every process on the node, and the device memory no
+  // ledger knows about (HIP runtime, code objects, allocations outside libuda). The latter is what the
+  // device reports in use beyond every process's tracked bytes; reserve() admits against the device's
+  // own figure too, so a round sized from a headroom without it could pass here and never be granted.
+  return d.budget - others_resident(d) - d.resident - untracked(device, d);
+}
+
+int64_t HbmLedger::untracked(int device, Dev& d) {
+  const int64_t dev_used = device_used(device, d);
+  if (dev_used <= 0) return 0;
+  // others() counts the other processes' reservations too (not yet allocated): this underestimates the
+  // untracked bytes a little, which only lets a task try a round the admission check may still refuse
+  return std::max<int64_t>(0, dev_used - (others(d) + d.used));
 }
 
 std::unique_ptr<HbmLedger::Reservation> HbmLedger::reserve(int device, int64_t bytes, const std::function<bool()>& stop,
@@ -267,6 +283,15 @@ std::unique_ptr<HbmLedger::Reservation> HbmLedger::reserve(int device, int64_t b
       const int64_t freed = trim_pools(device, over);
       lk.lock();
       if (freed > 0) continue;
+      // nothing that could ever be freed is held: no reservation of this process, no working set of a
+      // running task here or in another process, no idle pooled object left. Waiting would only hold
+      // every later reservation of the device behind this one for the whole timeout.
+      if (d.reserved == 0 && d.used - d.resident <= 0 && others(d) - others_resident(d) <= 0) {
+        leave();
+        throw HbmBudgetError("a " + mb(bytes) + " working set never fits on device " + std::to_string(device) +
+                             ": " + mb(device_used(device, d)) + " in use by the device's resident data and " +
+                             "untracked allocations, budget " + mb(d.budget));
+      }
     }
     if (stop && stop()) {
       leave();

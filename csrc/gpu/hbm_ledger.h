@@ -107,6 +107,9 @@ class HbmLedger {
   Stats stats(int device);
   // Tests: account allocations of a device without touching HIP (fake HBM size and key).
   void set_fake_device(int device, int64_t total_bytes, const std::string& key);
+  // Tests: device memory a fake device reports in use beyond what the ledgers track (HIP runtime, code
+  // objects, allocations outside libuda).
+  void set_fake_untracked(int device, int64_t bytes);
 
  private:
   HbmLedger() = default;
@@ -115,6 +118,7 @@ class HbmLedger {
     std::string key;  // node-registry key (PCI bus id)
     int64_t total = 0, budget = 0;
     bool fake = false;  // set_fake_device: no HIP device behind it
+    int64_t fake_untracked = 0;  // set_fake_untracked
     int64_t used = 0, reserved = 0, peak = 0, resident = 0, trimmed = 0, over = 0, waits = 0;
     int64_t device_peak = 0;  // HBM in use on the device (hipMemGetInfo) seen at reservations
     double wait_ms = 0;
@@ -126,6 +130,7 @@ class HbmLedger {
   int64_t others(Dev& d);  // mu_ held: bytes the node's other processes hold
   int64_t others_resident(Dev& d);  // mu_ held: resident bytes of the node's other processes
   int64_t device_used(int device, Dev& d);  // HBM in use on the device, tracked or not (0 if unknown)
+  int64_t untracked(int device, Dev& d);    // mu_ held: device HBM in use that no process's ledger counts
   int64_t trim_pools(int device, int64_t want);  // mu_ NOT held
   int64_t idle_bytes(int device);                // mu_ NOT held
 

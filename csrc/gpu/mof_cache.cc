@@ -15,6 +15,7 @@
 #include "device_engine.h"
 #include "sdma.h"
 #include "uda/aio.h"
+#include "uda/fault.h"
 #include "uda/log.h"
 #include "uda/node_registry.h"
 
@@ -65,6 +66,7 @@ struct MofCache::Loader {
   SdmaEngine* sdma = nullptr;
   hipStream_t stream = nullptr;
   bool ready = false;
+  bool failed = false;  // setup failed: every entry of this device is declined (mu_)
   std::string setup_error;
 };
 
@@ -206,9 +208,23 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
     return false;
   }
   const int64_t len = (int64_t)sb.st_size;
-  int device = opt_.devices[0];
-  for (int d : opt_.devices)
-    if (per_device_ - used_[d] > per_device_ - used_[device]) device = d;
+  // a device whose loader could not be set up (no HIP device, no pinned memory, ...) takes nothing:
+  // its entries would never load and their waiters never be answered
+  int device = -1;
+  std::string dead;
+  for (int d : opt_.devices) {
+    auto l = loaders_.find(d);
+    if (l != loaders_.end() && l->second->failed) {
+      dead = l->second->setup_error;
+      continue;
+    }
+    if (device < 0 || per_device_ - used_[d] > per_device_ - used_[device]) device = d;
+  }
+  if (device < 0) {
+    if (why) *why = "provider HBM store unavailable: " + dead;
+    st_.declined++;
+    return false;
+  }
   if (!make_room(device, std::max<int64_t>(len, 1), now)) {
     if (why) *why = "provider HBM budget exhausted (every resident MOF is held by a reducer)";
     st_.declined++;
@@ -345,6 +361,7 @@ void MofCache::opener_main(Loader* L) {
     lk.lock();
     --L->opening;
     st_.open_ms += dt * 1000.0;
+    if (err.empty() && L->failed) err = "provider HBM store loader failed: " + L->setup_error;
     if (!err.empty() || e->failed) {
       if (fd >= 0) ::close(fd);
       fail_entry(*e, err.empty() ? e->error : err, &fire);
@@ -378,6 +395,7 @@ void MofCache::loader_main(Loader* L) {
   const int64_t C = opt_.chunk_bytes;
   std::vector<Fire> fire;
   try {
+    if (fault_hit("STORE_SETUP")) throw std::runtime_error("injected provider HBM store setup failure");
     const int node = device_numa_node(L->device);
     bind_thread_to_numa(node);
     HIP_CHECK(hipSetDevice(L->device));
@@ -408,6 +426,28 @@ void MofCache::loader_main(Loader* L) {
   }
 
   std::unique_lock<std::mutex> lk(mu_);
+  if (!L->ready) {
+    // the device cannot load files: decline everything queued on it (the reducers fetch the bytes
+    // instead) and every later request for it (acquire_async skips a failed loader); the slot table may
+    // be empty and the I/O ring null, so nothing below may run
+    UDA_LOG(kWarn, "provider HBM store: loader of device %d failed to start: %s", L->device, L->setup_error.c_str());
+    L->failed = true;
+    for (auto& e : L->active) fail_entry(*e, "provider HBM store loader failed: " + L->setup_error, &fire);
+    L->active.clear();
+    for (auto& e : L->pending) fail_entry(*e, "provider HBM store loader failed: " + L->setup_error, &fire);
+    L->pending.clear();
+    lk.unlock();
+    for (Fire& f : fire) f.ready(f.ok, f.ref, f.why);
+    if (L->aio) L->aio->drain();
+    for (auto& sl : L->slots) {
+      if (L->sdma && sl.sig.handle) L->sdma->destroy_signal(sl.sig);
+      if (sl.ev) (void)hipEventDestroy(sl.ev);
+    }
+    if (L->stream) (void)hipStreamDestroy(L->stream);
+    if (L->ring) pinned_host_free(L->ring);
+    L->ring = nullptr;
+    return;
+  }
   bool was_busy = false;
   for (;;) {
     if (L->stop) {  // the store is going away: nothing new starts, loads in progress fail

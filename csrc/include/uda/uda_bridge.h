@@ -84,10 +84,25 @@ int uda_provider_register_mof_device(uda_handle* h, const char* job_id, const ch
                                      const void* data, int64_t len, const int64_t* index,
                                      int32_t num_partitions, int32_t device);
 
-/* Consumer/provider statistics as a JSON object (bytes fetched, GB/s, wait time, ...). */
+/* Consumer/provider statistics as a JSON object (bytes fetched, GB/s, wait time, ...), written
+ * NUL-terminated into out. Returns the length of the whole object (like snprintf): a result >= outlen
+ * means it was cut and a buffer of result + 1 bytes holds it; -1 on a bad handle or buffer. */
 int uda_stats_json(uda_handle* h, char* out, int32_t outlen);
 
 #ifdef __cplusplus
+}
+
+#include <string>
+#include <vector>
+/* The whole statistics object, whatever its size ("{}" on a bad handle). */
+inline std::string uda_stats_string(uda_handle* h) {
+  std::vector<char> buf(8192);
+  for (;;) {
+    const int n = uda_stats_json(h, buf.data(), (int32_t)buf.size());
+    if (n < 0) return "{}";
+    if (n < (int)buf.size()) return std::string(buf.data(), (size_t)n);
+    buf.resize((size_t)n + 1);
+  }
 }
 #endif
 

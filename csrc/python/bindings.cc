@@ -542,11 +542,7 @@ PYBIND11_MODULE(_uda_native, m) {
              return uda_provider_register_mof_device(b.h, job.c_str(), map.c_str(), reinterpret_cast<const void*>(dev_ptr),
                                                      len, index.data(), (int32_t)(index.size() / 3), device);
            })
-      .def("stats", [](PyBridge& b) {
-        std::vector<char> buf(4096);
-        uda_stats_json(b.h, buf.data(), (int32_t)buf.size());
-        return std::string(buf.data());
-      });
+      .def("stats", [](PyBridge& b) { return uda_stats_string(b.h); });
   // node-local shared-memory control plane of the IPC exchange (CPU-testable, no HIP)
   py::class_<ShmGroup>(m, "ShmGroup")
       .def(py::init<const std::string&, int, int, size_t, size_t, double>(), py::arg("name"), py::arg("rank"),
@@ -613,6 +609,7 @@ PYBIND11_MODULE(_uda_native, m) {
   m.def("hbm_fake_device", [](int d, int64_t total, const std::string& key) {
     gpu::HbmLedger::get().set_fake_device(d, total, key);
   });
+  m.def("hbm_fake_untracked", [](int d, int64_t b) { gpu::HbmLedger::get().set_fake_untracked(d, b); });
   m.def("hbm_configure", [](int d, double conf) { gpu::HbmLedger::get().configure(d, conf); });
   m.def("hbm_alloc", [](int d, int64_t b, bool resident) { gpu::HbmLedger::get().on_alloc(d, b, resident); },
         py::arg("device"), py::arg("bytes"), py::arg("resident") = false);

@@ -187,6 +187,9 @@ def _budget_and_trim(n, key):
         out["too_big"] = "granted"
     except Exception as e:  # noqa: BLE001
         out["too_big"] = str(e)
+    n.hbm_alloc(d, 45 * GB)  # outside any reservation, past the budget: allowed, but counted
+    out["over_outside"] = n.hbm_stats(d)["over"]
+    n.hbm_free(d, 45 * GB)
     n.hbm_configure(d, 0.5)  # a fraction of the device
     out["budget_fraction"] = n.hbm_stats(d)["budget"]
     return out
@@ -203,6 +206,7 @@ def test_hbm_budget_trims_idle_pools_and_refuses_oversize():
     assert o["reserved_after_release"] == 0
     assert "exceeds the HBM budget headroom" in o["too_big"], o["too_big"]
     assert o["budget_fraction"] == 50 * GB
+    assert o["over_outside"] == 45 * GB  # reported as hbm_over_budget_bytes in the bench JSON
 
 
 def _hold_bytes(n, key, go_file, hold_s):
@@ -246,3 +250,33 @@ def test_hbm_reservation_waits_for_another_process(tmp_path):
     assert o["node_before"] == 60 * GB  # the other process's bytes, seen through the registry
     assert o["granted"] == 40 * GB
     assert o["wait_ms"] > 800  # granted only once the holder freed its 60 GB
+
+
+def _untracked_headroom(n, key):
+    d = 102
+    n.hbm_fake_device(d, 100 * GB, key)
+    n.hbm_configure(d, 50 * GB)
+    n.hbm_alloc(d, 10 * GB, resident=True)  # the provider's MOF store
+    n.hbm_fake_untracked(d, 15 * GB)  # HIP runtime, code objects, allocations outside libuda
+    out = {"headroom": n.hbm_headroom(d)}
+    t0 = time.time()
+    try:
+        n.hbm_reserve(d, 30 * GB, 30.0)  # fits the ledger (10 + 30 <= 50), never the device (15 + 10 + 30 > 50)
+        out["big"] = "granted"
+    except Exception as e:  # noqa: BLE001
+        out["big"] = str(e)
+    out["big_s"] = time.time() - t0
+    r = n.hbm_reserve(d, 25 * GB, 5.0)  # exactly the headroom: granted at once
+    out["granted"] = r.granted
+    return out
+
+
+def test_hbm_headroom_counts_untracked_device_memory():
+    """headroom() is what round sizing shrinks to; it must include the device memory no ledger
+    tracks, or a task sized from it passes the headroom check and then polls until the 1800 s timeout
+    (blocking every later reservation of the device behind it, FIFO)."""
+    o = _in_proc(_untracked_headroom, "fake-untracked-" + secrets.token_hex(3))
+    assert not isinstance(o, str), o
+    assert o["headroom"] == 25 * GB
+    assert "exceeds the HBM budget headroom" in o["big"] and o["big_s"] < 5, o
+    assert o["granted"] == 25 * GB
