@@ -96,6 +96,7 @@ int main(int argc, char** argv) {
   const double t_exec = (double)uda::process_start_ticks((int)getpid()) * 1000.0 / (double)sysconf(_SC_CLK_TCK);
   Host host;
   int64_t kv_buf = 1 << 20, expect = -1;
+  bool kv_buf_set = false;
   bool check_order = false;
   std::vector<std::string> start_args;
   for (int i = 1; i < argc; ++i) {
@@ -106,6 +107,7 @@ int main(int argc, char** argv) {
       if (eq != std::string::npos) host.conf[kv.substr(0, eq)] = kv.substr(eq + 1);
     } else if (a == "--kv-buf" && i + 1 < argc) {
       kv_buf = std::atoll(argv[++i]);
+      kv_buf_set = true;
     } else if (a == "--expect" && i + 1 < argc) {
       expect = std::atoll(argv[++i]);
     } else if (a == "--check-order") {
@@ -117,7 +119,9 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  host.conf["mapred.uda.kv.buf.size"] = std::to_string(kv_buf);
+  // the job's configuration holds only the -D keys (a node-shape run passes none); --kv-buf sets the
+  // dataFromUda buffer size on both sides
+  if (kv_buf_set) host.conf["mapred.uda.kv.buf.size"] = std::to_string(kv_buf);
   uda::gpu::J2CSink sink(1, kv_buf);  // UDA_J2C_THREADS=1: copy on the delivering thread, walk on this one
   sink.set_check_order(check_order);
   sink.set_key_kind(1);

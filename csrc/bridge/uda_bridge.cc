@@ -12,6 +12,7 @@
 #include "../gpu/hbm_ledger.h"
 #include "../provider/supplier.h"
 #include "../service/merge_service.h"
+#include "../service/node_daemon.h"
 #include "uda/cmd.h"
 #include "uda/host.h"
 #include "uda/log.h"
@@ -25,7 +26,8 @@ struct uda_handle {
   std::unique_ptr<uda::Supplier> supplier;
   std::unique_ptr<uda::ReduceTask> task;
   std::unique_ptr<uda::RemoteReduceTask> remote;  // NetMerger hosted by the node's merge service
-  std::unique_ptr<uda::MergeService> service;     // provider: hosts the node's NetMergers
+  std::unique_ptr<uda::MergeService> service;     // provider without a node daemon: an explicit in-process service
+  std::shared_ptr<uda::NodeDaemonClient> daemon;  // provider: the node daemon (HBM store + merge service)
   std::string last_error;
   std::mutex mu;
 };
@@ -83,52 +85,90 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
   UDA_LOG(uda::kInfo, "UDA: The version is %s role=%s", UDA_VERSION_STRING, h->is_merger ? "NetMerger" : "MOFSupplier");
   try {
     if (h->is_merger) {
-      // a node merge service hosts the NetMerger where the GPU context, the pools and the provider's
-      // HBM store already live (merge_service.h); without one, the task merges in this process
-      const std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "");
+      // The node merge service (in the node daemon) hosts the NetMerger where the GPU context, the pools
+      // and the provider's HBM store already live (merge_service.h). Default "auto": the node's service
+      // of the provider on this task's data port, if one runs; none (a node without GPUs, a provider
+      // without its daemon): the task merges in this process.
+      const std::string tr = h->host->get_conf("mapred.uda.transport", "tcp");
+      std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "auto");
+      const bool auto_svc = svc == "auto";
+      if (auto_svc) svc = tr == "tcp" ? uda::MergeService::default_path(h->opt.data_port) : std::string();
+      if (svc == "off" || svc == "0" || svc == "false") svc.clear();
       if (!svc.empty()) {
         try {
           h->remote = std::make_unique<uda::RemoteReduceTask>(svc, args, h->host.get());
           UDA_LOG(uda::kInfo, "NetMerger hosted by the merge service at %s", svc.c_str());
         } catch (const std::exception& e) {
-          UDA_LOG(uda::kWarn, "merge service unavailable (%s): merging in this process", e.what());
+          // no service on the node is the normal case of "auto" without a GPU: not worth a warning
+          const bool absent = auto_svc && std::string(e.what()).find("not reachable") != std::string::npos;
+          UDA_LOG(absent ? uda::kInfo : uda::kWarn, "merge service unavailable at %s (%s): merging in this process",
+                  svc.c_str(), e.what());
         }
       }
       if (!h->remote) h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());
     } else {
       uda::Supplier::Options so;
-      so.transport = h->host->get_conf("mapred.uda.transport", "loopback");
+      so.transport = h->host->get_conf("mapred.uda.transport", "tcp");
       so.loopback_host = h->host->get_conf("mapred.uda.loopback.host", "*");
       so.bind_addr = h->host->get_conf("mapred.uda.provider.bind.address", "");
       so.io_threads = (int)h->host->conf_i64("mapred.uda.provider.blocked.threads.per.disk", 4);
       so.workers = (int)h->host->conf_i64("mapred.uda.provider.workers", 8);
       so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);
-      so.hbm_bytes = h->host->conf_i64("mapred.uda.provider.hbm.bytes", 0);
-      so.hbm_lease_s = h->host->conf_f64("mapred.uda.provider.hbm.lease.s", 600);
-      if (so.hbm_bytes > 0) {
-        // default: stripe the store over every GPU the provider sees, so a node's reduce tasks (placed
-        // over all GPUs, mapred.uda.gpu.device=auto) find their map outputs spread the same way
-        std::string devs = h->host->get_conf("mapred.uda.provider.hbm.devices", "all");
-        if (devs == "all") {
-          devs.clear();
-          const int n = (int)uda::gpu::visible_device_keys().size();
-          for (int d = 0; d < n; ++d) devs += (d ? "," : "") + std::to_string(d);
-          if (devs.empty()) devs = "0";
+      // The node daemon (node_daemon.h) holds the node's GPU state: the HBM store of MOF files and the
+      // merge service. "auto": on a node with a GPU driver and the TCP transport (the loopback transport
+      // only reaches reducers in this very process).
+      const std::string dm = h->host->get_conf("mapred.uda.daemon", "auto");
+      const bool use_daemon = so.transport == "tcp" && (dm == "1" || dm == "true" ||
+                                                        (dm == "auto" && uda::NodeDaemonClient::node_has_gpu()));
+      std::shared_ptr<uda::DeviceStore> local_store;
+      if (!use_daemon) {
+        // no daemon: the store runs in this process only when sized explicitly, the service only at an
+        // explicit path (tests and benchmarks that measure the in-process shapes)
+        const std::string hb = h->host->get_conf("mapred.uda.provider.hbm.bytes", "auto");
+        uda::LocalStoreOptions lo;
+        lo.capacity = hb == "auto" ? 0 : std::atoll(hb.c_str());
+        lo.lease_s = h->host->conf_f64("mapred.uda.provider.hbm.lease.s", 600);
+        if (lo.capacity > 0) {
+          // default: stripe the store over every GPU the provider sees, so a node's reduce tasks (placed
+          // over all GPUs, mapred.uda.gpu.device=auto) find their map outputs spread the same way
+          std::string devs = h->host->get_conf("mapred.uda.provider.hbm.devices", "all");
+          if (devs == "all") {
+            devs.clear();
+            const int n = (int)uda::gpu::visible_device_keys().size();
+            for (int d = 0; d < n; ++d) devs += (d ? "," : "") + std::to_string(d);
+            if (devs.empty()) devs = "0";
+          }
+          lo.devices.clear();
+          for (size_t b = 0; b <= devs.size();) {
+            const size_t e = devs.find(',', b);
+            const std::string t = devs.substr(b, e == std::string::npos ? std::string::npos : e - b);
+            if (!t.empty()) lo.devices.push_back(std::atoi(t.c_str()));
+            if (e == std::string::npos) break;
+            b = e + 1;
+          }
+          local_store = uda::make_local_device_store(lo);
+          UDA_LOG(uda::kInfo, "MOFSupplier HBM store in process: %ld bytes over %zu GPU(s)", (long)lo.capacity,
+                  lo.devices.size());
         }
-        so.hbm_devices.clear();
-        for (size_t b = 0; b <= devs.size();) {
-          const size_t e = devs.find(',', b);
-          const std::string t = devs.substr(b, e == std::string::npos ? std::string::npos : e - b);
-          if (!t.empty()) so.hbm_devices.push_back(std::atoi(t.c_str()));
-          if (e == std::string::npos) break;
-          b = e + 1;
-        }
+        // before the supplier allocates its pinned rings, so they are shareable with the service's clients
+        const std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "auto");
+        if (svc != "auto" && svc != "off" && svc != "0" && svc != "false" && !svc.empty())
+          h->service = std::make_unique<uda::MergeService>(svc);
       }
-      // before the supplier allocates its pinned rings, so they are shareable with the service's clients
-      const std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "");
-      if (!svc.empty()) h->service = std::make_unique<uda::MergeService>(svc);
       h->supplier = std::make_unique<uda::Supplier>(h->opt, so, h->host.get());
+      if (local_store) h->supplier->set_store(local_store);
       h->supplier->start();
+      if (use_daemon) {
+        uda::NodeDaemonClient::Options dopt;
+        dopt.exe = h->host->get_conf("mapred.uda.daemon.exe", "");
+        dopt.start_args = args;
+        dopt.data_port = h->supplier->port();
+        dopt.start_timeout_s = h->host->conf_f64("mapred.uda.daemon.start.timeout.s", 120);
+        dopt.max_restarts = (int)h->host->conf_i64("mapred.uda.daemon.restarts", 3);
+        dopt.log_path = h->host->get_conf("mapred.uda.daemon.log", "");
+        h->daemon = std::make_shared<uda::NodeDaemonClient>(dopt, h->host.get());
+        h->supplier->set_store(h->daemon);
+      }
     }
   } catch (const std::exception& e) {
     UDA_LOG(uda::kError, "startNative failed: %s", e.what());
@@ -156,6 +196,7 @@ int uda_do_command(uda_handle* h, const char* cmd) {
       if (c.header == uda::kExitMsg && h->supplier) {
         h->service.reset();
         h->supplier->stop();
+        h->daemon.reset();  // after the supplier: no worker asks it any more
         UDA_LOG(uda::kInfo, "MOFSupplier stopped");
       } else if (c.header == uda::kJobOverMsg && h->supplier && !c.params.empty()) {
         h->supplier->job_over(c.params[0]);
@@ -178,6 +219,7 @@ int uda_reduce_exit(uda_handle* h) {
     if (h->remote) h->remote->exit();
     h->service.reset();
     if (h->supplier) h->supplier->stop();
+    h->daemon.reset();
   } catch (const std::exception& e) {
     return fail_call(h, e.what());
   }
@@ -192,6 +234,7 @@ void uda_destroy(uda_handle* h) {
     if (h->remote) h->remote->exit();
     h->service.reset();
     if (h->supplier) h->supplier->stop();
+    h->daemon.reset();
     h->task.reset();
     h->remote.reset();
     h->supplier.reset();

@@ -394,9 +394,18 @@ void ReduceTask::on_init(const InitParams& p) {
   }
   if (fault_hit("HOST_ALLOC")) throw UdaError("injected allocation failure for the fetch buffer pool");
   kv_buf_size_ = host_->conf_i64("mapred.uda.kv.buf.size", 1 << 20);
-  backend_ = host_->get_conf("mapred.uda.merge.backend", "cpu");
-  const std::string tr = host_->get_conf("mapred.uda.transport", "loopback");
-  transport_ = (tr == "tcp") ? make_tcp_client(net_.data_port, net_.wqes_per_conn) : make_loopback_client();
+  fault_spec_ = host_->get_conf("mapred.uda.fault.inject", "");
+  // "auto" (default): the GPU merge when this process sees a HIP device, else the CPU (reference) merge
+  backend_ = host_->get_conf("mapred.uda.merge.backend", "auto");
+  if (backend_ == "auto") {
+    backend_ = gpu::visible_device_keys().empty() ? "cpu" : "gpu";
+    UDA_LOG(kInfo, "mapred.uda.merge.backend=auto: %s merge", backend_.c_str());
+  }
+  if (backend_ != "cpu" && backend_ != "gpu") throw ProtocolError("unknown mapred.uda.merge.backend " + backend_);
+  // the reference's consumer always fetches over the network from the providers (RdmaClient,
+  // src/Merger/reducer.cc:412-437); loopback only reaches a provider in this very process
+  const std::string tr = host_->get_conf("mapred.uda.transport", "tcp");
+  transport_ = (tr == "loopback") ? make_loopback_client() : make_tcp_client(net_.data_port, net_.wqes_per_conn);
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.backend = backend_;
@@ -585,6 +594,7 @@ void ReduceTask::fetch_end() {
 
 void ReduceTask::merge_main() {
   auto t0 = std::chrono::steady_clock::now();
+  FaultScope faults(fault_spec_);  // this task's own injected faults (mapred.uda.fault.inject)
   try {
     const std::string gfetch = host_->get_conf("mapred.uda.gpu.fetch", "auto");  // auto | device | host
     // a resumed attempt (LPQ checkpoint of an earlier staged attempt) merges its restored runs on the

@@ -83,6 +83,8 @@ class ReduceTask {
   // Close (reduceExitMsg): stop and join the merge thread.
   void exit();
   bool finished() const { return finished_.load(); }
+  // attempt id from INIT ("" before INIT); read once the task has exited
+  std::string task_id() const { return inited_ ? init_.reduce_task_id : std::string(); }
   ReduceStats stats() const;
   std::string stats_json() const;
 
@@ -129,6 +131,7 @@ class ReduceTask {
   void place_on_gpu();
   std::once_flag placed_;
   std::string device_conf_ = "auto";   // read on the INIT thread
+  std::string fault_spec_;             // mapred.uda.fault.inject (tests: faults of this task only)
   double hbm_budget_conf_ = 0;
   int device_ = 0;
   int registry_slot_ = -1;

@@ -3,6 +3,7 @@
 #include "hbm_ledger.h"
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -21,6 +22,7 @@
 #include "secgen.h"
 #include "uda/codec.h"
 #include "uda/cmd.h"
+#include "uda/ifile.h"
 #include "uda/uda_bridge.h"
 
 namespace uda {
@@ -106,7 +108,10 @@ ConfTable& bench_conf(const ApiBenchConfig& c) {
           {"mapred.uda.gpu.device", std::to_string(c.device)},
           {"mapred.uda.kv.buf.size", std::to_string(c.kv_buf_bytes)},
           {"mapred.uda.gpu.round.bytes", std::to_string(c.round_bytes)},
-          {"mapred.uda.provider.bind.address", c.bind_addr}};
+          {"mapred.uda.provider.bind.address", c.bind_addr},
+          // this benchmark measures the in-process shapes (bench.py --api --node runs the node daemon)
+          {"mapred.uda.daemon", "0"},
+          {"mapred.uda.gpu.merge.service", "off"}};
   if (c.provider_workers > 0) t.kv["mapred.uda.provider.workers"] = std::to_string(c.provider_workers);
   if (c.max_concurrent_merges >= 0) t.kv["mapred.uda.gpu.max.concurrent.merges"] = std::to_string(c.max_concurrent_merges);
   if (c.provider_hbm_bytes > 0) {
@@ -145,7 +150,13 @@ ApiTeraSortBench::~ApiTeraSortBench() {
     uda_destroy(h);
   }
   delete static_cast<ProviderCtx*>(provider_ctx_);
-  for (auto& kv : file_path_) ::unlink(kv.second.c_str());
+  if (!cfg_.keep_mof_files)
+    for (auto& kv : file_path_) {
+      ::unlink(kv.second.c_str());
+      ::unlink((kv.second + ".index").c_str());
+      const size_t slash = kv.second.rfind('/');
+      if (slash != std::string::npos) ::rmdir(kv.second.substr(0, slash).c_str());
+    }
 }
 
 bool ApiTeraSortBench::resolve(const std::string& map, int reduce, int64_t rec[3], std::string* path) const {
@@ -199,20 +210,25 @@ void ApiTeraSortBench::setup() {
   gen_->generate();
   if (cfg_.world == 1) expected_ = gen_->local_dest_records();
   // MOFSupplier handle (TaskTracker / NodeManager side)
-  ConfTable& conf = bench_conf(cfg_);
-  auto* pctx = new ProviderCtx{&conf, this};
-  provider_ctx_ = pctx;
-  uda_callbacks cb{};
-  cb.ctx = pctx;
-  cb.get_conf = provider_conf_cb;
-  cb.get_path = provider_path_cb;
-  cb.log = log_cb;
-  const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
-                                         "-m", "1", "-g", "/tmp", "-s", "1024"};
-  auto av = cargs(args);
-  uda_handle* h = uda_start(0, (int)av.size(), av.data(), 2, 0, &cb);
-  if (!h) throw std::runtime_error("api bench: uda_start (provider) failed");
-  provider_ = h;
+  uda_handle* h = nullptr;
+  if (cfg_.start_provider) {
+    ConfTable& conf = bench_conf(cfg_);
+    auto* pctx = new ProviderCtx{&conf, this};
+    provider_ctx_ = pctx;
+    uda_callbacks cb{};
+    cb.ctx = pctx;
+    cb.get_conf = provider_conf_cb;
+    cb.get_path = provider_path_cb;
+    cb.log = log_cb;
+    const std::vector<std::string> args = {"-w", "256", "-r", std::to_string(cfg_.port > 0 ? cfg_.port : 9011),
+                                           "-m", "1", "-g", "/tmp", "-s", "1024"};
+    auto av = cargs(args);
+    h = uda_start(0, (int)av.size(), av.data(), 2, 0, &cb);
+    if (!h) throw std::runtime_error("api bench: uda_start (provider) failed");
+    provider_ = h;
+  } else if (cfg_.mof_dir.empty() || !cfg_.codec.empty()) {
+    throw std::runtime_error("api bench: a map phase without a provider writes uncompressed MOF files (mof_dir)");
+  }
   map_ids_.clear();
   for (int m = 0; m < cfg_.maps; ++m) {
     const std::string id = map_id(cfg_.rank * cfg_.maps + m);
@@ -222,9 +238,15 @@ void ApiTeraSortBench::setup() {
       const auto ir = gen_->index_record(m, r);
       index.insert(index.end(), ir.begin(), ir.end());
     }
-    if (!cfg_.mof_dir.empty()) {  // the map task's file.out (the provider finds it through getPathUda)
-      const std::string path = cfg_.mof_dir + "/" + id + ".file.out";
-      const int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+    if (!cfg_.mof_dir.empty()) {
+      // the map task's output in Hadoop's layout, <dir>/<attempt>/file.out + file.out.index (the provider
+      // finds it through getPathUda: IndexCache + LocalDirAllocator in Hadoop)
+      const std::string dir = cfg_.mof_dir + "/" + id;
+      if (::mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST)
+        throw std::runtime_error("api bench: cannot create " + dir + ": " + strerror(errno));
+      const std::string path = dir + "/file.out";
+      write_spill_index(path + ".index", index);
+      const int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0644);
       if (fd < 0) throw std::runtime_error("api bench: cannot create " + path + ": " + strerror(errno));
       const int64_t len = gen_->mof_bytes(m);
       std::vector<uint8_t> buf((size_t)std::min<int64_t>(len, 256ll << 20));

@@ -50,6 +50,8 @@ struct ApiBenchConfig {
   // through getPathUda (no registration); the provider's HBM store (provider_hbm_bytes > 0) loads a
   // file into HBM on first touch and answers descriptor fetches from it
   std::string mof_dir;
+  bool keep_mof_files = false;       // leave the files (and their directories) behind (a map phase of its own)
+  bool start_provider = true;        // false: write the map outputs only (no MOFSupplier in this process)
   int64_t provider_hbm_bytes = 0;
   // "terasort" or "secondary": variable-length Text keys with long common prefixes, `skew` of every
   // map's records in reduce task 0 of every rank (BASELINE config #5; device generator secgen.h)

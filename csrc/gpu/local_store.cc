@@ -1,0 +1,65 @@
+// DeviceStore over the HBM store of this process (provider/device_store.h, gpu/mof_cache.h).
+#include <memory>
+#include <string>
+
+#include "../provider/device_store.h"
+#include "device_ptr.h"
+#include "mof_cache.h"
+#include "uda/transport.h"
+
+namespace uda {
+
+namespace {
+
+class LocalDeviceStore : public DeviceStore {
+ public:
+  explicit LocalDeviceStore(const LocalStoreOptions& o) {
+    gpu::MofCache::Options co;
+    co.capacity = o.capacity;
+    co.devices = o.devices;
+    co.odirect = true;
+    co.lease_s = o.lease_s;
+    cache_ = std::make_unique<gpu::MofCache>(co);
+  }
+
+  bool acquire(const std::string& job, const std::string& path, const std::string& holder, int64_t offset,
+               int64_t len, Done done, std::string* why) override {
+    const int64_t need = offset + len;
+    return cache_->acquire_async(
+        job, path, holder, need,
+        [done, offset, need, path](bool ok, const gpu::MofCache::Ref& ref, const std::string& w) {
+          if (!ok) return done(kNotDeviceResident, "provider HBM store: " + w);
+          if (need > ref.len) return done(-4, "index beyond MOF file " + path);
+          done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, ref.ipc, /*leased=*/true));
+        },
+        why);
+  }
+  void release(const std::string& path, const std::string& holder) override { cache_->release(path, holder); }
+  void release_holder(const std::string& job, const std::string& holder) override {
+    cache_->release_holder(job, holder);
+  }
+  void job_over(const std::string& job) override { cache_->job_over(job); }
+  std::string stats_json() override {
+    const gpu::MofCache::Stats st = cache_->stats();
+    return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
+           ",\"holders\":" + std::to_string(st.holders) + ",\"releases\":" + std::to_string(st.releases) +
+           ",\"holders_reaped\":" + std::to_string(st.holders_reaped) + ",\"load_wall_ms\":" +
+           std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) + ",\"load_gbps\":" +
+           std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
+           ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
+           ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
+           std::to_string(st.resident_bytes) + ",\"capacity\":" + std::to_string(cache_->capacity()) +
+           ",\"load_ms\":" + std::to_string(st.load_ms) + "}";
+  }
+
+ private:
+  std::unique_ptr<gpu::MofCache> cache_;
+};
+
+}  // namespace
+
+std::unique_ptr<DeviceStore> make_local_device_store(const LocalStoreOptions& o) {
+  return std::make_unique<LocalDeviceStore>(o);
+}
+
+}  // namespace uda

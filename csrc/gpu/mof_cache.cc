@@ -288,7 +288,7 @@ void MofCache::release_holder(const std::string& job, const std::string& holder)
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : entries_) {
     Entry& e = *kv.second;
-    if (e.job != job) continue;
+    if (job != "*" && e.job != job) continue;
     auto h = e.holders.find(holder);
     if (h == e.holders.end()) continue;
     st_.releases += h->second.first;

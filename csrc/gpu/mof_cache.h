@@ -80,6 +80,7 @@ class MofCache {
   MofCache& operator=(const MofCache&) = delete;
 
   bool enabled() const { return opt_.capacity > 0 && !opt_.devices.empty(); }
+  int64_t capacity() const { return opt_.capacity; }
   // Take `holder`'s reference on the MOF file `path` of job `job` (loading it on first touch) and
   // call ready() once its first need_end bytes are resident: inline if they already are, else from
   // a loader thread. false (reason in *why; ready never called) when it cannot be cached now.
@@ -87,7 +88,8 @@ class MofCache {
                      Ready ready, std::string* why);
   // Blocking form (tests): the whole file.
   bool acquire(const std::string& job, const std::string& path, const std::string& holder, Ref* out, std::string* why);
-  // Drop one of holder's references on `path` / all of holder's references on job's MOFs.
+  // Drop one of holder's references on `path` / all of holder's references on job's MOFs (job "*": on
+  // every job's).
   void release(const std::string& path, const std::string& holder);
   void release_holder(const std::string& job, const std::string& holder);
   // The job is over: its MOFs may be evicted at once, whoever still holds them.

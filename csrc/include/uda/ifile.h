@@ -166,4 +166,13 @@ class StreamValidator {
 // Records and checksum of one IFile partition stream (stops at EOF or at the end of the bytes).
 uint64_t ifile_checksum(const uint8_t* p, size_t n, int64_t* records, int64_t* bytes);
 
+
+// A map output's index file (Hadoop SpillRecord, file.out.index): per partition three big-endian longs
+// {startOffset, rawLength, partLength}, then the CRC32 of those bytes as a big-endian long. index holds
+// 3 values per partition. The record getPathUda returns (IndexRecordBridge.java:26-34).
+void write_spill_index(const std::string& path, const std::vector<int64_t>& index);
+// false (why set) if the file is missing, short or fails its checksum
+bool read_spill_index(const std::string& path, std::vector<int64_t>* index, std::string* why);
+uint32_t crc32_ieee(const uint8_t* p, size_t n, uint32_t crc = 0);
+
 }  // namespace uda

@@ -6,7 +6,6 @@
 #include <cstring>
 
 #include "../gpu/device_ptr.h"
-#include "../gpu/mof_cache.h"
 #include "uda/log.h"
 #include "uda/trace.h"
 
@@ -16,15 +15,6 @@ Supplier::Supplier(const NetlevOptions& net, const Options& o, Host* host) : net
   AsyncIO::Options ao;
   ao.threads = o.io_threads;
   aio_ = AsyncIO::create(ao);
-  if (o.hbm_bytes > 0) {
-    gpu::MofCache::Options co;
-    co.capacity = o.hbm_bytes;
-    co.devices = o.hbm_devices;
-    co.odirect = true;
-    co.lease_s = o.hbm_lease_s;
-    hbm_ = std::make_unique<gpu::MofCache>(co);
-    UDA_LOG(kInfo, "MOFSupplier HBM store: %ld bytes over %zu GPU(s)", (long)o.hbm_bytes, o.hbm_devices.size());
-  }
 }
 
 Supplier::~Supplier() { stop(); }
@@ -55,7 +45,7 @@ void Supplier::stop() {
   for (auto& t : workers_) t.join();
   workers_.clear();
   if (aio_) aio_->drain();
-  hbm_.reset();  // after the workers: no fetch is being answered from it
+  set_store(nullptr);  // after the workers: no fetch is being answered from it
   std::lock_guard<std::mutex> g(fd_mu_);
   for (auto& kv : fds_)
     if (kv.second.fd >= 0) ::close(kv.second.fd);
@@ -76,7 +66,7 @@ void Supplier::register_mof(const std::string& job, const std::string& map, cons
 }
 
 void Supplier::job_over(const std::string& job) {
-  if (hbm_) hbm_->job_over(job);
+  if (auto st = store()) st->job_over(job);
   std::lock_guard<std::mutex> g(idx_mu_);
   const std::string pre = job + "|";
   for (auto it = idx_cache_.begin(); it != idx_cache_.end();)
@@ -84,16 +74,8 @@ void Supplier::job_over(const std::string& job) {
 }
 
 std::string Supplier::hbm_stats_json() {
-  if (!hbm_) return "{}";
-  const gpu::MofCache::Stats st = hbm_->stats();
-  return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
-         ",\"holders\":" + std::to_string(st.holders) + ",\"releases\":" + std::to_string(st.releases) +
-         ",\"holders_reaped\":" + std::to_string(st.holders_reaped) + ",\"load_wall_ms\":" +
-         std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) + ",\"load_gbps\":" +
-         std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
-         ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
-         ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
-         std::to_string(st.resident_bytes) + ",\"load_ms\":" + std::to_string(st.load_ms) + "}";
+  auto st = store();
+  return st ? st->stats_json() : "{}";
 }
 
 void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
@@ -196,11 +178,11 @@ void Supplier::process(Job& j) {
   if (j.req.buf_len == kDescriptorRelease) {
     // the reducer is done with descriptors it fetched (chunk release on SEND completion,
     // src/MOFServer/IndexInfo.cc:276-301): the store may free the MOFs nobody holds any more
-    if (hbm_) {
+    if (auto st = store()) {
       if (j.req.map_id == "*") {
-        hbm_->release_holder(j.req.job_id, j.req.holder);
+        st->release_holder(j.req.job_id, j.req.holder);
       } else if (resolve(j.req, &rec, &mem) && !mem) {
-        hbm_->release(rec.path, j.req.holder);
+        st->release(rec.path, j.req.holder);
       }
     }
     releases_++;
@@ -226,22 +208,20 @@ void Supplier::process(Job& j) {
   if (j.req.buf_len == kDescriptorFetch) {
     // zero-copy fetch: the reducer reads the partition where it lives (RDMA WRITE analogue)
     std::string why;
-    if (!mem && hbm_) {
-      // a Hadoop-written MOF file, made resident in the provider's HBM store: answered once the file
-      // has landed up to the end of this partition (the loader fills files in turn)
-      const int64_t need = rec.start_offset + rec.part_length;
+    std::shared_ptr<DeviceStore> st = mem ? nullptr : store();
+    if (st) {
+      // a Hadoop-written MOF file, made resident in the provider's HBM store (this process's or the node
+      // daemon's): answered once the file has landed up to the end of this partition (the loader fills
+      // files in turn)
       auto done = j.done;
-      const bool taken = hbm_->acquire_async(
-          j.req.job_id, rec.path, j.req.holder, need,
-          [this, ack, done, rec, need](bool ok, const gpu::MofCache::Ref& ref, const std::string& w) mutable {
-            if (!ok) {
-              ack.status = kNotDeviceResident;  // the reducer fetches the bytes instead
-              ack.error = "provider HBM store: " + w;
-            } else if (need > ref.len) {
-              ack.status = -4;
-              ack.error = "index beyond MOF file " + rec.path;
+      const bool taken = st->acquire(
+          j.req.job_id, rec.path, j.req.holder, rec.start_offset, rec.part_length,
+          [this, ack, done](int status, const std::string& desc) mutable {
+            if (status != 0) {
+              ack.status = status;  // kNotDeviceResident: the reducer fetches the bytes instead
+              ack.error = desc;
             } else {
-              ack.path = gpu::make_device_descriptor(ref.device, ref.data + rec.start_offset, ref.ipc, /*leased=*/true);
+              ack.path = desc;
               ack.sent = 0;
               descriptors_++;
             }

@@ -24,12 +24,7 @@
 #include "uda/cmd.h"
 #include "uda/host.h"
 #include "uda/transport.h"
-
-namespace uda {
-namespace gpu {
-class MofCache;
-}
-}  // namespace uda
+#include "device_store.h"
 
 namespace uda {
 
@@ -43,15 +38,21 @@ class Supplier : public DataServer {
     std::string transport = "loopback";  // loopback | tcp
     std::string loopback_host = "*";
     std::string bind_addr;       // tcp: listen address (mapred.uda.provider.bind.address; empty = any)
-    // HBM store for file MOFs (gpu/mof_cache.h): descriptor fetches of MOFs found through getPathUda
-    // load the file into HBM once and are answered with device descriptors
-    int64_t hbm_bytes = 0;               // mapred.uda.provider.hbm.bytes (0: off)
-    std::vector<int> hbm_devices{0};     // mapred.uda.provider.hbm.devices ("0,1,...")
-    double hbm_lease_s = 600;            // mapred.uda.provider.hbm.lease.s: a holder on another node idle
-                                         // this long is presumed dead (same-node holders: process liveness)
   };
   Supplier(const NetlevOptions& net, const Options& o, Host* host);
   ~Supplier() override;
+  // HBM store for file MOFs (device_store.h): descriptor fetches of MOFs found through getPathUda are
+  // answered with device descriptors of the file's copy in HBM (loaded on first touch). Set before
+  // start() or later (a node daemon is started once the listener has its port); none: such fetches are
+  // declined (the reducer fetches the bytes).
+  void set_store(std::shared_ptr<DeviceStore> store) {
+    std::lock_guard<std::mutex> g(store_mu_);
+    store_ = std::move(store);
+  }
+  std::shared_ptr<DeviceStore> store() {
+    std::lock_guard<std::mutex> g(store_mu_);
+    return store_;
+  }
   void start();
   void stop();
 
@@ -68,7 +69,7 @@ class Supplier : public DataServer {
   int64_t descriptors_served() const { return descriptors_.load(); }
   // JOB_OVER: the job's MOFs held in the HBM store may be freed.
   void job_over(const std::string& job);
-  // {"loads":..,"hits":..,...} of the HBM store ("{}" when off)
+  // {"loads":..,"hits":..,...} of the HBM store ("{}" when there is none)
   std::string hbm_stats_json();
   const char* io_backend() const { return aio_ ? aio_->backend() : "none"; }
 
@@ -102,7 +103,8 @@ class Supplier : public DataServer {
   Host* host_;
   std::unique_ptr<AsyncIO> aio_;
   std::unique_ptr<ServerTransport> server_;
-  std::unique_ptr<gpu::MofCache> hbm_;
+  std::mutex store_mu_;
+  std::shared_ptr<DeviceStore> store_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Job> q_;

@@ -19,6 +19,7 @@
 #include "device_engine.h"
 #include "device_ptr.h"
 #include "mof_cache.h"
+#include "service/merge_service.h"
 #include "exchange.h"
 #include "api_bench.h"
 #include "generic_merger.h"
@@ -735,6 +736,11 @@ PYBIND11_MODULE(_uda_native, m) {
         return d;
       });
   m.def("reducer_holder_id", &gpu::reducer_holder_id);
+  // the merge service's peer-credential rule (mapred.uda.gpu.merge.service.users)
+  m.def("merge_service_user_allowed", [](const std::string& users, int uid) {
+    return MergeService::user_allowed(users, (uid_t)uid);
+  });
+  m.def("merge_service_default_path", &MergeService::default_path);
   m.def("open_ipc_mappings", &gpu::open_ipc_mappings);
   m.def("device_read", [](uint64_t addr, int64_t len) {  // device bytes back to the host (tests)
     std::string out((size_t)len, '\0');

@@ -9,6 +9,7 @@
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/un.h>
+#include <pwd.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -23,6 +24,7 @@
 #include "../gpu/sdma.h"
 #include "uda/cmd.h"
 #include "uda/error.h"
+#include "uda/frame.h"
 #include "uda/log.h"
 #include "uda/transport.h"
 
@@ -52,111 +54,11 @@ enum Msg : uint32_t {
   kStats = 18,     // s->c: stats JSON (reply to EXIT)
 };
 
-constexpr uint32_t kMaxPayload = 64u << 20;
-
-bool write_all(int fd, const void* p, size_t n) {
-  const char* c = static_cast<const char*>(p);
-  while (n > 0) {
-    const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
-    if (w < 0 && errno == EINTR) continue;
-    if (w <= 0) return false;
-    c += w;
-    n -= (size_t)w;
-  }
-  return true;
-}
-
-bool send_msg(int sock, uint32_t type, const std::string& payload, int pass_fd = -1) {
-  uint32_t hdr[2] = {type, (uint32_t)payload.size()};
-  if (pass_fd < 0) {
-    std::string buf(reinterpret_cast<const char*>(hdr), sizeof(hdr));
-    buf += payload;
-    return write_all(sock, buf.data(), buf.size());
-  }
-  msghdr mh{};
-  iovec iov{hdr, sizeof(hdr)};
-  mh.msg_iov = &iov;
-  mh.msg_iovlen = 1;
-  alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(int))];
-  std::memset(cbuf, 0, sizeof(cbuf));
-  mh.msg_control = cbuf;
-  mh.msg_controllen = sizeof(cbuf);
-  cmsghdr* cm = CMSG_FIRSTHDR(&mh);
-  cm->cmsg_level = SOL_SOCKET;
-  cm->cmsg_type = SCM_RIGHTS;
-  cm->cmsg_len = CMSG_LEN(sizeof(int));
-  std::memcpy(CMSG_DATA(cm), &pass_fd, sizeof(int));
-  ssize_t w;
-  do {
-    w = ::sendmsg(sock, &mh, MSG_NOSIGNAL);
-  } while (w < 0 && errno == EINTR);
-  if (w <= 0) return false;
-  if ((size_t)w < sizeof(hdr) && !write_all(sock, reinterpret_cast<char*>(hdr) + w, sizeof(hdr) - (size_t)w))
-    return false;
-  return write_all(sock, payload.data(), payload.size());
-}
-
-// false on EOF or error. *fd_out gets a passed descriptor (-1 if none).
-bool recv_msg(int sock, uint32_t* type, std::string* payload, int* fd_out) {
-  uint32_t hdr[2];
-  size_t got = 0;
-  *fd_out = -1;
-  while (got < sizeof(hdr)) {
-    msghdr mh{};
-    iovec iov{reinterpret_cast<char*>(hdr) + got, sizeof(hdr) - got};
-    mh.msg_iov = &iov;
-    mh.msg_iovlen = 1;
-    alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(int))];
-    mh.msg_control = cbuf;
-    mh.msg_controllen = sizeof(cbuf);
-    const ssize_t r = ::recvmsg(sock, &mh, MSG_CMSG_CLOEXEC);
-    if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) return false;
-    for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
-      if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(fd_out, CMSG_DATA(cm), sizeof(int));
-    got += (size_t)r;
-  }
-  *type = hdr[0];
-  if (hdr[1] > kMaxPayload) return false;
-  payload->resize(hdr[1]);
-  got = 0;
-  while (got < hdr[1]) {
-    const ssize_t r = ::recv(sock, &(*payload)[got], hdr[1] - got, 0);
-    if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) return false;
-    got += (size_t)r;
-  }
-  return true;
-}
-
-template <typename T>
-void put(std::string& s, T v) {
-  s.append(reinterpret_cast<const char*>(&v), sizeof(T));
-}
-template <typename T>
-T get(const std::string& s, size_t at) {
-  T v{};
-  if (at + sizeof(T) <= s.size()) std::memcpy(&v, s.data() + at, sizeof(T));
-  return v;
-}
-
-// Wait up to `us` for `fd` to become readable by polling it, before the caller's blocking read: a
-// merged buffer's hand-over is a request/reply in tens of microseconds, less than two scheduler
-// wake-ups cost on a loaded node.
-void spin_readable(int fd, int us) {
-  pollfd pf{fd, POLLIN, 0};
-  const auto t0 = std::chrono::steady_clock::now();
-  while (::poll(&pf, 1, 0) == 0 && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(us)) {
-  }
-}
-
-sockaddr_un unix_addr(const std::string& path) {
-  sockaddr_un a{};
-  a.sun_family = AF_UNIX;
-  if (path.size() >= sizeof(a.sun_path)) throw UdaError("merge service socket path too long: " + path);
-  std::memcpy(a.sun_path, path.c_str(), path.size() + 1);
-  return a;
-}
+using frame::get;
+using frame::put;
+using frame::recv_msg;
+using frame::send_msg;
+using frame::spin_readable;
 
 }  // namespace
 
@@ -187,6 +89,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   std::unique_ptr<ReduceTask> task;
   std::vector<std::string> args;  // startNative arguments (HELLO)
   std::atomic<bool> finished{false};  // the runner has returned: the session can be reaped
+  pid_t peer_pid = 0;
   std::thread reader, runner;
 
   Session(MergeService* s, int fd) : svc(s), sock(fd) {}
@@ -230,7 +133,15 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     p += dflt;
     if (!send(kConfReq, p)) return dflt;
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return closed || conf_replies.count(id); });
+    const auto limit = std::chrono::duration<double>(svc->opt_.conf_timeout_s);
+    if (!cv.wait_for(lk, limit, [&] { return closed || conf_replies.count(id); })) {
+      // a client that stops answering would hold its task (and its HBM reservation) forever: end the
+      // session; the task sees the client gone and stops
+      UDA_LOG(kError, "merge service: client pid %d did not answer a configuration pull (%s) within %.0f s; "
+              "ending its session", (int)peer_pid, key.c_str(), svc->opt_.conf_timeout_s);
+      ::shutdown(sock, SHUT_RDWR);
+      return dflt;
+    }
     if (!conf_replies.count(id)) return dflt;
     std::string v = std::move(conf_replies[id]);
     conf_replies.erase(id);
@@ -332,6 +243,18 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     send(kReady, "");
     svc->sessions_.fetch_add(1);
     run_commands();
+    // the task is over, however it ended: whatever its descriptors still hold in this process's HBM
+    // store goes (a hosted task's holder id carries this process's pid, which never dies with the task)
+    if (svc->opt_.session_ended) {
+      const std::string tid = task ? task->task_id() : std::string();
+      if (!tid.empty()) {
+        try {
+          svc->opt_.session_ended(tid);
+        } catch (const std::exception& e) {
+          UDA_LOG(kWarn, "merge service: session end of %s: %s", tid.c_str(), e.what());
+        }
+      }
+    }
     finished = true;
   }
 
@@ -410,7 +333,13 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   }
 };
 
-MergeService::MergeService(const std::string& path) : path_(path) {
+MergeService::MergeService(const std::string& path) : MergeService([&] {
+        Options o;
+        o.path = path;
+        return o;
+      }()) {}
+
+MergeService::MergeService(const Options& o) : opt_(o) {
   // every shareable pinned allocation keeps its memfd open for the clients that will map it: allow
   // the process as many descriptors as the host lets it have
   rlimit nl{};
@@ -419,30 +348,33 @@ MergeService::MergeService(const std::string& path) : path_(path) {
     (void)setrlimit(RLIMIT_NOFILE, &nl);
   }
   gpu::set_pinned_shareable(true);
-  set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider without a socket
-  listen_fd_ = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-  if (listen_fd_ < 0) throw UdaError(std::string("merge service: socket: ") + strerror(errno));
-  ::unlink(path.c_str());
-  sockaddr_un a = unix_addr(path);
-  const mode_t old = ::umask(0077);  // the node's tasks run as the service's user
-  const int rc = ::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a));
-  ::umask(old);
-  if (rc != 0 || ::listen(listen_fd_, 256) != 0) {
-    const std::string e = strerror(errno);
-    close(listen_fd_);
-    throw UdaError("merge service: cannot listen on " + path + ": " + e);
-  }
+  set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider (if any) without a socket
+  listen_fd_ = frame::unix_listen(opt_.path, 256);
   acceptor_ = std::thread([this] { accept_main(); });
-  UDA_LOG(kInfo, "merge service listening on %s", path.c_str());
+  UDA_LOG(kInfo, "merge service listening on %s (users: %s, max sessions %d)", opt_.path.c_str(), opt_.users.c_str(),
+          opt_.max_sessions);
 }
 
 MergeService::~MergeService() {
-  stop_ = true;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+    sess_cv_.notify_all();
+  }
   ::shutdown(listen_fd_, SHUT_RDWR);
   if (acceptor_.joinable()) acceptor_.join();
   close(listen_fd_);
-  ::unlink(path_.c_str());
+  if (!opt_.path.empty() && opt_.path[0] != '@') ::unlink(opt_.path.c_str());
+  std::map<uint64_t, std::thread> shakes;
   std::vector<std::shared_ptr<Session>> live;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    shakes.swap(shakes_);
+  }
+  // a handshake still waiting returns within the HELLO timeout (or at once, on stop_, when it waits for
+  // its session's registration)
+  for (auto& kv : shakes)
+    if (kv.second.joinable()) kv.second.join();
   {
     std::lock_guard<std::mutex> g(mu_);
     live.swap(live_);
@@ -454,11 +386,43 @@ MergeService::~MergeService() {
   }
 }
 
+std::string MergeService::default_path(int data_port) { return "@uda-merge-" + std::to_string(data_port); }
+
+bool MergeService::user_allowed(const std::string& users, uid_t uid) {
+  if (uid == ::getuid() || uid == ::geteuid()) return true;
+  for (size_t b = 0; b <= users.size();) {
+    size_t e = users.find(',', b);
+    if (e == std::string::npos) e = users.size();
+    std::string u = users.substr(b, e - b);
+    while (!u.empty() && u.front() == ' ') u.erase(0, 1);
+    while (!u.empty() && u.back() == ' ') u.pop_back();
+    if (u == "*") return true;
+    if (!u.empty()) {
+      if (u.find_first_not_of("0123456789") == std::string::npos) {
+        if ((uid_t)std::strtoul(u.c_str(), nullptr, 10) == uid) return true;
+      } else {
+        passwd pw{}, *res = nullptr;
+        std::vector<char> buf(16384);
+        if (getpwnam_r(u.c_str(), &pw, buf.data(), buf.size(), &res) == 0 && res && res->pw_uid == uid) return true;
+      }
+    }
+    b = e + 1;
+  }
+  return false;
+}
+
+std::string MergeService::stats_json() const {
+  return "{\"path\":\"" + opt_.path + "\",\"sessions\":" + std::to_string(sessions_.load()) +
+         ",\"refused\":" + std::to_string(refused_.load()) + ",\"zero_copy_buffers\":" +
+         std::to_string(zero_copy_.load()) + ",\"bounced_buffers\":" + std::to_string(bounced_.load()) + "}";
+}
+
 void MergeService::accept_main() {
   while (!stop_) {
     pollfd pf{listen_fd_, POLLIN, 0};
     const int pr = ::poll(&pf, 1, 200);
-    {  // reap finished sessions
+    {  // reap finished sessions and handshakes
+      std::vector<std::thread> done_shakes;
       std::lock_guard<std::mutex> g(mu_);
       for (auto it = live_.begin(); it != live_.end();) {
         Session& s = **it;
@@ -475,39 +439,84 @@ void MergeService::accept_main() {
           ++it;
         }
       }
+      for (uint64_t id : shakes_done_) {
+        auto t = shakes_.find(id);
+        if (t != shakes_.end()) {
+          t->second.join();  // it has returned
+          shakes_.erase(t);
+        }
+      }
+      shakes_done_.clear();
     }
     if (pr <= 0 || !(pf.revents & POLLIN)) continue;
     const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) continue;
-    auto s = std::make_shared<Session>(this, fd);
-    timeval hello_wait{10, 0};
-    (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &hello_wait, sizeof(hello_wait));
-    uint32_t t;
-    std::string p;
-    int pfd;
-    if (!recv_msg(fd, &t, &p, &pfd) || (t != kHello && t != kDataHello) || p.size() < 8) {
-      if (pfd >= 0) close(pfd);
-      continue;  // ~Session closes the socket
-    }
-    const uint64_t token = get<uint64_t>(p, 0);
-    if (t == kDataHello) {  // a task's data connection: attach it to its session
-      timeval none{0, 0};
-      (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
-      std::shared_ptr<Session> owner;
-      {
-        std::lock_guard<std::mutex> g(mu_);
+    // the HELLO is read on a thread of the connection's own: one slow or stalled client never delays
+    // another task's admission or its data connection
+    std::lock_guard<std::mutex> g(mu_);
+    const uint64_t id = next_shake_++;
+    shakes_[id] = std::thread([this, fd, id] {
+      handshake(fd);
+      std::lock_guard<std::mutex> g2(mu_);
+      shakes_done_.insert(id);
+    });
+  }
+}
+
+void MergeService::handshake(int fd) {
+  auto s = std::make_shared<Session>(this, fd);  // ~Session closes the socket unless it is handed on
+  uid_t uid = (uid_t)-1;
+  pid_t pid = 0;
+  if (!frame::peer_cred(fd, &uid, &pid) || !user_allowed(opt_.users, uid)) {
+    refused_.fetch_add(1);
+    UDA_LOG(kWarn, "merge service: refusing pid %d (uid %d): not in mapred.uda.gpu.merge.service.users (%s)",
+            (int)pid, (int)uid, opt_.users.c_str());
+    send_msg(fd, kRefused, "uid " + std::to_string((int)uid) + " is not allowed to use the merge service");
+    return;
+  }
+  s->peer_pid = pid;
+  timeval hello_wait{(time_t)opt_.hello_timeout_s, (suseconds_t)((opt_.hello_timeout_s - (time_t)opt_.hello_timeout_s) * 1e6)};
+  (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &hello_wait, sizeof(hello_wait));
+  uint32_t t;
+  std::string p;
+  int pfd;
+  if (!recv_msg(fd, &t, &p, &pfd) || (t != kHello && t != kDataHello) || p.size() < 8) {
+    if (pfd >= 0) close(pfd);
+    return;
+  }
+  timeval none{0, 0};
+  (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+  const uint64_t token = get<uint64_t>(p, 0);
+  if (t == kDataHello) {  // a task's data connection: attach it to its session (same peer process)
+    // the control connection's handshake (its own thread) may not have registered the session yet
+    std::shared_ptr<Session> owner;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      sess_cv_.wait_for(g, std::chrono::duration<double>(opt_.hello_timeout_s), [&] {
         for (auto& x : live_)
-          if (x->token == token) owner = x;
+          if (x->token == token && x->peer_pid == pid) owner = x;
+        return owner != nullptr || stop_.load();
+      });
+    }
+    if (owner) {
+      std::lock_guard<std::mutex> g(owner->mu);
+      if (owner->dsock.load() < 0 && !owner->closed) {
+        owner->dsock.store(s->sock);
+        s->sock = -1;  // now the owner's
+        owner->cv.notify_all();
       }
-      if (owner) {
-        std::lock_guard<std::mutex> g(owner->mu);
-        if (owner->dsock.load() < 0 && !owner->closed) {
-          owner->dsock.store(s->sock);
-          s->sock = -1;  // now the owner's
-          owner->cv.notify_all();
-        }
-      }
-      continue;
+    }
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    int running = 0;
+    for (auto& x : live_) running += x->finished.load() ? 0 : 1;
+    if (stop_ || running >= opt_.max_sessions) {
+      refused_.fetch_add(1);
+      send_msg(fd, kRefused, stop_ ? std::string("merge service stopping")
+                                   : "merge service full (" + std::to_string(running) + " hosted tasks)");
+      return;
     }
     s->token = token;
     p.erase(0, 8);
@@ -517,12 +526,10 @@ void MergeService::accept_main() {
       if (e == std::string::npos) break;
       b = e + 1;
     }
-    timeval none{0, 0};
-    (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
     s->reader = std::thread([s] { s->read_loop(); });
     s->runner = std::thread([s] { s->run(); });
-    std::lock_guard<std::mutex> g(mu_);
     live_.push_back(s);
+    sess_cv_.notify_all();
   }
 }
 
@@ -536,7 +543,7 @@ struct RemoteReduceTask::Impl {
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::pair<int32_t, std::string>> results;
-  bool have_stats = false, closed = false, exited = false;
+  bool have_stats = false, closed = false, exited = false, refused = false;
   std::string stats = "{}";
   std::map<uint64_t, std::pair<uint8_t*, size_t>> regions;  // id -> our mapping
 
@@ -634,13 +641,14 @@ struct RemoteReduceTask::Impl {
             results.emplace_back(0, std::string());
           } else if (t == kRefused) {
             results.emplace_back(-1, p);
+            refused = true;  // the start fails in the constructor: no task to report a failure for
           }
           cv.notify_all();
         }
       }
     }
     std::lock_guard<std::mutex> g(mu);
-    const bool unexpected = !exited;
+    const bool unexpected = !exited && !refused;
     closed = true;
     cv.notify_all();
     if (unexpected) host->fail("merge service connection lost");
@@ -665,11 +673,8 @@ struct RemoteReduceTask::Impl {
 RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<std::string>& args, Host* host)
     : impl_(new Impl) {
   impl_->host = host;
-  impl_->sock = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-  if (impl_->sock < 0) throw UdaError(std::string("merge service client: socket: ") + strerror(errno));
-  sockaddr_un a = unix_addr(path);
-  if (::connect(impl_->sock, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
-    throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
+  impl_->sock = frame::unix_connect(path);
+  if (impl_->sock < 0) throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
   uint64_t token = 0;
   {
     std::random_device rd;
@@ -682,11 +687,10 @@ RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<st
     hello += args[i];
   }
   if (!send_msg(impl_->sock, kHello, hello)) throw UdaError("merge service " + path + ": HELLO failed");
-  impl_->dsock = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  impl_->dsock = frame::unix_connect(path);
   std::string dh;
   put<uint64_t>(dh, token);
-  if (impl_->dsock < 0 || ::connect(impl_->dsock, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 ||
-      !send_msg(impl_->dsock, kDataHello, dh))
+  if (impl_->dsock < 0 || !send_msg(impl_->dsock, kDataHello, dh))
     throw UdaError("merge service " + path + ": data connection failed");
   Impl* im = impl_.get();
   impl_->data_reader = std::thread([im] { im->data_loop(); });

@@ -1,14 +1,15 @@
 // Node merge service: every reduce task of the node runs its NetMerger inside one long-lived process
-// per node (the provider process, i.e. the NodeManager aux service), and the process Hadoop starts
-// for a reduce task (a YarnChild JVM loading libuda.so) is a thin client of it.
+// per node -- the node daemon (uda_mof_supplier, started by the provider front end in the NodeManager;
+// node_daemon.h) -- and the process Hadoop starts for a reduce task (a YarnChild JVM loading libuda.so)
+// is a thin client of it.
 //
 // Why (MI355X): a fresh process pays the HIP runtime and ROCr start (~330 ms), the library's code
 // objects (~70 ms), its workspaces and pinned rings (~90 ms) and hipIpc mappings of the provider's
 // HBM before its first merged byte, and 15 such processes starting together contend in the driver.
 // The reference runs the NetMerger inside every reduce task JVM (src/UdaBridge.cc:187-263,
 // src/Merger/NetMergerMain.cc:44-77), which is cheap for a CPU heap merge over RDMA; for a GPU merge
-// the process that holds the GPU context, the pools and the provider's HBM store is the one that
-// should merge. The client forwards the host interface 1:1, so the Java side sees no difference:
+// the process that holds the GPU context, the pools and the HBM store is the one that should merge.
+// The client forwards the host interface 1:1, so the Java side sees no difference:
 //   startNative / doCommandNative / reduceExitMsgNative   -> HELLO / CMD / EXIT frames
 //   getConfData                                           <- CONF_REQ (answered by the client's host)
 //   dataFromUda                                           <- DATA: the merged buffer stays where the
@@ -16,17 +17,29 @@
 //       passed over the socket); the client hands a pointer into its mapping of it to dataFromUda
 //       and acknowledges, so no byte is copied on the way
 //   fetchOverMessage / failureInUda                       <- FETCH_OVER / FAIL
-// A client whose service is unreachable falls back to an in-process NetMerger (uda_bridge.cc).
+// A client whose service is unreachable (or that the service refuses) falls back to an in-process
+// NetMerger (uda_bridge.cc).
 //
-// Transport: one Unix stream socket per reduce task (path: mapred.uda.gpu.merge.service). A service
-// session whose client disappears stops its task; a client whose service disappears reports a
-// failure to its host (Hadoop then falls back to its vanilla shuffle).
+// Transport: one Unix stream socket per reduce task (mapred.uda.gpu.merge.service: "auto" =
+// "@uda-merge-<data port>" in the abstract namespace, any node-local process can reach it; or a path).
+// Access: the peer's uid (SO_PEERCRED) must be the service's own or be listed in
+// mapred.uda.gpu.merge.service.users ("*" = any local user, the default: the provider's TCP port already
+// serves the same map outputs to any client, as the reference's RDMA port does). A session whose
+// client disappears stops its task; a client whose service disappears reports a failure to its host
+// (Hadoop then falls back to its vanilla shuffle). A hung client cannot hold up the others: every
+// connection's HELLO is read on a thread of its own, and a configuration pull it does not answer
+// within conf.timeout ends its session.
 #pragma once
+#include <sys/types.h>
+
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -37,28 +50,50 @@ namespace uda {
 
 class MergeService {
  public:
+  struct Options {
+    std::string path;          // socket path or "@abstract-name"
+    std::string users = "*";   // allowed client users: "*", or user names / uids separated by ','
+    int max_sessions = 256;    // live hosted tasks; more are refused (the client merges in its own process)
+    double conf_timeout_s = 60;
+    double hello_timeout_s = 10;
+    // a hosted task ended (its session is over): e.g. drop the references its descriptors hold in the
+    // HBM store living in this process, whether or not the task released them itself
+    std::function<void(const std::string& reduce_task_id)> session_ended;
+  };
   // Listen on `path` (a stale socket file is replaced). Pinned host memory allocated by this process
   // from now on is shareable with clients (sdma.h set_pinned_shareable).
   explicit MergeService(const std::string& path);
+  explicit MergeService(const Options& o);
   ~MergeService();  // stops accepting, stops every session's task, joins
   MergeService(const MergeService&) = delete;
   MergeService& operator=(const MergeService&) = delete;
-  const std::string& path() const { return path_; }
+  const std::string& path() const { return opt_.path; }
   int64_t sessions() const { return sessions_.load(); }
+  int64_t refused() const { return refused_.load(); }
   int64_t zero_copy_buffers() const { return zero_copy_.load(); }
   int64_t bounced_buffers() const { return bounced_.load(); }
+  std::string stats_json() const;
+  // "auto" -> the node's default name for the provider on `data_port`
+  static std::string default_path(int data_port);
+  // true when `uid` may use the service under `users` (the service's own uid always may)
+  static bool user_allowed(const std::string& users, uid_t uid);
 
   struct Session;
 
  private:
   void accept_main();
-  std::string path_;
+  void handshake(int fd);  // on a thread per connection: credentials, HELLO, session start
+  Options opt_;
   int listen_fd_ = -1;
   std::atomic<bool> stop_{false};
   std::thread acceptor_;
   std::mutex mu_;
+  std::condition_variable sess_cv_;  // a session was registered (a data connection waits for its owner)
   std::vector<std::shared_ptr<Session>> live_;
-  std::atomic<int64_t> sessions_{0};
+  std::map<uint64_t, std::thread> shakes_;  // handshake threads (by a sequence number)
+  std::set<uint64_t> shakes_done_;
+  uint64_t next_shake_ = 0;
+  std::atomic<int64_t> sessions_{0}, refused_{0};
   std::atomic<int64_t> zero_copy_{0}, bounced_{0};
   friend struct Session;
 };

@@ -1,0 +1,676 @@
+// The node daemon and its supervisor in the provider front end. See node_daemon.h.
+#include "node_daemon.h"
+
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <deque>
+
+#include "../gpu/device_ptr.h"
+#include "../gpu/hbm_ledger.h"
+#include "merge_service.h"
+#include "uda/cmd.h"
+#include "uda/error.h"
+#include "uda/frame.h"
+#include "uda/log.h"
+#include "uda/transport.h"
+#include "uda/uda_bridge.h"
+
+extern char** environ;
+
+namespace uda {
+
+namespace {
+
+using frame::get;
+using frame::get_str;
+using frame::put;
+using frame::put_str;
+using frame::recv_msg;
+using frame::send_msg;
+
+enum DMsg : uint32_t {
+  // front end -> daemon
+  kDStart = 1,          // str startNative args ('\0'-joined), i32 data port
+  kDAcquire = 2,        // u64 id, str job, str path, str holder, i64 offset, i64 len
+  kDRelease = 3,        // str path, str holder
+  kDReleaseHolder = 4,  // str job, str holder
+  kDJobOver = 5,        // str job
+  kDStats = 6,          // u64 id
+  kDExit = 7,
+  kDConfReply = 8,  // u32 id, str value
+  // daemon -> front end
+  kDReady = 20,       // str merge service path ("" = none), i64 store bytes
+  kDFailed = 21,      // str why
+  kDAcquired = 22,    // u64 id, i32 status, str descriptor or why
+  kDConfReq = 23,     // u32 id, str key, str default
+  kDLog = 24,         // i32 severity, str message
+  kDStatsReply = 25,  // u64 id, str json
+};
+
+std::string join_args(const std::vector<std::string>& a) {
+  std::string s;
+  for (size_t i = 0; i < a.size(); ++i) {
+    if (i) s.push_back('\0');
+    s += a[i];
+  }
+  return s;
+}
+
+std::vector<std::string> split_args(const std::string& s) {
+  std::vector<std::string> v;
+  if (s.empty()) return v;
+  for (size_t b = 0; b <= s.size();) {
+    const size_t e = s.find('\0', b);
+    v.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+    if (e == std::string::npos) break;
+    b = e + 1;
+  }
+  return v;
+}
+
+std::string exit_text(int status) {
+  if (WIFEXITED(status)) return "exit code " + std::to_string(WEXITSTATUS(status));
+  if (WIFSIGNALED(status)) return std::string("signal ") + strsignal(WTERMSIG(status));
+  return "status " + std::to_string(status);
+}
+
+// wait for `pid` up to `s` seconds, then SIGKILL it; returns how it ended
+std::string reap(pid_t pid, double s) {
+  int status = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const pid_t r = ::waitpid(pid, &status, WNOHANG);
+    if (r == pid) return exit_text(status);
+    if (r < 0) return errno == ECHILD ? "already reaped" : std::string("waitpid: ") + strerror(errno);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(s)) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  ::kill(pid, SIGKILL);
+  if (::waitpid(pid, &status, 0) == pid) return "killed after " + std::to_string((int)s) + " s (" + exit_text(status) + ")";
+  return "killed";
+}
+
+}  // namespace
+
+// ==================================================================================== front end side
+
+std::string NodeDaemonClient::default_exe() {
+  if (const char* e = std::getenv("UDA_DAEMON_EXE")) return e;
+  Dl_info info{};
+  if (!dladdr(reinterpret_cast<void*>(&uda_start), &info) || !info.dli_fname) return "";
+  std::string dir = info.dli_fname;
+  const size_t slash = dir.rfind('/');
+  dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
+  for (const std::string& c : {dir + "/../bin/uda_mof_supplier", dir + "/bin/uda_mof_supplier", dir + "/uda_mof_supplier"})
+    if (::access(c.c_str(), X_OK) == 0) return c;
+  return "";
+}
+
+bool NodeDaemonClient::node_has_gpu() { return ::access("/dev/kfd", R_OK | W_OK) == 0; }
+
+NodeDaemonClient::NodeDaemonClient(const Options& o, Host* host) : opt_(o), host_(host) {
+  if (opt_.exe.empty()) opt_.exe = default_exe();
+  if (opt_.exe.empty()) {
+    why_ = "node daemon executable (uda_mof_supplier) not found next to libuda.so";
+    UDA_LOG(kWarn, "%s: descriptor fetches are declined (reducers fetch bytes)", why_.c_str());
+    return;
+  }
+  if (!spawn()) return;
+  wait_ready(opt_.start_timeout_s);
+  std::lock_guard<std::mutex> g(mu_);
+  if (ready_)
+    UDA_LOG(kInfo, "node daemon pid %d ready: HBM store %.1f GB, merge service %s", (int)pid_.load(),
+            (double)store_bytes_ / 1e9, service_path_.empty() ? "off" : service_path_.c_str());
+  else
+    UDA_LOG(kWarn, "node daemon not ready (%s): descriptor fetches are declined (reducers fetch bytes)", why_.c_str());
+}
+
+NodeDaemonClient::~NodeDaemonClient() {
+  stopping_ = true;
+  send(kDExit, "");
+  const pid_t p = pid_.exchange(0);
+  if (p > 0) {
+    const std::string how = reap(p, 30);
+    UDA_LOG(kInfo, "node daemon pid %d stopped (%s)", (int)p, how.c_str());
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);  // the reader sees EOF
+  }
+  if (reader_.joinable()) reader_.join();
+  for (auto& t : old_readers_)
+    if (t.joinable()) t.join();
+  std::lock_guard<std::mutex> g(mu_);
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+}
+
+bool NodeDaemonClient::spawn() {
+  int sv[2];
+  if (::socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
+    std::lock_guard<std::mutex> g(mu_);
+    why_ = std::string("socketpair: ") + strerror(errno);
+    return false;
+  }
+  // the daemon's end lands on a fixed descriptor number in the child (dup2 there clears close-on-exec)
+  const int child_fd = sv[1] == 100 ? 101 : 100;
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, sv[1], child_fd);
+  posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+  posix_spawn_file_actions_addopen(&fa, 1, opt_.log_path.empty() ? "/dev/null" : opt_.log_path.c_str(),
+                                   O_WRONLY | O_CREAT | O_APPEND, 0644);
+  posix_spawn_file_actions_adddup2(&fa, 1, 2);
+  posix_spawnattr_t attr;
+  posix_spawnattr_init(&attr);
+  sigset_t none, all;
+  sigemptyset(&none);
+  sigfillset(&all);
+  posix_spawnattr_setsigmask(&attr, &none);    // a JVM host blocks signals the daemon must see
+  posix_spawnattr_setsigdefault(&attr, &all);  // and installs handlers it must not inherit
+  posix_spawnattr_setflags(&attr, POSIX_SPAWN_SETSIGMASK | POSIX_SPAWN_SETSIGDEF);
+  const std::string fd_arg = std::to_string(child_fd);
+  std::vector<char*> argv = {const_cast<char*>(opt_.exe.c_str()), const_cast<char*>("--daemon-fd"),
+                             const_cast<char*>(fd_arg.c_str()), nullptr};
+  pid_t pid = 0;
+  const int rc = ::posix_spawn(&pid, opt_.exe.c_str(), &fa, &attr, argv.data(), environ);
+  posix_spawn_file_actions_destroy(&fa);
+  posix_spawnattr_destroy(&attr);
+  ::close(sv[1]);
+  if (rc != 0) {
+    ::close(sv[0]);
+    std::lock_guard<std::mutex> g(mu_);
+    why_ = "cannot start " + opt_.exe + ": " + strerror(rc);
+    UDA_LOG(kError, "%s", why_.c_str());
+    return false;
+  }
+  uint64_t gen;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> gs(send_mu_);
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = sv[0];
+    gen = ++gen_;
+    failed_start_ = false;
+    why_ = "node daemon starting";
+    pid_ = pid;
+    if (reader_.joinable()) old_readers_.push_back(std::move(reader_));  // maybe this very thread (a restart)
+    reader_ = std::thread([this, fd = sv[0], gen] { reader_main(fd, gen); });
+  }
+  std::string st;
+  put_str(st, join_args(opt_.start_args));
+  put<int32_t>(st, opt_.data_port);
+  send(kDStart, st);
+  UDA_LOG(kInfo, "node daemon %s started, pid %d (generation %llu)", opt_.exe.c_str(), (int)pid,
+          (unsigned long long)gen);
+  return true;
+}
+
+bool NodeDaemonClient::wait_ready(double s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait_for(lk, std::chrono::duration<double>(s), [&] { return ready_.load() || failed_start_ || stopping_; });
+  if (!ready_ && !failed_start_ && pid_.load() > 0 && why_ == "node daemon starting")
+    why_ = "node daemon not ready within " + std::to_string((int)s) + " s";
+  return ready_;
+}
+
+std::string NodeDaemonClient::why() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return why_;
+}
+
+std::string NodeDaemonClient::service_path() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return service_path_;
+}
+
+bool NodeDaemonClient::send(uint32_t type, const std::string& payload) {
+  std::lock_guard<std::mutex> gs(send_mu_);
+  int fd;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    fd = fd_;
+  }
+  return fd >= 0 && send_msg(fd, type, payload);
+}
+
+void NodeDaemonClient::reader_main(int fd, uint64_t gen) {
+  for (;;) {
+    uint32_t t;
+    std::string p;
+    int pfd;
+    if (!recv_msg(fd, &t, &p, &pfd)) break;
+    if (pfd >= 0) ::close(pfd);
+    if (t == kDAcquired) {
+      const uint64_t id = get<uint64_t>(p, 0);
+      const int32_t status = get<int32_t>(p, 8);
+      size_t at = 12;
+      const std::string desc = get_str(p, &at);
+      Done done;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = pending_.find(id);
+        if (it == pending_.end()) continue;
+        done = std::move(it->second);
+        pending_.erase(it);
+      }
+      done(status, desc);
+    } else if (t == kDConfReq) {
+      const uint32_t id = get<uint32_t>(p, 0);
+      size_t at = 4;
+      const std::string key = get_str(p, &at), dflt = get_str(p, &at);
+      std::string r;
+      put<uint32_t>(r, id);
+      put_str(r, host_ ? host_->get_conf(key, dflt) : dflt);
+      std::lock_guard<std::mutex> gs(send_mu_);
+      (void)send_msg(fd, kDConfReply, r);
+    } else if (t == kDLog) {
+      const int32_t sev = get<int32_t>(p, 0);
+      size_t at = 4;
+      const std::string msg = get_str(p, &at);
+      UDA_LOG(sev, "[node daemon %d] %s", (int)pid_.load(), msg.c_str());
+    } else if (t == kDReady) {
+      size_t at = 0;
+      const std::string svc = get_str(p, &at);
+      const int64_t bytes = get<int64_t>(p, at);
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen != gen_) continue;
+      service_path_ = svc;
+      store_bytes_ = bytes;
+      why_.clear();
+      ready_ = true;
+      cv_.notify_all();
+    } else if (t == kDFailed) {
+      size_t at = 0;
+      const std::string w = get_str(p, &at);
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen != gen_) continue;
+      why_ = w;
+      failed_start_ = true;
+      cv_.notify_all();
+    } else if (t == kDStatsReply) {
+      const uint64_t id = get<uint64_t>(p, 0);
+      size_t at = 8;
+      std::lock_guard<std::mutex> g(mu_);
+      stats_replies_[id] = get_str(p, &at);
+      cv_.notify_all();
+    }
+  }
+  daemon_gone(gen, "control connection closed");
+}
+
+void NodeDaemonClient::daemon_gone(uint64_t gen, const std::string& why) {
+  std::map<uint64_t, Done> pending;
+  bool restart = false;
+  std::string how;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (gen != gen_) return;
+    ready_ = false;
+    pending.swap(pending_);
+    if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+  }
+  const pid_t p = pid_.exchange(0);
+  if (p > 0) how = reap(p, 5);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    const bool was_started = !failed_start_;
+    why_ = "node daemon" + (p > 0 ? " pid " + std::to_string((int)p) : std::string()) + " gone (" + why +
+           (how.empty() ? "" : ", " + how) + ")";
+    restart = !stopping_ && was_started && restarts_.load() < opt_.max_restarts;
+    cv_.notify_all();
+  }
+  if (!stopping_) UDA_LOG(kError, "%s; %s", why_.c_str(), restart ? "restarting it" : "descriptor fetches are declined from now on");
+  for (auto& kv : pending) kv.second(kNotDeviceResident, "node daemon gone: " + why);
+  if (restart) {
+    restarts_++;
+    std::this_thread::sleep_for(std::chrono::seconds(1));
+    if (!stopping_ && spawn()) wait_ready(opt_.start_timeout_s);
+  }
+}
+
+bool NodeDaemonClient::acquire(const std::string& job, const std::string& path, const std::string& holder,
+                               int64_t offset, int64_t len, Done done, std::string* why) {
+  uint64_t id;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!ready_) {
+      if (why) *why = why_;
+      return false;
+    }
+    id = next_id_++;
+    pending_[id] = std::move(done);
+  }
+  std::string m;
+  put<uint64_t>(m, id);
+  put_str(m, job);
+  put_str(m, path);
+  put_str(m, holder);
+  put<int64_t>(m, offset);
+  put<int64_t>(m, len);
+  if (send(kDAcquire, m)) return true;
+  std::lock_guard<std::mutex> g(mu_);
+  if (pending_.erase(id) == 0) return true;  // the daemon-gone path already answered it
+  if (why) *why = "node daemon unreachable";
+  return false;
+}
+
+void NodeDaemonClient::release(const std::string& path, const std::string& holder) {
+  if (!ready_) return;
+  std::string m;
+  put_str(m, path);
+  put_str(m, holder);
+  send(kDRelease, m);
+}
+
+void NodeDaemonClient::release_holder(const std::string& job, const std::string& holder) {
+  if (!ready_) return;
+  std::string m;
+  put_str(m, job);
+  put_str(m, holder);
+  send(kDReleaseHolder, m);
+}
+
+void NodeDaemonClient::job_over(const std::string& job) {
+  if (!ready_) return;
+  std::string m;
+  put_str(m, job);
+  send(kDJobOver, m);
+}
+
+std::string NodeDaemonClient::stats_json() {
+  std::string body = "{}";
+  uint64_t id = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (ready_) id = next_id_++;
+  }
+  if (id) {
+    std::string m;
+    put<uint64_t>(m, id);
+    if (send(kDStats, m)) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_for(lk, std::chrono::seconds(10), [&] { return stats_replies_.count(id) || !ready_; });
+      auto it = stats_replies_.find(id);
+      if (it != stats_replies_.end()) {
+        body = it->second;
+        stats_replies_.erase(it);
+      }
+    }
+  }
+  std::string d;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    std::string w;
+    for (char c : why_) w += (c == '"' || c == '\\') ? ' ' : c;
+    d = "\"daemon\":{\"pid\":" + std::to_string((int)pid_.load()) + ",\"ready\":" + (ready_ ? "true" : "false") +
+        ",\"restarts\":" + std::to_string(restarts_.load()) + ",\"service\":\"" + service_path_ + "\",\"why\":\"" + w +
+        "\"}";
+  }
+  if (body.size() < 2 || body.back() != '}') body = "{}";
+  return body.size() == 2 ? "{" + d + "}" : body.substr(0, body.size() - 1) + "," + d + "}";
+}
+
+// ==================================================================================== daemon side
+
+namespace {
+
+struct Daemon {
+  int ctl = -1;
+  std::mutex send_mu;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint32_t, std::string> conf_replies;
+  uint32_t next_conf = 1;
+  bool closed = false, exit_req = false;
+  std::shared_ptr<DeviceStore> store;
+  std::unique_ptr<MergeService> svc;
+  std::deque<std::string> starts;
+
+  bool send(uint32_t t, const std::string& p) {
+    std::lock_guard<std::mutex> g(send_mu);
+    return send_msg(ctl, t, p);
+  }
+
+  // getConfData of the NodeManager, through the front end
+  std::string conf(const std::string& key, const std::string& dflt) {
+    uint32_t id;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (closed) return dflt;
+      id = next_conf++;
+    }
+    std::string m;
+    put<uint32_t>(m, id);
+    put_str(m, key);
+    put_str(m, dflt);
+    if (!send(kDConfReq, m)) return dflt;
+    std::unique_lock<std::mutex> lk(mu);
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return closed || conf_replies.count(id); })) return dflt;
+    auto it = conf_replies.find(id);
+    if (it == conf_replies.end()) return dflt;
+    std::string v = std::move(it->second);
+    conf_replies.erase(it);
+    return v;
+  }
+
+  static void log_sink(void* ctx, const char* msg, int sev) {
+    auto* d = static_cast<Daemon*>(ctx);
+    std::string m;
+    put<int32_t>(m, sev);
+    put_str(m, msg ? msg : "");
+    (void)d->send(kDLog, m);
+  }
+
+  std::string stats() {
+    std::shared_ptr<DeviceStore> st;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      st = store;
+    }
+    std::string s = st ? st->stats_json() : "{}";
+    const std::string ms = svc ? svc->stats_json() : "{}";
+    return s.size() <= 2 ? "{\"merge_service\":" + ms + "}" : s.substr(0, s.size() - 1) + ",\"merge_service\":" + ms + "}";
+  }
+
+  void read_loop() {
+    for (;;) {
+      uint32_t t;
+      std::string p;
+      int pfd;
+      if (!recv_msg(ctl, &t, &p, &pfd)) break;
+      if (pfd >= 0) ::close(pfd);
+      std::shared_ptr<DeviceStore> st;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        st = store;
+      }
+      if (t == kDConfReply) {
+        size_t at = 4;
+        std::lock_guard<std::mutex> g(mu);
+        conf_replies[get<uint32_t>(p, 0)] = get_str(p, &at);
+        cv.notify_all();
+      } else if (t == kDStart) {
+        std::lock_guard<std::mutex> g(mu);
+        starts.push_back(p);
+        cv.notify_all();
+      } else if (t == kDAcquire) {
+        const uint64_t id = get<uint64_t>(p, 0);
+        size_t at = 8;
+        const std::string job = get_str(p, &at), path = get_str(p, &at), holder = get_str(p, &at);
+        const int64_t off = get<int64_t>(p, at), len = get<int64_t>(p, at + 8);
+        auto reply = [this, id](int status, const std::string& desc) {
+          std::string r;
+          put<uint64_t>(r, id);
+          put<int32_t>(r, status);
+          put_str(r, desc);
+          (void)send(kDAcquired, r);
+        };
+        std::string why;
+        if (!st) {
+          reply(kNotDeviceResident, "the node daemon has no HBM store");
+        } else if (!st->acquire(job, path, holder, off, len, reply, &why)) {
+          reply(kNotDeviceResident, "provider HBM store: " + why);
+        }
+      } else if (t == kDRelease) {
+        size_t at = 0;
+        const std::string path = get_str(p, &at), holder = get_str(p, &at);
+        if (st) st->release(path, holder);
+      } else if (t == kDReleaseHolder) {
+        size_t at = 0;
+        const std::string job = get_str(p, &at), holder = get_str(p, &at);
+        if (st) st->release_holder(job, holder);
+      } else if (t == kDJobOver) {
+        size_t at = 0;
+        if (st) st->job_over(get_str(p, &at));
+      } else if (t == kDStats) {
+        std::string r;
+        put<uint64_t>(r, get<uint64_t>(p, 0));
+        put_str(r, stats());
+        (void)send(kDStatsReply, r);
+      } else if (t == kDExit) {
+        std::lock_guard<std::mutex> g(mu);
+        exit_req = true;
+        cv.notify_all();
+      }
+    }
+    std::lock_guard<std::mutex> g(mu);
+    closed = true;
+    cv.notify_all();
+  }
+};
+
+// "auto" / bytes (> 1) / a fraction of the device's HBM budget (0 < f <= 1) of every store device
+int64_t store_capacity(const std::string& conf, const std::vector<int>& devices) {
+  double f = 0.6;  // auto: the rest of the budget stays with the hosted tasks' working sets
+  if (conf != "auto") {
+    const double v = std::atof(conf.c_str());
+    if (v > 1.0) return (int64_t)v;
+    if (v <= 0) return 0;
+    f = v;
+  }
+  int64_t total = 0;
+  for (int d : devices) total += (int64_t)((double)gpu::HbmLedger::get().budget(d) * f);
+  return total;
+}
+
+}  // namespace
+
+int run_node_daemon(int ctl_fd) {
+  ::signal(SIGPIPE, SIG_IGN);
+  auto d = std::make_unique<Daemon>();
+  d->ctl = ctl_fd;
+  std::thread reader([&] { d->read_loop(); });
+  int rc = 0;
+  try {
+    // START comes first: the provider's startNative arguments and its TCP port
+    std::string start;
+    {
+      std::unique_lock<std::mutex> lk(d->mu);
+      d->cv.wait(lk, [&] { return d->closed || !d->starts.empty(); });
+      if (d->starts.empty()) throw UdaError("front end gone before START");
+      start = d->starts.front();
+    }
+    size_t at = 0;
+    const std::vector<std::string> args = split_args(get_str(start, &at));
+    const int port = get<int32_t>(start, at);
+    NetlevOptions opt;
+    std::string err;
+    if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
+    log_set_sink(&Daemon::log_sink, d.get());  // the daemon's log lands in the NodeManager's
+    log_set_threshold((int)std::atoi(d->conf("mapred.uda.log.level", std::to_string(log_threshold())).c_str()));
+    UDA_LOG(kInfo, "node daemon up (pid %d), provider port %d", (int)getpid(), port);
+    // GPUs: every visible one carries a share of the store; tasks are placed over all of them
+    const std::vector<std::string> keys = gpu::visible_device_keys();
+    const std::string force = d->conf("mapred.uda.daemon", "auto");
+    if (keys.empty() && force != "1" && force != "true")
+      throw UdaError("no HIP device visible to the node daemon");
+    const double budget = std::atof(d->conf("mapred.uda.gpu.hbm.budget", "0").c_str());
+    std::vector<int> devs;
+    std::string dconf = d->conf("mapred.uda.provider.hbm.devices", "all");
+    if (dconf == "all") {
+      for (int i = 0; i < (int)keys.size(); ++i) devs.push_back(i);
+    } else {
+      for (size_t b = 0; b <= dconf.size();) {
+        const size_t e = dconf.find(',', b);
+        const std::string t = dconf.substr(b, e == std::string::npos ? std::string::npos : e - b);
+        if (!t.empty()) devs.push_back(std::atoi(t.c_str()));
+        if (e == std::string::npos) break;
+        b = e + 1;
+      }
+    }
+    for (int dv : devs) gpu::HbmLedger::get().configure(dv, budget);
+    int64_t store_bytes = 0;
+    if (!keys.empty() && !devs.empty()) {
+      LocalStoreOptions so;
+      so.devices = devs;
+      so.capacity = store_capacity(d->conf("mapred.uda.provider.hbm.bytes", "auto"), devs);
+      so.lease_s = std::atof(d->conf("mapred.uda.provider.hbm.lease.s", "600").c_str());
+      if (so.capacity > 0) {
+        std::lock_guard<std::mutex> g(d->mu);
+        d->store = make_local_device_store(so);
+        store_bytes = so.capacity;
+      }
+    }
+    // the merge service, after which pinned host memory of this process is shareable with its clients
+    std::string svc_path = d->conf("mapred.uda.gpu.merge.service", "auto");
+    if (svc_path == "auto") svc_path = MergeService::default_path(port);
+    if (svc_path == "off" || svc_path == "0" || svc_path == "false") svc_path.clear();
+    if (!svc_path.empty()) {
+      MergeService::Options mo;
+      mo.path = svc_path;
+      mo.users = d->conf("mapred.uda.gpu.merge.service.users", "*");
+      mo.max_sessions = (int)std::atoi(d->conf("mapred.uda.gpu.merge.service.max.sessions", "256").c_str());
+      mo.conf_timeout_s = std::atof(d->conf("mapred.uda.gpu.merge.service.conf.timeout.s", "60").c_str());
+      Daemon* dp = d.get();
+      mo.session_ended = [dp](const std::string& task) {
+        std::shared_ptr<DeviceStore> st;
+        {
+          std::lock_guard<std::mutex> g(dp->mu);
+          st = dp->store;
+        }
+        // whatever a hosted task's descriptors still hold goes with its session
+        if (st) st->release_holder("*", gpu::reducer_holder_id(task));
+      };
+      d->svc = std::make_unique<MergeService>(mo);
+    }
+    std::string ready;
+    put_str(ready, svc_path);
+    put<int64_t>(ready, store_bytes);
+    d->send(kDReady, ready);
+    std::unique_lock<std::mutex> lk(d->mu);
+    d->cv.wait(lk, [&] { return d->closed || d->exit_req; });
+  } catch (const std::exception& e) {
+    std::string m;
+    put_str(m, e.what());
+    d->send(kDFailed, m);
+    rc = 1;
+  }
+  // teardown: hosted tasks first (they read the store), then the store
+  d->svc.reset();
+  {
+    std::shared_ptr<DeviceStore> st;
+    {
+      std::lock_guard<std::mutex> g(d->mu);
+      st.swap(d->store);
+    }
+    st.reset();
+  }
+  log_set_sink(nullptr, nullptr);
+  ::shutdown(ctl_fd, SHUT_RDWR);
+  reader.join();
+  ::close(ctl_fd);
+  return rc;
+}
+
+}  // namespace uda

@@ -1,0 +1,115 @@
+// The node daemon: the process that holds a node's GPU state for UDA -- the provider's HBM store of map
+// output files and the merge service hosting the node's reduce tasks' NetMergers -- started and
+// supervised by the provider front end (the MOFSupplier inside the NodeManager's aux service, or the
+// TaskTracker).
+//
+// Reference shape: the MOFSupplier runs inside the NodeManager / TaskTracker JVM
+// (src/MOFServer/MOFSupplierMain.cc:87-143) and each NetMerger inside its ReduceTask JVM, so a native
+// failure of one reducer falls back for that reducer only (src/UdaBridge.cc:506-530,
+// UdaShuffleConsumerPluginShared.java:205-232) and never reaches the NodeManager.
+//
+// MI355X design: the GPU work of a node -- HBM store loads, hosted merges -- wants one warm process per
+// node (one HIP context, the pools, no per-task hipIpc mappings: merge_service.h), but a GPU fault there
+// must not take the NodeManager down. So the front end keeps what the reference's MOFSupplier does
+// (TCP listener, getPathUda resolution, byte fetches read from the MOF files) and never touches a GPU;
+// the daemon is a child process of it (uda_amd/bin/uda_mof_supplier --daemon-fd N) reached over a
+// socket pair:
+//   front end -> daemon: START (startNative args, data port), ACQUIRE (a descriptor fetch of a resolved
+//                        MOF file: job, path, holder, partition offset/length), RELEASE, RELEASE_HOLDER,
+//                        JOB_OVER, STATS, EXIT
+//   daemon -> front end: READY / FAILED, ACQUIRED (descriptor or decline), CONF_REQ (getConfData of the
+//                        NodeManager's configuration), LOG (into the NodeManager's log), STATS_REPLY
+// Failure containment:
+//   * an error inside one hosted task fails that task only (its client reports failureInUda);
+//   * a daemon that dies (a GPU fault, an abort, the OOM killer) fails the hosted tasks of that moment
+//     (their clients see the session gone) and nothing else: the front end declines descriptor fetches
+//     (reducers fetch the bytes it serves from the MOF files), restarts the daemon (up to
+//     mapred.uda.daemon.restarts times), and keeps serving;
+//   * the daemon exits when the front end goes away (control socket EOF).
+#pragma once
+#include <sys/types.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../provider/device_store.h"
+#include "uda/host.h"
+
+namespace uda {
+
+class NodeDaemonClient : public DeviceStore {
+ public:
+  struct Options {
+    std::string exe;                       // daemon executable; "" = uda_mof_supplier next to libuda.so
+    std::vector<std::string> start_args;   // the provider's startNative arguments
+    int data_port = 0;                     // the front end's TCP port (names the merge service socket)
+    double start_timeout_s = 120;          // READY within this (a fresh HIP runtime start included)
+    int max_restarts = 3;                  // restarts after the daemon died (0: none)
+    std::string log_path;                  // the daemon's stderr ("" = /dev/null; its log goes to LOG frames)
+  };
+  // Spawn the daemon and wait for its READY (or FAILED). Never throws: a daemon that cannot start leaves
+  // a client that declines every fetch (ready() false, why() says what happened).
+  NodeDaemonClient(const Options& o, Host* host);
+  ~NodeDaemonClient() override;  // EXIT, waits for the daemon (then kills it)
+
+  bool ready() const { return ready_.load(); }
+  std::string why() const;
+  pid_t pid() const { return pid_.load(); }
+  int restarts() const { return restarts_.load(); }
+  std::string service_path() const;
+  // Wait until the daemon is ready (after a restart), up to `s` seconds.
+  bool wait_ready(double s);
+
+  bool acquire(const std::string& job, const std::string& path, const std::string& holder, int64_t offset,
+               int64_t len, Done done, std::string* why) override;
+  void release(const std::string& path, const std::string& holder) override;
+  void release_holder(const std::string& job, const std::string& holder) override;
+  void job_over(const std::string& job) override;
+  std::string stats_json() override;
+
+  // The daemon executable next to the loaded libuda.so ("" if none is found).
+  static std::string default_exe();
+  // The node has a GPU driver (/dev/kfd): "auto" starts a daemon. Checked without initialising HIP in
+  // this (the NodeManager's) process.
+  static bool node_has_gpu();
+
+ private:
+  bool spawn();                 // mu_ NOT held
+  void reader_main(int fd, uint64_t gen);
+  bool send(uint32_t type, const std::string& payload);
+  void daemon_gone(uint64_t gen, const std::string& why);
+
+  Options opt_;
+  Host* host_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  int fd_ = -1;                 // control socket (the front end's end)
+  uint64_t gen_ = 0;            // daemon generation (restarts)
+  std::atomic<pid_t> pid_{0};
+  std::atomic<bool> ready_{false};
+  std::atomic<bool> stopping_{false};
+  std::atomic<int> restarts_{0};
+  bool failed_start_ = false;
+  std::string why_ = "node daemon not started";
+  std::string service_path_;
+  int64_t store_bytes_ = 0;
+  uint64_t next_id_ = 1;
+  std::map<uint64_t, Done> pending_;
+  std::map<uint64_t, std::string> stats_replies_;
+  std::thread reader_;
+  std::vector<std::thread> old_readers_;
+  std::mutex send_mu_;
+};
+
+// The daemon's main (uda_mof_supplier --daemon-fd N): serve the front end on `ctl_fd` until it says EXIT
+// or goes away. Returns the process exit code.
+int run_node_daemon(int ctl_fd);
+
+}  // namespace uda

@@ -178,3 +178,22 @@ def test_hbm_budget_counts_untracked_device_memory(require_gpu, native):
         assert native.hbm_stats(d)["device_peak"] >= used + (5 << 30)
     finally:
         native.hbm_configure(d, 0.0)  # back to the default fraction
+
+
+def test_store_declines_after_an_injected_loader_setup_failure(require_gpu, native, tmp_path, monkeypatch):
+    """a loader whose setup fails (UDA_FAULT_STORE_SETUP) answers its queued request with a
+    decline and declines every later one at once, instead of reading an empty slot table."""
+    f = _files(tmp_path, 1, 4 * MB)
+    monkeypatch.setenv("UDA_FAULT_STORE_SETUP", "1")
+    store = native.MofStore(capacity=64 * MB, devices=[0])
+    t0 = time.time()
+    ok, why, _, _, _ = store.acquire("job", f[0], "r1")
+    assert not ok and "injected" in why, why
+    time.sleep(0.3)
+    ok, why, _, _, _ = store.acquire("job", f[0], "r2")
+    assert not ok and "unavailable" in why, why
+    assert time.time() - t0 < 30
+    monkeypatch.delenv("UDA_FAULT_STORE_SETUP")
+    store2 = native.MofStore(capacity=64 * MB, devices=[0])  # a new store's loader starts normally
+    ok, why, a, n, _ = store2.acquire("job", f[0], "r3")
+    assert ok and n == 4 * MB, why

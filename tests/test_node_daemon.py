@@ -1,0 +1,264 @@
+"""CPU tier: the deployment as documented -- a provider front end (the NodeManager's aux service) and
+reduce task processes (one per ReduceTask JVM), both with the library's defaults -- and the node daemon
+that holds the node's GPU state and hosts the reduce tasks' NetMergers.
+
+* Defaults: no mapred.uda.* key on either side. The reduce task fetches over TCP from the provider
+  process (the reference's consumer always builds a network client, src/Merger/reducer.cc:412-437) and
+  merges on the CPU here (mapred.uda.merge.backend=auto: no HIP device).
+* Node daemon (forced on with mapred.uda.daemon=1, since this machine has no GPU driver): reduce tasks
+  with default configuration are hosted by its merge service; a fault injected into one hosted task fails
+  that task only (failureInUda exactly once, the others validated); a daemon killed mid-task fails the
+  hosted task of that moment while the front end keeps serving byte fetches and restarts the daemon.
+* Access: the merge service admits clients by their peer credentials (SO_PEERCRED) against
+  mapred.uda.gpu.merge.service.users.
+
+Reference: src/UdaBridge.cc:506-530 (a native failure falls back for that reducer only),
+plugins/shared/.../UdaShuffleConsumerPluginShared.java:205-232, src/MOFServer/MOFSupplierMain.cc:87-143."""
+import json
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import time
+
+import pytest
+
+from uda_amd.bridge import FETCH, INIT
+from uda_amd.utils import datagen
+from uda_amd.utils.mof import write_mof
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SUP = os.path.join(ROOT, "uda_amd", "bin", "uda_mof_supplier")
+EXE = os.path.join(ROOT, "uda_amd", "bin", "uda_reduce_task")
+pytestmark = pytest.mark.skipif(not (os.access(SUP, os.X_OK) and os.access(EXE, os.X_OK)), reason="apps not built")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class FrontEnd:
+    """uda_mof_supplier mode=frontend: uda_start(provider) with getPathUda over Hadoop-layout MOFs."""
+
+    def __init__(self, mof_dir, port, conf=None):
+        argv = [SUP, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"]
+        for k, v in (conf or {}).items():
+            argv.append(f"-D{k}={v}")
+        self.p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT)
+        line = self.p.stdout.readline()
+        assert line, f"front end exited rc={self.p.poll()}"
+        self.info = json.loads(line)
+        self.port = port
+
+    def stats(self):
+        self.p.stdin.write("stats\n")
+        self.p.stdin.flush()
+        return json.loads(self.p.stdout.readline())
+
+    def close(self):
+        if self.p.poll() is None:
+            try:
+                self.p.stdin.write("exit\n")
+                self.p.stdin.flush()
+                self.p.wait(60)
+            except (OSError, subprocess.TimeoutExpired):
+                self.p.kill()
+                self.p.wait()
+
+
+def _job(tmp_path, job, maps=4, reducers=3, rows=1200, seed=5):
+    d = tmp_path / "mofs"
+    data = datagen.terasort(num_maps=maps, reducers=reducers, rows_per_map=rows, seed=seed)
+    ids = []
+    for i, parts in enumerate(datagen.streams(data)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        write_mof(str(d), mid, parts)
+        ids.append(mid)
+    return str(d), data, ids
+
+
+def _cmds(native, job, ids, r):
+    init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_{r:06d}_0", "0", str(1 << 20),
+                                  str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0", "0"])
+    return [init] + [native.form_cmd(FETCH, ["127.0.0.1", job, m, str(r)]) for m in ids]
+
+
+def _task_argv(port, expect, conf=(), exe=EXE):
+    argv = [exe]
+    for kv in conf:
+        argv += ["-D", kv]
+    return argv + ["--expect", str(expect), "--check-order", "--", "-w", "256", "-r", str(port), "-a", "1",
+                   "-m", "1", "-g", "/tmp", "-s", "1024"]
+
+
+def _run_task(native, port, job, ids, r, expect, conf=(), exe=EXE, **popen):
+    p = subprocess.run(_task_argv(port, expect, conf, exe), input="\n".join(_cmds(native, job, ids, r)) + "\n",
+                       capture_output=True, text=True, timeout=120, **popen)
+    lines = p.stdout.strip().splitlines()
+    assert lines, f"no output, rc={p.returncode}, stderr={p.stderr[-2000:]}"
+    return p.returncode, json.loads(lines[-1])
+
+
+def _want(data, r):
+    return sum(len(m[r]) for m in data)
+
+
+def test_default_configuration_fetches_across_processes(native, tmp_path):
+    """zero mapred.uda.* keys in the provider process and in the reduce task process.
+    Before: loopback transport by default ("no loopback provider for host") and a CPU-only default."""
+    job = "job_50_0001"
+    mof_dir, data, ids = _job(tmp_path, job)
+    port = _port()
+    fe = FrontEnd(mof_dir, port)
+    try:
+        for r in range(3):
+            rc, out = _run_task(native, port, job, ids, r, _want(data, r))
+            assert rc == 0 and out["error"] == "", out
+            assert out["records"] == _want(data, r) and out["order_errors"] == 0
+            t = out["task"]
+            assert t["maps_fetched"] == 4 and t["bytes_fetched"] > 0, t
+            assert t["backend"] == ("gpu" if native.device_count() > 0 else "cpu"), t  # merge.backend=auto
+        st = fe.stats()
+        assert st["port"] == port and st["requests"] >= 12, st
+    finally:
+        fe.close()
+
+
+def _daemon_front(tmp_path, job, conf=None, **kw):
+    mof_dir, data, ids = _job(tmp_path, job, **kw)
+    port = _port()
+    c = {"mapred.uda.daemon": "1"}  # no GPU driver here: force the daemon on (a GPU node starts it by default)
+    c.update(conf or {})
+    fe = FrontEnd(mof_dir, port, c)
+    d = fe.info["provider"]["hbm_store"]["daemon"]
+    assert d["ready"] is True and d["pid"] > 0 and d["service"] == f"@uda-merge-{port}", fe.info
+    return fe, data, ids, port
+
+
+def test_daemon_hosts_default_tasks_and_contains_a_task_fault(native, tmp_path):
+    """Four reduce task processes with default configuration are hosted by the node daemon's merge service;
+    one of them carries an injected fault (its own mapred.uda.fault.inject, applied on its merge thread
+    only): exactly that task fails (failureInUda once), the other three deliver validated streams, and the
+    daemon keeps running."""
+    import concurrent.futures as cf
+    job = "job_50_0002"
+    fe, data, ids, port = _daemon_front(tmp_path, job, reducers=4)
+    try:
+        pid0 = fe.stats()["hbm_store"]["daemon"]["pid"]
+
+        def run(r):
+            conf = ["mapred.uda.fault.inject=FETCH=2"] if r == 2 else []
+            return r, _run_task(native, port, job, ids, r, _want(data, r), conf)
+
+        with cf.ThreadPoolExecutor(4) as ex:
+            outs = dict(ex.map(run, range(4)))
+        for r, (rc, out) in outs.items():
+            if r == 2:
+                assert rc == 1 and "injected fetch failure" in out["error"], out
+            else:
+                assert rc == 0 and out["error"] == "" and out["records"] == _want(data, r), out
+                assert out["task"].get("merge_service") is True, out["task"]
+        st = fe.stats()
+        d = st["hbm_store"]["daemon"]
+        assert d["pid"] == pid0 and d["ready"] is True and d["restarts"] == 0, d
+        ms = st["hbm_store"]["merge_service"]
+        assert ms["sessions"] >= 4 and ms["refused"] == 0, ms
+    finally:
+        fe.close()
+
+
+def test_daemon_death_fails_hosted_tasks_only_and_is_restarted(native, tmp_path):
+    """The daemon dies (SIGKILL, as after a GPU fault) while a hosted task waits for its FETCHes: that task
+    reports the failure and exits; the front end keeps answering byte fetches (a task merging in its own
+    process is served) and restarts the daemon, whose service hosts the next default task."""
+    job = "job_50_0003"
+    fe, data, ids, port = _daemon_front(tmp_path, job)
+    try:
+        pid0 = fe.stats()["hbm_store"]["daemon"]["pid"]
+        cmds = _cmds(native, job, ids, 0)
+        p = subprocess.Popen(_task_argv(port, _want(data, 0)), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, text=True)
+        p.stdin.write(cmds[0] + "\n" + cmds[1] + "\n")  # INIT + one FETCH; the rest never comes
+        p.stdin.flush()
+        time.sleep(1.0)
+        os.kill(pid0, signal.SIGKILL)
+        out, _ = p.communicate(timeout=60)
+        res = json.loads(out.strip().splitlines()[-1])
+        assert p.returncode == 1 and "merge service" in res["error"], res
+        # byte fetches from the front end go on while the daemon is down or restarting
+        rc, out = _run_task(native, port, job, ids, 1, _want(data, 1), ["mapred.uda.gpu.merge.service=off"])
+        assert rc == 0 and out["records"] == _want(data, 1) and "merge_service" not in out["task"], out
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            d = fe.stats()["hbm_store"]["daemon"]
+            if d["ready"]:
+                break
+            time.sleep(0.2)
+        assert d["ready"] is True and d["restarts"] == 1 and d["pid"] not in (0, pid0), d
+        rc, out = _run_task(native, port, job, ids, 2, _want(data, 2))
+        assert rc == 0 and out["task"].get("merge_service") is True, out
+        assert fe.p.poll() is None  # the front end (the NodeManager) never went down
+    finally:
+        fe.close()
+
+
+@pytest.fixture
+def request_cleanup():
+    dirs = []
+    yield dirs
+    for d in dirs:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_merge_service_user_rule(native):
+    me = os.getuid()
+    assert native.merge_service_user_allowed("", me)  # the service's own user always may
+    assert native.merge_service_user_allowed("*", 4242)
+    assert native.merge_service_user_allowed("root,4242", 4242)
+    assert native.merge_service_user_allowed(" nobody ", 65534)
+    assert not native.merge_service_user_allowed("root,4243", 4242)
+    assert not native.merge_service_user_allowed("", 4242)
+    assert native.merge_service_default_path(9011) == "@uda-merge-9011"
+
+
+@pytest.mark.skipif(os.geteuid() != 0, reason="needs root to run a task process as another user")
+def test_merge_service_admits_by_peer_credentials(native, request_cleanup):
+    """A task process of a user outside mapred.uda.gpu.merge.service.users is refused (and merges in its
+    own process); listed, it is hosted. Before: a 0600 socket file silently kept other users out."""
+    # the task binary, its library and the MOFs where user nobody can read them (pytest's tmp_path is
+    # private to root)
+    import pathlib
+    import tempfile
+    tmp_path = pathlib.Path(tempfile.mkdtemp(prefix="uda-peercred-"))
+    request_cleanup.append(tmp_path)
+    app = tmp_path / "app"
+    (app / "bin").mkdir(parents=True)
+    (app / "lib").mkdir()
+    shutil.copy2(EXE, app / "bin" / "uda_reduce_task")
+    shutil.copy2(os.path.join(ROOT, "uda_amd", "lib", "libuda.so"), app / "lib" / "libuda.so")
+    for x in (tmp_path, app, app / "bin", app / "lib"):
+        os.chmod(x, 0o755)
+    exe = str(app / "bin" / "uda_reduce_task")
+
+    def as_nobody():
+        os.setgid(65534)
+        os.setuid(65534)
+
+    for users, hosted in (("root", False), ("root,nobody", True)):
+        job = f"job_50_00{4 if hosted else 5}"
+        sub = tmp_path / job
+        sub.mkdir()
+        os.chmod(sub, 0o755)
+        fe, data, ids, port = _daemon_front(sub, job, {"mapred.uda.gpu.merge.service.users": users})
+        try:
+            os.chmod(sub / "mofs", 0o755)
+            rc, out = _run_task(native, port, job, ids, 0, _want(data, 0), exe=exe, preexec_fn=as_nobody, cwd="/tmp")
+            assert rc == 0 and out["records"] == _want(data, 0), out
+            assert (out["task"].get("merge_service") is True) == hosted, out["task"]
+            ms = fe.stats()["hbm_store"]["merge_service"]
+            assert (ms["refused"] == 0) == hosted, ms
+        finally:
+            fe.close()
