@@ -99,7 +99,9 @@ def parse_args(argv=None):
                          "decode on the device straight from the descriptors (F6)")
     ap.add_argument("--mof-dir", default="",
                     help="--api: write every map output as a file.out under this directory; the provider finds "
-                         "them through getPathUda (Hadoop-written MOFs) and serves them from its HBM store")
+                         "them through getPathUda (Hadoop-written MOFs) and serves them from its HBM store. "
+                         "With --node: the documented deployment end to end (map phase writes the files, provider "
+                         "front end + node daemon with default configuration, reduce tasks with no mapred.uda.* key)")
     ap.add_argument("--provider-hbm-gb", type=float, default=-1.0,
                     help="--api --mof-dir: mapred.uda.provider.hbm.bytes in GB (default: 1.25x the MOF bytes; "
                          "0 = store off: descriptor fetches are declined and reducers fetch bytes)")
@@ -183,7 +185,7 @@ def main(argv=None) -> int:
         print(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)", file=sys.stderr)
         return 2
     if args.api and args.node:  # every GPU call in native processes (this one only orchestrates)
-        return run_node(args, ctx)
+        return run_node_files(args, ctx) if args.mof_dir else run_node(args, ctx)
     if args.api:
         torch.cuda.set_device(0 if args.one_gpu else ctx.local_rank)
         return run_api(args, ctx)
@@ -368,17 +370,35 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
     info = json.loads(first) if first.strip() else {"error": f"supplier exited rc={supplier.poll()}"}
     if "error" in info:
         raise RuntimeError(f"MOF supplier failed: {info['error']}")
-    R, port, cmds, expected = args.reducers, info["port"], info["commands"], info["expected"]
+    R, port = args.reducers, info["port"]
     print(f"# node setup {time.perf_counter() - t:.1f}s store={info['store_bytes'] / 1e9:.1f}GB supplier pid "
           f"{supplier.pid} port {port}, {R} reduce task processes per wave, {args.node_slots} at once",
           file=sys.stderr, flush=True)
     conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.fetch": "device", "mapred.uda.transport": "tcp",
-            "mapred.uda.gpu.device": "auto", "mapred.uda.gpu.round.bytes": str(args.round_mb << 20)}
-    if args.service_path:
-        conf["mapred.uda.gpu.merge.service"] = args.service_path
+            "mapred.uda.gpu.device": "auto", "mapred.uda.gpu.round.bytes": str(args.round_mb << 20),
+            "mapred.uda.gpu.merge.service": args.service_path or "off"}
     for kv in filter(None, os.environ.get("UDA_API_CONF", "").split(",")):
         k, _, v = kv.partition("=")
         conf[k] = v
+    warm, stats, validated = _run_waves(args, port, info["commands"], info["expected"], exe, errlog, conf, sp,
+                                        statistics)
+    supplier.stdin.write("stats\n")
+    supplier.stdin.flush()
+    provider = json.loads(supplier.stdout.readline())
+    out = _node_result(args, stats, warm, validated, provider)
+    out["config"]["shuffle"] = (
+        "node shape: one MOFSupplier process (uda_mof_supplier: map outputs in its HBM, TCP control) + one fresh "
+        "process per reduce task (uda_reduce_task: INIT/FETCH/dataFromUda), " +
+        ("NetMergers hosted by the supplier's merge service, merged buffers read in place from its shared pinned "
+         "rings" if args.service_path else "descriptors mapped over hipIpc"))
+    out["node"]["merge_service"] = bool(args.service_path)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def _run_waves(args, port, cmds, expected, exe, errlog, conf, sp, statistics):
+    """Warmup waves, timed waves and the validated wave of R fresh reduce task processes."""
+    R = args.reducers
     start = ["-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
 
     def wave(validate: bool) -> dict:
@@ -439,21 +459,24 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
                                                        "fetch_to_first_data_ms", "fetch_to_eof_ms", "exit_ms")},
                 "task0": out[0]["task"]}
 
+    warm = []
     for i in range(args.warmup):
-        st = wave(False)
+        warm.append(wave(False))
         if args.verbose:
-            print(f"# warmup {i}: {json.dumps(st)}", file=sys.stderr, flush=True)
+            print(f"# warmup {i}: {json.dumps(warm[-1])}", file=sys.stderr, flush=True)
     stats = [wave(False) for _ in range(args.steps)]
     validated = None
     if not args.no_validate:
         validated = wave(True)["order_errors"] == 0
-    supplier.stdin.write("stats\n")
-    supplier.stdin.flush()
-    provider = json.loads(supplier.stdout.readline())
+    return warm, stats, validated
+
+
+def _node_result(args, stats, warm, validated, provider) -> dict:
+    R = args.reducers
     ms = sum(s["wall_ms"] for s in stats) / len(stats)
     fetch_ms = sum(s["from_fetch_ms"] for s in stats) / len(stats)
     nbytes = stats[0]["bytes"]
-    out = {
+    return {
         "metric": "TeraSort shuffle+merge GB/s whole-node",
         "value": round(nbytes / ms / 1e6, 3),
         "unit": "GB/s",
@@ -471,14 +494,11 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
         "config": {"model": "terasort" if args.workload == "terasort" else "secondary-sort",
                    "global_batch": int(stats[0]["records"]), "seq_len": 104, "parallelism": "dp1",
                    "rows_per_gpu": args.rows_per_gpu, "maps_per_gpu": args.maps_per_gpu, "reducers_per_gpu": R,
-                   "shuffle": "node shape: one MOFSupplier process (uda_mof_supplier: map outputs in its HBM, TCP "
-                              "control) + one fresh process per reduce task (uda_reduce_task: INIT/FETCH/"
-                              "dataFromUda), " + ("NetMergers hosted by the supplier's merge service, merged "
-                                                  "buffers read in place from its shared pinned rings"
-                                                  if args.service_path else "descriptors mapped over hipIpc"),
+                   "shuffle": "",
                    "delivery": "dataFromUda -> J2C consumer (KVBuf memcpy + VInt walk) in each task process"},
-        "node": {"slots": args.node_slots, "gap_s": args.node_gap, "merge_service": bool(args.service_path),
+        "node": {"slots": args.node_slots, "gap_s": args.node_gap,
                  "gbps_from_fetch": round(nbytes / fetch_ms / 1e6, 3), "from_fetch_ms": round(fetch_ms, 1),
+                 "warmup_step_ms": [round(st["wall_ms"], 1) for st in warm],
                  "step_ms": [round(st["wall_ms"], 1) for st in stats],
                  "task_ms_median": stats[-1]["task_ms_median"],
                  "timeline_ms": {"columns": ["exec", "first_fetch", "first_data", "eof", "end"],
@@ -488,8 +508,86 @@ def _node_waves(args, supplier, exe, errlog, statistics, sp) -> int:
         "validated": validated,
         "reference_envelope_gbps_per_node": 5.0,
     }
-    print(json.dumps(out), flush=True)
-    return 0
+
+
+def run_node_files(args, ctx) -> int:
+    """The deployment as documented, end to end, on one GPU node: Hadoop-written map output files, the
+    provider front end (the NodeManager's aux service: uda_mof_supplier mode=frontend, getPathUda over
+    <mof-dir>/<map attempt>/file.out + file.out.index, no GPU call) with the library's defaults -- which
+    start the node daemon holding the HBM store (files loaded on first touch) and the merge service -- and
+    waves of fresh reduce task processes with NO mapred.uda.* key: each is hosted by the daemon's merge
+    service, fetches its partitions as descriptors of the store and reads the merged buffers from its
+    shared pinned rings. The first wave includes reading every MOF file from disk (a job reads each map
+    output once): first_step_gbps; later waves merge from the store."""
+    import shutil
+    import statistics
+    import subprocess as sp
+
+    if ctx.world != 1:
+        print("bench: --node runs one provider per node (--gpus 1)", file=sys.stderr)
+        return 2
+    if os.environ.get("UDA_API_CONF"):
+        print("bench: --node --mof-dir measures the default configuration: unset UDA_API_CONF", file=sys.stderr)
+        return 2
+    bindir = os.path.join(ROOT, "uda_amd", "bin")
+    exe, sup = os.path.join(bindir, "uda_reduce_task"), os.path.join(bindir, "uda_mof_supplier")
+    R = args.reducers
+    logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+    errlog = open(os.path.join(logdir, "node_tasks.err"), "a")
+    mof_dir = os.path.join(args.mof_dir, f"uda-node-{os.getpid()}")
+    os.makedirs(mof_dir, exist_ok=True)
+    frontend = None
+    try:
+        t = time.perf_counter()
+        g = sp.run([sup, "mode=mapgen", f"mof_dir={mof_dir}", "device=0", f"maps={args.maps_per_gpu}",
+                    f"reducers={R}", f"records_per_map={max(1, args.rows_per_gpu // args.maps_per_gpu)}",
+                    f"workload={args.workload}", f"skew={args.skew}"],
+                   stdout=sp.PIPE, stderr=errlog, text=True, cwd=ROOT, timeout=1800)
+        lines = g.stdout.strip().splitlines()
+        job = json.loads(lines[-1]) if lines else {"error": f"map phase exited rc={g.returncode}"}
+        if g.returncode != 0 or "error" in job:
+            raise RuntimeError(f"map phase failed: {job.get('error')}")
+        t_map = time.perf_counter() - t
+        port = _free_port()
+        t = time.perf_counter()
+        frontend = sp.Popen([sup, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"], stdin=sp.PIPE,
+                            stdout=sp.PIPE, stderr=errlog, text=True, cwd=ROOT,
+                            env=dict(os.environ, UDA_DAEMON_LOG=os.path.join(logdir, "node_daemon.err")))
+        first = frontend.stdout.readline()
+        info = json.loads(first) if first.strip() else {"error": f"front end exited rc={frontend.poll()}"}
+        if "error" in info:
+            raise RuntimeError(f"provider front end failed: {info['error']}")
+        daemon = info["provider"].get("hbm_store", {}).get("daemon", {})
+        print(f"# node files: map phase {t_map:.1f}s ({job['store_bytes'] / 1e9:.1f} GB in {args.maps_per_gpu} "
+              f"file.out), front end up in {time.perf_counter() - t:.1f}s, node daemon {daemon}", file=sys.stderr,
+              flush=True)
+        warm, stats, validated = _run_waves(args, port, job["commands"], job["expected"], exe, errlog, {}, sp,
+                                            statistics)
+        frontend.stdin.write("stats\n")
+        frontend.stdin.flush()
+        provider = json.loads(frontend.stdout.readline())
+        out = _node_result(args, stats, warm, validated, provider)
+        out["config"]["shuffle"] = (
+            "the documented deployment: Hadoop-layout MOF files -> provider front end (getPathUda, defaults) -> "
+            "node daemon (HBM store, merge service) -> fresh reduce task processes with no mapred.uda.* keys")
+        waves = warm + stats
+        out["first_step_ms"] = round(waves[0]["wall_ms"], 1)
+        out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
+        out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)
+        out["conf_keys"] = 0
+        out["task0_hosted"] = bool(stats[-1]["task0"].get("merge_service"))
+        print(json.dumps(out), flush=True)
+        return 0
+    finally:
+        if frontend is not None and frontend.poll() is None:
+            try:
+                frontend.stdin.write("exit\n")
+                frontend.stdin.flush()
+                frontend.wait(120)
+            except (OSError, sp.TimeoutExpired):
+                frontend.kill()
+                frontend.wait()
+        shutil.rmtree(mof_dir, ignore_errors=True)
 
 
 def run_api(args, ctx) -> int:

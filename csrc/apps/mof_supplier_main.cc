@@ -198,6 +198,8 @@ int main(int argc, char** argv) {
   try {
     if (mode == "mapgen") {
       if (c.mof_dir.empty()) throw std::runtime_error("mode=mapgen needs mof_dir=");
+      if (c.workload != "terasort" || !c.codec.empty())
+        throw std::runtime_error("mode=mapgen writes uncompressed TeraSort map outputs only");
       c.start_provider = false;
       c.keep_mof_files = true;
       uda::gpu::ApiTeraSortBench b(c);

@@ -2,6 +2,7 @@
 // (src/UdaBridge.cc:187-263): is_net_merger selects the NetMerger (ReduceTask) or the MOFSupplier.
 #include "uda/uda_bridge.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -165,7 +166,12 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
         dopt.data_port = h->supplier->port();
         dopt.start_timeout_s = h->host->conf_f64("mapred.uda.daemon.start.timeout.s", 120);
         dopt.max_restarts = (int)h->host->conf_i64("mapred.uda.daemon.restarts", 3);
-        dopt.log_path = h->host->get_conf("mapred.uda.daemon.log", "");
+        // the daemon's own stderr (HIP runtime messages, a crash's last words); its log lines go to ours
+        const char* env_log = std::getenv("UDA_DAEMON_LOG");
+        dopt.log_path = h->host->get_conf("mapred.uda.daemon.log",
+                                          env_log ? env_log
+                                                  : (h->opt.log_dir.empty() ? std::string("/tmp") : h->opt.log_dir) +
+                                                        "/udaNodeDaemon.log");
         h->daemon = std::make_shared<uda::NodeDaemonClient>(dopt, h->host.get());
         h->supplier->set_store(h->daemon);
       }

@@ -168,8 +168,13 @@ bool NodeDaemonClient::spawn() {
   posix_spawn_file_actions_init(&fa);
   posix_spawn_file_actions_adddup2(&fa, sv[1], child_fd);
   posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
-  posix_spawn_file_actions_addopen(&fa, 1, opt_.log_path.empty() ? "/dev/null" : opt_.log_path.c_str(),
-                                   O_WRONLY | O_CREAT | O_APPEND, 0644);
+  std::string log = opt_.log_path.empty() ? std::string("/dev/null") : opt_.log_path;
+  if (const int probe = ::open(log.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644); probe >= 0) {
+    ::close(probe);
+  } else {
+    log = "/dev/null";  // an unwritable log must not keep the daemon from starting
+  }
+  posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
   posix_spawn_file_actions_adddup2(&fa, 1, 2);
   posix_spawnattr_t attr;
   posix_spawnattr_init(&attr);
@@ -196,8 +201,8 @@ bool NodeDaemonClient::spawn() {
   }
   uint64_t gen;
   {
+    std::lock_guard<std::mutex> gs(send_mu_);  // lock order: send_mu_, then mu_ (as in send())
     std::lock_guard<std::mutex> g(mu_);
-    std::lock_guard<std::mutex> gs(send_mu_);
     if (fd_ >= 0) ::close(fd_);
     fd_ = sv[0];
     gen = ++gen_;

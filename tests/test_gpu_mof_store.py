@@ -197,3 +197,26 @@ def test_store_declines_after_an_injected_loader_setup_failure(require_gpu, nati
     store2 = native.MofStore(capacity=64 * MB, devices=[0])  # a new store's loader starts normally
     ok, why, a, n, _ = store2.acquire("job", f[0], "r3")
     assert ok and n == 4 * MB, why
+
+
+def test_bench_node_files_default_configuration(require_gpu, tmp_path):
+    """bench.py --api --node --mof-dir: Hadoop-layout MOF files, the provider front end with the library's
+    defaults (it starts the node daemon: HBM store + merge service) and reduce task processes with no
+    mapred.uda.* key -- each hosted by the daemon, merging the store's copies of the files in place."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "UDA_API_CONF"}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--api", "--node", "--mof-dir", str(tmp_path), "--reducers",
+           "3", "--rows-per-gpu", "3000000", "--maps-per-gpu", "6", "--steps", "1", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["validated"] is True and out["conf_keys"] == 0, out
+    t0 = out["task0_stats"]
+    assert out["task0_hosted"] and t0["backend"] == "gpu" and t0["device_descriptors"] == 6, t0
+    assert t0["host_fetched_bytes"] == 0, t0
+    hs = out["provider"]["hbm_store"]
+    assert hs["daemon"]["ready"] and hs["loads"] == 6 and hs["merge_service"]["sessions"] >= 9, hs
+    assert hs["holders"] == 0, hs  # every hosted task released its descriptors (or its session did)
+    assert not os.listdir(tmp_path), "the map outputs are removed after the run"

@@ -47,6 +47,8 @@ RECIPES: dict[str, tuple[int, str]] = {
     "node": (600, f"{PY} bench.py --api --node --no-node-service --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "node130": (700, f"{PY} bench.py --api --node --no-node-service --reducers 15 --steps 2 --warmup 1"),
     "node_gap": (600, f"{PY} bench.py --api --node --reducers 15 --node-gap 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles41": (900, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles62": (1000, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 600000000 --steps 2 --warmup 1"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
     "coldnode": (400, f"{PY} tools/cold_task_bench.py --node --repeat 3"),
