@@ -115,6 +115,7 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
       so.io_threads = (int)h->host->conf_i64("mapred.uda.provider.blocked.threads.per.disk", 4);
       so.workers = (int)h->host->conf_i64("mapred.uda.provider.workers", 8);
       so.odirect = h->host->conf_bool("mapred.uda.provider.odirect", false);
+      so.copy_serve = h->host->conf_bool("mapred.uda.provider.copy.serve", false);
       // The node daemon (node_daemon.h) holds the node's GPU state: the HBM store of MOF files and the
       // merge service. "auto": on a node with a GPU driver and the TCP transport (the loopback transport
       // only reaches reducers in this very process).

@@ -206,7 +206,7 @@ int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off
     req.map_id = f.map_id;
     req.reduce_id = f.reduce_id;
     req.fetched = at;
-    req.buf_len = std::min(buffer_size_, end - at);
+    req.buf_len = std::min(direct_chunk_, end - at);
     const int64_t want = req.buf_len;
     fetch_begin();
     const int64_t ti = trace::host_enabled() ? trace::now_ns() : 0;
@@ -225,7 +225,7 @@ int64_t ReduceTask::fetch_direct(const FetchParams& f, uint8_t* dst, int64_t off
   for (;;) {
     while (next < end && inflight < depth && err.empty() && !stop_) {
       const int64_t at = next;
-      next += std::min(buffer_size_, end - at);
+      next += std::min(direct_chunk_, end - at);
       ++inflight;
       lk.unlock();
       issue(at);  // a transport may complete inline
@@ -395,6 +395,9 @@ void ReduceTask::on_init(const InitParams& p) {
   if (fault_hit("HOST_ALLOC")) throw UdaError("injected allocation failure for the fetch buffer pool");
   kv_buf_size_ = host_->conf_i64("mapred.uda.kv.buf.size", 1 << 20);
   fault_spec_ = host_->get_conf("mapred.uda.fault.inject", "");
+  // fetches straight into a partition-sized destination (the GPU staged path) are not bound to the
+  // double-buffer size: larger requests mean fewer answers to frame and dispatch per byte
+  direct_chunk_ = std::max<int64_t>(buffer_size_, host_->conf_i64("mapred.uda.fetch.request.bytes", 4 << 20));
   // "auto" (default): the GPU merge when this process sees a HIP device, else the CPU (reference) merge
   backend_ = host_->get_conf("mapred.uda.merge.backend", "auto");
   if (backend_ == "auto") {
@@ -405,7 +408,9 @@ void ReduceTask::on_init(const InitParams& p) {
   // the reference's consumer always fetches over the network from the providers (RdmaClient,
   // src/Merger/reducer.cc:412-437); loopback only reaches a provider in this very process
   const std::string tr = host_->get_conf("mapred.uda.transport", "tcp");
-  transport_ = (tr == "loopback") ? make_loopback_client() : make_tcp_client(net_.data_port, net_.wqes_per_conn);
+  transport_ = (tr == "loopback") ? make_loopback_client()
+                                  : make_tcp_client(net_.data_port, net_.wqes_per_conn,
+                                                    (int)host_->conf_i64("mapred.uda.tcp.connections", 4));
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.backend = backend_;

@@ -150,6 +150,7 @@ class ReduceTask {
   KeyKind kind_ = KeyKind::kText;
   Codec codec_ = Codec::kNone;
   int64_t buffer_size_ = 0;        // per fetch buffer (pair = 2 of these)
+  int64_t direct_chunk_ = 0;       // request size of fetch_direct (mapred.uda.fetch.request.bytes, >= buffer_size_)
   int64_t fetch_buf_ = 0;          // fetch chunk (== buffer_size_ uncompressed, the "rdma" half when compressed)
   int64_t kv_buf_size_ = 1 << 20;  // delivery buffer (NETLEV_KV_POOL_EXPO)
   int num_kv_bufs_ = 0;

@@ -70,6 +70,24 @@ class DataServer {
  public:
   virtual ~DataServer() = default;
   virtual void serve(const FetchRequest& req, uint8_t* dst, FetchDone done) = 0;
+
+  // The bytes of a byte fetch by reference, for a transport that sends them itself instead of copying
+  // them into a buffer first: memory (ptr) or a file range (fd, file_off: sendfile). release() runs once
+  // the transport is done with them (always, whatever happened to the connection).
+  struct Bytes {
+    const uint8_t* ptr = nullptr;
+    int fd = -1;
+    int64_t file_off = 0;
+    std::function<void()> release;
+  };
+  using RefDone = std::function<void(const FetchAck& ack, Bytes bytes)>;
+  // Serve `req` by reference (ack.sent bytes in `bytes`). false: this server cannot (the transport uses
+  // serve() with a buffer of its own).
+  virtual bool serve_ref(const FetchRequest& req, RefDone done) {
+    (void)req;
+    (void)done;
+    return false;
+  }
 };
 
 // Client side.
@@ -102,7 +120,10 @@ std::unique_ptr<ServerTransport> make_loopback_server(const std::string& host);
 // bind_addr: IPv4 listen address ("" = any). Several providers on one host (one per GPU) listen on
 // the same port at different addresses, as providers on different hosts do.
 std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr = std::string());
-std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits);
+// connections: sockets per provider host; requests go to the one with the fewest in flight (the
+// credits apply per socket). One stream over loopback or a NIC queue moves ~5 GB/s; several move the
+// partition bytes in parallel (the reference spreads them over RDMA QPs of one connection).
+std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits, int connections = 4);
 // A process hosting both a provider and reduce tasks (the node merge service): TCP fetches that name a
 // provider of this process (a local address and its port) are served in process, zero-copy.
 void set_tcp_local_bypass(bool on);

@@ -93,6 +93,16 @@ void Supplier::serve(const FetchRequest& req, uint8_t* dst, FetchDone done) {
   done(a);
 }
 
+bool Supplier::serve_ref(const FetchRequest& req, RefDone done) {
+  if (req.buf_len <= 0) return false;  // descriptor fetches and releases carry no bytes
+  if (opt_.copy_serve) return false;  // A/B: every answer through a chunk copy
+  std::lock_guard<std::mutex> g(mu_);
+  if (stop_) return false;  // serve() answers it (with the stopped error)
+  q_.push_back(Job{req, nullptr, nullptr, std::move(done)});
+  cv_.notify_one();
+  return true;
+}
+
 void Supplier::worker() {
   for (;;) {
     Job j;
@@ -104,12 +114,18 @@ void Supplier::worker() {
       q_.pop_front();
     }
     try {
-      process(j);
+      if (j.ref_done)
+        process_ref(j);
+      else
+        process(j);
     } catch (const std::exception& e) {
       FetchAck a;
       a.status = -9;
       a.error = e.what();
-      j.done(a);
+      if (j.ref_done)
+        j.ref_done(a, Bytes{});
+      else
+        j.done(a);
     }
   }
 }
@@ -311,6 +327,88 @@ void Supplier::process(Job& j) {
       done(ack);
     });
   }
+}
+
+}  // namespace uda
+
+namespace uda {
+
+void Supplier::process_ref(Job& j) {
+  requests_++;
+  IndexRec rec;
+  const MemMof* mem = nullptr;
+  FetchAck ack;
+  RefDone done = std::move(j.ref_done);
+  if (!resolve(j.req, &rec, &mem)) {
+    ack.status = -2;
+    ack.error = "cannot resolve MOF " + j.req.job_id + "/" + j.req.map_id + "/" + std::to_string(j.req.reduce_id);
+    return done(ack, Bytes{});
+  }
+  if ((int)rec.path.size() > kMofPathMax) {
+    ack.status = -3;
+    ack.error = "MOF path too long";
+    return done(ack, Bytes{});
+  }
+  ack.raw_len = rec.raw_length;
+  ack.part_len = rec.part_length;
+  ack.mof_offset = rec.start_offset;
+  ack.path = rec.path;
+  const int64_t len = std::max<int64_t>(0, std::min<int64_t>(rec.part_length - j.req.fetched, j.req.buf_len));
+  ack.sent = len;
+  const int64_t off = rec.start_offset + j.req.fetched;
+  if (len == 0) return done(ack, Bytes{});
+  if (mem) {
+    if (off + len > mem->len) {
+      ack.status = -4;
+      ack.error = "index beyond registered MOF";
+      return done(ack, Bytes{});
+    }
+    Bytes b;
+    if (mem->device < 0) {
+      b.ptr = mem->data + off;  // the registered memory itself goes to the socket
+    } else {
+      uint8_t* chunk = new uint8_t[(size_t)len];
+      gpu::copy_device_to_host(chunk, mem->data + off, len);
+      b.ptr = chunk;
+      b.release = [chunk] { delete[] chunk; };
+    }
+    bytes_ += len;
+    return done(ack, std::move(b));
+  }
+  const int fd = acquire_fd(rec.path);
+  if (fd < 0) {
+    ack.status = -5;
+    ack.error = "cannot open " + rec.path + ": " + strerror(errno);
+    return done(ack, Bytes{});
+  }
+  const std::string path = rec.path;
+  if (!opt_.odirect) {
+    // a file range: the transport sends it from the page cache (sendfile), no copy through this process
+    Bytes b;
+    b.fd = fd;
+    b.file_off = off;
+    b.release = [this, path] { release_fd(path); };
+    bytes_ += len;
+    return done(ack, std::move(b));
+  }
+  // O_DIRECT: aligned read into a bounce chunk, sent from there
+  const int64_t aoff = off - off % kAioAlignment;
+  const int64_t alen = ((off + len - aoff) + kAioAlignment - 1) / kAioAlignment * kAioAlignment;
+  uint8_t* bounce = (uint8_t*)aligned_alloc_io((size_t)alen);
+  aio_->read(fd, aoff, alen, bounce, [this, bounce, off, aoff, len, ack, done, path](int64_t r) mutable {
+    release_fd(path);
+    if (r < off - aoff + len) {
+      aligned_free_io(bounce);
+      ack.status = -6;
+      ack.error = "short read";
+      return done(ack, Bytes{});
+    }
+    bytes_ += len;
+    Bytes b;
+    b.ptr = bounce + (off - aoff);
+    b.release = [bounce] { aligned_free_io(bounce); };
+    done(ack, std::move(b));
+  });
 }
 
 }  // namespace uda

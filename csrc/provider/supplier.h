@@ -34,6 +34,7 @@ class Supplier : public DataServer {
     int workers = 8;             // DataEngine threads (mapred.uda.provider.workers)
     int io_threads = 4;          // AsyncIO pool size (blocked.threads.per.disk analogue)
     bool odirect = false;        // read MOF files with O_DIRECT (4 KiB aligned bounce chunks)
+    bool copy_serve = false;     // mapred.uda.provider.copy.serve: no by-reference answers (A/B of serve_ref)
     int max_open_files = 512;    // fd cache bound (rlimit analogue)
     std::string transport = "loopback";  // loopback | tcp
     std::string loopback_host = "*";
@@ -62,6 +63,9 @@ class Supplier : public DataServer {
   void register_mof(const std::string& job, const std::string& map, const uint8_t* data, int64_t len,
                     std::vector<IndexRec> index, int device = -1);
   void serve(const FetchRequest& req, uint8_t* dst, FetchDone done) override;
+  // Byte fetches by reference (the TCP transport's zero-copy send): host-memory MOFs as they lie, MOF
+  // files as a file range (sendfile); HBM MOFs and O_DIRECT reads through a chunk of this request's own.
+  bool serve_ref(const FetchRequest& req, RefDone done) override;
 
   int port() const { return server_ ? server_->port() : -1; }
   int64_t requests() const { return requests_.load(); }
@@ -78,6 +82,7 @@ class Supplier : public DataServer {
     FetchRequest req;
     uint8_t* dst;
     FetchDone done;
+    RefDone ref_done;  // serve_ref: answer by reference (dst and done unused)
   };
   struct MemMof {
     const uint8_t* data;
@@ -94,6 +99,7 @@ class Supplier : public DataServer {
   };
   void worker();
   void process(Job& j);
+  void process_ref(Job& j);
   bool resolve(const FetchRequest& req, IndexRec* rec, const MemMof** mem);
   int acquire_fd(const std::string& path);
   void release_fd(const std::string& path);

@@ -37,6 +37,7 @@
 #include "uda/vint.h"
 #include "uda/shm_group.h"
 #include "uda/node_registry.h"
+#include "uda/transport.h"
 #include "../gpu/hbm_ledger.h"
 #include <atomic>
 #include <thread>
@@ -741,6 +742,64 @@ PYBIND11_MODULE(_uda_native, m) {
     return MergeService::user_allowed(users, (uid_t)uid);
   });
   m.def("merge_service_default_path", &MergeService::default_path);
+  // fetch throughput of the TCP transport alone: every listed partition fetched whole into one buffer,
+  // `maps_at_once` partitions at a time with `depth` requests of `chunk` bytes in flight each
+  m.def("tcp_fetch_probe", [](const std::string& host, int port, const std::string& job,
+                              const std::vector<std::string>& maps, int reduce, const std::vector<int64_t>& sizes,
+                              int64_t chunk, int depth, int connections, int maps_at_once) {
+    auto nogil = std::make_unique<py::gil_scoped_release>();
+    auto cl = make_tcp_client(port, 256, connections);
+    int64_t total = 0;
+    std::vector<int64_t> base(maps.size() + 1, 0);
+    for (size_t i = 0; i < maps.size(); ++i) base[i + 1] = base[i] + sizes[i];
+    total = base.back();
+    std::unique_ptr<uint8_t[]> buf(new uint8_t[(size_t)std::max<int64_t>(total, 1)]);
+    std::mutex m;
+    std::condition_variable cv;
+    std::string err;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::atomic<size_t> next_map{0};
+    std::vector<std::thread> ts;
+    for (int w = 0; w < std::max(1, maps_at_once); ++w)
+      ts.emplace_back([&] {
+        for (size_t i; (i = next_map++) < maps.size();) {
+          int inflight = 0;
+          int64_t at = 0;
+          std::unique_lock<std::mutex> lk(m);
+          while (at < sizes[i] || inflight > 0) {
+            while (at < sizes[i] && inflight < depth && err.empty()) {
+              FetchRequest rq;
+              rq.job_id = job;
+              rq.map_id = maps[i];
+              rq.reduce_id = reduce;
+              rq.fetched = at;
+              rq.buf_len = std::min(chunk, sizes[i] - at);
+              at += rq.buf_len;
+              ++inflight;
+              lk.unlock();
+              cl->fetch(host, rq, buf.get() + base[i] + rq.fetched, [&](const FetchAck& a) {
+                std::lock_guard<std::mutex> g(m);
+                if (a.status != 0 && err.empty()) err = a.error;
+                --inflight;
+                cv.notify_all();
+              });
+              lk.lock();
+            }
+            if (!err.empty() && inflight == 0) break;
+            cv.wait(lk, [&] { return inflight == 0 || (at < sizes[i] && inflight < depth && err.empty()); });
+            if (!err.empty() && inflight == 0) break;
+          }
+        }
+      });
+    for (auto& t : ts) t.join();
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    cl->close();
+    uint64_t sum = 0;
+    for (int64_t k = 0; k < total; k += 4096) sum += buf[(size_t)k];
+    nogil.reset();  // the GIL again before any Python object is made
+    if (!err.empty()) throw std::runtime_error("tcp_fetch_probe: " + err);
+    return py::make_tuple(total, s, sum);
+  });
   m.def("open_ipc_mappings", &gpu::open_ipc_mappings);
   m.def("device_read", [](uint64_t addr, int64_t len) {  // device bytes back to the host (tests)
     std::string out((size_t)len, '\0');

@@ -10,6 +10,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -55,10 +56,10 @@ bool read_full(int fd, void* p, size_t n) {
   return true;
 }
 
-bool write_full(int fd, const void* p, size_t n) {
+bool write_full(int fd, const void* p, size_t n, int flags = 0) {
   const uint8_t* b = (const uint8_t*)p;
   while (n) {
-    ssize_t r = ::send(fd, b, n, MSG_NOSIGNAL);
+    ssize_t r = ::send(fd, b, n, MSG_NOSIGNAL | flags);
     if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     b += r;
@@ -202,22 +203,56 @@ class TcpServer : public ServerTransport {
       if (h.type != kMsgRts) continue;
       FetchRequest req;
       if (!parse_rts(std::string(payload.data(), payload.size()), &req, nullptr, nullptr)) continue;
-      // chunk for the data (the provider's registered chunk, NETLEV_RDMA_MEM_CHUNKS_NUM pool)
-      auto chunk = std::make_shared<std::vector<uint8_t>>((size_t)std::max<int64_t>(0, req.buf_len));
       {
         std::unique_lock<std::mutex> lk(c->mu);
         c->cv.wait(lk, [&] { return c->inflight < credits_; });
         c->inflight++;
       }
       const uint64_t id = h.src_req;
-      server_->serve(req, chunk->data(), [c, chunk, id](const FetchAck& a) {
+      // by reference first: the provider's memory or the MOF file goes to the socket as it is (send /
+      // sendfile), instead of being copied into a chunk and then into the socket
+      if (req.buf_len > 0 && server_->serve_ref(req, [c, id](const FetchAck& a, DataServer::Bytes b) {
+            const std::string ack = format_ack(a);
+            const uint32_t ack_len = (uint32_t)ack.size();
+            const uint64_t data_len = a.status == 0 ? (uint64_t)a.sent : 0;
+            Header r{kMsgAck, 1, 0, (uint32_t)(4 + ack_len + data_len), id};
+            {
+              std::lock_guard<std::mutex> g(c->mu);
+              const int more = data_len ? MSG_MORE : 0;
+              bool ok = write_full(c->fd, &r, sizeof(r), MSG_MORE) && write_full(c->fd, &ack_len, 4, MSG_MORE) &&
+                        write_full(c->fd, ack.data(), ack_len, more);
+              if (ok && data_len) {
+                if (b.ptr) {
+                  ok = write_full(c->fd, b.ptr, data_len);
+                } else {
+                  off_t off = (off_t)b.file_off;
+                  for (uint64_t left = data_len; ok && left > 0;) {
+                    const ssize_t w = ::sendfile(c->fd, b.fd, &off, (size_t)std::min<uint64_t>(left, 1u << 30));
+                    if (w < 0 && errno == EINTR) continue;
+                    if (w <= 0) ok = false;  // error, or the file is shorter than its index says
+                    else left -= (uint64_t)w;
+                  }
+                }
+              }
+              if (!ok) ::shutdown(c->fd, SHUT_RDWR);
+              c->inflight--;
+              c->cv.notify_all();
+            }
+            if (b.release) b.release();
+          }))
+        continue;
+      // a chunk of the request's size for the bytes (the provider's registered chunk,
+      // NETLEV_RDMA_MEM_CHUNKS_NUM pool); not zero-filled, every byte sent is written first
+      std::shared_ptr<uint8_t[]> chunk(new uint8_t[(size_t)std::max<int64_t>(1, req.buf_len)]);
+      server_->serve(req, chunk.get(), [c, chunk, id](const FetchAck& a) {
         std::string ack = format_ack(a);
         const uint32_t ack_len = (uint32_t)ack.size();
         const uint64_t data_len = a.status == 0 ? (uint64_t)a.sent : 0;
         Header r{kMsgAck, 1, 0, (uint32_t)(4 + ack_len + data_len), id};
         std::lock_guard<std::mutex> g(c->mu);
-        bool ok = write_full(c->fd, &r, sizeof(r)) && write_full(c->fd, &ack_len, 4) &&
-                  write_full(c->fd, ack.data(), ack_len) && (data_len == 0 || write_full(c->fd, chunk->data(), data_len));
+        bool ok = write_full(c->fd, &r, sizeof(r), MSG_MORE) && write_full(c->fd, &ack_len, 4, MSG_MORE) &&
+                  write_full(c->fd, ack.data(), ack_len, data_len ? MSG_MORE : 0) &&
+                  (data_len == 0 || write_full(c->fd, chunk.get(), data_len));
         if (!ok) ::shutdown(c->fd, SHUT_RDWR);
         c->inflight--;
         c->cv.notify_all();
@@ -241,7 +276,8 @@ class TcpServer : public ServerTransport {
 // ------------------------------------------------------------------------------------ client
 class TcpClient : public ClientTransport {
  public:
-  TcpClient(int port, int credits) : port_(port), credits_(credits > 0 ? credits : 1) {}
+  TcpClient(int port, int credits, int connections)
+      : port_(port), credits_(credits > 0 ? credits : 1), nconn_(std::max(1, connections)) {}
   ~TcpClient() override { close(); }
 
   void fetch(const std::string& host, const FetchRequest& req, uint8_t* dst, FetchDone done) override {
@@ -289,6 +325,7 @@ class TcpClient : public ClientTransport {
         return;
       }
       c->pending[id] = Pending{dst, req.buf_len, std::move(done)};
+      c->inflight++;
       Header h{kMsgRts, (uint8_t)credits_, 0, (uint32_t)rts.size(), id};
       if (!write_full(c->fd, &h, sizeof(h)) || !write_full(c->fd, rts.data(), rts.size())) {
         c->dead = true;
@@ -301,8 +338,12 @@ class TcpClient : public ClientTransport {
     std::vector<std::shared_ptr<Conn>> cs;
     {
       std::lock_guard<std::mutex> g(mu_);
-      for (auto& kv : conns_) cs.push_back(kv.second);
+      for (auto& kv : conns_)
+        for (auto& c : kv.second)
+          if (c) cs.push_back(c);
       conns_.clear();
+      for (auto& c : retired_) cs.push_back(c);
+      retired_.clear();
     }
     for (auto& c : cs) {
       ::shutdown(c->fd, SHUT_RDWR);
@@ -323,7 +364,8 @@ class TcpClient : public ClientTransport {
     std::mutex mu;
     std::condition_variable cv;
     std::map<uint64_t, Pending> pending;
-    bool dead = false;
+    std::atomic<bool> dead{false};
+    std::atomic<size_t> inflight{0};  // requests sent, answer not yet read (the least loaded takes the next)
     std::thread reader;
   };
 
@@ -362,10 +404,37 @@ class TcpClient : public ClientTransport {
     return it == local_servers().end() ? nullptr : it->second;
   }
 
+  // The live connection to host_spec with the fewest requests in flight; the host's connections are
+  // opened on first use, a lost one is reopened when its turn comes.
   std::shared_ptr<Conn> connect(const std::string& host_spec) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = conns_.find(host_spec);
-    if (it != conns_.end() && !it->second->dead) return it->second;
+    auto& v = conns_[host_spec];
+    if (v.empty()) v.resize((size_t)nconn_);
+    std::shared_ptr<Conn> best;
+    size_t best_load = SIZE_MAX;
+    std::string err;
+    for (auto& c : v) {
+      if (!c || c->dead.load()) {
+        if (c && c->reader.joinable()) retired_.push_back(c);  // its reader has failed its requests
+        c.reset();
+        try {
+          c = open_conn(host_spec);
+        } catch (const std::exception& e) {
+          err = e.what();  // another connection of the host may do
+          continue;
+        }
+      }
+      const size_t load = c->inflight.load();
+      if (load < best_load) {
+        best = c;
+        best_load = load;
+      }
+    }
+    if (!best) throw std::runtime_error(err.empty() ? "cannot connect to " + host_spec : err);
+    return best;
+  }
+
+  std::shared_ptr<Conn> open_conn(const std::string& host_spec) {
     std::string host = host_spec;
     int port = port_;
     auto colon = host_spec.rfind(':');
@@ -393,7 +462,6 @@ class TcpClient : public ClientTransport {
     auto c = std::make_shared<Conn>();
     c->fd = fd;
     c->reader = std::thread([c] { reader(c); });
-    conns_[host_spec] = c;
     return c;
   }
 
@@ -414,6 +482,7 @@ class TcpClient : public ClientTransport {
         c->pending.erase(it);
       }
       c->cv.notify_all();
+      // (inflight drops once the bytes are read: a connection still streaming an answer is busy)
       FetchAck a;
       if (!parse_ack(ack, &a)) {
         a.status = -10;
@@ -421,12 +490,14 @@ class TcpClient : public ClientTransport {
       }
       const uint64_t data_len = (uint64_t)h.tot_len - 4 - ack_len;
       if (data_len > (uint64_t)p.cap || (data_len && !read_full(c->fd, p.dst, data_len))) {
+        c->inflight--;
         FetchAck e;
         e.status = -8;
         e.error = "bad or truncated response";
         p.done(e);
         break;
       }
+      c->inflight--;
       p.done(a);  // data landed zero-copy in the client buffer
     }
     // connection lost: fail everything pending
@@ -449,7 +520,9 @@ class TcpClient : public ClientTransport {
   int credits_;
   std::atomic<uint64_t> next_id_{1};
   std::mutex mu_;
-  std::unordered_map<std::string, std::shared_ptr<Conn>> conns_;
+  int nconn_;
+  std::unordered_map<std::string, std::vector<std::shared_ptr<Conn>>> conns_;
+  std::vector<std::shared_ptr<Conn>> retired_;  // lost connections, joined and closed at close()
   std::unordered_map<std::string, std::pair<uint32_t, int>> resolved_;  // host spec -> (IPv4, port)
 };
 }  // namespace
@@ -459,8 +532,8 @@ void set_tcp_local_bypass(bool on) { g_local_bypass.store(on); }
 std::unique_ptr<ServerTransport> make_tcp_server(int port, int credits, const std::string& bind_addr) {
   return std::make_unique<TcpServer>(port, credits > 0 ? credits : 256, bind_addr);
 }
-std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits) {
-  return std::make_unique<TcpClient>(default_port, credits);
+std::unique_ptr<ClientTransport> make_tcp_client(int default_port, int credits, int connections) {
+  return std::make_unique<TcpClient>(default_port, credits, connections);
 }
 
 }  // namespace uda

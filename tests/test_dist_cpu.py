@@ -209,3 +209,43 @@ def test_tcp_providers_share_a_port_on_distinct_addresses():
     finally:
         for p in provs:
             p.close()
+
+
+def test_tcp_connections_and_by_reference_answers(native, tmp_path):
+    """Several TCP connections per provider (mapred.uda.tcp.connections) and answers sent by reference
+    (sendfile of the MOF file, the registered memory itself) deliver the same bytes as one connection
+    with chunk copies; every byte lands at its offset (out-of-order completions across connections)."""
+    import random
+    import socket
+    import zlib
+    from uda_amd.bridge import UdaProvider
+    from uda_amd.utils.mof import write_index
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    rnd = random.Random(7)
+    sizes = [rnd.randrange(1, 3 << 20) for _ in range(6)]
+    blobs = [rnd.randbytes(n) for n in sizes]
+    for copy in ("0", "1"):
+        p = UdaProvider(transport="tcp", data_port=port,
+                        conf={"mapred.uda.provider.bind.address": "127.0.0.1", "mapred.uda.daemon": "0",
+                              "mapred.uda.provider.copy.serve": copy})
+        try:
+            ids = []
+            for i, b in enumerate(blobs):
+                if i % 2:
+                    p.add_mof_memory("job_tcp", f"m{i}", b, [(0, len(b), len(b))])
+                else:
+                    d = tmp_path / f"m{i}"
+                    d.mkdir(exist_ok=True)
+                    (d / "file.out").write_bytes(b)
+                    write_index(str(d / "file.out.index"), [(0, len(b), len(b))])
+                    p.add_mof_file("job_tcp", f"m{i}", str(d / "file.out"))
+                ids.append(f"m{i}")
+            want = sum(b[k] for b in [b"".join(blobs)] for k in range(0, len(b), 4096))
+            for conns, chunk, depth, par in ((1, 1 << 20, 1, 1), (4, 256 << 10, 4, 3), (3, 1 << 20, 8, 6)):
+                tot, sec, got = native.tcp_fetch_probe("127.0.0.1", port, "job_tcp", ids, 0, sizes, chunk, depth,
+                                                       conns, par)
+                assert tot == sum(sizes) and got == want, (copy, conns, chunk)
+        finally:
+            p.close()
