@@ -131,6 +131,8 @@ def test_init_parameters_in_native_order(native):
                   "com/mellanox/hadoop/mapred/UdaShuffleProviderPlugin.java",
                   "org/apache/hadoop/mapred/UdaMapredBridge.java",
                   "org/apache/hadoop/mapred/LRUCacheBridgeHadoop1.java"]),
+    ("hadoop-1-old", ["com/mellanox/hadoop/mapred/UdaShuffleConsumerPlugin.java"]),
+    ("yarn-2.0", ["com/mellanox/hadoop/mapred/UdaShuffleHandler.java"]),
 ])
 def test_version_front_ends_present(flavor, classes):
     for c in classes:
@@ -145,3 +147,16 @@ def test_health_signal_strings():
     src = _read(os.path.join(SHARED, "UdaShuffleConsumerPluginShared.java"))
     assert "init - Using UdaShuffleConsumerPlugin" in src
     assert "====XXX Successfully closed UdaShuffleConsumerPlugin XXX====" in src
+
+
+def test_older_front_end_apis():
+    """mlx-1.x-old: the consumer extends the abstract ShuffleConsumerPlugin with the 4-argument init;
+    mlx-2.0.x: the provider is an AbstractService implementing AuxServices.AuxiliaryService (initApp /
+    stopApp), and still sends JOB_OVER when an application stops."""
+    old = _read(os.path.join(JAVA, "hadoop-1-old", "com/mellanox/hadoop/mapred/UdaShuffleConsumerPlugin.java"))
+    assert "extends ShuffleConsumerPlugin implements UdaConsumerPluginCallable" in old
+    assert "init(ReduceTask reduceTask, TaskUmbilicalProtocol umb, JobConf conf, Reporter reporter)" in old
+    y20 = _read(os.path.join(JAVA, "yarn-2.0", "com/mellanox/hadoop/mapred/UdaShuffleHandler.java"))
+    assert "extends AbstractService" in y20 and "AuxServices.AuxiliaryService" in y20
+    assert "public void initApp(String user, ApplicationId appId, ByteBuffer secret)" in y20
+    assert "public void stopApp(ApplicationId appId)" in y20 and "JOB_OVER_COMMAND" in y20
