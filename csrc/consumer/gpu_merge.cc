@@ -2064,6 +2064,35 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     std::vector<int64_t> roff;
     int64_t blocks = 0;
     const bool dev_frames = gpu::plan_block_streams_device(codec_, cp, cl, &bp, ws.frame_scratch, ws.frame_descs, s);
+    // TeraSort-shaped partitions: decode per key-range round, only the blocks each round covers, so the
+    // task's device memory is round-sized instead of its decoded partitions (DecompressorWrapper decodes
+    // block by block next to the merge too, src/Merger/DecompressorWrapper.cc:85-114)
+    if (dev_frames && kind_ == KeyKind::kText && host_->conf_i64("mapred.uda.gpu.decode.stream", 1) != 0) {
+      gpu::DeviceReduceConfig cfg;
+      cfg.device = device;
+      cfg.kv_buf_bytes = kv_buf_size_;
+      cfg.round_bytes = round_bytes;
+      cfg.stop = [&] { return stop_.load(); };
+      bool streamed = false;
+      const gpu::DeviceReduceStats ds = gpu::device_reduce_fixed_blocks(cfg, (int)codec_, bp, sink, &streamed);
+      if (streamed) {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.hbm_wait_ms += ds.hbm_wait_ms;
+        st_.hbm_reserved = ds.hbm_reserved;
+        st_.round_bytes = ds.round_bytes;
+        st_.records = ds.records;
+        st_.rpq_rounds = ds.rounds;
+        st_.device_decoded_blocks += ds.decoded_blocks;
+        st_.gpu_device_ms = ds.plan_ms + ds.merge_wait_ms;
+        st_.gpu_d2h_wait_ms = ds.d2h_wait_ms;
+        st_.gpu_sink_ms = ds.sink_ms;
+        st_.fetch_ms = fetch_ms;
+        st_.merge_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() - fetch_ms;
+        st_.merge_path = "device-fixed10-stream";
+        ws_lease.clean = true;
+        return true;
+      }
+    }
     if (dev_frames) {
       // decode output and the merge's rounds at once: a task holding its decoded partitions must
       // not then wait for merge memory behind tasks doing the same

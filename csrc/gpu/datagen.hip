@@ -158,7 +158,38 @@ __global__ void __launch_bounds__(256) sample_fixed_kernel(uint8_t* const* bases
   out[g].lo = kl << 48;
 }
 
+// First full record's key of every block of a block-compressed FIXED10 stream, from the block's decoded
+// prefix (prefix + b * slot; the record starts first_off[b] bytes in, -1: no whole key in the block).
+__global__ void __launch_bounds__(256) block_first_keys_kernel(const uint8_t* prefix, int64_t slot,
+                                                               const int32_t* first_off, int n, Elem* out,
+                                                               int* bad) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const int f = first_off[b];
+  if (f < 0) {
+    out[b] = Elem{~0ull, ~0ull};
+    return;
+  }
+  const uint8_t* r = prefix + (int64_t)b * slot + f;
+  if (r[0] != 0x0B || r[1] != 0x5B || r[2] != 0x0A) {  // not the TeraSort record layout
+    atomicOr(bad, 1);
+    out[b] = Elem{~0ull, ~0ull};
+    return;
+  }
+  uint64_t hi = 0;
+  for (int i = 0; i < 8; ++i) hi = (hi << 8) | r[kTeraKeyOffset + i];
+  const uint64_t lo16 = ((uint64_t)r[kTeraKeyOffset + 8] << 8) | r[kTeraKeyOffset + 9];
+  out[b] = Elem{hi, lo16 << 48};
+}
+
 }  // namespace
+
+void launch_block_first_keys(const uint8_t* prefix, int64_t slot, const int32_t* first_off, int n, Elem* out, int* bad,
+                             hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(block_first_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, prefix, slot,
+                     first_off, n, out, bad);
+}
 
 void launch_sample_fixed(uint8_t* const* bases, const int64_t* nrec, int nruns, int64_t every,
                          const int64_t* sample_off, int64_t total, Elem* out, hipStream_t s) {

@@ -33,6 +33,8 @@ struct Wave {
   int64_t win_end;    // stream offset one past the valid window bytes
   int64_t in_end;     // end of this block's compressed bytes
   int64_t flushed;    // output offset below which every store of this wave has completed
+  int64_t clip;       // prefix decode: no byte at or past this output offset is written
+  bool prefix;        // a prefix decode (stops at clip); else clip is the block's end
   int lane;
 };
 
@@ -91,11 +93,14 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, int6
 }
 
 __device__ __forceinline__ void copy_literal(Wave& w, int64_t op, int64_t ip, int64_t len) {
-  wave_copy(w.out + op, w.in + ip, len, w.lane);
+  len = min(len, w.clip - op);  // a prefix decode keeps only the bytes below its clip
+  if (len > 0) wave_copy(w.out + op, w.in + ip, len, w.lane);
 }
 
 // out[op .. op+len) = out[op-off ...] with LZ77 overlap semantics.
 __device__ __forceinline__ void copy_match(Wave& w, int64_t op, int64_t off, int64_t len) {
+  len = min(len, w.clip - op);  // the source bytes below the clip were all written
+  if (len <= 0) return;
   const int64_t src = op - off;
   if (src + min(off, len) > w.flushed) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -126,6 +131,10 @@ __device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int6
   if (op + ulen > oend) return false;
   const int64_t op0 = op, uend = op + ulen;
   while (ip < cend) {
+    if (w.prefix && op >= w.clip) {  // prefix decode: everything wanted is out
+      *produced = ulen;
+      return true;
+    }
     if (!ensure(w, ip, 1)) return false;
     const uint32_t tag = byte_at(w, ip++);
     const uint32_t type = tag & 3;
@@ -189,6 +198,10 @@ __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64
     lit_first = true;
   }
   for (;;) {
+    if (w.prefix && op >= w.clip) {  // prefix decode: everything wanted is out
+      *produced = oend - out0;
+      return true;
+    }
     if (lit_first) {
       lit_first = false;
       goto copy_literal_run;
@@ -289,9 +302,11 @@ __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
+// clip > 0: prefix decode. Only the first `clip` bytes of each block's output (at d.dst) are written and
+// the decode stops once they are out; d.raw stays the block's full raw size for the format checks.
 template <int kCodec>
 __global__ void __launch_bounds__(64 * kWavesPerBlock)
-    block_decode_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status) {
+    block_decode_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status, int64_t clip) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][kWin + 16];
   const int wid = threadIdx.x >> 6;
   const int b = blockIdx.x * kWavesPerBlock + wid;
@@ -307,9 +322,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
   w.lane = threadIdx.x & 63;
   int64_t ip = d.src, op = d.dst;
   const int64_t oend = d.dst + d.raw;
+  w.prefix = clip > 0 && clip < d.raw;
+  w.clip = w.prefix ? d.dst + clip : oend;
   bool ok = true;
   // one block = one or more [u32 BE compressed_len][chunk] records until its raw bytes are produced
   while (ok && op < oend) {
+    if (w.prefix && op >= w.clip) return;  // prefix decode done
     if (ip + 4 > d.src_end) {
       ok = false;
       break;
@@ -418,13 +436,13 @@ void launch_frame_streams(const uint8_t* const* ptrs, const int64_t* lens, int n
 }
 
 void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
-                         hipStream_t s) {
+                         hipStream_t s, int64_t clip) {
   if (n <= 0) return;
   const int grid = (n + kWavesPerBlock - 1) / kWavesPerBlock;
   if (codec == 1)
-    block_decode_kernel<1><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status);
+    block_decode_kernel<1><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
   else
-    block_decode_kernel<2><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status);
+    block_decode_kernel<2><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
 }
 
 }  // namespace gpu

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <stdexcept>
 
+#include "block_decoder.h"
 #include "device_engine.h"
 #include "hbm_ledger.h"
 #include "sdma.h"
@@ -56,6 +57,9 @@ struct FixedWs {
   std::unique_ptr<DeviceMerger> merger;
   DeviceBuffer out[2];
   DeviceBuffer d_bases, d_nrec, d_soff, d_samp, d_bset, d_out, d_bounds, d_runs, flag;
+  // streaming decode of block-compressed runs (device_reduce_fixed_blocks): the round inputs, the block
+  // prefixes + first keys, and the per-round decode descriptors
+  DeviceBuffer in[2], prefix, d_first, d_keys, d_descs[2];
   hipStream_t s = nullptr;
   hipEvent_t merged[2] = {nullptr, nullptr};
   FixedWs() {
@@ -74,7 +78,7 @@ struct FixedWs {
   int64_t device_bytes() const {
     int64_t n = merger ? merger->device_bytes() : 0;
     for (const DeviceBuffer* b : {&out[0], &out[1], &d_bases, &d_nrec, &d_soff, &d_samp, &d_bset, &d_out, &d_bounds,
-                                  &d_runs, &flag})
+                                  &d_runs, &flag, &in[0], &in[1], &prefix, &d_first, &d_keys, &d_descs[0], &d_descs[1]})
       n += (int64_t)b->held();
     return n;
   }
@@ -433,6 +437,365 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   }
   if (merger.bad_layout()) throw std::runtime_error("device reduce: non-TeraSort record in a FIXED10 run");
   st.records = N;
+  HIP_CHECK(hipStreamSynchronize(s));
+  lease.clean = true;
+  return st;
+}
+
+}  // namespace gpu
+}  // namespace uda
+
+namespace uda {
+namespace gpu {
+
+namespace {
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+bool key_less(const Elem& a, const Elem& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+}  // namespace
+
+// Streaming decode (F6 per key-range round) of block-compressed FIXED10 partitions.
+//
+// Reference: DecompressorWrapper decodes block by block into a cyclic buffer next to the merge, so a
+// reducer never holds a partition's decoded bytes whole (src/Merger/DecompressorWrapper.cc:85-114,
+// 168-197). Here the partitions stay compressed in HBM and each key-range round decodes only the
+// blocks its key range covers:
+//   1. prefix pass: every block's first 128 raw bytes (launch_block_decode with a clip) give the key of
+//      the first record that starts in it (records are 104 bytes from the partition's start, so the
+//      offset is known) -- a block first-key index, one wave per block, ~0.1 % of a full decode;
+//   2. round bounds: quantiles of those keys; per round and partition, the blocks from the last one
+//      whose first key is below the round's low bound to the first one whose first key reaches its
+//      high bound hold every record of the range (boundary blocks are decoded by both neighbours);
+//   3. per round: decode those blocks into one of two round input buffers (record starts 16-byte
+//      aligned), cut each run to exactly the round's keys (split_fixed), merge into one of two output
+//      slots, deliver as device_reduce_fixed does. Device memory: two round inputs + two round outputs.
+DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int codec, const BlockPlan& plan,
+                                             const std::function<int(const uint8_t*, int64_t)>& sink,
+                                             bool* streamed) {
+  trace::Range tr("uda.device_reduce_blocks");
+  *streamed = false;
+  DeviceReduceStats st;
+  HIP_CHECK(hipSetDevice(cfg.device));
+  const double t0 = now_ms();
+  const int K = (int)plan.raw_offset.size() - 1;
+  const int64_t NB = (int64_t)plan.descs.size();
+  if (K <= 0 || K > 65536) return st;
+  // ---- streams: FIXED10 raw sizes (records + the 2-byte EOF), their blocks
+  std::vector<int64_t> nrec(K), raw0(K), blk0(K + 1, NB);
+  int64_t N = 0;
+  for (int k = 0; k < K; ++k) {
+    raw0[k] = plan.raw_offset[k];
+    const int64_t raw = plan.raw_offset[k + 1] - plan.raw_offset[k];
+    if (raw < kEofBytes || (raw - kEofBytes) % kTeraRecordBytes != 0) return st;  // not FIXED10
+    nrec[k] = (raw - kEofBytes) / kTeraRecordBytes;
+    N += nrec[k];
+  }
+  {
+    // descriptors are in stream order with ascending dst: stream k's blocks are those with dst in
+    // [raw_offset[k], raw_offset[k + 1])
+    int64_t b = 0;
+    for (int k = 0; k < K; ++k) {
+      while (b < NB && plan.descs[(size_t)b].dst < plan.raw_offset[k]) ++b;
+      blk0[k] = b;
+    }
+    blk0[K] = NB;
+  }
+  auto R = [&](int64_t b, int k) { return plan.descs[(size_t)b].dst - raw0[k]; };  // block's raw offset in its stream
+  // ---- prefix pass: the block first-key index
+  constexpr int64_t kSlot = 128;  // >= 103 bytes to the first record start + 13 bytes of record head and key
+  WsLease lease(cfg.device, N * kTeraRecordBytes);
+  FixedWs& ws = *lease.w;
+  hipStream_t s = ws.s;
+  std::vector<int32_t> first(NB, -1);
+  std::vector<DecodeDesc> pd(plan.descs);
+  for (int k = 0; k < K; ++k)
+    for (int64_t b = blk0[k]; b < blk0[k + 1]; ++b) {
+      const int64_t rel = R(b, k);
+      const int64_t f = (kTeraRecordBytes - rel % kTeraRecordBytes) % kTeraRecordBytes;
+      if (rel + f + kTeraRecordBytes <= nrec[k] * kTeraRecordBytes && f + kTeraKeyOffset + kTeraKeyBytes <= pd[(size_t)b].raw)
+        first[(size_t)b] = (int32_t)f;
+      pd[(size_t)b].dst = b * kSlot;
+    }
+  if (NB > 0) {
+    FixedWs::ensure(ws.prefix, (size_t)NB * kSlot);
+    FixedWs::ensure(ws.d_first, (size_t)NB * 4);
+    FixedWs::ensure(ws.d_keys, (size_t)NB * sizeof(Elem));
+    FixedWs::ensure(ws.d_descs[0], (size_t)NB * sizeof(DecodeDesc));
+    FixedWs::ensure(ws.flag, 2 * sizeof(int));
+    HIP_CHECK(hipMemcpyAsync(ws.d_descs[0].as(), pd.data(), (size_t)NB * sizeof(DecodeDesc), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(ws.d_first.as(), first.data(), (size_t)NB * 4, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemsetAsync(ws.flag.as(), 0, 2 * sizeof(int), s));
+    launch_block_decode(codec, nullptr, ws.prefix.as<uint8_t>(), ws.d_descs[0].as<DecodeDesc>(), (int)NB,
+                        ws.flag.as<int>(), s, kSlot);
+    launch_block_first_keys(ws.prefix.as<uint8_t>(), kSlot, ws.d_first.as<int32_t>(), (int)NB, ws.d_keys.as<Elem>(),
+                            ws.flag.as<int>() + 1, s);
+    HIP_CHECK(hipGetLastError());
+  }
+  std::vector<Elem> keys((size_t)NB);
+  int flags[2] = {0, 0};
+  if (NB > 0) {
+    HIP_CHECK(hipMemcpyAsync(keys.data(), ws.d_keys.as(), (size_t)NB * sizeof(Elem), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(flags, ws.flag.as(), sizeof(flags), hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (flags[0]) throw UdaError("corrupt compressed block in a map output partition");
+  if (flags[1]) {  // not TeraSort-shaped records: the caller decodes whole partitions (generic merge)
+    lease.clean = true;
+    return st;
+  }
+  // per stream: the blocks where a record starts, with its key (ascending in a sorted run)
+  std::vector<std::vector<std::pair<int64_t, Elem>>> idx(K);
+  std::vector<Elem> samp;
+  for (int k = 0; k < K; ++k)
+    for (int64_t b = blk0[k]; b < blk0[k + 1]; ++b)
+      if (first[(size_t)b] >= 0) {
+        if (!idx[k].empty() && key_less(keys[(size_t)b], idx[k].back().second)) {  // not a sorted run
+          lease.clean = true;
+          return st;
+        }
+        idx[k].emplace_back(b, keys[(size_t)b]);
+        samp.push_back(keys[(size_t)b]);
+      }
+  std::sort(samp.begin(), samp.end(), key_less);
+  *streamed = true;
+  auto emit_eof_only = [&] {
+    uint8_t eof[2] = {0xFF, 0xFF};
+    if (sink(eof, kEofBytes) != 0) throw std::runtime_error("dataFromUda callback failed");
+    st.buffers++;
+  };
+  if (N == 0) {
+    emit_eof_only();
+    lease.clean = true;
+    return st;
+  }
+  // ---- rounds: bounds from the block keys, each round's block range and input layout per stream
+  HbmLedger& led = HbmLedger::get();
+  int64_t round_bytes = std::max<int64_t>(cfg.round_bytes, kTeraRecordBytes);
+  struct Span {
+    int64_t b0 = 0, b1 = -1;        // blocks [b0, b1]
+    int64_t rec0 = 0, rec1 = 0;     // whole records inside, stream record indices
+    int64_t in_off = 0;             // decoded byte R(b0) lands here in the round input
+  };
+  int Q = 1;
+  std::vector<Elem> bounds;
+  std::vector<std::vector<Span>> spans;
+  std::vector<int64_t> in_bytes, in_recs;
+  auto plan_rounds = [&](int64_t rb) {
+    Q = (int)std::max<int64_t>(1, (N * kTeraRecordBytes + rb - 1) / rb);
+    bounds.assign((size_t)std::max(0, Q - 1), Elem{0, 0});
+    for (int q = 1; q < Q; ++q) bounds[(size_t)q - 1] = samp.empty() ? Elem{~0ull, ~0ull} : samp[samp.size() * (size_t)q / (size_t)Q];
+    spans.assign((size_t)Q, std::vector<Span>((size_t)K));
+    in_bytes.assign((size_t)Q, 0);
+    in_recs.assign((size_t)Q, 0);
+    for (int q = 0; q < Q; ++q) {
+      int64_t cur = 0;
+      for (int k = 0; k < K; ++k) {
+        Span& sp = spans[(size_t)q][(size_t)k];
+        if (nrec[k] == 0 || blk0[k] == blk0[k + 1]) continue;
+        const auto& ix = idx[k];
+        // b0: the last block starting a record with a key below the low bound (round 0: the first block)
+        sp.b0 = blk0[k];
+        if (q > 0) {
+          const Elem lo = bounds[(size_t)q - 1];
+          auto it = std::lower_bound(ix.begin(), ix.end(), lo, [](const std::pair<int64_t, Elem>& a, const Elem& v) {
+            return key_less(a.second, v);
+          });
+          if (it != ix.begin()) sp.b0 = std::prev(it)->first;
+        }
+        // b1: the first block starting a record with a key at or above the high bound (last round: the last block)
+        sp.b1 = blk0[k + 1] - 1;
+        if (q + 1 < Q) {
+          const Elem hi = bounds[(size_t)q];
+          auto it = std::lower_bound(ix.begin(), ix.end(), hi, [](const std::pair<int64_t, Elem>& a, const Elem& v) {
+            return key_less(a.second, v);
+          });
+          if (it != ix.end()) sp.b1 = it->first;
+        }
+        if (sp.b1 < sp.b0) sp.b1 = sp.b0;
+        const int64_t r0 = R(sp.b0, k), r1 = R(sp.b1, k) + plan.descs[(size_t)sp.b1].raw;
+        sp.rec0 = (r0 + kTeraRecordBytes - 1) / kTeraRecordBytes;
+        sp.rec1 = std::min(r1 / kTeraRecordBytes, nrec[k]);
+        if (sp.rec1 < sp.rec0) sp.rec1 = sp.rec0;
+        const int64_t lead = sp.rec0 * kTeraRecordBytes - r0;  // partial record before the first whole one
+        sp.in_off = align_up(cur + lead, 16) - lead;            // record starts 16-byte aligned
+        cur = sp.in_off + (r1 - r0);
+        in_recs[(size_t)q] += sp.rec1 - sp.rec0;
+      }
+      in_bytes[(size_t)q] = align_up(cur, 256);
+    }
+  };
+  auto need = [&](int64_t rb) {
+    plan_rounds(rb);
+    int64_t mi = 0, mr = 0;
+    for (int q = 0; q < Q; ++q) {
+      mi = std::max(mi, in_bytes[(size_t)q]);
+      mr = std::max(mr, in_recs[(size_t)q]);
+    }
+    const int64_t have = ws.device_bytes();
+    const int64_t want = 2 * (mi + mi / 8) + 2 * (mr * kTeraRecordBytes * 9 / 8) + (int64_t)(0.02 * (double)(mr * kTeraRecordBytes)) +
+                         (int64_t)K * 4096 + (16ll << 20) + 2 * (int64_t)NB * (int64_t)sizeof(DecodeDesc);
+    return std::max<int64_t>(0, want - have);
+  };
+  std::unique_ptr<HbmLedger::Reservation> res;
+  const bool caller_reserved = led.bound() != nullptr && led.bound()->device() == cfg.device;
+  if (!caller_reserved) {
+    const int64_t hr = led.headroom(cfg.device);
+    while (round_bytes > (64ll << 20) && need(round_bytes) > hr) round_bytes /= 2;
+    res = led.reserve(cfg.device, need(round_bytes), cfg.stop);
+    st.hbm_wait_ms = res->wait_ms();
+    st.hbm_reserved = res->granted();
+  } else {
+    plan_rounds(round_bytes);
+  }
+  st.round_bytes = round_bytes;
+  int64_t max_in = 0, max_recs = 0;
+  for (int q = 0; q < Q; ++q) {
+    max_in = std::max(max_in, in_bytes[(size_t)q]);
+    max_recs = std::max(max_recs, in_recs[(size_t)q]);
+  }
+  for (auto& b : ws.in) FixedWs::ensure(b, (size_t)std::max<int64_t>(max_in, 256));
+  for (auto& b : ws.out) FixedWs::ensure(b, (size_t)std::max<int64_t>(max_recs, 1) * kTeraRecordBytes);
+  for (auto& b : ws.d_descs) FixedWs::ensure(b, (size_t)std::max<int64_t>(NB, 1) * sizeof(DecodeDesc));
+  FixedWs::ensure(ws.d_bases, 2 * (size_t)K * sizeof(uint8_t*));
+  FixedWs::ensure(ws.d_nrec, 2 * (size_t)K * 8);
+  FixedWs::ensure(ws.d_bset, (size_t)K * sizeof(int));
+  FixedWs::ensure(ws.d_bounds, 2 * 2 * sizeof(Elem));
+  FixedWs::ensure(ws.d_out, 2 * (size_t)K * 4 * 8);
+  HIP_CHECK(hipMemsetAsync(ws.d_bset.as(), 0, (size_t)K * sizeof(int), s));
+  if (!ws.merger || ws.merger->max_records() < max_recs || ws.merger->max_runs() < K) {
+    const int64_t mr = std::max<int64_t>(max_recs, ws.merger ? ws.merger->max_records() : 0);
+    const int mk = std::max(K, ws.merger ? ws.merger->max_runs() : 0);
+    ws.merger.reset();
+    ws.merger.reset(new DeviceMerger(mr, mk));
+  }
+  DeviceMerger& merger = *ws.merger;
+  st.rounds = Q;
+  const int64_t buf_records = std::max<int64_t>(1, cfg.kv_buf_bytes / kTeraRecordBytes);
+  const int64_t buf_bytes = buf_records * kTeraRecordBytes;
+  const int64_t piece = std::max<int64_t>(1, cfg.piece_bytes / buf_bytes) * buf_bytes;
+  const int SL = std::max(2, cfg.pinned_slots);
+  Ring ring(SdmaEngine::for_device(cfg.device), (size_t)piece * SL, SL);
+  std::vector<uint8_t> tail((size_t)cfg.kv_buf_bytes + 16);
+  auto emit = [&](const uint8_t* p, int64_t len) {
+    const double a = now_ms();
+    if (sink(p, len) != 0) throw std::runtime_error("dataFromUda callback failed");
+    st.sink_ms += now_ms() - a;
+    st.buffers++;
+  };
+  st.plan_ms = now_ms() - t0;
+  std::vector<int64_t> round_recs((size_t)Q, 0);
+  int64_t decoded_blocks = 0;
+  // ---- round q: decode its blocks, cut the runs to its key range, merge
+  auto enqueue_round = [&](int q) {
+    const int par = q & 1;
+    uint8_t* in = ws.in[par].as<uint8_t>();
+    std::vector<DecodeDesc> rd;
+    std::vector<uint8_t*> bases((size_t)K, in);
+    std::vector<int64_t> n((size_t)K, 0);
+    for (int k = 0; k < K; ++k) {
+      const Span& sp = spans[(size_t)q][(size_t)k];
+      if (sp.b1 < sp.b0 || nrec[k] == 0) continue;
+      const int64_t r0 = R(sp.b0, k);
+      for (int64_t b = sp.b0; b <= sp.b1; ++b) {
+        DecodeDesc d = plan.descs[(size_t)b];
+        d.dst = sp.in_off + (R(b, k) - r0);
+        rd.push_back(d);
+      }
+      bases[(size_t)k] = in + sp.in_off + (sp.rec0 * kTeraRecordBytes - r0);
+      n[(size_t)k] = sp.rec1 - sp.rec0;
+    }
+    decoded_blocks += (int64_t)rd.size();
+    HIP_CHECK(hipMemcpyAsync(ws.d_descs[par].as(), rd.data(), rd.size() * sizeof(DecodeDesc), hipMemcpyHostToDevice, s));
+    launch_block_decode(codec, nullptr, in, ws.d_descs[par].as<DecodeDesc>(), (int)rd.size(), ws.flag.as<int>(), s);
+    // exactly the round's records of every run: [lower_bound(low), lower_bound(high))
+    const Elem b2[2] = {q > 0 ? bounds[(size_t)q - 1] : Elem{0, 0}, q + 1 < Q ? bounds[(size_t)q] : Elem{~0ull, ~0ull}};
+    uint8_t** dbases = ws.d_bases.as<uint8_t*>() + (size_t)par * K;
+    int64_t* dn = ws.d_nrec.as<int64_t>() + (size_t)par * K;
+    Elem* dbd = ws.d_bounds.as<Elem>() + 2 * par;
+    int64_t* dpos = ws.d_out.as<int64_t>() + (size_t)par * K * 4;
+    HIP_CHECK(hipMemcpyAsync(dbases, bases.data(), (size_t)K * sizeof(uint8_t*), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(dn, n.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(dbd, b2, sizeof(b2), hipMemcpyHostToDevice, s));
+    launch_split_fixed(dbases, dn, dbd, ws.d_bset.as<int>(), K, 2, dpos, s);
+    HIP_CHECK(hipGetLastError());
+    std::vector<int64_t> pos((size_t)K * 4);
+    HIP_CHECK(hipMemcpyAsync(pos.data(), dpos, pos.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(flags, ws.flag.as(), sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (flags[0]) throw UdaError("corrupt compressed block in a map output partition");
+    std::vector<RunDesc> rq((size_t)K);
+    int64_t total = 0;
+    for (int k = 0; k < K; ++k) {
+      const int64_t a = q > 0 ? pos[(size_t)k * 4 + 1] : 0;
+      const int64_t e = q + 1 < Q ? pos[(size_t)k * 4 + 2] : n[(size_t)k];
+      rq[(size_t)k].base = bases[(size_t)k] + a * kTeraRecordBytes;
+      rq[(size_t)k].nrec = std::max<int64_t>(0, e - a);
+      rq[(size_t)k].nbytes = rq[(size_t)k].nrec * kTeraRecordBytes;
+      rq[(size_t)k].offsets = nullptr;
+      total += rq[(size_t)k].nrec;
+    }
+    round_recs[(size_t)q] = total;
+    merger.merge_fixed(rq, {0, K}, ws.out[par].as<uint8_t>(), s);
+    HIP_CHECK(hipGetLastError());
+    st.merge_passes = std::max(st.merge_passes, merger.last_passes());
+    HIP_CHECK(hipEventRecord(ws.merged[par], s));
+  };
+  SdmaEngine& eng = ring.eng;
+  bool eof_sent = false;
+  auto deliver_round = [&](int q) {
+    const uint8_t* src = ws.out[q & 1].as<uint8_t>();
+    const int64_t bytes = round_recs[(size_t)q] * kTeraRecordBytes;
+    const bool last_round = q == Q - 1;
+    const int64_t np = (bytes + piece - 1) / piece;
+    auto issue = [&](int64_t k) {
+      const int64_t off = k * piece, len = std::min(piece, bytes - off);
+      hsa_signal_t sg = ring.sig[(size_t)(k % SL)];
+      SdmaEngine::arm(sg, eng.parts((size_t)len, 1));
+      eng.copy_d2h(ring.p + (k % SL) * piece, src + off, (size_t)len, sg, 1);
+    };
+    for (int64_t k = 0; k < std::min<int64_t>(np, SL); ++k) issue(k);
+    for (int64_t k = 0; k < np; ++k) {
+      const double a = now_ms();
+      SdmaEngine::wait(ring.sig[(size_t)(k % SL)]);
+      st.d2h_wait_ms += now_ms() - a;
+      const uint8_t* base = ring.p + (k % SL) * piece;
+      const int64_t plen = std::min(piece, bytes - k * piece);
+      for (int64_t off = 0; off < plen; off += buf_bytes) {
+        const int64_t len = std::min(buf_bytes, plen - off);
+        const bool final_chunk = last_round && k == np - 1 && off + len >= plen;
+        if (final_chunk && len + kEofBytes <= cfg.kv_buf_bytes) {
+          std::memcpy(tail.data(), base + off, (size_t)len);
+          tail[(size_t)len] = tail[(size_t)len + 1] = 0xFF;
+          emit(tail.data(), len + kEofBytes);
+          eof_sent = true;
+        } else {
+          emit(base + off, len);
+        }
+      }
+      if (k + SL < np) issue(k + SL);
+    }
+    st.bytes += bytes;
+    if (last_round && !eof_sent) {
+      tail[0] = tail[1] = 0xFF;
+      emit(tail.data(), kEofBytes);
+      eof_sent = true;
+    }
+  };
+  enqueue_round(0);
+  for (int q = 0; q < Q; ++q) {
+    if (q + 1 < Q) enqueue_round(q + 1);  // its slots held round q-1, delivered in the last iteration
+    const double a = now_ms();
+    HIP_CHECK(hipEventSynchronize(ws.merged[q & 1]));
+    st.merge_wait_ms += now_ms() - a;
+    deliver_round(q);
+  }
+  if (merger.bad_layout()) throw std::runtime_error("device reduce: non-TeraSort record in a FIXED10 run");
+  int64_t got = 0;
+  for (int q = 0; q < Q; ++q) got += round_recs[(size_t)q];
+  if (got != N)
+    throw UdaError("streaming decode: the key-range rounds hold " + std::to_string(got) + " records, the partitions " +
+                   std::to_string(N));
+  st.records = N;
+  st.decoded_blocks = decoded_blocks;
   HIP_CHECK(hipStreamSynchronize(s));
   lease.clean = true;
   return st;

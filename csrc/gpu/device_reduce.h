@@ -45,6 +45,7 @@ struct DeviceReduceStats {
   double hbm_wait_ms = 0;      // waiting for the HBM reservation
   int64_t hbm_reserved = 0;    // bytes reserved for the round working set
   int64_t round_bytes = 0;     // round size used (after any shrink to fit the budget)
+  int64_t decoded_blocks = 0;  // device_reduce_fixed_blocks: blocks decoded over all rounds
 };
 
 // Build what a FIXED10 task's first round would otherwise build on its critical path (a fresh reduce
@@ -65,6 +66,16 @@ bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s);
 // A nonzero sink return aborts with an exception.
 DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::vector<RunDesc>& runs,
                                       const std::function<int(const uint8_t*, int64_t)>& sink);
+
+struct BlockPlan;
+// Block-compressed FIXED10 partitions (plan: plan_block_streams_device, every block of every run, dst =
+// the run's raw offset + the block's) merged in key-range rounds that decode only the blocks each round
+// covers (block first-key index from a prefix decode): device memory is two round inputs and two round
+// outputs, not the decoded partitions. *streamed false (nothing delivered): not TeraSort-shaped sorted
+// runs; the caller decodes the partitions whole. codec: uda::Codec value.
+DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int codec, const BlockPlan& plan,
+                                             const std::function<int(const uint8_t*, int64_t)>& sink,
+                                             bool* streamed);
 
 }  // namespace gpu
 }  // namespace uda

@@ -75,6 +75,12 @@ void launch_split_fixed(uint8_t* const* bases, const int64_t* nrec, const Elem* 
 void launch_sample_fixed(uint8_t* const* bases, const int64_t* nrec, int nruns, int64_t every,
                          const int64_t* sample_off, int64_t total, Elem* out, hipStream_t s);
 
+// Block first-key index of block-compressed FIXED10 streams: for every block b, the key of the first
+// record that starts in it, read from its decoded prefix at prefix + b * slot + first_off[b] (-1: none:
+// Elem{~0, ~0}). *bad |= 1 when a record there is not the TeraSort layout.
+void launch_block_first_keys(const uint8_t* prefix, int64_t slot, const int32_t* first_off, int n, Elem* out, int* bad,
+                             hipStream_t s);
+
 // ---------------------------------------------------------------- key extraction (F2)
 // Build Elem keys for all records of `nruns` FIXED10 runs; run r's elements start at
 // elem_off[r]. Sets *bad_layout to 1 if any record header is not the TeraSort layout.
@@ -236,8 +242,9 @@ struct DecodeDesc {
   int64_t raw;
 };
 // codec: 1 = Snappy, 2 = LZO1X (uda::Codec values). *status |= 1 if any block is corrupt.
+// clip > 0: prefix decode, only the first `clip` raw bytes of every block are produced (at its dst).
 void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
-                         hipStream_t s);
+                         hipStream_t s, int64_t clip = 0);
 // Framing walk of device-resident streams (one lane per stream). out == nullptr: per-stream block
 // counts and raw bytes; else the descriptors with absolute src addresses (decode with in = nullptr).
 // status[s] = 1: framing not resolvable without decoding (zero status first).

@@ -144,9 +144,12 @@ p.close()
 """
 
 
-def test_cross_process_provider_over_ipc(require_gpu, tmp_path):
+@pytest.mark.parametrize("service", ["off", "auto"])
+def test_cross_process_provider_over_ipc(require_gpu, tmp_path, service):
     """A provider in another process serves descriptors over TCP; the reducer maps the provider's
-    HBM with hipIpcOpenMemHandle and merges in place (the registered-MR/rkey analogue)."""
+    HBM with hipIpcOpenMemHandle and merges in place (the registered-MR/rkey analogue). service=off: the
+    reducer merges in this process; auto (the default): the provider's node daemon hosts it, and the
+    daemon maps the provider's HBM."""
     import socket
     maps = datagen.terasort(num_maps=5, reducers=2, rows_per_map=2000, seed=8)
     payload = [(f"attempt_job_9_0005_m_{i:06d}_0", [p.hex() for p in parts])
@@ -161,11 +164,12 @@ def test_cross_process_provider_over_ipc(require_gpu, tmp_path):
     try:
         assert proc.stdout.readline().strip() == "READY"
         ids = [mid for mid, _ in payload]
-        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device"})
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.merge.service": service})
         recs, st, _ = run_reduce("127.0.0.1", "job_9_0005", ids, 1, datagen.TEXT, conf=conf, transport="tcp",
                                  data_port=port)
         assert recs == expected(maps, 1, datagen.TEXT)
-        assert st["device_descriptors"] == 5 and st["host_fetched_bytes"] == 0
+        assert st["device_descriptors"] == 5 and st["host_fetched_bytes"] == 0, st
+        assert st.get("merge_service", False) == (service == "auto"), st
     finally:
         proc.stdin.close()
         out = proc.stdout.read()
@@ -329,6 +333,31 @@ def test_compressed_device_mofs_decode_in_place(require_gpu, provider, codec, ge
         assert st["device_decoded_blocks"] > 0 and st["merge_path"].startswith("device"), st
 
 
+@pytest.mark.parametrize("codec", ["snappy", "lzo"])
+def test_compressed_terasort_streaming_decode_rounds(require_gpu, provider, codec):
+    """compressed TeraSort partitions decoded per key-range round, only the blocks each
+    round covers (block first-key index from a prefix decode). Small blocks and rounds put many round
+    bounds inside blocks and records across block boundaries; the stream must equal the whole-partition
+    decode path's, record for record."""
+    job = f"job_9_035{len(codec)}"
+    maps = datagen.terasort(num_maps=7, reducers=2, rows_per_map=4000, seed=61)
+    ids = []
+    for i, parts in enumerate(datagen.streams(maps)):
+        mid = f"attempt_{job}_m_{i:06d}_0"
+        data, index = encode_partitions(parts, codec, block_size=5000)  # not a multiple of 104
+        provider.add_mof_device(job, mid, data, index, device=0)
+        ids.append(mid)
+    base = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.round.bytes": 96 << 10})
+    for r in range(2):
+        recs, st, _ = run_reduce("h", job, ids, r, datagen.TEXT, codec=codec, conf=base, kv_buf_size=32 << 10)
+        assert recs == expected(maps, r, datagen.TEXT)
+        assert st["merge_path"] == "device-fixed10-stream" and st["rpq_rounds"] > 4, st
+        assert st["device_descriptors"] == 7 and st["device_decoded_blocks"] > 0, st
+        whole, st2, _ = run_reduce("h", job, ids, r, datagen.TEXT, codec=codec, kv_buf_size=32 << 10,
+                                   conf=dict(base, **{"mapred.uda.gpu.decode.stream": 0}))
+        assert st2["merge_path"] == "device-fixed10" and whole == recs, st2
+
+
 def test_compressed_host_mofs_device_fetch_pipelined(require_gpu, provider):
     """Compressed MOFs in host memory under mapred.uda.gpu.fetch=device: fetched as bytes in pipelined
     chunks (H2D overlapping the next fetch), then decoded and merged on the device."""
@@ -372,3 +401,4 @@ def test_bench_api_compressed_mofs(require_gpu, codec):
     assert out["validated"] is True and out["codec"] == codec and 0 < out["compressed_gb"]
     t0 = out["task0_stats"]
     assert t0["device_descriptors"] == 4 and t0["device_decoded_blocks"] > 0, t0
+    assert t0["merge_path"] == "device-fixed10-stream", t0
