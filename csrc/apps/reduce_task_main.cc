@@ -180,12 +180,12 @@ int main(int argc, char** argv) {
       "{\"pid\":%d,\"records\":%lld,\"bytes\":%lld,\"buffers\":%lld,\"order_errors\":%lld,\"error\":\"%s\","
       "\"exec_to_main_ms\":%.1f,\"start_ms\":%.1f,\"init_ms\":%.1f,\"first_fetch_ms\":%.1f,\"fetch_to_first_data_ms\":%.1f,"
       "\"fetch_to_eof_ms\":%.1f,\"exit_ms\":%.1f,\"exec_to_end_ms\":%.1f,\"t_exec_boot_ms\":%.1f,\"t_end_boot_ms\":%.1f,"
-      "\"task\":%s}\n",
+      "\"j2c\":%s,\"task\":%s}\n",
       (int)getpid(), (long long)sink.records(0), (long long)sink.bytes(0), (long long)sink.buffers(0),
       (long long)sink.order_errors(0), json_escape(err).c_str(), t_main - t_exec, t_started - t_main,
       t_init > 0 ? t_init - t_started : -1.0, t_first_fetch > 0 ? t_first_fetch - t_exec : -1.0,
       t_first_fetch > 0 && host.t_first_data > 0 ? host.t_first_data - t_first_fetch : -1.0,
-      t_first_fetch > 0 ? t_eof - t_first_fetch : -1.0, t_end - t_eof, t_end - t_exec, t_exec, t_end, js.c_str());
+      t_first_fetch > 0 ? t_eof - t_first_fetch : -1.0, t_end - t_eof, t_end - t_exec, t_exec, t_end, sink.placement_json(0).c_str(), js.c_str());
   std::fflush(stdout);
   (void)t_last_cmd;
   return err.empty() ? 0 : 1;

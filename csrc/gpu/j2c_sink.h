@@ -12,15 +12,24 @@
 // It also validates the delivery contract: every buffer holds whole records, is at most
 // kv_buf_bytes long, and each reducer's stream ends with exactly one EOF marker (-1, -1).
 #pragma once
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <fstream>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <set>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -52,6 +61,10 @@ class J2CSink {
     }
     if (threaded_)
       for (int r = 0; r < reducers; ++r) st_[(size_t)r]->walker = std::thread([this, r] { walk_loop(r); });
+    // UDA_J2C_PIN: l3 (default) = the walker and the copying thread share the copier's last-level cache
+    // (the walker reads the KVBuf the copier just wrote); none = leave both to the scheduler
+    const char* pin = std::getenv("UDA_J2C_PIN");
+    pin_l3_ = !(pin && std::string(pin) == "none");
   }
   ~J2CSink() {
     for (auto& sp : st_) {
@@ -81,20 +94,56 @@ class J2CSink {
       return walk(r, s, kb, len);
     }
     const int i = s.cur;
-    {
+    if (s.handed == 0) place(s);
+    if ((s.handed & 63) == 0) sample_cpu(s.copier_cpus);
+    // kv_buf_recv_ready: the walker usually hands a KVBuf back within microseconds, sooner than a
+    // sleeping thread is woken, so spin a little before blocking
+    if (!spin_until([&] { return !s.full[i].load(std::memory_order_acquire); })) {
       std::unique_lock<std::mutex> lk(s.mu);
-      s.cv.wait(lk, [&] { return !s.full[i]; });  // kv_buf_recv_ready
+      ++s.copier_blocks;
+      s.cv.wait(lk, [&] { return !s.full[i].load(); });
     }
     std::memcpy(s.buf[i].get(), data, (size_t)len);
     {
       std::lock_guard<std::mutex> g(s.mu);
       s.len[i] = len;
-      s.full[i] = true;  // kv_buf_redc_ready
+      s.full[i].store(true, std::memory_order_release);  // kv_buf_redc_ready
       ++s.handed;
     }
-    s.cv.notify_all();
+    if (s.walker_waiting.load()) s.cv.notify_all();
     s.cur ^= 1;
     return s.error.load(std::memory_order_relaxed);
+  }
+
+  // Where reducer r's copier and walker ran (threaded mode): CPUs, last-level caches and NUMA nodes
+  // seen in samples, and how often each side had to block (the handshake's sleeps).
+  std::string placement_json(int r) const {
+    const State& s = *st_[(size_t)r];
+    std::lock_guard<std::mutex> g(s.mu);
+    auto desc = [](const std::map<int, int64_t>& cpus) {
+      std::set<int> l3, node;
+      for (auto& kv : cpus) {
+        l3.insert(cpu_l3(kv.first));
+        node.insert(cpu_node(kv.first));
+      }
+      std::string o = "{\"cpus\":" + std::to_string(cpus.size()) + ",\"l3\":[";
+      bool first = true;
+      for (int x : l3) {
+        o += (first ? "" : ",") + std::to_string(x);
+        first = false;
+      }
+      o += "],\"nodes\":[";
+      first = true;
+      for (int x : node) {
+        o += (first ? "" : ",") + std::to_string(x);
+        first = false;
+      }
+      return o + "]}";
+    };
+    return "{\"threaded\":" + std::string(threaded_ ? "true" : "false") + ",\"pinned_l3\":" +
+           std::to_string(s.pinned_l3) + ",\"copier\":" + desc(s.copier_cpus) + ",\"walker\":" +
+           desc(s.walker_cpus) + ",\"copier_blocks\":" + std::to_string(s.copier_blocks) +
+           ",\"walker_blocks\":" + std::to_string(s.walker_blocks) + "}";
   }
 
   // Every buffer handed over so far has been walked (threaded mode; no-op inline).
@@ -137,13 +186,18 @@ class J2CSink {
     std::unique_ptr<uint8_t[]> buf[2];
     int cur = 0;  // next KVBuf dataFromUda fills
     // handshake (threaded mode)
-    std::mutex mu;
+    mutable std::mutex mu;
     std::condition_variable cv;
-    bool full[2] = {false, false};
+    std::atomic<bool> full[2] = {{false}, {false}};
     int64_t len[2] = {0, 0};
     int64_t handed = 0, walked = 0;
     bool stop = false;
+    std::atomic<bool> walker_waiting{false};
     std::thread walker;
+    // placement (sampled every 64 buffers) and handshake sleeps
+    std::map<int, int64_t> copier_cpus, walker_cpus;
+    int64_t copier_blocks = 0, walker_blocks = 0;
+    int pinned_l3 = -1;
     // walk results (written by the walking thread)
     int64_t records = 0, bytes = 0, buffers = 0, key_bytes = 0, order_errors = 0;
     std::atomic<bool> eof{false};
@@ -222,27 +276,112 @@ class J2CSink {
   void walk_loop(int r) {
     State& s = *st_[(size_t)r];
     int i = 0;
+    int64_t n = 0;
     for (;;) {
       int64_t len;
-      {
+      if (!spin_until([&] { return s.full[i].load(std::memory_order_acquire); })) {
         std::unique_lock<std::mutex> lk(s.mu);
-        s.cv.wait(lk, [&] { return s.full[i] || s.stop; });
-        if (!s.full[i]) return;  // stopped with nothing left
+        if (!s.full[i].load()) ++s.walker_blocks;
+        s.walker_waiting.store(true);
+        s.cv.wait(lk, [&] { return s.full[i].load() || s.stop; });
+        s.walker_waiting.store(false);
+        if (!s.full[i].load()) return;  // stopped with nothing left
+      }
+      {
+        std::lock_guard<std::mutex> g(s.mu);
         len = s.len[i];
+        if ((n++ & 63) == 0) sample_cpu(s.walker_cpus);
       }
       walk(r, s, s.buf[i].get(), len);
       {
         std::lock_guard<std::mutex> g(s.mu);
-        s.full[i] = false;
+        s.full[i].store(false, std::memory_order_release);
         ++s.walked;
       }
-      s.cv.notify_all();
+      s.cv.notify_all();  // a copier may block on this KVBuf, or flush() wait for the walk
       i ^= 1;
     }
   }
 
+  // Spin up to ~50 us for pred(); false: the caller blocks.
+  template <typename P>
+  static bool spin_until(P pred) {
+    if (pred()) return true;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; ++k) {
+      if (pred()) return true;
+      if ((k & 31) == 31 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) return false;
+      __builtin_ia32_pause();
+    }
+  }
+
+  static void sample_cpu(std::map<int, int64_t>& m) {  // caller holds the state's lock or owns the map
+    const int c = sched_getcpu();
+    if (c >= 0) m[c]++;
+  }
+  static int read_int(const std::string& path) {
+    std::ifstream f(path);
+    int v = -1;
+    if (f) f >> v;
+    return v;
+  }
+  static int cpu_l3(int cpu) { return read_int("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache/index3/id"); }
+  static int cpu_node(int cpu) {
+    for (int n = 0; n < 64; ++n) {
+      std::ifstream g("/sys/devices/system/node/node" + std::to_string(n) + "/cpulist");
+      if (!g) continue;
+      // the node's CPU list "a-b,c-d"
+      std::string list;
+      std::getline(g, list);
+      for (size_t b = 0; b < list.size();) {
+        size_t e = list.find(',', b);
+        if (e == std::string::npos) e = list.size();
+        const std::string r = list.substr(b, e - b);
+        const size_t dash = r.find('-');
+        const int lo = std::atoi(r.c_str()), hi = dash == std::string::npos ? lo : std::atoi(r.c_str() + dash + 1);
+        if (cpu >= lo && cpu <= hi) return n;
+        b = e + 1;
+      }
+    }
+    return -1;
+  }
+  // The CPUs sharing `cpu`'s last-level cache (empty if the host does not say).
+  static std::vector<int> l3_cpus(int cpu) {
+    std::ifstream f("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache/index3/shared_cpu_list");
+    std::vector<int> v;
+    std::string list;
+    if (!f || !std::getline(f, list)) return v;
+    for (size_t b = 0; b < list.size();) {
+      size_t e = list.find(',', b);
+      if (e == std::string::npos) e = list.size();
+      const std::string r = list.substr(b, e - b);
+      const size_t dash = r.find('-');
+      const int lo = std::atoi(r.c_str()), hi = dash == std::string::npos ? lo : std::atoi(r.c_str() + dash + 1);
+      for (int c = lo; c <= hi; ++c) v.push_back(c);
+      b = e + 1;
+    }
+    return v;
+  }
+  // First buffer of reducer r: the copying thread and the walker move onto the copier's last-level
+  // cache domain (both stay free to move within it), so the KVBuf the copier wrote is read from that
+  // cache instead of across the fabric or from DRAM.
+  void place(State& s) {
+    if (!threaded_ || !pin_l3_) return;
+    const int c = sched_getcpu();
+    if (c < 0) return;
+    const std::vector<int> cpus = l3_cpus(c);
+    if (cpus.size() < 2) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int x : cpus) CPU_SET(x, &set);
+    if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set) != 0) return;
+    if (s.walker.joinable()) (void)pthread_setaffinity_np(s.walker.native_handle(), sizeof(set), &set);
+    s.pinned_l3 = cpu_l3(c);
+  }
+
   int64_t kv_;
   bool threaded_;
+  bool pin_l3_ = true;
   bool check_order_ = false;
   int key_kind_ = 0;
   std::function<void(int)> on_eof_;
