@@ -386,9 +386,23 @@ SdmaEngine::SdmaEngine(int device) {
     if (use & (1u << b)) engine_ids_.push_back(1u << b);
   uint32_t hmask = 0;
   if (hsa_amd_memory_copy_engine_status(gpu_, cpu_, &hmask) != HSA_STATUS_SUCCESS) hmask = 0;
-  const uint32_t other = hmask & ~use;  // staging on a different engine than delivery
+  uint32_t other = hmask & ~use;  // staging on a different engine than delivery
+  if (other & 0xFu) other &= 0xFu;  // engines 4-7 stream at half the rate (r2_sdma_engine_sweep.md)
   const uint32_t pick = other ? other : hmask;
   h2d_engine_ = pick & (~pick + 1u);
+  // Several processes staging on one GPU (rank processes sharing a device, or the store loader next to a
+  // staging task) each get their own SDMA queue; on one engine those queues take turns. Spread them:
+  // the process's local rank (or its pid) picks among the candidate engines. UDA_SDMA_H2D_SPREAD=0 keeps
+  // every process on the lowest one.
+  const char* spread = std::getenv("UDA_SDMA_H2D_SPREAD");
+  if (!(spread && std::atoi(spread) == 0)) {
+    std::vector<uint32_t> cand;
+    for (int b = 0; b < 16; ++b)
+      if (pick & (1u << b)) cand.push_back(1u << b);
+    const char* lr = std::getenv("LOCAL_RANK");
+    const int who = lr ? std::atoi(lr) : (int)getpid();
+    if (cand.size() > 1) h2d_engine_ = cand[(size_t)who % cand.size()];
+  }
   UDA_LOG(kInfo, "SDMA delivery: device %d numa %d engines mask 0x%x preferred 0x%x", device, numa_node_, mask, pref);
 }
 
@@ -545,7 +559,10 @@ std::string SdmaEngine::describe() const {
     while (b < 16 && !(id & (1u << b))) ++b;
     e += std::to_string(b);
   }
-  return "sdma[numa=" + std::to_string(numa_node_) + " engines=" + (e.empty() ? "auto" : e) + "]";
+  int hb = 0;
+  while (hb < 16 && !(h2d_engine_ & (1u << hb))) ++hb;
+  return "sdma[numa=" + std::to_string(numa_node_) + " engines=" + (e.empty() ? "auto" : e) +
+         " h2d=" + (h2d_engine_ ? std::to_string(hb) : std::string("auto")) + "]";
 }
 
 }  // namespace gpu
