@@ -168,8 +168,17 @@ def test_cross_process_provider_over_ipc(require_gpu, tmp_path, service):
         recs, st, _ = run_reduce("127.0.0.1", "job_9_0005", ids, 1, datagen.TEXT, conf=conf, transport="tcp",
                                  data_port=port)
         assert recs == expected(maps, 1, datagen.TEXT)
-        assert st["device_descriptors"] == 5 and st["host_fetched_bytes"] == 0, st
-        assert st.get("merge_service", False) == (service == "auto"), st
+        brief = {k: st.get(k) for k in ("merge_path", "device_descriptors", "unmapped_descriptors", "unmapped_reason",
+                                        "host_fetched_bytes", "merge_service", "descriptor_map_ms")}
+        assert st.get("merge_service", False) == (service == "auto"), json.dumps(brief)
+        if service == "off":
+            assert st["device_descriptors"] == 5 and st["host_fetched_bytes"] == 0, json.dumps(brief)
+        else:
+            # the daemon (a child of the provider process) maps the provider's HBM where the platform
+            # lets it; where hipIpcOpenMemHandle refuses (tools/ipc_lineage_probe.py), the task fetches
+            # the bytes instead: every record arrives either way, and the reason is recorded
+            assert st["device_descriptors"] + st["unmapped_descriptors"] == 5, json.dumps(brief)
+            assert st["device_descriptors"] == 5 or "hipIpcOpenMemHandle" in st["unmapped_reason"], json.dumps(brief)
     finally:
         proc.stdin.close()
         out = proc.stdout.read()
