@@ -571,6 +571,8 @@ def run_node_files(args, ctx) -> int:
             "the documented deployment: Hadoop-layout MOF files -> provider front end (getPathUda, defaults) -> "
             "node daemon (HBM store, merge service) -> fresh reduce task processes with no mapred.uda.* keys")
         waves = warm + stats
+        out["first_wave"] = {"timeline_ms": waves[0]["timeline"], "task_ms_median": waves[0]["task_ms_median"],
+                             "task0": waves[0]["task0"]}
         out["first_step_ms"] = round(waves[0]["wall_ms"], 1)
         out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
         out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)

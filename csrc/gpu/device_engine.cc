@@ -64,7 +64,17 @@ void DeviceBuffer::alloc(size_t bytes, bool resident) {
   if (e != hipSuccess) {
     ptr_ = nullptr;
     HbmLedger::get().on_free(dev, (int64_t)held, resident);
-    HIP_CHECK(e);
+    (void)hipGetLastError();
+    const HbmLedger::Stats ls = HbmLedger::get().stats(dev);
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " allocating " +
+                             std::to_string(held) + " bytes on device " + std::to_string(dev) + " (" +
+                             std::to_string(free_b) + " free of " + std::to_string(total_b) +
+                             "; this process: used " + std::to_string(ls.used) + ", reserved " +
+                             std::to_string(ls.reserved) + ", node " + std::to_string(ls.node_bytes) +
+                             ", budget " + std::to_string(ls.budget) + (HbmLedger::get().bound() ? ", in a reservation" : "") +
+                             ")");
   }
   if (tt) trace::host_event("device_alloc", (int64_t)bytes, 0, tt, trace::now_ns());
   size_ = bytes;

@@ -43,6 +43,7 @@ enum Msg : uint32_t {
   kAck = 4,        // c->s: i32 dataFromUda status
   kExit = 5,       // c->s: reduce task close
   kDataHello = 6,  // c->s, on the task's second (data) connection: u64 session token
+  kCmdAsync = 7,   // c->s: a FETCH command; no result frame (a failure is reported as FAIL)
   kReady = 10,     // s->c: task started
   kRefused = 11,     // s->c: HELLO refused (reason)
   kConfReq = 12,   // s->c: u32 request id, key '\0' default
@@ -75,7 +76,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   uint32_t next_conf = 1;
   bool closed = false;  // the client went away
   // commands run on their own thread: INIT pulls configuration, which the reader thread answers
-  std::deque<std::string> cmds;
+  std::deque<std::pair<std::string, bool>> cmds;  // (command, async: no result frame)
   bool exit_requested = false;
   std::set<uint64_t> regions_sent;
   uint64_t token = 0;
@@ -261,12 +262,13 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   void run_commands() {
     for (;;) {
       std::string c;
-      bool ex;
+      bool ex, async = false;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return closed || exit_requested || !cmds.empty(); });
         if (!cmds.empty()) {
-          c = std::move(cmds.front());
+          c = std::move(cmds.front().first);
+          async = cmds.front().second;
           cmds.pop_front();
           ex = false;
         } else {
@@ -287,6 +289,10 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
           st = -1;
           why = e.what();
         }
+      }
+      if (async) {  // a FETCH: the client did not wait; its failure is the task's (failureInUda)
+        if (st != 0) host->fail(why);
+        continue;
       }
       std::string r;
       put<int32_t>(r, st);
@@ -317,8 +323,8 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
       if (!recv_msg(sock, &t, &p, &fd)) break;
       if (fd >= 0) close(fd);
       std::lock_guard<std::mutex> g(mu);
-      if (t == kCmd) {
-        cmds.push_back(std::move(p));
+      if (t == kCmd || t == kCmdAsync) {
+        cmds.emplace_back(std::move(p), t == kCmdAsync);
       } else if (t == kConfReply) {
         conf_replies[get<uint32_t>(p, 0)] = p.size() > 4 ? p.substr(4) : std::string();
       } else if (t == kExit) {
@@ -714,6 +720,14 @@ RemoteReduceTask::~RemoteReduceTask() {
 }
 
 void RemoteReduceTask::handle(const std::string& cmd) {
+  // FETCH commands do not wait for the service (a task's 32+ FETCHes arrive back to back and each
+  // round trip costs two thread wake-ups on a loaded node); the reference queues them on the native
+  // side too. INIT / FINAL / EXIT stay synchronous: their errors belong to the call.
+  HadoopCmd c;
+  if (parse_cmd(cmd, &c) && c.header == kFetchMsg) {
+    if (!impl_->send(kCmdAsync, cmd)) throw UdaError("merge service connection lost");
+    return;
+  }
   if (!impl_->send(kCmd, cmd)) throw UdaError("merge service connection lost");
   const auto r = impl_->wait_result();
   if (r.first != 0) throw UdaError(r.second);
