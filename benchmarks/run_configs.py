@@ -335,6 +335,56 @@ def _netmerger_concurrent(args, rows: int) -> dict:
     return out
 
 
+def hybrid_budget(args) -> dict:
+    """BASELINE config #4's mechanism on one GPU: one reduce task whose partition is several times its
+    device budget. The map outputs are in host memory (the DRAM tier), mapred.uda.gpu.hbm.budget caps
+    the device at --budget-gb and mapred.uda.gpu.merge.bytes at --merge-gb, so the task takes the GPU
+    hybrid merge (direct RPQ key-range rounds over the fetched partitions; the reference's LPQ/RPQ,
+    src/Merger/MergeManager.cc:202-288). The stream is validated natively (framing, key order, record
+    checksum against the generated runs)."""
+    import resource
+    from uda_amd import native
+    from uda_amd.bridge import UdaConsumer, UdaProvider
+    from uda_amd.utils.datagen import TEXT
+    from uda_amd.utils.mof import encode_partitions
+    n = native()
+    rows = int(args.gb * 1e9 / 100 / args.maps)
+    prov = UdaProvider()
+    total, want_sum = 0, 0
+    for m in range(args.maps):  # one map at a time: the host holds the encoded MOFs, not the runs too
+        parts = n.generate_runs("secondary", 1, 1, rows, 1000 + m)[0]
+        want_sum = (want_sum + n.ifile_checksum(parts[0])[2]) & 0xFFFFFFFFFFFFFFFF
+        data, index = encode_partitions(parts)
+        total += len(data) - 2
+        prov.add_mof_memory("job_hb", f"attempt_hb_m_{m:06d}_0", data, index)
+        del parts
+    budget = int(args.budget_gb * 1e9)
+    conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.hbm.budget": budget,
+            "mapred.uda.gpu.merge.bytes": int(args.merge_gb * 1e9), "mapred.uda.gpu.spill": "host"}
+    c = UdaConsumer(args.maps, "job_hb", "attempt_hb_r_000000_0", TEXT, conf=conf, keep_records=False, validate=True)
+    t0 = time.perf_counter()
+    for m in range(args.maps):
+        c.fetch("localhost", "job_hb", f"attempt_hb_m_{m:06d}_0", 0)
+    c.wait(3600)
+    wall = time.perf_counter() - t0
+    st = c.close()
+    v = c.validator
+    prov.close()
+    hs = n.hbm_stats(0)
+    out = {"config": "one NetMerger task over host MOFs, partition >> device budget (GPU hybrid)",
+           "gb": round(total / 1e9, 3), "maps": args.maps, "budget_gb": args.budget_gb, "merge_gb": args.merge_gb,
+           "ratio_partition_to_budget": round(total / budget, 2), "gbps": round(total / wall / 1e9, 3),
+           "wall_s": round(wall, 2), "merge_path": st.get("merge_path"), "hybrid_direct": st.get("hybrid_direct"),
+           "rpq_rounds": st.get("rpq_rounds"), "lpqs": st.get("lpqs"), "delivered_ok": st["bytes_delivered"] - 2 == total,
+           "ledger_peak_gb": round(hs["peak"] / 1e9, 2), "device_peak_gb": round(hs["device_peak"] / 1e9, 2),
+           "over_budget_bytes": hs["over"], "max_rss_gb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 1)}
+    out["validation"] = {"records": v.records, "order_errors": v.order_errors, "framing_errors": v.framing_errors,
+                         "eof": v.eof, "checksum_ok": v.checksum == want_sum}
+    out["validated"] = bool(v.order_errors == 0 and v.framing_errors == 0 and v.eof and v.checksum == want_sum
+                            and out["delivered_ok"])
+    return out
+
+
 def aio(args) -> dict:
     """AsyncIO read bandwidth vs a sequential pread loop (the reference's AIOHandler_test)."""
     from uda_amd import native
@@ -395,7 +445,7 @@ def radix(args) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("config", choices=["wordcount_loopback", "wordcount_tcp", "cpu_reference", "secondary_sort", "spill", "decode", "aio",
-                                       "netmerger", "radix"])
+                                       "netmerger", "radix", "hybrid_budget"])
     ap.add_argument("--dir", default="/tmp")
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lzo"])
     ap.add_argument("--gb", type=float, default=1.0)
@@ -403,6 +453,8 @@ def main() -> int:
     ap.add_argument("--reducers", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--validate", action="store_true")
+    ap.add_argument("--budget-gb", type=float, default=10.0, help="hybrid_budget: mapred.uda.gpu.hbm.budget")
+    ap.add_argument("--merge-gb", type=float, default=8.0, help="hybrid_budget: mapred.uda.gpu.merge.bytes")
     a = ap.parse_args()
     fn = globals()[a.config]
     out = fn(a)

@@ -49,6 +49,17 @@ RECIPES: dict[str, tuple[int, str]] = {
     "node_gap": (600, f"{PY} bench.py --api --node --reducers 15 --node-gap 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodefiles41": (900, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodefiles62": (1000, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 600000000 --steps 2 --warmup 1"),
+    "hybrid40": (900, f"{PY} benchmarks/run_configs.py hybrid_budget --gb 40 --maps 64 --budget-gb 10 --merge-gb 8"),
+    "budget_capi": (600, f"UDA_API_CONF=mapred.uda.gpu.hbm.budget=60000000000,mapred.uda.gpu.merge.bytes=1000000000 "
+                         f"{PY} bench.py --api --api-host-mofs --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "apihost2": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 2 --warmup 1"),
+    "coldnode5": (500, f"{PY} tools/cold_task_bench.py --node --repeat 5"),
+    "coldnode5_j2c": (500, f"UDA_J2C_THREADS=1 {PY} tools/cold_task_bench.py --node --repeat 5"),
+    "ipc4_host_nospread": (600, f"UDA_SDMA_H2D_SPREAD=0 {PY} bench.py --gpus 4 --one-gpu --exchange ipc --store host "
+                                f"--rows-per-gpu 100000000 --steps 2 --warmup 1"),
+    "hostmem": (60, "cat /proc/meminfo | head -5; cat /sys/fs/cgroup/memory.max 2>/dev/null; "
+                    "cat /sys/fs/cgroup/memory/memory.limit_in_bytes 2>/dev/null; nproc; "
+                    "cat /sys/fs/cgroup/cpu.max 2>/dev/null; cat /proc/sys/kernel/yama/ptrace_scope 2>/dev/null; true"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
     "coldnode": (400, f"{PY} tools/cold_task_bench.py --node --repeat 3"),
