@@ -116,7 +116,7 @@ struct DeviceWorkspace {
   hipStream_t cs = nullptr;
   static void ensure(gpu::DeviceBuffer& b, int64_t bytes) {
     bytes = std::max<int64_t>(bytes, 16);
-    if ((int64_t)b.size() < bytes) b.alloc((size_t)(bytes + bytes / 8));
+    if ((int64_t)b.size() < bytes) b.alloc_local((size_t)(bytes + bytes / 8));
   }
   int64_t device_bytes() const {
     return (int64_t)(in.held() + out.held() + packed.held() + out2.held() + frame_scratch.held() + frame_descs.held()) +
@@ -801,6 +801,52 @@ void ReduceTask::release_descriptors(const std::set<std::string>& hosts, const s
     throw UdaError("descriptor release not acknowledged by " + std::to_string(w->left) + " provider(s)");
 }
 
+namespace {
+// once per process: the context and the library's code objects (loaded at the first kernel launch);
+// later prewarms must not hipFree (it synchronizes the device under running tasks)
+void warm_code(int device) {
+  static std::once_flag code_once;
+  std::call_once(code_once, [device] {
+    uint8_t* tmp = nullptr;  // raw hipMalloc: the prewarm is not the merge (fault injection hits the merge)
+    HIP_CHECK(hipMalloc(&tmp, 4096));
+    HIP_CHECK(hipMemsetAsync(tmp, 0, 64, nullptr));
+    gpu::launch_max_i32(reinterpret_cast<int32_t*>(tmp), 1, reinterpret_cast<unsigned int*>(tmp + 32), nullptr);
+    HIP_CHECK(hipStreamSynchronize(nullptr));
+    try {  // the SDMA engines' queues (staging H2D, delivery D2H)
+      gpu::SdmaEngine::for_device(device).warm(tmp);
+    } catch (const std::exception& e) {
+      UDA_LOG(kWarn, "GPU prewarm: SDMA warm-up: %s", e.what());
+    }
+    HIP_CHECK(hipFree(tmp));
+  });
+}
+
+// `n` pooled merge workspaces with their pinned D2H rings (NUMA-local), held at once so the pool keeps n
+void warm_workspaces(int device, int n) {
+  std::vector<std::unique_ptr<PoolLease<DeviceWorkspace>>> held;
+  for (int i = 0; i < std::max(1, n); ++i) {
+    held.emplace_back(new PoolLease<DeviceWorkspace>{
+        device, DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); })});
+    auto& wl = *held.back();
+    if (wl.obj->ring.size() < (size_t)(2 * kPieceBytes))
+      wl.obj->ring.alloc_on_node((size_t)(2 * kPieceBytes), gpu::device_numa_node(device));
+    wl.clean = true;
+  }
+}
+}  // namespace
+
+void prewarm_node_merges(int device, int tasks, int64_t round_bytes, int maps, int64_t kv_buf) {
+  HIP_CHECK(hipSetDevice(device));
+  (void)gpu::SdmaEngine::for_device(device);
+  warm_code(device);
+  warm_workspaces(device, tasks);
+  gpu::DeviceReduceConfig cfg;
+  cfg.device = device;
+  cfg.kv_buf_bytes = kv_buf;
+  cfg.round_bytes = round_bytes;
+  gpu::prewarm_device_reduce(cfg, std::max(1, maps), tasks);
+}
+
 // Every reduce task of a Hadoop job usually runs in a fresh JVM (YarnChild), so what a warm process
 // keeps in its pools (HIP context, code objects, pinned rings and arenas, workspaces) a task would build
 // on its critical path: a 2 GB task went 27 -> 3.9 GB/s cold (profiles/r3_netmerger2.json). INIT comes
@@ -829,31 +875,10 @@ void ReduceTask::prewarm_gpu(PrewarmConf pc) {
     } catch (const std::exception&) {
     }
     lap("sdma");
-    // once per process: the context and the library's code objects (loaded at the first kernel
-    // launch); later prewarms must not hipFree (it synchronizes the device under running tasks)
-    static std::once_flag code_once;
-    std::call_once(code_once, [device] {
-      uint8_t* tmp = nullptr;  // raw hipMalloc: the prewarm is not the merge (fault injection hits the merge)
-      HIP_CHECK(hipMalloc(&tmp, 4096));
-      HIP_CHECK(hipMemsetAsync(tmp, 0, 64, nullptr));
-      gpu::launch_max_i32(reinterpret_cast<int32_t*>(tmp), 1, reinterpret_cast<unsigned int*>(tmp + 32), nullptr);
-      HIP_CHECK(hipStreamSynchronize(nullptr));
-      try {  // the SDMA engines' queues (staging H2D, delivery D2H)
-        gpu::SdmaEngine::for_device(device).warm(tmp);
-      } catch (const std::exception& e) {
-        UDA_LOG(kWarn, "GPU prewarm: SDMA warm-up: %s", e.what());
-      }
-      HIP_CHECK(hipFree(tmp));
-    });
+    warm_code(device);
     lap("code");
     // a workspace with its pinned D2H ring (NUMA-local), and an early stager, into the device pools
-    {
-      PoolLease<DeviceWorkspace> wl{device, DevicePool<DeviceWorkspace>::get().acquire(
-                                                device, [] { return std::make_unique<DeviceWorkspace>(); })};
-      if (wl.obj->ring.size() < (size_t)(2 * kPieceBytes))
-        wl.obj->ring.alloc_on_node((size_t)(2 * kPieceBytes), gpu::device_numa_node(device));
-      wl.clean = true;
-    }
+    warm_workspaces(device, 1);
     if (pc.early_h2d) {
       PoolLease<EarlyStager> sl{device, DevicePool<EarlyStager>::get().acquire(
                                             device, [device] { return std::make_unique<EarlyStager>(device); })};

@@ -35,6 +35,12 @@ class MofFetcher;
 // Map task id of a map attempt id (drops the trailing "_<attempt>").
 std::string map_task_of(const std::string& attempt);
 
+// A node daemon hosting reduce tasks' merges (service/node_daemon.h) builds once, at its start, what
+// each hosted task's GPU prewarm would build on the first wave's critical path: the device's code
+// objects and SDMA queues, and `tasks` pooled merge workspaces with their pinned delivery rings (rounds
+// of `round_bytes`, `maps` runs, dataFromUda buffers of `kv_buf` bytes). Throws on failure.
+void prewarm_node_merges(int device, int tasks, int64_t round_bytes, int maps, int64_t kv_buf);
+
 struct ReduceStats {
   int64_t maps_fetched = 0;
   int64_t bytes_fetched = 0;      // partition bytes received (compressed if compressed)

@@ -49,13 +49,13 @@ void hip_check(hipError_t e, const char* what, const char* file, int line) {
 
 // ------------------------------------------------------------------------------------ buffers
 DeviceBuffer::~DeviceBuffer() { reset(); }
-void DeviceBuffer::alloc(size_t bytes, bool resident) {
+void DeviceBuffer::alloc_impl(size_t bytes, bool resident, bool exportable) {
   reset();
   if (bytes == 0) return;
   if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
   // Blocks another process may map over hipIpc (our descriptor fetch, RCCL's peer registration of
   // send/receive buffers) must stay out of the size range that hangs the importer (device_ptr.h).
-  const size_t held = ipc_safe_bytes(bytes);
+  const size_t held = exportable ? ipc_safe_bytes(bytes) : bytes;
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
   HbmLedger::get().on_alloc(dev, (int64_t)held, resident);
@@ -309,11 +309,11 @@ int64_t DeviceMerger::merge_fixed(const std::vector<RunDesc>& runs, const std::v
   }
 
   if (!elems_a_.size()) {
-    elems_a_.alloc((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
-    elems_b_.alloc((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
+    elems_a_.alloc_local((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
+    elems_b_.alloc_local((size_t)std::max<int64_t>(max_records_, 1) * sizeof(Elem));
     // tiles per pass <= records/2048 + pairs; splits buffer sized for one pass
     const int64_t max_tiles = max_records_ / kMergeTile + max_runs_ + 2;
-    splits_.alloc((size_t)max_tiles * sizeof(int64_t));
+    splits_.alloc_local((size_t)max_tiles * sizeof(int64_t));
   }
   Slot& slot = slots_[next_slot_];
   next_slot_ = (next_slot_ + 1) % (int)slots_.size();
@@ -474,7 +474,7 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   gsamp[G] = soff[K];
   const int64_t per = nbmax + 2;
   auto ensure = [](DeviceBuffer& b, size_t bytes) {
-    if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+    if (b.size() < bytes) b.alloc_local(bytes + bytes / 8);
   };
   ensure(pb.samp_a, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
   ensure(pb.samp_b, (size_t)std::max<int64_t>(ns, 1) * sizeof(Elem));
@@ -567,7 +567,7 @@ int64_t DeviceMerger::run_kway(const KwayPlan& kp, uint8_t* out, hipStream_t s) 
   static const bool prof = std::getenv("UDA_KWAY_PROF") != nullptr;
   if (prof) {
     auto ensure = [](DeviceBuffer& b, size_t bytes) {
-      if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+      if (b.size() < bytes) b.alloc_local(bytes + bytes / 8);
     };
     ensure(kw_prof_, (size_t)kp.ncells * 5 * 8);
     HIP_CHECK(hipMemsetAsync(kw_prof_.as(), 0, (size_t)kp.ncells * 5 * 8, s));

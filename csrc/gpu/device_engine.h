@@ -69,7 +69,11 @@ class DeviceBuffer {
     }
     return *this;
   }
-  void alloc(size_t bytes, bool resident = false);
+  // padded by ipc_safe_bytes(): another process may map the block over hipIpc
+  void alloc(size_t bytes, bool resident = false) { alloc_impl(bytes, resident, true); }
+  // a task's working set that never leaves this process: no hipIpc padding (a 2.3 GB round buffer
+  // would otherwise hold 4.06 GB, past what its HBM reservation counted)
+  void alloc_local(size_t bytes) { alloc_impl(bytes, false, false); }
   void reset();
   template <typename T = uint8_t>
   T* as() const {
@@ -81,6 +85,7 @@ class DeviceBuffer {
   int device() const { return dev_; }
 
  private:
+  void alloc_impl(size_t bytes, bool resident, bool exportable);
   void take(DeviceBuffer& o) {
     ptr_ = o.ptr_;
     size_ = o.size_;

@@ -73,8 +73,10 @@ struct FixedWs {
     if (s) (void)hipStreamDestroy(s);
   }
   static void ensure(DeviceBuffer& b, size_t bytes) {
-    if (b.size() < bytes) b.alloc(bytes + bytes / 8);
+    if (b.size() < bytes) b.alloc_local(bytes + bytes / 8);
   }
+  // the bytes ensure(b, bytes) allocates
+  static int64_t grow(const DeviceBuffer& b, int64_t bytes) { return (int64_t)b.size() >= bytes ? 0 : bytes + bytes / 8; }
   int64_t device_bytes() const {
     int64_t n = merger ? merger->device_bytes() : 0;
     for (const DeviceBuffer* b : {&out[0], &out[1], &d_bases, &d_nrec, &d_soff, &d_samp, &d_bset, &d_out, &d_bounds,
@@ -200,20 +202,24 @@ int64_t fixed_round_ws_bytes(int64_t round_bytes, int runs) {
   return (int64_t)(2 * slot + 0.02 * (double)round_bytes) + (int64_t)runs * 4096 + (16ll << 20);
 }
 
-void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs) {
+void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs, int count) {
   HIP_CHECK(hipSetDevice(cfg.device));
-  WsLease lease(cfg.device);
-  FixedWs& ws = *lease.w;
   const int64_t rec = std::max<int64_t>(1, cfg.round_bytes / kTeraRecordBytes);
   const int64_t mr = rec + rec / 8;  // rounds run a little over their mean
-  if (!ws.merger || ws.merger->max_records() < mr || ws.merger->max_runs() < runs) ws.merger.reset(new DeviceMerger(mr, runs));
   const int64_t buf_bytes = std::max<int64_t>(1, cfg.kv_buf_bytes / kTeraRecordBytes) * kTeraRecordBytes;
   const int64_t piece = std::max<int64_t>(1, cfg.piece_bytes / buf_bytes) * buf_bytes;
   const int S = std::max(2, cfg.pinned_slots);
-  {
-    Ring ring(SdmaEngine::for_device(cfg.device), (size_t)piece * S, S);  // back to the engine's cache
+  // `count` workspaces and rings held at once, so the pools keep that many for concurrent tasks
+  std::vector<std::unique_ptr<WsLease>> leases;
+  std::vector<std::unique_ptr<Ring>> rings;
+  for (int i = 0; i < std::max(1, count); ++i) {
+    leases.push_back(std::make_unique<WsLease>(cfg.device));
+    FixedWs& ws = *leases.back()->w;
+    if (!ws.merger || ws.merger->max_records() < mr || ws.merger->max_runs() < runs) ws.merger.reset(new DeviceMerger(mr, runs));
+    rings.push_back(std::make_unique<Ring>(SdmaEngine::for_device(cfg.device), (size_t)piece * S, S));
   }
-  lease.clean = true;
+  rings.clear();  // back to the engine's cache
+  for (auto& l : leases) l->clean = true;
 }
 
 bool runs_are_fixed10(const std::vector<RunDesc>& runs, hipStream_t s) {
@@ -281,7 +287,11 @@ DeviceReduceStats device_reduce_fixed(const DeviceReduceConfig& cfg, const std::
   std::unique_ptr<HbmLedger::Reservation> res;
   if (!caller_reserved) {
     auto need = [&](int64_t rb) {
-      return std::max<int64_t>(0, fixed_round_ws_bytes(std::min(rb, N * kTeraRecordBytes), K) - ws.device_bytes());
+      // what this task allocates beyond the workspace's buffers that are already large enough (a pooled
+      // workspace's other buffers do not shrink what a grown one takes: alloc frees, then allocates anew)
+      const int64_t r = std::min(rb, N * kTeraRecordBytes), slot = (int64_t)((double)r * 1.1);
+      return FixedWs::grow(ws.out[0], slot) + FixedWs::grow(ws.out[1], slot) + (int64_t)(0.02 * (double)r) + (int64_t)K * 4096 +
+             (16ll << 20);
     };
     const int64_t hr = led.headroom(cfg.device);
     while (round_bytes > (64ll << 20) && need(round_bytes) > hr) round_bytes /= 2;
@@ -630,10 +640,10 @@ DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int 
       mi = std::max(mi, in_bytes[(size_t)q]);
       mr = std::max(mr, in_recs[(size_t)q]);
     }
-    const int64_t have = ws.device_bytes();
-    const int64_t want = 2 * (mi + mi / 8) + 2 * (mr * kTeraRecordBytes * 9 / 8) + (int64_t)(0.02 * (double)(mr * kTeraRecordBytes)) +
-                         (int64_t)K * 4096 + (16ll << 20) + 2 * (int64_t)NB * (int64_t)sizeof(DecodeDesc);
-    return std::max<int64_t>(0, want - have);
+    const int64_t ob = std::max<int64_t>(mr, 1) * kTeraRecordBytes, db = std::max<int64_t>(NB, 1) * (int64_t)sizeof(DecodeDesc);
+    return FixedWs::grow(ws.in[0], std::max<int64_t>(mi, 256)) + FixedWs::grow(ws.in[1], std::max<int64_t>(mi, 256)) +
+           FixedWs::grow(ws.out[0], ob) + FixedWs::grow(ws.out[1], ob) + FixedWs::grow(ws.d_descs[0], db) + FixedWs::grow(ws.d_descs[1], db) +
+           (int64_t)(0.02 * (double)ob) + (int64_t)K * 4096 + (16ll << 20);
   };
   std::unique_ptr<HbmLedger::Reservation> res;
   const bool caller_reserved = led.bound() != nullptr && led.bound()->device() == cfg.device;

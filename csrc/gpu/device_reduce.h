@@ -52,7 +52,8 @@ struct DeviceReduceStats {
 // task process: Hadoop runs every reduce task in its own JVM): a pooled workspace with its stream,
 // a merger sized for `runs` runs and rounds of `round_bytes` (its upload slots and plan tables; the
 // round's output slots stay for the HBM admission), and the delivery ring in the SDMA engine's cache.
-void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs);
+// count > 1: that many at once (a node daemon ahead of the concurrent tasks it will host).
+void prewarm_device_reduce(const DeviceReduceConfig& cfg, int runs, int count = 1);
 
 // HBM a FIXED10 round working set of `round_bytes` merged bytes needs (two output slots and the
 // merger's per-round tables), for admission.

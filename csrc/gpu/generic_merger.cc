@@ -46,13 +46,13 @@ void GenericMerger::reserve(int64_t records, int runs) {
   if (records <= cap_records_ && runs <= cap_runs_) return;
   records = std::max<int64_t>(records, 1);
   const int64_t max_tiles = records / kGenericMergeTile + runs + 2;
-  elems_a_.alloc((size_t)records * sizeof(Elem));
-  elems_b_.alloc((size_t)records * sizeof(Elem));
-  splits_.alloc((size_t)max_tiles * 8);
-  sizes_.alloc((size_t)records * 8);
-  out_off_.alloc((size_t)(std::max<int64_t>(records, runs) + 1) * 8);  // also holds elem_off (runs+1)
-  scan_tmp_.alloc((size_t)scan_tmp_elems(records) * 8);
-  side_.alloc((size_t)records * 24);  // keyptr(8) recptr(8) keylen(4) reclen(4)
+  elems_a_.alloc_local((size_t)records * sizeof(Elem));
+  elems_b_.alloc_local((size_t)records * sizeof(Elem));
+  splits_.alloc_local((size_t)max_tiles * 8);
+  sizes_.alloc_local((size_t)records * 8);
+  out_off_.alloc_local((size_t)(std::max<int64_t>(records, runs) + 1) * 8);  // also holds elem_off (runs+1)
+  scan_tmp_.alloc_local((size_t)scan_tmp_elems(records) * 8);
+  side_.alloc_local((size_t)records * 24);  // keyptr(8) recptr(8) keylen(4) reclen(4)
   cap_records_ = records;
   cap_runs_ = std::max(runs, cap_runs_);
 }
@@ -95,7 +95,7 @@ bool GenericMerger::kway_level(int depth, const Elem* in, const std::vector<int6
   if (gk_.size() < 3) gk_.resize(3);  // depth <= 2; sized up front so `b` stays valid across recursion
   KwayBuffers& b = gk_[(size_t)depth];
   auto ensure = [](DeviceBuffer& x, size_t bytes) {
-    if (x.size() < bytes) x.alloc(bytes + bytes / 8 + 64);
+    if (x.size() < bytes) x.alloc_local(bytes + bytes / 8 + 64);
   };
   const size_t ns_b = sizeof(Elem) * (size_t)std::max<int64_t>(ns, 1);
   ensure(b.tab, 8 * (size_t)(K + 1));

@@ -120,7 +120,9 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     static_cast<Session*>(ctx)->send(kFail, reason && *reason ? reason : "merge service task failure");
   }
 
-  std::string conf(const std::string& key, const std::string& dflt) {
+  std::string conf(const std::string& key, const std::string& dflt_in) {
+    const auto od = svc->opt_.conf_defaults.find(key);
+    const std::string& dflt = od != svc->opt_.conf_defaults.end() ? od->second : dflt_in;
     uint32_t id;
     {
       std::lock_guard<std::mutex> g(mu);

@@ -59,6 +59,9 @@ class MergeService {
     // a hosted task ended (its session is over): e.g. drop the references its descriptors hold in the
     // HBM store living in this process, whether or not the task released them itself
     std::function<void(const std::string& reduce_task_id)> session_ended;
+    // defaults of this host for keys a hosted task reads: sent as the default of the configuration pull,
+    // so the client's own value (a key its job sets) still wins
+    std::map<std::string, std::string> conf_defaults;
   };
   // Listen on `path` (a stale socket file is replaced). Pinned host memory allocated by this process
   // from now on is shareable with clients (sdma.h set_pinned_shareable).

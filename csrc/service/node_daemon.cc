@@ -14,7 +14,9 @@
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <thread>
 
+#include "../consumer/reduce_task.h"
 #include "../gpu/device_ptr.h"
 #include "../gpu/hbm_ledger.h"
 #include "merge_service.h"
@@ -440,6 +442,7 @@ struct Daemon {
   bool closed = false, exit_req = false;
   std::shared_ptr<DeviceStore> store;
   std::unique_ptr<MergeService> svc;
+  std::thread prewarm;  // GPU prewarm for the first wave of hosted tasks
   std::deque<std::string> starts;
 
   bool send(uint32_t t, const std::string& p) {
@@ -637,6 +640,9 @@ int run_node_daemon(int ctl_fd) {
       mo.users = d->conf("mapred.uda.gpu.merge.service.users", "*");
       mo.max_sessions = (int)std::atoi(d->conf("mapred.uda.gpu.merge.service.max.sessions", "256").c_str());
       mo.conf_timeout_s = std::atof(d->conf("mapred.uda.gpu.merge.service.conf.timeout.s", "60").c_str());
+      // a task hosted next to an HBM store fetches device descriptors: no pinned fetch arena to prewarm
+      // (15 hosted tasks pinning 1 GB each serialized the first wave in the driver, ~150 ms a task)
+      if (store_bytes > 0) mo.conf_defaults["mapred.uda.gpu.prewarm.pinned.mb"] = "0";
       Daemon* dp = d.get();
       mo.session_ended = [dp](const std::string& task) {
         std::shared_ptr<DeviceStore> st;
@@ -653,6 +659,28 @@ int run_node_daemon(int ctl_fd) {
     put_str(ready, svc_path);
     put<int64_t>(ready, store_bytes);
     d->send(kDReady, ready);
+    // what the first wave of hosted tasks would each build on its critical path (code objects, pooled
+    // workspaces, shareable pinned delivery rings), built once now, long before the first task comes
+    const int warm_tasks = d->svc && !devs.empty()
+                               ? (int)std::atoi(d->conf("mapred.uda.daemon.prewarm.tasks", "16").c_str())
+                               : 0;
+    if (warm_tasks > 0) {
+      const int64_t rb = std::atoll(d->conf("mapred.uda.gpu.round.bytes", std::to_string(2ll << 30)).c_str());
+      const int64_t kvb = std::atoll(d->conf("mapred.uda.kv.buf.size", std::to_string(1 << 20)).c_str());
+      const int per = (warm_tasks + (int)devs.size() - 1) / (int)devs.size();
+      d->prewarm = std::thread([devs, per, rb, kvb] {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int dv : devs) {
+          try {
+            prewarm_node_merges(dv, per, rb, 32, kvb);
+          } catch (const std::exception& e) {
+            UDA_LOG(kWarn, "node daemon: GPU prewarm of device %d: %s", dv, e.what());
+          }
+        }
+        UDA_LOG(kInfo, "node daemon: prewarmed %d task workspace(s) on %d device(s) in %.0f ms", per, (int)devs.size(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      });
+    }
     std::unique_lock<std::mutex> lk(d->mu);
     d->cv.wait(lk, [&] { return d->closed || d->exit_req; });
   } catch (const std::exception& e) {
@@ -662,6 +690,7 @@ int run_node_daemon(int ctl_fd) {
     rc = 1;
   }
   // teardown: hosted tasks first (they read the store), then the store
+  if (d->prewarm.joinable()) d->prewarm.join();
   d->svc.reset();
   {
     std::shared_ptr<DeviceStore> st;
