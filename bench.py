@@ -557,7 +557,19 @@ def run_node_files(args, ctx) -> int:
         info = json.loads(first) if first.strip() else {"error": f"front end exited rc={frontend.poll()}"}
         if "error" in info:
             raise RuntimeError(f"provider front end failed: {info['error']}")
-        daemon = info["provider"].get("hbm_store", {}).get("daemon", {})
+        # a NodeManager is up long before its first reduce task: wait for the node daemon (HBM store, merge
+        # service) and its first-wave prewarm, as a job would find them
+        t_ready = time.perf_counter()
+        while True:
+            frontend.stdin.write("stats\n")
+            frontend.stdin.flush()
+            hs = json.loads(frontend.stdout.readline()).get("hbm_store", {})
+            if (hs.get("daemon", {}).get("ready") and hs.get("prewarm", {}).get("done", True)) or \
+                    time.perf_counter() - t_ready > 120:
+                break
+            time.sleep(0.2)
+        node_ready_s = time.perf_counter() - t
+        daemon = dict(hs.get("daemon", {}), prewarm=hs.get("prewarm"))
         print(f"# node files: map phase {t_map:.1f}s ({job['store_bytes'] / 1e9:.1f} GB in {args.maps_per_gpu} "
               f"file.out), front end up in {time.perf_counter() - t:.1f}s, node daemon {daemon}", file=sys.stderr,
               flush=True)
@@ -577,6 +589,8 @@ def run_node_files(args, ctx) -> int:
         out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
         out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)
         out["conf_keys"] = 0
+        out["node_ready_s"] = round(node_ready_s, 2)
+        out["daemon_prewarm"] = daemon.get("prewarm")
         out["task0_hosted"] = bool(stats[-1]["task0"].get("merge_service"))
         print(json.dumps(out), flush=True)
         return 0

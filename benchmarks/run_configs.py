@@ -358,6 +358,8 @@ def hybrid_budget(args) -> dict:
         total += len(data) - 2
         prov.add_mof_memory("job_hb", f"attempt_hb_m_{m:06d}_0", data, index)
         del parts
+        if m % 8 == 7:  # progress (a GPU box takes a silent minute for a hung run)
+            print(f"# hybrid_budget: {m + 1}/{args.maps} maps, {total / 1e9:.1f} GB", file=sys.stderr, flush=True)
     budget = int(args.budget_gb * 1e9)
     conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.hbm.budget": budget,
             "mapred.uda.gpu.merge.bytes": int(args.merge_gb * 1e9), "mapred.uda.gpu.spill": "host"}
@@ -365,7 +367,10 @@ def hybrid_budget(args) -> dict:
     t0 = time.perf_counter()
     for m in range(args.maps):
         c.fetch("localhost", "job_hb", f"attempt_hb_m_{m:06d}_0", 0)
-    c.wait(3600)
+    while not c._done.wait(30):
+        print(f"# hybrid_budget: merging, {time.perf_counter() - t0:.0f} s, "
+              f"{c.validator.records if c.validator else 0} records delivered", file=sys.stderr, flush=True)
+    c.wait(1)
     wall = time.perf_counter() - t0
     st = c.close()
     v = c.validator

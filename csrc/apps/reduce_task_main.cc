@@ -12,9 +12,9 @@
 // they arrive; the task runs until its merged stream's EOF marker has been walked. stdout: one JSON
 // line (consumer counts, the phases of the process's life, the task's own stats). Exit code 0 only if
 // the task delivered every expected record with intact framing (and key order, --check-order).
-// UDA_J2C_THREADS=1 runs the consumer as the plugin does: dataFromUda copies into the KVBuf on the
-// delivering thread, the walk runs on a walker thread of its own, the reducer's thread in the plugin
-// (default: both inline on the delivering thread).
+// The consumer runs as the plugin does: dataFromUda copies into the KVBuf on the delivering thread, the
+// walk runs on a walker thread of its own (the reducer's thread in the plugin), both pinned to the
+// copier's last-level cache (j2c_sink.h). UDA_J2C_THREADS=0: both inline on the delivering thread.
 #include <time.h>
 #include <unistd.h>
 
@@ -122,7 +122,10 @@ int main(int argc, char** argv) {
   // the job's configuration holds only the -D keys (a node-shape run passes none); --kv-buf sets the
   // dataFromUda buffer size on both sides
   if (kv_buf_set) host.conf["mapred.uda.kv.buf.size"] = std::to_string(kv_buf);
-  uda::gpu::J2CSink sink(1, kv_buf);  // UDA_J2C_THREADS=1: copy on the delivering thread, walk on this one
+  // the plugin's two threads unless UDA_J2C_THREADS=0: a service-hosted cold task 12.8-13.4 GB/s in 5 of 5
+  // trials against 10.7-11.3 inline (profiles/r5_j2c_consumer_ab.md)
+  const char* jt = std::getenv("UDA_J2C_THREADS");
+  uda::gpu::J2CSink sink(1, kv_buf, !jt || std::atoi(jt) != 0);
   sink.set_check_order(check_order);
   sink.set_key_kind(1);
   sink.set_on_eof([&host](int) {

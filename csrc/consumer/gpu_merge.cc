@@ -2098,11 +2098,19 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       cfg.kv_buf_bytes = kv_buf_size_;
       cfg.round_bytes = round_bytes;
       cfg.stop = [&] { return stop_.load(); };
+      // the node's tasks take turns for each round's block decode (mapred.uda.gpu.decode.slots, FIFO)
+      if (const int slots = (int)host_->conf_i64("mapred.uda.gpu.decode.slots", 1); slots > 0) {
+        cfg.decode_turn = [this, device, slots] {
+          return DeviceGate::get(1).acquire(device, slots, [&] { return stop_.load(); });
+        };
+        cfg.decode_done = [device] { DeviceGate::get(1).release(device); };
+      }
       bool streamed = false;
       const gpu::DeviceReduceStats ds = gpu::device_reduce_fixed_blocks(cfg, (int)codec_, bp, sink, &streamed);
       if (streamed) {
         std::lock_guard<std::mutex> g(st_mu_);
         st_.hbm_wait_ms += ds.hbm_wait_ms;
+        st_.gpu_gate_wait_ms += ds.decode_wait_ms;
         st_.hbm_reserved = ds.hbm_reserved;
         st_.round_bytes = ds.round_bytes;
         st_.records = ds.records;

@@ -8,11 +8,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "block_decoder.h"
 #include "device_engine.h"
@@ -61,6 +64,7 @@ struct FixedWs {
   // prefixes + first keys, and the per-round decode descriptors
   DeviceBuffer in[2], prefix, d_first, d_keys, d_descs[2];
   hipStream_t s = nullptr;
+  hipStream_t ds = nullptr;  // streaming decode: round decodes and cuts, beside the merges on s
   hipEvent_t merged[2] = {nullptr, nullptr};
   FixedWs() {
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -68,6 +72,10 @@ struct FixedWs {
   }
   ~FixedWs() {
     if (s) (void)hipStreamSynchronize(s);
+    if (ds) {
+      (void)hipStreamSynchronize(ds);
+      (void)hipStreamDestroy(ds);
+    }
     for (auto e : merged)
       if (e) (void)hipEventDestroy(e);
     if (s) (void)hipStreamDestroy(s);
@@ -691,6 +699,14 @@ DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int 
     st.sink_ms += now_ms() - a;
     st.buffers++;
   };
+  if (!ws.ds) HIP_CHECK(hipStreamCreateWithFlags(&ws.ds, hipStreamNonBlocking));
+  // the prefix pass and this task's earlier use of the buffers (on s) come first
+  hipEvent_t planned = nullptr;
+  HIP_CHECK(hipEventCreateWithFlags(&planned, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(planned, s));
+  HIP_CHECK(hipStreamWaitEvent(ws.ds, planned, 0));
+  HIP_CHECK(hipEventDestroy(planned));
+  hipStream_t ds = ws.ds;
   st.plan_ms = now_ms() - t0;
   std::vector<int64_t> round_recs((size_t)Q, 0);
   int64_t decoded_blocks = 0;
@@ -714,23 +730,39 @@ DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int 
       n[(size_t)k] = sp.rec1 - sp.rec0;
     }
     decoded_blocks += (int64_t)rd.size();
-    HIP_CHECK(hipMemcpyAsync(ws.d_descs[par].as(), rd.data(), rd.size() * sizeof(DecodeDesc), hipMemcpyHostToDevice, s));
-    launch_block_decode(codec, nullptr, in, ws.d_descs[par].as<DecodeDesc>(), (int)rd.size(), ws.flag.as<int>(), s);
+    struct Turn {
+      const DeviceReduceConfig& c;
+      bool held = false;
+      ~Turn() {
+        if (held && c.decode_done) c.decode_done();
+      }
+    } turn{cfg};
+    if (cfg.decode_turn) {
+      const double w = now_ms();
+      if (!cfg.decode_turn()) throw UdaError("reduce task stopped while waiting for a device decode turn");
+      turn.held = true;
+      st.decode_wait_ms += now_ms() - w;
+    }
+    // the round input was last read by round q-2's merge (on s)
+    if (q >= 2) HIP_CHECK(hipStreamWaitEvent(ds, ws.merged[par], 0));
+    HIP_CHECK(hipMemcpyAsync(ws.d_descs[par].as(), rd.data(), rd.size() * sizeof(DecodeDesc), hipMemcpyHostToDevice, ds));
+    launch_block_decode(codec, nullptr, in, ws.d_descs[par].as<DecodeDesc>(), (int)rd.size(), ws.flag.as<int>(), ds);
     // exactly the round's records of every run: [lower_bound(low), lower_bound(high))
     const Elem b2[2] = {q > 0 ? bounds[(size_t)q - 1] : Elem{0, 0}, q + 1 < Q ? bounds[(size_t)q] : Elem{~0ull, ~0ull}};
     uint8_t** dbases = ws.d_bases.as<uint8_t*>() + (size_t)par * K;
     int64_t* dn = ws.d_nrec.as<int64_t>() + (size_t)par * K;
     Elem* dbd = ws.d_bounds.as<Elem>() + 2 * par;
     int64_t* dpos = ws.d_out.as<int64_t>() + (size_t)par * K * 4;
-    HIP_CHECK(hipMemcpyAsync(dbases, bases.data(), (size_t)K * sizeof(uint8_t*), hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(dn, n.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(dbd, b2, sizeof(b2), hipMemcpyHostToDevice, s));
-    launch_split_fixed(dbases, dn, dbd, ws.d_bset.as<int>(), K, 2, dpos, s);
+    HIP_CHECK(hipMemcpyAsync(dbases, bases.data(), (size_t)K * sizeof(uint8_t*), hipMemcpyHostToDevice, ds));
+    HIP_CHECK(hipMemcpyAsync(dn, n.data(), (size_t)K * 8, hipMemcpyHostToDevice, ds));
+    HIP_CHECK(hipMemcpyAsync(dbd, b2, sizeof(b2), hipMemcpyHostToDevice, ds));
+    launch_split_fixed(dbases, dn, dbd, ws.d_bset.as<int>(), K, 2, dpos, ds);
     HIP_CHECK(hipGetLastError());
     std::vector<int64_t> pos((size_t)K * 4);
-    HIP_CHECK(hipMemcpyAsync(pos.data(), dpos, pos.size() * 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(flags, ws.flag.as(), sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMemcpyAsync(pos.data(), dpos, pos.size() * 8, hipMemcpyDeviceToHost, ds));
+    HIP_CHECK(hipMemcpyAsync(flags, ws.flag.as(), sizeof(int), hipMemcpyDeviceToHost, ds));
+    // the decode stream only: round q-1's merge keeps running on s (the merge of q follows it there)
+    HIP_CHECK(hipStreamSynchronize(ds));
     if (flags[0]) throw UdaError("corrupt compressed block in a map output partition");
     std::vector<RunDesc> rq((size_t)K);
     int64_t total = 0;
@@ -790,14 +822,62 @@ DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int 
       eof_sent = true;
     }
   };
-  enqueue_round(0);
-  for (int q = 0; q < Q; ++q) {
-    if (q + 1 < Q) enqueue_round(q + 1);  // its slots held round q-1, delivered in the last iteration
-    const double a = now_ms();
-    HIP_CHECK(hipEventSynchronize(ws.merged[q & 1]));
-    st.merge_wait_ms += now_ms() - a;
-    deliver_round(q);
+  // Rounds are delivered by a thread of their own, in order, while this one decodes, cuts and merges the
+  // next: enqueue_round waits for its split positions (a stream sync that also covers the previous
+  // round's merge), which in one thread held the round before it back from the link. Round q reuses
+  // round q-2's slots, so it is enqueued once q-2 is delivered.
+  std::mutex dmu;
+  std::condition_variable dcv;
+  int enqueued = 0, delivered = 0;
+  bool abort = false;
+  std::exception_ptr derr;
+  std::thread dthr([&] {
+    try {
+      HIP_CHECK(hipSetDevice(cfg.device));
+      for (int q = 0; q < Q; ++q) {
+        {
+          std::unique_lock<std::mutex> lk(dmu);
+          dcv.wait(lk, [&] { return abort || enqueued > q; });
+          if (abort) return;
+        }
+        const double a = now_ms();
+        HIP_CHECK(hipEventSynchronize(ws.merged[q & 1]));
+        st.merge_wait_ms += now_ms() - a;
+        deliver_round(q);
+        std::lock_guard<std::mutex> g(dmu);
+        delivered = q + 1;
+        dcv.notify_all();
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> g(dmu);
+      derr = std::current_exception();
+      abort = true;
+      dcv.notify_all();
+    }
+  });
+  try {
+    for (int q = 0; q < Q; ++q) {
+      {
+        std::unique_lock<std::mutex> lk(dmu);
+        dcv.wait(lk, [&] { return abort || delivered >= q - 1; });
+        if (abort) break;
+      }
+      enqueue_round(q);
+      std::lock_guard<std::mutex> g(dmu);
+      enqueued = q + 1;
+      dcv.notify_all();
+    }
+  } catch (...) {
+    {
+      std::lock_guard<std::mutex> g(dmu);
+      abort = true;
+      dcv.notify_all();
+    }
+    dthr.join();
+    throw;
   }
+  dthr.join();
+  if (derr) std::rethrow_exception(derr);
   if (merger.bad_layout()) throw std::runtime_error("device reduce: non-TeraSort record in a FIXED10 run");
   int64_t got = 0;
   for (int q = 0; q < Q; ++q) got += round_recs[(size_t)q];
@@ -806,6 +886,7 @@ DeviceReduceStats device_reduce_fixed_blocks(const DeviceReduceConfig& cfg, int 
                    std::to_string(N));
   st.records = N;
   st.decoded_blocks = decoded_blocks;
+  HIP_CHECK(hipStreamSynchronize(ds));
   HIP_CHECK(hipStreamSynchronize(s));
   lease.clean = true;
   return st;

@@ -33,7 +33,12 @@ struct DeviceReduceConfig {
   // round that could never fit the budget is halved until it does. A reservation already bound to
   // the calling thread (a caller that reserved for decode + merge at once) is drawn from instead.
   std::function<bool()> stop;         // gives up waiting for HBM when true
-}; 
+  // device_reduce_fixed_blocks: a device-wide turn for each round's block decode (the node's tasks decode
+  // one at a time, FIFO: the first rounds reach the link after one decode instead of all of them).
+  // decode_turn() returns false when the task stopped while waiting; decode_done() ends the turn.
+  std::function<bool()> decode_turn;
+  std::function<void()> decode_done;
+};
 
 struct DeviceReduceStats {
   int64_t records = 0;
@@ -43,6 +48,7 @@ struct DeviceReduceStats {
   int merge_passes = 0;
   double plan_ms = 0, merge_wait_ms = 0, d2h_wait_ms = 0, sink_ms = 0;
   double hbm_wait_ms = 0;      // waiting for the HBM reservation
+  double decode_wait_ms = 0;   // device_reduce_fixed_blocks: waiting for decode turns
   int64_t hbm_reserved = 0;    // bytes reserved for the round working set
   int64_t round_bytes = 0;     // round size used (after any shrink to fit the budget)
   int64_t decoded_blocks = 0;  // device_reduce_fixed_blocks: blocks decoded over all rounds

@@ -10,8 +10,10 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <thread>
@@ -443,6 +445,8 @@ struct Daemon {
   std::shared_ptr<DeviceStore> store;
   std::unique_ptr<MergeService> svc;
   std::thread prewarm;  // GPU prewarm for the first wave of hosted tasks
+  std::atomic<int> prewarm_tasks{0}, prewarm_done{0};
+  std::atomic<int64_t> prewarm_us{0};
   std::deque<std::string> starts;
 
   bool send(uint32_t t, const std::string& p) {
@@ -487,7 +491,11 @@ struct Daemon {
       st = store;
     }
     std::string s = st ? st->stats_json() : "{}";
-    const std::string ms = svc ? svc->stats_json() : "{}";
+    std::string ms = svc ? svc->stats_json() : "{}";
+    char pw[96];
+    std::snprintf(pw, sizeof(pw), "\"prewarm\":{\"tasks\":%d,\"done\":%s,\"ms\":%.1f}", prewarm_tasks.load(),
+                  prewarm_done.load() ? "true" : "false", (double)prewarm_us.load() / 1e3);
+    ms = ms + "," + pw;
     return s.size() <= 2 ? "{\"merge_service\":" + ms + "}" : s.substr(0, s.size() - 1) + ",\"merge_service\":" + ms + "}";
   }
 
@@ -668,7 +676,9 @@ int run_node_daemon(int ctl_fd) {
       const int64_t rb = std::atoll(d->conf("mapred.uda.gpu.round.bytes", std::to_string(2ll << 30)).c_str());
       const int64_t kvb = std::atoll(d->conf("mapred.uda.kv.buf.size", std::to_string(1 << 20)).c_str());
       const int per = (warm_tasks + (int)devs.size() - 1) / (int)devs.size();
-      d->prewarm = std::thread([devs, per, rb, kvb] {
+      d->prewarm_tasks = per * (int)devs.size();
+      Daemon* dp = d.get();
+      d->prewarm = std::thread([dp, devs, per, rb, kvb] {
         const auto t0 = std::chrono::steady_clock::now();
         for (int dv : devs) {
           try {
@@ -677,8 +687,10 @@ int run_node_daemon(int ctl_fd) {
             UDA_LOG(kWarn, "node daemon: GPU prewarm of device %d: %s", dv, e.what());
           }
         }
-        UDA_LOG(kInfo, "node daemon: prewarmed %d task workspace(s) on %d device(s) in %.0f ms", per, (int)devs.size(),
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        dp->prewarm_us = (int64_t)(ms * 1e3);
+        dp->prewarm_done = 1;
+        UDA_LOG(kInfo, "node daemon: prewarmed %d task workspace(s) on %d device(s) in %.0f ms", per, (int)devs.size(), ms);
       });
     }
     std::unique_lock<std::mutex> lk(d->mu);

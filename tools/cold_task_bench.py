@@ -104,6 +104,8 @@ def node(args) -> int:
                     argv.append("--check-order")
                 if svc:
                     argv += ["-D", f"mapred.uda.gpu.merge.service={path}"]
+                for kv in args.conf:
+                    argv += ["-D", kv]
                 argv += ["--", "-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
                 init = n.form_cmd(INIT, [str(args.maps), "job_cold", "attempt_cold_r_000000_0", "0", str(1 << 20),
                                          str(16 << 10), TEXT, "null", str(256 << 10), "0", "0"])
@@ -129,7 +131,7 @@ def node(args) -> int:
                                   "fetch_to_first_data_ms": res["fetch_to_first_data_ms"],
                                   **{k: round(st.get(k, -1), 1) for k in ("gpu_h2d_ms", "gpu_device_ms", "gpu_d2h_wait_ms",
                                                                            "gpu_sink_ms")},
-                                  "merge_path": st.get("merge_path")}), flush=True)
+                                  "merge_path": st.get("merge_path"), "j2c": res.get("j2c")}), flush=True)
         finally:
             prov.close()
     return 0
@@ -145,6 +147,7 @@ def main() -> int:
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--backend", default="gpu", help="--node: mapred.uda.merge.backend of the tasks")
     ap.add_argument("--service-only", action="store_true", help="--node: only the merge-service trials")
+    ap.add_argument("--conf", action="append", default=[], help="--node: extra -D key=value of every task")
     ap.add_argument("--node", action="store_true",
                     help="provider (and merge service) in this process, each task a fresh uda_reduce_task process")
     args = ap.parse_args()

@@ -39,6 +39,8 @@ RECIPES: dict[str, tuple[int, str]] = {
     "sec2_one_gpu": (600, f"{PY} bench.py --api --workload secondary --gpus 2 --one-gpu --rows-per-gpu 235000000 --steps 3 --warmup 1"),
     "snappy41": (400, f"{PY} bench.py --api --api-codec snappy --rows-per-gpu 400000000 --steps 3 --warmup 1"),
     "snappy130": (600, f"{PY} bench.py --api --api-codec snappy --steps 2 --warmup 1"),
+    "snappy130x5": (600, f"{PY} bench.py --api --api-codec snappy --steps 5 --warmup 1 --verbose"),
+    "lzo130x5": (600, f"{PY} bench.py --api --api-codec lzo --steps 5 --warmup 1 --verbose"),
     "lzo41": (400, f"{PY} bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 3 --warmup 1"),
     "ipc2": (400, f"{PY} bench.py --gpus 2 --one-gpu --exchange ipc --rows-per-gpu 300000000 --steps 3 --warmup 1"),
     "ipc4": (400, f"{PY} bench.py --gpus 4 --one-gpu --exchange ipc --rows-per-gpu 150000000 --steps 3 --warmup 1"),
@@ -55,11 +57,17 @@ RECIPES: dict[str, tuple[int, str]] = {
     "apihost2": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 2 --warmup 1"),
     "coldnode5": (500, f"{PY} tools/cold_task_bench.py --node --repeat 5"),
     "coldnode5_j2c": (500, f"UDA_J2C_THREADS=1 {PY} tools/cold_task_bench.py --node --repeat 5"),
+    "coldnode5_inline": (500, f"UDA_J2C_THREADS=0 {PY} tools/cold_task_bench.py --node --repeat 5"),
+    "coldnode5_c8": (500, f"{PY} tools/cold_task_bench.py --node --repeat 5 --conf mapred.uda.tcp.connections=8"),
+    "hybrid41api": (600, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000,mapred.uda.gpu.merge.bytes=8000000000 "
+                         f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 1 --warmup 0"),
     "ipc4_host_nospread": (600, f"UDA_SDMA_H2D_SPREAD=0 {PY} bench.py --gpus 4 --one-gpu --exchange ipc --store host "
                                 f"--rows-per-gpu 100000000 --steps 2 --warmup 1"),
     "hostmem": (60, "cat /proc/meminfo | head -5; cat /sys/fs/cgroup/memory.max 2>/dev/null; "
                     "cat /sys/fs/cgroup/memory/memory.limit_in_bytes 2>/dev/null; nproc; "
                     "cat /sys/fs/cgroup/cpu.max 2>/dev/null; cat /proc/sys/kernel/yama/ptrace_scope 2>/dev/null; true"),
+    "aio20": (300, f"{PY} benchmarks/run_configs.py aio --gb 20 --dir /tmp"),
+    "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
     "coldnode": (400, f"{PY} tools/cold_task_bench.py --node --repeat 3"),
@@ -81,6 +89,15 @@ PMC_PASSES = [
 ]
 for i, counters in enumerate(PMC_PASSES):
     RECIPES[f"pmc{i + 1}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/pmc{i + 1} -o run -- {PMC_PROG}")
+# the K-way kernel against a plain device copy of the same bytes (tools/hbm_copy_roof.py): L2 traffic
+# and hit rates per pass, each within the TCC block's 4 counters
+ROOF_PASSES = {"a": "FETCH_SIZE TCC_HIT_sum", "b": "WRITE_SIZE TCC_MISS_sum",
+               "c": "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"}
+for k, counters in ROOF_PASSES.items():
+    RECIPES[f"roof_kw_{k}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_kw_{k} -o run -- "
+                                   f"{PMC_PROG}")
+    RECIPES[f"roof_copy_{k}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_copy_{k} -o run -- "
+                                     f"python3 tools/hbm_copy_roof.py")
 
 
 def summarize(path: str, keys: list[str]) -> str:
