@@ -965,6 +965,16 @@ void ReduceTask::merge_gpu() {
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     budget = (int64_t)(free_b / 4);
   }
+  // and within the device's HBM budget (mapred.uda.gpu.hbm.budget, hbm_ledger.h): the staged input, the
+  // pipelined RPQ rounds' workspaces and the stagers come to ~4x the input budget
+  {
+    const int64_t hr = gpu::HbmLedger::get().headroom(device);
+    if (hr > 0 && budget > hr / 4) {
+      budget = std::max<int64_t>(hr / 4, 64ll << 20);
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.merge_budget_from_ledger = 1;
+    }
+  }
   const std::string tier = host_->get_conf("mapred.uda.gpu.spill", init_.local_dirs.empty() ? "host" : "disk");
   StreamGuard sg;
   HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
@@ -1360,6 +1370,10 @@ void ReduceTask::merge_gpu() {
         for (auto& f : ready) tot += std::max<int64_t>(f->part_len(), 0);
         progressive = drained == 0 && tot <= budget && (!prog_auto || staged_merges(device).load() == 1);
         if (progressive) {
+          {
+            std::lock_guard<std::mutex> g(st_mu_);
+            st_.merge_path = "staged-progressive";
+          }
           prog = std::make_unique<ProgFetch>();
           ProgFetch& pf = *prog;
           pf.P = prog_phases;

@@ -880,7 +880,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"records\":" << s.records << ",\"buffers\":" << s.buffers << ",\"lpqs\":" << s.lpqs
     << ",\"spill_bytes\":" << s.spill_bytes << ",\"fetch_ms\":" << s.fetch_ms << ",\"merge_ms\":" << s.merge_ms
     << ",\"total_ms\":" << s.total_ms << ",\"device_decoded_blocks\":" << s.device_decoded_blocks
-    << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"hybrid_direct\":" << s.hybrid_direct << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
+    << ",\"rpq_rounds\":" << s.rpq_rounds << ",\"hybrid_direct\":" << s.hybrid_direct << ",\"merge_budget_from_ledger\":" << s.merge_budget_from_ledger << ",\"gpu_h2d_ms\":" << s.gpu_h2d_ms
     << ",\"gpu_device_ms\":" << s.gpu_device_ms << ",\"gpu_d2h_wait_ms\":" << s.gpu_d2h_wait_ms
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"gpu_prewarm_phases\":\"" << json_escape(s.gpu_prewarm_phases) << "\"" << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs

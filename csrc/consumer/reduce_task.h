@@ -54,6 +54,7 @@ struct ReduceStats {
   int64_t device_decoded_blocks = 0;  // compressed blocks decoded in HBM by the F6 kernels
   int64_t rpq_rounds = 0;             // GPU hybrid: key-range rounds of the RPQ merge; device fetch: merge rounds
   int64_t hybrid_direct = 0;          // GPU hybrid: RPQ rounds straight over the fetched partitions (no LPQ level)
+  int64_t merge_budget_from_ledger = 0;  // staged path: input budget capped by the HBM ledger's headroom
   int64_t gpu_ws_bytes = 0;           // device fetch, generic keys: HBM held by the merge workspaces
   // GPU backend phase split: H2D staging, device decode+merge, waits on D2H pieces, host consumers
   // (dataFromUda / spill writes) of the pinned pieces

@@ -20,6 +20,7 @@ class LocalDeviceStore : public DeviceStore {
     co.odirect = true;
     co.lease_s = o.lease_s;
     cache_ = std::make_unique<gpu::MofCache>(co);
+    cache_->start_loaders();  // the loaders come up now, not under the first wave
   }
 
   bool acquire(const std::string& job, const std::string& path, const std::string& holder, int64_t offset,

@@ -78,6 +78,24 @@ MofCache::MofCache(const Options& o) : opt_(o) {
   for (int d : opt_.devices) used_[d] = 0;
 }
 
+MofCache::Loader* MofCache::loader_locked(int device) {
+  std::unique_ptr<Loader>& L = loaders_[device];
+  if (!L) {
+    L.reset(new Loader);
+    L->device = device;
+    Loader* lp = L.get();
+    L->thr = std::thread([this, lp] { loader_main(lp); });
+    L->opener = std::thread([this, lp] { opener_main(lp); });
+  }
+  return L.get();
+}
+
+void MofCache::start_loaders() {
+  if (!enabled()) return;
+  std::lock_guard<std::mutex> g(mu_);
+  for (int d : opt_.devices) (void)loader_locked(d);
+}
+
 MofCache::~MofCache() {
   std::vector<std::unique_ptr<Loader>> ls;
   {
@@ -240,14 +258,7 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
   e->waiters.push_back(Waiter{need_end, std::move(ready)});
   used_[device] += std::max<int64_t>(len, 1);
   entries_[path] = e;
-  std::unique_ptr<Loader>& L = loaders_[device];
-  if (!L) {
-    L.reset(new Loader);
-    L->device = device;
-    Loader* lp = L.get();
-    L->thr = std::thread([this, lp] { loader_main(lp); });
-    L->opener = std::thread([this, lp] { opener_main(lp); });
-  }
+  Loader* L = loader_locked(device);
   L->pending.push_back(e);
   L->ocv.notify_all();
   return true;

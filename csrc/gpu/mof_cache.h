@@ -80,6 +80,9 @@ class MofCache {
   MofCache& operator=(const MofCache&) = delete;
 
   bool enabled() const { return opt_.capacity > 0 && !opt_.devices.empty(); }
+  // Start every device's loader now (its I/O ring, pinned staging, SDMA signals) instead of at the
+  // first file: a node daemon does this at start, off the first wave's critical path.
+  void start_loaders();
   int64_t capacity() const { return opt_.capacity; }
   // Take `holder`'s reference on the MOF file `path` of job `job` (loading it on first touch) and
   // call ready() once its first need_end bytes are resident: inline if they already are, else from
@@ -134,6 +137,7 @@ class MofCache {
   Ref ref_of(const Entry& e) const;
   void loader_main(Loader* L);
   void opener_main(Loader* L);
+  Loader* loader_locked(int device);  // the device's loader, started on first use (mu_ held)
   void fail_entry(Entry& e, const std::string& why, std::vector<Fire>* fire);  // mu_ held
   void collect_ready(Entry& e, std::vector<Fire>* fire);                      // mu_ held
 

@@ -67,6 +67,18 @@ RECIPES: dict[str, tuple[int, str]] = {
                     "cat /sys/fs/cgroup/memory/memory.limit_in_bytes 2>/dev/null; nproc; "
                     "cat /sys/fs/cgroup/cpu.max 2>/dev/null; cat /proc/sys/kernel/yama/ptrace_scope 2>/dev/null; true"),
     "aio20": (300, f"{PY} benchmarks/run_configs.py aio --gb 20 --dir /tmp"),
+    "hybrid41b": (600, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000 "
+                       f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 1 --warmup 0"),
+    "sec100_j2c": (600, f"UDA_J2C_THREADS=1 {PY} bench.py --api --workload secondary --rows-per-gpu 970000000 --steps 2 --warmup 1"),
+    "api130_j2c": (500, f"UDA_J2C_THREADS=1 {PY} bench.py --api --steps 3 --warmup 1"),
+    "bench_j2c": (400, f"UDA_J2C_THREADS=1 {PY} bench.py --steps 3 --warmup 1"),
+    "counters": (90, "timeout -k 10 60 rocprofv3 --list-avail > gpurun_out/counters_avail.txt 2>&1; true"),
+    "lzo130_s2": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.slots=2 {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1"),
+    "snappy130_s2": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.slots=2 {PY} bench.py --api --api-codec snappy --steps 5 --warmup 1"),
+    "apihost2_c8": (600, f"UDA_API_CONF=mapred.uda.tcp.connections=8 {PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu "
+                         f"--rows-per-gpu 200000000 --steps 2 --warmup 1"),
+    "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
+    "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
     "node1": (300, f"{PY} bench.py --api --node --reducers 1 --node-slots 1 --rows-per-gpu 20000000 --maps-per-gpu 32 --steps 3 --warmup 1"),
     "cold": (400, f"{PY} tools/cold_task_bench.py --repeat 2"),
@@ -93,6 +105,8 @@ for i, counters in enumerate(PMC_PASSES):
 # and hit rates per pass, each within the TCC block's 4 counters
 ROOF_PASSES = {"a": "FETCH_SIZE TCC_HIT_sum", "b": "WRITE_SIZE TCC_MISS_sum",
                "c": "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"}
+# raw L2 -> fabric read requests by size (FETCH_SIZE's derivation is checked against a copy of known bytes)
+ROOF_PASSES["d"] = "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum"
 for k, counters in ROOF_PASSES.items():
     RECIPES[f"roof_kw_{k}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_kw_{k} -o run -- "
                                    f"{PMC_PROG}")
