@@ -124,8 +124,7 @@ int main(int argc, char** argv) {
   if (kv_buf_set) host.conf["mapred.uda.kv.buf.size"] = std::to_string(kv_buf);
   // the plugin's two threads unless UDA_J2C_THREADS=0: a service-hosted cold task 12.8-13.4 GB/s in 5 of 5
   // trials against 10.7-11.3 inline (profiles/r5_j2c_consumer_ab.md)
-  const char* jt = std::getenv("UDA_J2C_THREADS");
-  uda::gpu::J2CSink sink(1, kv_buf, !jt || std::atoi(jt) != 0);
+  uda::gpu::J2CSink sink(1, kv_buf, uda::gpu::J2CSink::plugin_threaded());
   sink.set_check_order(check_order);
   sink.set_key_kind(1);
   sink.set_on_eof([&host](int) {

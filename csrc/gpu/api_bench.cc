@@ -445,7 +445,7 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   std::condition_variable cv;
   int done = 0;
   std::vector<TaskHost> hosts(R);  // before the sink: its reduce-task threads report EOF into them
-  J2CSink sink(R, cfg_.kv_buf_bytes);
+  J2CSink sink(R, cfg_.kv_buf_bytes, J2CSink::plugin_threaded());
   sink.set_on_eof([&hosts](int r) {  // the reduce task's thread walked its EOF marker
     TaskHost& t = hosts[(size_t)r];
     std::lock_guard<std::mutex> g(*t.mu);

@@ -50,6 +50,13 @@ class J2CSink {
     const char* e = std::getenv("UDA_J2C_THREADS");
     return e && std::atoi(e) != 0;
   }
+  // The reduce task's stand-in (C ABI bench, uda_reduce_task): the plugin's own shape, two threads
+  // pinned to one last-level cache, unless UDA_J2C_THREADS=0. Config #5 at 100 GB, whose skewed task is
+  // consumer-bound: 40.1 GB/s against 29.6 inline (profiles/r5/r5k_sec100_j2c.log).
+  static bool plugin_threaded() {
+    const char* e = std::getenv("UDA_J2C_THREADS");
+    return !e || std::atoi(e) != 0;
+  }
   J2CSink(int reducers, int64_t kv_buf_bytes, bool threaded = default_threaded())
       : kv_(kv_buf_bytes), threaded_(threaded) {
     st_.reserve((size_t)reducers);

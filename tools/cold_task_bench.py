@@ -137,6 +137,75 @@ def node(args) -> int:
     return 0
 
 
+def files(args) -> int:
+    """The documented deployment for one cold task: TeraSort map outputs written as Hadoop-layout MOF
+    files, the provider front end (uda_mof_supplier mode=frontend, library defaults: node daemon with
+    the HBM store and the merge service), and every trial a fresh uda_reduce_task process with no
+    mapred.uda.* key. Trial 0 reads the files from disk into the store (a job's first reducer touching
+    them); later trials are cold task processes over a warm store, as every later reducer of the job."""
+    import shutil
+    import socket
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bindir = os.path.join(root, "uda_amd", "bin")
+    exe, sup = os.path.join(bindir, "uda_reduce_task"), os.path.join(bindir, "uda_mof_supplier")
+    mof_dir = tempfile.mkdtemp(prefix="uda-cold-files-", dir=args.mof_dir)
+    fe = None
+    try:
+        recs = int(args.gb * 1e9 / 104 / args.maps)
+        g = subprocess.run([sup, "mode=mapgen", f"mof_dir={mof_dir}", "device=0", f"maps={args.maps}", "reducers=1",
+                            f"records_per_map={recs}", "workload=terasort"], stdout=subprocess.PIPE, text=True,
+                           timeout=600)
+        job = json.loads(g.stdout.strip().splitlines()[-1])
+        cmds, expect = job["commands"][0], job["expected"][0]
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        fe = subprocess.Popen([sup, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"], stdin=subprocess.PIPE,
+                              stdout=subprocess.PIPE, text=True)
+        json.loads(fe.stdout.readline())
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 120:  # the node daemon and its prewarm, as a job finds them
+            fe.stdin.write("stats\n")
+            fe.stdin.flush()
+            hs = json.loads(fe.stdout.readline()).get("hbm_store", {})
+            if hs.get("daemon", {}).get("ready") and hs.get("prewarm", {}).get("done", True):
+                break
+            time.sleep(0.2)
+        start = ["-w", "256", "-r", str(port), "-a", "1", "-m", "1", "-g", "/tmp", "-s", "1024"]
+        for t in range(args.repeat + 1):
+            argv = [exe, "--expect", str(expect)] + (["--check-order"] if t == args.repeat else [])
+            for kv in args.conf:
+                argv += ["-D", kv]
+            p = subprocess.Popen(argv + ["--"] + start, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            p.stdin.write(cmds[0] + "\n")
+            p.stdin.flush()
+            time.sleep(args.gap)
+            p.stdin.write("\n".join(cmds[1:]) + "\n")
+            p.stdin.close()
+            out = p.stdout.read()
+            p.wait(timeout=300)
+            res = json.loads(out.strip().splitlines()[-1])
+            if p.returncode != 0 or res.get("error"):
+                print(json.dumps({"error": res.get("error"), "rc": p.returncode}), flush=True)
+                return 1
+            st = res["task"]
+            print(json.dumps({"mode": "files", "trial": t, "store": "cold (files read)" if t == 0 else "warm",
+                              "order_checked": t == args.repeat, "gb": round(res["bytes"] / 1e9, 3),
+                              "gbps": round(res["bytes"] / res["fetch_to_eof_ms"] / 1e6, 2),
+                              "fetch_to_eof_ms": res["fetch_to_eof_ms"], "fetch_to_first_data_ms": res["fetch_to_first_data_ms"],
+                              "fetch_ms": round(st.get("fetch_ms", -1), 1), "merge_ms": round(st.get("merge_ms", -1), 1),
+                              "gpu_sink_ms": round(st.get("gpu_sink_ms", -1), 1), "merge_service": st.get("merge_service"),
+                              "merge_path": st.get("merge_path"), "j2c": res.get("j2c")}), flush=True)
+        return 0
+    finally:
+        if fe is not None and fe.poll() is None:
+            fe.stdin.write("exit\n")
+            fe.stdin.flush()
+            fe.wait(120)
+        shutil.rmtree(mof_dir, ignore_errors=True)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gb", type=float, default=2.0)
@@ -147,12 +216,18 @@ def main() -> int:
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--backend", default="gpu", help="--node: mapred.uda.merge.backend of the tasks")
     ap.add_argument("--service-only", action="store_true", help="--node: only the merge-service trials")
-    ap.add_argument("--conf", action="append", default=[], help="--node: extra -D key=value of every task")
+    ap.add_argument("--conf", action="append", default=[], help="--node/--files: extra -D key=value of every task")
+    ap.add_argument("--files", action="store_true",
+                    help="MOF files -> provider front end with library defaults (node daemon, HBM store, merge "
+                         "service) -> each trial a fresh uda_reduce_task with no mapred.uda.* key")
+    ap.add_argument("--mof-dir", default="/tmp", help="--files: where the MOF files are written")
     ap.add_argument("--node", action="store_true",
                     help="provider (and merge service) in this process, each task a fresh uda_reduce_task process")
     args = ap.parse_args()
     if args.child:
         return child(args)
+    if args.files:
+        return files(args)
     if args.node:
         return node(args)
     for _ in range(args.repeat):

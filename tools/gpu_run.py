@@ -77,6 +77,11 @@ RECIPES: dict[str, tuple[int, str]] = {
     "snappy130_s2": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.slots=2 {PY} bench.py --api --api-codec snappy --steps 5 --warmup 1"),
     "apihost2_c8": (600, f"UDA_API_CONF=mapred.uda.tcp.connections=8 {PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu "
                          f"--rows-per-gpu 200000000 --steps 2 --warmup 1"),
+    "coldfiles5": (500, f"{PY} tools/cold_task_bench.py --files --repeat 5"),
+    "lzo130_s3": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.stream.slots=3 {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1"),
+    "lzo130_s4": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.stream.slots=4 {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1"),
+    "sec100_inline": (600, f"UDA_J2C_THREADS=0 {PY} bench.py --api --workload secondary --rows-per-gpu 970000000 --steps 2 --warmup 1"),
+    "api130_inline": (500, f"UDA_J2C_THREADS=0 {PY} bench.py --api --steps 3 --warmup 1"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
