@@ -2113,9 +2113,10 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       cfg.round_bytes = round_bytes;
       cfg.stop = [&] { return stop_.load(); };
       // the node's tasks take turns for each round's block decode (FIFO, this many at once; 0 = no
-      // limit). One round's decode (a wave per 256 KiB block, ~8k blocks) leaves the device half idle:
-      // 130 GB LZO 38.7 GB/s with one at a time, 45.7 with two; Snappy 54.0 / 53.9 (r5j, r5k)
-      if (const int slots = (int)host_->conf_i64("mapred.uda.gpu.decode.stream.slots", 2); slots > 0) {
+      // limit). One round's decode (a wave per 256 KiB block, ~8k blocks) leaves the device idle: 130 GB
+      // LZO 38.7 GB/s with one at a time, 45.7 with two, 49.3 with three; Snappy 54.0 / 53.9 / 53.3,
+      // link-bound (profiles/r5/r5{j,k,l}_*130*.log)
+      if (const int slots = (int)host_->conf_i64("mapred.uda.gpu.decode.stream.slots", 3); slots > 0) {
         cfg.decode_turn = [this, device, slots] {
           return DeviceGate::get(1).acquire(device, slots, [&] { return stop_.load(); });
         };

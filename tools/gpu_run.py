@@ -82,6 +82,8 @@ RECIPES: dict[str, tuple[int, str]] = {
     "lzo130_s4": (600, f"UDA_API_CONF=mapred.uda.gpu.decode.stream.slots=4 {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1"),
     "sec100_inline": (600, f"UDA_J2C_THREADS=0 {PY} bench.py --api --workload secondary --rows-per-gpu 970000000 --steps 2 --warmup 1"),
     "api130_inline": (500, f"UDA_J2C_THREADS=0 {PY} bench.py --api --steps 3 --warmup 1"),
+    "aio60": (300, f"{PY} benchmarks/run_configs.py aio --gb 60 --dir /tmp"),
+    "coldfiles6": (500, f"{PY} tools/cold_task_bench.py --files --repeat 6"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
@@ -91,9 +93,9 @@ RECIPES: dict[str, tuple[int, str]] = {
     "nodesvc": (400, f"{PY} bench.py --api --node --node-service --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodesvc130": (500, f"{PY} bench.py --api --node --node-service --reducers 15 --steps 2 --warmup 1"),
     "netmerger": (400, f"{PY} benchmarks/run_configs.py netmerger --gb 2 --maps 64 --reducers 1"),
-    "prof_bench": (500, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- "
+    "prof_bench": (500, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- "
                         "python3 bench.py --steps 3 --warmup 1"),
-    "prof_device_only": (400, "rocprofv3 --kernel-trace --stats -d gpurun_out/prof_device_only -o run -- "
+    "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }
 
