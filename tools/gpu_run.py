@@ -84,6 +84,10 @@ RECIPES: dict[str, tuple[int, str]] = {
     "api130_inline": (500, f"UDA_J2C_THREADS=0 {PY} bench.py --api --steps 3 --warmup 1"),
     "aio60": (300, f"{PY} benchmarks/run_configs.py aio --gb 60 --dir /tmp"),
     "coldfiles6": (500, f"{PY} tools/cold_task_bench.py --files --repeat 6"),
+    "apihost2_g4": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 2 --warmup 1 "
+                         f"--api-gpu-slots 4"),
+    "apihost2_g3": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 2 --warmup 1 "
+                         f"--api-gpu-slots 3"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
