@@ -257,6 +257,13 @@ class EarlyStager {
     copies_ = 0;
     bytes_ = 0;
   }
+  // reset() and give the device blocks back (a task switching to direct RPQ rounds: its staged copies
+  // are not used, and the rounds' workspaces need that HBM within the budget)
+  void release_blocks() {
+    reset();
+    std::lock_guard<std::mutex> g(mu_);
+    blocks_.clear();
+  }
   double issue_ms() const { return issue_ms_; }
   int64_t copies() const { return copies_; }
   int64_t bytes() const { return bytes_; }
@@ -965,12 +972,13 @@ void ReduceTask::merge_gpu() {
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     budget = (int64_t)(free_b / 4);
   }
-  // and within the device's HBM budget (mapred.uda.gpu.hbm.budget, hbm_ledger.h): the staged input, the
-  // pipelined RPQ rounds' workspaces and the stagers come to ~4x the input budget
+  // and within the device's HBM budget (mapred.uda.gpu.hbm.budget, hbm_ledger.h): three pipelined RPQ
+  // rounds of budget/2 input, each workspace ~3x its input, come to ~4.5x the input budget (the stager's
+  // blocks are released at the switch to direct rounds)
   {
     const int64_t hr = gpu::HbmLedger::get().headroom(device);
-    if (hr > 0 && budget > hr / 4) {
-      budget = std::max<int64_t>(hr / 4, 64ll << 20);
+    if (hr > 0 && budget > hr / 5) {
+      budget = std::max<int64_t>(hr / 5, 64ll << 20);
       std::lock_guard<std::mutex> g(st_mu_);
       st_.merge_budget_from_ledger = 1;
     }
@@ -1282,7 +1290,7 @@ void ReduceTask::merge_gpu() {
     if (direct) return;
     direct = true;
     if (stager) {
-      stager->reset();  // the partitions' HBM copies are not used: RPQ rounds copy their slices
+      stager->release_blocks();  // the partitions' HBM copies are not used: RPQ rounds copy their slices
       stager = nullptr;
     }
     // indexed beside the fetch (which goes on filling `group`; the spans indexed here are a copy)

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import sys
 import secrets
 import time
 
@@ -82,10 +83,16 @@ class TeraSortShuffle:
         t0 = time.perf_counter()
         if self.ctx.world > 1:
             if self.cfg.exchange == "ipc" and not self._ipc_preflight():
-                # every rank saw the same verdict (all-gathered). No silent switch to another backend:
-                # RCCL runs only when asked for (--exchange rccl)
-                raise RuntimeError(f"IPC exchange preflight failed ({self.ipc_fallback}); the job stops here. "
-                                   "Fix the cause, or run with --exchange rccl to use RCCL instead")
+                # every rank saw the same verdict (all-gathered), so all switch together: the shuffle runs
+                # over RCCL, and the reason stays in the job's record (ipc_fallback, the bench JSON).
+                # UDA_IPC_FALLBACK=0 stops the job instead.
+                if os.environ.get("UDA_IPC_FALLBACK", "1") == "0":
+                    raise RuntimeError(f"IPC exchange preflight failed ({self.ipc_fallback}); the job stops here "
+                                       "(UDA_IPC_FALLBACK=0)")
+                if self.ctx.rank == 0:
+                    print(f"uda: IPC exchange preflight failed, shuffling over RCCL ({self.ipc_fallback})",
+                          file=sys.stderr, flush=True)
+                self.cfg.exchange = "rccl"
             if self.cfg.exchange == "ipc":
                 name = f"uda.{os.getpid()}.{secrets.token_hex(6)}".encode() if self.ctx.rank == 0 else None
                 self.job.init_ipc(self.ctx.broadcast_bytes(name).decode())
@@ -147,7 +154,7 @@ class TeraSortShuffle:
         if bad:
             self.ipc_fallback = "; ".join(bad)[:500]
             if r == 0:
-                print(f"uda: IPC exchange preflight failed ({self.ipc_fallback})", flush=True)
+                print(f"uda: IPC exchange preflight failed ({self.ipc_fallback})", file=sys.stderr, flush=True)
             return False
         return True
 
