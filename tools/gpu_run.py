@@ -88,6 +88,8 @@ RECIPES: dict[str, tuple[int, str]] = {
                          f"--api-gpu-slots 4"),
     "apihost2_g3": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 2 --warmup 1 "
                          f"--api-gpu-slots 3"),
+    "apihost2_41": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 400000000 --steps 3 --warmup 1"),
+    "apihost2_s5": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 5 --warmup 1"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
