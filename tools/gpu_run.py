@@ -90,6 +90,8 @@ RECIPES: dict[str, tuple[int, str]] = {
                          f"--api-gpu-slots 3"),
     "apihost2_41": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 400000000 --steps 3 --warmup 1"),
     "apihost2_s5": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 5 --warmup 1"),
+    "coldfiles6_nopin": (500, f"UDA_J2C_PIN=none {PY} tools/cold_task_bench.py --files --repeat 6"),
+    "coldnode5_nopin": (500, f"UDA_J2C_PIN=none {PY} tools/cold_task_bench.py --node --repeat 5"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
