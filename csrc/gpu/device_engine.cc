@@ -248,6 +248,8 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   slot_bytes_ += (size_t)max_runs * (sizeof(RunDesc) + 4 * sizeof(int64_t) + 2 * sizeof(int)) + 64 * 16;
   if (const char* e = std::getenv("UDA_KWAY")) kway_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("UDA_KWAY_CAP")) kw_cap_ = std::atoi(e);
+  if (const char* e = std::getenv("UDA_KWAY_STAGED")) kw_staged_ = std::atoi(e) != 0;
+  if (kw_staged_ && kw_cap_ > 1024) kw_cap_ = 1024;  // a staged cell's records must fit LDS
   if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536, 1792 or 2048");
   kw_overflow_.alloc(sizeof(int));
   HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
@@ -555,6 +557,11 @@ DeviceMerger::KwayPlan DeviceMerger::plan_kway(const std::vector<RunDesc>& runs,
   kd.bad_layout = flag_.as<int>();
   kd.cap = (int)cap;
   kd.kmax = kmax;
+  // the staged kernel reads each record's words from LDS at the run's own alignment mod 16: 8-byte
+  // aligned runs only (partitions of Hadoop MOF files start 2 bytes after the previous one's EOF marker)
+  bool aligned8 = true;
+  for (const auto& r : runs) aligned8 = aligned8 && ((uintptr_t)r.base & 7) == 0;
+  kd.staged = kw_staged_ && aligned8 ? 1 : 0;
   kp.ncells = cell_first[G];
   kp.total = total_records(runs);
   return kp;

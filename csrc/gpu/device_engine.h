@@ -219,6 +219,7 @@ class DeviceMerger {
   // single-pass K-way merge (kway.hip): samples (ping-pong), splitters, cell split table, overflow
   bool kway_ = true;
   int kw_cap_ = 2048;  // records per k-way cell (UDA_KWAY_CAP); in-place LDS merge: 4 workgroups per CU
+  bool kw_staged_ = false;  // UDA_KWAY_STAGED: records staged in LDS once (kway_staged_kernel)
   DeviceBuffer kw_prof_, kw_overflow_;
   struct PlanBufs {  // per plan slot: samples, splitters, cell splits, sample-merge scratch
     DeviceBuffer samp_runs, samp_a, samp_b, bounds, split, splits;

@@ -159,6 +159,7 @@ struct KwayDesc {
   int cap = kKwCap;           // records per cell on the LDS path (kway_cap_supported)
   unsigned long long* prof = nullptr;  // optional [cell][5] phase timestamps (UDA_KWAY_PROF)
   int kmax = kKwMaxRuns;      // most runs in one group of this plan (sizes the per-slice LDS tables)
+  int staged = 0;             // records staged in LDS once (kway_staged_kernel; cap 512 or 1024)
 };
 // bounds[g*nbmax + j] = splitter j of group g (sample (j+1)*ns_g/C_g of the group's merged samples),
 // +infinity for j >= C_g - 1.

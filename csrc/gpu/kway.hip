@@ -44,6 +44,8 @@ __device__ __forceinline__ bool kle(const Elem& a, const Elem& b) {
 }
 
 typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
+typedef __attribute__((address_space(1))) const void GlobalVoid;
+typedef __attribute__((address_space(3))) void LdsVoid;
 // Run pointers are generic; the records live in global memory, so load through that address space.
 __device__ __forceinline__ const GlobalU64* gptr(const void* p) { return (const GlobalU64*)(uintptr_t)p; }
 
@@ -213,6 +215,146 @@ __device__ __forceinline__ void kw_gather64(const uint8_t* const* sbase, const E
   }
 }
 
+// A cell that does not fit LDS (only massively duplicated keys): a wave-level priority queue. Lane l
+// owns slices l, l + 64, ... (K <= 256: four per lane, their remaining and taken counts in registers);
+// each step a wave argmin picks the next record. Wave 0 only.
+__device__ void kw_overflow_pq(const KwayDesc& kd, const int* seg, const uint8_t* const* sbase, int K, int n,
+                             uint8_t* obase) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  constexpr int kWords = kTeraRecordBytes / 8;
+  constexpr int kPer = kKwMaxRuns / 64;
+  int left[kPer], taken[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = lane + 64 * j;
+    left[j] = k < K ? seg[k + 1] - seg[k] : 0;
+    taken[j] = 0;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    Elem best{~0ull, ~0ull};
+    int bk = -1;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = lane + 64 * j;
+      if (left[j] > 0) {
+        const Elem e = load_key_elem(sbase[k] + (int64_t)taken[j] * kTeraRecordBytes, k, taken[j], kd.bad_layout);
+        if (bk < 0 || kle(e, best)) {
+          best = e;
+          bk = k;
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t oh = __shfl_xor(best.hi, off, 64), ol = __shfl_xor(best.lo, off, 64);
+      const int ok = __shfl_xor(bk, off, 64);
+      const bool take = ok >= 0 && (bk < 0 || oh < best.hi || (oh == best.hi && ol < best.lo));
+      if (take) {
+        best.hi = oh;
+        best.lo = ol;
+        bk = ok;
+      }
+    }
+    const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(sbase[bk] + pos * kTeraRecordBytes);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
+    if (lane < kWords) dst[lane] = src[lane];
+    if (lane == (bk & 63)) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if ((bk >> 6) == j) {
+          ++taken[j];
+          --left[j];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// F3: the K sorted slices of the cell's n keys at src[0, n) (slice k at [seg[k], seg[k+1])) merged pairwise
+// in place, log2 K levels (merge path per thread over ceil(n / 256) outputs held in registers).
+template <int ITEMS>
+__device__ __forceinline__ void kw_merge_levels(Elem* src, const int* seg, int K, int n) {
+  // outputs per thread: n spread evenly over the workgroup, so a cell filled to 65 % of its capacity
+  // keeps every thread busy with a 65 % long merge chain
+  const int ipt = (n + 256 - 1) / 256;
+  const int o0 = threadIdx.x * ipt;
+  uint64_t held_hi[ITEMS], held_lo[ITEMS];  // this thread's outputs of the current level
+  for (int w = 1; w < K; w <<= 1) {
+    if (o0 < n) {
+      const int npairs = (K + 2 * w - 1) / (2 * w);
+      // pair p covers segments [2pw, 2pw + 2w): find the pair holding output o0
+      int pl = 0, ph = npairs;
+      while (ph - pl > 1) {
+        const int mid = (pl + ph) >> 1;
+        if (seg[min(2 * mid * w, K)] <= o0)
+          pl = mid;
+        else
+          ph = mid;
+      }
+      int p = pl;
+      int a0 = seg[min(2 * p * w, K)], a1 = seg[min((2 * p + 1) * w, K)], b1 = seg[min((2 * p + 2) * w, K)];
+      // merge path at diagonal o0 - a0 within the pair
+      int d = o0 - a0, la = a1 - a0, lb = b1 - a1;
+      int ml = d > lb ? d - lb : 0, mh = d < la ? d : la;
+      while (ml < mh) {
+        const int mid = (ml + mh) >> 1;
+        if (kle(src[a0 + mid], src[a1 + d - 1 - mid]))
+          ml = mid + 1;
+        else
+          mh = mid;
+      }
+      int ia = ml, ib = d - ml;
+      const int todo = min(ipt, n - o0);
+      // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
+      // to the cell so a run's end never reads past the buffer
+      Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
+        const int o = o0 + k;
+        while (o == b1) {  // next pair (empty pairs are skipped)
+          ++p;
+          a0 = b1;
+          a1 = seg[min((2 * p + 1) * w, K)];
+          b1 = seg[min((2 * p + 2) * w, K)];
+          la = a1 - a0;
+          lb = b1 - a1;
+          ia = 0;
+          ib = 0;
+          va = src[min(a0, n - 1)];
+          vb = src[min(a1, n - 1)];
+        }
+        // straight-line step: bitwise conditions, the advancing side's next index selected, one
+        // ds_read_b128 for the whole wave (as two exec-masked reads behind branches: same speed, more
+        // LDS instructions; profiles/r4_kway_one_read_ab.md). Field-wise selects: a select of the two
+        // structs becomes a scratch slot + indexed load.
+        const bool take_a = (ib >= lb) | ((ia < la) & kle(va, vb));
+        held_hi[k] = take_a ? va.hi : vb.hi;
+        held_lo[k] = take_a ? va.lo : vb.lo;
+        ia += take_a ? 1 : 0;
+        ib += take_a ? 0 : 1;
+        const Elem nv = src[min(take_a ? a0 + ia : a1 + ib, n - 1)];
+        va.hi = take_a ? nv.hi : va.hi;
+        va.lo = take_a ? nv.lo : va.lo;
+        vb.hi = take_a ? vb.hi : nv.hi;
+        vb.lo = take_a ? vb.lo : nv.lo;
+      }
+    }
+    __syncthreads();
+    // every thread has read the level: overwrite it with the merged order
+    if (o0 < n) {
+      const int todo = min(ipt, n - o0);
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k)
+        if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ITEMS records per thread: the cell capacity is ITEMS * 256 and the LDS buffer is dynamic, so
@@ -264,59 +406,7 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
   uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
   if (n > kCap) {  // uniform across the block
     if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
-    // wave-level priority queue: lane l owns slices l, l + 64, ... (K <= 256: four per lane, their
-    // remaining counts and taken counts in registers); each step a wave argmin picks the next record
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;
-    constexpr int kWords = kTeraRecordBytes / 8;
-    constexpr int kPer = kKwMaxRuns / 64;
-    int left[kPer], taken[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int k = lane + 64 * j;
-      left[j] = k < K ? seg[k + 1] - seg[k] : 0;
-      taken[j] = 0;
-    }
-    for (int64_t i = 0; i < n; ++i) {
-      Elem best{~0ull, ~0ull};
-      int bk = -1;
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        const int k = lane + 64 * j;
-        if (left[j] > 0) {
-          const Elem e = load_key_elem(sbase[k] + (int64_t)taken[j] * kTeraRecordBytes, k, taken[j], kd.bad_layout);
-          if (bk < 0 || kle(e, best)) {
-            best = e;
-            bk = k;
-          }
-        }
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t oh = __shfl_xor(best.hi, off, 64), ol = __shfl_xor(best.lo, off, 64);
-        const int ok = __shfl_xor(bk, off, 64);
-        const bool take = ok >= 0 && (bk < 0 || oh < best.hi || (oh == best.hi && ol < best.lo));
-        if (take) {
-          best.hi = oh;
-          best.lo = ol;
-          bk = ok;
-        }
-      }
-      const int64_t pos = (int64_t)(best.lo & 0xFFFFFFFFull);
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(sbase[bk] + pos * kTeraRecordBytes);
-      uint64_t* dst = reinterpret_cast<uint64_t*>(obase + i * kTeraRecordBytes);
-      if (lane < kWords) dst[lane] = src[lane];
-      if (lane == (bk & 63)) {
-#pragma unroll
-        for (int j = 0; j < kPer; ++j)
-          if ((bk >> 6) == j) {
-            ++taken[j];
-            --left[j];
-          }
-      }
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-    }
+    kw_overflow_pq(kd, seg, sbase, K, n, obase);
     return;
   }
   // ---- F2: keys of every slice into LDS (all of a thread's key loads in flight at once)
@@ -356,82 +446,7 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
   stamp(2);
   // ---- F3: pairwise merge levels inside LDS
   Elem* src = bufA;
-  // outputs per thread: n spread evenly over the workgroup, so a cell filled to 65 % of its capacity
-  // keeps every thread busy with a 65 % long merge chain
-  const int ipt = (n + kKwThreads - 1) / kKwThreads;
-  const int o0 = threadIdx.x * ipt;
-  uint64_t held_hi[kKwItems], held_lo[kKwItems];  // this thread's outputs of the current level
-  for (int w = 1; w < K; w <<= 1) {
-    if (o0 < n) {
-      const int npairs = (K + 2 * w - 1) / (2 * w);
-      // pair p covers segments [2pw, 2pw + 2w): find the pair holding output o0
-      int pl = 0, ph = npairs;
-      while (ph - pl > 1) {
-        const int mid = (pl + ph) >> 1;
-        if (seg[min(2 * mid * w, K)] <= o0)
-          pl = mid;
-        else
-          ph = mid;
-      }
-      int p = pl;
-      int a0 = seg[min(2 * p * w, K)], a1 = seg[min((2 * p + 1) * w, K)], b1 = seg[min((2 * p + 2) * w, K)];
-      // merge path at diagonal o0 - a0 within the pair
-      int d = o0 - a0, la = a1 - a0, lb = b1 - a1;
-      int ml = d > lb ? d - lb : 0, mh = d < la ? d : la;
-      while (ml < mh) {
-        const int mid = (ml + mh) >> 1;
-        if (kle(src[a0 + mid], src[a1 + d - 1 - mid]))
-          ml = mid + 1;
-        else
-          mh = mid;
-      }
-      int ia = ml, ib = d - ml;
-      const int todo = min(ipt, n - o0);
-      // the two heads stay in registers: one LDS read per output (the side that advanced), clamped
-      // to the cell so a run's end never reads past the buffer
-      Elem va = src[min(a0 + ia, n - 1)], vb = src[min(a1 + ib, n - 1)];
-#pragma unroll
-      for (int k = 0; k < kKwItems; ++k) {
-        if (k >= todo) continue;  // (not break: keeps the loop fully unrolled, held[] in registers)
-        const int o = o0 + k;
-        while (o == b1) {  // next pair (empty pairs are skipped)
-          ++p;
-          a0 = b1;
-          a1 = seg[min((2 * p + 1) * w, K)];
-          b1 = seg[min((2 * p + 2) * w, K)];
-          la = a1 - a0;
-          lb = b1 - a1;
-          ia = 0;
-          ib = 0;
-          va = src[min(a0, n - 1)];
-          vb = src[min(a1, n - 1)];
-        }
-        // straight-line step: bitwise conditions, the advancing side's next index selected, one
-        // ds_read_b128 for the whole wave (as two exec-masked reads behind branches: same speed, more
-        // LDS instructions; profiles/r4_kway_one_read_ab.md). Field-wise selects: a select of the two
-        // structs becomes a scratch slot + indexed load.
-        const bool take_a = (ib >= lb) | ((ia < la) & kle(va, vb));
-        held_hi[k] = take_a ? va.hi : vb.hi;
-        held_lo[k] = take_a ? va.lo : vb.lo;
-        ia += take_a ? 1 : 0;
-        ib += take_a ? 0 : 1;
-        const Elem nv = src[min(take_a ? a0 + ia : a1 + ib, n - 1)];
-        va.hi = take_a ? nv.hi : va.hi;
-        va.lo = take_a ? nv.lo : va.lo;
-        vb.hi = take_a ? vb.hi : nv.hi;
-        vb.lo = take_a ? vb.lo : nv.lo;
-      }
-    }
-    __syncthreads();
-    // every thread has read the level: overwrite it with the merged order
-    if (o0 < n) {
-      const int todo = min(ipt, n - o0);
-#pragma unroll
-      for (int k = 0; k < kKwItems; ++k)
-        if (k < todo) src[o0 + k] = Elem{held_hi[k], held_lo[k]};
-    }
-    __syncthreads();
-  }
+  kw_merge_levels<kKwItems>(src, seg, K, n);
   stamp(3);
   // ---- F4: records in merged order straight to the output
   const int wave = threadIdx.x >> 6;
@@ -443,6 +458,155 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     stamp(4);
+  }
+}
+
+// LDS-staged variant (KwayDesc::staged, UDA_KWAY_STAGED=1): every slice's records are copied into LDS
+// once, as whole 16-byte chunks of the slice's aligned window (global_load_lds_dwordx4: per-lane global
+// address, wave-linear LDS image), F2 reads the keys from there and F4 writes the output from there. In
+// kway_tile_kernel F2 pulls each record's first line for its key and F4 pulls the whole record again
+// after the merge, and in between the XCD's other cells have evicted it from L2: 2.07x the record bytes
+// cross the fabric (profiles/r5_kway_roofline.md). Staged, each byte crosses once, at the price of a
+// cap x 104-byte record image in LDS (cap 1024: 122 KB, one workgroup per CU; cap 512: two).
+// LDS layout: keys[cap] | windows (cap*104 + kmax*32 + 1 KiB) | sbase[kmax] | seg[kmax+1] | wfirst[kmax+1] | roff[kmax]
+template <int ITEMS>
+__global__ void __launch_bounds__(256) kway_staged_kernel(KwayDesc kd, uint8_t* out) {
+  constexpr int kCap = ITEMS * 256;
+  constexpr int kWaves = 4;
+  extern __shared__ __attribute__((aligned(16))) Elem kw_dyn[];
+  Elem* keys = kw_dyn;
+  uint8_t* win = reinterpret_cast<uint8_t*>(kw_dyn + kCap);
+  const size_t win_bytes = (size_t)kCap * kTeraRecordBytes + (size_t)kd.kmax * 32 + 1024;
+  const uint8_t** sbase = reinterpret_cast<const uint8_t**>(win + win_bytes);
+  int* seg = reinterpret_cast<int*>(sbase + kd.kmax);
+  int* wfirst = seg + kd.kmax + 1;  // [K + 1]: first 16-byte chunk of slice k's window
+  int* roff = wfirst + kd.kmax + 1;  // [K]: offset of slice k's first record in its first chunk (0 or 8)
+  __shared__ int64_t s_start;
+  int64_t b = blockIdx.x;
+  {
+    const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+    b = x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+  }
+  int lo = 0, hi = kd.G;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (kd.cell_first[mid] <= b)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const int g = lo;
+  const int c = (int)(b - kd.cell_first[g]);
+  const int ncell = (int)(kd.cell_first[g + 1] - kd.cell_first[g]);
+  const int r0 = kd.group_first[g], K = kd.group_first[g + 1] - r0;
+  kw_slices(kd, c, ncell, r0, K, seg, sbase, &s_start);
+  __syncthreads();
+  const int n = seg[K];
+  uint8_t* obase = out + (kd.group_out[g] + s_start) * kTeraRecordBytes;
+  if (n > kCap) {
+    if (threadIdx.x == 0) atomicAdd(kd.overflow, 1);
+    kw_overflow_pq(kd, seg, sbase, K, n, obase);
+    return;
+  }
+  if (n == 0) return;
+  // ---- windows: slice k's bytes rounded out to 16-byte chunks, the windows back to back (wave 0 scans)
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int carry = 0;
+    if (lane == 0) wfirst[0] = 0;
+    for (int base = 0; base < K; base += 64) {
+      const int k = base + lane;
+      int chunks = 0;
+      if (k < K) {
+        const int len = seg[k + 1] - seg[k];
+        const uintptr_t a = (uintptr_t)sbase[k];
+        roff[k] = (int)(a & 15);
+        if (len > 0) chunks = (int)((((a + (uintptr_t)len * kTeraRecordBytes + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4);
+      }
+      int x = chunks;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (k < K) wfirst[k + 1] = carry + x;
+      carry += __shfl(x, 63, 64);
+    }
+  }
+  __syncthreads();
+  // ---- stage: chunk i of the flattened windows lands at win + 16 i. A window's last chunk may run 8 bytes
+  // past the slice's last record, possibly past its allocation: that lane reads a chunk inside the slice
+  // instead and the chunk's 8 valid bytes are patched below.
+  const int T = wfirst[K];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int base = wave * 64; base < T; base += kWaves * 64) {
+    const int i = base + lane;
+    const int ic = min(i, T - 1);
+    int sl = 0, sh = K;  // wfirst[sl] <= ic < wfirst[sl + 1]
+    while (sh - sl > 1) {
+      const int mid = (sl + sh) >> 1;
+      if (wfirst[mid] <= ic)
+        sl = mid;
+      else
+        sh = mid;
+    }
+    const uintptr_t a0 = (uintptr_t)sbase[sl] & ~(uintptr_t)15;
+    const uintptr_t end = (uintptr_t)sbase[sl] + (uintptr_t)(seg[sl + 1] - seg[sl]) * kTeraRecordBytes;
+    uintptr_t src = a0 + (uintptr_t)(ic - wfirst[sl]) * 16;
+    if (src + 16 > end) src = a0;  // the tail chunk (patched below), or a lane past T
+    // C casts: the address-space conversions have no named-cast form
+    __builtin_amdgcn_global_load_lds((const GlobalVoid*)src, (LdsVoid*)(win + (size_t)base * 16), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const int len = seg[k + 1] - seg[k];
+    const uintptr_t end = (uintptr_t)sbase[k] + (uintptr_t)len * kTeraRecordBytes;
+    if (len > 0 && (end & 15))
+      *reinterpret_cast<uint64_t*>(win + (size_t)(wfirst[k + 1] - 1) * 16) = *reinterpret_cast<const GlobalU64*>(end - 8);
+  }
+  __syncthreads();
+  auto rec = [&](int sl, int pos) {
+    return win + (size_t)wfirst[sl] * 16 + roff[sl] + (size_t)pos * kTeraRecordBytes;
+  };
+  // ---- F2 from LDS
+  {
+    int bad = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      int sl = 0, sh = K;
+      while (sh - sl > 1) {
+        const int mid = (sl + sh) >> 1;
+        if (seg[mid] <= i)
+          sl = mid;
+        else
+          sh = mid;
+      }
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(rec(sl, i - seg[sl]));
+      keys[i] = key_elem(w[0], w[1], sl, i - seg[sl], bad);
+    }
+    if (bad) *kd.bad_layout = 1;
+  }
+  __syncthreads();
+  // ---- F3
+  kw_merge_levels<ITEMS>(keys, seg, K, n);
+  // ---- F4 from LDS: one wave per 64 output records, 13 consecutive 8-byte words per record
+  constexpr int kWords = kTeraRecordBytes / 8;
+  for (int base = wave * 64; base < n; base += kWaves * 64) {
+    const int valid = min(64, n - base);
+    uint32_t my = 0;  // LDS offset of this lane's record
+    if (lane < valid) {
+      const Elem e = keys[base + lane];
+      my = (uint32_t)(rec((int)((e.lo >> 32) & 0xFFFF), (int)(e.lo & 0xFFFFFFFFull)) - win);
+    }
+    uint64_t* d = reinterpret_cast<uint64_t*>(obase + (int64_t)base * kTeraRecordBytes);
+    const int words = valid * kWords;
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) {
+      const int w = j * 64 + lane;
+      const int r = w / kWords;
+      const uint32_t o = __shfl(my, r < 64 ? r : 63, 64);
+      if (w < words) d[w] = *reinterpret_cast<const uint64_t*>(win + o + (uint32_t)(w - r * kWords) * 8);
+    }
   }
 }
 
@@ -487,8 +651,39 @@ void launch_kway(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s
 }
 }  // namespace
 
+template <int ITEMS>
+void launch_kway_staged(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
+  auto lds_for = [](int k) {
+    const size_t cap = (size_t)ITEMS * 256;
+    return cap * sizeof(Elem) + cap * kTeraRecordBytes + (size_t)k * 32 + 1024 + (size_t)k * sizeof(void*) +
+           (size_t)(3 * k + 2) * sizeof(int) + 16;
+  };
+  if (kd.kmax < 1 || kd.kmax > kKwMaxRuns) throw std::runtime_error("kway: bad runs per group " + std::to_string(kd.kmax));
+  const size_t lds = lds_for(kd.kmax);
+  if (lds > (160u << 10)) throw std::runtime_error("kway staged: cell of " + std::to_string(ITEMS * 256) + " records with " +
+                                                   std::to_string(kd.kmax) + " runs needs " + std::to_string(lds) +
+                                                   " bytes of LDS");
+  static std::once_flag once;
+  static hipError_t attr = hipSuccess;
+  std::call_once(once, [lds_for] {
+    attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kway_staged_kernel<ITEMS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_for(kKwMaxRuns));
+    if (attr != hipSuccess) (void)hipGetLastError();
+  });
+  if (attr != hipSuccess && lds > (64u << 10))
+    throw std::runtime_error(std::string("kway staged: cannot raise the LDS limit: ") + hipGetErrorString(attr));
+  hipLaunchKernelGGL((kway_staged_kernel<ITEMS>), dim3((unsigned)ncells), dim3(256), lds, s, kd, out);
+}
+
 void launch_kway_tiles(const KwayDesc& kd, int64_t ncells, uint8_t* out, hipStream_t s) {
   if (ncells <= 0) return;
+  if (kd.staged) {
+    switch (kd.cap) {
+      case 1024: launch_kway_staged<4>(kd, ncells, out, s); return;
+      case 512: launch_kway_staged<2>(kd, ncells, out, s); return;
+      default: throw std::runtime_error("kway staged: cell capacity must be 512 or 1024 (UDA_KWAY_CAP)");
+    }
+  }
   switch (kd.cap) {
     case 2048: launch_kway<8>(kd, ncells, out, s); break;
     case 1792: launch_kway<7>(kd, ncells, out, s); break;  // 28.4 KiB, 5 workgroups per CU

@@ -214,7 +214,9 @@ def test_spill_tiers_multirank_staged(require_gpu, tmp_path, monkeypatch, world,
 
 
 @pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}, {"UDA_KWAY_CAP": "1536"},
-                                 {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"}, {"UDA_KWAY_CAP": "1024"}])
+                                 {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"}, {"UDA_KWAY_CAP": "1024"},
+                                 {"UDA_KWAY_STAGED": "1"}, {"UDA_KWAY_STAGED": "1", "UDA_KWAY_CAP": "512"},
+                                 {"UDA_KWAY_STAGED": "1", "UDA_KWAY_TARGET": "5000"}])
 def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
     """The single-pass K-way merge (default) and the pairwise merge-path tree (UDA_KWAY=0) order
     records identically; UDA_KWAY_TARGET above the LDS capacity routes every cell through the
@@ -237,7 +239,7 @@ def test_kway_merge_matches_pairwise_tree(require_gpu, monkeypatch, env):
         assert st2["merge_passes"] == 3  # ceil(log2(6)) pairwise passes
 
 
-@pytest.mark.parametrize("env", [{}, {"UDA_KWAY_TARGET": "100000"}, {"UDA_KWAY_CAP": "1792"}])
+@pytest.mark.parametrize("env", [{}, {"UDA_KWAY_TARGET": "100000"}, {"UDA_KWAY_CAP": "1792"}, {"UDA_KWAY_STAGED": "1"}])
 def test_kway_many_runs_per_group(require_gpu, monkeypatch, env):
     """200 runs per group (an 8-GPU round has 8 x 32 = 256): the single-pass merge sizes its per-slice
     LDS tables by the plan's largest group and must order records like the pairwise tree, on the LDS
@@ -245,7 +247,7 @@ def test_kway_many_runs_per_group(require_gpu, monkeypatch, env):
     ref_env = {"UDA_KWAY": "0"}
     out = []
     for e in (ref_env, env):
-        for k in ("UDA_KWAY", "UDA_KWAY_TARGET", "UDA_KWAY_CAP"):
+        for k in ("UDA_KWAY", "UDA_KWAY_TARGET", "UDA_KWAY_CAP", "UDA_KWAY_STAGED"):
             monkeypatch.delenv(k, raising=False)
         for k, v in e.items():
             monkeypatch.setenv(k, v)

@@ -92,6 +92,10 @@ RECIPES: dict[str, tuple[int, str]] = {
     "apihost2_s5": (600, f"{PY} bench.py --api --api-host-mofs --gpus 2 --one-gpu --rows-per-gpu 200000000 --steps 5 --warmup 1"),
     "coldfiles6_nopin": (500, f"UDA_J2C_PIN=none {PY} tools/cold_task_bench.py --files --repeat 6"),
     "coldnode5_nopin": (500, f"UDA_J2C_PIN=none {PY} tools/cold_task_bench.py --node --repeat 5"),
+    "kwtests": (300, f"{PY} -m pytest tests/test_gpu_terasort.py -m gpu -x -v --timeout 170 --timeout-method thread -k kway"),
+    "do_staged": (300, f"UDA_KWAY_STAGED=1 {PY} bench.py --device-only --steps 3 --warmup 1"),
+    "do_staged512": (300, f"UDA_KWAY_STAGED=1 UDA_KWAY_CAP=512 {PY} bench.py --device-only --steps 3 --warmup 1"),
+    "do_cap1024": (300, f"UDA_KWAY_CAP=1024 {PY} bench.py --device-only --steps 3 --warmup 1"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
@@ -123,6 +127,8 @@ ROOF_PASSES = {"a": "FETCH_SIZE TCC_HIT_sum", "b": "WRITE_SIZE TCC_MISS_sum",
 # raw L2 -> fabric read requests by size (FETCH_SIZE's derivation is checked against a copy of known bytes)
 ROOF_PASSES["d"] = "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum"
 for k, counters in ROOF_PASSES.items():
+    RECIPES[f"roof_kws_{k}"] = (90, f"UDA_KWAY_STAGED=1 rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_kws_{k} "
+                                    f"-o run -- {PMC_PROG}")
     RECIPES[f"roof_kw_{k}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_kw_{k} -o run -- "
                                    f"{PMC_PROG}")
     RECIPES[f"roof_copy_{k}"] = (90, f"rocprofv3 --pmc {counters} --output-format csv -d gpurun_out/roof_copy_{k} -o run -- "
