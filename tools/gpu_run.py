@@ -107,6 +107,8 @@ RECIPES: dict[str, tuple[int, str]] = {
     "netmerger": (400, f"{PY} benchmarks/run_configs.py netmerger --gb 2 --maps 64 --reducers 1"),
     "prof_bench": (500, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- "
                         "python3 bench.py --steps 3 --warmup 1"),
+    "prof_lzo41": (500, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lzo41 -o run -- "
+                        "python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }
