@@ -109,6 +109,9 @@ RECIPES: dict[str, tuple[int, str]] = {
                         "python3 bench.py --steps 3 --warmup 1"),
     "prof_lzo41": (500, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lzo41 -o run -- "
                         "python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "pmc_lzo41": (300, "timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY "
+                       "SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d gpurun_out/pmc_lzo41 -o run -- "
+                       "python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 --steps 1 --warmup 0"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }
