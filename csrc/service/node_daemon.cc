@@ -663,18 +663,19 @@ int run_node_daemon(int ctl_fd) {
       };
       d->svc = std::make_unique<MergeService>(mo);
     }
+    // what the first wave of hosted tasks would each build on its critical path (code objects, pooled
+    // workspaces, shareable pinned delivery rings), built once after READY, long before the first task
+    const int warm_tasks = d->svc && !devs.empty()
+                               ? (int)std::atoi(d->conf("mapred.uda.daemon.prewarm.tasks", "16").c_str())
+                               : 0;
+    if (warm_tasks <= 0) d->prewarm_done = 1;  // nothing to build: the node is as warm as it gets
+    const int64_t rb = std::atoll(d->conf("mapred.uda.gpu.round.bytes", std::to_string(2ll << 30)).c_str());
+    const int64_t kvb = std::atoll(d->conf("mapred.uda.kv.buf.size", std::to_string(1 << 20)).c_str());
     std::string ready;
     put_str(ready, svc_path);
     put<int64_t>(ready, store_bytes);
     d->send(kDReady, ready);
-    // what the first wave of hosted tasks would each build on its critical path (code objects, pooled
-    // workspaces, shareable pinned delivery rings), built once now, long before the first task comes
-    const int warm_tasks = d->svc && !devs.empty()
-                               ? (int)std::atoi(d->conf("mapred.uda.daemon.prewarm.tasks", "16").c_str())
-                               : 0;
     if (warm_tasks > 0) {
-      const int64_t rb = std::atoll(d->conf("mapred.uda.gpu.round.bytes", std::to_string(2ll << 30)).c_str());
-      const int64_t kvb = std::atoll(d->conf("mapred.uda.kv.buf.size", std::to_string(1 << 20)).c_str());
       const int per = (warm_tasks + (int)devs.size() - 1) / (int)devs.size();
       d->prewarm_tasks = per * (int)devs.size();
       Daemon* dp = d.get();

@@ -135,6 +135,9 @@ def _daemon_front(tmp_path, job, conf=None, **kw):
     fe = FrontEnd(mof_dir, port, c)
     d = fe.info["provider"]["hbm_store"]["daemon"]
     assert d["ready"] is True and d["pid"] > 0 and d["service"] == f"@uda-merge-{port}", fe.info
+    # no GPU to prewarm for: the daemon reports its first-wave prewarm as done (what a bench waits for)
+    pw = fe.stats()["hbm_store"].get("prewarm")
+    assert pw is not None and pw["done"] is True, pw
     return fe, data, ids, port
 
 
