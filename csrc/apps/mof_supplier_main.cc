@@ -21,6 +21,9 @@
 // After setup the serving modes print one JSON line (the port, ...; the bench mode also every reduce
 // task's expected record count and commands), then serve until stdin says "exit" (or closes); "stats"
 // prints the provider's stats as one JSON line.
+#include <dirent.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -145,9 +148,28 @@ std::string task_json(const uda::gpu::ApiTeraSortBench& b, int reducers) {
 }
 }  // namespace
 
+// The node daemon inherits every descriptor its front end's process did not mark close-on-exec (a
+// NodeManager JVM's listening sockets, its log files): closed before anything else runs, so the daemon
+// never holds the NodeManager's ports or files open past the NodeManager.
+static void close_inherited(int keep) {
+  std::vector<int> fds;
+  if (DIR* d = ::opendir("/proc/self/fd")) {
+    while (const dirent* e = ::readdir(d)) {
+      const int fd = std::atoi(e->d_name);
+      if (e->d_name[0] != '.' && fd > 2 && fd != keep) fds.push_back(fd);
+    }
+    ::closedir(d);  // its own descriptor is in the list: closing it again below is a harmless EBADF
+  }
+  for (int fd : fds) ::close(fd);
+}
+
 int main(int argc, char** argv) {
   // the node daemon a provider front end starts (node_daemon.h): its control socket is descriptor N
-  if (argc == 3 && std::string(argv[1]) == "--daemon-fd") return uda::run_node_daemon(std::atoi(argv[2]));
+  if (argc == 3 && std::string(argv[1]) == "--daemon-fd") {
+    const int ctl = std::atoi(argv[2]);
+    close_inherited(ctl);
+    return uda::run_node_daemon(ctl);
+  }
   uda::gpu::ApiBenchConfig c;
   c.transport = "tcp";
   c.bind_addr = "127.0.0.1";

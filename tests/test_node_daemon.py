@@ -43,11 +43,12 @@ def _port():
 class FrontEnd:
     """uda_mof_supplier mode=frontend: uda_start(provider) with getPathUda over Hadoop-layout MOFs."""
 
-    def __init__(self, mof_dir, port, conf=None):
+    def __init__(self, mof_dir, port, conf=None, pass_fds=()):
         argv = [SUP, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"]
         for k, v in (conf or {}).items():
             argv.append(f"-D{k}={v}")
-        self.p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT)
+        self.p = subprocess.Popen(argv, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT,
+                                  pass_fds=pass_fds)
         line = self.p.stdout.readline()
         assert line, f"front end exited rc={self.p.poll()}"
         self.info = json.loads(line)
@@ -125,6 +126,36 @@ def test_default_configuration_fetches_across_processes(native, tmp_path):
         assert st["port"] == port and st["requests"] >= 12, st
     finally:
         fe.close()
+
+
+def test_daemon_does_not_inherit_front_end_descriptors(tmp_path):
+    """A NodeManager JVM holds descriptors without close-on-exec (listening sockets, logs); the daemon it
+    starts closes every inherited descriptor but its control socket, so it never keeps the NodeManager's
+    port or files open."""
+    mof_dir, _, _ = _job(tmp_path, "job_fds")
+    marker = tmp_path / "nodemanager-held.log"
+    fd = os.open(str(marker), os.O_WRONLY | os.O_CREAT, 0o644)  # inheritable (no O_CLOEXEC in the child)
+    fe = None
+    try:
+        fe = FrontEnd(mof_dir, _port(), {"mapred.uda.daemon": "1"}, pass_fds=(fd,))
+        dpid = fe.info["provider"]["hbm_store"]["daemon"]["pid"]
+        fepid = fe.p.pid
+
+        def targets(pid):
+            out = set()
+            for e in os.listdir(f"/proc/{pid}/fd"):
+                try:
+                    out.add(os.readlink(f"/proc/{pid}/fd/{e}"))
+                except OSError:
+                    pass
+            return out
+
+        assert str(marker) in targets(fepid)  # the front end (the "JVM") holds it
+        assert str(marker) not in targets(dpid), targets(dpid)
+    finally:
+        os.close(fd)
+        if fe is not None:
+            fe.close()
 
 
 def _daemon_front(tmp_path, job, conf=None, **kw):
