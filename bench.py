@@ -510,6 +510,16 @@ def _node_result(args, stats, warm, validated, provider) -> dict:
     }
 
 
+def _check_space(path: str, need: int) -> None:
+    """The map outputs must fit the file system they are written to (a GPU box's /tmp is ~79 GB)."""
+    os.makedirs(path, exist_ok=True)
+    st = os.statvfs(path)
+    free = st.f_bavail * st.f_frsize
+    if free < need * 1.02:
+        raise SystemExit(f"bench: {need / 1e9:.1f} GB of MOF files do not fit {path} ({free / 1e9:.1f} GB free); "
+                         "lower --rows-per-gpu or point --mof-dir elsewhere")
+
+
 def run_node_files(args, ctx) -> int:
     """The deployment as documented, end to end, on one GPU node: Hadoop-written map output files, the
     provider front end (the NodeManager's aux service: uda_mof_supplier mode=frontend, getPathUda over
@@ -534,6 +544,7 @@ def run_node_files(args, ctx) -> int:
     R = args.reducers
     logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
     errlog = open(os.path.join(logdir, "node_tasks.err"), "a")
+    _check_space(args.mof_dir, args.rows_per_gpu * RECORD_BYTES)
     mof_dir = os.path.join(args.mof_dir, f"uda-node-{os.getpid()}")
     os.makedirs(mof_dir, exist_ok=True)
     frontend = None
@@ -623,6 +634,7 @@ def run_api(args, ctx) -> int:
     hbm_bytes = 0
     if args.mof_dir:
         os.makedirs(args.mof_dir, exist_ok=True)
+        _check_space(args.mof_dir, args.rows_per_gpu * RECORD_BYTES * (ctx.world if args.one_gpu else 1))
         per_rank = args.rows_per_gpu * RECORD_BYTES
         hbm_bytes = int(per_rank * 1.25) if args.provider_hbm_gb < 0 else int(args.provider_hbm_gb * 1e9)
     b = native().ApiTeraSortBench(dict(device=device, maps=args.maps_per_gpu, reducers=R,
