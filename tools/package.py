@@ -10,6 +10,8 @@ Layout of the tarball (installs under /usr/lib64/uda-amd like the reference's /u
     lib/uda-amd-hadoop-*.jar           Hadoop plugin jars, when java/build.sh produced them
     java/                              plugin sources (build them against the cluster's Hadoop)
     python/uda_amd/                    Python package incl. the pybind11 module
+    bin/uda_mof_supplier               the node daemon libuda.so starts (found at <libuda dir>/../bin)
+    bin/uda_reduce_task                a reduce task in a process of its own (node-shape runs, tests)
     bin/uda-regression, bin/uda-bench  entry points
     share/doc/                         README, ARCHITECTURE, BENCHMARKS
     VERSION                            version string reported by libuda.so ("The version is ...")
@@ -41,6 +43,8 @@ def stage(dest: str) -> None:
     shutil.copytree(os.path.join(ROOT, "uda_amd"), os.path.join(dest, "python", "uda_amd"),
                     ignore=shutil.ignore_patterns("__pycache__", "*.pyc"))
     os.makedirs(os.path.join(dest, "bin"))
+    for exe in ("uda_mof_supplier", "uda_reduce_task"):  # next to lib/: NodeDaemonClient::default_exe
+        shutil.copy2(os.path.join(ROOT, "uda_amd", "bin", exe), os.path.join(dest, "bin", exe))
     for name, target in (("uda-regression", "tools/regression.py"), ("uda-bench", "bench.py")):
         src = os.path.join(ROOT, target)
         shutil.copy2(src, os.path.join(dest, "bin", os.path.basename(target)))
