@@ -544,7 +544,7 @@ def run_node_files(args, ctx) -> int:
     R = args.reducers
     logdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
     errlog = open(os.path.join(logdir, "node_tasks.err"), "a")
-    _check_space(args.mof_dir, args.rows_per_gpu * RECORD_BYTES)
+    _check_space(args.mof_dir, args.rows_per_gpu * 104)  # TeraSort IFile records
     mof_dir = os.path.join(args.mof_dir, f"uda-node-{os.getpid()}")
     os.makedirs(mof_dir, exist_ok=True)
     frontend = None
