@@ -399,6 +399,7 @@ def aio(args) -> dict:
     for be in ("", "threadpool"):
         r = native().aio_bench(path, size, 1 << 20, 16, True, be)
         out[(r["backend"]) + "_mbps"] = round(r["aio_mbps"], 1)
+        out[(r["backend"]) + "_streaming_mbps"] = round(r["aio_streaming_mbps"], 1)
         out["sequential_mbps"] = round(r["sequential_mbps"], 1)
         assert r["ok"]
     return out
