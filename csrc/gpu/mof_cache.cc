@@ -71,6 +71,9 @@ struct MofCache::Loader {
 };
 
 MofCache::MofCache(const Options& o) : opt_(o) {
+  // tuning A/Bs of the load path (tools/gpu_run.py): chunk size and chunks in flight per loader
+  if (const char* e = std::getenv("UDA_STORE_CHUNK_MB")) opt_.chunk_bytes = std::atoll(e) << 20;
+  if (const char* e = std::getenv("UDA_STORE_CHUNKS")) opt_.chunks = std::atoi(e);
   opt_.chunk_bytes = align_io(std::max<int64_t>(opt_.chunk_bytes, 1 << 20));
   opt_.chunks = std::max(2, opt_.chunks);
   if (!enabled()) return;
@@ -412,6 +415,7 @@ void MofCache::loader_main(Loader* L) {
     HIP_CHECK(hipSetDevice(L->device));
     AsyncIO::Options ao;
     ao.threads = 2;
+    if (const char* e = std::getenv("UDA_STORE_AIO_THREADS")) ao.threads = std::max(1, std::atoi(e));
     ao.queue_depth = 2 * C_slots;
     L->aio = AsyncIO::create(ao);
     L->ring = static_cast<uint8_t*>(pinned_host_alloc((size_t)(C * C_slots), node));

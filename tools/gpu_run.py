@@ -96,6 +96,9 @@ RECIPES: dict[str, tuple[int, str]] = {
     "do_staged": (300, f"UDA_KWAY_STAGED=1 {PY} bench.py --device-only --steps 3 --warmup 1"),
     "do_staged512": (300, f"UDA_KWAY_STAGED=1 UDA_KWAY_CAP=512 {PY} bench.py --device-only --steps 3 --warmup 1"),
     "do_cap1024": (300, f"UDA_KWAY_CAP=1024 {PY} bench.py --device-only --steps 3 --warmup 1"),
+    "nodefiles41_c32": (900, f"UDA_STORE_CHUNKS=32 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles41_4mb": (900, f"UDA_STORE_CHUNKS=64 UDA_STORE_CHUNK_MB=4 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles41_t4": (900, f"UDA_STORE_AIO_THREADS=4 UDA_STORE_CHUNKS=32 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
     "host198": (900, f"{PY} bench.py --store host --rows-per-gpu 1900000000 --steps 2 --warmup 1"),
