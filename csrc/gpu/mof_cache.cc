@@ -420,7 +420,8 @@ void MofCache::loader_main(Loader* L) {
     L->aio = AsyncIO::create(ao);
     L->ring = static_cast<uint8_t*>(pinned_host_alloc((size_t)(C * C_slots), node));
     try {
-      L->sdma = &SdmaEngine::for_device(L->device);
+      const char* h2d = std::getenv("UDA_STORE_H2D");  // A/B: "blit" copies chunks with hipMemcpyAsync
+      L->sdma = h2d && std::string(h2d) == "blit" ? nullptr : &SdmaEngine::for_device(L->device);
     } catch (const std::exception& ex) {
       UDA_LOG(kWarn, "provider HBM store: no SDMA engine on device %d (%s); hipMemcpyAsync", L->device, ex.what());
       L->sdma = nullptr;
