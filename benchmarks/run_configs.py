@@ -402,6 +402,8 @@ def aio(args) -> dict:
         out[(r["backend"]) + "_streaming_mbps"] = round(r["aio_streaming_mbps"], 1)
         out["sequential_mbps"] = round(r["sequential_mbps"], 1)
         assert r["ok"]
+    # the store loader's pattern: 32 files read round-robin in 16 MiB chunks, 16 in flight
+    out["interleaved_32x16MiB_gbps"] = round(native().aio_interleave_bench(args.dir, 32, size // 32, 16 << 20, 16), 2)
     return out
 
 

@@ -511,6 +511,70 @@ PYBIND11_MODULE(_uda_native, m) {
   }, py::arg("path"), py::arg("size"), py::arg("block") = 1 << 20, py::arg("depth") = 16, py::arg("direct") = true,
      py::arg("backend") = "");
 
+  // The provider store's read pattern without the store: `files` files of `file_bytes` written and synced,
+  // then read round-robin in `chunk` pieces with `depth` reads kept in flight (O_DIRECT), as a loader
+  // streams a job's MOF files. Returns GB/s; the files are removed.
+  m.def("aio_interleave_bench", [](const std::string& dir, int files, int64_t file_bytes, int64_t chunk, int depth) {
+    py::gil_scoped_release rel;
+    file_bytes = file_bytes / chunk * chunk;
+    std::vector<std::string> paths;
+    std::vector<int> fds;
+    {
+      std::vector<uint8_t> buf((size_t)(8 << 20));
+      for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 2654435761u >> 13);
+      for (int f = 0; f < files; ++f) {
+        paths.push_back(dir + "/uda_interleave." + std::to_string(getpid()) + "." + std::to_string(f));
+        const int fd = ::open(paths.back().c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+        if (fd < 0) throw std::runtime_error("open for write failed");
+        for (int64_t off = 0; off < file_bytes; off += (int64_t)buf.size())
+          if (::pwrite(fd, buf.data(), (size_t)std::min<int64_t>((int64_t)buf.size(), file_bytes - off), off) <= 0)
+            throw std::runtime_error("pwrite failed");
+        ::fdatasync(fd);
+        ::close(fd);
+      }
+    }
+    for (const auto& p : paths) {
+      int fd = ::open(p.c_str(), O_RDONLY | O_CLOEXEC | O_DIRECT);
+      if (fd < 0) fd = ::open(p.c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) throw std::runtime_error("open for read failed");
+      fds.push_back(fd);
+    }
+    AsyncIO::Options o;
+    o.queue_depth = std::max(depth, 1) * 2;
+    auto io = AsyncIO::create(o);
+    std::vector<void*> bufs;
+    for (int i = 0; i < depth; ++i) bufs.push_back(aligned_alloc_io((size_t)chunk));
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<int> free_bufs;
+    for (int i = 0; i < depth; ++i) free_bufs.push_back(i);
+    std::atomic<int64_t> bad{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int64_t off = 0; off < file_bytes; off += chunk)
+      for (int f = 0; f < files; ++f) {
+        int bi;
+        {
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [&] { return !free_bufs.empty(); });
+          bi = free_bufs.back();
+          free_bufs.pop_back();
+        }
+        io->read(fds[(size_t)f], off, chunk, bufs[(size_t)bi], [&, bi](int64_t r) {
+          if (r < 0) bad++;
+          std::lock_guard<std::mutex> g(m);
+          free_bufs.push_back(bi);
+          cv.notify_all();
+        });
+      }
+    io->drain();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int fd : fds) ::close(fd);
+    for (void* b : bufs) aligned_free_io(b);
+    for (const auto& p : paths) ::unlink(p.c_str());
+    if (bad.load()) throw std::runtime_error("interleaved read failed");
+    return (double)file_bytes * files / secs / 1e9;
+  }, py::arg("dir"), py::arg("files"), py::arg("file_bytes"), py::arg("chunk") = 16 << 20, py::arg("depth") = 16);
+
   // ---------------------------------------------------------------- bridge (C ABI)
   py::class_<PyBridge, std::shared_ptr<PyBridge>>(m, "Bridge")
       .def(py::init([](bool is_net_merger, const std::vector<std::string>& args, int log_level, py::object fetch_over,
