@@ -403,7 +403,11 @@ def aio(args) -> dict:
         out["sequential_mbps"] = round(r["sequential_mbps"], 1)
         assert r["ok"]
     # the store loader's pattern: 32 files read round-robin in 16 MiB chunks, 16 in flight
-    out["interleaved_32x16MiB_gbps"] = round(native().aio_interleave_bench(args.dir, 32, size // 32, 16 << 20, 16), 2)
+    ib = native().aio_interleave_bench
+    out["interleaved_32x16MiB_gbps"] = round(ib(args.dir, 32, size // 32, 16 << 20, 16), 2)
+    out["interleaved_32x64MiB_gbps"] = round(ib(args.dir, 32, size // 32, 64 << 20, 8), 2)
+    out["interleaved_8x16MiB_gbps"] = round(ib(args.dir, 8, size // 8, 16 << 20, 16), 2)
+    out["interleaved_1x16MiB_gbps"] = round(ib(args.dir, 1, size, 16 << 20, 16), 2)
     return out
 
 
