@@ -405,9 +405,10 @@ def aio(args) -> dict:
     # the store loader's pattern: 32 files read round-robin in 16 MiB chunks, 16 in flight
     ib = native().aio_interleave_bench
     out["interleaved_32x16MiB_gbps"] = round(ib(args.dir, 32, size // 32, 16 << 20, 16), 2)
-    out["interleaved_32x64MiB_gbps"] = round(ib(args.dir, 32, size // 32, 64 << 20, 8), 2)
-    out["interleaved_8x16MiB_gbps"] = round(ib(args.dir, 8, size // 8, 16 << 20, 16), 2)
-    out["interleaved_1x16MiB_gbps"] = round(ib(args.dir, 1, size, 16 << 20, 16), 2)
+    out["interleaved_32x1MiB_d64_gbps"] = round(ib(args.dir, 32, size // 32, 1 << 20, 64), 2)
+    out["interleaved_32x2MiB_d64_gbps"] = round(ib(args.dir, 32, size // 32, 2 << 20, 64), 2)
+    out["interleaved_32x4MiB_d32_gbps"] = round(ib(args.dir, 32, size // 32, 4 << 20, 32), 2)
+    out["interleaved_32x1MiB_d256_gbps"] = round(ib(args.dir, 32, size // 32, 1 << 20, 256), 2)
     return out
 
 

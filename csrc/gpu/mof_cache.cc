@@ -50,6 +50,7 @@ struct MofCache::Loader {
     bool read_done = false;
     hsa_signal_t sig{};
     hipEvent_t ev = nullptr;
+    int parts = 0;  // disk reads of this chunk still in flight
   };
   int device = 0;
   std::thread thr;
@@ -76,6 +77,9 @@ MofCache::MofCache(const Options& o) : opt_(o) {
   if (const char* e = std::getenv("UDA_STORE_CHUNKS")) opt_.chunks = std::atoi(e);
   opt_.chunk_bytes = align_io(std::max<int64_t>(opt_.chunk_bytes, 1 << 20));
   opt_.chunks = std::max(2, opt_.chunks);
+  if (const char* e = std::getenv("UDA_STORE_READ_MB")) opt_.read_bytes = std::atoll(e) << 20;
+  opt_.read_bytes = opt_.read_bytes <= 0 ? opt_.chunk_bytes
+                                         : align_io(std::min(opt_.read_bytes, opt_.chunk_bytes));
   if (!enabled()) return;
   per_device_ = opt_.capacity / (int64_t)opt_.devices.size();
   for (int d : opt_.devices) used_[d] = 0;
@@ -416,7 +420,7 @@ void MofCache::loader_main(Loader* L) {
     AsyncIO::Options ao;
     ao.threads = 2;
     if (const char* e = std::getenv("UDA_STORE_AIO_THREADS")) ao.threads = std::max(1, std::atoi(e));
-    ao.queue_depth = 2 * C_slots;
+    ao.queue_depth = 2 * C_slots * (int)((C + opt_.read_bytes - 1) / opt_.read_bytes);
     L->aio = AsyncIO::create(ao);
     L->ring = static_cast<uint8_t*>(pinned_host_alloc((size_t)(C * C_slots), node));
     try {
@@ -586,14 +590,28 @@ void MofCache::loader_main(Loader* L) {
     }
     if (!subs.empty() || !fire.empty()) {
       lk.unlock();
+      // a chunk goes to disk as reads of opt_.read_bytes (the device sustains more small O_DIRECT reads in
+      // flight than large ones); the chunk is landed when the last of them completes
+      const int64_t R = opt_.read_bytes;
       for (const Submit& sb : subs) {
         Loader::Slot* sp = &L->slots[(size_t)sb.slot];
-        L->aio->read(sb.fd, sb.off, sb.len, L->ring + (int64_t)sb.slot * C, [this, L, sp](int64_t r) {
+        {
           std::lock_guard<std::mutex> g(mu_);
-          sp->result = r;
-          sp->read_done = true;
-          L->cv.notify_all();
-        });
+          sp->parts = (int)((sb.len + R - 1) / R);
+        }
+        for (int64_t p = 0; p < sb.len; p += R)
+          L->aio->read(sb.fd, sb.off + p, std::min(R, sb.len - p), L->ring + (int64_t)sb.slot * C + p,
+                       [this, L, sp](int64_t r) {
+                         std::lock_guard<std::mutex> g(mu_);
+                         if (r < 0 || sp->result < 0)
+                           sp->result = -1;
+                         else
+                           sp->result += r;
+                         if (--sp->parts == 0) {
+                           sp->read_done = true;
+                           L->cv.notify_all();
+                         }
+                       });
       }
       for (Fire& f : fire) f.ready(f.ok, f.ref, f.why);
       fire.clear();

@@ -55,6 +55,7 @@ class MofCache {
     std::vector<int> devices{0};    // GPUs the MOFs are striped over (mapred.uda.provider.hbm.devices)
     int64_t chunk_bytes = 16 << 20;  // disk read granule
     int chunks = 16;                 // reads + copies in flight per loader
+    int64_t read_bytes = 0;          // disk request size a chunk is read in (0: one read per chunk)
     bool odirect = true;
     double lease_s = 600;            // a holder on another node idle this long is presumed dead
   };
