@@ -453,6 +453,7 @@ def _run_waves(args, port, cmds, expected, exe, errlog, conf, sp, statistics):
             timeline.append([round(x - t_base) for x in (o["t_exec_boot_ms"], ff, ff + o["fetch_to_first_data_ms"],
                                                          eof, o["t_end_boot_ms"])])
         return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "timeline": timeline,
+                "t_base_boot_ms": t_base,
                 "bytes": sum(o["bytes"] for o in out.values()), "records": sum(o["records"] for o in out.values()),
                 "order_errors": sum(o["order_errors"] for o in out.values()),
                 "task_ms_median": {k: med(k) for k in ("exec_to_main_ms", "start_ms", "init_ms",
@@ -596,6 +597,10 @@ def run_node_files(args, ctx) -> int:
         waves = warm + stats
         out["first_wave"] = {"timeline_ms": waves[0]["timeline"], "task_ms_median": waves[0]["task_ms_median"],
                              "task0": waves[0]["task0"]}
+        hs = provider.get("hbm_store", {})
+        if hs.get("first_miss_boot_ms"):  # the store's loads on the first wave's timeline (same clock)
+            out["first_wave"]["store_ms"] = {k: round(hs[k + "_boot_ms"] - waves[0]["t_base_boot_ms"])
+                                             for k in ("first_miss", "first_read", "last_landed")}
         out["first_step_ms"] = round(waves[0]["wall_ms"], 1)
         out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
         out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)

@@ -50,7 +50,9 @@ class LocalDeviceStore : public DeviceStore {
            ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
            ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
            std::to_string(st.resident_bytes) + ",\"capacity\":" + std::to_string(cache_->capacity()) +
-           ",\"load_ms\":" + std::to_string(st.load_ms) + "}";
+           ",\"load_ms\":" + std::to_string(st.load_ms) + ",\"first_miss_boot_ms\":" +
+           std::to_string(st.first_miss_boot_ms) + ",\"first_read_boot_ms\":" + std::to_string(st.first_read_boot_ms) +
+           ",\"last_landed_boot_ms\":" + std::to_string(st.last_landed_boot_ms) + "}";
   }
 
  private:

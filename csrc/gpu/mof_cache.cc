@@ -41,6 +41,12 @@ bool holder_alive(const std::string& h, double last, double now, double lease_s)
 }
 }  // namespace
 
+static double boot_ms() {
+  timespec ts{};
+  clock_gettime(CLOCK_BOOTTIME, &ts);
+  return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec / 1e6;
+}
+
 struct MofCache::Loader {
   enum State { kFree = 0, kReading = 1, kCopying = 2 };
   struct Slot {
@@ -261,6 +267,7 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
   e->device = device;
   e->len = len;
   e->last_served = e->t_start = now;
+  if (st_.first_miss_boot_ms == 0) st_.first_miss_boot_ms = boot_ms();
   e->holders[holder] = {1, now};
   e->waiters.push_back(Waiter{need_end, std::move(ready)});
   used_[device] += std::max<int64_t>(len, 1);
@@ -540,6 +547,7 @@ void MofCache::loader_main(Loader* L) {
           st_.loads++;
           st_.bytes_loaded += e.len;
           st_.load_ms += (now_s() - e.t_start) * 1000.0;
+          st_.last_landed_boot_ms = boot_ms();
           collect_ready(e, &fire);
         }
       }
@@ -588,6 +596,7 @@ void MofCache::loader_main(Loader* L) {
       if (!busy && --busy_loaders_ == 0) st_.load_wall_ms += (now_s() - busy_since_) * 1000.0;
       was_busy = busy;
     }
+    if (!subs.empty() && st_.first_read_boot_ms == 0) st_.first_read_boot_ms = boot_ms();
     if (!subs.empty() || !fire.empty()) {
       lk.unlock();
       // a chunk goes to disk as reads of opt_.read_bytes (the device sustains more small O_DIRECT reads in

@@ -71,6 +71,9 @@ class MofCache {
     double load_ms = 0;       // summed per-file load time
     double load_wall_ms = 0;  // time any load was in progress (loads overlap)
     double open_ms = 0;       // summed HBM allocation + IPC export + open of new entries
+    // CLOCK_BOOTTIME ms (the task processes' clock) of the first miss, the first disk read issued and
+    // the latest file fully landed: the loads' place on a wave's timeline
+    double first_miss_boot_ms = 0, first_read_boot_ms = 0, last_landed_boot_ms = 0;
   };
   // ok: the bytes [0, need_end) are in HBM (ref valid); else why says what failed.
   using Ready = std::function<void(bool ok, const Ref& ref, const std::string& why)>;
