@@ -1966,6 +1966,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   int resolved = 0;
   while (resolved < maps) {
     std::vector<FetchParams> batch;
+    const auto tw = std::chrono::steady_clock::now();
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || !fetch_list_.empty(); });
@@ -1975,6 +1976,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         fetch_list_.pop_front();
       }
     }
+    const auto ta = std::chrono::steady_clock::now();
     std::vector<FetchAck> acks(batch.size());
     std::mutex m;
     std::condition_variable c;
@@ -1999,6 +2001,11 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     {
       std::unique_lock<std::mutex> lk(m);
       c.wait(lk, [&] { return left == 0; });
+    }
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.fetch_cmd_wait_ms += std::chrono::duration<double, std::milli>(ta - tw).count();
+      st_.fetch_ack_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
     }
     if (probe && resolved == 0 && descriptors == 0) {
       // auto mode: the first answers decide; host-resident map outputs keep the staged path

@@ -75,6 +75,8 @@ struct ReduceStats {
   int64_t unmapped_descriptors = 0;   // descriptors not mappable here (other node, no handle): bytes fetched
   std::string unmapped_reason;        // why the first of them could not be mapped
   double descriptor_map_ms = 0;       // resolving descriptors (hipIpcOpenMemHandle of another process's HBM)
+  double fetch_cmd_wait_ms = 0;       // device fetch: waiting for the host's FETCH commands
+  double fetch_ack_wait_ms = 0;       // device fetch: waiting for the providers' descriptor answers
   double first_data_ms = -1;          // device fetch: from the merge's start to the first dataFromUda
   int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
   std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)
