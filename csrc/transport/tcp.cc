@@ -148,21 +148,17 @@ class TcpServer : public ServerTransport {
     ::shutdown(lfd_, SHUT_RDWR);
     ::close(lfd_);
     if (acceptor_.joinable()) acceptor_.join();
-    std::vector<std::thread> ts;
+    std::vector<std::shared_ptr<Conn>> cs;
     {
       std::lock_guard<std::mutex> g(mu_);
       for (auto& c : conns_) ::shutdown(c->fd, SHUT_RDWR);
-      ts.swap(readers_);
+      cs.swap(conns_);
     }
-    for (auto& t : ts) t.join();
-    std::lock_guard<std::mutex> g(mu_);
-    // wait for in-flight serves to drain before closing sockets
-    for (auto& c : conns_) {
-      std::unique_lock<std::mutex> lk(c->mu);
-      c->cv.wait(lk, [&] { return c->inflight == 0; });
+    // each reader ends once its serves have drained (read_loop), then its socket is closed
+    for (auto& c : cs) {
+      if (c->reader.joinable()) c->reader.join();
       ::close(c->fd);
     }
-    conns_.clear();
   }
   int port() const override { return port_; }
 
@@ -172,7 +168,23 @@ class TcpServer : public ServerTransport {
     std::mutex mu;  // serializes writes
     std::condition_variable cv;
     int inflight = 0;
+    std::thread reader;
+    std::atomic<bool> ended{false};  // the reader returned and no serve is writing to fd
   };
+
+  // Connections whose client went away (one reduce task's, after its fetches): join the reader and
+  // close the socket, so a long-lived provider holds threads and descriptors for live clients only.
+  void reap_locked() {
+    for (auto it = conns_.begin(); it != conns_.end();) {
+      if (!(*it)->ended.load()) {
+        ++it;
+        continue;
+      }
+      if ((*it)->reader.joinable()) (*it)->reader.join();
+      ::close((*it)->fd);
+      it = conns_.erase(it);
+    }
+  }
 
   void accept_loop() {
     while (running_) {
@@ -187,12 +199,18 @@ class TcpServer : public ServerTransport {
       auto c = std::make_shared<Conn>();
       c->fd = fd;
       std::lock_guard<std::mutex> g(mu_);
+      reap_locked();
       conns_.push_back(c);
-      readers_.emplace_back([this, c] { read_loop(c); });
+      c->reader = std::thread([this, c] {
+        read_loop(c);
+        std::unique_lock<std::mutex> lk(c->mu);  // serves still answering on this socket finish first
+        c->cv.wait(lk, [&] { return c->inflight == 0; });
+        c->ended = true;
+      });
     }
   }
 
-  void read_loop(std::shared_ptr<Conn> c) {
+  void read_loop(const std::shared_ptr<Conn>& c) {
     std::vector<char> payload;
     for (;;) {
       Header h;
@@ -270,7 +288,6 @@ class TcpServer : public ServerTransport {
   std::thread acceptor_;
   std::mutex mu_;
   std::vector<std::shared_ptr<Conn>> conns_;
-  std::vector<std::thread> readers_;
 };
 
 // ------------------------------------------------------------------------------------ client

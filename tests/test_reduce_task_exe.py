@@ -63,6 +63,34 @@ def test_reduce_task_processes_against_a_provider_process(native):
         prov.close()
 
 
+@pytest.mark.skipif(not os.access(EXE, os.X_OK), reason="uda_reduce_task not built")
+def test_provider_releases_the_connections_of_finished_tasks(native):
+    """A NodeManager's provider outlives thousands of reduce tasks: the sockets and reader threads of a
+    task's connections go when the task does, not at provider shutdown."""
+    port = _port()
+    prov = UdaProvider(transport="tcp", data_port=port, conf={"mapred.uda.provider.bind.address": "127.0.0.1"})
+    try:
+        job = "job_7_0002"
+        maps = datagen.terasort(num_maps=3, reducers=1, rows_per_map=500, seed=79)
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_{job}_m_{i:06d}_0"
+            data, index = encode_partitions(parts, None)
+            prov.add_mof_memory(job, mid, data, index)
+            ids.append(mid)
+        want = sum(len(m[0]) for m in maps)
+        rc, out = _task(native, port, job, ids, 0, want)
+        assert rc == 0 and out["error"] == "", out
+        fds0 = len(os.listdir("/proc/self/fd"))
+        for _ in range(12):
+            rc, out = _task(native, port, job, ids, 0, want)
+            assert rc == 0 and out["error"] == "", out
+        # the provider reaps a finished connection when the next one arrives: allow one task's worth
+        assert len(os.listdir("/proc/self/fd")) - fds0 <= 8
+    finally:
+        prov.close()
+
+
 def _service_provider(tmp_path, port):
     path = str(tmp_path / "merge.sock")
     prov = UdaProvider(transport="tcp", data_port=port, conf={"mapred.uda.provider.bind.address": "127.0.0.1",
