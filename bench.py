@@ -601,6 +601,9 @@ def run_node_files(args, ctx) -> int:
         if hs.get("first_miss_boot_ms"):  # the store's loads on the first wave's timeline (same clock)
             out["first_wave"]["store_ms"] = {k: round(hs[k + "_boot_ms"] - waves[0]["t_base_boot_ms"])
                                              for k in ("first_miss", "first_read", "last_landed")}
+            if provider.get("first_descriptor_request_boot_ms"):  # the front end's first descriptor FETCH
+                out["first_wave"]["store_ms"]["front_end_first_request"] = round(
+                    provider["first_descriptor_request_boot_ms"] - waves[0]["t_base_boot_ms"])
         out["first_step_ms"] = round(waves[0]["wall_ms"], 1)
         out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
         out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)

@@ -284,7 +284,9 @@ int uda_stats_json(uda_handle* h, char* out, int32_t outlen) {
   } else if (h->supplier) {
     s = "{\"role\":\"mof_supplier\",\"requests\":" + std::to_string(h->supplier->requests()) +
         ",\"bytes_served\":" + std::to_string(h->supplier->bytes_served()) +
-        ",\"descriptors_served\":" + std::to_string(h->supplier->descriptors_served()) + ",\"port\":" +
+        ",\"descriptors_served\":" + std::to_string(h->supplier->descriptors_served()) +
+        ",\"first_descriptor_request_boot_ms\":" + std::to_string(h->supplier->first_descriptor_request_boot_ms()) +
+        ",\"port\":" +
         std::to_string(h->supplier->port()) + ",\"io\":\"" + h->supplier->io_backend() + "\",\"hbm_store\":" +
         h->supplier->hbm_stats_json() + "}";
   } else {

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <ctime>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -1868,6 +1869,15 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   // (UDA_FAULT_DEVICE_ALLOC) also counts the task taking its workspaces.
   if (fault_hit("DEVICE_ALLOC")) throw UdaError("injected device allocation failure (GPU merge workspaces)");
   auto t0 = std::chrono::steady_clock::now();
+  auto boot_ms = [] {
+    timespec ts{};
+    clock_gettime(CLOCK_BOOTTIME, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec / 1e6;
+  };
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.merge_start_boot_ms = boot_ms();
+  }
   const int maps = init_.num_maps;
   const int device = device_;
   HIP_CHECK(hipSetDevice(device));
@@ -1977,6 +1987,10 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       }
     }
     const auto ta = std::chrono::steady_clock::now();
+    if (resolved == 0) {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.fetch_sent_boot_ms = boot_ms();
+    }
     std::vector<FetchAck> acks(batch.size());
     std::mutex m;
     std::condition_variable c;

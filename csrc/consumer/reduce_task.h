@@ -77,6 +77,8 @@ struct ReduceStats {
   double descriptor_map_ms = 0;       // resolving descriptors (hipIpcOpenMemHandle of another process's HBM)
   double fetch_cmd_wait_ms = 0;       // device fetch: waiting for the host's FETCH commands
   double fetch_ack_wait_ms = 0;       // device fetch: waiting for the providers' descriptor answers
+  double merge_start_boot_ms = 0;     // device fetch: CLOCK_BOOTTIME ms when the merge began / sent its
+  double fetch_sent_boot_ms = 0;      // first descriptor requests (a wave's timeline, bench.py --node)
   double first_data_ms = -1;          // device fetch: from the merge's start to the first dataFromUda
   int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
   std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)

@@ -223,6 +223,12 @@ void Supplier::process(Job& j) {
   ack.path = rec.path;
   if (j.req.buf_len == kDescriptorFetch) {
     // zero-copy fetch: the reducer reads the partition where it lives (RDMA WRITE analogue)
+    if (first_desc_boot_ms_.load() == 0) {
+      timespec ts{};
+      clock_gettime(CLOCK_BOOTTIME, &ts);
+      double zero = 0;
+      first_desc_boot_ms_.compare_exchange_strong(zero, (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec / 1e6);
+    }
     std::string why;
     std::shared_ptr<DeviceStore> st = mem ? nullptr : store();
     if (st) {

@@ -71,6 +71,8 @@ class Supplier : public DataServer {
   int64_t requests() const { return requests_.load(); }
   int64_t bytes_served() const { return bytes_.load(); }
   int64_t descriptors_served() const { return descriptors_.load(); }
+  // CLOCK_BOOTTIME ms of the first descriptor request (0: none yet): the fetch chain's place on a timeline
+  double first_descriptor_request_boot_ms() const { return first_desc_boot_ms_.load(); }
   // JOB_OVER: the job's MOFs held in the HBM store may be freed.
   void job_over(const std::string& job);
   // {"loads":..,"hits":..,...} of the HBM store ("{}" when there is none)
@@ -123,6 +125,7 @@ class Supplier : public DataServer {
   std::unordered_map<std::string, OpenFile> fds_;
   uint64_t fd_clock_ = 0;
   std::atomic<int64_t> requests_{0}, bytes_{0}, descriptors_{0}, releases_{0};
+  std::atomic<double> first_desc_boot_ms_{0};
 };
 
 }  // namespace uda
