@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <map>
@@ -51,13 +52,30 @@ void hip_check(hipError_t e, const char* what, const char* file, int line) {
 
 // ------------------------------------------------------------------------------------ buffers
 DeviceBuffer::~DeviceBuffer() { reset(); }
+namespace {
+// UDA_DEVICE_GUARD=1 (debug): every device buffer gets a tail of kGuardByte past its size (local
+// buffers: 64 KiB more; exportable ones: their IPC padding), checked when the buffer is freed. A kernel
+// writing past the end of its buffer then shows as a logged violation instead of silently changing the
+// next allocation's bytes.
+constexpr size_t kGuardBytes = 64 << 10;
+constexpr int kGuardByte = 0xA5;
+std::atomic<int64_t> g_guard_violations{0};
+bool guard_enabled() {
+  const char* e = std::getenv("UDA_DEVICE_GUARD");
+  return e && std::atoi(e) != 0;
+}
+}  // namespace
+
+int64_t device_guard_violations() { return g_guard_violations.load(); }
+
 void DeviceBuffer::alloc_impl(size_t bytes, bool resident, bool exportable) {
   reset();
   if (bytes == 0) return;
   if (fault_hit("DEVICE_ALLOC")) throw std::runtime_error("injected device allocation failure");
   // Blocks another process may map over hipIpc (our descriptor fetch, RCCL's peer registration of
   // send/receive buffers) must stay out of the size range that hangs the importer (device_ptr.h).
-  const size_t held = exportable ? ipc_safe_bytes(bytes) : bytes;
+  const bool guard = guard_enabled();
+  const size_t held = exportable ? ipc_safe_bytes(bytes + (guard ? 1 : 0)) : bytes + (guard ? kGuardBytes : 0);
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
   HbmLedger::get().on_alloc(dev, (int64_t)held, resident);
@@ -83,8 +101,29 @@ void DeviceBuffer::alloc_impl(size_t bytes, bool resident, bool exportable) {
   held_ = held;
   dev_ = dev;
   resident_ = resident;
+  guarded_ = guard && held > bytes;
+  if (guarded_)
+    HIP_CHECK(hipMemset(static_cast<uint8_t*>(ptr_) + bytes, kGuardByte, std::min(held - bytes, kGuardBytes)));
 }
 void DeviceBuffer::reset() {
+  if (ptr_ && guarded_) {
+    const size_t n = std::min(held_ - size_, kGuardBytes);
+    std::vector<uint8_t> tail(n);
+    if (hipMemcpy(tail.data(), static_cast<uint8_t*>(ptr_) + size_, n, hipMemcpyDeviceToHost) == hipSuccess) {
+      size_t bad = 0, first = n;
+      for (size_t i = 0; i < n; ++i)
+        if (tail[i] != (uint8_t)kGuardByte) {
+          ++bad;
+          first = std::min(first, i);
+        }
+      if (bad) {
+        g_guard_violations.fetch_add(1);
+        UDA_LOG(kError, "device buffer of %zu bytes: %zu guard bytes overwritten, the first %zu past its end", size_,
+                bad, first);
+      }
+    }
+    guarded_ = false;
+  }
   if (ptr_) note_device_free(ptr_);  // an exporter's cached IPC identity of this address is stale now
   if (ptr_ && trace::host_enabled()) {
     const int64_t tt = trace::now_ns();

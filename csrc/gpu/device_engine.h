@@ -92,14 +92,17 @@ class DeviceBuffer {
     held_ = o.held_;
     dev_ = o.dev_;
     resident_ = o.resident_;
+    guarded_ = o.guarded_;
     o.ptr_ = nullptr;
     o.size_ = o.held_ = 0;
+    o.guarded_ = false;
   }
   void* ptr_ = nullptr;
   size_t size_ = 0;
   size_t held_ = 0;
   int dev_ = -1;
   bool resident_ = false;
+  bool guarded_ = false;  // UDA_DEVICE_GUARD: the tail past size_ holds the guard pattern
 };
 
 // Owning pinned host allocation (pinned_host_alloc).
@@ -460,6 +463,8 @@ int device_count();
 // hosted tasks waited up to 106 ms for theirs). A stream handed back may still hold queued work; its
 // next user orders behind it. prewarm_streams() fills the device's pool ahead of a first wave.
 hipStream_t pooled_stream(int priority = 0);
+// UDA_DEVICE_GUARD=1: device buffers freed so far whose guard tail a kernel overwrote
+int64_t device_guard_violations();
 void return_stream(hipStream_t s);
 void prewarm_streams(int device, int n);
 

@@ -514,6 +514,8 @@ PYBIND11_MODULE(_uda_native, m) {
   // The provider store's read pattern without the store: `files` files of `file_bytes` written and synced,
   // then read round-robin in `chunk` pieces with `depth` reads kept in flight (O_DIRECT), as a loader
   // streams a job's MOF files. Returns GB/s; the files are removed.
+  m.def("device_guard_violations", [] { return uda::gpu::device_guard_violations(); });
+
   m.def("aio_interleave_bench", [](const std::string& dir, int files, int64_t file_bytes, int64_t chunk, int depth) {
     py::gil_scoped_release rel;
     file_bytes = file_bytes / chunk * chunk;

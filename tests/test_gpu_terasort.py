@@ -213,6 +213,33 @@ def test_spill_tiers_multirank_staged(require_gpu, tmp_path, monkeypatch, world,
                 jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
 
 
+@pytest.mark.parametrize("world,maps,rounds,reducers,map_sort", [(8, 2, 16, 1, False), (4, 3, 4, 3, True),
+                                                                  (1, 6, 2, 2, False)])
+def test_no_kernel_writes_past_its_buffers(require_gpu, monkeypatch, world, maps, rounds, reducers, map_sort):
+    """UDA_DEVICE_GUARD=1 puts a guard tail behind every device buffer and checks it at free: the map
+    sort, exchange, K-way plan + merge, validation and delivery of a multi-rank schedule (8 ranks on one
+    GPU, 16 rounds, as in a one-off checksum mismatch of that case) leave every tail intact."""
+    import gc
+
+    from uda_amd import native
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    monkeypatch.setenv("UDA_DEVICE_GUARD", "1")
+    before = native().device_guard_violations()
+    cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, reducers=reducers,
+                         validate=True, sample_every=64, map_sort=map_sort, **SMALL)
+    jobs, ck, rec = make_local_group(world, cfg, group=f"guard{world}{maps}{rounds}{reducers}")
+    readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(reducers)] for _ in range(world)]
+    for d in range(world):
+        jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
+    for _ in range(2):
+        stats = run_collective(jobs, lambda j: j.run_step(True))
+        for d, st in enumerate(stats):
+            check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+    del jobs, stats
+    gc.collect()
+    assert native().device_guard_violations() == before
+
+
 @pytest.mark.parametrize("env", [{"UDA_KWAY": "0"}, {"UDA_KWAY_TARGET": "5000"}, {"UDA_KWAY_CAP": "1536"},
                                  {"UDA_KWAY_FILL": "85", "UDA_KWAY_CAP": "512"}, {"UDA_KWAY_CAP": "1024"},
                                  {"UDA_KWAY_STAGED": "1"}, {"UDA_KWAY_STAGED": "1", "UDA_KWAY_CAP": "512"},
