@@ -228,10 +228,10 @@ def test_no_kernel_writes_past_its_buffers(require_gpu, monkeypatch, world, maps
     cfg = TeraSortConfig(rows_per_gpu=12000 * maps, maps_per_rank=maps, rounds=rounds, reducers=reducers,
                          validate=True, sample_every=64, map_sort=map_sort, **SMALL)
     jobs, ck, rec = make_local_group(world, cfg, group=f"guard{world}{maps}{rounds}{reducers}")
-    readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(reducers)] for _ in range(world)]
-    for d in range(world):
-        jobs[d].set_python_sink(lambda r, b, d=d: readers[d][r].feed(b), True)
     for _ in range(2):
+        readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(reducers)] for _ in range(world)]
+        for d in range(world):
+            jobs[d].set_python_sink(lambda r, b, d=d, rd=readers: rd[d][r].feed(b), True)
         stats = run_collective(jobs, lambda j: j.run_step(True))
         for d, st in enumerate(stats):
             check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
