@@ -45,7 +45,9 @@ class LocalDeviceStore : public DeviceStore {
     return "{\"loads\":" + std::to_string(st.loads) + ",\"hits\":" + std::to_string(st.hits) +
            ",\"holders\":" + std::to_string(st.holders) + ",\"releases\":" + std::to_string(st.releases) +
            ",\"holders_reaped\":" + std::to_string(st.holders_reaped) + ",\"load_wall_ms\":" +
-           std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) + ",\"load_gbps\":" +
+           std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) +
+           ",\"open_alloc_ms\":" + std::to_string(st.open_alloc_ms) + ",\"open_export_ms\":" +
+           std::to_string(st.open_export_ms) + ",\"load_gbps\":" +
            std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
            ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
            ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +

@@ -60,7 +60,7 @@ struct MofCache::Loader {
   };
   int device = 0;
   std::thread thr;
-  std::thread opener;          // allocates HBM and opens the file of new entries (never stalls the reads)
+  std::vector<std::thread> openers;  // allocate HBM and open the file of new entries (never stall the reads)
   std::condition_variable cv;  // with MofCache::mu_
   std::condition_variable ocv; // opener: new pending entries (with MofCache::mu_)
   bool stop = false;
@@ -98,7 +98,9 @@ MofCache::Loader* MofCache::loader_locked(int device) {
     L->device = device;
     Loader* lp = L.get();
     L->thr = std::thread([this, lp] { loader_main(lp); });
-    L->opener = std::thread([this, lp] { opener_main(lp); });
+    int n = 1;  // A/B: UDA_STORE_OPENERS entries allocated + exported + opened at once
+    if (const char* e = std::getenv("UDA_STORE_OPENERS")) n = std::max(1, std::min(16, std::atoi(e)));
+    for (int i = 0; i < n; ++i) L->openers.emplace_back([this, lp] { opener_main(lp); });
   }
   return L.get();
 }
@@ -120,7 +122,8 @@ MofCache::~MofCache() {
   }
   for (auto& kv : loaders_) {
     kv.second->ocv.notify_all();
-    if (kv.second->opener.joinable()) kv.second->opener.join();
+    for (auto& t : kv.second->openers)
+      if (t.joinable()) t.join();
     if (kv.second->thr.joinable()) kv.second->thr.join();
   }
   std::lock_guard<std::mutex> g(mu_);
@@ -368,10 +371,13 @@ void MofCache::opener_main(Loader* L) {
     IpcExport ipc;
     lk.unlock();
     const double t0 = now_s();
+    double t_alloc = t0, t_export = t0;
     if (err.empty()) {
       try {
         mem.reset(new DeviceBuffer((size_t)std::max<int64_t>(e->len, 1), /*resident=*/true));
+        t_alloc = now_s();
         ipc = ipc_export(mem->as<uint8_t>());
+        t_export = now_s();
         fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
         if (fd < 0 && direct) {
           direct = false;
@@ -386,6 +392,10 @@ void MofCache::opener_main(Loader* L) {
     lk.lock();
     --L->opening;
     st_.open_ms += dt * 1000.0;
+    if (t_alloc > t0) {
+      st_.open_alloc_ms += (t_alloc - t0) * 1000.0;
+      st_.open_export_ms += (t_export - t_alloc) * 1000.0;
+    }
     if (err.empty() && L->failed) err = "provider HBM store loader failed: " + L->setup_error;
     if (!err.empty() || e->failed) {
       if (fd >= 0) ::close(fd);

@@ -103,6 +103,7 @@ RECIPES: dict[str, tuple[int, str]] = {
     "nodefiles41_r1": (900, f"UDA_STORE_READ_MB=1 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodefiles41_r2": (900, f"UDA_STORE_READ_MB=2 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodefiles41_r4": (900, f"UDA_STORE_READ_MB=4 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles41_o4": (900, f"UDA_STORE_OPENERS=4 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "nodefiles41_64mb": (900, f"UDA_STORE_CHUNKS=8 UDA_STORE_CHUNK_MB=64 {PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "diskfree": (60, "df -h /tmp /dev/shm . 2>&1; true"),
     "nodefiles130": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --steps 2 --warmup 1"),
