@@ -1,4 +1,7 @@
 // DeviceStore over the HBM store of this process (provider/device_store.h, gpu/mof_cache.h).
+#include <unistd.h>
+
+#include <cstdlib>
 #include <memory>
 #include <string>
 
@@ -10,6 +13,17 @@
 namespace uda {
 
 namespace {
+
+// the pid field of a reducer holder id (node:pid:start:task); -1 for any other form
+int holder_pid(const std::string& holder) {
+  const size_t a = holder.find(':');
+  if (a == std::string::npos) return -1;
+  const size_t b = holder.find(':', a + 1);
+  if (b == std::string::npos) return -1;
+  const std::string p = holder.substr(a + 1, b - a - 1);
+  if (p.empty() || p.find_first_not_of("0123456789") != std::string::npos) return -1;
+  return std::atoi(p.c_str());
+}
 
 class LocalDeviceStore : public DeviceStore {
  public:
@@ -26,12 +40,20 @@ class LocalDeviceStore : public DeviceStore {
   bool acquire(const std::string& job, const std::string& path, const std::string& holder, int64_t offset,
                int64_t len, Done done, std::string* why) override {
     const int64_t need = offset + len;
+    // a holder in this process (node:pid:start:task, gpu::reducer_holder_id) reads the HBM directly;
+    // any other process maps it through the entry's hipIpc export, made on its first such fetch
+    const bool local = holder_pid(holder) == (int)getpid() && holder.compare(0, holder.find(':'), gpu::node_id()) == 0;
+    gpu::MofCache* cache = cache_.get();
     return cache_->acquire_async(
         job, path, holder, need,
-        [done, offset, need, path](bool ok, const gpu::MofCache::Ref& ref, const std::string& w) {
+        [done, offset, need, path, local, cache](bool ok, const gpu::MofCache::Ref& ref, const std::string& w) {
           if (!ok) return done(kNotDeviceResident, "provider HBM store: " + w);
           if (need > ref.len) return done(-4, "index beyond MOF file " + path);
-          done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, ref.ipc, /*leased=*/true));
+          if (local || ref.ipc.handle_hex != "-")
+            return done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, ref.ipc, /*leased=*/true));
+          gpu::IpcExport x = cache->export_of(path);
+          if (x.handle_hex == "-") x.base = ref.ipc.base;  // not exportable: the descriptor says so
+          done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, x, /*leased=*/true));
         },
         why);
   }

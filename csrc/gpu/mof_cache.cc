@@ -84,6 +84,7 @@ MofCache::MofCache(const Options& o) : opt_(o) {
   opt_.chunk_bytes = align_io(std::max<int64_t>(opt_.chunk_bytes, 1 << 20));
   opt_.chunks = std::max(2, opt_.chunks);
   if (const char* e = std::getenv("UDA_STORE_READ_MB")) opt_.read_bytes = std::atoll(e) << 20;
+  if (const char* e = std::getenv("UDA_STORE_EAGER_EXPORT")) eager_export_ = std::atoi(e) != 0;  // A/B
   opt_.read_bytes = opt_.read_bytes <= 0 ? opt_.chunk_bytes
                                          : align_io(std::min(opt_.read_bytes, opt_.chunk_bytes));
   if (!enabled()) return;
@@ -281,6 +282,33 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
   return true;
 }
 
+IpcExport MofCache::export_of(const std::string& path) {
+  std::shared_ptr<Entry> e;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = entries_.find(path);
+    if (it == entries_.end() || it->second->failed || !it->second->dptr) {
+      IpcExport none;
+      none.handle_hex = "-";
+      return none;
+    }
+    e = it->second;
+    if (e->exported) return e->ipc;
+  }
+  std::lock_guard<std::mutex> eg(e->export_mu);  // the entry (and its memory) lives while `e` is held
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (e->exported) return e->ipc;
+  }
+  const double t0 = now_s();
+  IpcExport x = ipc_export(e->dptr);
+  std::lock_guard<std::mutex> g(mu_);
+  st_.open_export_ms += (now_s() - t0) * 1000.0;
+  e->ipc = x;
+  e->exported = true;
+  return x;
+}
+
 bool MofCache::acquire(const std::string& job, const std::string& path, const std::string& holder, Ref* out,
                        std::string* why) {
   std::mutex m;
@@ -376,7 +404,9 @@ void MofCache::opener_main(Loader* L) {
       try {
         mem.reset(new DeviceBuffer((size_t)std::max<int64_t>(e->len, 1), /*resident=*/true));
         t_alloc = now_s();
-        ipc = ipc_export(mem->as<uint8_t>());
+        ipc.handle_hex = "-";  // exported on first need (export_of)
+        ipc.base = mem->as<uint8_t>();
+        if (eager_export_) ipc = ipc_export(mem->as<uint8_t>());
         t_export = now_s();
         fd = ::open(e->path.c_str(), O_RDONLY | O_CLOEXEC | (direct ? O_DIRECT : 0));
         if (fd < 0 && direct) {
@@ -404,6 +434,7 @@ void MofCache::opener_main(Loader* L) {
       e->mem = std::move(mem);
       e->dptr = e->mem->as<uint8_t>();
       e->ipc = ipc;
+      e->exported = eager_export_;
       e->fd = fd;
       e->direct = direct;
       if (e->len == 0) {
