@@ -560,12 +560,6 @@ def run_node_files(args, ctx) -> int:
         if g.returncode != 0 or "error" in job:
             raise RuntimeError(f"map phase failed: {job.get('error')}")
         t_map = time.perf_counter() - t
-        # the map outputs reach the disk before the reduce phase reads them (a job's maps finish long
-        # before its last reducer; here the map phase ends right before the first wave): write-back of
-        # the just-written files would otherwise run under the first wave's O_DIRECT opens and reads
-        t = time.perf_counter()
-        os.sync()
-        t_sync = time.perf_counter() - t
         port = _free_port()
         t = time.perf_counter()
         frontend = sp.Popen([sup, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"], stdin=sp.PIPE,
@@ -588,7 +582,7 @@ def run_node_files(args, ctx) -> int:
             time.sleep(0.2)
         node_ready_s = time.perf_counter() - t
         daemon = dict(hs.get("daemon", {}), prewarm=hs.get("prewarm"))
-        print(f"# node files: map phase {t_map:.1f}s + sync {t_sync:.1f}s ({job['store_bytes'] / 1e9:.1f} GB in {args.maps_per_gpu} "
+        print(f"# node files: map phase {t_map:.1f}s ({job['store_bytes'] / 1e9:.1f} GB in {args.maps_per_gpu} "
               f"file.out), front end up in {time.perf_counter() - t:.1f}s, node daemon {daemon}", file=sys.stderr,
               flush=True)
         warm, stats, validated = _run_waves(args, port, job["commands"], job["expected"], exe, errlog, {}, sp,
@@ -610,7 +604,6 @@ def run_node_files(args, ctx) -> int:
             if provider.get("first_descriptor_request_boot_ms"):  # the front end's first descriptor FETCH
                 out["first_wave"]["store_ms"]["front_end_first_request"] = round(
                     provider["first_descriptor_request_boot_ms"] - waves[0]["t_base_boot_ms"])
-        out["map_sync_s"] = round(t_sync, 2)
         out["first_step_ms"] = round(waves[0]["wall_ms"], 1)
         out["first_step_gbps"] = round(waves[0]["bytes"] / waves[0]["wall_ms"] / 1e6, 3)
         out["mof_files_gb"] = round(job["store_bytes"] / 1e9, 2)
