@@ -425,6 +425,8 @@ void MofCache::opener_main(Loader* L) {
     if (t_alloc > t0) {
       st_.open_alloc_ms += (t_alloc - t0) * 1000.0;
       st_.open_export_ms += (t_export - t_alloc) * 1000.0;
+      st_.open_file_ms += (t0 + dt - t_export) * 1000.0;
+      st_.open_file_max_ms = std::max(st_.open_file_max_ms, (t0 + dt - t_export) * 1000.0);
     }
     if (err.empty() && L->failed) err = "provider HBM store loader failed: " + L->setup_error;
     if (!err.empty() || e->failed) {
