@@ -70,8 +70,7 @@ class LocalDeviceStore : public DeviceStore {
            std::to_string(st.load_wall_ms) + ",\"open_ms\":" + std::to_string(st.open_ms) +
            ",\"open_alloc_ms\":" + std::to_string(st.open_alloc_ms) + ",\"open_export_ms\":" +
            std::to_string(st.open_export_ms) + ",\"open_file_ms\":" + std::to_string(st.open_file_ms) +
-           ",\"open_file_max_ms\":" + std::to_string(st.open_file_max_ms) + ",\"open_warm_ms\":" +
-           std::to_string(st.open_warm_ms) + ",\"load_gbps\":" +
+           ",\"open_file_max_ms\":" + std::to_string(st.open_file_max_ms) + ",\"load_gbps\":" +
            std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
            ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
            ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +

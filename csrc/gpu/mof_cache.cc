@@ -384,15 +384,6 @@ MofCache::Stats MofCache::stats() {
 // export takes milliseconds; 32 of them serialized in the read loop cost the first step a second).
 void MofCache::opener_main(Loader* L) {
   (void)hipSetDevice(L->device);
-  {
-    // a thread's first open(2) measured 140-175 ms on the GPU boxes (one per opener thread, whatever the
-    // file): pay it here, when the store starts, rather than on the first wave's critical path
-    const double t = now_s();
-    const int fd = ::open("/proc/self/stat", O_RDONLY | O_CLOEXEC);
-    if (fd >= 0) ::close(fd);
-    std::lock_guard<std::mutex> g(mu_);
-    st_.open_warm_ms = std::max(st_.open_warm_ms, (now_s() - t) * 1000.0);
-  }
   std::vector<Fire> fire;
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {

@@ -73,7 +73,6 @@ class MofCache {
     double open_ms = 0;       // summed HBM allocation + IPC export + open of new entries
     double open_alloc_ms = 0, open_export_ms = 0;  // the allocation and export parts of open_ms
     double open_file_ms = 0, open_file_max_ms = 0;  // open(2) of the files: summed, slowest
-    double open_warm_ms = 0;                         // an opener thread's first open(2), at start
     // CLOCK_BOOTTIME ms (the task processes' clock) of the first miss, the first disk read issued and
     // the latest file fully landed: the loads' place on a wave's timeline
     double first_miss_boot_ms = 0, first_read_boot_ms = 0, last_landed_boot_ms = 0;
