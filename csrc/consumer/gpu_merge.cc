@@ -125,10 +125,11 @@ struct DeviceWorkspace {
   }
 };
 
-// a task's stream from the device's pool (gpu::pooled_stream), handed back when the task is done
 struct StreamGuard {
   hipStream_t s = nullptr;
-  ~StreamGuard() { gpu::return_stream(s); }
+  ~StreamGuard() {
+    if (s) (void)hipStreamDestroy(s);
+  }
 };
 
 // Merge host-resident runs on the device. `codec` != kNone: the runs are block-compressed streams
@@ -151,7 +152,7 @@ class EarlyStager {
   // hipMemcpyAsync H2D from pinned memory runs as a blit kernel whose host reads slowed the
   // concurrent fetch memcpys into the same arena about 8x when partitions were staged piecewise.
   explicit EarlyStager(int device) : device_(device) {
-    s_ = gpu::pooled_stream();
+    HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
     const char* e = std::getenv("UDA_EARLY_H2D_SDMA");
     if (!e || std::atoi(e) != 0) {
       try {
@@ -177,7 +178,7 @@ class EarlyStager {
     cv_.notify_all();
     thr_.join();
     (void)hipStreamSynchronize(s_);
-    gpu::return_stream(s_);
+    (void)hipStreamDestroy(s_);
     if (sdma_) {
       std::vector<hsa_signal_t> all{sig_};
       all.insert(all.end(), gsig_, gsig_ + kGroups);
@@ -847,7 +848,6 @@ void prewarm_node_merges(int device, int tasks, int64_t round_bytes, int maps, i
   (void)gpu::SdmaEngine::for_device(device);
   warm_code(device);
   warm_workspaces(device, tasks);
-  gpu::prewarm_streams(device, tasks);
   gpu::DeviceReduceConfig cfg;
   cfg.device = device;
   cfg.kv_buf_bytes = kv_buf;
@@ -986,7 +986,7 @@ void ReduceTask::merge_gpu() {
   }
   const std::string tier = host_->get_conf("mapred.uda.gpu.spill", init_.local_dirs.empty() ? "host" : "disk");
   StreamGuard sg;
-  sg.s = gpu::pooled_stream();
+  HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
   PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
@@ -1785,8 +1785,8 @@ void ReduceTask::merge_gpu() {
       ws3 = ws3_lease.obj.get();
       ws3->reset_stats();
       StreamGuard sg2, sg3;
-      sg2.s = gpu::pooled_stream();
-      sg3.s = gpu::pooled_stream();
+      HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
+      HIP_CHECK(hipStreamCreateWithFlags(&sg3.s, hipStreamNonBlocking));
       DeviceWorkspace* wsv[3] = {&ws, ws2, ws3};
       hipStream_t sv[3] = {s, sg2.s, sg3.s};
       gpu::PinnedArena slice_mem[3];
@@ -1883,7 +1883,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   HIP_CHECK(hipSetDevice(device));
   HIP_PENDING("the device fetch");
   StreamGuard sg;
-  sg.s = gpu::pooled_stream();
+  HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
   hipStream_t s = sg.s;
   // Descriptors are references the providers keep for this task (gpu/mof_cache.h): released when the
   // task is done with them -- its merge finished, or it failed -- after the device has stopped
@@ -2288,9 +2288,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_CHECK(hipStreamSynchronize(s));
-    gpu::return_stream(sg.s);
+    HIP_CHECK(hipStreamDestroy(sg.s));
     sg.s = nullptr;
-    sg.s = gpu::pooled_stream(hi);
+    HIP_CHECK(hipStreamCreateWithPriority(&sg.s, hipStreamNonBlocking, hi));
     s = sg.s;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);

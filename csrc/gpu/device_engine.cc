@@ -270,58 +270,6 @@ int device_count() {
   return n;
 }
 
-namespace {
-struct StreamPool {
-  std::mutex mu;
-  std::map<std::pair<int, int>, std::vector<hipStream_t>> idle;  // (device, priority) -> streams
-  std::map<hipStream_t, std::pair<int, int>> owner;               // every pooled stream's key
-  static StreamPool& get() {
-    static StreamPool* p = new StreamPool;  // never destroyed: streams outlive static teardown order
-    return *p;
-  }
-};
-}  // namespace
-
-hipStream_t pooled_stream(int priority) {
-  int dev = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  StreamPool& p = StreamPool::get();
-  {
-    std::lock_guard<std::mutex> g(p.mu);
-    auto& v = p.idle[{dev, priority}];
-    if (!v.empty()) {
-      hipStream_t s = v.back();
-      v.pop_back();
-      return s;
-    }
-  }
-  hipStream_t s = nullptr;
-  HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
-  std::lock_guard<std::mutex> g(p.mu);
-  p.owner[s] = {dev, priority};
-  return s;
-}
-
-void return_stream(hipStream_t s) {
-  if (!s) return;
-  StreamPool& p = StreamPool::get();
-  std::lock_guard<std::mutex> g(p.mu);
-  auto it = p.owner.find(s);
-  if (it == p.owner.end()) {
-    (void)hipStreamDestroy(s);  // not one of ours
-    return;
-  }
-  p.idle[it->second].push_back(s);
-}
-
-void prewarm_streams(int device, int n) {
-  HIP_CHECK(hipSetDevice(device));
-  std::vector<hipStream_t> v;
-  for (int i = 0; i < n; ++i) v.push_back(pooled_stream(0));
-  for (hipStream_t s : v) return_stream(s);
-}
-
-
 // ------------------------------------------------------------------------------ DeviceMerger
 // Per-round plan blob layout (all int64 unless noted), uploaded with one H2D copy:
 //   RunDesc runs[K] | int64 elem_off[K+1] | uint8_t* bases[K] | per pass: pairs[3P], tile_prefix[P+1]

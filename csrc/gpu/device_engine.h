@@ -458,15 +458,8 @@ class ShuffleJob {
 std::string nccl_unique_id();
 int device_count();
 
-// Streams of finished tasks, kept per (device, priority) for the next task on the current device:
-// creating a stream costs milliseconds and concurrent creations serialize in the runtime (a wave of 15
-// hosted tasks waited up to 106 ms for theirs). A stream handed back may still hold queued work; its
-// next user orders behind it. prewarm_streams() fills the device's pool ahead of a first wave.
-hipStream_t pooled_stream(int priority = 0);
 // UDA_DEVICE_GUARD=1: device buffers freed so far whose guard tail a kernel overwrote
 int64_t device_guard_violations();
-void return_stream(hipStream_t s);
-void prewarm_streams(int device, int n);
 
 }  // namespace gpu
 }  // namespace uda
