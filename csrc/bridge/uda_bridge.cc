@@ -192,8 +192,18 @@ int uda_do_command(uda_handle* h, const char* cmd) {
   try {
     if (h->is_merger) {
       if (h->remote) {
-        h->remote->handle(cmd);
-        return 0;
+        try {
+          h->remote->handle(cmd);
+          return 0;
+        } catch (const std::exception& e) {
+          // the service runs this task for another user and refuses its files (local dirs outside the
+          // node's own): this process merges instead, with the files its own user may touch
+          if (c.header != uda::kInitMsg || std::string(e.what()).find("confined task") == std::string::npos) throw;
+          UDA_LOG(uda::kWarn, "merge service refused the task's files (%s): merging in this process", e.what());
+          h->remote->exit();
+          h->remote.reset();
+          h->task = std::make_unique<uda::ReduceTask>(h->opt, h->host.get());
+        }
       }
       if (!h->task) return fail_call(h, "reduce task already closed");
       h->task->handle(c);

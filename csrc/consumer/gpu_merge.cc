@@ -54,6 +54,7 @@
 #include "uda/compare.h"
 #include "uda/ifile.h"
 #include "uda/log.h"
+#include "uda/safe_file.h"
 #include "uda/trace.h"
 
 namespace uda {
@@ -125,11 +126,10 @@ struct DeviceWorkspace {
   }
 };
 
+// a task's stream from the device's pool (gpu::pooled_stream), handed back when the task is done
 struct StreamGuard {
   hipStream_t s = nullptr;
-  ~StreamGuard() {
-    if (s) (void)hipStreamDestroy(s);
-  }
+  ~StreamGuard() { gpu::return_stream(s); }
 };
 
 // Merge host-resident runs on the device. `codec` != kNone: the runs are block-compressed streams
@@ -152,7 +152,7 @@ class EarlyStager {
   // hipMemcpyAsync H2D from pinned memory runs as a blit kernel whose host reads slowed the
   // concurrent fetch memcpys into the same arena about 8x when partitions were staged piecewise.
   explicit EarlyStager(int device) : device_(device) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+    s_ = gpu::pooled_stream();
     const char* e = std::getenv("UDA_EARLY_H2D_SDMA");
     if (!e || std::atoi(e) != 0) {
       try {
@@ -178,7 +178,7 @@ class EarlyStager {
     cv_.notify_all();
     thr_.join();
     (void)hipStreamSynchronize(s_);
-    (void)hipStreamDestroy(s_);
+    gpu::return_stream(s_);
     if (sdma_) {
       std::vector<hsa_signal_t> all{sig_};
       all.insert(all.end(), gsig_, gsig_ + kGroups);
@@ -848,6 +848,7 @@ void prewarm_node_merges(int device, int tasks, int64_t round_bytes, int maps, i
   (void)gpu::SdmaEngine::for_device(device);
   warm_code(device);
   warm_workspaces(device, tasks);
+  gpu::prewarm_streams(device, tasks);
   gpu::DeviceReduceConfig cfg;
   cfg.device = device;
   cfg.kv_buf_bytes = kv_buf;
@@ -986,7 +987,7 @@ void ReduceTask::merge_gpu() {
   }
   const std::string tier = host_->get_conf("mapred.uda.gpu.spill", init_.local_dirs.empty() ? "host" : "disk");
   StreamGuard sg;
-  HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+  sg.s = gpu::pooled_stream();
   hipStream_t s = sg.s;
   PoolLease<DeviceWorkspace> ws_lease{device, DevicePool<DeviceWorkspace>::get().acquire(
                                                   device, [] { return std::make_unique<DeviceWorkspace>(); })};
@@ -1105,7 +1106,7 @@ void ReduceTask::merge_gpu() {
       char name[64];
       snprintf(name, sizeof(name), ".gpu-lpq-%03d", (int)spills.size());
       run.path = dirs[spills.size() % dirs.size()] + "/uda." + init_.reduce_task_id + name;
-      run.fd = ::open(run.path.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0600);
+      run.fd = create_private_file(run.path, O_RDWR);
       if (run.fd < 0) throw UdaError("cannot create spill file " + run.path + ": " + strerror(errno));
     } else {
       run.mem = spill_mem.alloc((size_t)std::max<int64_t>(run.bytes, 1));
@@ -1176,27 +1177,23 @@ void ReduceTask::merge_gpu() {
       if (::fsync(run_fd) != 0) throw UdaError("spill fsync failed");
       const std::string ip = run_path + ".idx";
       {
-        std::ofstream ix(ip, std::ios::binary | std::ios::trunc);
+        std::string ix;
         const int64_t n = (int64_t)idx_cut.size();
-        ix.write(reinterpret_cast<const char*>(&n), 8);
+        ix.append(reinterpret_cast<const char*>(&n), 8);
         for (size_t j = 0; j < idx_cut.size(); ++j) {
           const int32_t kl = (int32_t)idx_key[j].size();
-          ix.write(reinterpret_cast<const char*>(&idx_cut[j]), 8);
-          ix.write(reinterpret_cast<const char*>(&kl), 4);
-          ix.write(idx_key[j].data(), kl);
+          ix.append(reinterpret_cast<const char*>(&idx_cut[j]), 8);
+          ix.append(reinterpret_cast<const char*>(&kl), 4);
+          ix.append(idx_key[j].data(), (size_t)kl);
         }
-        ix.flush();
-        if (!ix) throw UdaError("cannot write LPQ index " + ip);
+        const int ifd = create_private_file(ip, O_WRONLY);
+        const bool ok = ifd >= 0 && write_all(ifd, ix.data(), ix.size()) && ::fsync(ifd) == 0;
+        if (ifd >= 0) ::close(ifd);
+        if (!ok) throw UdaError("cannot write LPQ index " + ip);
       }
-      const int ifd = ::open(ip.c_str(), O_RDONLY | O_CLOEXEC);
-      if (ifd < 0 || ::fsync(ifd) != 0) throw UdaError("LPQ index fsync failed");
-      ::close(ifd);
       std::string line = "glpq " + std::to_string(spills.size() - 1) + " " + std::to_string(run_bytes) + " " + run_path + " ";
       for (size_t j = 0; j < ids.size(); ++j) line += (j ? "," : "") + ids[j];
-      std::ofstream mf(manifest, std::ios::app);
-      mf << line << "\n";
-      mf.flush();
-      if (!mf) throw UdaError("cannot append to LPQ manifest " + manifest);
+      if (!append_owned_line(manifest, line)) throw UdaError("cannot append to LPQ manifest " + manifest);
       checkpointed = spills.size();
       if (fault_hit("LPQ_DONE")) throw UdaError("injected failure after an LPQ spill");
     }
@@ -1785,8 +1782,8 @@ void ReduceTask::merge_gpu() {
       ws3 = ws3_lease.obj.get();
       ws3->reset_stats();
       StreamGuard sg2, sg3;
-      HIP_CHECK(hipStreamCreateWithFlags(&sg2.s, hipStreamNonBlocking));
-      HIP_CHECK(hipStreamCreateWithFlags(&sg3.s, hipStreamNonBlocking));
+      sg2.s = gpu::pooled_stream();
+      sg3.s = gpu::pooled_stream();
       DeviceWorkspace* wsv[3] = {&ws, ws2, ws3};
       hipStream_t sv[3] = {s, sg2.s, sg3.s};
       gpu::PinnedArena slice_mem[3];
@@ -1883,7 +1880,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   HIP_CHECK(hipSetDevice(device));
   HIP_PENDING("the device fetch");
   StreamGuard sg;
-  HIP_CHECK(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+  sg.s = gpu::pooled_stream();
   hipStream_t s = sg.s;
   // Descriptors are references the providers keep for this task (gpu/mof_cache.h): released when the
   // task is done with them -- its merge finished, or it failed -- after the device has stopped
@@ -2288,9 +2285,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_CHECK(hipStreamSynchronize(s));
-    HIP_CHECK(hipStreamDestroy(sg.s));
+    gpu::return_stream(sg.s);
     sg.s = nullptr;
-    HIP_CHECK(hipStreamCreateWithPriority(&sg.s, hipStreamNonBlocking, hi));
+    sg.s = gpu::pooled_stream(hi);
     s = sg.s;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);

@@ -2,6 +2,8 @@
 #include "uda/fault.h"
 
 #include <fcntl.h>
+#include <climits>
+#include <cstdlib>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -20,6 +22,7 @@
 #include "uda/log.h"
 #include "uda/node_registry.h"
 #include "uda/queues.h"
+#include "uda/safe_file.h"
 #include "uda/trace.h"
 
 namespace uda {
@@ -327,8 +330,45 @@ void ReduceTask::handle(const HadoopCmd& cmd) {
   }
 }
 
-void ReduceTask::on_init(const InitParams& p) {
+std::string sandbox_check_dir(const std::vector<std::string>& roots, const std::string& p) {
+  char buf[PATH_MAX];
+  if (!::realpath(p.c_str(), buf)) return p + ": " + strerror(errno);
+  const std::string c(buf);
+  for (const auto& r : roots) {
+    if (r.empty()) continue;
+    if (c == r || (c.size() > r.size() && c.compare(0, r.size(), r) == 0 && (r.back() == '/' || c[r.size()] == '/')))
+      return "";
+  }
+  return p + " is outside the node's local directories";
+}
+
+bool sandbox_trusted_file(const std::vector<std::string>& dirs, const std::string& path) {
+  if (!owned_regular_file(path)) return false;
+  if (dirs.empty()) return true;
+  const size_t slash = path.rfind('/');
+  if (slash == std::string::npos) return false;
+  return sandbox_check_dir(dirs, path.substr(0, slash == 0 ? 1 : slash)).empty();
+}
+
+void ReduceTask::on_init(const InitParams& p_in) {
   if (inited_) throw ProtocolError("INIT received twice");
+  InitParams p = p_in;
+  if (sandbox_.enabled) {
+    // a task run for another local user: its id names files, and its local dirs are where this
+    // process's user creates, reads back and unlinks them
+    if (p.reduce_task_id.empty() || p.reduce_task_id.find("..") != std::string::npos ||
+        p.reduce_task_id.find_first_not_of("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_.-") !=
+            std::string::npos)
+      throw ProtocolError("reduce task id '" + p.reduce_task_id + "' is not allowed for a confined task");
+    std::vector<std::string> canon;
+    for (const auto& d : p.local_dirs) {
+      const std::string why = sandbox_check_dir(sandbox_.roots, d);
+      if (!why.empty()) throw ProtocolError("confined task: local dir " + why);
+      char buf[PATH_MAX];
+      canon.push_back(::realpath(d.c_str(), buf) ? std::string(buf) : d);
+    }
+    p.local_dirs = canon;
+  }
   init_ = p;
   kind_ = key_kind_from_class(p.key_class.c_str());
   if (kind_ == KeyKind::kUnsupported)
@@ -424,6 +464,7 @@ void ReduceTask::on_init(const InitParams& p) {
           codec_name(codec_), key_kind_name(kind_), backend_.c_str());
   // CPU: the hybrid (approach 2) LPQ files; GPU: the disk-tier LPQ spills of the GPU hybrid merge
   checkpoint_ = host_->conf_i64("mapred.uda.lpq.checkpoint", 0) != 0 && (backend_ == "gpu" || net_.online == 2);
+  if (checkpoint_ && sandbox_.enabled && init_.local_dirs.empty()) checkpoint_ = false;  // no /tmp manifests
   if (checkpoint_) load_checkpoint();
   if (backend_ == "gpu") {
     device_conf_ = host_->get_conf("mapred.uda.gpu.device", "auto");
@@ -503,6 +544,10 @@ std::string ReduceTask::checkpoint_path() const {
 // continues the LPQ sequence, its file exists with that size and it holds the MOF count the LPQ
 // geometry gives that index (same num_maps / lpq_size as the failed attempt).
 void ReduceTask::load_checkpoint() {
+  // only a manifest this process's user wrote, listing files it wrote (in a confined task: inside its
+  // local dirs); anything else is not ours to read back or unlink
+  const std::vector<std::string> trust_dirs = sandbox_.enabled ? init_.local_dirs : std::vector<std::string>();
+  if (!sandbox_trusted_file(trust_dirs, checkpoint_path())) return;
   std::ifstream in(checkpoint_path());
   if (!in) return;
   const int maps = init_.num_maps;
@@ -516,7 +561,8 @@ void ReduceTask::load_checkpoint() {
       if (!(ls >> tag >> idx >> bytes >> path >> ids) || tag != "glpq") break;
       struct stat sb, si;
       if (idx != (int)restored_files_.size() || ::stat(path.c_str(), &sb) != 0 || (long long)sb.st_size != bytes ||
-          ::stat((path + ".idx").c_str(), &si) != 0)
+          ::stat((path + ".idx").c_str(), &si) != 0 || !sandbox_trusted_file(trust_dirs, path) ||
+          !sandbox_trusted_file(trust_dirs, path + ".idx"))
         break;
       std::set<std::string> v;
       for (size_t b = 0;;) {
@@ -550,7 +596,9 @@ void ReduceTask::load_checkpoint() {
     if (!(ls >> tag >> idx >> bytes >> path >> ids) || tag != "lpq") break;
     const int want = (idx < regular) ? per : per + 1;
     struct stat sb;
-    if (idx != (int)restored_files_.size() || ::stat(path.c_str(), &sb) != 0 || (long long)sb.st_size != bytes) break;
+    if (idx != (int)restored_files_.size() || ::stat(path.c_str(), &sb) != 0 || (long long)sb.st_size != bytes ||
+        !sandbox_trusted_file(trust_dirs, path))
+      break;
     std::vector<std::string> v;
     for (size_t b = 0; b <= ids.size();) {
       const size_t e = ids.find(',', b);
@@ -782,7 +830,7 @@ void ReduceTask::merge_hybrid() {
       if (!item.first) break;
       std::unique_ptr<MergeQueue> q(item.first);
       // LPQ merge -> spill file (write_kv_to_file, StreamRW.cc:863-887): records + EOF marker
-      int fd = ::open(item.second.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0600);
+      int fd = create_private_file(item.second, O_WRONLY);
       if (fd < 0) throw UdaError("cannot create spill file " + item.second + ": " + strerror(errno));
       files.push_back(item.second);
       KVWriter w(q.get());
@@ -814,10 +862,8 @@ void ReduceTask::merge_hybrid() {
           std::lock_guard<std::mutex> g(ids_mu);
           for (const auto& m : lpq_ids[item.second]) ids += (ids.empty() ? "" : ",") + m;
         }
-        std::ofstream mf(manifest, std::ios::app);
-        mf << "lpq " << i << " " << written + 2 << " " << item.second << " " << ids << "\n";
-        mf.flush();
-        if (!mf) {
+        if (!append_owned_line(manifest, "lpq " + std::to_string(i) + " " + std::to_string(written + 2) + " " +
+                                              item.second + " " + ids)) {
           ::close(fd);
           throw UdaError("cannot append to LPQ manifest " + manifest);
         }

@@ -85,10 +85,25 @@ struct ReduceStats {
   std::string backend;
 };
 
+// File confinement of a reduce task that runs on behalf of another local user (a merge-service session
+// whose client's uid is not the service's): what the task creates, reads back and unlinks must stay in the
+// node's own local directories, and it trusts only files this process's user owns.
+struct TaskSandbox {
+  bool enabled = false;
+  std::vector<std::string> roots;  // canonical local directories a confined task may use (its local_dirs)
+};
+// Returns "" if `p` (canonicalised) lies inside one of `roots`, else why not.
+std::string sandbox_check_dir(const std::vector<std::string>& roots, const std::string& p);
+// A file the task may read back / unlink: a regular file (not a symlink) owned by this process's euid
+// inside one of `dirs`.
+bool sandbox_trusted_file(const std::vector<std::string>& dirs, const std::string& path);
+
 class ReduceTask {
  public:
   ReduceTask(const NetlevOptions& net, Host* host);
   ~ReduceTask();
+  // before INIT: confine the task's files (merge service, foreign client)
+  void set_sandbox(const TaskSandbox& sb) { sandbox_ = sb; }
   // Downcall from the host. Throws ProtocolError on a malformed/unsupported command.
   void handle(const HadoopCmd& cmd);
   // Close (reduceExitMsg): stop and join the merge thread.
@@ -141,6 +156,7 @@ class ReduceTask {
   // take a while in a fresh process and INIT must not wait for it.
   void place_on_gpu();
   std::once_flag placed_;
+  TaskSandbox sandbox_;
   std::string device_conf_ = "auto";   // read on the INIT thread
   std::string fault_spec_;             // mapred.uda.fault.inject (tests: faults of this task only)
   double hbm_budget_conf_ = 0;

@@ -4,6 +4,8 @@
 
 #include <cerrno>
 #include <cstring>
+
+#include "uda/safe_file.h"
 #include <stdexcept>
 
 #include "uda/ifile.h"
@@ -44,7 +46,7 @@ void write_spill_index(const std::string& path, const std::vector<int64_t>& inde
   std::vector<uint8_t> b(index.size() * 8 + 8);
   for (size_t i = 0; i < index.size(); ++i) put_be64(&b[i * 8], index[i]);
   put_be64(&b[index.size() * 8], (int64_t)crc32_ieee(b.data(), index.size() * 8));
-  const int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0644);
+  const int fd = create_private_file(path, O_WRONLY);
   if (fd < 0) throw std::runtime_error("cannot create " + path + ": " + strerror(errno));
   const bool ok = ::write(fd, b.data(), b.size()) == (ssize_t)b.size();
   ::close(fd);

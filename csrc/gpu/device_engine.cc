@@ -270,6 +270,58 @@ int device_count() {
   return n;
 }
 
+namespace {
+struct StreamPool {
+  std::mutex mu;
+  std::map<std::pair<int, int>, std::vector<hipStream_t>> idle;  // (device, priority) -> streams
+  std::map<hipStream_t, std::pair<int, int>> owner;               // every pooled stream's key
+  static StreamPool& get() {
+    static StreamPool* p = new StreamPool;  // never destroyed: streams outlive static teardown order
+    return *p;
+  }
+};
+}  // namespace
+
+hipStream_t pooled_stream(int priority) {
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  StreamPool& p = StreamPool::get();
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    auto& v = p.idle[{dev, priority}];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  std::lock_guard<std::mutex> g(p.mu);
+  p.owner[s] = {dev, priority};
+  return s;
+}
+
+void return_stream(hipStream_t s) {
+  if (!s) return;
+  StreamPool& p = StreamPool::get();
+  std::lock_guard<std::mutex> g(p.mu);
+  auto it = p.owner.find(s);
+  if (it == p.owner.end()) {
+    (void)hipStreamDestroy(s);  // not one of ours
+    return;
+  }
+  p.idle[it->second].push_back(s);
+}
+
+void prewarm_streams(int device, int n) {
+  HIP_CHECK(hipSetDevice(device));
+  std::vector<hipStream_t> v;
+  for (int i = 0; i < n; ++i) v.push_back(pooled_stream(0));
+  for (hipStream_t s : v) return_stream(s);
+}
+
+
 // ------------------------------------------------------------------------------ DeviceMerger
 // Per-round plan blob layout (all int64 unless noted), uploaded with one H2D copy:
 //   RunDesc runs[K] | int64 elem_off[K+1] | uint8_t* bases[K] | per pass: pairs[3P], tile_prefix[P+1]
@@ -990,15 +1042,11 @@ void ShuffleJob::compute_plans() {
           const int r = m * W + p, c = i * Q_ + q;
           send_counts[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = pos(r, c + 1) - pos(r, c);
         }
-  std::vector<int64_t> recv_ck;
-  if (W == 1) {
-    recv_counts = send_counts;
-  } else {
-    if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
-    exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), n_per_peer, s_comm_);
-    // checksums of every slice this rank sends: per (run, cell) in run batches, then laid out
-    // [p][q][i][m] like the counts
-    std::vector<int64_t> cell_ck((size_t)nruns * C_, 0);
+  // checksums of every (run, cell) slice of the local runs: what this rank sends (exchange
+  // verification at the peers) and its own cells (checked where the merge reads them); then laid out
+  // [p][q][i][m] like the counts
+  std::vector<int64_t> cell_ck((size_t)nruns * C_, 0);
+  {
     DeviceBuffer d_sl((size_t)nruns * C_ * sizeof(RunDesc)), d_ck((size_t)nruns * C_ * 8);
     for_run_batches([&](int r0, int nr, uint8_t* const* bases, const int64_t*, const int*) {
       std::vector<uint8_t*> hb(nr);
@@ -1025,16 +1073,33 @@ void ShuffleJob::compute_plans() {
                                s_compute_));
       HIP_CHECK(hipStreamSynchronize(s_compute_));
     });
-    std::vector<int64_t> sl((size_t)W * n_per_peer);
-    for (int p = 0; p < W; ++p)
-      for (int q = 0; q < Q_; ++q)
-        for (int i = 0; i < R_; ++i)
-          for (int m = 0; m < M; ++m)
-            sl[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = cell_ck[(size_t)(m * W + p) * C_ + i * Q_ + q];
-    const std::vector<int64_t>& send_ck = sl;
-    recv_ck.assign(send_ck.size(), 0);
+  }
+  std::vector<int64_t> send_ck((size_t)W * n_per_peer), recv_ck((size_t)W * n_per_peer, 0);
+  for (int p = 0; p < W; ++p)
+    for (int q = 0; q < Q_; ++q)
+      for (int i = 0; i < R_; ++i)
+        for (int m = 0; m < M; ++m)
+          send_ck[(size_t)p * n_per_peer + ((size_t)q * R_ + i) * M + m] = cell_ck[(size_t)(m * W + p) * C_ + i * Q_ + q];
+  if (W == 1) {
+    recv_counts = send_counts;
+    recv_ck = send_ck;
+  } else {
+    if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
+    exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), n_per_peer, s_comm_);
     exchange_->alltoall_i64(send_ck.data(), recv_ck.data(), n_per_peer, s_comm_);
   }
+  // own cells: this rank's plan-time checksums, whatever the counts exchange carried for the self entry
+  for (int q = 0; q < Q_; ++q)
+    for (int i = 0; i < R_; ++i)
+      for (int m = 0; m < M; ++m)
+        recv_ck[(size_t)me * n_per_peer + ((size_t)q * R_ + i) * M + m] =
+            send_ck[(size_t)me * n_per_peer + ((size_t)q * R_ + i) * M + m];
+  expect_group_ck_.assign((size_t)Q_ * R_, 0);
+  for (int q = 0; q < Q_; ++q)
+    for (int s = 0; s < W; ++s)
+      for (int i = 0; i < R_; ++i)
+        for (int m = 0; m < M; ++m)
+          expect_group_ck_[(size_t)q * R_ + i] += (uint64_t)recv_ck[(size_t)s * n_per_peer + ((size_t)q * R_ + i) * M + m];
 
   plans_.assign(Q_, RoundPlan());
   reducer_records_.assign(R_, 0);
@@ -1170,8 +1235,44 @@ void ShuffleJob::compute_plans() {
     HIP_CHECK(hipMemcpy(d_verify_expect_[q].as(), vexp[q].data(), vexp[q].size() * 8, hipMemcpyHostToDevice));
     max_v = std::max(max_v, verify_n_[q]);
   }
+  // own cells, where the merge reads them (build_runs in run_step)
+  d_own_runs_.clear();
+  d_own_expect_.clear();
+  d_own_runs_.resize(Q_);
+  d_own_expect_.resize(Q_);
+  own_n_.assign(Q_, 0);
+  own_max_nrec_.assign(Q_, 0);
+  for (int q = 0; q < Q_; ++q) {
+    const RoundPlan& rp = plans_[q];
+    std::vector<RunDesc> v;
+    std::vector<int64_t> e;
+    for (int i = 0; i < R_; ++i)
+      for (int j = 0; j < M; ++j) {
+        const size_t x = ((size_t)me * R_ + i) * M + j;
+        if (rp.recv_cnt[x] <= 0) continue;
+        RunDesc d;
+        d.nrec = rp.recv_cnt[x];
+        d.nbytes = d.nrec * kTeraRecordBytes;
+        d.offsets = nullptr;
+        d.base = rp.recv_off[x] >= 0 ? recv_slots_[q % kSlots].as<uint8_t>() + rp.recv_off[x]
+                                     : store_dev_base_ + run_off_[j * W + me] + rp.self_beg[(size_t)i * M + j] * kTeraRecordBytes;
+        v.push_back(d);
+        e.push_back(cell_ck[(size_t)(j * W + me) * C_ + i * Q_ + q]);
+        own_max_nrec_[q] = std::max(own_max_nrec_[q], d.nrec);
+      }
+    own_n_[q] = (int)v.size();
+    max_v = std::max(max_v, own_n_[q]);
+    if (v.empty()) continue;
+    d_own_runs_[q].alloc(v.size() * sizeof(RunDesc));
+    d_own_expect_[q].alloc(e.size() * 8);
+    HIP_CHECK(hipMemcpy(d_own_runs_[q].as(), v.data(), v.size() * sizeof(RunDesc), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_own_expect_[q].as(), e.data(), e.size() * 8, hipMemcpyHostToDevice));
+  }
   if (max_v > 65535) throw std::runtime_error("exchange verification: too many slices per round");
   if (max_v > 0) d_verify_got_.alloc((size_t)max_v * 8);
+  d_diag_.alloc((size_t)Q_ * diag_stride() * 8);
+  d_d2h_runs_.alloc((size_t)R_ * sizeof(RunDesc));
+  d_d2h_ck_.alloc((size_t)R_ * 8);
   // pinned-DRAM tier: each round's H2D (own cells into the receive slot, and for W > 1 the outgoing
   // slices into the send staging) is one batched-copy launch over fixed descriptors. The kernel reads
   // the pinned store over PCIe; hipMemcpyAsync would queue these copies on the same SDMA engine as
@@ -1264,6 +1365,32 @@ void ShuffleJob::copy_loop() {
       HIP_CHECK(hipEventSynchronize(merged_ev_[r.slot]));
       const uint8_t* src = out_slots_[r.slot].as<uint8_t>();
       const bool last_round = (r.q == Q_ - 1);
+      bool check;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        check = step_check_delivery_;
+      }
+      if (check) {  // the output slot as the D2H is about to read it, per reducer
+        std::vector<RunDesc> gr(R_);
+        int64_t o = 0, mx = 0;
+        for (int i = 0; i < R_; ++i) {
+          gr[i].base = src + o * kTeraRecordBytes;
+          gr[i].nrec = r.group_recs[i];
+          gr[i].nbytes = gr[i].nrec * kTeraRecordBytes;
+          gr[i].offsets = nullptr;
+          o += r.group_recs[i];
+          mx = std::max(mx, r.group_recs[i]);
+        }
+        std::vector<uint64_t> ck(R_, 0);
+        HIP_CHECK(hipMemcpyAsync(d_d2h_runs_.as(), gr.data(), (size_t)R_ * sizeof(RunDesc), hipMemcpyHostToDevice, s_copy_));
+        launch_slice_checksums(d_d2h_runs_.as<RunDesc>(), R_, std::max<int64_t>(mx, 1),
+                               d_d2h_ck_.as<unsigned long long>(), s_copy_);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(ck.data(), d_d2h_ck_.as(), (size_t)R_ * 8, hipMemcpyDeviceToHost, s_copy_));
+        HIP_CHECK(hipStreamSynchronize(s_copy_));
+        std::lock_guard<std::mutex> g(mu_);
+        for (int i = 0; i < R_; ++i) pre_d2h_ck_[(size_t)r.q * R_ + i] = ck[i];
+      }
       std::vector<int> used;
       int64_t goff = 0;
       for (int i = 0; i < R_; ++i) {
@@ -1271,7 +1398,7 @@ void ShuffleJob::copy_loop() {
         if (bytes == 0 && last_round) {
           {
             std::lock_guard<std::mutex> g(mu_);
-            items_[i].push_back(Item{-1, 0, true, now_ms()});
+            items_[i].push_back(Item{-1, 0, true, now_ms(), r.q});
           }
           cv_.notify_all();
         }
@@ -1307,7 +1434,7 @@ void ShuffleJob::copy_loop() {
           used.push_back(k);
           {
             std::lock_guard<std::mutex> g(mu_);
-            items_[i].push_back(Item{k, len, last_round && off >= bytes, now_ms()});
+            items_[i].push_back(Item{k, len, last_round && off >= bytes, now_ms(), r.q});
           }
           cv_.notify_all();
         }
@@ -1344,13 +1471,16 @@ void ShuffleJob::consume_loop(int i) {
     uint8_t* eb = eof_bufs_[i].get();
     for (;;) {
       Item it;
+      bool check;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || !items_[i].empty(); });
         if (stop_) return;
         it = items_[i].front();
         items_[i].pop_front();
+        check = step_check_delivery_;
       }
+      uint64_t got_ck = 0;
       int err = 0;
       int64_t nb = 0;
       double waited = 0;
@@ -1362,6 +1492,9 @@ void ShuffleJob::consume_loop(int i) {
           HIP_CHECK(hipEventSynchronize(piece_ev_[it.pslot]));
         waited = now_ms() - it.issued_ms;
         const uint8_t* base = ring_ + (int64_t)it.pslot * piece_bytes_;
+        if (check)
+          for (int64_t off = 0; off + kTeraRecordBytes <= it.bytes; off += kTeraRecordBytes)
+            got_ck += record_hash(base + off, kTeraRecordBytes);
         for (int64_t off = 0; off < it.bytes; off += buf_bytes) {
           const int64_t len = std::min(buf_bytes, it.bytes - off);
           const bool final_chunk = it.last && off + len >= it.bytes;
@@ -1386,6 +1519,7 @@ void ShuffleJob::consume_loop(int i) {
       {
         std::lock_guard<std::mutex> g(mu_);
         if (it.pslot >= 0) pinned_free_[it.pslot] = true;
+        if (check && it.q >= 0 && it.q < Q_) delivered_ck_[(size_t)it.q * R_ + i] += got_ck;
         step_buffers_ += nb;
         step_d2h_ms_ += waited;
         if (err && !step_error_) step_error_ = err;
@@ -1433,6 +1567,60 @@ void ShuffleJob::refresh_plan() {
             throw std::runtime_error("replan: a peer's counts changed since plan()");
 }
 
+// Validate steps: where a wrong total checksum came from. Per (round q, reducer i): the received
+// slices and own cells against their plan-time checksums right before and right after the merge, the
+// merged output against the sum of its inputs, and (check_delivery) the output slot right before its
+// D2H and the bytes the consumer received against the merged output.
+void ShuffleJob::localize_mismatch(StepStats& st) {
+  const int F = diag_stride();
+  std::vector<uint64_t> dg((size_t)Q_ * F);
+  HIP_CHECK(hipMemcpy(dg.data(), d_diag_.as(), dg.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> pre_d2h, deliv;
+  bool check;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    pre_d2h = pre_d2h_ck_;
+    deliv = delivered_ck_;
+    check = step_check_delivery_;
+  }
+  st.pre_merge_errors = st.own_errors = st.merge_errors = 0;
+  st.pre_d2h_errors = st.delivery_errors = check ? 0 : -1;
+  std::string first[5];
+  auto note = [](std::string& f, const char* what, int q, int i, uint64_t a, uint64_t b) {
+    if (!f.empty()) return;
+    char buf[160];
+    std::snprintf(buf, sizeof(buf), "%s: round %d reducer %d (%016llx vs %016llx)", what, q, i, (unsigned long long)a,
+                  (unsigned long long)b);
+    f = buf;
+  };
+  for (int q = 0; q < Q_; ++q) {
+    const uint64_t* d = &dg[(size_t)q * F];
+    st.pre_merge_errors += (int64_t)d[0];
+    st.own_errors += (int64_t)(d[2] + d[3]);
+    if (d[0]) note(first[0], "received slices wrong before the merge", q, -1, d[0], d[1]);
+    if (d[2] || d[3]) note(first[1], "own cells wrong (before, after the merge)", q, -1, d[2], d[3]);
+    for (int i = 0; i < R_; ++i) {
+      const uint64_t merged = d[4 + i], expect = expect_group_ck_[(size_t)q * R_ + i];
+      if (merged != expect) {
+        ++st.merge_errors;
+        note(first[2], "merged output differs from its inputs", q, i, merged, expect);
+      }
+      if (!check) continue;
+      if (pre_d2h[(size_t)q * R_ + i] != merged) {
+        ++st.pre_d2h_errors;
+        note(first[3], "output slot changed between the merge and its D2H", q, i, pre_d2h[(size_t)q * R_ + i], merged);
+      }
+      if (deliv[(size_t)q * R_ + i] != merged) {
+        ++st.delivery_errors;
+        note(first[4], "consumer received other bytes than the merge wrote", q, i, deliv[(size_t)q * R_ + i], merged);
+      }
+    }
+  }
+  st.diag.clear();
+  for (const auto& f : first)
+    if (!f.empty()) st.diag += (st.diag.empty() ? "" : "; ") + f;
+}
+
 StepStats ShuffleJob::run_step(bool validate) {
   trace::Range tr_step("uda.step");
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -1450,6 +1638,9 @@ StepStats ShuffleJob::run_step(bool validate) {
     step_buffers_ = 0;
     step_error_ = 0;
     step_d2h_ms_ = 0;
+    step_check_delivery_ = validate && cfg_.check_delivery && deliver;
+    pre_d2h_ck_.assign((size_t)Q_ * R_, 0);
+    delivered_ck_.assign((size_t)Q_ * R_, 0);
   }
   std::vector<hipEvent_t> ev(4 * (size_t)Q_);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -1457,7 +1648,10 @@ StepStats ShuffleJob::run_step(bool validate) {
   Elem* vprev = reinterpret_cast<Elem*>(d_validate_.as<uint8_t>() + 64);
   Elem* vlast = vprev + R_;
   std::vector<bool> has_prev(R_, false);
-  if (validate) HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 64, s_compute_));
+  if (validate) {
+    HIP_CHECK(hipMemsetAsync(d_validate_.as(), 0, 64, s_compute_));
+    HIP_CHECK(hipMemsetAsync(d_diag_.as(), 0, (size_t)Q_ * diag_stride() * 8, s_compute_));
+  }
   if (cfg_.replan) {
     const double tp = now_ms();
     refresh_plan();
@@ -1684,6 +1878,28 @@ StepStats ShuffleJob::run_step(bool validate) {
       wait_until([&] { return out_free_[q - kSlots] != 0; });
       st.wait_out_ms += now_ms() - tw;
     }
+    unsigned long long* dg = d_diag_.as<unsigned long long>() + (size_t)q * diag_stride();
+    // the merge's inputs as it is about to read them: received slices and own cells against their
+    // plan-time checksums (the same checks after the merge tell a late write from a late read)
+    auto check_inputs = [&](int at) {
+      if (W > 1 && verify_n_[q] > 0) {
+        launch_slice_checksums(d_verify_runs_[q].as<RunDesc>(), verify_n_[q], verify_max_nrec_[q],
+                               d_verify_got_.as<unsigned long long>(), s_compute_);
+        launch_count_mismatch(d_verify_got_.as<unsigned long long>(), d_verify_expect_[q].as<unsigned long long>(),
+                              verify_n_[q], dg + at, s_compute_);
+        if (at == 1)
+          launch_count_mismatch(d_verify_got_.as<unsigned long long>(),
+                                d_verify_expect_[q].as<unsigned long long>(), verify_n_[q], vstats + 2, s_compute_);
+      }
+      if (own_n_[q] > 0) {
+        launch_slice_checksums(d_own_runs_[q].as<RunDesc>(), own_n_[q], own_max_nrec_[q],
+                               d_verify_got_.as<unsigned long long>(), s_compute_);
+        launch_count_mismatch(d_verify_got_.as<unsigned long long>(), d_own_expect_[q].as<unsigned long long>(),
+                              own_n_[q], dg + at + 2, s_compute_);
+      }
+      HIP_CHECK(hipGetLastError());
+    };
+    if (validate) check_inputs(0);
     HIP_CHECK(hipEventRecord(ev[4 * q + 2], s_compute_));
     uint8_t* out = out_slots_[slot].as<uint8_t>();
     int64_t n = 0;
@@ -1704,19 +1920,13 @@ StepStats ShuffleJob::run_step(bool validate) {
         const int64_t g = rp.group_recs[i];
         if (g > 0) {
           launch_validate_fixed(out + goff * kTeraRecordBytes, g, vprev + i, has_prev[i] ? 1 : 0, vlast + i, vstats,
-                                s_compute_);
+                                s_compute_, dg + 4 + i);
           HIP_CHECK(hipMemcpyAsync(vprev + i, vlast + i, sizeof(Elem), hipMemcpyDeviceToDevice, s_compute_));
           has_prev[i] = true;
         }
         goff += g;
       }
-      if (W > 1 && verify_n_[q] > 0) {
-        launch_slice_checksums(d_verify_runs_[q].as<RunDesc>(), verify_n_[q], verify_max_nrec_[q],
-                               d_verify_got_.as<unsigned long long>(), s_compute_);
-        launch_count_mismatch(d_verify_got_.as<unsigned long long>(), d_verify_expect_[q].as<unsigned long long>(),
-                              verify_n_[q], vstats + 2, s_compute_);
-      }
-      HIP_CHECK(hipGetLastError());
+      check_inputs(1);
     }
     HIP_CHECK(hipEventRecord(ev[4 * q + 3], s_compute_));
     HIP_CHECK(hipEventRecord(merged_ev_[slot], s_compute_));
@@ -1771,6 +1981,7 @@ StepStats ShuffleJob::run_step(bool validate) {
     st.order_errors = (int64_t)v[0];
     st.checksum = v[1];
     st.exchange_errors = W > 1 ? (int64_t)v[2] : 0;
+    localize_mismatch(st);
   }
   st.bad_layout = merger_->bad_layout();
   if (step_error_) throw std::runtime_error("delivery sink reported error " + std::to_string(step_error_));

@@ -262,6 +262,9 @@ struct ShuffleConfig {
   std::string local_dirs;                // store=disk: comma-separated directories for the MOF files
   bool replan = false;                   // every step recomputes the cell splits and exchanges the counts
   bool map_sort = false;                 // setup: generate unsorted map input and sort it on the device (F8)
+  // validate steps: also checksum every round's merged output right before its D2H (device) and as the
+  // consumer threads receive it (host), per (round, reducer); costs a host hash of every record
+  bool check_delivery = false;
 };
 
 struct StepStats {
@@ -283,6 +286,13 @@ struct StepStats {
   uint64_t checksum = 0;       // validate only: sum of record hashes seen by the device
   int64_t exchange_errors = -1;  // validate only: received slices whose checksum differs from the sender's
   bool bad_layout = false;
+  // validate only, per-round localisation of a checksum mismatch (all counts over the step's rounds):
+  int64_t pre_merge_errors = -1;  // received slices that differed from the sender's right before the merge
+  int64_t own_errors = -1;        // own cells (read in place or staged) that differ from their plan-time checksum
+  int64_t merge_errors = -1;      // (round, reducer) outputs whose checksum differs from the sum of their inputs'
+  int64_t pre_d2h_errors = -1;    // check_delivery: outputs that changed between the merge and their D2H
+  int64_t delivery_errors = -1;   // check_delivery: outputs the consumer received differently from the merge
+  std::string diag;               // the first mismatching (round, reducer) of each kind, "" when all agree
 };
 
 class ShuffleJob {
@@ -363,6 +373,7 @@ class ShuffleJob {
   void copy_loop();
   void consume_loop(int reducer);
   void wait_exchange_ok();
+  void localize_mismatch(StepStats& st);
   // Host-visible address of a run (device address for the HBM store, host address for the host
   // tier); kernels use the device-mapped addresses in d_run_bases_.
   uint8_t* run_base(int m, int d) const { return store_base_ + run_off_[m * cfg_.world + d]; }
@@ -409,6 +420,22 @@ class ShuffleJob {
   std::vector<int> verify_n_;
   std::vector<int64_t> verify_max_nrec_;
   DeviceBuffer d_verify_got_;
+  // validate steps, per round: the own cells the merge reads (in place, or staged into the receive slot)
+  // with their plan-time checksums, the expected checksum of every (round, reducer) output (the sum of
+  // its input slices' plan-time checksums), and the device-side per-round results:
+  //   diag[q * diag_stride() + {0,1,2,3}] = peer-slice mismatches before / after the merge, own-cell
+  //   mismatches before / after; + 4 + i: the checksum of reducer i's merged output
+  std::vector<DeviceBuffer> d_own_runs_, d_own_expect_;
+  std::vector<int> own_n_;
+  std::vector<int64_t> own_max_nrec_;
+  std::vector<uint64_t> expect_group_ck_;  // [q * R + i]
+  DeviceBuffer d_diag_;
+  int diag_stride() const { return 4 + R_; }
+  // check_delivery: per (round, reducer) checksum of the output slot right before its D2H (copy thread)
+  // and of the bytes the consumer threads received
+  std::vector<uint64_t> pre_d2h_ck_, delivered_ck_;
+  bool step_check_delivery_ = false;
+  DeviceBuffer d_d2h_runs_, d_d2h_ck_;
   // pinned-DRAM tier: per-round batched H2D copy descriptors (device), their count and largest size
   std::vector<DeviceBuffer> h2d_descs_;
   std::vector<int> h2d_n_;
@@ -435,6 +462,7 @@ class ShuffleJob {
     int64_t bytes;
     bool last;          // this reducer's final data: append EOF
     double issued_ms;
+    int q;              // round of the bytes (check_delivery)
   };
   std::mutex mu_;
   std::condition_variable cv_;
@@ -458,8 +486,15 @@ class ShuffleJob {
 std::string nccl_unique_id();
 int device_count();
 
+// Streams of finished tasks, kept per (device, priority) for the next task on the current device:
+// creating a stream costs milliseconds and concurrent creations serialize in the runtime (a wave of 15
+// hosted tasks waited up to 106 ms for theirs). A stream handed back may still hold queued work; its
+// next user orders behind it. prewarm_streams() fills the device's pool ahead of a first wave.
+hipStream_t pooled_stream(int priority = 0);
 // UDA_DEVICE_GUARD=1: device buffers freed so far whose guard tail a kernel overwrote
 int64_t device_guard_violations();
+void return_stream(hipStream_t s);
+void prewarm_streams(int device, int n);
 
 }  // namespace gpu
 }  // namespace uda

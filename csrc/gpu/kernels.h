@@ -256,9 +256,10 @@ void launch_frame_streams(const uint8_t* const* ptrs, const int64_t* lens, int n
 // ---------------------------------------------------------------- validation
 // Checks key order of `n` FIXED10 records at `recs` (and against *prev_key if has_prev) and
 // accumulates an order-independent checksum. Results: stats[0] += out-of-order count,
-// stats[1] += checksum. Writes the last key to *last_key.
+// stats[1] += checksum (and *group_ck += checksum when given). Writes the last key to *last_key.
 void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key, int has_prev,
-                           Elem* last_key, unsigned long long* stats, hipStream_t s);
+                           Elem* last_key, unsigned long long* stats, hipStream_t s,
+                           unsigned long long* group_ck = nullptr);
 
 // out[i] = sum of record hashes of FIXED10 slice runs[i] (device array of n RunDesc; out zeroed
 // here). max_nrec sizes the grid.

@@ -386,7 +386,8 @@ __global__ void __launch_bounds__(256) gather_fixed_kernel(const Elem* elems, in
 __global__ void __launch_bounds__(256) validate_fixed_kernel(const uint8_t* recs, int64_t n,
                                                              const Elem* prev_key, int has_prev,
                                                              Elem* last_key,
-                                                             unsigned long long* stats) {
+                                                             unsigned long long* stats,
+                                                             unsigned long long* group_ck) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long bad = 0, h = 0;
   if (i < n) {
@@ -416,6 +417,7 @@ __global__ void __launch_bounds__(256) validate_fixed_kernel(const uint8_t* recs
   if ((threadIdx.x & 63) == 0) {
     if (bad) atomicAdd(stats + 0, bad);
     if (h) atomicAdd(stats + 1, h);
+    if (h && group_ck) atomicAdd(group_ck, h);
   }
 }
 
@@ -499,10 +501,10 @@ void launch_gather_fixed(const Elem* elems, int64_t n, uint8_t* const* run_bases
 }
 
 void launch_validate_fixed(const uint8_t* recs, int64_t n, const Elem* prev_key, int has_prev,
-                           Elem* last_key, unsigned long long* stats, hipStream_t s) {
+                           Elem* last_key, unsigned long long* stats, hipStream_t s, unsigned long long* group_ck) {
   if (n <= 0) return;
   hipLaunchKernelGGL(validate_fixed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                     recs, n, prev_key, has_prev, last_key, stats);
+                     recs, n, prev_key, has_prev, last_key, stats, group_ck);
 }
 
 }  // namespace gpu

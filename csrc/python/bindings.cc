@@ -48,6 +48,13 @@ using namespace uda;
 
 namespace {
 
+struct GpuNoise {  // start_gpu_noise / stop_gpu_noise
+  std::atomic<bool> stop{false};
+  std::thread thr;
+  std::atomic<int64_t> ops{0};
+};
+GpuNoise* g_noise = nullptr;
+
 py::dict stats_to_dict(const gpu::StepStats& s) {
   py::dict d;
   d["wall_ms"] = s.wall_ms;
@@ -68,6 +75,12 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   d["exchange_errors"] = s.exchange_errors;
   d["validated"] = s.validated;
   d["bad_layout"] = s.bad_layout;
+  d["pre_merge_errors"] = s.pre_merge_errors;
+  d["own_errors"] = s.own_errors;
+  d["merge_errors"] = s.merge_errors;
+  d["pre_d2h_errors"] = s.pre_d2h_errors;
+  d["delivery_errors"] = s.delivery_errors;
+  d["diag"] = s.diag;
   return d;
 }
 
@@ -96,6 +109,7 @@ gpu::ShuffleConfig config_from_dict(const py::dict& d) {
   get("local_dirs", c.local_dirs);
   get("replan", c.replan);
   get("map_sort", c.map_sort);
+  get("check_delivery", c.check_delivery);
   return c;
 }
 
@@ -515,6 +529,55 @@ PYBIND11_MODULE(_uda_native, m) {
   // then read round-robin in `chunk` pieces with `depth` reads kept in flight (O_DIRECT), as a loader
   // streams a job's MOF files. Returns GB/s; the files are removed.
   m.def("device_guard_violations", [] { return uda::gpu::device_guard_violations(); });
+  // tests / tools: n idle streams on `device` kept alive until release_idle_streams() (mimics a process
+  // whose pooled streams are alive: they change how new streams map onto the hardware queues)
+  // tests / tools: a thread keeping `streams` extra streams of this process busy with device copies (and
+  // optionally a small kernel) until stop_gpu_noise(): other streams' work sharing the hardware queues
+  m.def("start_gpu_noise", [](int device, int streams, int64_t bytes) {
+    if (g_noise) return;
+    g_noise = new GpuNoise();
+    GpuNoise* nz = g_noise;
+    nz->thr = std::thread([nz, device, streams, bytes] {
+      try {
+        HIP_CHECK(hipSetDevice(device));
+        std::vector<hipStream_t> ss(streams);
+        for (auto& st : ss) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        gpu::DeviceBuffer a((size_t)bytes * streams), b((size_t)bytes * streams);
+        while (!nz->stop.load()) {
+          for (int i = 0; i < streams; ++i)
+            HIP_CHECK(hipMemcpyAsync(b.as<uint8_t>() + (size_t)i * bytes, a.as<uint8_t>() + (size_t)i * bytes,
+                                     (size_t)bytes, hipMemcpyDeviceToDevice, ss[i]));
+          for (auto& st : ss) HIP_CHECK(hipStreamSynchronize(st));
+          nz->ops.fetch_add(streams);
+        }
+        for (auto& st : ss) (void)hipStreamDestroy(st);
+      } catch (const std::exception& e) {
+        UDA_LOG(kError, "gpu noise: %s", e.what());
+      }
+    });
+  });
+  m.def("stop_gpu_noise", [] {
+    if (!g_noise) return (int64_t)0;
+    g_noise->stop = true;
+    {
+      py::gil_scoped_release rel;
+      if (g_noise->thr.joinable()) g_noise->thr.join();
+    }
+    const int64_t n = g_noise->ops.load();
+    delete g_noise;
+    g_noise = nullptr;
+    return n;
+  });
+  m.def("hold_idle_streams", [](int device, int n, int priority) {
+    static std::vector<hipStream_t>& held = *new std::vector<hipStream_t>();
+    HIP_CHECK(hipSetDevice(device));
+    for (int i = 0; i < n; ++i) {
+      hipStream_t s = nullptr;
+      HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+      held.push_back(s);
+    }
+    return (int)held.size();
+  }, py::arg("device"), py::arg("n"), py::arg("priority") = 0);
 
   m.def("aio_interleave_bench", [](const std::string& dir, int files, int64_t file_bytes, int64_t chunk, int depth) {
     py::gil_scoped_release rel;

@@ -91,6 +91,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
   std::vector<std::string> args;  // startNative arguments (HELLO)
   std::atomic<bool> finished{false};  // the runner has returned: the session can be reaped
   pid_t peer_pid = 0;
+  uid_t peer_uid = 0;
   std::thread reader, runner;
 
   Session(MergeService* s, int fd) : svc(s), sock(fd) {}
@@ -230,6 +231,12 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     std::string err;
     if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
     task = std::make_unique<ReduceTask>(opt, host.get());
+    if (peer_uid != ::getuid() && peer_uid != ::geteuid()) {  // a task run for another user: confined
+      TaskSandbox sb;
+      sb.enabled = true;
+      sb.roots = svc->opt_.local_roots;
+      task->set_sandbox(sb);
+    }
   }
 
   // The task's whole life on one thread: start (its constructor pulls configuration, which the reader
@@ -483,6 +490,7 @@ void MergeService::handshake(int fd) {
     return;
   }
   s->peer_pid = pid;
+  s->peer_uid = uid;
   timeval hello_wait{(time_t)opt_.hello_timeout_s, (suseconds_t)((opt_.hello_timeout_s - (time_t)opt_.hello_timeout_s) * 1e6)};
   (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &hello_wait, sizeof(hello_wait));
   uint32_t t;
@@ -518,12 +526,20 @@ void MergeService::handshake(int fd) {
   }
   {
     std::lock_guard<std::mutex> g(mu_);
-    int running = 0;
-    for (auto& x : live_) running += x->finished.load() ? 0 : 1;
-    if (stop_ || running >= opt_.max_sessions) {
+    int running = 0, mine = 0;
+    for (auto& x : live_) {
+      if (x->finished.load()) continue;
+      ++running;
+      mine += x->peer_uid == uid ? 1 : 0;
+    }
+    const bool foreign = uid != ::getuid() && uid != ::geteuid();
+    if (stop_ || running >= opt_.max_sessions || (foreign && mine >= opt_.max_sessions_per_user)) {
       refused_.fetch_add(1);
       send_msg(fd, kRefused, stop_ ? std::string("merge service stopping")
-                                   : "merge service full (" + std::to_string(running) + " hosted tasks)");
+                             : running >= opt_.max_sessions
+                                 ? "merge service full (" + std::to_string(running) + " hosted tasks)"
+                                 : "uid " + std::to_string((int)uid) + " already has " + std::to_string(mine) +
+                                       " hosted tasks");
       return;
     }
     s->token = token;
@@ -678,11 +694,24 @@ struct RemoteReduceTask::Impl {
   std::mutex send_mu;
 };
 
+// The service end of a connection must run as our own user, root, or a user the job names
+// (mapred.uda.gpu.merge.service.server.users): an abstract socket name is open to anyone to bind first.
+static void check_service_peer(int fd, const std::string& path, const std::string& server_users) {
+  uid_t uid = (uid_t)-1;
+  pid_t pid = 0;
+  if (!frame::peer_cred(fd, &uid, &pid)) throw UdaError("merge service " + path + ": no peer credentials");
+  if (uid == 0 || MergeService::user_allowed(server_users, uid)) return;
+  throw UdaError("merge service " + path + " is served by uid " + std::to_string((int)uid) + " (pid " +
+                 std::to_string((int)pid) + "), not a trusted user (mapred.uda.gpu.merge.service.server.users)");
+}
+
 RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<std::string>& args, Host* host)
     : impl_(new Impl) {
   impl_->host = host;
+  const std::string server_users = host->get_conf("mapred.uda.gpu.merge.service.server.users", "");
   impl_->sock = frame::unix_connect(path);
   if (impl_->sock < 0) throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
+  check_service_peer(impl_->sock, path, server_users);
   uint64_t token = 0;
   {
     std::random_device rd;
@@ -696,6 +725,7 @@ RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<st
   }
   if (!send_msg(impl_->sock, kHello, hello)) throw UdaError("merge service " + path + ": HELLO failed");
   impl_->dsock = frame::unix_connect(path);
+  if (impl_->dsock >= 0) check_service_peer(impl_->dsock, path, server_users);
   std::string dh;
   put<uint64_t>(dh, token);
   if (impl_->dsock < 0 || !send_msg(impl_->dsock, kDataHello, dh))

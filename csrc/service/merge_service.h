@@ -22,9 +22,16 @@
 //
 // Transport: one Unix stream socket per reduce task (mapred.uda.gpu.merge.service: "auto" =
 // "@uda-merge-<data port>" in the abstract namespace, any node-local process can reach it; or a path).
-// Access: the peer's uid (SO_PEERCRED) must be the service's own or be listed in
-// mapred.uda.gpu.merge.service.users ("*" = any local user, the default: the provider's TCP port already
-// serves the same map outputs to any client, as the reference's RDMA port does). A session whose
+// Access: the peer's uid (SO_PEERCRED) must be the service's own (the default: YARN without the Linux
+// container executor runs every task as the NodeManager's user) or be listed in
+// mapred.uda.gpu.merge.service.users (user names / uids, or "*" = any local user), at most
+// max.sessions.per.user sessions per foreign uid. A task hosted for a foreign uid is confined
+// (reduce_task.h TaskSandbox): its local dirs must lie inside the node's own local directories
+// (mapred.uda.gpu.merge.service.local.dirs, default yarn.nodemanager.local-dirs / mapred.local.dir), its id
+// may not name a path, and it reads back / unlinks only files this process's user wrote. The client
+// checks the service's uid the same way (the service's own or root, or
+// mapred.uda.gpu.merge.service.server.users), so a process squatting the abstract name never sees a
+// task's configuration or feeds it records. A session whose
 // client disappears stops its task; a client whose service disappears reports a failure to its host
 // (Hadoop then falls back to its vanilla shuffle). A hung client cannot hold up the others: every
 // connection's HELLO is read on a thread of its own, and a configuration pull it does not answer
@@ -52,8 +59,10 @@ class MergeService {
  public:
   struct Options {
     std::string path;          // socket path or "@abstract-name"
-    std::string users = "*";   // allowed client users: "*", or user names / uids separated by ','
+    std::string users;         // allowed client users besides our own: "*", or user names / uids separated by ','
     int max_sessions = 256;    // live hosted tasks; more are refused (the client merges in its own process)
+    int max_sessions_per_user = 64;  // live hosted tasks of one foreign uid
+    std::vector<std::string> local_roots;  // canonical directories a foreign uid's task may use
     double conf_timeout_s = 60;
     double hello_timeout_s = 10;
     // a hosted task ended (its session is over): e.g. drop the references its descriptors hold in the

@@ -12,6 +12,8 @@
 
 #include <atomic>
 #include <cerrno>
+#include <climits>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -77,6 +79,21 @@ std::vector<std::string> split_args(const std::string& s) {
     const size_t e = s.find('\0', b);
     v.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
     if (e == std::string::npos) break;
+    b = e + 1;
+  }
+  return v;
+}
+
+// "a, b,c" -> {"a", "b", "c"} (configuration lists)
+std::vector<std::string> split_list(const std::string& s) {
+  std::vector<std::string> v;
+  for (size_t b = 0; b <= s.size();) {
+    size_t e = s.find(',', b);
+    if (e == std::string::npos) e = s.size();
+    std::string t = s.substr(b, e - b);
+    while (!t.empty() && t.front() == ' ') t.erase(0, 1);
+    while (!t.empty() && t.back() == ' ') t.pop_back();
+    if (!t.empty()) v.push_back(t);
     b = e + 1;
   }
   return v;
@@ -645,8 +662,18 @@ int run_node_daemon(int ctl_fd) {
     if (!svc_path.empty()) {
       MergeService::Options mo;
       mo.path = svc_path;
-      mo.users = d->conf("mapred.uda.gpu.merge.service.users", "*");
+      mo.users = d->conf("mapred.uda.gpu.merge.service.users", "");
       mo.max_sessions = (int)std::atoi(d->conf("mapred.uda.gpu.merge.service.max.sessions", "256").c_str());
+      mo.max_sessions_per_user =
+          (int)std::atoi(d->conf("mapred.uda.gpu.merge.service.max.sessions.per.user", "64").c_str());
+      // where a foreign user's hosted task may keep files: the node's own local directories
+      std::string roots = d->conf("mapred.uda.gpu.merge.service.local.dirs", "");
+      if (roots.empty()) roots = d->conf("yarn.nodemanager.local-dirs", "");
+      if (roots.empty()) roots = d->conf("mapred.local.dir", "");
+      for (const std::string& r : split_list(roots)) {
+        char buf[PATH_MAX];
+        if (::realpath(r.c_str(), buf)) mo.local_roots.emplace_back(buf);
+      }
       mo.conf_timeout_s = std::atof(d->conf("mapred.uda.gpu.merge.service.conf.timeout.s", "60").c_str());
       // a task hosted next to an HBM store fetches device descriptors: no pinned fetch arena to prewarm
       // (15 hosted tasks pinning 1 GB each serialized the first wave in the driver, ~150 ms a task)

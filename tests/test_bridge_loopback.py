@@ -282,3 +282,32 @@ def test_checkpoint_resume_refuses_reexecuted_map(provider, tmp_path, monkeypatc
     recs, st, _ = run_reduce("h", "job_1_0016", ids2, 0, datagen.TEXT, **kw)
     check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
     assert st["restored_lpqs"] == 0 and st["maps_fetched"] == 23
+
+
+def test_checkpoint_and_spills_never_follow_planted_links(provider, tmp_path):
+    """A reduce task's local dirs may be writable by another user (YARN's usercache/<user>/appcache): a
+    checkpoint manifest that is a symlink (or somebody else's file) is not trusted, and LPQ spill files are
+    created fresh, never through a link planted at their names. The files the links point to survive
+    unchanged and the task still merges correctly."""
+    maps = datagen.terasort(num_maps=23, reducers=1, rows_per_map=200, seed=7)
+    job = "job_1_0017"
+    ids = publish(provider, tmp_path, job, maps)
+    d1 = tmp_path / "ld"
+    d1.mkdir()
+    victim = tmp_path / "victim.bin"
+    victim.write_bytes(b"precious" * 100)
+    fake_lpq = tmp_path / "fake.lpq"
+    fake_lpq.write_bytes(b"x" * 64)
+    # a manifest (outside the dir, linked in) naming a file the task would read back and unlink
+    real_manifest = tmp_path / "planted.manifest"
+    real_manifest.write_text(f"lpq 0 64 {fake_lpq} {','.join(ids[:4])}\n")
+    os.symlink(real_manifest, d1 / f"uda.attempt_{job}_r_000000.lpq.manifest")
+    for i in range(5):  # every LPQ spill name of the attempt points at the victim
+        os.symlink(victim, d1 / f"uda.attempt_{job}_r_000000_0.lpq-{i:03d}")
+    kw = dict(approach=2, lpq_size=5, local_dirs=(str(d1),), conf={"mapred.uda.lpq.checkpoint": 1})
+    recs, st, _ = run_reduce("h", job, ids, 0, datagen.TEXT, **kw)
+    check_output(recs, expected(maps, 0, datagen.TEXT), datagen.TEXT)
+    assert st["restored_lpqs"] == 0 and st["maps_fetched"] == 23
+    assert victim.read_bytes() == b"precious" * 100
+    assert fake_lpq.exists() and fake_lpq.read_bytes() == b"x" * 64
+    assert real_manifest.read_text().startswith("lpq 0 64")

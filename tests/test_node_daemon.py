@@ -81,9 +81,10 @@ def _job(tmp_path, job, maps=4, reducers=3, rows=1200, seed=5):
     return str(d), data, ids
 
 
-def _cmds(native, job, ids, r):
+def _cmds(native, job, ids, r, local_dirs=()):
     init = native.form_cmd(INIT, [str(len(ids)), job, f"attempt_{job}_r_{r:06d}_0", "0", str(1 << 20),
-                                  str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0", "0"])
+                                  str(16 << 10), datagen.TEXT, "null", str(256 << 10), "0",
+                                  str(len(local_dirs)), *local_dirs])
     return [init] + [native.form_cmd(FETCH, ["127.0.0.1", job, m, str(r)]) for m in ids]
 
 
@@ -95,8 +96,9 @@ def _task_argv(port, expect, conf=(), exe=EXE):
                    "-m", "1", "-g", "/tmp", "-s", "1024"]
 
 
-def _run_task(native, port, job, ids, r, expect, conf=(), exe=EXE, **popen):
-    p = subprocess.run(_task_argv(port, expect, conf, exe), input="\n".join(_cmds(native, job, ids, r)) + "\n",
+def _run_task(native, port, job, ids, r, expect, conf=(), exe=EXE, local_dirs=(), **popen):
+    p = subprocess.run(_task_argv(port, expect, conf, exe),
+                       input="\n".join(_cmds(native, job, ids, r, local_dirs)) + "\n",
                        capture_output=True, text=True, timeout=120, **popen)
     lines = p.stdout.strip().splitlines()
     assert lines, f"no output, rc={p.returncode}, stderr={p.stderr[-2000:]}"
@@ -261,7 +263,7 @@ def test_merge_service_user_rule(native):
 @pytest.mark.skipif(os.geteuid() != 0, reason="needs root to run a task process as another user")
 def test_merge_service_admits_by_peer_credentials(native, request_cleanup):
     """A task process of a user outside mapred.uda.gpu.merge.service.users is refused (and merges in its
-    own process); listed, it is hosted. Before: a 0600 socket file silently kept other users out."""
+    own process); listed, it is hosted. By default (no key) only the service's own user is hosted."""
     # the task binary, its library and the MOFs where user nobody can read them (pytest's tmp_path is
     # private to root)
     import pathlib
@@ -281,12 +283,13 @@ def test_merge_service_admits_by_peer_credentials(native, request_cleanup):
         os.setgid(65534)
         os.setuid(65534)
 
-    for users, hosted in (("root", False), ("root,nobody", True)):
-        job = f"job_50_00{4 if hosted else 5}"
+    for k, (users, hosted) in enumerate(((None, False), ("root", False), ("root,nobody", True))):
+        job = f"job_50_00{4 + k}"
         sub = tmp_path / job
         sub.mkdir()
         os.chmod(sub, 0o755)
-        fe, data, ids, port = _daemon_front(sub, job, {"mapred.uda.gpu.merge.service.users": users})
+        conf = {} if users is None else {"mapred.uda.gpu.merge.service.users": users}
+        fe, data, ids, port = _daemon_front(sub, job, conf)
         try:
             os.chmod(sub / "mofs", 0o755)
             rc, out = _run_task(native, port, job, ids, 0, _want(data, 0), exe=exe, preexec_fn=as_nobody, cwd="/tmp")
@@ -296,3 +299,89 @@ def test_merge_service_admits_by_peer_credentials(native, request_cleanup):
             assert (ms["refused"] == 0) == hosted, ms
         finally:
             fe.close()
+
+
+def _nobody_app(tmp_path):
+    """The task binary and its library where user nobody can run them."""
+    app = tmp_path / "app"
+    (app / "bin").mkdir(parents=True)
+    (app / "lib").mkdir()
+    shutil.copy2(EXE, app / "bin" / "uda_reduce_task")
+    shutil.copy2(os.path.join(ROOT, "uda_amd", "lib", "libuda.so"), app / "lib" / "libuda.so")
+    for x in (tmp_path, app, app / "bin", app / "lib"):
+        os.chmod(x, 0o755)
+    return str(app / "bin" / "uda_reduce_task")
+
+
+@pytest.mark.skipif(os.geteuid() != 0, reason="needs root to run a task process as another user")
+def test_confined_hosted_task_keeps_to_node_local_dirs(native, request_cleanup):
+    """A task the service hosts for another user: with local dirs inside the node's own
+    (mapred.uda.gpu.merge.service.local.dirs) it is hosted; with a local dir elsewhere the service refuses
+    its files and the task merges in its own process (as that user), and nothing of it lands in the
+    service's name in the foreign dir; a task id naming a path is refused the same way."""
+    import pathlib
+    import tempfile
+    tmp_path = pathlib.Path(tempfile.mkdtemp(prefix="uda-confine-"))
+    request_cleanup.append(tmp_path)
+    exe = _nobody_app(tmp_path)
+    node_dir = tmp_path / "nm-local"
+    elsewhere = tmp_path / "elsewhere"
+    for d in (node_dir, elsewhere):
+        d.mkdir()
+        os.chown(d, 65534, 65534)
+
+    def as_nobody():
+        os.setgid(65534)
+        os.setuid(65534)
+
+    job = "job_50_0020"
+    sub = tmp_path / job
+    sub.mkdir()
+    os.chmod(sub, 0o755)
+    fe, data, ids, port = _daemon_front(sub, job, {"mapred.uda.gpu.merge.service.users": "nobody",
+                                                   "mapred.uda.gpu.merge.service.local.dirs": str(node_dir)})
+    try:
+        os.chmod(sub / "mofs", 0o755)
+        for r, dirs, hosted in ((0, (str(node_dir),), True), (1, (str(elsewhere),), False)):
+            rc, out = _run_task(native, port, job, ids, r, _want(data, r), exe=exe, local_dirs=dirs,
+                                preexec_fn=as_nobody, cwd="/tmp")
+            assert rc == 0 and out["records"] == _want(data, r), out
+            assert (out["task"].get("merge_service") is True) == hosted, (dirs, out["task"])
+        for f in elsewhere.iterdir():  # whatever the in-process task left belongs to its own user
+            assert f.lstat().st_uid == 65534, f
+    finally:
+        fe.close()
+
+
+def test_client_refuses_a_service_of_an_untrusted_user(native, request_cleanup):
+    """The abstract socket name can be bound by anyone first; the client checks the peer's uid before it
+    sends its HELLO: a service run by an untrusted uid is not used and the task merges
+    in its own process."""
+    if os.geteuid() != 0:
+        pytest.skip("needs root to run the service as another user")
+    import pathlib
+    import tempfile
+    tmp_path = pathlib.Path(tempfile.mkdtemp(prefix="uda-squat-"))
+    request_cleanup.append(tmp_path)
+    job = "job_50_0021"
+    mof_dir, data, ids = _job(tmp_path, job)
+    port = _port()
+    fe = FrontEnd(mof_dir, port)  # provider without a daemon: serves bytes
+    squat = None
+    try:
+        # a process of user nobody squats the service name of this port
+        code = ("import socket,os,time\n"
+                "os.setgid(65534); os.setuid(65534)\n"
+                "s=socket.socket(socket.AF_UNIX); s.bind('\\0uda-merge-%d'); s.listen(8)\n"
+                "print('up', flush=True)\n"
+                "c,_=s.accept(); time.sleep(30)\n" % port)
+        squat = subprocess.Popen(["python3", "-c", code], stdout=subprocess.PIPE, text=True)
+        assert squat.stdout.readline().strip() == "up"
+        rc, out = _run_task(native, port, job, ids, 0, _want(data, 0))
+        assert rc == 0 and out["records"] == _want(data, 0), out
+        assert "merge_service" not in out["task"], out["task"]
+    finally:
+        if squat is not None:
+            squat.kill()
+            squat.wait()
+        fe.close()

@@ -54,6 +54,7 @@ class TeraSortConfig:
     local_dirs: str = "/tmp"            # store="disk": comma-separated directories for the MOF files
     replan: bool = False                # every step recomputes the cell splits and exchanges the counts
     map_sort: bool = False              # setup: unsorted map input sorted on the device (F8 radix sort)
+    check_delivery: bool = False        # validate steps: checksum every round output before its D2H and as received
     exchange: str = "ipc"               # world > 1: "ipc" (shared-memory control + hipIpc pulls) or "rccl"
 
 
@@ -72,7 +73,7 @@ class TeraSortShuffle:
             d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
             d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host,
             validate=cfg.validate, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan,
-            map_sort=cfg.map_sort))
+            map_sort=cfg.map_sort, check_delivery=cfg.check_delivery))
         self.sink = n.J2CSink(cfg.reducers, cfg.kv_buf_bytes)
         self.expected_checksum = None
         self.expected_records = None
@@ -203,8 +204,11 @@ def check_stats(stats: dict, expected_records: int, expected_checksum: int, redu
             raise AssertionError(f"{stats['order_errors']} out-of-order records")
         if stats["exchange_errors"] != 0:
             raise AssertionError(f"{stats['exchange_errors']} received slices differ from what their sender sent")
+        for k in ("pre_merge_errors", "own_errors", "merge_errors", "pre_d2h_errors", "delivery_errors"):
+            if stats.get(k, 0) > 0:
+                raise AssertionError(f"{k} {stats[k]}: {stats.get('diag', '')}")
         if stats["checksum"] != expected_checksum:
-            raise AssertionError("checksum mismatch")
+            raise AssertionError("checksum mismatch " + stats.get("diag", ""))
 
 
 def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: str = "local"):
@@ -220,7 +224,7 @@ def make_local_group(world: int, cfg: TeraSortConfig, device: int = 0, group: st
         kv_buf_bytes=cfg.kv_buf_bytes, d2h_piece_bytes=cfg.d2h_piece_bytes, pinned_slots=cfg.pinned_slots,
         d2h_engines=cfg.d2h_engines, d2h=cfg.d2h, deliver_host=cfg.deliver_host, validate=cfg.validate,
         local_group=group, store=cfg.store, local_dirs=cfg.local_dirs, replan=cfg.replan,
-        map_sort=cfg.map_sort))
+        map_sort=cfg.map_sort, check_delivery=cfg.check_delivery))
         for r in range(world)]
     for j in jobs:
         j.init_local()
