@@ -958,6 +958,44 @@ PYBIND11_MODULE(_uda_native, m) {
     if (!err.empty()) throw std::runtime_error("tcp_fetch_probe: " + err);
     return py::make_tuple(total, s, sum);
   });
+  // one TCP client, a fetch to an unreachable host on one thread and, while it is still trying, one to a
+  // live host: returns (live fetch ms, dead host error, dead host ms, second dead fetch ms)
+  m.def("tcp_dead_host_probe", [](const std::string& live, const std::string& dead, int port, const std::string& job,
+                                  const std::string& map, int reduce, int64_t size) {
+    py::gil_scoped_release rel;
+    auto cl = make_tcp_client(port, 256, 4);
+    std::unique_ptr<uint8_t[]> a(new uint8_t[(size_t)std::max<int64_t>(size, 1)]), b(new uint8_t[64]);
+    auto fetch = [&](const std::string& host, uint8_t* dst, int64_t len, std::string* err) {
+      std::mutex m;
+      std::condition_variable cv;
+      bool done = false;
+      FetchRequest rq;
+      rq.job_id = job;
+      rq.map_id = map;
+      rq.reduce_id = reduce;
+      rq.buf_len = len;
+      const auto t0 = std::chrono::steady_clock::now();
+      cl->fetch(host, rq, dst, [&](const FetchAck& k) {
+        std::lock_guard<std::mutex> g(m);
+        if (k.status != 0) *err = k.error.empty() ? "status " + std::to_string(k.status) : k.error;
+        done = true;
+        cv.notify_all();
+      });
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait(lk, [&] { return done; });
+      return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
+    std::string dead_err, live_err, dead2_err;
+    double dead_ms = 0;
+    std::thread t([&] { dead_ms = fetch(dead, b.get(), 64, &dead_err); });
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    const double live_ms = fetch(live, a.get(), size, &live_err);
+    t.join();
+    const double dead2_ms = fetch(dead, b.get(), 64, &dead2_err);
+    cl->close();
+    if (!live_err.empty()) throw std::runtime_error("live host fetch failed: " + live_err);
+    return std::make_tuple(live_ms, dead_err, dead_ms, dead2_ms);
+  });
   m.def("open_ipc_mappings", &gpu::open_ipc_mappings);
   m.def("device_read", [](uint64_t addr, int64_t len) {  // device bytes back to the host (tests)
     std::string out((size_t)len, '\0');

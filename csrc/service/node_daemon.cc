@@ -157,26 +157,45 @@ NodeDaemonClient::NodeDaemonClient(const Options& o, Host* host) : opt_(o), host
 }
 
 NodeDaemonClient::~NodeDaemonClient() {
-  stopping_ = true;
+  {
+    // under mu_: a restart on a reader thread (daemon_gone -> spawn) checks it under the same lock, so
+    // no daemon is started (and no reader_ replaced) from here on
+    std::lock_guard<std::mutex> g(mu_);
+    stopping_ = true;
+    cv_.notify_all();
+  }
   send(kDExit, "");
   const pid_t p = pid_.exchange(0);
   if (p > 0) {
     const std::string how = reap(p, 30);
     UDA_LOG(kInfo, "node daemon pid %d stopped (%s)", (int)p, how.c_str());
   }
+  std::vector<std::thread> readers;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);  // the reader sees EOF
+    if (reader_.joinable()) readers.push_back(std::move(reader_));
+    for (auto& t : old_readers_)
+      if (t.joinable()) readers.push_back(std::move(t));
+    old_readers_.clear();
   }
-  if (reader_.joinable()) reader_.join();
-  for (auto& t : old_readers_)
-    if (t.joinable()) t.join();
+  for (auto& t : readers) t.join();
+  // a daemon a restart published before it saw stopping_ (between the exchange above and now)
+  const pid_t late = pid_.exchange(0);
+  if (late > 0) {
+    ::kill(late, SIGKILL);
+    UDA_LOG(kInfo, "node daemon pid %d (late restart) stopped (%s)", (int)late, reap(late, 5).c_str());
+  }
   std::lock_guard<std::mutex> g(mu_);
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
 }
 
 bool NodeDaemonClient::spawn() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stopping_) return false;
+  }
   int sv[2];
   if (::socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
     std::lock_guard<std::mutex> g(mu_);
@@ -223,7 +242,14 @@ bool NodeDaemonClient::spawn() {
   uint64_t gen;
   {
     std::lock_guard<std::mutex> gs(send_mu_);  // lock order: send_mu_, then mu_ (as in send())
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> g(mu_);
+    if (stopping_) {  // the client is being destroyed: this daemon never serves
+      g.unlock();
+      ::close(sv[0]);
+      ::kill(pid, SIGKILL);
+      (void)reap(pid, 5);
+      return false;
+    }
     if (fd_ >= 0) ::close(fd_);
     fd_ = sv[0];
     gen = ++gen_;

@@ -353,14 +353,22 @@ class TcpClient : public ClientTransport {
 
   void close() override {
     std::vector<std::shared_ptr<Conn>> cs;
+    std::vector<std::thread> hs;
     {
       std::lock_guard<std::mutex> g(mu_);
-      for (auto& kv : conns_)
-        for (auto& c : kv.second)
+      closing_ = true;
+      hs.swap(helpers_);
+    }
+    for (auto& t : hs) t.join();  // background refills (they install under mu_, into retired_ once closed)
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& kv : hosts_)
+        for (auto& c : kv.second.v)
           if (c) cs.push_back(c);
-      conns_.clear();
+      hosts_.clear();
       for (auto& c : retired_) cs.push_back(c);
       retired_.clear();
+      closing_ = false;
     }
     for (auto& c : cs) {
       ::shutdown(c->fd, SHUT_RDWR);
@@ -421,34 +429,103 @@ class TcpClient : public ClientTransport {
     return it == local_servers().end() ? nullptr : it->second;
   }
 
-  // The live connection to host_spec with the fewest requests in flight; the host's connections are
-  // opened on first use, a lost one is reopened when its turn comes.
-  std::shared_ptr<Conn> connect(const std::string& host_spec) {
-    std::lock_guard<std::mutex> g(mu_);
-    auto& v = conns_[host_spec];
-    if (v.empty()) v.resize((size_t)nconn_);
-    std::shared_ptr<Conn> best;
-    size_t best_load = SIZE_MAX;
-    std::string err;
-    for (auto& c : v) {
-      if (!c || c->dead.load()) {
-        if (c && c->reader.joinable()) retired_.push_back(c);  // its reader has failed its requests
-        c.reset();
-        try {
-          c = open_conn(host_spec);
-        } catch (const std::exception& e) {
-          err = e.what();  // another connection of the host may do
-          continue;
-        }
-      }
-      const size_t load = c->inflight.load();
-      if (load < best_load) {
-        best = c;
-        best_load = load;
+  // The host's connection slots. Connections are opened outside mu_ (an unreachable host costs
+  // kReconnectTries tries, ~1.5 s, which must not stall fetches to every other host): one thread at a
+  // time opens a host's missing slots while the others use its live connections or wait for the
+  // outcome; after a failed open the host is in backoff and fetches to it fail at once.
+  struct HostConns {
+    std::vector<std::shared_ptr<Conn>> v;
+    bool connecting = false;
+    std::chrono::steady_clock::time_point backoff_until{};
+    std::string last_err;
+  };
+  static constexpr double kHostBackoffS = 1.0;
+
+  // Open up to `want` connections; stops at the first failure (the host's other slots would fail alike).
+  std::vector<std::shared_ptr<Conn>> open_some(const std::string& host_spec, int want, std::string* err) {
+    std::vector<std::shared_ptr<Conn>> out;
+    for (int k = 0; k < want; ++k) {
+      try {
+        out.push_back(open_conn(host_spec));
+      } catch (const std::exception& e) {
+        *err = e.what();
+        break;
       }
     }
-    if (!best) throw std::runtime_error(err.empty() ? "cannot connect to " + host_spec : err);
-    return best;
+    return out;
+  }
+
+  // Put freshly opened connections into the host's empty slots; record a failure. Under mu_.
+  void install(HostConns& hc, std::vector<std::shared_ptr<Conn>>& got, const std::string& err) {
+    for (auto& c : hc.v)
+      if (!c && !got.empty()) {
+        c = std::move(got.back());
+        got.pop_back();
+      }
+    for (auto& c : got) retired_.push_back(c);  // more than the empty slots (close() raced)
+    hc.connecting = false;
+    if (!err.empty()) {
+      hc.last_err = err;
+      hc.backoff_until = std::chrono::steady_clock::now() +
+                         std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                             std::chrono::duration<double>(kHostBackoffS));
+    }
+    conn_cv_.notify_all();
+  }
+
+  // The live connection to host_spec with the fewest requests in flight.
+  std::shared_ptr<Conn> connect(const std::string& host_spec) {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      HostConns& hc = hosts_[host_spec];
+      if (hc.v.empty()) hc.v.resize((size_t)nconn_);
+      std::shared_ptr<Conn> best;
+      size_t best_load = SIZE_MAX;
+      int missing = 0;
+      for (auto& c : hc.v) {
+        if (c && c->dead.load()) {
+          if (c->reader.joinable()) retired_.push_back(c);  // its reader has failed its requests
+          c.reset();
+        }
+        if (!c) {
+          ++missing;
+          continue;
+        }
+        const size_t load = c->inflight.load();
+        if (load < best_load) {
+          best = c;
+          best_load = load;
+        }
+      }
+      const bool may_open = missing > 0 && !hc.connecting && !closing_ &&
+                            std::chrono::steady_clock::now() >= hc.backoff_until;
+      if (best) {
+        if (may_open) {  // refill lost slots in the background; this fetch takes a live connection
+          hc.connecting = true;
+          helpers_.emplace_back([this, host_spec, missing] {
+            std::string err;
+            auto got = open_some(host_spec, missing, &err);
+            std::lock_guard<std::mutex> g(mu_);
+            install(hosts_[host_spec], got, err);
+          });
+        }
+        return best;
+      }
+      if (may_open) {  // nothing live: this thread opens the host's connections, without mu_
+        hc.connecting = true;
+        lk.unlock();
+        std::string err;
+        auto got = open_some(host_spec, missing, &err);
+        lk.lock();
+        install(hosts_[host_spec], got, err);
+        continue;
+      }
+      if (hc.connecting) {  // another thread is opening them: its outcome is ours
+        conn_cv_.wait(lk);
+        continue;
+      }
+      throw std::runtime_error(hc.last_err.empty() ? "cannot connect to " + host_spec : hc.last_err);
+    }
   }
 
   std::shared_ptr<Conn> open_conn(const std::string& host_spec) {
@@ -538,7 +615,10 @@ class TcpClient : public ClientTransport {
   std::atomic<uint64_t> next_id_{1};
   std::mutex mu_;
   int nconn_;
-  std::unordered_map<std::string, std::vector<std::shared_ptr<Conn>>> conns_;
+  std::unordered_map<std::string, HostConns> hosts_;
+  std::condition_variable conn_cv_;  // a host's open finished
+  std::vector<std::thread> helpers_;  // background refills of lost connection slots (joined at close())
+  bool closing_ = false;
   std::vector<std::shared_ptr<Conn>> retired_;  // lost connections, joined and closed at close()
   std::unordered_map<std::string, std::pair<uint32_t, int>> resolved_;  // host spec -> (IPv4, port)
 };

@@ -249,3 +249,30 @@ def test_tcp_connections_and_by_reference_answers(native, tmp_path):
                 assert tot == sum(sizes) and got == want, (copy, conns, chunk)
         finally:
             p.close()
+
+
+def test_tcp_dead_host_does_not_delay_live_hosts(native, tmp_path):
+    """the TCP client opened a host's connections (5 tries each, ~1.5 s) while holding
+    its client-wide lock, so one unreachable provider stalled every other host's fetches for ~6 s. Now a
+    host's connections open outside the lock: a live host's fetch issued while the dead host is still
+    being tried completes at once, and the dead host, once failed, fails the next fetch at once (backoff)."""
+    import random
+    import socket
+    from uda_amd.bridge import UdaProvider
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    blob = random.Random(3).randbytes(1 << 20)
+    p = UdaProvider(transport="tcp", data_port=port,
+                    conf={"mapred.uda.provider.bind.address": "127.0.0.1", "mapred.uda.daemon": "0"})
+    try:
+        p.add_mof_memory("job_dead", "m0", blob, [(0, len(blob), len(blob))])
+        # nothing listens on 127.0.0.3:<port> (the provider is bound to 127.0.0.1 only): refused at once
+        live_ms, dead_err, dead_ms, dead2_ms = native.tcp_dead_host_probe(
+            "127.0.0.1", f"127.0.0.3:{port}", port, "job_dead", "m0", 0, len(blob))
+        assert dead_err, "the dead host's fetch must fail"
+        assert dead_ms > 1000, dead_ms  # it was really tried (5 tries with backoff)
+        assert live_ms < 500, live_ms   # not held behind those tries
+        assert dead2_ms < 200, dead2_ms  # backoff: fails at once
+    finally:
+        p.close()
