@@ -250,6 +250,7 @@ def main(argv=None) -> int:
 
     bytes_per_gpu = stats[0]["bytes_in"]
     total_bytes = sum(ctx.all_gather_object(bytes_per_gpu))
+    details = ctx.all_gather_object(rank_detail(args, ctx, job, device, stats))
     sent = ctx.all_gather_object(int(sum(s["bytes_sent"] for s in stats) // max(1, len(stats))))
     ms_per_step = elapsed * 1000.0 / max(1, args.steps)
     gbps = total_bytes / (ms_per_step / 1000.0) / 1e9
@@ -307,10 +308,80 @@ def main(argv=None) -> int:
             "ipc_fallback": getattr(job, "ipc_fallback", None),
             "hbm_over_budget_bytes": int(native().hbm_stats(device)["over"]),
             "reference_envelope_gbps_per_node": 5.0,
+            # self-diagnosis of a multi-GPU record: where every rank's threads, rings and bytes went
+            "peer_access": native().peer_access_matrix(),
+            "ipc_preflight": (None if ctx.world == 1 or args.exchange != "ipc" else
+                              "skipped (UDA_IPC_PREFLIGHT=0)" if os.environ.get("UDA_IPC_PREFLIGHT", "1") == "0" else
+                              "passed" if getattr(job, "ipc_fallback", None) is None else "failed"),
+            "ranks_detail": details,
         }
+        out["record_complete"] = record_problems(out) == []
         print(json.dumps(out), flush=True)
     ctx.close()
     return 0
+
+
+RANK_DETAIL_KEYS = {"rank": int, "device": int, "numa_node": int, "consumer_cpus": str, "delivery": str,
+                    "exchange_why": str, "peer_send_bytes": list, "round_comm_ms": list, "round_merge_ms": list,
+                    "wall_ms": float, "comm_ms": float, "merge_ms": float, "d2h_ms": float, "wait_out_ms": float,
+                    "bytes_in": int}
+
+
+def record_problems(out: dict) -> list[str]:
+    """What a multi-GPU record lacks to be diagnosable: one ranks_detail entry per rank with every field
+    of RANK_DETAIL_KEYS, per-peer bytes for every peer, a per-round span for every round, and the
+    peer-access matrix."""
+    probs = []
+    det = out.get("ranks_detail") or []
+    if len(det) != out.get("ranks"):
+        probs.append(f"ranks_detail has {len(det)} entries for {out.get('ranks')} ranks")
+    rounds = (out.get("config") or {}).get("rounds")
+    for d in det:
+        for k, t in RANK_DETAIL_KEYS.items():
+            v = d.get(k)
+            if v is None or not isinstance(v, (int, float) if t is float else t):
+                probs.append(f"rank {d.get('rank')}: {k} missing or not {t.__name__}")
+        if len(d.get("peer_send_bytes") or []) != out.get("ranks"):
+            probs.append(f"rank {d.get('rank')}: peer_send_bytes is not per peer")
+        if rounds and len(d.get("round_merge_ms") or []) != rounds:
+            probs.append(f"rank {d.get('rank')}: round_merge_ms is not per round")
+    if not isinstance(out.get("peer_access"), list):
+        probs.append("peer_access matrix missing")
+    return probs
+
+
+def rank_detail(args, ctx, job, device, stats) -> dict:
+    """One rank's placement and timings for the bench record (rank 0 gathers every rank's): GPU -> NUMA
+    node -> consumer CPU slice, delivery ring / SDMA engines, exchange backend and why, bytes per peer,
+    per-round exchange and merge spans, and the delivery-side waits (d2h, wait_out)."""
+    from uda_amd import native
+    n = len(stats)
+    mean = lambda k: round(sum(s[k] for s in stats) / max(1, n), 2)  # noqa: E731
+    per_round = lambda k: [round(sum(s[k][q] for s in stats) / max(1, n), 2)  # noqa: E731
+                           for q in range(len(stats[0].get(k, [])))]
+    if ctx.world == 1:
+        why = "single GPU: no all-to-all"
+    elif getattr(job, "ipc_fallback", None):
+        why = f"IPC preflight failed, RCCL instead: {job.ipc_fallback}"
+    else:
+        why = f"--exchange {args.exchange}" + (" (default)" if args.exchange == "ipc" else "")
+    d = {"rank": ctx.rank, "device": device}
+    d.update(native().device_placement(device))
+    d.update({
+        "delivery": job.job.delivery_name,  # SDMA engines for D2H / H2D and the pinned ring's NUMA pages
+        "exchange": job.job.exchange_name if ctx.world > 1 else None,
+        "exchange_why": why,
+        "peer_send_bytes": list(job.job.peer_send_bytes()),
+        "round_comm_ms": per_round("round_comm_ms"),
+        "round_merge_ms": per_round("round_merge_ms"),
+        "wall_ms": mean("wall_ms"),
+        "comm_ms": mean("comm_ms"),
+        "merge_ms": mean("merge_ms"),
+        "d2h_ms": mean("d2h_ms"),
+        "wait_out_ms": mean("wait_out_ms"),
+        "bytes_in": stats[0]["bytes_in"],
+    })
+    return d
 
 
 def _free_port() -> int:

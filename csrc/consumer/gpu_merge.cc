@@ -55,6 +55,7 @@
 #include "uda/ifile.h"
 #include "uda/log.h"
 #include "uda/safe_file.h"
+#include "uda/topology.h"
 #include "uda/trace.h"
 
 namespace uda {
@@ -2314,7 +2315,7 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   std::string derr;
   std::thread dthr([&] {
     try {
-      gpu::bind_thread_to_numa(gpu::device_numa_node(device));  // the D2H ring and the consumer copies
+      bind_thread_to_cpus(gpu::device_consumer_cpus(device));  // the D2H ring and the consumer copies
       HIP_CHECK(hipSetDevice(device));
       for (;;) {
         DJob j;

@@ -5,6 +5,7 @@
 #include "merge_plan.h"
 #include "sdma.h"
 #include "uda/fault.h"
+#include "uda/topology.h"
 #include "uda/trace.h"
 
 #include <rccl/rccl.h>
@@ -1351,7 +1352,7 @@ void ShuffleJob::wait_exchange_ok() {
 // Copy thread: merged rounds -> D2H pieces in the pinned ring, per reducer, in round order.
 void ShuffleJob::copy_loop() {
   try {
-    bind_thread_to_numa(sdma_ ? sdma_->numa_node() : device_numa_node(cfg_.device));
+    bind_thread_to_cpus(device_consumer_cpus(cfg_.device));
     HIP_CHECK(hipSetDevice(cfg_.device));
     for (;;) {
       RoundOut r;
@@ -1465,7 +1466,7 @@ void ShuffleJob::copy_loop() {
 // most kv_buf_bytes; the reducer's final buffer carries the IFile EOF marker (-1, -1).
 void ShuffleJob::consume_loop(int i) {
   try {
-    bind_thread_to_numa(sdma_ ? sdma_->numa_node() : device_numa_node(cfg_.device));
+    bind_thread_to_cpus(device_consumer_cpus(cfg_.device));
     HIP_CHECK(hipSetDevice(cfg_.device));
     const int64_t buf_bytes = buf_records_ * kTeraRecordBytes;
     uint8_t* eb = eof_bufs_[i].get();
@@ -1958,6 +1959,8 @@ StepStats ShuffleJob::run_step(bool validate) {
     float a = 0, b = 0;
     if (staged() && hipEventElapsedTime(&a, ev[4 * q + 0], ev[4 * q + 1]) == hipSuccess) st.comm_ms += a;
     if (hipEventElapsedTime(&b, ev[4 * q + 2], ev[4 * q + 3]) == hipSuccess) st.merge_ms += b;
+    st.round_comm_ms.push_back(a);
+    st.round_merge_ms.push_back(b);
   }
   static const bool round_trace = std::getenv("UDA_ROUND_TRACE") != nullptr;  // tools: per-round timeline
   if (round_trace && staged()) {

@@ -293,6 +293,7 @@ struct StepStats {
   int64_t pre_d2h_errors = -1;    // check_delivery: outputs that changed between the merge and their D2H
   int64_t delivery_errors = -1;   // check_delivery: outputs the consumer received differently from the merge
   std::string diag;               // the first mismatching (round, reducer) of each kind, "" when all agree
+  std::vector<double> round_comm_ms, round_merge_ms;  // per round: exchange / merge span (device events)
 };
 
 class ShuffleJob {
@@ -344,6 +345,14 @@ class ShuffleJob {
   }
   int64_t mof_bytes(int m) const { return mof_off_.at(m + 1) - mof_off_.at(m); }
   int64_t max_round_records() const { return max_round_records_; }
+  // bytes this rank sends to each peer per step (self: 0)
+  std::vector<int64_t> peer_send_bytes() const {
+    std::vector<int64_t> v((size_t)cfg_.world, 0);
+    for (const auto& rp : plans_)
+      for (int p = 0; p < (int)rp.send.size() && p < cfg_.world; ++p)
+        for (const auto& sp : rp.send[p]) v[(size_t)p] += sp.bytes;
+    return v;
+  }
   int comm_ranks() const { return exchange_ ? exchange_->comm_ranks() : 1; }
   std::string exchange_name() const { return exchange_ ? exchange_->name() : "none"; }
   std::string delivery_name() const;

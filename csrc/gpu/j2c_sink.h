@@ -376,7 +376,13 @@ class J2CSink {
     if (!threaded_ || !pin_l3_) return;
     const int c = sched_getcpu();
     if (c < 0) return;
-    const std::vector<int> cpus = l3_cpus(c);
+    // within the thread's own placement (a GPU's consumer slice of its NUMA node, uda/topology.h): the
+    // L3 domain is narrowed to it, never widened past it into another GPU's slice
+    cpu_set_t mine;
+    if (pthread_getaffinity_np(pthread_self(), sizeof(mine), &mine) != 0) return;
+    std::vector<int> cpus;
+    for (int x : l3_cpus(c))
+      if (x >= 0 && x < CPU_SETSIZE && CPU_ISSET(x, &mine)) cpus.push_back(x);
     if (cpus.size() < 2) return;
     cpu_set_t set;
     CPU_ZERO(&set);

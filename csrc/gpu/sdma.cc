@@ -1,5 +1,6 @@
 // Explicit SDMA delivery copies and NUMA-local pinned memory. See sdma.h.
 #include "sdma.h"
+#include "uda/topology.h"
 
 #include <hip/hip_runtime.h>
 #include <sched.h>
@@ -121,6 +122,23 @@ int device_numa_node(int device) {
   const std::string s = read_line(path);
   if (s.empty()) return -1;
   return std::atoi(s.c_str());
+}
+
+std::vector<int> device_consumer_cpus(int device) {
+  // the process's CPUs as it started (threads bound later must not narrow the slice of the next one)
+  static const std::vector<int> allowed = allowed_cpus();
+  const PciAddr a = hip_pci(device);
+  if (!a.ok) return {};
+  GpuLocation me;
+  me.domain = a.domain;
+  me.bus = a.bus;
+  me.dev = a.dev;
+  me.func = a.func;
+  me.numa_node = pci_numa_node(a.domain, a.bus, a.dev, a.func);
+  const char* e = std::getenv("UDA_CONSUMER_CPUS");
+  if (e && std::string(e) == "node") return consumer_cpus(me, {me}, allowed);
+  static const std::vector<GpuLocation> gpus = node_gpus();
+  return consumer_cpus(me, gpus, allowed);
 }
 
 void bind_thread_to_numa(int node) {

@@ -85,6 +85,10 @@ class SdmaEngine {
 // CPUs of that node (no-op when unknown). Used for the delivery/consumer threads.
 int device_numa_node(int device);
 void bind_thread_to_numa(int node);
+// The CPUs the host-side consumer threads of `device` run on: its disjoint slice of its NUMA node's CPUs
+// among the node's GPUs (uda/topology.h consumer_cpus); UDA_CONSUMER_CPUS=node: the whole NUMA node
+// (every GPU of the node shares it); empty if the topology is unknown.
+std::vector<int> device_consumer_cpus(int device);
 // Pinned host memory, preferably on NUMA node `node` (< 0: anywhere). Pages are created by the
 // caller's threads, not under the runtime's registration: mmap, MADV_HUGEPAGE, first touch from up to
 // 8 threads, then hipHostRegister (8 x 256 MiB: ~30 ms, against ~400 ms of hipHostMalloc, which zeroes

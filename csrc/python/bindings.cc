@@ -38,6 +38,7 @@
 #include "uda/vint.h"
 #include "uda/shm_group.h"
 #include "uda/node_registry.h"
+#include "uda/topology.h"
 #include "uda/transport.h"
 #include "../gpu/hbm_ledger.h"
 #include <atomic>
@@ -81,6 +82,8 @@ py::dict stats_to_dict(const gpu::StepStats& s) {
   d["pre_d2h_errors"] = s.pre_d2h_errors;
   d["delivery_errors"] = s.delivery_errors;
   d["diag"] = s.diag;
+  d["round_comm_ms"] = s.round_comm_ms;
+  d["round_merge_ms"] = s.round_merge_ms;
   return d;
 }
 
@@ -567,6 +570,44 @@ PYBIND11_MODULE(_uda_native, m) {
     delete g_noise;
     g_noise = nullptr;
     return n;
+  });
+  // node topology (uda/topology.h): every GPU of the node with its NUMA node and consumer CPU slice
+  // (UDA_SYSFS_ROOT lets a test describe any node); `allowed` empty = no affinity restriction
+  m.def("topology_plan", [](const std::vector<int>& allowed) {
+    py::list out;
+    const auto gpus = node_gpus();
+    for (const auto& g : gpus) {
+      py::dict d;
+      d["bdf"] = g.bdf();
+      d["numa_node"] = g.numa_node;
+      d["cpus"] = consumer_cpus(g, gpus, allowed);
+      out.append(d);
+    }
+    return out;
+  }, py::arg("allowed") = std::vector<int>());
+  m.def("format_cpulist", &format_cpulist);
+  m.def("parse_cpulist", &parse_cpulist);
+  // a rank's placement record (bench.py JSON): PCI address, NUMA node, consumer CPU slice
+  m.def("device_placement", [](int device) {
+    py::dict d;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) == hipSuccess) d["pci"] = std::string(bus);
+    d["numa_node"] = gpu::device_numa_node(device);
+    d["consumer_cpus"] = format_cpulist(gpu::device_consumer_cpus(device));
+    return d;
+  });
+  // hipDeviceCanAccessPeer over the visible devices: m[i][j] (diagonal 1)
+  m.def("peer_access_matrix", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    std::vector<std::vector<int>> m2((size_t)n, std::vector<int>((size_t)n, 0));
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        int can = i == j ? 1 : 0;
+        if (i != j && hipDeviceCanAccessPeer(&can, i, j) != hipSuccess) can = -1;
+        m2[(size_t)i][(size_t)j] = can;
+      }
+    return m2;
   });
   m.def("hold_idle_streams", [](int device, int n, int priority) {
     static std::vector<hipStream_t>& held = *new std::vector<hipStream_t>();
@@ -1432,5 +1473,6 @@ PYBIND11_MODULE(_uda_native, m) {
       .def("mof_bytes", &gpu::ShuffleJob::mof_bytes)
       .def_property_readonly("store_bytes", &gpu::ShuffleJob::store_bytes)
       .def_property_readonly("map_sort_ms", &gpu::ShuffleJob::map_sort_ms)
-      .def_property_readonly("max_round_records", &gpu::ShuffleJob::max_round_records);
+      .def_property_readonly("max_round_records", &gpu::ShuffleJob::max_round_records)
+      .def("peer_send_bytes", &gpu::ShuffleJob::peer_send_bytes);
 }
