@@ -28,7 +28,7 @@ struct uda_handle {
   std::unique_ptr<uda::ReduceTask> task;
   std::unique_ptr<uda::RemoteReduceTask> remote;  // NetMerger hosted by the node's merge service
   std::unique_ptr<uda::MergeService> service;     // provider without a node daemon: an explicit in-process service
-  std::shared_ptr<uda::NodeDaemonClient> daemon;  // provider: the node daemon (HBM store + merge service)
+  std::shared_ptr<uda::NodeDaemonSet> daemon;  // provider: the node daemons (HBM store + merge service), one per GPU
   std::string last_error;
   std::mutex mu;
 };
@@ -173,7 +173,19 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
                                           env_log ? env_log
                                                   : (h->opt.log_dir.empty() ? std::string("/tmp") : h->opt.log_dir) +
                                                         "/udaNodeDaemon.log");
-        h->daemon = std::make_shared<uda::NodeDaemonClient>(dopt, h->host.get());
+        // one daemon per GPU (node_daemon.h NodeDaemonSet): a GPU's fault fails its own hosted tasks only,
+        // and every GPU's tasks get their own process (HIP context, hardware queues)
+        uda::NodeDaemonSet::Options so2;
+        so2.daemon = dopt;
+        so2.per_gpu = h->host->conf_bool("mapred.uda.daemon.per.gpu", true);
+        const std::string cnt = h->host->get_conf("mapred.uda.daemon.count", "auto");
+        so2.count = cnt == "auto" ? (so2.per_gpu ? std::max(1, uda::NodeDaemonSet::node_gpu_count()) : 1)
+                                  : std::max(1, std::atoi(cnt.c_str()));
+        std::string svc = h->host->get_conf("mapred.uda.gpu.merge.service", "auto");
+        if (svc == "auto") svc = uda::MergeService::default_path(h->supplier->port());
+        if (svc == "off" || svc == "0" || svc == "false") svc.clear();
+        so2.service_path = svc;
+        h->daemon = std::make_shared<uda::NodeDaemonSet>(so2, h->host.get());
         h->supplier->set_store(h->daemon);
       }
     }

@@ -484,7 +484,7 @@ void ReduceTask::on_init(const InitParams& p_in) {
 }
 
 void ReduceTask::place_on_gpu() {
-  const std::string& conf = device_conf_;
+  const std::string conf = forced_device_ >= 0 ? std::to_string(forced_device_) : device_conf_;
   const std::vector<std::string> keys = gpu::visible_device_keys();
   if (keys.empty()) {
     device_ = 0;  // merge_gpu reports "no HIP device" when the task gets there

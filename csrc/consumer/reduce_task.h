@@ -104,6 +104,8 @@ class ReduceTask {
   ~ReduceTask();
   // before INIT: confine the task's files (merge service, foreign client)
   void set_sandbox(const TaskSandbox& sb) { sandbox_ = sb; }
+  // before INIT: merge on this HIP device whatever mapred.uda.gpu.device says (a per-GPU node daemon)
+  void set_forced_device(int d) { forced_device_ = d; }
   // Downcall from the host. Throws ProtocolError on a malformed/unsupported command.
   void handle(const HadoopCmd& cmd);
   // Close (reduceExitMsg): stop and join the merge thread.
@@ -157,6 +159,7 @@ class ReduceTask {
   void place_on_gpu();
   std::once_flag placed_;
   TaskSandbox sandbox_;
+  int forced_device_ = -1;
   std::string device_conf_ = "auto";   // read on the INIT thread
   std::string fault_spec_;             // mapred.uda.fault.inject (tests: faults of this task only)
   double hbm_budget_conf_ = 0;

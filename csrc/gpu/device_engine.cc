@@ -103,8 +103,10 @@ void DeviceBuffer::alloc_impl(size_t bytes, bool resident, bool exportable) {
   dev_ = dev;
   resident_ = resident;
   guarded_ = guard && held > bytes;
-  if (guarded_)
-    HIP_CHECK(hipMemset(static_cast<uint8_t*>(ptr_) + bytes, kGuardByte, std::min(held - bytes, kGuardBytes)));
+  if (guarded_) {  // complete before any non-blocking stream writes near it
+    HIP_CHECK(hipMemsetAsync(static_cast<uint8_t*>(ptr_) + bytes, kGuardByte, std::min(held - bytes, kGuardBytes), nullptr));
+    HIP_CHECK(hipStreamSynchronize(nullptr));
+  }
 }
 void DeviceBuffer::reset() {
   if (ptr_ && guarded_) {
@@ -331,7 +333,7 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   // the merge-tree buffers (2 x 16 B per record) are allocated on the tree path's first use: the
   // single-pass K-way merge, which takes every group of <= kKwMaxRuns runs, never touches them
   flag_.alloc(sizeof(int));
-  HIP_CHECK(hipMemset(flag_.as(), 0, sizeof(int)));
+  HIP_CHECK(hipMemsetAsync(flag_.as(), 0, sizeof(int), nullptr));
   int passes = 1;
   while ((1 << passes) < max_runs) ++passes;
   ++passes;  // groups that are not a power of two may need one extra copy-through level
@@ -345,7 +347,9 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   if (kw_staged_ && kw_cap_ > 1024) kw_cap_ = 1024;  // a staged cell's records must fit LDS
   if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536, 1792 or 2048");
   kw_overflow_.alloc(sizeof(int));
-  HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
+  HIP_CHECK(hipMemsetAsync(kw_overflow_.as(), 0, sizeof(int), nullptr));
+  // the merges run on non-blocking streams, which do not wait for the null stream
+  HIP_CHECK(hipStreamSynchronize(nullptr));
   slots_.resize(4);
   for (auto& s : slots_) {
     s.host.alloc(slot_bytes_);
@@ -844,7 +848,18 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(d_lo.as(), key_lo.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sp.as(), key_span.data(), nruns * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(d_sd.as(), seeds.data(), nruns * 8, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemset(d_ck.as(), 0, nruns * 8));
+  // on the stream the generation kernels accumulate on: a hipMemset goes to the null stream, which a
+  // non-blocking stream does not wait for, and it returns before the device ran it -- the kernels then
+  // added onto stale bytes or were zeroed midway, and the job's expected checksums came out wrong
+  // (the r5 multi-rank "checksum mismatch" with records, order and every slice correct)
+  static const bool old_memset = [] {  // tools/multirank_stress.py --old-memset: the r5 code, to show the race
+    const char* e = std::getenv("UDA_GEN_NULL_STREAM_MEMSET");
+    return e && std::atoi(e) != 0;
+  }();
+  if (old_memset)
+    HIP_CHECK(hipMemset(d_ck.as(), 0, nruns * 8));
+  else
+    HIP_CHECK(hipMemsetAsync(d_ck.as(), 0, nruns * 8, s_compute_));
   // cfg.map_sort: the map side's own work — each partition is generated unsorted into the sort
   // workspace and the device radix sort (F8) gathers it, sorted, into the store. The checksums are
   // order-independent.
@@ -909,6 +924,7 @@ void ShuffleJob::generate() {
   HIP_CHECK(hipMemcpy(ck.data(), d_ck.as(), nruns * 8, hipMemcpyDeviceToHost));
   dest_checksum_.assign(W, 0);
   dest_records_.assign(W, 0);
+  run_gen_ck_ = ck;
   for (int m = 0; m < M; ++m)
     for (int d = 0; d < W; ++d) {
       dest_checksum_[d] += ck[m * W + d];
@@ -1088,6 +1104,16 @@ void ShuffleJob::compute_plans() {
     if (!exchange_) throw std::runtime_error("world > 1 requires init_comm() or init_local()");
     exchange_->alltoall_i64(send_counts.data(), recv_counts.data(), n_per_peer, s_comm_);
     exchange_->alltoall_i64(send_ck.data(), recv_ck.data(), n_per_peer, s_comm_);
+  }
+  // The generation-time checksum of every run (what a validated step is checked against) must be what
+  // the store holds: a mismatch is a wrong expectation, not a shuffle error. Checked after the
+  // collectives, so a failing rank never leaves its peers waiting in one.
+  for (int r = 0; r < nruns && (size_t)r < run_gen_ck_.size(); ++r) {
+    uint64_t sum = 0;
+    for (int c = 0; c < C_; ++c) sum += (uint64_t)cell_ck[(size_t)r * C_ + c];
+    if (sum != run_gen_ck_[(size_t)r])
+      throw std::runtime_error("plan: map output run " + std::to_string(r) + " of rank " + std::to_string(me) +
+                               " holds records whose checksum differs from the one its generation computed");
   }
   // own cells: this rank's plan-time checksums, whatever the counts exchange carried for the self entry
   for (int q = 0; q < Q_; ++q)

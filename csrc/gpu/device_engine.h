@@ -408,6 +408,7 @@ class ShuffleJob {
   double map_sort_ms_ = 0;
   std::vector<int64_t> mof_off_, run_off_, run_nrec_;  // run index m*W + d
   std::vector<uint64_t> dest_checksum_;
+  std::vector<uint64_t> run_gen_ck_;  // per run: the checksum its generation kernel computed
   std::vector<int64_t> dest_records_;
   std::vector<int64_t> reducer_records_;
   std::vector<uint64_t> bounds_;  // W x (C-1) x 2

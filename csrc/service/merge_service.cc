@@ -231,6 +231,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
     std::string err;
     if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
     task = std::make_unique<ReduceTask>(opt, host.get());
+    if (svc->opt_.force_device >= 0) task->set_forced_device(svc->opt_.force_device);
     if (peer_uid != ::getuid() && peer_uid != ::geteuid()) {  // a task run for another user: confined
       TaskSandbox sb;
       sb.enabled = true;
@@ -248,6 +249,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
       send(kRefused, e.what());
       ::shutdown(sock, SHUT_RDWR);
       finished = true;
+      if (svc->opt_.session_closed) svc->opt_.session_closed(token);
       return;
     }
     send(kReady, "");
@@ -266,6 +268,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
       }
     }
     finished = true;
+    if (svc->opt_.session_closed) svc->opt_.session_closed(token);
   }
 
   void run_commands() {
@@ -364,7 +367,7 @@ MergeService::MergeService(const Options& o) : opt_(o) {
   }
   gpu::set_pinned_shareable(true);
   set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider (if any) without a socket
-  listen_fd_ = frame::unix_listen(opt_.path, 256);
+  if (!opt_.path.empty()) listen_fd_ = frame::unix_listen(opt_.path, 256);
   acceptor_ = std::thread([this] { accept_main(); });
   UDA_LOG(kInfo, "merge service listening on %s (users: %s, max sessions %d)", opt_.path.c_str(), opt_.users.c_str(),
           opt_.max_sessions);
@@ -376,9 +379,9 @@ MergeService::~MergeService() {
     stop_ = true;
     sess_cv_.notify_all();
   }
-  ::shutdown(listen_fd_, SHUT_RDWR);
+  if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
   if (acceptor_.joinable()) acceptor_.join();
-  close(listen_fd_);
+  if (listen_fd_ >= 0) close(listen_fd_);
   if (!opt_.path.empty() && opt_.path[0] != '@') ::unlink(opt_.path.c_str());
   std::map<uint64_t, std::thread> shakes;
   std::vector<std::shared_ptr<Session>> live;
@@ -432,10 +435,25 @@ std::string MergeService::stats_json() const {
          std::to_string(zero_copy_.load()) + ",\"bounced_buffers\":" + std::to_string(bounced_.load()) + "}";
 }
 
+void MergeService::adopt(int fd) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (stop_) {
+    ::close(fd);
+    return;
+  }
+  const uint64_t id = next_shake_++;
+  shakes_[id] = std::thread([this, fd, id] {
+    handshake(fd);
+    std::lock_guard<std::mutex> g2(mu_);
+    shakes_done_.insert(id);
+  });
+}
+
 void MergeService::accept_main() {
   while (!stop_) {
     pollfd pf{listen_fd_, POLLIN, 0};
-    const int pr = ::poll(&pf, 1, 200);
+    // no listener (connections come by adopt()): the loop only reaps finished sessions and handshakes
+    const int pr = listen_fd_ >= 0 ? ::poll(&pf, 1, 200) : (::poll(nullptr, 0, 200), 0);
     {  // reap finished sessions and handshakes
       std::vector<std::thread> done_shakes;
       std::lock_guard<std::mutex> g(mu_);
@@ -480,6 +498,29 @@ void MergeService::accept_main() {
 
 void MergeService::handshake(int fd) {
   auto s = std::make_shared<Session>(this, fd);  // ~Session closes the socket unless it is handed on
+  // a router (session_closed set) counts the sessions it sent here by their HELLO token: every HELLO
+  // that does not become a session reports its end here, a session reports it when its task is over
+  struct Closed {
+    MergeService* m;
+    uint64_t token = 0;
+    bool pending = false;
+    ~Closed() {
+      if (pending && m->opt_.session_closed) m->opt_.session_closed(token);
+    }
+  } closed_guard{this};
+  if (opt_.session_closed) {
+    timeval w{(time_t)opt_.hello_timeout_s, 0};
+    (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &w, sizeof(w));
+    uint8_t head[16];
+    if (::recv(fd, head, sizeof(head), MSG_PEEK | MSG_WAITALL) == (ssize_t)sizeof(head)) {
+      uint32_t ty;
+      std::memcpy(&ty, head, 4);
+      if (ty == kHello) {
+        std::memcpy(&closed_guard.token, head + 8, 8);
+        closed_guard.pending = true;
+      }
+    }
+  }
   uid_t uid = (uid_t)-1;
   pid_t pid = 0;
   if (!frame::peer_cred(fd, &uid, &pid) || !user_allowed(opt_.users, uid)) {
@@ -552,6 +593,7 @@ void MergeService::handshake(int fd) {
     }
     s->reader = std::thread([s] { s->read_loop(); });
     s->runner = std::thread([s] { s->run(); });
+    closed_guard.pending = false;  // the session reports its own end
     live_.push_back(s);
     sess_cv_.notify_all();
   }

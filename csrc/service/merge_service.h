@@ -58,11 +58,14 @@ namespace uda {
 class MergeService {
  public:
   struct Options {
-    std::string path;          // socket path or "@abstract-name"
+    std::string path;          // socket path or "@abstract-name"; "" = no listener (connections come by adopt())
     std::string users;         // allowed client users besides our own: "*", or user names / uids separated by ','
     int max_sessions = 256;    // live hosted tasks; more are refused (the client merges in its own process)
     int max_sessions_per_user = 64;  // live hosted tasks of one foreign uid
     std::vector<std::string> local_roots;  // canonical directories a foreign uid's task may use
+    int force_device = -1;     // >= 0: every hosted task merges on this HIP device (a per-GPU node daemon)
+    // a session is over (its task finished or it was refused): its HELLO token (a router's bookkeeping)
+    std::function<void(uint64_t token)> session_closed;
     double conf_timeout_s = 60;
     double hello_timeout_s = 10;
     // a hosted task ended (its session is over): e.g. drop the references its descriptors hold in the
@@ -80,6 +83,9 @@ class MergeService {
   MergeService(const MergeService&) = delete;
   MergeService& operator=(const MergeService&) = delete;
   const std::string& path() const { return opt_.path; }
+  // A client connection accepted elsewhere (a router that passed its descriptor over SCM_RIGHTS): handled
+  // as if this service had accepted it. Takes ownership of fd.
+  void adopt(int fd);
   int64_t sessions() const { return sessions_.load(); }
   int64_t refused() const { return refused_.load(); }
   int64_t zero_copy_buffers() const { return zero_copy_.load(); }

@@ -18,6 +18,8 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <poll.h>
 #include <thread>
 
 #include "../consumer/reduce_task.h"
@@ -28,6 +30,7 @@
 #include "uda/error.h"
 #include "uda/frame.h"
 #include "uda/log.h"
+#include "uda/topology.h"
 #include "uda/transport.h"
 #include "uda/uda_bridge.h"
 
@@ -54,6 +57,7 @@ enum DMsg : uint32_t {
   kDStats = 6,          // u64 id
   kDExit = 7,
   kDConfReply = 8,  // u32 id, str value
+  kDAdopt = 9,      // + fd: a merge-service client connection the front end's router accepted
   // daemon -> front end
   kDReady = 20,       // str merge service path ("" = none), i64 store bytes
   kDFailed = 21,      // str why
@@ -61,6 +65,7 @@ enum DMsg : uint32_t {
   kDConfReq = 23,     // u32 id, str key, str default
   kDLog = 24,         // i32 severity, str message
   kDStatsReply = 25,  // u64 id, str json
+  kDSessionEnd = 26,  // u64 HELLO token: a routed merge-service session is over (or was refused)
 };
 
 std::string join_args(const std::vector<std::string>& a) {
@@ -262,6 +267,8 @@ bool NodeDaemonClient::spawn() {
   std::string st;
   put_str(st, join_args(opt_.start_args));
   put<int32_t>(st, opt_.data_port);
+  put<int32_t>(st, opt_.device);
+  put<int32_t>(st, opt_.ndaemons);
   send(kDStart, st);
   UDA_LOG(kInfo, "node daemon %s started, pid %d (generation %llu)", opt_.exe.c_str(), (int)pid,
           (unsigned long long)gen);
@@ -356,6 +363,9 @@ void NodeDaemonClient::reader_main(int fd, uint64_t gen) {
       std::lock_guard<std::mutex> g(mu_);
       stats_replies_[id] = get_str(p, &at);
       cv_.notify_all();
+    } else if (t == kDSessionEnd) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen == gen_) sessions_.erase(get<uint64_t>(p, 0));
     }
   }
   daemon_gone(gen, "control connection closed");
@@ -370,6 +380,7 @@ void NodeDaemonClient::daemon_gone(uint64_t gen, const std::string& why) {
     if (gen != gen_) return;
     ready_ = false;
     pending.swap(pending_);
+    sessions_.clear();  // the hosted tasks of that moment are gone with it
     if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
   }
   const pid_t p = pid_.exchange(0);
@@ -415,6 +426,29 @@ bool NodeDaemonClient::acquire(const std::string& job, const std::string& path, 
   if (pending_.erase(id) == 0) return true;  // the daemon-gone path already answered it
   if (why) *why = "node daemon unreachable";
   return false;
+}
+
+bool NodeDaemonClient::adopt(int fd, uint64_t token) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!ready_) return false;
+    if (token) sessions_.insert(token);
+  }
+  std::lock_guard<std::mutex> gs(send_mu_);
+  int cfd;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    cfd = fd_;
+  }
+  if (cfd >= 0 && send_msg(cfd, kDAdopt, "", fd)) return true;
+  std::lock_guard<std::mutex> g(mu_);
+  if (token) sessions_.erase(token);
+  return false;
+}
+
+int NodeDaemonClient::live_sessions() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return (int)sessions_.size();
 }
 
 void NodeDaemonClient::release(const std::string& path, const std::string& holder) {
@@ -529,12 +563,13 @@ struct Daemon {
 
   std::string stats() {
     std::shared_ptr<DeviceStore> st;
+    std::string ms = "{}";
     {
       std::lock_guard<std::mutex> g(mu);
       st = store;
+      if (svc) ms = svc->stats_json();
     }
     std::string s = st ? st->stats_json() : "{}";
-    std::string ms = svc ? svc->stats_json() : "{}";
     char pw[96];
     std::snprintf(pw, sizeof(pw), "\"prewarm\":{\"tasks\":%d,\"done\":%s,\"ms\":%.1f}", prewarm_tasks.load(),
                   prewarm_done.load() ? "true" : "false", (double)prewarm_us.load() / 1e3);
@@ -548,6 +583,14 @@ struct Daemon {
       std::string p;
       int pfd;
       if (!recv_msg(ctl, &t, &p, &pfd)) break;
+      if (t == kDAdopt) {  // a client connection routed to this daemon's merge service
+        std::lock_guard<std::mutex> g(mu);
+        if (svc && pfd >= 0)
+          svc->adopt(pfd);
+        else if (pfd >= 0)
+          ::close(pfd);
+        continue;
+      }
       if (pfd >= 0) ::close(pfd);
       std::shared_ptr<DeviceStore> st;
       {
@@ -643,6 +686,10 @@ int run_node_daemon(int ctl_fd) {
     size_t at = 0;
     const std::vector<std::string> args = split_args(get_str(start, &at));
     const int port = get<int32_t>(start, at);
+    // a per-GPU daemon (node_daemon.h NodeDaemonSet): its GPU, how many daemons the node runs, and the
+    // merge service without a listener of its own (the front end routes client connections to it)
+    const int my_device = start.size() >= at + 8 ? get<int32_t>(start, at + 4) : -1;
+    const int ndaemons = start.size() >= at + 12 ? std::max(1, get<int32_t>(start, at + 8)) : 1;
     NetlevOptions opt;
     std::string err;
     if (!parse_options(args, &opt, &err)) throw UdaError("bad startNative options: " + err);
@@ -657,7 +704,12 @@ int run_node_daemon(int ctl_fd) {
     const double budget = std::atof(d->conf("mapred.uda.gpu.hbm.budget", "0").c_str());
     std::vector<int> devs;
     std::string dconf = d->conf("mapred.uda.provider.hbm.devices", "all");
-    if (dconf == "all") {
+    if (my_device >= 0) {
+      if (!keys.empty() && my_device >= (int)keys.size())
+        throw UdaError("node daemon for GPU " + std::to_string(my_device) + " but " + std::to_string(keys.size()) +
+                       " GPU(s) are visible");
+      if (!keys.empty()) devs.push_back(my_device);
+    } else if (dconf == "all") {
       for (int i = 0; i < (int)keys.size(); ++i) devs.push_back(i);
     } else {
       for (size_t b = 0; b <= dconf.size();) {
@@ -687,7 +739,16 @@ int run_node_daemon(int ctl_fd) {
     if (svc_path == "off" || svc_path == "0" || svc_path == "false") svc_path.clear();
     if (!svc_path.empty()) {
       MergeService::Options mo;
-      mo.path = svc_path;
+      mo.path = my_device >= 0 ? std::string() : svc_path;  // per-GPU: the front end listens and routes
+      if (my_device >= 0) {
+        mo.force_device = my_device;
+        Daemon* dp = d.get();
+        mo.session_closed = [dp](uint64_t token) {
+          std::string m;
+          put<uint64_t>(m, token);
+          (void)dp->send(kDSessionEnd, m);
+        };
+      }
       mo.users = d->conf("mapred.uda.gpu.merge.service.users", "");
       mo.max_sessions = (int)std::atoi(d->conf("mapred.uda.gpu.merge.service.max.sessions", "256").c_str());
       mo.max_sessions_per_user =
@@ -714,7 +775,9 @@ int run_node_daemon(int ctl_fd) {
         // whatever a hosted task's descriptors still hold goes with its session
         if (st) st->release_holder("*", gpu::reducer_holder_id(task));
       };
-      d->svc = std::make_unique<MergeService>(mo);
+      auto svc = std::make_unique<MergeService>(mo);
+      std::lock_guard<std::mutex> g(d->mu);
+      d->svc = std::move(svc);
     }
     // what the first wave of hosted tasks would each build on its critical path (code objects, pooled
     // workspaces, shareable pinned delivery rings), built once after READY, long before the first task
@@ -729,7 +792,8 @@ int run_node_daemon(int ctl_fd) {
     put<int64_t>(ready, store_bytes);
     d->send(kDReady, ready);
     if (warm_tasks > 0) {
-      const int per = (warm_tasks + (int)devs.size() - 1) / (int)devs.size();
+      // the node's first wave spreads over every GPU (and every per-GPU daemon)
+      const int per = (warm_tasks + (int)devs.size() * ndaemons - 1) / ((int)devs.size() * ndaemons);
       d->prewarm_tasks = per * (int)devs.size();
       Daemon* dp = d.get();
       d->prewarm = std::thread([dp, devs, per, rb, kvb] {
@@ -757,7 +821,14 @@ int run_node_daemon(int ctl_fd) {
   }
   // teardown: hosted tasks first (they read the store), then the store
   if (d->prewarm.joinable()) d->prewarm.join();
-  d->svc.reset();
+  {
+    std::unique_ptr<MergeService> svc;
+    {
+      std::lock_guard<std::mutex> g(d->mu);  // the reader adopts connections under it
+      svc.swap(d->svc);
+    }
+    svc.reset();
+  }
   {
     std::shared_ptr<DeviceStore> st;
     {
@@ -771,6 +842,222 @@ int run_node_daemon(int ctl_fd) {
   reader.join();
   ::close(ctl_fd);
   return rc;
+}
+
+}  // namespace uda
+
+namespace uda {
+
+// ============================================================================ one daemon per GPU
+
+namespace {
+// The JSON object (or number) after "key": in `s` ("" if absent). Brace matching: the daemons' stats
+// carry no braces inside strings.
+std::string json_member(const std::string& s, const std::string& key) {
+  const std::string k = "\"" + key + "\":";
+  const size_t at = s.find(k);
+  if (at == std::string::npos) return "";
+  size_t b = at + k.size(), e = b;
+  if (b < s.size() && s[b] == '{') {
+    int depth = 0;
+    for (; e < s.size(); ++e) {
+      if (s[e] == '{') ++depth;
+      if (s[e] == '}' && --depth == 0) {
+        ++e;
+        break;
+      }
+    }
+  } else {
+    while (e < s.size() && s[e] != ',' && s[e] != '}') ++e;
+  }
+  return s.substr(b, e - b);
+}
+int64_t json_int(const std::string& obj, const std::string& key) {
+  const std::string v = json_member(obj, key);
+  return v.empty() ? 0 : std::atoll(v.c_str());
+}
+
+// GPUs of the node as the daemons will number them: the KFD topology's GPU count, or the number of
+// entries of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES when one restricts it. No HIP call: the front
+// end lives in the NodeManager and never initialises a GPU runtime.
+int visible_gpu_count() {
+  int n = (int)node_gpus().size();
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"}) {
+    const char* e = std::getenv(var);
+    if (!e) continue;
+    int k = 0;
+    for (const std::string& t : split_list(e)) k += t.empty() ? 0 : 1;
+    n = n > 0 ? std::min(n, k) : k;
+  }
+  return n;
+}
+}  // namespace
+
+int NodeDaemonSet::node_gpu_count() { return visible_gpu_count(); }
+
+NodeDaemonSet::NodeDaemonSet(const Options& o, Host* host) : opt_(o) {
+  const int n = std::max(1, o.count);
+  // start them together: each pays a HIP runtime start (seconds on a fresh node)
+  std::vector<std::unique_ptr<NodeDaemonClient>> ds((size_t)n);
+  std::vector<std::thread> ts;
+  for (int i = 0; i < n; ++i)
+    ts.emplace_back([&, i] {
+      NodeDaemonClient::Options d = o.daemon;
+      d.device = n > 1 || o.per_gpu ? i : -1;
+      d.ndaemons = n;
+      ds[(size_t)i] = std::make_unique<NodeDaemonClient>(d, host);
+    });
+  for (auto& t : ts) t.join();
+  d_ = std::move(ds);
+  // the node's merge-service name is the front end's: it routes every client connection to the daemon
+  // of the GPU with the fewest live hosted tasks (passing the accepted socket over SCM_RIGHTS)
+  if (!opt_.service_path.empty() && (n > 1 || o.per_gpu)) {
+    try {
+      listen_fd_ = frame::unix_listen(opt_.service_path, 256);
+      router_ = std::thread([this] { route_main(); });
+      UDA_LOG(kInfo, "merge service %s: routing client connections over %d node daemon(s)",
+              opt_.service_path.c_str(), n);
+    } catch (const std::exception& e) {
+      UDA_LOG(kWarn, "merge service %s: cannot listen (%s): reduce tasks merge in their own processes",
+              opt_.service_path.c_str(), e.what());
+    }
+  }
+}
+
+NodeDaemonSet::~NodeDaemonSet() {
+  stop_ = true;
+  if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  if (router_.joinable()) router_.join();
+  if (listen_fd_ >= 0) ::close(listen_fd_);
+  std::vector<std::thread> ts;
+  for (auto& d : d_) ts.emplace_back([&d] { d.reset(); });  // EXIT them together
+  for (auto& t : ts) t.join();
+}
+
+// Accept, wait (poll) for each connection's first frame header + token, hand it to a daemon. A client
+// writes HELLO on its control connection before it opens the data one, so the data connection's token
+// is known by the time its DATA_HELLO is read; a connection that says nothing within 10 s is dropped.
+void NodeDaemonSet::route_main() {
+  struct Pend {
+    int fd;
+    std::chrono::steady_clock::time_point deadline;
+  };
+  std::vector<Pend> pend;
+  std::map<uint64_t, std::pair<size_t, std::chrono::steady_clock::time_point>> data_route;  // token -> daemon
+  while (!stop_) {
+    std::vector<pollfd> pf;
+    pf.push_back(pollfd{listen_fd_, POLLIN, 0});
+    for (auto& p : pend) pf.push_back(pollfd{p.fd, POLLIN, 0});
+    (void)::poll(pf.data(), pf.size(), 200);
+    if (pf[0].revents & POLLIN) {
+      const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+      if (fd >= 0) pend.push_back(Pend{fd, std::chrono::steady_clock::now() + std::chrono::seconds(10)});
+    }
+    const auto now = std::chrono::steady_clock::now();
+    for (auto it = data_route.begin(); it != data_route.end();)  // data connections that never came
+      it = now > it->second.second ? data_route.erase(it) : std::next(it);
+    for (size_t k = 0; k < pend.size();) {
+      uint8_t head[16];
+      const ssize_t r = ::recv(pend[k].fd, head, sizeof(head), MSG_PEEK | MSG_DONTWAIT);
+      bool done = false;
+      if (r == (ssize_t)sizeof(head)) {
+        uint32_t type;
+        uint64_t token;
+        std::memcpy(&type, head, 4);
+        std::memcpy(&token, head + 8, 8);
+        long target = -1;
+        if (type == 1) {  // HELLO: the ready daemon with the fewest live sessions
+          int best = INT32_MAX;
+          for (size_t i = 0; i < d_.size(); ++i)
+            if (d_[i] && d_[i]->ready() && d_[i]->live_sessions() < best) {
+              best = d_[i]->live_sessions();
+              target = (long)i;
+            }
+          if (target >= 0) data_route[token] = {(size_t)target, now + std::chrono::seconds(30)};
+        } else if (type == 6) {  // DATA_HELLO: where its control connection went
+          auto it = data_route.find(token);
+          if (it != data_route.end()) {
+            target = (long)it->second.first;
+            data_route.erase(it);
+          } else if (now < pend[k].deadline) {
+            ++k;  // its HELLO is still being routed
+            continue;
+          }
+        }
+        if (target >= 0 && d_[(size_t)target]->adopt(pend[k].fd, type == 1 ? token : 0)) {
+          routed_++;
+        } else {
+          refused_++;
+        }
+        done = true;
+      } else if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) || now > pend[k].deadline) {
+        done = true;  // gone, broken or silent
+      }
+      if (done) {
+        ::close(pend[k].fd);  // the daemon holds its own copy now (or nobody wants it)
+        pend.erase(pend.begin() + (long)k);
+      } else {
+        ++k;
+      }
+    }
+  }
+  for (auto& p : pend) ::close(p.fd);
+}
+
+size_t NodeDaemonSet::store_of(const std::string& path) const {
+  return d_.size() <= 1 ? 0 : std::hash<std::string>()(path) % d_.size();
+}
+
+bool NodeDaemonSet::acquire(const std::string& job, const std::string& path, const std::string& holder,
+                            int64_t offset, int64_t len, Done done, std::string* why) {
+  return d_[store_of(path)]->acquire(job, path, holder, offset, len, std::move(done), why);
+}
+void NodeDaemonSet::release(const std::string& path, const std::string& holder) {
+  d_[store_of(path)]->release(path, holder);
+}
+void NodeDaemonSet::release_holder(const std::string& job, const std::string& holder) {
+  for (auto& d : d_) d->release_holder(job, holder);
+}
+void NodeDaemonSet::job_over(const std::string& job) {
+  for (auto& d : d_) d->job_over(job);
+}
+
+std::string NodeDaemonSet::stats_json() {
+  std::vector<std::string> js;
+  for (auto& d : d_) js.push_back(d->stats_json());
+  std::string daemons;
+  int64_t sessions = 0, refused = 0, pw_tasks = 0;
+  bool pw_done = true, any_pw = false;
+  for (size_t i = 0; i < js.size(); ++i) {
+    const std::string ms = json_member(js[i], "merge_service"), pw = json_member(js[i], "prewarm");
+    sessions += json_int(ms, "sessions");
+    refused += json_int(ms, "refused");
+    if (!pw.empty()) {
+      any_pw = true;
+      pw_tasks += json_int(pw, "tasks");
+      pw_done = pw_done && json_member(pw, "done") == "true";
+    }
+    const std::string dm = json_member(js[i], "daemon");
+    daemons += (i ? "," : "") + std::string("{\"device\":") + std::to_string(d_[i]->device()) +
+               ",\"live_sessions\":" + std::to_string(d_[i]->live_sessions()) +
+               (dm.size() > 2 ? "," + dm.substr(1, dm.size() - 2) : std::string()) + "}";
+  }
+  std::string routing = "\"router\":{\"path\":\"" + opt_.service_path + "\",\"routed\":" + std::to_string(routed_.load()) +
+                        ",\"refused\":" + std::to_string(refused_.load()) + ",\"listening\":" +
+                        (listen_fd_ >= 0 ? "true" : "false") + "}";
+  if (js.size() == 1) {  // one daemon: its own record, plus the per-daemon list and the router
+    const std::string& b = js[0];
+    return (b.size() > 2 ? b.substr(0, b.size() - 1) + "," : std::string("{")) + "\"daemons\":[" + daemons + "]," +
+           routing + "}";
+  }
+  // several: the node's totals where a caller reads one daemon's fields, and each daemon's full record
+  std::string all;
+  for (size_t i = 0; i < js.size(); ++i) all += (i ? "," : "") + js[i];
+  const std::string d0 = json_member(js[0], "daemon");
+  return "{\"daemon\":" + (d0.empty() ? std::string("{}") : d0) + ",\"merge_service\":{\"path\":\"" +
+         opt_.service_path + "\",\"sessions\":" + std::to_string(sessions) + ",\"refused\":" + std::to_string(refused) +
+         "}" + (any_pw ? ",\"prewarm\":{\"tasks\":" + std::to_string(pw_tasks) + ",\"done\":" + (pw_done ? "true" : "false") + "}" : "") +
+         ",\"daemons\":[" + daemons + "]," + routing + ",\"daemon_stats\":[" + all + "]}";
 }
 
 }  // namespace uda

@@ -33,6 +33,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -53,6 +54,8 @@ class NodeDaemonClient : public DeviceStore {
     double start_timeout_s = 120;          // READY within this (a fresh HIP runtime start included)
     int max_restarts = 3;                  // restarts after the daemon died (0: none)
     std::string log_path;                  // the daemon's stderr ("" = /dev/null; its log goes to LOG frames)
+    int device = -1;                       // >= 0: a per-GPU daemon (store, hosted tasks and prewarm on it)
+    int ndaemons = 1;                      // daemons of the node (the first wave's prewarm is split over them)
   };
   // Spawn the daemon and wait for its READY (or FAILED). Never throws: a daemon that cannot start leaves
   // a client that declines every fetch (ready() false, why() says what happened).
@@ -73,6 +76,12 @@ class NodeDaemonClient : public DeviceStore {
   void release_holder(const std::string& job, const std::string& holder) override;
   void job_over(const std::string& job) override;
   std::string stats_json() override;
+  // Hand a merge-service client connection (accepted by the front end's router) to the daemon's
+  // service; `token` (its HELLO token, 0 for a data connection) counts as a live session until the
+  // daemon reports it over. false: the daemon is not ready (the caller keeps fd).
+  bool adopt(int fd, uint64_t token);
+  int live_sessions() const;
+  int device() const { return opt_.device; }
 
   // The daemon executable next to the loaded libuda.so ("" if none is found).
   static std::string default_exe();
@@ -103,9 +112,58 @@ class NodeDaemonClient : public DeviceStore {
   uint64_t next_id_ = 1;
   std::map<uint64_t, Done> pending_;
   std::map<uint64_t, std::string> stats_replies_;
+  std::set<uint64_t> sessions_;  // routed HELLO tokens whose sessions are live
   std::thread reader_;
   std::vector<std::thread> old_readers_;
   std::mutex send_mu_;
+};
+
+// One node daemon per GPU (mapred.uda.daemon.per.gpu, default on): daemon i holds GPU i's share of the
+// HBM store (MOF files by a hash of their path) and hosts the reduce tasks merging on GPU i, with its own
+// HIP context and hardware queues. A fault on one GPU then fails that GPU's hosted tasks only; the other
+// daemons keep serving and the dead one is restarted (its NodeDaemonClient supervises it).
+// The node's merge-service name (@uda-merge-<port>) is the front end's: a router thread accepts each
+// client connection, peeks its first frame (HELLO / DATA_HELLO + the session token) and passes the
+// socket (SCM_RIGHTS) to the daemon of the GPU with the fewest live hosted tasks -- a task's data
+// connection to the same daemon as its control one. The client is unchanged (merge_service.h); the
+// daemon checks the client's credentials on the passed socket as if it had accepted it.
+class NodeDaemonSet : public DeviceStore {
+ public:
+  struct Options {
+    NodeDaemonClient::Options daemon;
+    int count = 1;             // daemons (one per GPU)
+    bool per_gpu = true;       // count 1 included: the daemon is GPU 0's and the front end routes
+    std::string service_path;  // the node's merge-service name ("" = none)
+  };
+  NodeDaemonSet(const Options& o, Host* host);
+  ~NodeDaemonSet() override;
+  size_t size() const { return d_.size(); }
+  NodeDaemonClient& daemon(size_t i) { return *d_.at(i); }
+  bool ready() const {
+    for (auto& d : d_)
+      if (d && d->ready()) return true;
+    return false;
+  }
+
+  bool acquire(const std::string& job, const std::string& path, const std::string& holder, int64_t offset,
+               int64_t len, Done done, std::string* why) override;
+  void release(const std::string& path, const std::string& holder) override;
+  void release_holder(const std::string& job, const std::string& holder) override;
+  void job_over(const std::string& job) override;
+  std::string stats_json() override;
+
+  // GPUs of the node (KFD topology; HIP_VISIBLE_DEVICES honoured), without initialising HIP.
+  static int node_gpu_count();
+
+ private:
+  void route_main();
+  size_t store_of(const std::string& path) const;
+  Options opt_;
+  std::vector<std::unique_ptr<NodeDaemonClient>> d_;
+  int listen_fd_ = -1;
+  std::thread router_;
+  std::atomic<bool> stop_{false};
+  std::atomic<int64_t> routed_{0}, refused_{0};
 };
 
 // The daemon's main (uda_mof_supplier --daemon-fd N): serve the front end on `ctl_fd` until it says EXIT

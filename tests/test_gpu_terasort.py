@@ -301,3 +301,25 @@ def test_replan_every_step(require_gpu, world, store):
         for d, st in enumerate(stats):
             check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
             assert st["plan_ms"] > 0
+
+
+def test_multirank_schedule_beside_busy_streams(require_gpu, native):
+    """Regression for the r5 multi-rank "checksum mismatch" (records, order and every slice correct): the
+    generation checksums were zeroed by a null-stream hipMemset, which the generation kernels on a
+    non-blocking stream did not wait for. Other streams of the process kept busy with device copies
+    (`start_gpu_noise`, the same queue pressure the per-device stream pool added) made it fail every group
+    after the first; now every fresh group plans (its generation checksums match the store: plan()
+    checks) and validates."""
+    from uda_amd.models.terasort import TeraSortConfig, check_stats, make_local_group, run_collective
+    native.start_gpu_noise(0, 8, 8 << 20)
+    try:
+        for g in range(4):
+            cfg = TeraSortConfig(rows_per_gpu=24000, maps_per_rank=2, rounds=16, reducers=1, validate=True,
+                                 sample_every=64, kv_buf_bytes=64 << 10, d2h_piece_bytes=256 << 10)
+            jobs, ck, rec = make_local_group(8, cfg, group=f"busy{g}")
+            stats = run_collective(jobs, lambda j: j.run_step(True))
+            for d, st in enumerate(stats):
+                check_stats(st, rec[d], ck[d], jobs[d].reducer_records())
+            del jobs
+    finally:
+        assert native.stop_gpu_noise() > 0

@@ -385,3 +385,57 @@ def test_client_refuses_a_service_of_an_untrusted_user(native, request_cleanup):
             squat.kill()
             squat.wait()
         fe.close()
+
+
+def test_per_gpu_daemons_contain_a_daemon_death(native, tmp_path):
+    """one node daemon per GPU (forced to 2 here, no GPU on this machine). The front end
+    routes each reduce task's connections to the daemon with the fewest live sessions: task 0 lands on
+    daemon 0, task 1 on daemon 1. Killing daemon 1 mid-task (as a fault on its GPU would) fails task 1 only;
+    task 0, hosted by daemon 0, delivers its validated stream; daemon 1 is restarted, daemon 0 never was."""
+    job = "job_50_0030"
+    fe, data, ids, port = _daemon_front(tmp_path, job, {"mapred.uda.daemon.count": "2"}, reducers=3)
+    procs = []
+    try:
+        def daemons():
+            return fe.stats()["hbm_store"]["daemons"]
+
+        def wait_for(pred, what, timeout=30):
+            t0 = time.time()
+            while time.time() - t0 < timeout:
+                ds = daemons()
+                if pred(ds):
+                    return ds
+                time.sleep(0.1)
+            raise AssertionError(f"timed out waiting for {what}: {daemons()}")
+
+        ds = wait_for(lambda d: len(d) == 2 and all(x["ready"] for x in d), "two ready daemons")
+        assert [d["device"] for d in ds] == [0, 1] and ds[0]["pid"] != ds[1]["pid"], ds
+        pid0, pid1 = ds[0]["pid"], ds[1]["pid"]
+        cmds = [_cmds(native, job, ids, r) for r in range(2)]
+        for r in range(2):  # INIT + one FETCH each; the rest of task 0's FETCHes come after the kill
+            p = subprocess.Popen(_task_argv(port, _want(data, r)), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                 stderr=subprocess.DEVNULL, text=True)
+            p.stdin.write(cmds[r][0] + "\n" + cmds[r][1] + "\n")
+            p.stdin.flush()
+            procs.append(p)
+            wait_for(lambda d, r=r: d[r]["live_sessions"] == 1, f"task {r} hosted by daemon {r}")
+        os.kill(pid1, signal.SIGKILL)
+        out1, _ = procs[1].communicate(timeout=60)
+        res1 = json.loads(out1.strip().splitlines()[-1])
+        assert procs[1].returncode == 1 and "merge service" in res1["error"], res1
+        procs[0].stdin.write("\n".join(cmds[0][2:]) + "\n")
+        out0, _ = procs[0].communicate(timeout=120)
+        res0 = json.loads(out0.strip().splitlines()[-1])
+        assert procs[0].returncode == 0 and res0["error"] == "" and res0["records"] == _want(data, 0), res0
+        assert res0["task"].get("merge_service") is True, res0["task"]
+        ds = wait_for(lambda d: d[1]["ready"] and d[1]["restarts"] == 1, "daemon 1 restarted")
+        assert ds[0]["pid"] == pid0 and ds[0]["restarts"] == 0, ds
+        assert ds[1]["pid"] not in (0, pid1), ds
+        rc, out = _run_task(native, port, job, ids, 2, _want(data, 2))  # the node keeps hosting tasks
+        assert rc == 0 and out["task"].get("merge_service") is True, out
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        fe.close()

@@ -35,9 +35,13 @@ def main() -> int:
     ap.add_argument("--python-sink", type=int, default=1, help="1: consumers feed Python readers (as the test)")
     ap.add_argument("--check-delivery", type=int, default=1)
     ap.add_argument("--stop-on-fail", type=int, default=0)
+    ap.add_argument("--old-memset", type=int, default=0,
+                    help="1: zero the generation checksums with a null-stream hipMemset (the r5 code) to show the race")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
+    if a.old_memset:
+        os.environ["UDA_GEN_NULL_STREAM_MEMSET"] = "1"
     from uda_amd import native
     from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
     from uda_amd.utils.ifile import J2CQueueReader
@@ -56,7 +60,12 @@ def main() -> int:
         cfg = TeraSortConfig(rows_per_gpu=a.rows_per_map * a.maps, maps_per_rank=a.maps, rounds=a.rounds,
                              reducers=a.reducers, validate=True, sample_every=64, kv_buf_bytes=64 << 10,
                              d2h_piece_bytes=256 << 10, check_delivery=bool(a.check_delivery))
-        jobs, ck, rec = make_local_group(a.world, cfg, group=f"stress{g}")
+        try:
+            jobs, ck, rec = make_local_group(a.world, cfg, group=f"stress{g}")
+        except RuntimeError as e:  # the plan's self-check: generation checksum != store content
+            fails.append({"group": g, "step": -1, "setup_error": str(e)[:300]})
+            print("SETUP FAIL", json.dumps(fails[-1]), flush=True)
+            continue
         if a.python_sink:
             readers = [[J2CQueueReader(max_len=64 << 10) for _ in range(a.reducers)] for _ in range(a.world)]
             for d in range(a.world):
