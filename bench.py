@@ -523,7 +523,26 @@ def _run_waves(args, port, cmds, expected, exe, errlog, conf, sp, statistics):
             eof = o["t_end_boot_ms"] - o["exit_ms"]
             timeline.append([round(x - t_base) for x in (o["t_exec_boot_ms"], ff, ff + o["fetch_to_first_data_ms"],
                                                          eof, o["t_end_boot_ms"])])
+        # which path each task's partitions took: device descriptors of the provider's HBM store, or bytes
+        # (declined by a full store, fetched over TCP and staged); per-path task times
+        paths = {}
+        for o in out.values():
+            t = o["task"]
+            kind = "bytes_and_descriptors" if t.get("host_fetched_bytes", 0) > 0 and t.get("device_descriptors", 0) > 0 \
+                else "bytes_only" if t.get("host_fetched_bytes", 0) > 0 else "descriptors_only"
+            pth = paths.setdefault(kind, {"tasks": 0, "fetch_to_eof_ms": []})
+            pth["tasks"] += 1
+            pth["fetch_to_eof_ms"].append(o["fetch_to_eof_ms"])
+        for pth in paths.values():
+            v = sorted(pth.pop("fetch_to_eof_ms"))
+            pth["fetch_to_eof_ms_median"] = round(v[len(v) // 2], 1)
+            pth["fetch_to_eof_ms_max"] = round(v[-1], 1)
+        split = {"descriptors": sum(int(o["task"].get("device_descriptors", 0)) for o in out.values()),
+                 "bytes_fetched_as_bytes": sum(int(o["task"].get("host_fetched_bytes", 0)) for o in out.values()),
+                 "hbm_wait_ms_max": round(max(float(o["task"].get("hbm_wait_ms", 0)) for o in out.values()), 1),
+                 "paths": paths}
         return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "timeline": timeline,
+                "fetch_split": split,
                 "t_base_boot_ms": t_base,
                 "bytes": sum(o["bytes"] for o in out.values()), "records": sum(o["records"] for o in out.values()),
                 "order_errors": sum(o["order_errors"] for o in out.values()),
@@ -633,7 +652,10 @@ def run_node_files(args, ctx) -> int:
         t_map = time.perf_counter() - t
         port = _free_port()
         t = time.perf_counter()
-        frontend = sp.Popen([sup, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"], stdin=sp.PIPE,
+        fe_conf = []
+        if args.provider_hbm_gb >= 0:  # a store smaller than the map outputs: the mixed regime
+            fe_conf.append(f"-Dmapred.uda.provider.hbm.bytes={int(args.provider_hbm_gb * 1e9)}")
+        frontend = sp.Popen([sup, "mode=frontend", f"mof_dir={mof_dir}", f"port={port}"] + fe_conf, stdin=sp.PIPE,
                             stdout=sp.PIPE, stderr=errlog, text=True, cwd=ROOT,
                             env=dict(os.environ, UDA_DAEMON_LOG=os.path.join(logdir, "node_daemon.err")))
         first = frontend.stdout.readline()
@@ -682,6 +704,10 @@ def run_node_files(args, ctx) -> int:
         out["node_ready_s"] = round(node_ready_s, 2)
         out["daemon_prewarm"] = daemon.get("prewarm")
         out["task0_hosted"] = bool(stats[-1]["task0"].get("merge_service"))
+        out["provider_hbm_gb"] = args.provider_hbm_gb if args.provider_hbm_gb >= 0 else "default"
+        out["fetch_split_first_step"] = waves[0]["fetch_split"]
+        out["fetch_split_last_step"] = stats[-1]["fetch_split"]
+        out["step_gbps"] = [round(w["bytes"] / w["wall_ms"] / 1e6, 2) for w in waves]
         print(json.dumps(out), flush=True)
         return 0
     finally:

@@ -776,6 +776,48 @@ SpillRun index_host_run(uint8_t* p, int64_t len, int64_t spacing) {
   return run;
 }
 
+// index_host_run for a partition that lands in byte phases: walks the complete records of [pos, limit)
+// (the bytes landed so far), a sample every `spacing` bytes; a record the landed bytes cut is left for
+// the next call. Samples go to the caller's vectors; the cursor and the last complete record stay here.
+struct RunCursor {
+  int64_t pos = 0, next_cut = 0;
+  int64_t last = -1;  // start of the last complete record walked
+  bool eof = false;
+  void advance(const uint8_t* p, int64_t limit, int64_t spacing, std::vector<int64_t>* cut, std::vector<std::string>* key) {
+    while (!eof && pos < limit) {
+      while (pos < next_cut && pos + 2 <= limit) {  // one-byte VInt headers: skip without parsing
+        const int8_t k1 = (int8_t)p[pos], v1 = (int8_t)p[pos + 1];
+        if ((k1 | v1) < 0) break;
+        const int64_t nx = pos + 2 + k1 + v1;
+        if (nx > limit) break;
+        last = pos;
+        pos = nx;
+      }
+      if (pos >= limit) break;
+      RecordView rv;
+      const Parse ps = ifile_parse(p + pos, (size_t)(limit - pos), &rv);
+      if (ps == Parse::kEof) {
+        eof = true;
+        break;
+      }
+      if (ps == Parse::kPartial) break;  // the rest of it lands with a later phase
+      if (ps != Parse::kRecord) throw UdaError("hybrid index: bad record in a fetched partition");
+      if (pos >= next_cut) {
+        cut->push_back(pos);
+        key->emplace_back(reinterpret_cast<const char*>(rv.key), (size_t)rv.klen);
+        next_cut = pos + spacing;
+      }
+      last = pos;
+      pos += rv.size();
+    }
+  }
+  std::string last_key(const uint8_t* p) const {
+    RecordView rv;
+    if (last < 0 || ifile_parse(p + last, (size_t)(pos - last), &rv) != Parse::kRecord) return std::string();
+    return std::string(reinterpret_cast<const char*>(rv.key), (size_t)rv.klen);
+  }
+};
+
 }  // namespace
 
 void ReduceTask::release_descriptors(const std::set<std::string>& hosts, const std::string& holder) {
@@ -1043,6 +1085,8 @@ void ReduceTask::merge_gpu() {
   const bool prog_auto = prog_conf < 0;
   StagedCount staged_count(device);
   const bool prog_ok = prog_phases > 1 && stager && stager->sdma() && restored_files_.empty() && !ckpt;
+  // over budget, DRAM tier: phases into pinned DRAM, RPQ rounds of every fully arrived key range (DirectProg)
+  const int pdirect_phases = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.hybrid.progressive.phases", 8));
   bool prog_decided = false, progressive = false;
   struct ProgFetch {
     int P = 0, K = 0;
@@ -1063,6 +1107,40 @@ void ReduceTask::merge_gpu() {
     }
   };
   std::unique_ptr<ProgFetch> prog;
+  // Progressive direct RPQ (mapred.uda.gpu.hybrid.progressive, default on): a task whose input outgrows
+  // the device budget on the DRAM tier fetches every partition in P byte phases into pinned DRAM, and the
+  // fetch threads index each run as its phases land (in order per run). After phase p the key range below
+  // the least last-complete key of the unfinished runs has fully arrived in every run: it is merged in
+  // RPQ rounds (slices H2D, merge, D2H, as the direct RPQ) while later phases still come in. Without it
+  // the RPQ rounds start after the last byte landed (the reference's fetcher-ahead-of-LPQ pipeline,
+  // MergeManager.cc:202-288, is what this recovers).
+  struct DirectProg {
+    int P = 0, K = 0;
+    std::vector<std::shared_ptr<MofFetcher>> f;
+    std::vector<uint8_t*> dst;
+    std::vector<int64_t> cap;
+    std::vector<std::vector<char>> fetched;  // [k][p]
+    std::vector<int> indexed;                // [k]: phases of run k indexed
+    std::vector<char> indexing;              // [k]: a thread is indexing run k
+    std::vector<RunCursor> cur;              // [k]: touched by the thread indexing run k only
+    std::vector<std::vector<int64_t>> cut;   // [k]: samples so far (appended under mu)
+    std::vector<std::vector<std::string>> key;
+    std::vector<int64_t> complete;           // [k]: end of the last complete record indexed
+    std::vector<std::string> last_key;       // [k]: key of that record ("" none yet)
+    std::vector<char> eof;                   // [k]: the partition is indexed to its EOF marker
+    std::vector<int> phase_runs;             // [p]: runs indexed through phase p
+    std::mutex mu;
+    std::condition_variable cv;
+    std::exception_ptr err;
+    std::atomic<int64_t> next{0};
+    std::vector<std::thread> threads;
+    std::chrono::steady_clock::time_point t_end;
+    ~DirectProg() {
+      for (auto& t : threads)
+        if (t.joinable()) t.join();
+    }
+  };
+  std::unique_ptr<DirectProg> dprog;
   const std::string manifest = ckpt ? checkpoint_path() : std::string();
   size_t checkpointed = 0;
   std::vector<std::string> group_ids;  // MOFs of the current group (for the manifest)
@@ -1256,6 +1334,7 @@ void ReduceTask::merge_gpu() {
   const bool direct_ok = tier == "host" && codec_ == Codec::kNone && restored_files_.empty() && !ckpt &&
                          host_->conf_i64("mapred.uda.gpu.hybrid.direct", 1) != 0 &&
                          maps <= host_->conf_i64("mapred.uda.gpu.hybrid.direct.max.runs", 1024);
+  const bool pdirect_ok = direct_ok && pdirect_phases > 1 && host_->conf_i64("mapred.uda.gpu.hybrid.progressive", 1) != 0;
   bool direct = false;
   std::vector<SpillRun> direct_runs;  // one per partition drained after the switch, in `group` order
   auto index_spans = [&](const std::vector<Span>& spans, size_t first, std::vector<SpillRun>* out) {
@@ -1370,12 +1449,100 @@ void ReduceTask::merge_gpu() {
         }
       }
       for (auto& f : to_start) f->start();
-      if (prog_ok && !prog_decided) {
+      if ((prog_ok || pdirect_ok) && !prog_decided) {
         if (drained + (int)ready.size() < maps) continue;  // every partition's length before deciding
         prog_decided = true;
         int64_t tot = 0;
         for (auto& f : ready) tot += std::max<int64_t>(f->part_len(), 0);
-        progressive = drained == 0 && tot <= budget && (!prog_auto || staged_merges(device).load() == 1);
+        progressive = prog_ok && drained == 0 && tot <= budget && (!prog_auto || staged_merges(device).load() == 1);
+        if (!progressive && pdirect_ok && drained == 0 && tot > budget) {
+          {
+            std::lock_guard<std::mutex> g(st_mu_);
+            st_.merge_path = "staged-progressive-direct";
+            st_.hybrid_direct = 1;
+          }
+          if (stager) {  // the partitions never go to HBM whole: RPQ rounds copy their slices
+            stager->release_blocks();
+            stager = nullptr;
+          }
+          dprog = std::make_unique<DirectProg>();
+          DirectProg& dp = *dprog;
+          dp.P = pdirect_phases;
+          dp.K = (int)ready.size();
+          dp.f = ready;
+          for (auto& f : ready) {
+            const int64_t cap = std::max<int64_t>(f->part_len(), 0);
+            dp.cap.push_back(cap);
+            dp.dst.push_back(fill_mem->alloc((size_t)std::max<int64_t>(cap, 1)));
+          }
+          const size_t K = (size_t)dp.K;
+          dp.fetched.assign(K, std::vector<char>((size_t)dp.P, 0));
+          dp.indexed.assign(K, 0);
+          dp.indexing.assign(K, 0);
+          dp.cur.assign(K, RunCursor());
+          dp.cut.assign(K, {});
+          dp.key.assign(K, {});
+          dp.complete.assign(K, 0);
+          dp.last_key.assign(K, std::string());
+          dp.eof.assign(K, 0);
+          dp.phase_runs.assign((size_t)dp.P, 0);
+          auto work = [this, &dp, depth] {
+            for (int64_t i; (i = dp.next++) < (int64_t)dp.P * dp.K;) {
+              {
+                std::lock_guard<std::mutex> g(dp.mu);
+                if (stop_ || dp.err) break;
+              }
+              const int p = (int)(i / dp.K), k = (int)(i % dp.K);
+              try {
+                MofFetcher& f = *dp.f[(size_t)k];
+                const int64_t cap = dp.cap[(size_t)k];
+                const int64_t b = cap * p / dp.P, e = cap * (p + 1) / dp.P;
+                if (p == 0) {
+                  const int64_t off = f.take_first(dp.dst[(size_t)k], cap);
+                  if (off < e) fetch_direct(f.params(), dp.dst[(size_t)k], off, e, depth, nullptr, 0);
+                } else if (b < e) {
+                  fetch_direct(f.params(), dp.dst[(size_t)k], b, e, depth, nullptr, 0);
+                }
+                // index run k through every phase landed in order (one thread per run at a time)
+                std::unique_lock<std::mutex> lk(dp.mu);
+                dp.fetched[(size_t)k][(size_t)p] = 1;
+                while (!dp.indexing[(size_t)k] && dp.indexed[(size_t)k] < dp.P &&
+                       dp.fetched[(size_t)k][(size_t)dp.indexed[(size_t)k]]) {
+                  dp.indexing[(size_t)k] = 1;
+                  const int q = dp.indexed[(size_t)k];
+                  const int64_t limit = cap * (q + 1) / dp.P;
+                  lk.unlock();
+                  std::vector<int64_t> c;
+                  std::vector<std::string> kk;
+                  RunCursor& rc = dp.cur[(size_t)k];
+                  rc.advance(dp.dst[(size_t)k], limit, kSampleSpacing, &c, &kk);
+                  std::string lkey = rc.last_key(dp.dst[(size_t)k]);
+                  lk.lock();
+                  auto& vc = dp.cut[(size_t)k];
+                  auto& vk = dp.key[(size_t)k];
+                  vc.insert(vc.end(), c.begin(), c.end());
+                  for (auto& x : kk) vk.push_back(std::move(x));
+                  dp.complete[(size_t)k] = rc.pos;
+                  if (!lkey.empty()) dp.last_key[(size_t)k] = std::move(lkey);
+                  if (rc.eof || q + 1 == dp.P) dp.eof[(size_t)k] = 1;
+                  dp.indexed[(size_t)k] = q + 1;
+                  dp.indexing[(size_t)k] = 0;
+                  if (++dp.phase_runs[(size_t)q] == dp.K && q + 1 == dp.P) dp.t_end = std::chrono::steady_clock::now();
+                  dp.cv.notify_all();
+                }
+              } catch (...) {
+                std::lock_guard<std::mutex> g(dp.mu);
+                if (!dp.err) dp.err = std::current_exception();
+                dp.cv.notify_all();
+              }
+            }
+          };
+          const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(drains > 0 ? drains : 8, dp.K));
+          for (int w = 0; w < nthreads; ++w) dp.threads.emplace_back(work);
+          drained = maps;
+          ready.clear();
+          continue;
+        }
         if (progressive) {
           {
             std::lock_guard<std::mutex> g(st_mu_);
@@ -1568,7 +1735,195 @@ void ReduceTask::merge_gpu() {
 
     lpq_wait();  // an LPQ of the fetch phase may still be merging
     double prog_fetch_ms = -1;
-    if (progressive) {
+    if (dprog) {
+      DirectProg& dp = *dprog;
+      const int K = dp.K;
+      // merge-owned views of the runs: the landed, indexed prefix of every partition
+      std::vector<SpillRun> runs((size_t)K);
+      for (int k = 0; k < K; ++k) runs[(size_t)k].mem = dp.dst[(size_t)k];
+      std::vector<int64_t> at((size_t)K, 0);  // merged so far (a record boundary)
+      std::vector<size_t> taken((size_t)K, 0);  // samples copied into runs[k]
+      // first record of `run` (indexed prefix) whose key is >= k
+      auto boundary = [&](const SpillRun& run, const std::string& k) -> int64_t {
+        int lo = -1, hi = (int)run.cut.size();
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) / 2;
+          if (cmp_key(kind_, run.key[(size_t)mid], k) < 0)
+            lo = mid;
+          else
+            hi = mid;
+        }
+        if (lo < 0) return 0;
+        const int64_t b = run.cut[(size_t)lo];
+        const int64_t e = (size_t)lo + 1 < run.cut.size() ? run.cut[(size_t)lo + 1] : run.bytes;
+        int64_t p = 0;
+        while (b + p < e) {
+          RecordView rv;
+          if (ifile_parse(run.mem + b + p, (size_t)(e - b - p), &rv) != Parse::kRecord)
+            throw UdaError("progressive hybrid: bad record in an indexed prefix");
+          if (key_compare(kind_, rv.key, rv.klen, reinterpret_cast<const uint8_t*>(k.data()), (int)k.size()) >= 0) break;
+          p += rv.size();
+        }
+        return b + p;
+      };
+      // three workspaces, two rounds prepared ahead (as the direct RPQ below)
+      ws2_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
+      ws2 = ws2_lease.obj.get();
+      ws2->reset_stats();
+      ws3_lease.obj = DevicePool<DeviceWorkspace>::get().acquire(device, [] { return std::make_unique<DeviceWorkspace>(); });
+      ws3 = ws3_lease.obj.get();
+      ws3->reset_stats();
+      StreamGuard sg2, sg3;
+      sg2.s = gpu::pooled_stream();
+      sg3.s = gpu::pooled_stream();
+      DeviceWorkspace* wsv[3] = {&ws, ws2, ws3};
+      hipStream_t sv[3] = {s, sg2.s, sg3.s};
+      // every round is a list of per-run [b, e) slices of the pinned partitions; rounds queue up as the
+      // phases land and the pipeline below takes them in order
+      std::vector<std::vector<std::pair<int64_t, int64_t>>> rounds;
+      bool planned_all = false;
+      const int64_t target = std::max<int64_t>(budget / 2, kSampleSpacing);
+      int epoch = 0;
+      // plan the rounds of every key range that has fully arrived; false while nothing new can be planned
+      auto plan_more = [&](bool wait) -> bool {
+        std::unique_lock<std::mutex> lk(dp.mu);
+        auto ready_epoch = [&] { return epoch < dp.P && dp.phase_runs[(size_t)epoch] == K; };
+        if (wait)
+          while (!dp.cv.wait_for(lk, std::chrono::milliseconds(50), [&] { return ready_epoch() || dp.err || stop_; })) {
+          }
+        if (dp.err) std::rethrow_exception(dp.err);
+        if (stop_) throw UdaError("reduce task stopped during fetch");
+        if (!ready_epoch()) return false;
+        while (ready_epoch()) ++epoch;  // take every phase indexed by now
+        bool all_eof = true, blocked = false;
+        std::string bound;
+        bool have_bound = false;
+        for (int k = 0; k < K; ++k) {
+          SpillRun& r = runs[(size_t)k];
+          auto& vc = dp.cut[(size_t)k];
+          auto& vk = dp.key[(size_t)k];
+          for (size_t j = taken[(size_t)k]; j < vc.size(); ++j) {
+            r.cut.push_back(vc[j]);
+            r.key.push_back(vk[j]);
+          }
+          taken[(size_t)k] = vc.size();
+          r.bytes = dp.complete[(size_t)k];
+          if (dp.eof[(size_t)k]) continue;
+          all_eof = false;
+          if (dp.last_key[(size_t)k].empty()) {
+            blocked = true;  // no complete record of this run yet: nothing below any bound is known
+            continue;
+          }
+          if (!have_bound || cmp_key(kind_, dp.last_key[(size_t)k], bound) < 0) {
+            bound = dp.last_key[(size_t)k];
+            have_bound = true;
+          }
+        }
+        lk.unlock();
+        if (!all_eof && (blocked || !have_bound)) return true;  // wait for more phases
+        std::vector<int64_t> end((size_t)K);
+        for (int k = 0; k < K; ++k)
+          end[(size_t)k] = all_eof ? runs[(size_t)k].bytes : std::max(at[(size_t)k], boundary(runs[(size_t)k], bound));
+        // splitters every ~budget/2 bytes of the range (samples inside it, by key)
+        struct Sample {
+          int run;
+          int idx;
+        };
+        std::vector<Sample> smp;
+        for (int k = 0; k < K; ++k) {
+          const SpillRun& r = runs[(size_t)k];
+          for (int j = 0; j < (int)r.cut.size(); ++j)
+            if (r.cut[(size_t)j] >= at[(size_t)k] && r.cut[(size_t)j] < end[(size_t)k]) smp.push_back({k, j});
+        }
+        std::stable_sort(smp.begin(), smp.end(), [&](const Sample& a, const Sample& b) {
+          const int c = cmp_key(kind_, runs[(size_t)a.run].key[(size_t)a.idx], runs[(size_t)b.run].key[(size_t)b.idx]);
+          return c != 0 ? c < 0 : (a.run != b.run ? a.run < b.run : a.idx < b.idx);
+        });
+        std::vector<std::string> split;
+        int64_t acc = 0;
+        for (const Sample& sm : smp) {
+          const SpillRun& r = runs[(size_t)sm.run];
+          const int64_t nx = std::min(end[(size_t)sm.run], (size_t)sm.idx + 1 < r.cut.size() ? r.cut[(size_t)sm.idx + 1] : r.bytes);
+          if (acc >= target) {
+            const std::string& kk = r.key[(size_t)sm.idx];
+            if (split.empty() || cmp_key(kind_, split.back(), kk) < 0) {
+              split.push_back(kk);
+              acc = 0;
+            }
+          }
+          acc += nx - r.cut[(size_t)sm.idx];
+        }
+        std::vector<std::vector<int64_t>> b((size_t)K);
+        for (int k = 0; k < K; ++k) {
+          b[(size_t)k].push_back(at[(size_t)k]);
+          for (const auto& kk : split)
+            b[(size_t)k].push_back(std::min(end[(size_t)k], std::max(b[(size_t)k].back(), boundary(runs[(size_t)k], kk))));
+          b[(size_t)k].push_back(end[(size_t)k]);
+        }
+        for (size_t q = 0; q + 1 < b[0].size(); ++q) {
+          std::vector<std::pair<int64_t, int64_t>> rr((size_t)K);
+          int64_t bytes = 0;
+          for (int k = 0; k < K; ++k) {
+            rr[(size_t)k] = {b[(size_t)k][q], b[(size_t)k][q + 1]};
+            bytes += rr[(size_t)k].second - rr[(size_t)k].first;
+          }
+          if (bytes > 0 || (all_eof && q + 2 == b[0].size())) rounds.push_back(std::move(rr));
+        }
+        for (int k = 0; k < K; ++k) at[(size_t)k] = end[(size_t)k];
+        if (all_eof) planned_all = true;
+        return true;
+      };
+      auto prep = [&](size_t q) {
+        if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
+        std::vector<Span> views((size_t)K);
+        for (int k = 0; k < K; ++k)
+          views[(size_t)k] = Span{runs[(size_t)k].mem + rounds[q][(size_t)k].first,
+                                  rounds[q][(size_t)k].second - rounds[q][(size_t)k].first};
+        return device_merge(*wsv[q % 3], views, Codec::kNone, kind_, kv, sv[q % 3], nullptr, true);
+      };
+      std::vector<std::future<DeviceMergeOut>> next;
+      size_t issued = 0;
+      auto issue = [&] {  // keep two rounds in preparation ahead of the one being delivered
+        while (issued < rounds.size() && issued < next.size() + 0 + 2 && next.size() < issued + 1) {
+          next.push_back(std::async(std::launch::async, prep, issued));
+          ++issued;
+        }
+      };
+      (void)issue;
+      size_t q = 0;
+      while (!planned_all || q < rounds.size()) {
+        // plan what has arrived (wait only when nothing is queued)
+        while (!planned_all && (q + 2 >= rounds.size())) {
+          const size_t before = rounds.size();
+          if (!plan_more(q >= rounds.size())) break;
+          if (rounds.size() == before && q < rounds.size()) break;
+        }
+        while (next.size() < rounds.size() && next.size() < q + 3) next.push_back(std::async(std::launch::async, prep, next.size()));
+        if (q >= rounds.size()) continue;
+        DeviceMergeOut m = next[q].get();
+        while (next.size() < rounds.size() && next.size() < q + 3) next.push_back(std::async(std::launch::async, prep, next.size()));
+        deliver(m, planned_all && q + 1 == rounds.size(), sv[q % 3], *wsv[q % 3]);
+        ++q;
+      }
+      for (auto& t : dp.threads) t.join();
+      prog_fetch_ms = std::chrono::duration<double, std::milli>(dp.t_end - t0).count();
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.rpq_rounds = (int64_t)rounds.size();
+      }
+      for (int k = 0; k < K; ++k) {
+        progress_count_++;
+        total_count_++;
+        {
+          std::lock_guard<std::mutex> gl(st_mu_);
+          st_.maps_fetched++;
+        }
+        if (progress_count_ == 20 || total_count_ == maps) {
+          host_->fetch_over();
+          progress_count_ = 0;
+        }
+      }
+    } else if (progressive) {
       ProgFetch& pf = *prog;
       const int K = pf.K;
       std::vector<int64_t> start((size_t)K, 0), land((size_t)K, 0);

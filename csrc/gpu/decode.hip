@@ -15,6 +15,8 @@
 // corrupt block sets its status word and the caller raises.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace uda {
@@ -349,6 +351,211 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
   if (!ok && w.lane == 0) atomicOr(status, 1);
 }
 
+// ---- LZO1X, one lane per block (launch_block_decode default for LZO; UDA_LZO_LANE=0: the wave-per-block
+// kernel above). The wave-uniform parse spent ~20 scalar instructions per output byte on TeraSort data:
+// random 10-byte keys and 26-letter values compress into 3-4 byte matches between 1-3 byte literal runs,
+// so a 256 KiB block is ~60K tokens and every token paid the wave's whole scalar parse plus a 64-lane copy
+// for a few bytes. Here each lane runs the state machine of its own block: 64 blocks advance one token
+// per wave step, a token's bytes are copied by its lane (8-byte unaligned moves, a byte loop for the
+// overlapping short-offset matches), and the input is read 8 bytes at a time into a per-lane register.
+// A lane only ever reads back what it wrote itself, so no fence is needed between its copies.
+struct __attribute__((packed, aligned(1))) U64p {
+  uint64_t v;
+};
+
+struct LaneIn {  // the next input bytes of one lane, 8 at a time
+  const uint8_t* in;
+  int64_t end;     // one past the last readable byte of this block
+  int64_t base = -8;
+  uint64_t word = 0;
+  __device__ __forceinline__ uint32_t at(int64_t ip) {
+    const int64_t d = ip - base;
+    if (d < 0 || d >= 8) {
+      base = ip;
+      if (ip + 8 <= end) {
+        word = reinterpret_cast<const U64p*>(in + ip)->v;
+      } else {
+        word = 0;
+        for (int k = 0; k < 8 && ip + k < end; ++k) word |= (uint64_t)in[ip + k] << (8 * k);
+      }
+      return (uint32_t)(word & 0xFF);
+    }
+    return (uint32_t)((word >> (8 * d)) & 0xFF);
+  }
+};
+
+// dst[0, len) = src[0, len), non-overlapping or src >= dst + 8 behind (forward, 8 bytes per move)
+__device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, int64_t len) {
+  int64_t i = 0;
+  for (; i + 8 <= len; i += 8) reinterpret_cast<U64p*>(dst + i)->v = reinterpret_cast<const U64p*>(src + i)->v;
+  for (; i < len; ++i) dst[i] = src[i];
+}
+
+__device__ __forceinline__ void lane_match(uint8_t* out, int64_t op, int64_t off, int64_t len) {
+  if (off >= 8) {
+    lane_copy(out + op, out + op - off, len);
+  } else {
+    for (int64_t i = 0; i < len; ++i) out[op + i] = out[op - off + i];
+  }
+}
+
+// LZO1X chunk of one lane (csrc/codec/lzo.cc semantics, same bounds checks as lzo_chunk).
+__device__ bool lzo_lane_chunk(const uint8_t* in, uint8_t* out, int64_t ip, int64_t ip_end, int64_t op, int64_t oend,
+                               int64_t clip, bool prefix, int64_t* produced) {
+  LaneIn r{in, ip_end};
+  const int64_t out0 = op;
+  int64_t t = 0, next = 0, state = 0, m_pos = 0;
+  bool lit_first = false;
+  if (ip >= ip_end) return false;
+  auto lit = [&](int64_t len) {  // the bytes below the clip
+    const int64_t n = min(len, clip - op);
+    if (n > 0) lane_copy(out + op, in + ip, n);
+  };
+  auto match = [&](int64_t off, int64_t len) {
+    const int64_t n = min(len, clip - op);
+    if (n > 0) lane_match(out, op, off, n);
+  };
+  if (r.at(ip) > 17) {
+    t = (int64_t)r.at(ip) - 17;
+    ++ip;
+    if (t < 4) {
+      next = t;
+      goto match_next;
+    }
+    lit_first = true;
+  }
+  for (;;) {
+    if (prefix && op >= clip) {
+      *produced = oend - out0;
+      return true;
+    }
+    if (lit_first) {
+      lit_first = false;
+      goto copy_literal_run;
+    }
+    if (ip >= ip_end) return false;
+    t = r.at(ip++);
+    if (t < 16) {
+      if (state == 0) {
+        if (t == 0) {
+          for (;;) {
+            if (ip >= ip_end) return false;
+            if (r.at(ip) != 0) break;
+            t += 255;
+            ++ip;
+          }
+          t += 15 + r.at(ip++);
+        }
+        t += 3;
+      copy_literal_run:
+        if (ip + t + 3 > ip_end || op + t > oend) return false;
+        lit(t);
+        op += t;
+        ip += t;
+        state = 4;
+        continue;
+      } else if (state != 4) {  // M1: 2-byte match after 1..3 trailing literals
+        next = t & 3;
+        if (ip >= ip_end) return false;
+        m_pos = op - 1 - (t >> 2) - ((int64_t)r.at(ip++) << 2);
+        if (m_pos < out0 || m_pos >= op || op + 2 > oend) return false;
+        match(op - m_pos, 2);
+        op += 2;
+        goto match_next;
+      } else {  // M1 after a literal run: 3 bytes, offset 2049..3072
+        next = t & 3;
+        if (ip >= ip_end) return false;
+        m_pos = op - (1 + 0x0800) - (t >> 2) - ((int64_t)r.at(ip++) << 2);
+        t = 3;
+      }
+    } else if (t >= 64) {  // M2
+      next = t & 3;
+      if (ip >= ip_end) return false;
+      m_pos = op - 1 - ((t >> 2) & 7) - ((int64_t)r.at(ip++) << 3);
+      t = (t >> 5) - 1 + 2;
+    } else if (t >= 32) {  // M3
+      t = (t & 31) + 2;
+      if (t == 2) {
+        for (;;) {
+          if (ip >= ip_end) return false;
+          if (r.at(ip) != 0) break;
+          t += 255;
+          ++ip;
+        }
+        t += 31 + r.at(ip++);
+      }
+      if (ip + 2 > ip_end) return false;
+      next = (int64_t)r.at(ip) | ((int64_t)r.at(ip + 1) << 8);
+      ip += 2;
+      m_pos = op - 1 - (next >> 2);
+      next &= 3;
+    } else {  // M4 (16..31), or end of stream
+      m_pos = op - ((t & 8) << 11);
+      t = (t & 7) + 2;
+      if (t == 2) {
+        for (;;) {
+          if (ip >= ip_end) return false;
+          if (r.at(ip) != 0) break;
+          t += 255;
+          ++ip;
+        }
+        t += 7 + r.at(ip++);
+      }
+      if (ip + 2 > ip_end) return false;
+      next = (int64_t)r.at(ip) | ((int64_t)r.at(ip + 1) << 8);
+      ip += 2;
+      m_pos -= next >> 2;
+      next &= 3;
+      if (m_pos == op) {
+        *produced = op - out0;
+        return t == 3 && ip == ip_end;
+      }
+      m_pos -= 0x4000;
+    }
+    if (m_pos < out0 || m_pos >= op || op + t > oend) return false;
+    match(op - m_pos, t);
+    op += t;
+  match_next:
+    state = next;
+    t = next;
+    if (ip + t + 3 > ip_end || op + t > oend) return false;
+    lit(t);
+    op += t;
+    ip += t;
+  }
+}
+
+__global__ void __launch_bounds__(256) lzo_lane_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n,
+                                                       int* status, int64_t clip_in) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const DecodeDesc d = descs[b];
+  int64_t ip = d.src, op = d.dst;
+  const int64_t oend = d.dst + d.raw;
+  const bool prefix = clip_in > 0 && clip_in < d.raw;
+  const int64_t clip = prefix ? d.dst + clip_in : oend;
+  bool ok = true;
+  while (ok && op < oend) {
+    if (prefix && op >= clip) return;
+    if (ip + 4 > d.src_end) {
+      ok = false;
+      break;
+    }
+    const int64_t clen = (int64_t)be32(in + ip);
+    ip += 4;
+    if (ip + clen > d.src_end) {
+      ok = false;
+      break;
+    }
+    int64_t produced = 0;
+    ok = lzo_lane_chunk(in, out, ip, ip + clen, op, oend, clip, prefix, &produced);
+    ip += clen;
+    op += produced;
+  }
+  if (ok && (op != oend || ip != d.src_end)) ok = false;
+  if (!ok) atomicOr(status, 1);
+}
+
 }  // namespace
 
 // Framing walk of device-resident block-compressed streams (one lane per stream, following the
@@ -439,8 +646,12 @@ void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const Decod
                          hipStream_t s, int64_t clip) {
   if (n <= 0) return;
   const int grid = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+  const char* le = std::getenv("UDA_LZO_LANE");  // read per launch: tests compare both kernels in one process
+  const bool lzo_lane = !le || std::atoi(le) != 0;
   if (codec == 1)
     block_decode_kernel<1><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+  else if (lzo_lane)
+    lzo_lane_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, out, descs, n, status, clip);
   else
     block_decode_kernel<2><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
 }

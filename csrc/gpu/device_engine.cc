@@ -167,7 +167,8 @@ PinnedPool::Block PinnedPool::acquire(size_t min_bytes) {
   try {
     p = pinned_host_alloc(b.size);
   } catch (const std::exception&) {
-    // trim the cache and retry once
+    // memory the reaper still holds, then the cache: trim and retry once
+    drain_reaper();
     std::multimap<size_t, uint8_t*> drop;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -190,11 +191,51 @@ void PinnedPool::release(Block b) {
   if (!b.p) return;
   std::lock_guard<std::mutex> g(mu_);
   if (cached_ + b.size > cap_) {
-    pinned_host_free(b.p);
+    // unpinning and unmapping GBs takes hundreds of ms (a 41.6 GB over-budget task spent 486 ms closing
+    // on it): a reaper thread does it off the task's path
+    reap_.push_back(b);
+    if (!reaper_started_) {
+      reaper_started_ = true;
+      std::thread([this] { reaper_main(); }).detach();  // the pool is never destroyed
+    }
+    reap_cv_.notify_one();
     return;
   }
   free_.emplace(b.size, b.p);
   cached_ += b.size;
+}
+
+void PinnedPool::reaper_main() {
+  for (;;) {
+    Block b;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      reap_cv_.wait(lk, [&] { return !reap_.empty(); });
+      b = reap_.front();
+      reap_.pop_front();
+      ++reaping_;
+    }
+    pinned_host_free(b.p);
+    std::lock_guard<std::mutex> g(mu_);
+    --reaping_;
+    reap_cv_.notify_all();
+  }
+}
+
+void PinnedPool::drain_reaper() {
+  for (;;) {
+    Block b;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      if (reap_.empty()) {
+        reap_cv_.wait(lk, [&] { return reaping_ == 0 || !reap_.empty(); });
+        if (reap_.empty()) return;
+      }
+      b = reap_.front();
+      reap_.pop_front();
+    }
+    pinned_host_free(b.p);
+  }
 }
 
 void PinnedPool::set_cache_cap(size_t bytes) {
@@ -332,8 +373,13 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
     : max_records_(max_records), max_runs_(max_runs) {
   // the merge-tree buffers (2 x 16 B per record) are allocated on the tree path's first use: the
   // single-pass K-way merge, which takes every group of <= kKwMaxRuns runs, never touches them
+  static const bool old_null = [] {  // tools/multirank_stress.py --old-memset 2: the r5 code here too
+    const char* e = std::getenv("UDA_GEN_NULL_STREAM_MEMSET");
+    return e && std::atoi(e) >= 2;
+  }();
   flag_.alloc(sizeof(int));
-  HIP_CHECK(hipMemsetAsync(flag_.as(), 0, sizeof(int), nullptr));
+  if (old_null) HIP_CHECK(hipMemset(flag_.as(), 0, sizeof(int)));
+  else HIP_CHECK(hipMemsetAsync(flag_.as(), 0, sizeof(int), nullptr));
   int passes = 1;
   while ((1 << passes) < max_runs) ++passes;
   ++passes;  // groups that are not a power of two may need one extra copy-through level
@@ -347,9 +393,13 @@ DeviceMerger::DeviceMerger(int64_t max_records, int max_runs)
   if (kw_staged_ && kw_cap_ > 1024) kw_cap_ = 1024;  // a staged cell's records must fit LDS
   if (!kway_cap_supported(kw_cap_)) throw std::runtime_error("UDA_KWAY_CAP must be 512, 1024, 1536, 1792 or 2048");
   kw_overflow_.alloc(sizeof(int));
-  HIP_CHECK(hipMemsetAsync(kw_overflow_.as(), 0, sizeof(int), nullptr));
-  // the merges run on non-blocking streams, which do not wait for the null stream
-  HIP_CHECK(hipStreamSynchronize(nullptr));
+  if (old_null) {
+    HIP_CHECK(hipMemset(kw_overflow_.as(), 0, sizeof(int)));
+  } else {
+    HIP_CHECK(hipMemsetAsync(kw_overflow_.as(), 0, sizeof(int), nullptr));
+    // the merges run on non-blocking streams, which do not wait for the null stream
+    HIP_CHECK(hipStreamSynchronize(nullptr));
+  }
   slots_.resize(4);
   for (auto& s : slots_) {
     s.host.alloc(slot_bytes_);

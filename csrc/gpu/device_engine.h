@@ -144,9 +144,16 @@ class PinnedPool {
   void release(Block b);
   void set_cache_cap(size_t bytes);
   size_t cached_bytes();
+  // free every block the reaper has not freed yet, on this thread (before retrying a failed allocation)
+  void drain_reaper();
 
  private:
+  void reaper_main();
   std::mutex mu_;
+  std::condition_variable reap_cv_;
+  std::deque<Block> reap_;  // released past the cache cap: freed by the reaper thread
+  bool reaper_started_ = false;
+  int reaping_ = 0;
   std::multimap<size_t, uint8_t*> free_;
   size_t cached_ = 0;
   size_t cap_ = (size_t)32 << 30;

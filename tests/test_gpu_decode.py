@@ -116,3 +116,25 @@ def test_lzo1x_spec_vectors_on_device(require_gpu, native):
     outs, blocks, _ = native.gpu_block_decode("lzo", streams)
     assert blocks == len(VECTORS)
     assert outs == [want for _, _, want in VECTORS]
+
+
+@pytest.mark.parametrize("lane", ["1", "0"], ids=["lane-per-block", "wave-per-block"])
+def test_lzo_kernels_agree_on_terasort_records(require_gpu, native, monkeypatch, lane):
+    """Both LZO device kernels (one lane per block, the default; one wave per block, UDA_LZO_LANE=0)
+    decode TeraSort-shaped IFile records -- random keys, 26-letter values, the many-short-token streams
+    the lane kernel was built for -- and every other payload to the original bytes; a corrupt block is
+    reported by both."""
+    monkeypatch.setenv("UDA_LZO_LANE", lane)
+    tera = datagen.streams(datagen.terasort(2, 1, 6000, seed=5))[0][0]
+    raws = [tera] + [raw for _, raw in _payloads()]
+    for block in (4096, 262144):
+        streams = [native.block_compress(LZO, raw, block) for raw in raws]
+        outs, blocks, _ms = native.gpu_block_decode("lzo", streams)
+        assert blocks == sum((len(r) + block - 1) // block for r in raws)
+        assert all(o == r for o, r in zip(outs, raws))
+    raw = b"abcdefgh" * 4000 + os.urandom(1000)
+    st = bytearray(native.block_compress(LZO, raw, 65536))
+    for i in range(12, min(len(st), 60)):  # a broken back-reference, as test_corrupt_block_raises
+        st[i] = 0xFF
+    with pytest.raises(Exception, match="corrupt|framing"):
+        native.gpu_block_decode("lzo", [bytes(st)])

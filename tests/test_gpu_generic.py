@@ -219,6 +219,46 @@ def test_consumer_gpu_hybrid_lpq_rpq(require_gpu, tmp_path, tier, codec, direct)
         p.close()
 
 
+@pytest.mark.parametrize("workload,phases", [("secondary", 8), ("secondary", 2), ("secondary", 64), ("wordcount", 8),
+                                            ("secondary", 0)])
+def test_consumer_gpu_progressive_direct_rpq(require_gpu, tmp_path, workload, phases):
+    """Over-budget task on the DRAM tier, progressive direct RPQ: the partitions land
+    in byte phases, the fetch threads index each run as its phases arrive, and every key range that has
+    fully arrived in all runs is merged in RPQ rounds while later phases still come in. Equal keys across
+    the phase bounds (wordcount: few distinct words) must not be split or lost; phases=0 turns it off (the
+    plain direct RPQ after the whole fetch)."""
+    from uda_amd.utils.mof import write_mof
+    p = UdaProvider()
+    try:
+        if workload == "secondary":
+            maps = datagen.secondary_sort(num_maps=16, reducers=1, rows_per_map=6000, seed=9)
+        else:
+            maps = datagen.wordcount(num_maps=16, reducers=1, words_per_map=20000, seed=9)
+        job = f"job_pd{workload}{phases}"
+        ids = []
+        for i, parts in enumerate(datagen.streams(maps)):
+            mid = f"attempt_{job}_m_{i:06d}_0"
+            path, _ = write_mof(str(tmp_path), mid, parts)
+            p.add_mof_file(job, mid, path)
+            ids.append(mid)
+        conf = {"mapred.uda.merge.backend": "gpu", "mapred.uda.gpu.merge.bytes": 400_000,
+                "mapred.uda.gpu.spill": "host"}
+        if phases:
+            conf["mapred.uda.gpu.hybrid.progressive.phases"] = phases
+        else:
+            conf["mapred.uda.gpu.hybrid.progressive"] = 0
+        recs, st, c = run_reduce("h", job, ids, 0, datagen.TEXT, conf=conf, kv_buf_size=8192)
+        assert st["hybrid_direct"] == 1 and st["lpqs"] == 0 and st["rpq_rounds"] >= 2, st
+        assert st["merge_path"] == ("staged-progressive-direct" if phases else "staged"), st
+        want = sorted((kv for m in maps for kv in m[0]), key=datagen.sort_key(datagen.TEXT))
+        kf = datagen.sort_key(datagen.TEXT)
+        assert [kf(kv) for kv in recs] == [kf(kv) for kv in want]
+        assert sorted(recs) == sorted(want)
+        assert st["maps_fetched"] == 16
+    finally:
+        p.close()
+
+
 def test_consumer_gpu_hybrid_checkpoint_resume(require_gpu, tmp_path, monkeypatch):
     """mapred.uda.lpq.checkpoint with the GPU hybrid merge (disk tier): attempt 0 fails after its
     2nd LPQ spill; attempt 1 restores both spills (data + sparse index), fetches only the other MOFs

@@ -121,6 +121,26 @@ RECIPES: dict[str, tuple[int, str]] = {
     "pmc_lzo41": (300, "timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY "
                        "SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d gpurun_out/pmc_lzo41 -o run -- "
                        "python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 --steps 1 --warmup 0"),
+    # round 6
+    "pd_tests": (400, f"{PY} -m pytest tests/test_gpu_generic.py -m gpu -x -v --timeout 170 --timeout-method thread "
+                      f"-k 'progressive_direct or hybrid_lpq_rpq or hybrid_checkpoint'"),
+    "hybrid41b_s2": (700, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000 "
+                          f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "hybrid41b_noprog": (700, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000,mapred.uda.gpu.hybrid.progressive=0 "
+                              f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "nodefiles62_store20": (1100, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 600000000 "
+                                  f"--provider-hbm-gb 20 --steps 3 --warmup 1"),
+    "decode_tests": (300, f"{PY} -m pytest tests/test_gpu_decode.py -m gpu -x -v --timeout 170 --timeout-method thread"),
+    "lzo130x5_wave": (600, f"UDA_LZO_LANE=0 {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1 --verbose"),
+    "pmc_lzo41_wave": (300, "UDA_LZO_LANE=0 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS "
+                            "SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv "
+                            "-d gpurun_out/pmc_lzo41_wave -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
+                            "--steps 1 --warmup 0"),
+    "prof_lzo41_lane": (500, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lzo41_lane -o run -- "
+                             "python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "prof_lzo41_wave": (500, "UDA_LZO_LANE=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lzo41_wave "
+                             "-o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "ipc8_detail": (700, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }

@@ -36,12 +36,13 @@ def main() -> int:
     ap.add_argument("--check-delivery", type=int, default=1)
     ap.add_argument("--stop-on-fail", type=int, default=0)
     ap.add_argument("--old-memset", type=int, default=0,
-                    help="1: zero the generation checksums with a null-stream hipMemset (the r5 code) to show the race")
+                    help="1: zero the generation checksums with a null-stream hipMemset (the r5 code) to show the race; "
+                         "2: also the DeviceMerger's null-stream memsets without the stream sync (r5 exactly)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
     if a.old_memset:
-        os.environ["UDA_GEN_NULL_STREAM_MEMSET"] = "1"
+        os.environ["UDA_GEN_NULL_STREAM_MEMSET"] = str(a.old_memset)
     from uda_amd import native
     from uda_amd.models.terasort import TeraSortConfig, make_local_group, run_collective
     from uda_amd.utils.ifile import J2CQueueReader
