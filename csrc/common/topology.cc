@@ -2,6 +2,8 @@
 #include "uda/topology.h"
 
 #include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <sched.h>
 
@@ -83,11 +85,13 @@ std::vector<GpuLocation> node_gpus() {
     std::string k;
     uint64_t v = 0;
     uint64_t simd = 0, loc = 0, dom = 0;
+    int64_t minor = -1;
     bool has_loc = false;
     while (f >> k >> v) {
       if (k == "simd_count") simd = v;
       else if (k == "location_id") loc = v, has_loc = true;
       else if (k == "domain") dom = v;
+      else if (k == "drm_render_minor") minor = (int64_t)v;
     }
     if (simd == 0 || !has_loc) continue;  // a CPU node
     GpuLocation g;
@@ -96,12 +100,28 @@ std::vector<GpuLocation> node_gpus() {
     g.dev = (uint32_t)(loc >> 3) & 0x1F;
     g.func = (uint32_t)loc & 0x7;
     g.numa_node = pci_numa_node(g.domain, g.bus, g.dev, g.func);
+    g.render_minor = (int)minor;
     out.push_back(g);
   }
   ::closedir(d);
   std::sort(out.begin(), out.end(), [](const GpuLocation& a, const GpuLocation& b) {
     return std::tie(a.domain, a.bus, a.dev, a.func) < std::tie(b.domain, b.bus, b.dev, b.func);
   });
+  return out;
+}
+
+std::vector<GpuLocation> usable_gpus() {
+  std::vector<GpuLocation> out;
+  for (const auto& g : node_gpus()) {
+    if (g.render_minor < 0) continue;
+    const std::string dev = sysfs_root() + "/dev/dri/renderD" + std::to_string(g.render_minor);
+    // open, not access(): a container's device cgroup refuses the other GPUs' nodes only at open
+    const int fd = ::open(dev.c_str(), O_RDWR | O_CLOEXEC);
+    if (fd >= 0) {
+      ::close(fd);
+      out.push_back(g);
+    }
+  }
   return out;
 }
 

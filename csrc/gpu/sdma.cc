@@ -137,7 +137,9 @@ std::vector<int> device_consumer_cpus(int device) {
   me.numa_node = pci_numa_node(a.domain, a.bus, a.dev, a.func);
   const char* e = std::getenv("UDA_CONSUMER_CPUS");
   if (e && std::string(e) == "node") return consumer_cpus(me, {me}, allowed);
-  static const std::vector<GpuLocation> gpus = node_gpus();
+  // the GPUs this process can use share their nodes' CPUs (a one-GPU container on an 8-GPU host keeps
+  // its whole NUMA node; the eight ranks of an 8-GPU job get disjoint slices)
+  static const std::vector<GpuLocation> gpus = usable_gpus();
   return consumer_cpus(me, gpus, allowed);
 }
 

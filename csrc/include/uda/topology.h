@@ -24,6 +24,7 @@ namespace uda {
 struct GpuLocation {
   uint32_t domain = 0, bus = 0, dev = 0, func = 0;
   int numa_node = -1;
+  int render_minor = -1;    // /dev/dri/renderD<minor> (KFD drm_render_minor)
   std::string bdf() const;  // "dddd:bb:dd.f"
 };
 
@@ -35,6 +36,9 @@ std::string format_cpulist(const std::vector<int>& cpus);
 std::string sysfs_root();
 // Every GPU of the node (KFD topology, independent of HIP_VISIBLE_DEVICES), ordered by PCI address.
 std::vector<GpuLocation> node_gpus();
+// The GPUs this process can open (a container sees the host's whole KFD topology but only its own
+// render nodes), in node_gpus() order -- the devices HIP enumerates, without initialising HIP.
+std::vector<GpuLocation> usable_gpus();
 // NUMA node of the PCI function (-1 if the host does not say).
 int pci_numa_node(uint32_t domain, uint32_t bus, uint32_t dev, uint32_t func);
 // CPUs of NUMA node `node` (sysfs cpulist), empty if unknown.
@@ -42,7 +46,7 @@ std::vector<int> numa_node_cpus(int node);
 // This thread's allowed CPUs (sched_getaffinity).
 std::vector<int> allowed_cpus();
 
-// The consumer CPU slice of the GPU at PCI address `gpu` among `gpus` (node_gpus()): the allowed CPUs of
+// The consumer CPU slice of the GPU at PCI address `gpu` among `gpus` (usable_gpus()): the allowed CPUs of
 // its NUMA node cut into one contiguous piece per GPU of that node. Empty if the node is unknown (the
 // caller then leaves the threads unbound). `allowed` empty = no restriction.
 std::vector<int> consumer_cpus(const GpuLocation& gpu, const std::vector<GpuLocation>& gpus,

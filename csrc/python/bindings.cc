@@ -585,6 +585,11 @@ PYBIND11_MODULE(_uda_native, m) {
     }
     return out;
   }, py::arg("allowed") = std::vector<int>());
+  m.def("usable_gpu_bdfs", [] {
+    std::vector<std::string> v;
+    for (const auto& g : usable_gpus()) v.push_back(g.bdf());
+    return v;
+  });
   m.def("format_cpulist", &format_cpulist);
   m.def("parse_cpulist", &parse_cpulist);
   // a rank's placement record (bench.py JSON): PCI address, NUMA node, consumer CPU slice

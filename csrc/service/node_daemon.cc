@@ -881,7 +881,7 @@ int64_t json_int(const std::string& obj, const std::string& key) {
 // entries of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES when one restricts it. No HIP call: the front
 // end lives in the NodeManager and never initialises a GPU runtime.
 int visible_gpu_count() {
-  int n = (int)node_gpus().size();
+  int n = (int)usable_gpus().size();
   for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"}) {
     const char* e = std::getenv(var);
     if (!e) continue;
@@ -1004,8 +1004,22 @@ void NodeDaemonSet::route_main() {
   for (auto& p : pend) ::close(p.fd);
 }
 
-size_t NodeDaemonSet::store_of(const std::string& path) const {
-  return d_.size() <= 1 ? 0 : std::hash<std::string>()(path) % d_.size();
+// A MOF file's store: by a hash of its path, or (that daemon not ready when the file is first asked
+// for) the first ready one; remembered, so its releases go where its references are.
+size_t NodeDaemonSet::store_of(const std::string& path) {
+  if (d_.size() <= 1) return 0;
+  std::lock_guard<std::mutex> g(route_mu_);
+  auto it = route_.find(path);
+  if (it != route_.end()) return it->second;
+  size_t i = std::hash<std::string>()(path) % d_.size();
+  if (!d_[i]->ready())
+    for (size_t k = 0; k < d_.size(); ++k)
+      if (d_[(i + k) % d_.size()]->ready()) {
+        i = (i + k) % d_.size();
+        break;
+      }
+  route_[path] = i;
+  return i;
 }
 
 bool NodeDaemonSet::acquire(const std::string& job, const std::string& path, const std::string& holder,

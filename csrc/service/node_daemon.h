@@ -157,7 +157,9 @@ class NodeDaemonSet : public DeviceStore {
 
  private:
   void route_main();
-  size_t store_of(const std::string& path) const;
+  size_t store_of(const std::string& path);
+  std::mutex route_mu_;
+  std::map<std::string, size_t> route_;  // MOF path -> the daemon whose store holds it
   Options opt_;
   std::vector<std::unique_ptr<NodeDaemonClient>> d_;
   int listen_fd_ = -1;

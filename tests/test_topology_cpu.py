@@ -37,7 +37,8 @@ def _fake_node(root, gpus_per_node=4, nodes=2, cores_per_node=64):
             bus = 0x05 + 0x10 * g + 0x80 * n
             buses.append((bus, n))
             (kfd / str(k)).mkdir(parents=True)
-            (kfd / str(k) / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+            (kfd / str(k) / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {bus << 8}\n"
+                                                      f"domain 0\ndrm_render_minor {128 + len(buses) - 1}\n")
             p = root / "sys/bus/pci/devices" / f"0000:{bus:02x}:00.0"
             p.mkdir(parents=True)
             (p / "numa_node").write_text(f"{n}\n")
@@ -67,6 +68,21 @@ def test_eight_gpus_get_disjoint_numa_local_consumer_slices(native, tmp_path, mo
     got = [set(p["cpus"]) for p in plan2]
     assert all(got) and sum(len(g) for g in got) == len(allowed)
     assert all(not (a & b) for i, a in enumerate(got) for b in got[i + 1:])
+
+
+def test_usable_gpus_are_the_openable_render_nodes(native, tmp_path, monkeypatch):
+    """A one-GPU container on an 8-GPU host sees the whole KFD topology but opens one render node: the
+    node daemons and the consumer slices count only that one (no HIP call in the front end)."""
+    buses, _ = _fake_node(tmp_path)
+    monkeypatch.setenv("UDA_SYSFS_ROOT", str(tmp_path))
+    assert native.usable_gpu_bdfs() == []
+    dri = tmp_path / "dev/dri"
+    dri.mkdir(parents=True)
+    (dri / "renderD131").write_bytes(b"")  # the 4th GPU (render minor 128 + 3)
+    assert native.usable_gpu_bdfs() == [f"0000:{buses[3][0]:02x}:00.0"]
+    for m in range(128, 136):
+        (dri / f"renderD{m}").write_bytes(b"")
+    assert len(native.usable_gpu_bdfs()) == 8
 
 
 def test_cpulist_roundtrip(native):
