@@ -1873,23 +1873,21 @@ void ReduceTask::merge_gpu() {
         if (all_eof) planned_all = true;
         return true;
       };
-      auto prep = [&](size_t q) {
+      // a round's slices by value: `rounds` grows (and reallocates) on this thread while earlier rounds merge
+      auto prep = [&, mems = std::vector<uint8_t*>(dp.dst)](size_t q, std::vector<std::pair<int64_t, int64_t>> rr) {
         if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
         std::vector<Span> views((size_t)K);
         for (int k = 0; k < K; ++k)
-          views[(size_t)k] = Span{runs[(size_t)k].mem + rounds[q][(size_t)k].first,
-                                  rounds[q][(size_t)k].second - rounds[q][(size_t)k].first};
+          views[(size_t)k] = Span{mems[(size_t)k] + rr[(size_t)k].first, rr[(size_t)k].second - rr[(size_t)k].first};
         return device_merge(*wsv[q % 3], views, Codec::kNone, kind_, kv, sv[q % 3], nullptr, true);
       };
       std::vector<std::future<DeviceMergeOut>> next;
-      size_t issued = 0;
-      auto issue = [&] {  // keep two rounds in preparation ahead of the one being delivered
-        while (issued < rounds.size() && issued < next.size() + 0 + 2 && next.size() < issued + 1) {
-          next.push_back(std::async(std::launch::async, prep, issued));
-          ++issued;
-        }
+      // at most three rounds in flight (one delivering, two preparing): workspace q % 3 is free again
+      // once round q - 3 has been delivered
+      auto issue = [&](size_t q) {
+        while (next.size() < rounds.size() && next.size() < q + 3)
+          next.push_back(std::async(std::launch::async, prep, next.size(), rounds[next.size()]));
       };
-      (void)issue;
       size_t q = 0;
       while (!planned_all || q < rounds.size()) {
         // plan what has arrived (wait only when nothing is queued)
@@ -1898,10 +1896,10 @@ void ReduceTask::merge_gpu() {
           if (!plan_more(q >= rounds.size())) break;
           if (rounds.size() == before && q < rounds.size()) break;
         }
-        while (next.size() < rounds.size() && next.size() < q + 3) next.push_back(std::async(std::launch::async, prep, next.size()));
+        issue(q);
         if (q >= rounds.size()) continue;
         DeviceMergeOut m = next[q].get();
-        while (next.size() < rounds.size() && next.size() < q + 3) next.push_back(std::async(std::launch::async, prep, next.size()));
+        issue(q);
         deliver(m, planned_all && q + 1 == rounds.size(), sv[q % 3], *wsv[q % 3]);
         ++q;
       }

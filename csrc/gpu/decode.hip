@@ -300,7 +300,7 @@ __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64
   }
 }
 
-__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+__host__ __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
@@ -368,7 +368,7 @@ struct LaneIn {  // the next input bytes of one lane, 8 at a time
   int64_t end;     // one past the last readable byte of this block
   int64_t base = -8;
   uint64_t word = 0;
-  __device__ __forceinline__ uint32_t at(int64_t ip) {
+  __host__ __device__ __forceinline__ uint32_t at(int64_t ip) {
     const int64_t d = ip - base;
     if (d < 0 || d >= 8) {
       base = ip;
@@ -385,13 +385,13 @@ struct LaneIn {  // the next input bytes of one lane, 8 at a time
 };
 
 // dst[0, len) = src[0, len), non-overlapping or src >= dst + 8 behind (forward, 8 bytes per move)
-__device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, int64_t len) {
+__host__ __device__ __forceinline__ void lane_copy(uint8_t* dst, const uint8_t* src, int64_t len) {
   int64_t i = 0;
   for (; i + 8 <= len; i += 8) reinterpret_cast<U64p*>(dst + i)->v = reinterpret_cast<const U64p*>(src + i)->v;
   for (; i < len; ++i) dst[i] = src[i];
 }
 
-__device__ __forceinline__ void lane_match(uint8_t* out, int64_t op, int64_t off, int64_t len) {
+__host__ __device__ __forceinline__ void lane_match(uint8_t* out, int64_t op, int64_t off, int64_t len) {
   if (off >= 8) {
     lane_copy(out + op, out + op - off, len);
   } else {
@@ -400,7 +400,7 @@ __device__ __forceinline__ void lane_match(uint8_t* out, int64_t op, int64_t off
 }
 
 // LZO1X chunk of one lane (csrc/codec/lzo.cc semantics, same bounds checks as lzo_chunk).
-__device__ bool lzo_lane_chunk(const uint8_t* in, uint8_t* out, int64_t ip, int64_t ip_end, int64_t op, int64_t oend,
+__host__ __device__ bool lzo_lane_chunk(const uint8_t* in, uint8_t* out, int64_t ip, int64_t ip_end, int64_t op, int64_t oend,
                                int64_t clip, bool prefix, int64_t* produced) {
   LaneIn r{in, ip_end};
   const int64_t out0 = op;
@@ -408,11 +408,11 @@ __device__ bool lzo_lane_chunk(const uint8_t* in, uint8_t* out, int64_t ip, int6
   bool lit_first = false;
   if (ip >= ip_end) return false;
   auto lit = [&](int64_t len) {  // the bytes below the clip
-    const int64_t n = min(len, clip - op);
+    const int64_t n = len < clip - op ? len : clip - op;
     if (n > 0) lane_copy(out + op, in + ip, n);
   };
   auto match = [&](int64_t off, int64_t len) {
-    const int64_t n = min(len, clip - op);
+    const int64_t n = len < clip - op ? len : clip - op;
     if (n > 0) lane_match(out, op, off, n);
   };
   if (r.at(ip) > 17) {
@@ -557,6 +557,33 @@ __global__ void __launch_bounds__(256) lzo_lane_kernel(const uint8_t* in, uint8_
 }
 
 }  // namespace
+
+// The lane kernel's per-block decode run on the host over one block-compressed stream (tests: the same
+// code path the device lanes run, checked on a machine without a GPU). false on a corrupt block.
+bool lzo_lane_decode_host(const uint8_t* in, int64_t n, uint8_t* out, int64_t out_cap, int64_t* out_len) {
+  int64_t i = 0, op = 0;
+  while (i < n) {
+    if (i + 4 > n) return false;
+    const int64_t block_raw = (int64_t)be32(in + i);
+    i += 4;
+    if (block_raw == 0) continue;
+    if (op + block_raw > out_cap) return false;
+    const int64_t oend = op + block_raw;
+    while (op < oend) {
+      if (i + 4 > n) return false;
+      const int64_t clen = (int64_t)be32(in + i);
+      i += 4;
+      if (i + clen > n) return false;
+      int64_t produced = 0;
+      if (!lzo_lane_chunk(in, out, i, i + clen, op, oend, oend, false, &produced)) return false;
+      i += clen;
+      op += produced;
+    }
+    if (op != oend) return false;
+  }
+  *out_len = op;
+  return true;
+}
 
 // Framing walk of device-resident block-compressed streams (one lane per stream, following the
 // 4-byte headers; a header read per chunk). Pass 1 (out == nullptr): blocks and raw bytes per

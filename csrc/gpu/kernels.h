@@ -246,6 +246,8 @@ struct DecodeDesc {
 // clip > 0: prefix decode, only the first `clip` raw bytes of every block are produced (at its dst).
 void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status,
                          hipStream_t s, int64_t clip = 0);
+// The LZO lane kernel's per-block decode on the host (tests without a GPU).
+bool lzo_lane_decode_host(const uint8_t* in, int64_t n, uint8_t* out, int64_t out_cap, int64_t* out_len);
 // Framing walk of device-resident streams (one lane per stream). out == nullptr: per-stream block
 // counts and raw bytes; else the descriptors with absolute src addresses (decode with in = nullptr).
 // status[s] = 1: framing not resolvable without decoding (zero status first).

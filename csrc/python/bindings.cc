@@ -585,6 +585,16 @@ PYBIND11_MODULE(_uda_native, m) {
     }
     return out;
   }, py::arg("allowed") = std::vector<int>());
+  m.def("lzo_lane_decode_host", [](py::bytes stream, int64_t raw_cap) {
+    const std::string in = stream;
+    std::string out((size_t)std::max<int64_t>(raw_cap, 1), '\0');
+    int64_t n = 0;
+    if (!gpu::lzo_lane_decode_host(reinterpret_cast<const uint8_t*>(in.data()), (int64_t)in.size(),
+                                   reinterpret_cast<uint8_t*>(&out[0]), raw_cap, &n))
+      throw std::runtime_error("lzo lane decode: corrupt block");
+    out.resize((size_t)n);
+    return py::bytes(out);
+  });
   m.def("usable_gpu_bdfs", [] {
     std::vector<std::string> v;
     for (const auto& g : usable_gpus()) v.push_back(g.bdf());

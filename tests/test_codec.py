@@ -95,3 +95,29 @@ def test_lzo1x_spec_vectors(native, name):
     stream, want = {v[0]: (v[1], v[2]) for v in VECTORS}[name]
     assert native.lzo1x_decompress(stream, len(want)) == want
     assert native.block_decompress(2, hadoop_block(want, stream), 7) == want
+
+
+def test_lzo_lane_decoder_on_the_host(native):
+    """The LZO1X per-lane decode of the device lane kernel (one lane per block), run on the host: every
+    payload shape (TeraSort records, incompressible, period-1/3 repeats, odd-alignment back-references,
+    IFile streams) at every block size decodes to the original; a broken back-reference is refused."""
+    import os
+    import random
+
+    from uda_amd.utils import datagen
+    rng = random.Random(11)
+    base = os.urandom(5000)
+    pays = [datagen.streams(datagen.terasort(2, 1, 6000, seed=5))[0][0], os.urandom(300_000), b"\x00" * 100_000,
+            b"abc" * 50_000 + b"x", b"q", b"",
+            b"".join((os.urandom(rng.randint(1, 300)) if rng.random() < 0.5 else bytes([rng.randrange(256)]) *
+                      rng.randint(1, 900)) for _ in range(600)),
+            b"".join(base[o:o + k] for o, k in ((rng.randrange(4700), rng.randint(4, 300)) for _ in range(2000))),
+            datagen.streams(datagen.secondary_sort(3, 1, 3000, seed=2))[0][0]]
+    for block in (4096, 65536, 262144):
+        for p in pays:
+            assert native.lzo_lane_decode_host(native.block_compress(2, p, block), len(p)) == p
+    st = bytearray(native.block_compress(2, b"abcdefgh" * 4000 + os.urandom(1000), 65536))
+    for i in range(12, 60):
+        st[i] = 0xFF
+    with pytest.raises(RuntimeError, match="corrupt"):
+        native.lzo_lane_decode_host(bytes(st), 40_000)
