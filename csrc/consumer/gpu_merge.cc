@@ -1129,6 +1129,7 @@ void ReduceTask::merge_gpu() {
     std::vector<std::string> last_key;       // [k]: key of that record ("" none yet)
     std::vector<char> eof;                   // [k]: the partition is indexed to its EOF marker
     std::vector<int> phase_runs;             // [p]: runs indexed through phase p
+    std::vector<gpu::PinnedPool::Block> blocks;  // [k]: the pinned span of partition k (back to the pool at the end)
     std::mutex mu;
     std::condition_variable cv;
     std::exception_ptr err;
@@ -1138,6 +1139,7 @@ void ReduceTask::merge_gpu() {
     ~DirectProg() {
       for (auto& t : threads)
         if (t.joinable()) t.join();
+      for (auto& b : blocks) gpu::PinnedPool::instance().release(b);
     }
   };
   std::unique_ptr<DirectProg> dprog;
@@ -1470,12 +1472,12 @@ void ReduceTask::merge_gpu() {
           dp.P = pdirect_phases;
           dp.K = (int)ready.size();
           dp.f = ready;
-          for (auto& f : ready) {
-            const int64_t cap = std::max<int64_t>(f->part_len(), 0);
-            dp.cap.push_back(cap);
-            dp.dst.push_back(fill_mem->alloc((size_t)std::max<int64_t>(cap, 1)));
-          }
+          for (auto& f : ready) dp.cap.push_back(std::max<int64_t>(f->part_len(), 0));
           const size_t K = (size_t)dp.K;
+          // each partition's pinned span is taken by the thread that fetches its first phase (in parallel,
+          // beside the first fetches: pinning GBs serially here held up the whole fetch)
+          dp.dst.assign(K, nullptr);
+          dp.blocks.assign(K, gpu::PinnedPool::Block{});
           dp.fetched.assign(K, std::vector<char>((size_t)dp.P, 0));
           dp.indexed.assign(K, 0);
           dp.indexing.assign(K, 0);
@@ -1498,9 +1500,21 @@ void ReduceTask::merge_gpu() {
                 const int64_t cap = dp.cap[(size_t)k];
                 const int64_t b = cap * p / dp.P, e = cap * (p + 1) / dp.P;
                 if (p == 0) {
+                  const gpu::PinnedPool::Block blk = gpu::PinnedPool::instance().acquire((size_t)std::max<int64_t>(cap, 256));
+                  {
+                    std::lock_guard<std::mutex> g(dp.mu);
+                    dp.blocks[(size_t)k] = blk;
+                    dp.dst[(size_t)k] = blk.p;
+                    dp.cv.notify_all();
+                  }
                   const int64_t off = f.take_first(dp.dst[(size_t)k], cap);
                   if (off < e) fetch_direct(f.params(), dp.dst[(size_t)k], off, e, depth, nullptr, 0);
                 } else if (b < e) {
+                  {  // its first phase (another thread) may still be taking the span
+                    std::unique_lock<std::mutex> lk(dp.mu);
+                    dp.cv.wait(lk, [&] { return dp.dst[(size_t)k] != nullptr || dp.err; });
+                    if (dp.err) break;
+                  }
                   fetch_direct(f.params(), dp.dst[(size_t)k], b, e, depth, nullptr, 0);
                 }
                 // index run k through every phase landed in order (one thread per run at a time)
@@ -1537,7 +1551,9 @@ void ReduceTask::merge_gpu() {
               }
             }
           };
-          const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(drains > 0 ? drains : 8, dp.K));
+          // fetch threads: enough to stay ahead of the merge, few enough not to slow the consumer they overlap
+          const int64_t pt = host_->conf_i64("mapred.uda.gpu.hybrid.progressive.threads", drains > 0 ? drains : 8);
+          const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(pt, dp.K));
           for (int w = 0; w < nthreads; ++w) dp.threads.emplace_back(work);
           drained = maps;
           ready.clear();
@@ -1739,8 +1755,7 @@ void ReduceTask::merge_gpu() {
       DirectProg& dp = *dprog;
       const int K = dp.K;
       // merge-owned views of the runs: the landed, indexed prefix of every partition
-      std::vector<SpillRun> runs((size_t)K);
-      for (int k = 0; k < K; ++k) runs[(size_t)k].mem = dp.dst[(size_t)k];
+      std::vector<SpillRun> runs((size_t)K);  // .mem set once the fetch threads have pinned the spans
       std::vector<int64_t> at((size_t)K, 0);  // merged so far (a record boundary)
       std::vector<size_t> taken((size_t)K, 0);  // samples copied into runs[k]
       // first record of `run` (indexed prefix) whose key is >= k
@@ -1800,6 +1815,7 @@ void ReduceTask::merge_gpu() {
         bool have_bound = false;
         for (int k = 0; k < K; ++k) {
           SpillRun& r = runs[(size_t)k];
+          r.mem = dp.dst[(size_t)k];  // indexed through a phase: its span exists
           auto& vc = dp.cut[(size_t)k];
           auto& vk = dp.key[(size_t)k];
           for (size_t j = taken[(size_t)k]; j < vc.size(); ++j) {
@@ -1874,7 +1890,7 @@ void ReduceTask::merge_gpu() {
         return true;
       };
       // a round's slices by value: `rounds` grows (and reallocates) on this thread while earlier rounds merge
-      auto prep = [&, mems = std::vector<uint8_t*>(dp.dst)](size_t q, std::vector<std::pair<int64_t, int64_t>> rr) {
+      auto prep = [&](size_t q, std::vector<std::pair<int64_t, int64_t>> rr, std::vector<uint8_t*> mems) {
         if (hipSetDevice(device) != hipSuccess) throw UdaError("hipSetDevice failed");
         std::vector<Span> views((size_t)K);
         for (int k = 0; k < K; ++k)
@@ -1885,8 +1901,11 @@ void ReduceTask::merge_gpu() {
       // at most three rounds in flight (one delivering, two preparing): workspace q % 3 is free again
       // once round q - 3 has been delivered
       auto issue = [&](size_t q) {
-        while (next.size() < rounds.size() && next.size() < q + 3)
-          next.push_back(std::async(std::launch::async, prep, next.size(), rounds[next.size()]));
+        while (next.size() < rounds.size() && next.size() < q + 3) {
+          std::vector<uint8_t*> mems((size_t)K);
+          for (int k = 0; k < K; ++k) mems[(size_t)k] = runs[(size_t)k].mem;
+          next.push_back(std::async(std::launch::async, prep, next.size(), rounds[next.size()], std::move(mems)));
+        }
       };
       size_t q = 0;
       while (!planned_all || q < rounds.size()) {

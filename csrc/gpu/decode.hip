@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "kernels.h"
 
@@ -38,6 +39,7 @@ struct Wave {
   int64_t clip;       // prefix decode: no byte at or past this output offset is written
   bool prefix;        // a prefix decode (stops at clip); else clip is the block's end
   int lane;
+  uint32_t rw;        // register window: this lane's 4 bytes of the 256-byte window at win_base
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -48,10 +50,33 @@ __device__ __forceinline__ int64_t uni(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// Make [ip, ip+need) resident in the LDS window (need <= 64). Returns false past the block end.
+// Register window (R): the 256 compressed bytes at win_base spread 4 per lane over a VGPR; a byte is
+// one v_readlane (a few cycles) instead of a dependent LDS read (~100) on the parse's critical path.
+// Refilled by one coalesced 256-byte load; lanes past the block end hold zeros.
+constexpr int kRegWin = 256;
+struct __attribute__((packed, aligned(1))) U32p {
+  uint32_t v;
+};
+template <bool R>
 __device__ __forceinline__ bool ensure(Wave& w, int64_t ip, int need) {
   if (ip + need > w.in_end) return false;
   if (ip >= w.win_base && ip + need <= w.win_end) return true;
+  if (R) {
+    const int64_t base = ip & ~(int64_t)3;
+    const int64_t end = min(base + kRegWin, w.in_end);
+    const int64_t p = base + 4 * w.lane;
+    uint32_t v = 0;
+    if (p + 4 <= end) {
+      v = reinterpret_cast<const U32p*>(w.in + p)->v;
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (p + k < end) v |= (uint32_t)w.in[p + k] << (8 * k);
+    }
+    w.rw = v;
+    w.win_base = base;
+    w.win_end = end;
+    return true;
+  }
   wave_sync();
   const int64_t base = ip & ~(int64_t)15;
   const int64_t end = min(base + kWin, w.in_end);
@@ -76,7 +101,13 @@ __device__ __forceinline__ bool ensure(Wave& w, int64_t ip, int need) {
   return true;
 }
 
+template <bool R>
 __device__ __forceinline__ uint32_t byte_at(const Wave& w, int64_t ip) {
+  if (R) {
+    const int d = (int)(ip - w.win_base);
+    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)w.rw, d >> 2);
+    return (word >> (8 * (d & 3))) & 0xFF;
+  }
   return (uint32_t)w.win[ip - w.win_base];
 }
 
@@ -117,14 +148,15 @@ __device__ __forceinline__ void copy_match(Wave& w, int64_t op, int64_t off, int
   }
 }
 
+template <bool R>
 __device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int64_t oend, int64_t* produced) {
   w.in_end = cend;
   // varint uncompressed length
   int64_t ulen = 0;
   int shift = 0;
   for (;;) {
-    if (shift > 35 || !ensure(w, ip, 1)) return false;
-    const uint32_t b = byte_at(w, ip++);
+    if (shift > 35 || !ensure<R>(w, ip, 1)) return false;
+    const uint32_t b = byte_at<R>(w, ip++);
     ulen |= (int64_t)(b & 0x7F) << shift;
     if (!(b & 0x80)) break;
     shift += 7;
@@ -137,16 +169,16 @@ __device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int6
       *produced = ulen;
       return true;
     }
-    if (!ensure(w, ip, 1)) return false;
-    const uint32_t tag = byte_at(w, ip++);
+    if (!ensure<R>(w, ip, 1)) return false;
+    const uint32_t tag = byte_at<R>(w, ip++);
     const uint32_t type = tag & 3;
     if (type == 0) {
       int64_t len = tag >> 2;
       if (len >= 60) {
         const int nb = (int)len - 59;
-        if (!ensure(w, ip, nb)) return false;
+        if (!ensure<R>(w, ip, nb)) return false;
         len = 0;
-        for (int i = 0; i < nb; ++i) len |= (int64_t)byte_at(w, ip + i) << (8 * i);
+        for (int i = 0; i < nb; ++i) len |= (int64_t)byte_at<R>(w, ip + i) << (8 * i);
         ip += nb;
       }
       len += 1;
@@ -157,20 +189,20 @@ __device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int6
     } else {
       int64_t len, off;
       if (type == 1) {
-        if (!ensure(w, ip, 1)) return false;
+        if (!ensure<R>(w, ip, 1)) return false;
         len = 4 + ((tag >> 2) & 7);
-        off = ((int64_t)(tag >> 5) << 8) | byte_at(w, ip);
+        off = ((int64_t)(tag >> 5) << 8) | byte_at<R>(w, ip);
         ip += 1;
       } else if (type == 2) {
-        if (!ensure(w, ip, 2)) return false;
+        if (!ensure<R>(w, ip, 2)) return false;
         len = 1 + (tag >> 2);
-        off = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+        off = (int64_t)byte_at<R>(w, ip) | ((int64_t)byte_at<R>(w, ip + 1) << 8);
         ip += 2;
       } else {
-        if (!ensure(w, ip, 4)) return false;
+        if (!ensure<R>(w, ip, 4)) return false;
         len = 1 + (tag >> 2);
-        off = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8) | ((int64_t)byte_at(w, ip + 2) << 16) |
-              ((int64_t)byte_at(w, ip + 3) << 24);
+        off = (int64_t)byte_at<R>(w, ip) | ((int64_t)byte_at<R>(w, ip + 1) << 8) | ((int64_t)byte_at<R>(w, ip + 2) << 16) |
+              ((int64_t)byte_at<R>(w, ip + 3) << 24);
         ip += 4;
       }
       if (off == 0 || off > op - op0 || op + len > uend) return false;
@@ -184,14 +216,15 @@ __device__ bool snappy_chunk(Wave& w, int64_t ip, int64_t cend, int64_t op, int6
 }
 
 // LZO1X: the state machine of csrc/codec/lzo.cc, wave-uniform.
+template <bool R>
 __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64_t oend, int64_t* produced) {
   w.in_end = ip_end;
   const int64_t out0 = op;
   int64_t t = 0, next = 0, state = 0, m_pos = 0;
   bool lit_first = false;
-  if (!ensure(w, ip, 1)) return false;
-  if (byte_at(w, ip) > 17) {
-    t = (int64_t)byte_at(w, ip) - 17;
+  if (!ensure<R>(w, ip, 1)) return false;
+  if (byte_at<R>(w, ip) > 17) {
+    t = (int64_t)byte_at<R>(w, ip) - 17;
     ++ip;
     if (t < 4) {
       next = t;
@@ -208,18 +241,18 @@ __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64
       lit_first = false;
       goto copy_literal_run;
     }
-    if (!ensure(w, ip, 1)) return false;
-    t = byte_at(w, ip++);
+    if (!ensure<R>(w, ip, 1)) return false;
+    t = byte_at<R>(w, ip++);
     if (t < 16) {
       if (state == 0) {
         if (t == 0) {
           for (;;) {
-            if (!ensure(w, ip, 1)) return false;
-            if (byte_at(w, ip) != 0) break;
+            if (!ensure<R>(w, ip, 1)) return false;
+            if (byte_at<R>(w, ip) != 0) break;
             t += 255;
             ++ip;
           }
-          t += 15 + byte_at(w, ip++);
+          t += 15 + byte_at<R>(w, ip++);
         }
         t += 3;
       copy_literal_run:
@@ -231,36 +264,36 @@ __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64
         continue;
       } else if (state != 4) {  // M1: 2-byte match after 1..3 trailing literals
         next = t & 3;
-        if (!ensure(w, ip, 1)) return false;
-        m_pos = op - 1 - (t >> 2) - ((int64_t)byte_at(w, ip++) << 2);
+        if (!ensure<R>(w, ip, 1)) return false;
+        m_pos = op - 1 - (t >> 2) - ((int64_t)byte_at<R>(w, ip++) << 2);
         if (m_pos < out0 || m_pos >= op || op + 2 > oend) return false;
         copy_match(w, op, op - m_pos, 2);
         op += 2;
         goto match_next;
       } else {  // M1 after a literal run: 3 bytes, offset 2049..3072
         next = t & 3;
-        if (!ensure(w, ip, 1)) return false;
-        m_pos = op - (1 + 0x0800) - (t >> 2) - ((int64_t)byte_at(w, ip++) << 2);
+        if (!ensure<R>(w, ip, 1)) return false;
+        m_pos = op - (1 + 0x0800) - (t >> 2) - ((int64_t)byte_at<R>(w, ip++) << 2);
         t = 3;
       }
     } else if (t >= 64) {  // M2
       next = t & 3;
-      if (!ensure(w, ip, 1)) return false;
-      m_pos = op - 1 - ((t >> 2) & 7) - ((int64_t)byte_at(w, ip++) << 3);
+      if (!ensure<R>(w, ip, 1)) return false;
+      m_pos = op - 1 - ((t >> 2) & 7) - ((int64_t)byte_at<R>(w, ip++) << 3);
       t = (t >> 5) - 1 + 2;
     } else if (t >= 32) {  // M3
       t = (t & 31) + 2;
       if (t == 2) {
         for (;;) {
-          if (!ensure(w, ip, 1)) return false;
-          if (byte_at(w, ip) != 0) break;
+          if (!ensure<R>(w, ip, 1)) return false;
+          if (byte_at<R>(w, ip) != 0) break;
           t += 255;
           ++ip;
         }
-        t += 31 + byte_at(w, ip++);
+        t += 31 + byte_at<R>(w, ip++);
       }
-      if (!ensure(w, ip, 2)) return false;
-      next = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+      if (!ensure<R>(w, ip, 2)) return false;
+      next = (int64_t)byte_at<R>(w, ip) | ((int64_t)byte_at<R>(w, ip + 1) << 8);
       ip += 2;
       m_pos = op - 1 - (next >> 2);
       next &= 3;
@@ -269,15 +302,15 @@ __device__ bool lzo_chunk(Wave& w, int64_t ip, int64_t ip_end, int64_t op, int64
       t = (t & 7) + 2;
       if (t == 2) {
         for (;;) {
-          if (!ensure(w, ip, 1)) return false;
-          if (byte_at(w, ip) != 0) break;
+          if (!ensure<R>(w, ip, 1)) return false;
+          if (byte_at<R>(w, ip) != 0) break;
           t += 255;
           ++ip;
         }
-        t += 7 + byte_at(w, ip++);
+        t += 7 + byte_at<R>(w, ip++);
       }
-      if (!ensure(w, ip, 2)) return false;
-      next = (int64_t)byte_at(w, ip) | ((int64_t)byte_at(w, ip + 1) << 8);
+      if (!ensure<R>(w, ip, 2)) return false;
+      next = (int64_t)byte_at<R>(w, ip) | ((int64_t)byte_at<R>(w, ip + 1) << 8);
       ip += 2;
       m_pos -= next >> 2;
       next &= 3;
@@ -306,10 +339,10 @@ __host__ __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
 
 // clip > 0: prefix decode. Only the first `clip` bytes of each block's output (at d.dst) are written and
 // the decode stops once they are out; d.raw stays the block's full raw size for the format checks.
-template <int kCodec>
+template <int kCodec, bool R>
 __global__ void __launch_bounds__(64 * kWavesPerBlock)
     block_decode_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status, int64_t clip) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][kWin + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[R ? 1 : kWavesPerBlock][R ? 16 : kWin + 16];
   const int wid = threadIdx.x >> 6;
   const int b = blockIdx.x * kWavesPerBlock + wid;
   if (b >= n) return;
@@ -317,7 +350,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
   Wave w;
   w.in = in;
   w.out = out;
-  w.win = lds[wid];
+  w.win = lds[R ? 0 : wid];
+  w.rw = 0;
   w.win_base = 0;
   w.win_end = 0;
   w.flushed = d.dst;
@@ -342,8 +376,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
     }
     int64_t produced = 0;
     w.win_base = w.win_end = 0;
-    ok = (kCodec == 1) ? snappy_chunk(w, ip, ip + clen, op, oend, &produced)
-                       : lzo_chunk(w, ip, ip + clen, op, oend, &produced);
+    ok = (kCodec == 1) ? snappy_chunk<R>(w, ip, ip + clen, op, oend, &produced)
+                       : lzo_chunk<R>(w, ip, ip + clen, op, oend, &produced);
     ip += clen;
     op += produced;
   }
@@ -525,7 +559,7 @@ __host__ __device__ bool lzo_lane_chunk(const uint8_t* in, uint8_t* out, int64_t
   }
 }
 
-__global__ void __launch_bounds__(256) lzo_lane_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n,
+__global__ void __launch_bounds__(64) lzo_lane_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n,
                                                        int* status, int64_t clip_in) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
@@ -673,14 +707,23 @@ void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const Decod
                          hipStream_t s, int64_t clip) {
   if (n <= 0) return;
   const int grid = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-  const char* le = std::getenv("UDA_LZO_LANE");  // read per launch: tests compare both kernels in one process
-  const bool lzo_lane = !le || std::atoi(le) != 0;
-  if (codec == 1)
-    block_decode_kernel<1><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+  // read per launch: tests compare the kernels in one process
+  const char* le = std::getenv("UDA_LZO_LANE");  // 1: one lane per LZO block (too few blocks per round to hide latency)
+  const bool lzo_lane = le && std::atoi(le) != 0;
+  const char* we = std::getenv("UDA_DECODE_WINDOW");  // "lds": the LDS window of round 5
+  const bool reg = !we || std::string(we) != "lds";
+  if (codec == 1 && reg)
+    block_decode_kernel<1, true><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+  else if (codec == 1)
+    block_decode_kernel<1, false><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
   else if (lzo_lane)
-    lzo_lane_kernel<<<(n + 255) / 256, 256, 0, s>>>(in, out, descs, n, status, clip);
+    // one wave per workgroup: a round's few hundred waves spread over the CUs (each with its own L1 for
+    // its 64 lanes' input and output streams) instead of packing four on one CU
+    lzo_lane_kernel<<<(n + 63) / 64, 64, 0, s>>>(in, out, descs, n, status, clip);
+  else if (reg)
+    block_decode_kernel<2, true><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
   else
-    block_decode_kernel<2><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+    block_decode_kernel<2, false><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
 }
 
 }  // namespace gpu

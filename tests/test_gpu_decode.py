@@ -118,23 +118,29 @@ def test_lzo1x_spec_vectors_on_device(require_gpu, native):
     assert outs == [want for _, _, want in VECTORS]
 
 
-@pytest.mark.parametrize("lane", ["1", "0"], ids=["lane-per-block", "wave-per-block"])
-def test_lzo_kernels_agree_on_terasort_records(require_gpu, native, monkeypatch, lane):
-    """Both LZO device kernels (one lane per block, the default; one wave per block, UDA_LZO_LANE=0)
-    decode TeraSort-shaped IFile records -- random keys, 26-letter values, the many-short-token streams
-    the lane kernel was built for -- and every other payload to the original bytes; a corrupt block is
-    reported by both."""
-    monkeypatch.setenv("UDA_LZO_LANE", lane)
+@pytest.mark.parametrize("env", [{}, {"UDA_DECODE_WINDOW": "lds"}, {"UDA_LZO_LANE": "1"}],
+                         ids=["wave-register-window", "wave-lds-window", "lane-per-block"])
+@pytest.mark.parametrize("codec", ["lzo", "snappy"])
+def test_decode_kernels_agree_on_terasort_records(require_gpu, native, monkeypatch, env, codec):
+    """Every device decode kernel -- one wave per block parsing from a register window (default) or from
+    the LDS window of round 5, and for LZO one lane per block -- decodes TeraSort-shaped IFile records
+    (random keys, 26-letter values: streams of many 3-4 byte tokens) and every other payload to the
+    original bytes, and reports a corrupt block."""
+    if codec == "snappy" and "UDA_LZO_LANE" in env:
+        pytest.skip("LZO only")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cid = LZO if codec == "lzo" else SNAPPY
     tera = datagen.streams(datagen.terasort(2, 1, 6000, seed=5))[0][0]
     raws = [tera] + [raw for _, raw in _payloads()]
     for block in (4096, 262144):
-        streams = [native.block_compress(LZO, raw, block) for raw in raws]
-        outs, blocks, _ms = native.gpu_block_decode("lzo", streams)
+        streams = [native.block_compress(cid, raw, block) for raw in raws]
+        outs, blocks, _ms = native.gpu_block_decode(codec, streams)
         assert blocks == sum((len(r) + block - 1) // block for r in raws)
         assert all(o == r for o, r in zip(outs, raws))
     raw = b"abcdefgh" * 4000 + os.urandom(1000)
-    st = bytearray(native.block_compress(LZO, raw, 65536))
+    st = bytearray(native.block_compress(cid, raw, 65536))
     for i in range(12, min(len(st), 60)):  # a broken back-reference, as test_corrupt_block_raises
         st[i] = 0xFF
     with pytest.raises(Exception, match="corrupt|framing"):
-        native.gpu_block_decode("lzo", [bytes(st)])
+        native.gpu_block_decode(codec, [bytes(st)])

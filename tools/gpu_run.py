@@ -140,6 +140,16 @@ RECIPES: dict[str, tuple[int, str]] = {
                              "python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
     "prof_lzo41_wave": (500, "UDA_LZO_LANE=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_lzo41_wave "
                              "-o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "hybrid41b_t4": (700, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000,mapred.uda.gpu.hybrid.progressive.threads=4 "
+                          f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "hybrid41b_p16": (700, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000,mapred.uda.gpu.hybrid.progressive.phases=16 "
+                           f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 2 --warmup 1"),
+    "lzo130x5_lds": (600, f"UDA_DECODE_WINDOW=lds {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1 --verbose"),
+    "snappy130x5_r6": (600, f"{PY} bench.py --api --api-codec snappy --steps 5 --warmup 1 --verbose"),
+    "pmc_lzo41_lds": (300, "UDA_DECODE_WINDOW=lds timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS "
+                           "SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv "
+                           "-d gpurun_out/pmc_lzo41_lds -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
+                           "--steps 1 --warmup 0"),
     "ipc8_detail": (700, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
