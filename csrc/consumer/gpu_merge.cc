@@ -1086,7 +1086,7 @@ void ReduceTask::merge_gpu() {
   StagedCount staged_count(device);
   const bool prog_ok = prog_phases > 1 && stager && stager->sdma() && restored_files_.empty() && !ckpt;
   // over budget, DRAM tier: phases into pinned DRAM, RPQ rounds of every fully arrived key range (DirectProg)
-  const int pdirect_phases = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.hybrid.progressive.phases", 8));
+  const int pdirect_phases = (int)std::max<int64_t>(1, host_->conf_i64("mapred.uda.gpu.hybrid.progressive.phases", 16));
   bool prog_decided = false, progressive = false;
   struct ProgFetch {
     int P = 0, K = 0;
