@@ -507,6 +507,11 @@ def _run_waves(args, port, cmds, expected, exe, errlog, conf, sp, statistics):
                     line = p.stdout.read().strip().splitlines()
                     res = json.loads(line[-1]) if line else {"error": "no output"}
                     if p.returncode != 0 or res.get("error"):
+                        t = res.get("task") or {}
+                        print(f"# failed reduce task {r}: " + json.dumps({k: t.get(k) for k in (
+                            "merge_path", "device_descriptors", "host_fetched_bytes", "maps_fetched", "bytes_fetched",
+                            "records", "bytes_delivered", "unmapped_descriptors", "merge_service", "rpq_rounds")}),
+                              file=sys.stderr, flush=True)
                         raise RuntimeError(f"reduce task {r} (pid {p.pid}) failed rc={p.returncode}: {res.get('error')}")
                     out[r] = res
                     del running[r]
@@ -678,8 +683,13 @@ def run_node_files(args, ctx) -> int:
         print(f"# node files: map phase {t_map:.1f}s ({job['store_bytes'] / 1e9:.1f} GB in {args.maps_per_gpu} "
               f"file.out), front end up in {time.perf_counter() - t:.1f}s, node daemon {daemon}", file=sys.stderr,
               flush=True)
-        warm, stats, validated = _run_waves(args, port, job["commands"], job["expected"], exe, errlog, {}, sp,
-                                            statistics)
+        try:
+            warm, stats, validated = _run_waves(args, port, job["commands"], job["expected"], exe, errlog, {}, sp,
+                                                statistics)
+        except RuntimeError as e:  # say whether the provider front end is still there
+            rc = frontend.poll()
+            how = "running" if rc is None else f"exited rc={rc}" + (f" (signal {-rc})" if rc < 0 else "")
+            raise RuntimeError(f"{e}; provider front end pid {frontend.pid} {how}") from None
         frontend.stdin.write("stats\n")
         frontend.stdin.flush()
         provider = json.loads(frontend.stdout.readline())

@@ -34,6 +34,7 @@
 #include <string>
 #include <vector>
 
+#include "uda/log.h"
 #include "api_bench.h"
 #include "service/merge_service.h"
 #include "service/node_daemon.h"
@@ -168,8 +169,10 @@ int main(int argc, char** argv) {
   if (argc == 3 && std::string(argv[1]) == "--daemon-fd") {
     const int ctl = std::atoi(argv[2]);
     close_inherited(ctl);
+    uda::install_crash_reporter("uda node daemon");
     return uda::run_node_daemon(ctl);
   }
+  uda::install_crash_reporter("uda_mof_supplier");
   uda::gpu::ApiBenchConfig c;
   c.transport = "tcp";
   c.bind_addr = "127.0.0.1";

@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include "uda/log.h"
 #include "j2c_sink.h"
 #include "uda/node_registry.h"
 #include "uda/uda_bridge.h"
@@ -93,6 +94,7 @@ std::string json_escape(const std::string& s) {
 
 int main(int argc, char** argv) {
   const double t_main = boot_ms();
+  uda::install_crash_reporter("uda_reduce_task");
   const double t_exec = (double)uda::process_start_ticks((int)getpid()) * 1000.0 / (double)sysconf(_SC_CLK_TCK);
   Host host;
   int64_t kv_buf = 1 << 20, expect = -1;

@@ -4,7 +4,9 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <csignal>
 #include <ctime>
+#include <execinfo.h>
 #include <mutex>
 #include <sys/time.h>
 #include <unistd.h>
@@ -26,6 +28,35 @@ const char* sev_name(int s) {
   return (s >= 0 && s <= 6) ? names[s] : "?";
 }
 }  // namespace
+
+namespace {
+char g_who[64] = "uda";
+
+void crash_handler(int sig) {
+  char msg[160];
+  const int n = std::snprintf(msg, sizeof(msg), "%s pid %d: fatal signal %d (%s)\n", g_who, (int)::getpid(), sig,
+                              sig == SIGSEGV ? "SIGSEGV" : sig == SIGBUS ? "SIGBUS" : sig == SIGABRT ? "SIGABRT"
+                              : sig == SIGFPE ? "SIGFPE" : sig == SIGILL ? "SIGILL" : "?");
+  if (n > 0) (void)!::write(2, msg, (size_t)n);
+  void* frames[64];
+  const int k = ::backtrace(frames, 64);
+  ::backtrace_symbols_fd(frames, k, 2);
+  std::signal(sig, SIG_DFL);  // SA_RESETHAND already did; re-raise with the default action
+  ::raise(sig);
+}
+}  // namespace
+
+void install_crash_reporter(const char* who) {
+  std::snprintf(g_who, sizeof(g_who), "%s", who);
+  void* warm[1];
+  (void)::backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = crash_handler;
+  sa.sa_flags = SA_RESETHAND;
+  sigemptyset(&sa.sa_mask);
+  for (int sig : {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT}) ::sigaction(sig, &sa, nullptr);
+}
 
 void log_set_threshold(int s) { g_threshold.store(s < 0 ? 0 : (s > kTrace ? kTrace : s)); }
 int log_threshold() { return g_threshold.load(std::memory_order_relaxed); }

@@ -2332,6 +2332,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       }
       if (got.status != 0) throw UdaError("fetch of " + f.map_id + " failed: " + got.error);
       if (got.sent <= 0) throw UdaError("fetch of " + f.map_id + ": provider sent no data");
+      if (got.part_len != part_len || got.sent > part_len - off)
+        throw UdaError("fetch of " + f.map_id + ": provider's partition length " + std::to_string(got.part_len) +
+                       " differs from the " + std::to_string(part_len) + " bytes expected");
       HIP_CHECK(hipMemcpyAsync(part->own.as<uint8_t>() + off, buf, (size_t)got.sent, hipMemcpyHostToDevice, s));
       HIP_CHECK(hipEventRecord(chunk_ev[slot], s));
       pending[slot] = true;
@@ -2427,6 +2430,10 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         fetch_bytes(batch[i], a.part_len, part.get());
         ++unmapped;
       } else if (a.status == kNotDeviceResident) {
+        // every partition holds at least the IFile EOF marker: a length of 0 is a provider that did not say
+        if (a.part_len < kEofBytes)
+          throw UdaError("fetch of " + batch[i].map_id + ": declined descriptor fetch carries no partition length (" +
+                         std::to_string(a.part_len) + ")");
         fetch_bytes(batch[i], a.part_len, part.get());
       } else {
         throw UdaError("fetch of " + batch[i].map_id + " failed: " + (a.status ? a.error : "no device descriptor"));

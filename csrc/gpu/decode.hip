@@ -337,6 +337,249 @@ __host__ __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
+// ---- LZO1X, lean wave parse (launch_block_decode default for LZO). The r6 PMC pass of the kernels above
+// on TeraSort data (profiles/r6/r6f_pmc_lzo_decode_register_vs_lds.md): ~20 scalar instructions per output
+// byte with the LDS window and the same with the register window, i.e. the window reads were never the
+// cost -- the per-byte 64-bit bounds/window checks, the per-token prefix test and the loop scaffolding of
+// the 64-lane copies were. Here:
+//   * positions are 32-bit offsets from the block's input / output base (a Hadoop block is < 2 GiB),
+//   * a token's bytes come from one 4-byte peek of the register window (two v_readlane) instead of a
+//     checked read per byte: every token of a valid LZO1X stream starts with >= 3 bytes left (the stream
+//     ends with the 3-byte end marker and every literal check keeps that margin), so a token's fixed bytes
+//     need no bounds check; only the zero-run length extensions check as they go,
+//   * literals of up to 64 bytes are copied out of the register window with one ds_bpermute (no global
+//     load, so no load-to-store wait on the parse's path), longer ones by the 64-lane vector copy,
+//   * a match of up to 64 bytes is one masked byte move per lane,
+//   * the prefix decode (clip) is a template parameter, so the full decode pays nothing for it.
+struct LeanWin {
+  uint32_t rw = 0;    // this lane's 4 bytes of the 256-byte window at base
+  uint32_t base = 0;  // chunk-relative offset of window byte 0
+  uint32_t lim = 0;   // bytes [ip, ip + n) are in the window while ip + n <= lim (0: empty)
+};
+
+__device__ __forceinline__ void lean_fill(LeanWin& w, const uint8_t* ib, uint32_t ip, uint32_t ip_end, int lane) {
+  const uint32_t base = ip & ~3u;
+  const uint32_t end = min(base + (uint32_t)kRegWin, ip_end);
+  const uint32_t p = base + 4 * (uint32_t)lane;
+  uint32_t v = 0;
+  if (p + 4 <= end) {
+    v = reinterpret_cast<const U32p*>(ib + p)->v;
+  } else {
+    for (uint32_t k = 0; k < 4; ++k)
+      if (p + k < end) v |= (uint32_t)ib[p + k] << (8 * k);
+  }
+  w.rw = v;
+  w.base = base;
+  // the chunk's last window holds every remaining byte (zeros past the end): never refilled again
+  w.lim = end == ip_end ? 0xFFFFFFFFu : end;
+}
+
+// Bytes ip .. ip+3, little-endian (bytes past the chunk end read as zero).
+__device__ __forceinline__ uint32_t lean_peek4(LeanWin& w, const uint8_t* ib, uint32_t ip, uint32_t ip_end, int lane) {
+  if (ip + 4 > w.lim) lean_fill(w, ib, ip, ip_end, lane);
+  const uint32_t d = ip - w.base;
+  const uint32_t i = (d >> 2) & 63;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)w.rw, (int)i);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)w.rw, (int)((i + 1) & 63));
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (d & 3)));
+}
+
+template <bool P>
+__device__ __forceinline__ void lean_literal(LeanWin& w, const uint8_t* ib, uint8_t* ob, uint32_t op, uint32_t ip,
+                                             uint32_t ip_end, uint32_t len, uint32_t clip, int lane) {
+  if (P) {
+    if (op >= clip) return;
+    len = min(len, clip - op);
+  }
+  if (len == 0) return;
+  if (len <= 64) {
+    if (ip + len > w.lim) lean_fill(w, ib, ip, ip_end, lane);
+    const uint32_t e = ip - w.base + (uint32_t)lane;  // window offset of this lane's byte
+    const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(e & 0xFCu), (int)w.rw);
+    if ((uint32_t)lane < len) ob[op + lane] = (uint8_t)(word >> (8 * (e & 3)));
+  } else {
+    wave_copy(ob + op, ib + ip, len, lane);
+  }
+}
+
+template <bool P>
+__device__ __forceinline__ void lean_match(uint8_t* ob, uint32_t op, uint32_t off, uint32_t len, uint32_t clip,
+                                           uint32_t& flushed, int lane) {
+  if (P) {
+    if (op >= clip) return;
+    len = min(len, clip - op);  // the source bytes below the clip were all written
+  }
+  const uint32_t src = op - off;
+  if (src + min(off, len) > flushed) {  // reads bytes this wave stored since its last fence
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    flushed = op;
+  }
+  if (len <= 64) {
+    if ((uint32_t)lane < len) ob[op + lane] = ob[src + (off >= len ? (uint32_t)lane : (uint32_t)lane % off)];
+  } else if (off >= len) {
+    wave_copy(ob + op, ob + src, len, lane);
+  } else {
+    for (uint32_t i = lane; i < len; i += 64) ob[op + i] = ob[src + i % off];
+  }
+}
+
+// One LZO1X chunk [ip, ip_end) of the block at ib, output at ob + op (block-relative offsets).
+template <bool P>
+__device__ bool lzo_lean_chunk(const uint8_t* ib, uint8_t* ob, uint32_t ip, const uint32_t ip_end, uint32_t op,
+                               const uint32_t oend, const uint32_t clip, uint32_t& flushed, const int lane,
+                               uint32_t* produced) {
+  LeanWin w;
+  const uint32_t out0 = op;
+  uint32_t t = 0, next = 0, state = 0, m_pos = 0, v = 0;
+  if (ip + 3 > ip_end) return false;  // shortest stream: the end marker
+  v = lean_peek4(w, ib, ip, ip_end, lane);
+  if ((v & 0xFF) > 17) {
+    t = (v & 0xFF) - 17;
+    ++ip;
+    if (t < 4) {
+      next = t;
+      goto match_next;
+    }
+    goto literal_run;
+  }
+  for (;;) {
+    // here ip + 3 <= ip_end: the token byte and up to two more are in bounds
+    if (P && op >= clip) {
+      *produced = oend - out0;
+      return true;
+    }
+    v = lean_peek4(w, ib, ip, ip_end, lane);
+    t = v & 0xFF;
+    if (t < 16) {
+      if (state == 0) {
+        ++ip;
+        if (t == 0) {
+          uint32_t b;
+          for (;;) {
+            if (ip >= ip_end) return false;
+            b = lean_peek4(w, ib, ip, ip_end, lane) & 0xFF;
+            if (b != 0) break;
+            t += 255;
+            ++ip;
+          }
+          t += 15 + b;
+          ++ip;
+        }
+        t += 3;
+      literal_run:
+        if (ip + t + 3 > ip_end || op + t > oend) return false;
+        lean_literal<P>(w, ib, ob, op, ip, ip_end, t, clip, lane);
+        op += t;
+        ip += t;
+        state = 4;
+        continue;
+      } else if (state != 4) {  // M1: 2-byte match after 1..3 trailing literals
+        next = t & 3;
+        m_pos = op - 1 - (t >> 2) - (((v >> 8) & 0xFF) << 2);
+        ip += 2;
+        if (m_pos < out0 || m_pos >= op || op + 2 > oend) return false;
+        lean_match<P>(ob, op, op - m_pos, 2, clip, flushed, lane);
+        op += 2;
+        goto match_next;
+      } else {  // M1 after a literal run: 3 bytes, offset 2049..3072
+        next = t & 3;
+        m_pos = op - (1 + 0x0800) - (t >> 2) - (((v >> 8) & 0xFF) << 2);
+        ip += 2;
+        t = 3;
+      }
+    } else if (t >= 64) {  // M2
+      next = t & 3;
+      m_pos = op - 1 - ((t >> 2) & 7) - (((v >> 8) & 0xFF) << 3);
+      ip += 2;
+      t = (t >> 5) + 1;
+    } else {  // M3 (32..63) / M4 (16..31, or the end of the stream)
+      const bool m3 = t >= 32;
+      const uint32_t lmask = m3 ? 31u : 7u;
+      if (!m3) m_pos = op - ((t & 8) << 11);
+      t = (t & lmask) + 2;
+      if (t == 2) {  // zero-run length extension
+        ++ip;
+        uint32_t b;
+        for (;;) {
+          if (ip + 3 > ip_end) return false;  // this byte and the two offset bytes after the run
+          b = lean_peek4(w, ib, ip, ip_end, lane) & 0xFF;
+          if (b != 0) break;
+          t += 255;
+          ++ip;
+        }
+        t += lmask + b;
+        ++ip;
+        next = lean_peek4(w, ib, ip, ip_end, lane) & 0xFFFF;
+        ip += 2;
+      } else {
+        next = (v >> 8) & 0xFFFF;
+        ip += 3;
+      }
+      if (m3) {
+        m_pos = op - 1 - (next >> 2);
+        next &= 3;
+      } else {
+        m_pos -= next >> 2;
+        next &= 3;
+        if (m_pos == op) {
+          *produced = op - out0;
+          return t == 3 && ip == ip_end;
+        }
+        m_pos -= 0x4000;
+      }
+    }
+    // m_pos below 0 wraps above op and fails the second test
+    if (m_pos < out0 || m_pos >= op || op + t > oend) return false;
+    lean_match<P>(ob, op, op - m_pos, t, clip, flushed, lane);
+    op += t;
+  match_next:
+    state = next;
+    t = next;
+    if (ip + t + 3 > ip_end || op + t > oend) return false;
+    lean_literal<P>(w, ib, ob, op, ip, ip_end, t, clip, lane);
+    op += t;
+    ip += t;
+  }
+}
+
+template <bool P>
+__global__ void __launch_bounds__(64 * kWavesPerBlock)
+    lzo_lean_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status, int64_t clip_in) {
+  const int b = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (b >= n) return;
+  const DecodeDesc d = descs[b];
+  const int lane = threadIdx.x & 63;
+  const uint8_t* ib = in + d.src;
+  uint8_t* ob = out + d.dst;
+  const int64_t ilen = d.src_end - d.src;
+  bool ok = ilen >= 0 && ilen < (1ll << 31) && d.raw >= 0 && d.raw < (1ll << 31);
+  const uint32_t ie = ok ? (uint32_t)ilen : 0, oend = ok ? (uint32_t)d.raw : 0;
+  const uint32_t clip = P ? (uint32_t)min(clip_in, (int64_t)oend) : oend;
+  uint32_t ip = 0, op = 0, flushed = 0;
+  // one block = one or more [u32 BE compressed_len][chunk] records until its raw bytes are produced
+  while (ok && op < oend) {
+    if (P && op >= clip) return;  // prefix decode done
+    if (ip + 4 > ie) {
+      ok = false;
+      break;
+    }
+    const uint32_t clen = be32(ib + ip);
+    ip += 4;
+    if (clen > ie - ip) {
+      ok = false;
+      break;
+    }
+    uint32_t produced = 0;
+    ok = lzo_lean_chunk<P>(ib, ob, ip, ip + clen, op, oend, clip, flushed, lane, &produced);
+    ip += clen;
+    op += produced;
+  }
+  if (ok && (op != oend || ip != ie)) ok = false;
+  if (!ok && lane == 0) atomicOr(status, 1);
+}
+
 // clip > 0: prefix decode. Only the first `clip` bytes of each block's output (at d.dst) are written and
 // the decode stops once they are out; d.raw stays the block's full raw size for the format checks.
 template <int kCodec, bool R>
@@ -710,9 +953,17 @@ void launch_block_decode(int codec, const uint8_t* in, uint8_t* out, const Decod
   // read per launch: tests compare the kernels in one process
   const char* le = std::getenv("UDA_LZO_LANE");  // 1: one lane per LZO block (too few blocks per round to hide latency)
   const bool lzo_lane = le && std::atoi(le) != 0;
-  const char* we = std::getenv("UDA_DECODE_WINDOW");  // "lds": the LDS window of round 5
+  // "lds": the LDS window of round 5; "reg": the register window with the per-byte parse (LZO; Snappy's
+  // default); unset: the lean LZO parse
+  const char* we = std::getenv("UDA_DECODE_WINDOW");
   const bool reg = !we || std::string(we) != "lds";
-  if (codec == 1 && reg)
+  const bool lean = !we || !*we;
+  if (codec == 2 && lean && !lzo_lane) {
+    if (clip > 0)
+      lzo_lean_kernel<true><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+    else
+      lzo_lean_kernel<false><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
+  } else if (codec == 1 && reg)
     block_decode_kernel<1, true><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);
   else if (codec == 1)
     block_decode_kernel<1, false><<<grid, 64 * kWavesPerBlock, 0, s>>>(in, out, descs, n, status, clip);

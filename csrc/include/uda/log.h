@@ -32,6 +32,12 @@ void log_set_sink(LogSink sink, void* ctx);
 bool log_open_file(const std::string& dir, const std::string& role);
 void log_close_file();
 
+// Executables (never a library hosted by a JVM, which owns these signals): on SIGSEGV / SIGBUS / SIGILL /
+// SIGFPE / SIGABRT write "<who> pid N: fatal signal S" and a raw backtrace to stderr, then die of the
+// same signal. A process that dies silently (no exception text) otherwise leaves only "connection lost"
+// at its peers.
+void install_crash_reporter(const char* who);
+
 void log_write(int severity, const char* file, int line, const char* func, const char* fmt, ...)
     __attribute__((format(printf, 5, 6)));
 

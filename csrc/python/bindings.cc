@@ -1016,6 +1016,29 @@ PYBIND11_MODULE(_uda_native, m) {
   });
   // one TCP client, a fetch to an unreachable host on one thread and, while it is still trying, one to a
   // live host: returns (live fetch ms, dead host error, dead host ms, second dead fetch ms)
+  // ACK string codec (transport.h): format then parse, as a TCP reducer sees the provider's answer
+  m.def("ack_roundtrip", [](int status, int64_t raw_len, int64_t part_len, int64_t sent, int64_t mof_offset,
+                            const std::string& path, const std::string& error) {
+    uda::FetchAck a;
+    a.status = status;
+    a.raw_len = raw_len;
+    a.part_len = part_len;
+    a.sent = sent;
+    a.mof_offset = mof_offset;
+    a.path = path;
+    a.error = error;
+    uda::FetchAck b;
+    if (!uda::parse_ack(uda::format_ack(a), &b)) throw std::runtime_error("ack does not parse");
+    py::dict d;
+    d["status"] = b.status;
+    d["raw_len"] = b.raw_len;
+    d["part_len"] = b.part_len;
+    d["sent"] = b.sent;
+    d["mof_offset"] = b.mof_offset;
+    d["path"] = b.path;
+    d["error"] = b.error;
+    return d;
+  });
   m.def("tcp_dead_host_probe", [](const std::string& live, const std::string& dead, int port, const std::string& job,
                                   const std::string& map, int reduce, int64_t size) {
     py::gil_scoped_release rel;

@@ -62,8 +62,13 @@ bool parse_rts(const std::string& s, FetchRequest* r, uint64_t* remote_addr, uin
   return true;
 }
 
+// An error ack keeps the partition's lengths when the provider knows them: a declined descriptor fetch
+// (kNotDeviceResident) tells the reducer how many bytes to fetch instead. E:status:raw:part:offset:error
+// (the error last: it may contain ':').
 std::string format_ack(const FetchAck& a) {
-  if (a.status != 0) return "E:" + std::to_string(a.status) + ":" + a.error + ":";
+  if (a.status != 0)
+    return "E:" + std::to_string(a.status) + ":" + std::to_string(a.raw_len) + ":" + std::to_string(a.part_len) + ":" +
+           std::to_string(a.mof_offset) + ":" + a.error;
   return std::to_string(a.raw_len) + ":" + std::to_string(a.part_len) + ":" + std::to_string(a.sent) + ":" +
          std::to_string(a.mof_offset) + ":" + a.path + ":";
 }
@@ -71,9 +76,15 @@ std::string format_ack(const FetchAck& a) {
 bool parse_ack(const std::string& s, FetchAck* a) {
   if (s.rfind("E:", 0) == 0) {
     auto f = split(s, ':');
-    a->status = f.size() > 1 ? (int)to_i64(f[1]) : -1;
+    if (f.size() < 6) return false;
+    a->status = (int)to_i64(f[1]);
     if (a->status == 0) a->status = -1;
-    a->error = f.size() > 2 ? f[2] : "";
+    a->raw_len = to_i64(f[2]);
+    a->part_len = to_i64(f[3]);
+    a->mof_offset = to_i64(f[4]);
+    std::string e = f[5];
+    for (size_t i = 6; i < f.size(); ++i) e += ":" + f[i];
+    a->error = e;
     return true;
   }
   auto f = split(s, ':');

@@ -276,3 +276,17 @@ def test_tcp_dead_host_does_not_delay_live_hosts(native, tmp_path):
         assert dead2_ms < 200, dead2_ms  # backoff: fails at once
     finally:
         p.close()
+
+
+def test_declined_descriptor_ack_keeps_partition_lengths(native):
+    """A provider declining a descriptor fetch (kNotDeviceResident, -12: its HBM store is full) answers
+    with the partition's lengths, so the reducer knows how many bytes to fetch instead. Over TCP the
+    error ack used to carry only the status and text: 23 of 32 partitions were then "fetched" as 0
+    bytes and the merged output silently lacked them (r6 node run with a store smaller than the MOFs)."""
+    got = native.ack_roundtrip(-12, 1000, 993, 0, 4096, "", "provider HBM store: full: 3.0 of 3.0 GB held")
+    assert got["status"] == -12 and got["part_len"] == 993 and got["raw_len"] == 1000 and got["mof_offset"] == 4096
+    assert got["error"] == "provider HBM store: full: 3.0 of 3.0 GB held"  # the text may contain ':'
+    ok = native.ack_roundtrip(0, 10, 8, 8, 0, "/a:b/file.out", "")
+    assert (ok["status"], ok["part_len"], ok["sent"], ok["path"]) == (0, 8, 8, "/a:b/file.out")
+    err = native.ack_roundtrip(-2, 0, 0, 0, 0, "", "cannot resolve MOF j/m/0")
+    assert err["status"] == -2 and err["error"] == "cannot resolve MOF j/m/0"

@@ -118,12 +118,13 @@ def test_lzo1x_spec_vectors_on_device(require_gpu, native):
     assert outs == [want for _, _, want in VECTORS]
 
 
-@pytest.mark.parametrize("env", [{}, {"UDA_DECODE_WINDOW": "lds"}, {"UDA_LZO_LANE": "1"}],
-                         ids=["wave-register-window", "wave-lds-window", "lane-per-block"])
+@pytest.mark.parametrize("env", [{}, {"UDA_DECODE_WINDOW": "reg"}, {"UDA_DECODE_WINDOW": "lds"}, {"UDA_LZO_LANE": "1"}],
+                         ids=["wave-lean", "wave-register-window", "wave-lds-window", "lane-per-block"])
 @pytest.mark.parametrize("codec", ["lzo", "snappy"])
 def test_decode_kernels_agree_on_terasort_records(require_gpu, native, monkeypatch, env, codec):
-    """Every device decode kernel -- one wave per block parsing from a register window (default) or from
-    the LDS window of round 5, and for LZO one lane per block -- decodes TeraSort-shaped IFile records
+    """Every device decode kernel -- one wave per block parsing from a register window (LZO: the lean
+    parse by default, the per-byte parse with "reg"; Snappy: the register window for both) or from the LDS
+    window of round 5, and for LZO one lane per block -- decodes TeraSort-shaped IFile records
     (random keys, 26-letter values: streams of many 3-4 byte tokens) and every other payload to the
     original bytes, and reports a corrupt block."""
     if codec == "snappy" and "UDA_LZO_LANE" in env:

@@ -151,6 +151,14 @@ RECIPES: dict[str, tuple[int, str]] = {
                            "-d gpurun_out/pmc_lzo41_lds -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
                            "--steps 1 --warmup 0"),
     "ipc8_detail": (700, f"{PY} bench.py --gpus 8 --one-gpu --exchange ipc --rows-per-gpu 240000000 --steps 2 --warmup 1"),
+    "nodefiles10_store3": (400, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 100000000 "
+                                f"--provider-hbm-gb 3 --steps 1 --warmup 1"),
+    "nodefiles10": (400, f"{PY} bench.py --api --node --mof-dir /tmp --reducers 15 --rows-per-gpu 100000000 --steps 1 --warmup 1"),
+    "lzo130x5_reg": (600, f"UDA_DECODE_WINDOW=reg {PY} bench.py --api --api-codec lzo --steps 5 --warmup 1 --verbose"),
+    "pmc_lzo41_lean": (300, "timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS "
+                            "SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv "
+                            "-d gpurun_out/pmc_lzo41_lean -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
+                            "--steps 1 --warmup 0"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }
