@@ -89,6 +89,7 @@ struct SpillRun {
 struct DeviceWorkspace {
   int64_t pool_key = 0;  // input bytes of the task that last used it (DevicePool::acquire_fit)
   gpu::DeviceBuffer in, out, packed, out2;  // out2: second output of the generic key-range rounds
+  gpu::DeviceBuffer fetched;  // device fetch: bytes of the partitions the providers declined as descriptors
   gpu::GenericMerger merger;
   gpu::DeviceBlockDecoder decoder;
   gpu::PinnedBuffer ring;          // 2 x kPieceBytes, D2H staging of merged output
@@ -122,7 +123,8 @@ struct DeviceWorkspace {
     if ((int64_t)b.size() < bytes) b.alloc_local((size_t)(bytes + bytes / 8));
   }
   int64_t device_bytes() const {
-    return (int64_t)(in.held() + out.held() + packed.held() + out2.held() + frame_scratch.held() + frame_descs.held()) +
+    return (int64_t)(in.held() + out.held() + packed.held() + out2.held() + fetched.held() + frame_scratch.held() +
+                     frame_descs.held()) +
            merger.workspace_bytes();
   }
 };
@@ -2223,6 +2225,156 @@ void ReduceTask::merge_gpu() {
   }
 }
 
+// The partitions a device-fetch task gets no usable descriptor for (the provider's HBM store is full or
+// off, or the descriptor cannot be mapped here): `streams` workers (mapred.uda.gpu.fetch.bytes.streams,
+// default 4, one per TCP connection of the task's transport) each take partitions in turn and keep three
+// requests of `chunk` bytes (mapred.uda.gpu.fetch.bytes.chunk, default 8 MiB) in flight into pinned slots,
+// each landed chunk going on to the device (H2D on the worker's stream) while the next ones come in. The
+// round-5 loop had one request of the task's buffer size (1 MiB) in flight at a time: a round trip per
+// MiB, 3.3 GB/s per task and 20 GB/s for a node of 15 tasks with 42.9 GB of 62.4 GB declined per wave
+// (profiles/r6/r6j_nodefiles62_store20.log). The reference's fetcher keeps its requests in flight the
+// same way (Segment::send_request, src/Merger/StreamRW.cc; RDMAClient::start_fetch_req).
+int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::function<FetchParams(size_t)>& params,
+                                         const std::function<int64_t(size_t)>& len, gpu::DeviceBuffer& dst,
+                                         const std::function<void(size_t, const uint8_t*)>& placed) {
+  std::vector<int64_t> at(n + 1, 0);
+  for (size_t k = 0; k < n; ++k) at[k + 1] = at[k] + ((len(k) + 255) & ~(int64_t)255);
+  DeviceWorkspace::ensure(dst, at[n]);
+  uint8_t* base = dst.as<uint8_t>();
+  for (size_t k = 0; k < n; ++k) placed(k, base + at[k]);
+  const int streams = (int)std::clamp<int64_t>(host_->conf_i64("mapred.uda.gpu.fetch.bytes.streams", 4), 1, 16);
+  int64_t chunk = std::max<int64_t>(buffer_size_, host_->conf_i64("mapred.uda.gpu.fetch.bytes.chunk", 8ll << 20));
+  chunk = (chunk + 4095) & ~(int64_t)4095;
+  constexpr int kSlots = 3;
+  std::atomic<size_t> next{0};
+  std::atomic<int64_t> fetched{0};
+  std::mutex em;
+  std::string err;
+  auto failed = [&] {
+    std::lock_guard<std::mutex> g(em);
+    return !err.empty();
+  };
+  auto worker = [&] {
+    struct Slot {
+      gpu::PinnedPool::Block b;
+      hipEvent_t ev = nullptr;
+      bool h2d = false;   // an H2D from this slot may still be reading it
+      bool busy = false;  // a request into this slot is in flight
+      bool done = false;
+      int64_t off = 0, want = 0;
+      FetchAck a;
+    };
+    Slot sl[kSlots];
+    std::mutex m;
+    std::condition_variable cv;
+    hipStream_t hs = nullptr;
+    auto drain = [&] {  // every request answered (their callbacks touch sl), every H2D done
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait(lk, [&] {
+        for (auto& x : sl)
+          if (x.busy && !x.done) return false;
+        return true;
+      });
+      lk.unlock();
+      if (hs) (void)hipStreamSynchronize(hs);
+    };
+    try {
+      HIP_CHECK(hipSetDevice(device));
+      hs = gpu::pooled_stream();
+      for (auto& x : sl) {
+        x.b = gpu::PinnedPool::instance().acquire((size_t)chunk);
+        HIP_CHECK(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+      }
+      for (;;) {
+        const size_t k = next.fetch_add(1);
+        if (k >= n || failed() || stop_) break;
+        const FetchParams f = params(k);
+        const int64_t L = len(k);
+        uint8_t* dev = base + at[k];
+        int64_t issue_off = 0;
+        int outstanding = 0, head = 0, tail = 0;  // slots in request order: tail (oldest) .. head
+        auto issue = [&](int s) {
+          Slot& x = sl[s];
+          if (x.h2d) {
+            HIP_CHECK(hipEventSynchronize(x.ev));
+            x.h2d = false;
+          }
+          FetchRequest req;
+          req.job_id = f.job_id;
+          req.map_id = f.map_id;
+          req.reduce_id = f.reduce_id;
+          req.fetched = issue_off;
+          req.buf_len = chunk;
+          {
+            std::lock_guard<std::mutex> g(m);
+            x.busy = true;
+            x.done = false;
+            x.off = issue_off;
+            x.want = std::min(chunk, L - issue_off);
+          }
+          issue_off += x.want;
+          ++outstanding;
+          fetch_begin();
+          transport_->fetch(f.host, req, x.b.p, [&, s](const FetchAck& a) {
+            {
+              // notify under the lock: once drain() sees every answer the worker's frame (m, cv) goes away
+              std::lock_guard<std::mutex> g(m);
+              sl[s].a = a;
+              sl[s].done = true;
+              cv.notify_all();
+            }
+            fetch_end();
+          });
+        };
+        while (outstanding < kSlots && issue_off < L) {
+          issue(head);
+          head = (head + 1) % kSlots;
+        }
+        while (outstanding > 0) {
+          Slot& x = sl[tail];
+          {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return x.done; });
+            x.busy = false;
+          }
+          --outstanding;
+          if (x.a.status != 0) throw UdaError("fetch of " + f.map_id + " failed: " + x.a.error);
+          if (x.a.sent != x.want || x.a.part_len != L)
+            throw UdaError("fetch of " + f.map_id + ": provider sent " + std::to_string(x.a.sent) + " bytes of a " +
+                           std::to_string(x.a.part_len) + "-byte partition at offset " + std::to_string(x.off) +
+                           " (expected " + std::to_string(x.want) + " of " + std::to_string(L) + ")");
+          HIP_CHECK(hipMemcpyAsync(dev + x.off, x.b.p, (size_t)x.want, hipMemcpyHostToDevice, hs));
+          HIP_CHECK(hipEventRecord(x.ev, hs));
+          x.h2d = true;
+          fetched += x.want;
+          tail = (tail + 1) % kSlots;
+          if (issue_off < L) {
+            issue(head);
+            head = (head + 1) % kSlots;
+          }
+        }
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(em);
+      if (err.empty()) err = e.what();
+    }
+    drain();
+    for (auto& x : sl) {
+      if (x.ev) (void)hipEventDestroy(x.ev);
+      if (x.b.p) gpu::PinnedPool::instance().release(x.b);
+    }
+    if (hs) gpu::return_stream(hs);
+  };
+  std::vector<std::thread> ts;
+  const int nw = (int)std::min<size_t>((size_t)streams, n);
+  for (int i = 1; i < nw; ++i) ts.emplace_back(worker);
+  worker();
+  for (auto& t : ts) t.join();
+  if (!err.empty()) throw UdaError(err);
+  if (stop_) throw UdaError("reduce task stopped during fetch");
+  return fetched.load();
+}
+
 // GPU backend, device fetch (mapred.uda.gpu.fetch=device, uncompressed map outputs): every FETCH is
 // a descriptor fetch, so partitions the provider holds in HBM are merged where they live (same
 // process: the address; another process on the node: an IPC mapping) and never cross PCIe on the
@@ -2278,72 +2430,17 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   struct Part {
     const uint8_t* dptr = nullptr;
     int64_t part_len = 0;
-    gpu::DeviceBuffer own;  // bytes fetched from a host-resident MOF
   };
   std::vector<std::unique_ptr<Part>> parts;
   int64_t host_bytes = 0, descriptors = 0, unmapped = 0;
-  gpu::PinnedBuffer chunk;
-
-  // bytes of a MOF the provider does not hold in device memory: chunked fetches into two pinned
-  // chunks, each chunk's H2D (async on `s`) overlapping the fetch of the next one
-  hipEvent_t chunk_ev[2] = {nullptr, nullptr};
-  struct EvGuard {
-    hipEvent_t* e;
-    ~EvGuard() {
-      for (int i = 0; i < 2; ++i)
-        if (e[i]) (void)hipEventDestroy(e[i]);
-    }
-  } chunk_ev_guard{chunk_ev};
-  gpu::PinnedBuffer chunk2;
-  auto fetch_bytes = [&](const FetchParams& f, int64_t part_len, Part* part) {
-    part->own.alloc((size_t)std::max<int64_t>(part_len, 16));
-    part->dptr = part->own.as<uint8_t>();
-    part->part_len = part_len;
-    if (chunk.size() < (size_t)buffer_size_) chunk.alloc((size_t)buffer_size_);
-    if (chunk2.size() < (size_t)buffer_size_) chunk2.alloc((size_t)buffer_size_);
-    for (auto& e : chunk_ev)
-      if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    bool pending[2] = {false, false};
-    int slot = 0;
-    for (int64_t off = 0; off < part_len;) {
-      uint8_t* buf = slot ? chunk2.as<uint8_t>() : chunk.as<uint8_t>();
-      if (pending[slot]) HIP_CHECK(hipEventSynchronize(chunk_ev[slot]));  // its previous H2D read it
-      FetchRequest req;
-      req.job_id = f.job_id;
-      req.map_id = f.map_id;
-      req.reduce_id = f.reduce_id;
-      req.fetched = off;
-      req.buf_len = buffer_size_;
-      std::mutex m;
-      std::condition_variable c;
-      bool done = false;
-      FetchAck got;
-      fetch_begin();
-      transport_->fetch(f.host, req, buf, [&](const FetchAck& a) {
-        std::lock_guard<std::mutex> g(m);
-        got = a;
-        done = true;
-        c.notify_all();
-        fetch_end();
-      });
-      {
-        std::unique_lock<std::mutex> lk(m);
-        c.wait(lk, [&] { return done; });
-      }
-      if (got.status != 0) throw UdaError("fetch of " + f.map_id + " failed: " + got.error);
-      if (got.sent <= 0) throw UdaError("fetch of " + f.map_id + ": provider sent no data");
-      if (got.part_len != part_len || got.sent > part_len - off)
-        throw UdaError("fetch of " + f.map_id + ": provider's partition length " + std::to_string(got.part_len) +
-                       " differs from the " + std::to_string(part_len) + " bytes expected");
-      HIP_CHECK(hipMemcpyAsync(part->own.as<uint8_t>() + off, buf, (size_t)got.sent, hipMemcpyHostToDevice, s));
-      HIP_CHECK(hipEventRecord(chunk_ev[slot], s));
-      pending[slot] = true;
-      off += got.sent;
-      host_bytes += got.sent;
-      slot ^= 1;
-    }
-    HIP_CHECK(hipStreamSynchronize(s));
+  // partitions answered "not device-resident" (or with a descriptor this process cannot map): their
+  // bytes are fetched once every descriptor answer is in (fetch_declined, below)
+  struct Declined {
+    FetchParams f;
+    int64_t len;
+    size_t part;  // index into parts
   };
+  std::vector<Declined> declined;
 
   // ---- fetch phase: descriptors for every MOF as its FETCH arrives
   int resolved = 0;
@@ -2427,14 +2524,18 @@ bool ReduceTask::merge_gpu_device(bool probe) {
           std::lock_guard<std::mutex> g(st_mu_);
           st_.unmapped_reason = why;
         }
-        fetch_bytes(batch[i], a.part_len, part.get());
+        if (a.part_len < kEofBytes)
+          throw UdaError("fetch of " + batch[i].map_id + ": descriptor answer carries no partition length");
+        part->part_len = a.part_len;
+        declined.push_back(Declined{batch[i], a.part_len, parts.size()});
         ++unmapped;
       } else if (a.status == kNotDeviceResident) {
         // every partition holds at least the IFile EOF marker: a length of 0 is a provider that did not say
         if (a.part_len < kEofBytes)
           throw UdaError("fetch of " + batch[i].map_id + ": declined descriptor fetch carries no partition length (" +
                          std::to_string(a.part_len) + ")");
-        fetch_bytes(batch[i], a.part_len, part.get());
+        part->part_len = a.part_len;
+        declined.push_back(Declined{batch[i], a.part_len, parts.size()});
       } else {
         throw UdaError("fetch of " + batch[i].map_id + " failed: " + (a.status ? a.error : "no device descriptor"));
       }
@@ -2453,13 +2554,12 @@ bool ReduceTask::merge_gpu_device(bool probe) {
       }
     }
   }
-  const double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  double fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   HIP_PENDING("the end of the descriptor fetch");
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.device_descriptors = descriptors;
     st_.unmapped_descriptors = unmapped;
-    st_.host_fetched_bytes = host_bytes;
   }
 
   auto sink = [&](const uint8_t* p, int64_t len) -> int {
@@ -2479,6 +2579,17 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
   HIP_PENDING("the merge workspace");
+  if (!declined.empty()) {
+    const auto tf = std::chrono::steady_clock::now();
+    host_bytes = fetch_declined_bytes(device, declined.size(), [&](size_t k) { return declined[k].f; },
+                                      [&](size_t k) { return declined[k].len; }, ws.fetched,
+                                      [&](size_t k, const uint8_t* p) { parts[declined[k].part]->dptr = p; });
+    fetch_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
+  }
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.host_fetched_bytes = host_bytes;
+  }
   // HBM admission (gpu/hbm_ledger.h): the task's device working set -- decoded partitions, the
   // key-range round's output slots and merge tables -- is reserved before it is allocated, under the
   // device's byte budget shared with the provider's store and every other task on the node. A round

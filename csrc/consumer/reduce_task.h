@@ -31,6 +31,9 @@
 namespace uda {
 
 class MofFetcher;
+namespace gpu {
+class DeviceBuffer;
+}
 
 // Map task id of a map attempt id (drops the trailing "_<attempt>").
 std::string map_task_of(const std::string& attempt);
@@ -138,6 +141,11 @@ class ReduceTask {
   // Device fetch (descriptors, merge in place). probe: return false before consuming anything if the
   // first MOFs are not device-resident (the caller then runs merge_gpu()).
   bool merge_gpu_device(bool probe);
+  // Device fetch: the bytes of n partitions the providers would not answer with a descriptor, into one
+  // device buffer (grown as needed; placed(k, p): partition k landed at p). Returns the bytes fetched.
+  int64_t fetch_declined_bytes(int device, size_t n, const std::function<FetchParams(size_t)>& params,
+                               const std::function<int64_t(size_t)>& len, gpu::DeviceBuffer& dst,
+                               const std::function<void(size_t, const uint8_t*)>& placed);
   // Tell every provider in `hosts` that `holder` (this task) is done with its descriptors.
   void release_descriptors(const std::set<std::string>& hosts, const std::string& holder);
   // GPU backend: started at INIT on prewarm_thr_ (mapred.uda.gpu.prewarm): HIP context, SDMA engine,

@@ -547,7 +547,10 @@ __device__ bool lzo_lean_chunk(const uint8_t* ib, uint8_t* ob, uint32_t ip, cons
 template <bool P>
 __global__ void __launch_bounds__(64 * kWavesPerBlock)
     lzo_lean_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status, int64_t clip_in) {
-  const int b = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  // wave-uniform by construction, but the compiler's divergence analysis cannot see through
+  // threadIdx.x >> 6: say so, or every value derived from the descriptor -- the whole parse -- lives in
+  // VGPRs with exec-masked branches instead of SGPRs and scalar branches
+  const int b = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (b >= n) return;
   const DecodeDesc d = descs[b];
   const int lane = threadIdx.x & 63;
@@ -586,7 +589,7 @@ template <int kCodec, bool R>
 __global__ void __launch_bounds__(64 * kWavesPerBlock)
     block_decode_kernel(const uint8_t* in, uint8_t* out, const DecodeDesc* descs, int n, int* status, int64_t clip) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[R ? 1 : kWavesPerBlock][R ? 16 : kWin + 16];
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (see lzo_lean_kernel)
   const int b = blockIdx.x * kWavesPerBlock + wid;
   if (b >= n) return;
   const DecodeDesc d = descs[b];

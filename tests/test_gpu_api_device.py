@@ -290,6 +290,35 @@ def test_provider_hbm_store_budget_falls_back_to_bytes(require_gpu, tmp_path):
         p.close()
 
 
+@pytest.mark.parametrize("streams", [1, 3])
+def test_provider_hbm_store_declines_over_tcp(require_gpu, tmp_path, streams):
+    """As above, over TCP: a declined descriptor answer carries the partition's length on the wire, and
+    the declined partitions' bytes come in pipelined chunk requests (mapred.uda.gpu.fetch.bytes.*; here
+    16 KiB chunks, ~26 per partition) from `streams` workers. The round-5 TCP error ack dropped the
+    length and the declined partitions were merged as empty."""
+    import socket
+    maps = datagen.terasort(num_maps=6, reducers=1, rows_per_map=4000, seed=29)
+    size = len(datagen.streams(maps)[0][0]) + 64
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    p = UdaProvider(conf={"mapred.uda.provider.hbm.bytes": 3 * size}, transport="tcp", data_port=port)
+    try:
+        ids = _publish_files(p, tmp_path, "job_9_0102", maps)
+        conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.fetch.bytes.streams": streams,
+                            "mapred.uda.gpu.fetch.bytes.chunk": 16384})
+        recs, st, _ = run_reduce("127.0.0.1", "job_9_0102", ids, 0, datagen.TEXT, conf=conf, transport="tcp",
+                                 data_port=port, max_buf_kb=16)
+        assert recs == expected(maps, 0, datagen.TEXT)
+        hs = json.loads(p.stats())["hbm_store"]
+        assert 0 < hs["loads"] < 6 and hs["declined"] > 0, hs
+        want_bytes = sum(len(part[0]) for part in datagen.streams(maps))
+        assert st["device_descriptors"] == hs["loads"] and st["host_fetched_bytes"] > 0, st
+        assert st["maps_fetched"] == 6 and st["bytes_fetched"] == want_bytes, st
+    finally:
+        p.close()
+
+
 def test_bench_api_mof_files(require_gpu, tmp_path):
     """bench.py --api --mof-dir: TeraSort with Hadoop-written MOF files through the C ABI."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--mof-dir", str(tmp_path), "--rows-per-gpu",
