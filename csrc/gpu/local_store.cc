@@ -33,6 +33,7 @@ class LocalDeviceStore : public DeviceStore {
     co.devices = o.devices;
     co.odirect = true;
     co.lease_s = o.lease_s;
+    co.idle_evict_s = o.idle_evict_s;
     cache_ = std::make_unique<gpu::MofCache>(co);
     cache_->start_loaders();  // the loaders come up now, not under the first wave
   }

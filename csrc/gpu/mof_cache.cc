@@ -163,14 +163,19 @@ void MofCache::erase_entry(const std::string& path) {
   entries_.erase(it);  // the HBM goes when the last in-flight chunk of it is done
 }
 
-bool MofCache::make_room(int device, int64_t bytes, double now) {
+bool MofCache::make_room(int device, int64_t bytes, double now, const std::string& job) {
   if (bytes > per_device_) return false;
   while (used_[device] + bytes > per_device_) {
-    // finished jobs first, then unreferenced entries, least recently served first
+    // finished jobs first, then unreferenced entries, least recently served first; an entry of the same
+    // job (still running) only once idle (Options::idle_evict_s)
     std::shared_ptr<Entry> victim;
     for (auto& kv : entries_) {
       Entry& e = *kv.second;
+      const int64_t reaped = st_.holders_reaped;
       if (e.device != device || !evictable(e, now)) continue;
+      if (!e.job_done && e.job == job && opt_.idle_evict_s > 0 && now - e.last_served < opt_.idle_evict_s &&
+          st_.holders_reaped == reaped)  // (an entry whose holder just turned out dead is fair game)
+        continue;
       if (!victim || (e.job_done && !victim->job_done) ||
           (e.job_done == victim->job_done && e.last_served < victim->last_served))
         victim = kv.second;
@@ -260,8 +265,8 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
     st_.declined++;
     return false;
   }
-  if (!make_room(device, std::max<int64_t>(len, 1), now)) {
-    if (why) *why = "provider HBM budget exhausted (every resident MOF is held by a reducer)";
+  if (!make_room(device, std::max<int64_t>(len, 1), now, job)) {
+    if (why) *why = "provider HBM budget exhausted (every resident MOF is held by a reducer or recently served to its job)";
     st_.declined++;
     return false;
   }

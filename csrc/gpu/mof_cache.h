@@ -58,6 +58,13 @@ class MofCache {
     int64_t read_bytes = 0;          // disk request size a chunk is read in (0: one read per chunk)
     bool odirect = true;
     double lease_s = 600;            // a holder on another node idle this long is presumed dead
+    // An unreferenced entry is evicted to admit another file of ITS OWN job only after this many seconds
+    // without a fetch (mapred.uda.provider.hbm.idle.evict.s; 0: plain LRU). A job whose MOFs outgrow the
+    // store reads them in waves of reduce tasks, each wave every file in order: LRU then evicted the files
+    // the next wave starts with to load the ones it ends with, and reloaded 15 GB of a 20 GB store every
+    // wave (r6 node run, 62 GB of MOFs). Entries of finished jobs, of other jobs and of dead holders go
+    // as before.
+    double idle_evict_s = 0;
   };
   struct Ref {
     const uint8_t* data = nullptr;  // device address of the file's first byte
@@ -145,7 +152,8 @@ class MofCache {
     std::string why;
   };
 
-  bool make_room(int device, int64_t bytes, double now);  // mu_ held: evict until `bytes` fit
+  // mu_ held: evict until `bytes` fit (for a file of `job`)
+  bool make_room(int device, int64_t bytes, double now, const std::string& job);
   bool evictable(Entry& e, double now);                   // mu_ held (reaps dead holders)
   void erase_entry(const std::string& path);              // mu_ held
   Ref ref_of(const Entry& e) const;

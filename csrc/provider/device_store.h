@@ -38,6 +38,7 @@ struct LocalStoreOptions {
   int64_t capacity = 0;  // bytes over all devices
   std::vector<int> devices{0};
   double lease_s = 600;
+  double idle_evict_s = 0;  // gpu::MofCache::Options::idle_evict_s
 };
 // The store in this process (gpu/mof_cache.h).
 std::unique_ptr<DeviceStore> make_local_device_store(const LocalStoreOptions& o);

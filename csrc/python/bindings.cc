@@ -912,16 +912,18 @@ PYBIND11_MODULE(_uda_native, m) {
   // ---------------------------------------------------------------- GPU engine
   // the provider's HBM store of MOF files on its own (gpu/mof_cache.h): loads, holders, eviction
   py::class_<gpu::MofCache>(m, "MofStore")
-      .def(py::init([](int64_t capacity, std::vector<int> devices, double lease_s, int64_t chunk_bytes) {
+      .def(py::init([](int64_t capacity, std::vector<int> devices, double lease_s, int64_t chunk_bytes,
+                       double idle_evict_s) {
              gpu::MofCache::Options o;
              o.capacity = capacity;
              o.devices = devices;
              o.lease_s = lease_s;
              o.chunk_bytes = chunk_bytes;
+             o.idle_evict_s = idle_evict_s;
              return new gpu::MofCache(o);
            }),
            py::arg("capacity"), py::arg("devices") = std::vector<int>{0}, py::arg("lease_s") = 600.0,
-           py::arg("chunk_bytes") = 16 << 20)
+           py::arg("chunk_bytes") = 16 << 20, py::arg("idle_evict_s") = 0.0)
       .def("acquire",
            [](gpu::MofCache& c, const std::string& job, const std::string& path, const std::string& holder) {
              gpu::MofCache::Ref r;

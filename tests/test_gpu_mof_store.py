@@ -56,6 +56,29 @@ def test_held_entry_outlives_its_lease_under_budget_pressure(require_gpu, native
     assert st["evictions"] == 1 and st["releases"] == 1 and st["loads"] == 3, st
 
 
+def test_a_job_does_not_evict_its_own_recently_served_files(require_gpu, native, tmp_path):
+    """mapred.uda.provider.hbm.idle.evict.s: a job whose MOFs outgrow the store reads them in waves; a file
+    it was served recently is not evicted to load another of its files (the next wave would reload it),
+    while another job, or the same job once the file has been idle that long, may take the space."""
+    size = 8 * MB
+    f = _files(tmp_path, 4, size)
+    store = native.MofStore(capacity=2 * size + MB, devices=[0], idle_evict_s=0.6)
+    for p in f[:2]:
+        assert store.acquire("j", p, "a")[0]
+        store.release(p, "a")
+    ok, why, _, _, _ = store.acquire("j", f[2], "b")
+    assert not ok and "recently served" in why, why
+    ok, why, _, _, _ = store.acquire("k", f[3], "c")  # another job: the LRU file of j goes
+    assert ok, why
+    assert store.stats()["evictions"] == 1
+    time.sleep(0.8)
+    ok, why, a2, _, _ = store.acquire("j", f[2], "b")  # j's remaining file has been idle long enough
+    assert ok, why
+    assert native.device_read(a2, size) == open(f[2], "rb").read()
+    st = store.stats()
+    assert st["evictions"] == 2 and st["declined"] == 1, st
+
+
 def test_dead_or_foreign_holders_are_dropped(require_gpu, native, tmp_path):
     size = 8 * MB
     f = _files(tmp_path, 3, size)

@@ -159,8 +159,8 @@ RECIPES: dict[str, tuple[int, str]] = {
                             "SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv "
                             "-d gpurun_out/pmc_lzo41_lean -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
                             "--steps 1 --warmup 0"),
-    "store_tests": (300, f"{PY} -m pytest tests/test_gpu_api_device.py -m gpu -x -v --timeout 170 --timeout-method thread "
-                         f"-k 'hbm_store'"),
+    "store_tests": (300, f"{PY} -m pytest tests/test_gpu_api_device.py tests/test_gpu_mof_store.py -m gpu -x -v --timeout 170 "
+                         f"--timeout-method thread -k 'hbm_store or mof_store or evict or holders or release'"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
                               "python3 bench.py --device-only --rows-per-gpu 400000000 --steps 2 --warmup 1"),
 }
