@@ -544,6 +544,7 @@ def _run_waves(args, port, cmds, expected, exe, errlog, conf, sp, statistics):
             pth["fetch_to_eof_ms_max"] = round(v[-1], 1)
         split = {"descriptors": sum(int(o["task"].get("device_descriptors", 0)) for o in out.values()),
                  "bytes_fetched_as_bytes": sum(int(o["task"].get("host_fetched_bytes", 0)) for o in out.values()),
+                 "of_which_read_from_mof_files": sum(int(o["task"].get("local_read_bytes", 0)) for o in out.values()),
                  "hbm_wait_ms_max": round(max(float(o["task"].get("hbm_wait_ms", 0)) for o in out.values()), 1),
                  "paths": paths}
         return {"wall_ms": (t1 - t0) * 1e3, "from_fetch_ms": (t1 - t_fetch) * 1e3, "timeline": timeline,

@@ -487,9 +487,11 @@ class DeviceGate {
  public:
   // gate 0: staged GPU merges (mapred.uda.gpu.max.concurrent.merges); gate 1: device block decodes
   // of compressed descriptor tasks (mapred.uda.gpu.decode.slots)
+  // gate 2: declined-partition byte fetches of device-fetch tasks (mapred.uda.gpu.fetch.bytes.slots)
   static DeviceGate& get(int which = 0) {
-    static DeviceGate* g[2] = {new DeviceGate, new DeviceGate};  // never destroyed: tasks may outlive static teardown
-    return *g[which & 1];
+    // never destroyed: tasks may outlive static teardown
+    static DeviceGate* g[3] = {new DeviceGate, new DeviceGate, new DeviceGate};
+    return *g[(unsigned)which % 3];
   }
   // false if `stopped` became true while waiting
   template <class Stop>
@@ -2226,28 +2228,60 @@ void ReduceTask::merge_gpu() {
 }
 
 // The partitions a device-fetch task gets no usable descriptor for (the provider's HBM store is full or
-// off, or the descriptor cannot be mapped here): `streams` workers (mapred.uda.gpu.fetch.bytes.streams,
-// default 4, one per TCP connection of the task's transport) each take partitions in turn and keep three
-// requests of `chunk` bytes (mapred.uda.gpu.fetch.bytes.chunk, default 8 MiB) in flight into pinned slots,
-// each landed chunk going on to the device (H2D on the worker's stream) while the next ones come in. The
-// round-5 loop had one request of the task's buffer size (1 MiB) in flight at a time: a round trip per
-// MiB, 3.3 GB/s per task and 20 GB/s for a node of 15 tasks with 42.9 GB of 62.4 GB declined per wave
-// (profiles/r6/r6j_nodefiles62_store20.log). The reference's fetcher keeps its requests in flight the
-// same way (Segment::send_request, src/Merger/StreamRW.cc; RDMAClient::start_fetch_req).
-int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::function<FetchParams(size_t)>& params,
-                                         const std::function<int64_t(size_t)>& len, gpu::DeviceBuffer& dst,
-                                         const std::function<void(size_t, const uint8_t*)>& placed) {
+// off, or the descriptor cannot be mapped here). Two sources:
+//  * the MOF file itself, when the provider runs on this node and named the file in its answer, and the
+//    file is a regular file of this process's user (mapred.uda.gpu.fetch.local.read, default on; never for
+//    a confined task): pread into pinned slots, one copy out of the page cache;
+//  * otherwise the provider, over the transport: three requests of `chunk` bytes in flight per worker.
+// `streams` workers (mapred.uda.gpu.fetch.bytes.streams, default 4) take partitions in turn; every landed
+// chunk goes on to the device (H2D on the worker's stream) while the next ones come in. The round-5 loop
+// had one request of the task's buffer size (1 MiB) in flight at a time: a round trip per MiB, 3.3 GB/s
+// per task, 19.6 GB/s for a node of 15 tasks with 42.9 GB of 62.4 GB declined per wave; pipelined TCP
+// 24.0 (profiles/r6/r6j_*, r6k_nodefiles62_store20.log). Over TCP every byte is copied twice by the CPU
+// (the provider's sendfile, the reducer's receive) next to the consumers' own copies. The reference's
+// fetcher keeps its requests in flight the same way (Segment::send_request, src/Merger/StreamRW.cc).
+namespace {
+bool local_host(const std::string& spec) {
+  std::string h = spec;
+  if (const size_t c = h.rfind(':'); c != std::string::npos && h.find(':') == c) h = h.substr(0, c);
+  if (h == "127.0.0.1" || h == "localhost" || h == "::1" || h.empty()) return true;
+  char me[256] = {0};
+  if (::gethostname(me, sizeof(me) - 1) != 0) return false;
+  const std::string m = me;
+  return h == m || h == m.substr(0, m.find('.')) || m == h.substr(0, h.find('.'));
+}
+
+// A MOF file this process may read in place of fetching it: a regular file (no symlink) of our own user
+// holding [off, off + len). -1 if not.
+int open_local_mof(const std::string& path, int64_t off, int64_t len) {
+  if (path.empty() || path[0] != '/') return -1;
+  const int fd = ::open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+  if (fd < 0) return -1;
+  struct stat sb;
+  if (::fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_uid != ::geteuid() || sb.st_size < off + len) {
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+}  // namespace
+
+int64_t ReduceTask::fetch_declined_bytes(int device, const std::vector<DeclinedPart>& parts, gpu::DeviceBuffer& dst,
+                                         std::vector<const uint8_t*>* where, int64_t* local) {
+  const size_t n = parts.size();
   std::vector<int64_t> at(n + 1, 0);
-  for (size_t k = 0; k < n; ++k) at[k + 1] = at[k] + ((len(k) + 255) & ~(int64_t)255);
+  for (size_t k = 0; k < n; ++k) at[k + 1] = at[k] + ((parts[k].len + 255) & ~(int64_t)255);
   DeviceWorkspace::ensure(dst, at[n]);
   uint8_t* base = dst.as<uint8_t>();
-  for (size_t k = 0; k < n; ++k) placed(k, base + at[k]);
+  where->assign(n, nullptr);
+  for (size_t k = 0; k < n; ++k) (*where)[k] = base + at[k];
   const int streams = (int)std::clamp<int64_t>(host_->conf_i64("mapred.uda.gpu.fetch.bytes.streams", 4), 1, 16);
   int64_t chunk = std::max<int64_t>(buffer_size_, host_->conf_i64("mapred.uda.gpu.fetch.bytes.chunk", 8ll << 20));
   chunk = (chunk + 4095) & ~(int64_t)4095;
+  const bool local_ok = !sandbox_.enabled && host_->conf_i64("mapred.uda.gpu.fetch.local.read", 1) != 0;
   constexpr int kSlots = 3;
   std::atomic<size_t> next{0};
-  std::atomic<int64_t> fetched{0};
+  std::atomic<int64_t> fetched{0}, read_here{0};
   std::mutex em;
   std::string err;
   auto failed = [&] {
@@ -2268,6 +2302,7 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
     std::mutex m;
     std::condition_variable cv;
     hipStream_t hs = nullptr;
+    int fd = -1;
     auto drain = [&] {  // every request answered (their callbacks touch sl), every H2D done
       std::unique_lock<std::mutex> lk(m);
       cv.wait(lk, [&] {
@@ -2277,6 +2312,18 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
       });
       lk.unlock();
       if (hs) (void)hipStreamSynchronize(hs);
+    };
+    auto reuse = [&](Slot& x) {  // the slot's previous H2D has read it
+      if (x.h2d) {
+        HIP_CHECK(hipEventSynchronize(x.ev));
+        x.h2d = false;
+      }
+    };
+    auto to_device = [&](Slot& x, uint8_t* dev) {
+      HIP_CHECK(hipMemcpyAsync(dev + x.off, x.b.p, (size_t)x.want, hipMemcpyHostToDevice, hs));
+      HIP_CHECK(hipEventRecord(x.ev, hs));
+      x.h2d = true;
+      fetched += x.want;
     };
     try {
       HIP_CHECK(hipSetDevice(device));
@@ -2288,17 +2335,37 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
       for (;;) {
         const size_t k = next.fetch_add(1);
         if (k >= n || failed() || stop_) break;
-        const FetchParams f = params(k);
-        const int64_t L = len(k);
+        const DeclinedPart& d = parts[k];
+        const FetchParams& f = d.f;
+        const int64_t L = d.len;
         uint8_t* dev = base + at[k];
+        fd = local_ok && local_host(f.host) ? open_local_mof(d.path, d.file_off, L) : -1;
+        if (fd >= 0) {
+          for (int64_t off = 0, s = 0; off < L; s = (s + 1) % kSlots) {
+            Slot& x = sl[s];
+            reuse(x);
+            x.off = off;
+            x.want = std::min(chunk, L - off);
+            for (int64_t got = 0; got < x.want;) {
+              const ssize_t r = ::pread(fd, x.b.p + got, (size_t)(x.want - got), (off_t)(d.file_off + off + got));
+              if (r < 0 && errno == EINTR) continue;
+              if (r <= 0)
+                throw UdaError("reading " + d.path + " for " + f.map_id + ": " + (r < 0 ? strerror(errno) : "short file"));
+              got += r;
+            }
+            to_device(x, dev);
+            read_here += x.want;
+            off += x.want;
+          }
+          ::close(fd);
+          fd = -1;
+          continue;
+        }
         int64_t issue_off = 0;
         int outstanding = 0, head = 0, tail = 0;  // slots in request order: tail (oldest) .. head
         auto issue = [&](int s) {
           Slot& x = sl[s];
-          if (x.h2d) {
-            HIP_CHECK(hipEventSynchronize(x.ev));
-            x.h2d = false;
-          }
+          reuse(x);
           FetchRequest req;
           req.job_id = f.job_id;
           req.map_id = f.map_id;
@@ -2343,10 +2410,7 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
             throw UdaError("fetch of " + f.map_id + ": provider sent " + std::to_string(x.a.sent) + " bytes of a " +
                            std::to_string(x.a.part_len) + "-byte partition at offset " + std::to_string(x.off) +
                            " (expected " + std::to_string(x.want) + " of " + std::to_string(L) + ")");
-          HIP_CHECK(hipMemcpyAsync(dev + x.off, x.b.p, (size_t)x.want, hipMemcpyHostToDevice, hs));
-          HIP_CHECK(hipEventRecord(x.ev, hs));
-          x.h2d = true;
-          fetched += x.want;
+          to_device(x, dev);
           tail = (tail + 1) % kSlots;
           if (issue_off < L) {
             issue(head);
@@ -2358,6 +2422,7 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
       std::lock_guard<std::mutex> g(em);
       if (err.empty()) err = e.what();
     }
+    if (fd >= 0) ::close(fd);
     drain();
     for (auto& x : sl) {
       if (x.ev) (void)hipEventDestroy(x.ev);
@@ -2372,6 +2437,7 @@ int64_t ReduceTask::fetch_declined_bytes(int device, size_t n, const std::functi
   for (auto& t : ts) t.join();
   if (!err.empty()) throw UdaError(err);
   if (stop_) throw UdaError("reduce task stopped during fetch");
+  *local = read_here.load();
   return fetched.load();
 }
 
@@ -2435,12 +2501,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   int64_t host_bytes = 0, descriptors = 0, unmapped = 0;
   // partitions answered "not device-resident" (or with a descriptor this process cannot map): their
   // bytes are fetched once every descriptor answer is in (fetch_declined, below)
-  struct Declined {
-    FetchParams f;
-    int64_t len;
-    size_t part;  // index into parts
-  };
-  std::vector<Declined> declined;
+  std::vector<DeclinedPart> declined;
+  std::vector<size_t> declined_part;  // index into parts
 
   // ---- fetch phase: descriptors for every MOF as its FETCH arrives
   int resolved = 0;
@@ -2527,7 +2589,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         if (a.part_len < kEofBytes)
           throw UdaError("fetch of " + batch[i].map_id + ": descriptor answer carries no partition length");
         part->part_len = a.part_len;
-        declined.push_back(Declined{batch[i], a.part_len, parts.size()});
+        declined.push_back(DeclinedPart{batch[i], a.part_len, std::string(), 0});
+        declined_part.push_back(parts.size());
         ++unmapped;
       } else if (a.status == kNotDeviceResident) {
         // every partition holds at least the IFile EOF marker: a length of 0 is a provider that did not say
@@ -2535,7 +2598,8 @@ bool ReduceTask::merge_gpu_device(bool probe) {
           throw UdaError("fetch of " + batch[i].map_id + ": declined descriptor fetch carries no partition length (" +
                          std::to_string(a.part_len) + ")");
         part->part_len = a.part_len;
-        declined.push_back(Declined{batch[i], a.part_len, parts.size()});
+        declined.push_back(DeclinedPart{batch[i], a.part_len, a.path, a.mof_offset});
+        declined_part.push_back(parts.size());
       } else {
         throw UdaError("fetch of " + batch[i].map_id + " failed: " + (a.status ? a.error : "no device descriptor"));
       }
@@ -2579,16 +2643,31 @@ bool ReduceTask::merge_gpu_device(bool probe) {
   DeviceWorkspace& ws = *ws_lease.obj;
   ws.reset_stats();
   HIP_PENDING("the merge workspace");
+  int64_t local_bytes = 0;
   if (!declined.empty()) {
     const auto tf = std::chrono::steady_clock::now();
-    host_bytes = fetch_declined_bytes(device, declined.size(), [&](size_t k) { return declined[k].f; },
-                                      [&](size_t k) { return declined[k].len; }, ws.fetched,
-                                      [&](size_t k, const uint8_t* p) { parts[declined[k].part]->dptr = p; });
+    // the node's tasks take turns (FIFO, mapred.uda.gpu.fetch.bytes.slots at once; 0 = no limit): served
+    // in turn, the first tasks' bytes are in and their merges deliver while later tasks still fetch;
+    // all at once, every task's bytes landed late together and the link idled until then
+    GateLease bgate;
+    bgate.which = 2;
+    if (const int slots = (int)host_->conf_i64("mapred.uda.gpu.fetch.bytes.slots", 4); slots > 0) {
+      if (!DeviceGate::get(2).acquire(device, slots, [&] { return stop_.load(); }))
+        throw UdaError("reduce task stopped while waiting for its turn to fetch bytes");
+      bgate.device = device;
+    }
+    const double tg = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
+    std::vector<const uint8_t*> where;
+    host_bytes = fetch_declined_bytes(device, declined, ws.fetched, &where, &local_bytes);
+    for (size_t k = 0; k < declined.size(); ++k) parts[declined_part[k]]->dptr = where[k];
     fetch_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.gpu_gate_wait_ms += tg;
   }
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.host_fetched_bytes = host_bytes;
+    st_.local_read_bytes = local_bytes;
   }
   // HBM admission (gpu/hbm_ledger.h): the task's device working set -- decoded partitions, the
   // key-range round's output slots and merge tables -- is reserved before it is allocated, under the

@@ -932,7 +932,7 @@ std::string ReduceTask::stats_json() const {
     << ",\"gpu_sink_ms\":" << s.gpu_sink_ms << ",\"gpu_decode_ms\":" << s.gpu_decode_ms << ",\"gpu_gate_wait_ms\":" << s.gpu_gate_wait_ms << ",\"gpu_prewarm_ms\":" << s.gpu_prewarm_ms << ",\"gpu_prewarm_wait_ms\":" << s.gpu_prewarm_wait_ms << ",\"gpu_prewarm_phases\":\"" << json_escape(s.gpu_prewarm_phases) << "\"" << ",\"fetch_buf_bytes\":" << s.fetch_buf_bytes
     << ",\"uncomp_buf_bytes\":" << s.uncomp_buf_bytes << ",\"restored_lpqs\":" << s.restored_lpqs
     << ",\"restored_maps\":" << s.restored_maps << ",\"device_descriptors\":" << s.device_descriptors << ",\"unmapped_descriptors\":" << s.unmapped_descriptors << ",\"unmapped_reason\":\"" << json_escape(s.unmapped_reason) << "\"" << ",\"descriptor_map_ms\":" << s.descriptor_map_ms << ",\"fetch_cmd_wait_ms\":" << s.fetch_cmd_wait_ms << ",\"fetch_ack_wait_ms\":" << s.fetch_ack_wait_ms << ",\"merge_start_boot_ms\":" << std::fixed << std::setprecision(1) << s.merge_start_boot_ms << ",\"fetch_sent_boot_ms\":" << s.fetch_sent_boot_ms << std::defaultfloat << std::setprecision(6) << ",\"first_data_ms\":" << s.first_data_ms << ",\"gpu_ws_bytes\":" << s.gpu_ws_bytes
-    << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms
+    << ",\"host_fetched_bytes\":" << s.host_fetched_bytes << ",\"local_read_bytes\":" << s.local_read_bytes << ",\"hbm_wait_ms\":" << s.hbm_wait_ms
     << ",\"hbm_reserved\":" << s.hbm_reserved << ",\"round_bytes\":" << s.round_bytes << ",\"gpu_device\":" << s.gpu_device << ",\"merge_path\":\"" << s.merge_path << "\""
     << ",\"finished\":" << (finished_ ? "true" : "false") << "}";
   return o.str();

@@ -84,6 +84,7 @@ struct ReduceStats {
   double fetch_sent_boot_ms = 0;      // first descriptor requests (a wave's timeline, bench.py --node)
   double first_data_ms = -1;          // device fetch: from the merge's start to the first dataFromUda
   int64_t host_fetched_bytes = 0;     // GPU device fetch: bytes of MOFs that were not device-resident
+  int64_t local_read_bytes = 0;       // of those: read from the MOF files on this node (not over the network)
   std::string merge_path;             // which merge ran ("device-fixed10", "device-generic", ...)
   std::string backend;
 };
@@ -141,11 +142,17 @@ class ReduceTask {
   // Device fetch (descriptors, merge in place). probe: return false before consuming anything if the
   // first MOFs are not device-resident (the caller then runs merge_gpu()).
   bool merge_gpu_device(bool probe);
-  // Device fetch: the bytes of n partitions the providers would not answer with a descriptor, into one
-  // device buffer (grown as needed; placed(k, p): partition k landed at p). Returns the bytes fetched.
-  int64_t fetch_declined_bytes(int device, size_t n, const std::function<FetchParams(size_t)>& params,
-                               const std::function<int64_t(size_t)>& len, gpu::DeviceBuffer& dst,
-                               const std::function<void(size_t, const uint8_t*)>& placed);
+  // Device fetch: a partition the providers would not answer with a descriptor.
+  struct DeclinedPart {
+    FetchParams f;
+    int64_t len = 0;
+    std::string path;  // the MOF file the provider named, and the partition's offset in it
+    int64_t file_off = 0;
+  };
+  // Their bytes into one device buffer (grown as needed; (*at)[k]: where partition k landed). Returns the
+  // bytes fetched; *local: of those, read from the MOF files on this node.
+  int64_t fetch_declined_bytes(int device, const std::vector<DeclinedPart>& parts, gpu::DeviceBuffer& dst,
+                               std::vector<const uint8_t*>* at, int64_t* local);
   // Tell every provider in `hosts` that `holder` (this task) is done with its descriptors.
   void release_descriptors(const std::set<std::string>& hosts, const std::string& holder);
   // GPU backend: started at INIT on prewarm_thr_ (mapred.uda.gpu.prewarm): HIP context, SDMA engine,

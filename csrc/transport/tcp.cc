@@ -19,8 +19,6 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
-#include <deque>
-#include <functional>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -165,42 +163,24 @@ class TcpServer : public ServerTransport {
   int port() const override { return port_; }
 
  private:
-  // Answers are written by the connection's own writer thread, not by the provider worker that resolved
-  // the request: a worker only looks the partition up and queues (ack, bytes); the send (sendfile of up to
-  // a request's size) runs here. With the workers writing, 8 of them (mapred.uda.provider.workers) were
-  // the node's whole byte-serving capacity whatever the number of connections: ~20 GB/s for 15 tasks
-  // fetching 42.9 GB of declined partitions (r6 node run, a store smaller than the MOFs).
+  // Answers are written by the provider worker that resolved the request (sendfile / send of up to a
+  // request's size), so the node's byte serving runs mapred.uda.provider.workers sends at once, in request
+  // order. A writer thread per connection was measured too (r6l): 60 connections sending at once shared
+  // the box's CPUs fairly, every task's bytes finished late together and the node went from 24.0 to 18.2
+  // GB/s (15 tasks, 42.9 GB of declined partitions per wave).
   struct Conn {
     int fd;
-    std::mutex mu;  // inflight (the writer thread alone writes to fd)
+    std::mutex mu;  // serializes writes; inflight
     std::condition_variable cv;
     int inflight = 0;
-    std::thread reader, writer;
-    std::mutex wmu;
-    std::condition_variable wcv;
-    std::deque<std::function<void()>> sendq;  // answers to write, in order
-    bool wstop = false;
+    std::thread reader;
     std::atomic<bool> ended{false};  // the reader returned and no serve is writing to fd
   };
-
-  static void write_loop(const std::shared_ptr<Conn>& c) {
-    for (;;) {
-      std::function<void()> w;
-      {
-        std::unique_lock<std::mutex> lk(c->wmu);
-        c->wcv.wait(lk, [&] { return c->wstop || !c->sendq.empty(); });
-        if (c->sendq.empty()) return;
-        w = std::move(c->sendq.front());
-        c->sendq.pop_front();
-      }
-      w();
-    }
-  }
-  // Write one answer (on the connection's writer thread): header, ack, then the bytes from memory (ptr)
-  // or from a file range (sendfile). A failed write shuts the socket down: the client fails the fetches
-  // still waiting on it.
+  // Write one answer: header, ack, then the bytes from memory (ptr) or from a file range (sendfile). A
+  // failed write shuts the socket down: the client fails the fetches still waiting on it.
   static void answer(const std::shared_ptr<Conn>& c, uint64_t id, const FetchAck& a, const uint8_t* ptr, int fd,
                      int64_t file_off) {
+    std::lock_guard<std::mutex> g(c->mu);
     const std::string ack = format_ack(a);
     const uint32_t ack_len = (uint32_t)ack.size();
     const uint64_t data_len = a.status == 0 ? (uint64_t)a.sent : 0;
@@ -221,14 +201,8 @@ class TcpServer : public ServerTransport {
       }
     }
     if (!ok) ::shutdown(c->fd, SHUT_RDWR);
-    std::lock_guard<std::mutex> g(c->mu);  // the reader may take the next request's credit
     c->inflight--;
     c->cv.notify_all();
-  }
-  static void post(const std::shared_ptr<Conn>& c, std::function<void()> w) {
-    std::lock_guard<std::mutex> g(c->wmu);
-    c->sendq.push_back(std::move(w));
-    c->wcv.notify_one();
   }
 
   // Connections whose client went away (one reduce task's, after its fetches): join the reader and
@@ -260,19 +234,10 @@ class TcpServer : public ServerTransport {
       std::lock_guard<std::mutex> g(mu_);
       reap_locked();
       conns_.push_back(c);
-      c->writer = std::thread([c] { write_loop(c); });
       c->reader = std::thread([this, c] {
         read_loop(c);
-        {
-          std::unique_lock<std::mutex> lk(c->mu);  // serves still answering on this socket finish first
-          c->cv.wait(lk, [&] { return c->inflight == 0; });
-        }
-        {
-          std::lock_guard<std::mutex> g(c->wmu);
-          c->wstop = true;
-          c->wcv.notify_all();
-        }
-        c->writer.join();
+        std::unique_lock<std::mutex> lk(c->mu);  // serves still answering on this socket finish first
+        c->cv.wait(lk, [&] { return c->inflight == 0; });
         c->ended = true;
       });
     }
@@ -298,18 +263,14 @@ class TcpServer : public ServerTransport {
       // by reference first: the provider's memory or the MOF file goes to the socket as it is (send /
       // sendfile), instead of being copied into a chunk and then into the socket
       if (req.buf_len > 0 && server_->serve_ref(req, [c, id](const FetchAck& a, DataServer::Bytes b) {
-            post(c, [c, id, a, b = std::move(b)]() mutable {
-              answer(c, id, a, b.ptr, b.fd, b.file_off);
-              if (b.release) b.release();
-            });
+            answer(c, id, a, b.ptr, b.fd, b.file_off);
+            if (b.release) b.release();
           }))
         continue;
       // a chunk of the request's size for the bytes (the provider's registered chunk,
       // NETLEV_RDMA_MEM_CHUNKS_NUM pool); not zero-filled, every byte sent is written first
       std::shared_ptr<uint8_t[]> chunk(new uint8_t[(size_t)std::max<int64_t>(1, req.buf_len)]);
-      server_->serve(req, chunk.get(), [c, chunk, id](const FetchAck& a) {
-        post(c, [c, chunk, id, a] { answer(c, id, a, chunk.get(), -1, 0); });
-      });
+      server_->serve(req, chunk.get(), [c, chunk, id](const FetchAck& a) { answer(c, id, a, chunk.get(), -1, 0); });
     }
   }
 

@@ -62,29 +62,35 @@ bool parse_rts(const std::string& s, FetchRequest* r, uint64_t* remote_addr, uin
   return true;
 }
 
-// An error ack keeps the partition's lengths when the provider knows them: a declined descriptor fetch
-// (kNotDeviceResident) tells the reducer how many bytes to fetch instead. E:status:raw:part:offset:error
-// (the error last: it may contain ':').
+// An error ack keeps what the provider knows of the partition: a declined descriptor fetch
+// (kNotDeviceResident) tells the reducer how many bytes to fetch instead, and where they are in which MOF
+// file (a reducer on the provider's node may read them itself). E:status:raw:part:offset:pathlen:path:error
+// (path by length, error last: both may contain ':').
 std::string format_ack(const FetchAck& a) {
   if (a.status != 0)
     return "E:" + std::to_string(a.status) + ":" + std::to_string(a.raw_len) + ":" + std::to_string(a.part_len) + ":" +
-           std::to_string(a.mof_offset) + ":" + a.error;
+           std::to_string(a.mof_offset) + ":" + std::to_string(a.path.size()) + ":" + a.path + ":" + a.error;
   return std::to_string(a.raw_len) + ":" + std::to_string(a.part_len) + ":" + std::to_string(a.sent) + ":" +
          std::to_string(a.mof_offset) + ":" + a.path + ":";
 }
 
 bool parse_ack(const std::string& s, FetchAck* a) {
   if (s.rfind("E:", 0) == 0) {
-    auto f = split(s, ':');
-    if (f.size() < 6) return false;
-    a->status = (int)to_i64(f[1]);
-    if (a->status == 0) a->status = -1;
-    a->raw_len = to_i64(f[2]);
-    a->part_len = to_i64(f[3]);
-    a->mof_offset = to_i64(f[4]);
-    std::string e = f[5];
-    for (size_t i = 6; i < f.size(); ++i) e += ":" + f[i];
-    a->error = e;
+    int64_t v[5];
+    size_t at = 2;
+    for (int i = 0; i < 5; ++i) {  // status, raw, part, offset, path length
+      const size_t c = s.find(':', at);
+      if (c == std::string::npos) return false;
+      v[i] = to_i64(s.substr(at, c - at));
+      at = c + 1;
+    }
+    if (v[4] < 0 || at + (size_t)v[4] + 1 > s.size() || s[at + (size_t)v[4]] != ':') return false;
+    a->status = v[0] == 0 ? -1 : (int)v[0];
+    a->raw_len = v[1];
+    a->part_len = v[2];
+    a->mof_offset = v[3];
+    a->path = s.substr(at, (size_t)v[4]);
+    a->error = s.substr(at + (size_t)v[4] + 1);
     return true;
   }
   auto f = split(s, ':');

@@ -283,9 +283,10 @@ def test_declined_descriptor_ack_keeps_partition_lengths(native):
     with the partition's lengths, so the reducer knows how many bytes to fetch instead. Over TCP the
     error ack used to carry only the status and text: 23 of 32 partitions were then "fetched" as 0
     bytes and the merged output silently lacked them (r6 node run with a store smaller than the MOFs)."""
-    got = native.ack_roundtrip(-12, 1000, 993, 0, 4096, "", "provider HBM store: full: 3.0 of 3.0 GB held")
+    got = native.ack_roundtrip(-12, 1000, 993, 0, 4096, "/d:1/m_3/file.out", "provider HBM store: full: 3 of 3 GB")
     assert got["status"] == -12 and got["part_len"] == 993 and got["raw_len"] == 1000 and got["mof_offset"] == 4096
-    assert got["error"] == "provider HBM store: full: 3.0 of 3.0 GB held"  # the text may contain ':'
+    assert got["path"] == "/d:1/m_3/file.out"  # where the bytes are (a reducer on the node may read them)
+    assert got["error"] == "provider HBM store: full: 3 of 3 GB"  # path and text may contain ':'
     ok = native.ack_roundtrip(0, 10, 8, 8, 0, "/a:b/file.out", "")
     assert (ok["status"], ok["part_len"], ok["sent"], ok["path"]) == (0, 8, 8, "/a:b/file.out")
     err = native.ack_roundtrip(-2, 0, 0, 0, 0, "", "cannot resolve MOF j/m/0")

@@ -290,12 +290,13 @@ def test_provider_hbm_store_budget_falls_back_to_bytes(require_gpu, tmp_path):
         p.close()
 
 
-@pytest.mark.parametrize("streams", [1, 3])
-def test_provider_hbm_store_declines_over_tcp(require_gpu, tmp_path, streams):
-    """As above, over TCP: a declined descriptor answer carries the partition's length on the wire, and
-    the declined partitions' bytes come in pipelined chunk requests (mapred.uda.gpu.fetch.bytes.*; here
-    16 KiB chunks, ~26 per partition) from `streams` workers. The round-5 TCP error ack dropped the
-    length and the declined partitions were merged as empty."""
+@pytest.mark.parametrize("streams,local", [(1, 0), (3, 0), (3, 1)])
+def test_provider_hbm_store_declines_over_tcp(require_gpu, tmp_path, streams, local):
+    """As above, over TCP: a declined descriptor answer carries the partition's length and MOF file on the
+    wire, and the declined partitions' bytes come in pipelined chunk requests (mapred.uda.gpu.fetch.bytes.*;
+    here 16 KiB chunks, ~26 per partition) from `streams` workers -- or, the provider being on this node
+    and the file ours, straight from the file (mapred.uda.gpu.fetch.local.read). The round-5 TCP error ack
+    dropped the length and the declined partitions were merged as empty."""
     import socket
     maps = datagen.terasort(num_maps=6, reducers=1, rows_per_map=4000, seed=29)
     size = len(datagen.streams(maps)[0][0]) + 64
@@ -306,7 +307,7 @@ def test_provider_hbm_store_declines_over_tcp(require_gpu, tmp_path, streams):
     try:
         ids = _publish_files(p, tmp_path, "job_9_0102", maps)
         conf = dict(GPU, **{"mapred.uda.gpu.fetch": "device", "mapred.uda.gpu.fetch.bytes.streams": streams,
-                            "mapred.uda.gpu.fetch.bytes.chunk": 16384})
+                            "mapred.uda.gpu.fetch.bytes.chunk": 16384, "mapred.uda.gpu.fetch.local.read": local})
         recs, st, _ = run_reduce("127.0.0.1", "job_9_0102", ids, 0, datagen.TEXT, conf=conf, transport="tcp",
                                  data_port=port, max_buf_kb=16)
         assert recs == expected(maps, 0, datagen.TEXT)
@@ -315,6 +316,7 @@ def test_provider_hbm_store_declines_over_tcp(require_gpu, tmp_path, streams):
         want_bytes = sum(len(part[0]) for part in datagen.streams(maps))
         assert st["device_descriptors"] == hs["loads"] and st["host_fetched_bytes"] > 0, st
         assert st["maps_fetched"] == 6 and st["bytes_fetched"] == want_bytes, st
+        assert st["local_read_bytes"] == (st["host_fetched_bytes"] if local else 0), st
     finally:
         p.close()
 
