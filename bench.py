@@ -823,7 +823,11 @@ def run_api(args, ctx) -> int:
                      f"{args.skew:.0%} of every map's records to reduce task 0" + (" of every rank" if world > 1 else ""))
                     if args.workload == "secondary" else
                     "synthetic TeraGen-shaped (10B key/90B value, 104B IFile records generated in HBM)",
+            # device-wide, sampled (hipMemGetInfo): includes what no budget governs, the HIP runtime's own
+            # HBM (context, code objects, scratch)
             "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),
+            # what the HBM ledger tracked at its peak: reservations + pooled workspaces + the MOF store
+            "hbm_ledger_peak_gb": round(max(s.get("hbm_ledger_peak_bytes", 0) for s in stats) / 1e9, 2),
             "hbm_budget_gb": round(stats[-1].get("hbm_budget_bytes", 0) / 1e9, 2),
             "hbm_budget_waits": int(stats[-1].get("hbm_budget_waits", 0)),
             # bytes allocated outside a reservation while the device was over its budget (0 = the budget held)
