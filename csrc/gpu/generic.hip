@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(64 * kF1FnWaves) f1_fn_kernel(uint8_t* const* 
                                                                  int partial) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kF1FnWaves][kF1Chunk + 64];
   __shared__ int f1_live[kF1FnWaves][3 * kF1Entries];  // surviving chains: entry, position, count
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wv: wave-uniform
   const int64_t c = (int64_t)blockIdx.x * kF1FnWaves + wv;
   const bool valid = c < nchunks;
   uint8_t* buf = lds[wv];
@@ -409,7 +409,9 @@ __global__ void __launch_bounds__(256) f1_super_kernel(const int64_t* nbytes, co
                                                        const int64_t* sup_base, const int32_t* sup_run, int64_t nsup,
                                                        const int32_t* fx, const int32_t* fn, int64_t* sx,
                                                        int64_t* sn) {
-  const int64_t sidx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform (readfirstlane: the compiler takes threadIdx.x >> 6 as divergent, and everything loaded
+  // through it would be per-lane vector loads and VALU arithmetic)
+  const int64_t sidx = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (sidx >= nsup) return;
   const int r = sup_run[sidx];

@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(256) kway_tile_kernel(KwayDesc kd, uint8_t* ou
   kw_merge_levels<kKwItems>(src, seg, K, n);
   stamp(3);
   // ---- F4: records in merged order straight to the output
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: a scalar loop
   for (int base = wave * 64; base < n; base += kKwWaves * 64) {
     const int valid = min(64, n - base);
     kw_gather64(sbase, src, base, valid, obase + (int64_t)base * kTeraRecordBytes);
@@ -538,7 +538,7 @@ __global__ void __launch_bounds__(256) kway_staged_kernel(KwayDesc kd, uint8_t* 
   // past the slice's last record, possibly past its allocation: that lane reads a chunk inside the slice
   // instead and the chunk's 8 valid bytes are patched below.
   const int T = wfirst[K];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform
   for (int base = wave * 64; base < T; base += kWaves * 64) {
     const int i = base + lane;
     const int ic = min(i, T - 1);

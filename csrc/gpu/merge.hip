@@ -342,7 +342,8 @@ __global__ void __launch_bounds__(256) gather_fixed_kernel(const Elem* elems, in
                                                            uint8_t* out) {
   constexpr int kWords = kTeraRecordBytes / 8;  // 13
   const int lane = threadIdx.x & 63;
-  const int64_t rec0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+  const int64_t rec0 =
+      ((int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;  // wave-uniform
   if (rec0 >= n) return;
   const int valid = (n - rec0) < 64 ? (int)(n - rec0) : 64;
   unsigned long long src = 0;
