@@ -1120,6 +1120,7 @@ void ReduceTask::merge_gpu() {
   // MergeManager.cc:202-288, is what this recovers).
   struct DirectProg {
     int P = 0, K = 0;
+    int64_t spacing = kSampleSpacing;        // index sample spacing of the runs
     std::vector<std::shared_ptr<MofFetcher>> f;
     std::vector<uint8_t*> dst;
     std::vector<int64_t> cap;
@@ -1471,10 +1472,16 @@ void ReduceTask::merge_gpu() {
             stager->release_blocks();
             stager = nullptr;
           }
+          // the partitions' pinned spans come back to the pool when the task ends: keep them cached for the
+          // next task of this size instead of re-pinning them
+          gpu::PinnedPool::instance().raise_cache_cap((size_t)(tot + tot / 8));
           dprog = std::make_unique<DirectProg>();
           DirectProg& dp = *dprog;
           dp.P = pdirect_phases;
           dp.K = (int)ready.size();
+          // samples fine enough that a round of budget/2 can be cut from K runs (a few per run and round):
+          // 256 KiB for GB partitions, finer for small tasks under a small budget
+          dp.spacing = std::clamp<int64_t>(budget / 2 / (4 * std::max(1, dp.K)), 4 << 10, kSampleSpacing);
           dp.f = ready;
           for (auto& f : ready) dp.cap.push_back(std::max<int64_t>(f->part_len(), 0));
           const size_t K = (size_t)dp.K;
@@ -1533,7 +1540,7 @@ void ReduceTask::merge_gpu() {
                   std::vector<int64_t> c;
                   std::vector<std::string> kk;
                   RunCursor& rc = dp.cur[(size_t)k];
-                  rc.advance(dp.dst[(size_t)k], limit, kSampleSpacing, &c, &kk);
+                  rc.advance(dp.dst[(size_t)k], limit, dp.spacing, &c, &kk);
                   std::string lkey = rc.last_key(dp.dst[(size_t)k]);
                   lk.lock();
                   auto& vc = dp.cut[(size_t)k];
@@ -1801,7 +1808,7 @@ void ReduceTask::merge_gpu() {
       // phases land and the pipeline below takes them in order
       std::vector<std::vector<std::pair<int64_t, int64_t>>> rounds;
       bool planned_all = false;
-      const int64_t target = std::max<int64_t>(budget / 2, kSampleSpacing);
+      const int64_t target = std::max<int64_t>(budget / 2, dp.spacing);
       int epoch = 0;
       // plan the rounds of every key range that has fully arrived; false while nothing new can be planned
       auto plan_more = [&](bool wait) -> bool {

@@ -243,6 +243,24 @@ void PinnedPool::set_cache_cap(size_t bytes) {
   cap_ = bytes;
 }
 
+namespace {
+size_t host_memory_limit() {
+  size_t lim = (size_t)sysconf(_SC_PHYS_PAGES) * (size_t)sysconf(_SC_PAGESIZE);
+  if (FILE* f = std::fopen("/sys/fs/cgroup/memory.max", "r")) {  // cgroup v2 ("max" = none)
+    unsigned long long v = 0;
+    if (std::fscanf(f, "%llu", &v) == 1 && v > 0) lim = std::min<size_t>(lim, (size_t)v);
+    std::fclose(f);
+  }
+  return lim;
+}
+}  // namespace
+
+void PinnedPool::raise_cache_cap(size_t bytes) {
+  static const size_t ceiling = host_memory_limit() / 4;
+  std::lock_guard<std::mutex> g(mu_);
+  cap_ = std::max(cap_, std::min(bytes, ceiling));
+}
+
 size_t PinnedPool::cached_bytes() {
   std::lock_guard<std::mutex> g(mu_);
   return cached_;

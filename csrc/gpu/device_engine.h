@@ -143,6 +143,10 @@ class PinnedPool {
   Block acquire(size_t min_bytes);
   void release(Block b);
   void set_cache_cap(size_t bytes);
+  // Raise the cache cap to hold `bytes` (never lowers it), up to a quarter of the host memory this process
+  // may use (physical memory, or its cgroup's limit). A task that pins its whole input each time (the
+  // over-budget DRAM tier: 41.6 GB) otherwise re-pins what exceeds the default 32 GiB on every run.
+  void raise_cache_cap(size_t bytes);
   size_t cached_bytes();
   // free every block the reaper has not freed yet, on this thread (before retrying a failed allocation)
   void drain_reaper();
