@@ -826,7 +826,8 @@ def run_api(args, ctx) -> int:
             # device-wide, sampled (hipMemGetInfo): includes what no budget governs, the HIP runtime's own
             # HBM (context, code objects, scratch)
             "peak_hbm_gb": round(max(s["peak_hbm_bytes"] for s in stats) / 1e9, 2),
-            # what the HBM ledger tracked at its peak: reservations + pooled workspaces + the MOF store
+            # what the HBM ledger tracked at its peak during a timed step: reservations + pooled workspaces +
+            # map outputs this process holds in HBM
             "hbm_ledger_peak_gb": round(max(s.get("hbm_ledger_peak_bytes", 0) for s in stats) / 1e9, 2),
             "hbm_budget_gb": round(stats[-1].get("hbm_budget_bytes", 0) / 1e9, 2),
             "hbm_budget_waits": int(stats[-1].get("hbm_budget_waits", 0)),

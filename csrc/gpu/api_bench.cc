@@ -458,6 +458,7 @@ std::map<std::string, double> ApiTeraSortBench::step(bool validate, std::string*
   sink.set_check_order(validate);
   sink.set_key_kind(1);  // Text: content order (TeraSort's fixed keys order the same either way)
   // device-wide HBM in use, sampled through the step (the peak includes the map-output store)
+  HbmLedger::get().reset_peak(cfg_.device);  // the ledger's peak of this step alone
   std::atomic<bool> sampling{true};
   std::atomic<int64_t> peak_used{0};
   std::thread sampler([&] {

@@ -346,6 +346,12 @@ void HbmLedger::Reservation::unbind() {
   prev_bound_ = nullptr;
 }
 
+void HbmLedger::reset_peak(int device) {
+  std::lock_guard<std::mutex> g(mu_);
+  Dev& d = dev(device);
+  d.peak = d.used + d.reserved;
+}
+
 HbmLedger::Stats HbmLedger::stats(int device) {
   std::lock_guard<std::mutex> g(mu_);
   Dev& d = dev(device);

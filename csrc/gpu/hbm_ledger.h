@@ -105,6 +105,8 @@ class HbmLedger {
     double wait_ms = 0;
   };
   Stats stats(int device);
+  // Start a new peak window (benchmarks: the peak of one timed step, not of the setup before it).
+  void reset_peak(int device);
   // Tests: account allocations of a device without touching HIP (fake HBM size and key).
   void set_fake_device(int device, int64_t total_bytes, const std::string& key);
   // Tests: device memory a fake device reports in use beyond what the ledgers track (HIP runtime, code

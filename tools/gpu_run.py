@@ -159,6 +159,8 @@ RECIPES: dict[str, tuple[int, str]] = {
                             "SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv "
                             "-d gpurun_out/pmc_lzo41_lean -o run -- python3 bench.py --api --api-codec lzo --rows-per-gpu 100000000 "
                             "--steps 1 --warmup 0"),
+    "hybrid41b_s3": (700, "UDA_API_CONF=mapred.uda.gpu.hbm.budget=10000000000 "
+                          f"{PY} bench.py --api --api-host-mofs --reducers 1 --rows-per-gpu 400000000 --steps 3 --warmup 1"),
     "store_tests": (300, f"{PY} -m pytest tests/test_gpu_api_device.py tests/test_gpu_mof_store.py -m gpu -x -v --timeout 170 "
                          f"--timeout-method thread -k 'hbm_store or mof_store or evict or holders or release'"),
     "prof_device_only": (400, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_device_only -o run -- "
