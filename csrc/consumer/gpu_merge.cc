@@ -71,7 +71,13 @@ struct DeviceMergeOut {
   int64_t decoded_blocks = 0;
 };
 
-constexpr int64_t kPieceBytes = 64 << 20;  // D2H piece of the pinned double buffer
+constexpr int64_t kPieceBytes = 64 << 20;  // D2H piece of the pinned double buffer (hipMemcpy fallback)
+// stream_out's SDMA ring: a skewed task's delivery is the job's long pole (config #5: 60 GB in one task),
+// and two 64 MiB pieces through hipMemcpyAsync left its consumer waiting on D2H for 815 of 2742 ms while
+// 15 other tasks shared the link. Eight pieces of 16 MiB queued on the SDMA engines keep up to 128 MiB of
+// the task's output moving ahead of its consumer, as the TeraSort delivery does (device_reduce.cc).
+constexpr int kOutSlots = 8;
+constexpr int64_t kOutPiece = 16 << 20;
 
 // One merged LPQ output, resident in host memory or in a spill file.
 struct SpillRun {
@@ -96,10 +102,24 @@ struct DeviceWorkspace {
   gpu::GenericRoundsWs rounds;     // key-range round planner scratch (device fetch, generic keys)
   gpu::DeviceBuffer frame_scratch, frame_descs; // device framing walk of compressed partitions (device fetch)
   hipEvent_t piece_ev[2] = {nullptr, nullptr};
+  // SDMA delivery ring of stream_out: kOutSlots pieces of kOutPiece bytes on the GPU's NUMA node, each
+  // with its completion signal
+  gpu::SdmaEngine* oeng = nullptr;
+  uint8_t* oring = nullptr;
+  std::vector<hsa_signal_t> osig;
+  bool sdma_out_ok = true;
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
   ~DeviceWorkspace() {
+    for (auto sg : osig) {
+      try {
+        gpu::SdmaEngine::wait(sg);  // a copy still in flight lands before the ring is reused
+      } catch (...) {
+      }
+      oeng->destroy_signal(sg);
+    }
+    if (oring) oeng->release_ring(oring, (size_t)kOutSlots * kOutPiece);
     if (h2d_sig.handle) {
       try {
         gpu::SdmaEngine::wait(h2d_sig);
@@ -684,15 +704,87 @@ DeviceMergeOut device_merge(DeviceWorkspace& ws, const std::vector<Span>& in_run
   return res;
 }
 
-// Stream the merged output of `m` (in ws.out) to the host in pieces of up to kPieceBytes that end on
-// record boundaries (the cuts), double-buffered through pinned memory: the D2H of piece k+1 runs
-// while fn(piece k) consumes it. fn(ptr, first_cut, last_cut) gets the bytes of cuts
-// [first_cut, last_cut] (ptr = byte cuts[first_cut]).
+// piece boundaries (in cut indices) of a merged output: pieces of up to `limit` bytes ending on record
+// boundaries; empty if a single cut interval is larger than `limit`
+std::vector<size_t> piece_bounds(const std::vector<int64_t>& cuts, int64_t limit) {
+  const size_t nb = cuts.size() - 1;
+  std::vector<size_t> pb{0};
+  while (pb.back() < nb) {
+    const size_t j = pb.back();
+    if (cuts[j + 1] - cuts[j] > limit) return {};
+    size_t k = j + 1;
+    while (k < nb && cuts[k + 1] - cuts[j] <= limit) ++k;
+    pb.push_back(k);
+  }
+  return pb;
+}
+
+// Stream the merged output of `m` (in ws.out, complete on the device) to the host in pieces that end on
+// record boundaries (the cuts): up to kOutSlots pieces of kOutPiece bytes queued on the GPU's SDMA
+// engines ahead of the consumer, fn(piece k) running while pieces k+1.. land. fn(ptr, first_cut,
+// last_cut) gets the bytes of cuts [first_cut, last_cut] (ptr = byte cuts[first_cut]). A record larger
+// than a piece, or no SDMA engine: two 64 MiB pieces through hipMemcpyAsync on `s`.
 template <typename Fn>
 void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&& fn, const uint8_t* src = nullptr) {
   const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
   if (nb == 0) return;
   const uint8_t* out = src ? src : ws.out.as<uint8_t>();
+  if (ws.sdma_out_ok && !ws.oring) {
+    try {
+      int dev = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      ws.oeng = &gpu::SdmaEngine::for_device(dev);
+      ws.oring = static_cast<uint8_t*>(ws.oeng->acquire_ring((size_t)kOutSlots * kOutPiece));
+      for (int i = 0; i < kOutSlots; ++i) ws.osig.push_back(ws.oeng->make_signal());
+    } catch (const std::exception& e) {
+      UDA_LOG(kInfo, "stream_out: no SDMA delivery ring (%s): hipMemcpyAsync pieces", e.what());
+      ws.sdma_out_ok = false;
+    }
+  }
+  if (ws.oring) {
+    const std::vector<size_t> pb = piece_bounds(m.cuts, kOutPiece);
+    if (!pb.empty()) {
+      const size_t np = pb.size() - 1;
+      gpu::SdmaEngine& eng = *ws.oeng;
+      auto issue = [&](size_t k) {
+        const int64_t b = m.cuts[pb[k]], len = m.cuts[pb[k + 1]] - b;
+        hsa_signal_t sg = ws.osig[k % kOutSlots];
+        gpu::SdmaEngine::arm(sg, eng.parts((size_t)len, 1));
+        eng.copy_d2h(ws.oring + (k % kOutSlots) * kOutPiece, out + b, (size_t)len, sg, 1);
+      };
+      size_t issued = 0, k = 0;
+      // a consumer that throws (a stopped task) leaves copies in flight into the ring: they land before
+      // the ring and its signals serve the next output
+      struct Drain {
+        DeviceWorkspace& ws;
+        size_t& issued;
+        size_t& k;
+        ~Drain() {
+          for (size_t j = k; j < issued; ++j) {
+            try {
+              gpu::SdmaEngine::wait(ws.osig[j % kOutSlots]);
+            } catch (...) {
+            }
+          }
+        }
+      } drain{ws, issued, k};
+      for (; issued < std::min<size_t>(np, kOutSlots); ++issued) issue(issued);
+      for (; k < np; ++k) {
+        auto t0 = std::chrono::steady_clock::now();
+        gpu::SdmaEngine::wait(ws.osig[k % kOutSlots]);
+        auto t1 = std::chrono::steady_clock::now();
+        ws.d2h_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        const int64_t tp = trace::host_enabled() ? trace::now_ns() : 0;
+        if (tp) trace::host_event("so_wait", (int64_t)(uintptr_t)&ws, 0, tp - (int64_t)(t1 - t0).count(), tp);
+        fn(ws.oring + (k % kOutSlots) * kOutPiece, pb[k], pb[k + 1]);
+        ws.sink_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        if (tp) trace::host_event("so_sink", (int64_t)(uintptr_t)&ws, m.cuts[pb[k + 1]] - m.cuts[pb[k]], tp,
+                                  trace::now_ns());
+        if (k + kOutSlots < np) issue(issued++);  // its slot was just consumed
+      }
+      return;
+    }
+  }
   if (ws.ring.size() < (size_t)(2 * kPieceBytes)) {  // on the GPU's NUMA node, like the consumer copying out of it
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
