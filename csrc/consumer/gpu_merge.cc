@@ -108,6 +108,7 @@ struct DeviceWorkspace {
   uint8_t* oring = nullptr;
   std::vector<hsa_signal_t> osig;
   bool sdma_out_ok = true;
+  int out_ways = 1;  // SDMA engines each delivery piece is split over (the job's long pole: more)
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
@@ -131,7 +132,10 @@ struct DeviceWorkspace {
       if (e) (void)hipEventDestroy(e);
     if (cs) (void)hipStreamDestroy(cs);
   }
-  void reset_stats() { h2d_ms = device_ms = d2h_ms = sink_ms = 0; }
+  void reset_stats() {
+    h2d_ms = device_ms = d2h_ms = sink_ms = 0;
+    out_ways = 1;
+  }
   // D2H stream of streamed deliveries (the merge stream is busy with the next round)
   hipStream_t copy_stream() {
     if (!cs) HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
@@ -749,8 +753,8 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
       auto issue = [&](size_t k) {
         const int64_t b = m.cuts[pb[k]], len = m.cuts[pb[k + 1]] - b;
         hsa_signal_t sg = ws.osig[k % kOutSlots];
-        gpu::SdmaEngine::arm(sg, eng.parts((size_t)len, 1));
-        eng.copy_d2h(ws.oring + (k % kOutSlots) * kOutPiece, out + b, (size_t)len, sg, 1);
+        gpu::SdmaEngine::arm(sg, eng.parts((size_t)len, ws.out_ways));
+        eng.copy_d2h(ws.oring + (k % kOutSlots) * kOutPiece, out + b, (size_t)len, sg, ws.out_ways);
       };
       size_t issued = 0, k = 0;
       // a consumer that throws (a stopped task) leaves copies in flight into the ring: they land before
@@ -2958,6 +2962,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     sg.s = nullptr;
     sg.s = gpu::pooled_stream(hi);
     s = sg.s;
+    // and its delivery pieces go over two SDMA engines instead of one: the link is shared per queued copy,
+    // so while the other tasks deliver, this one's output keeps a larger share of it
+    ws.out_ways = 2;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
