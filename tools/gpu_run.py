@@ -251,7 +251,7 @@ def main() -> int:
     ap.add_argument("--cmd", action="append", default=[], help="ad-hoc step NAME=SECONDS=COMMAND")
     ap.add_argument("--keys", default="", help="extra JSON keys to print from each step's last JSON line")
     ap.add_argument("--list", action="store_true")
-    a = ap.parse_args()
+    a = ap.parse_intermixed_args()  # steps may follow --cmd
     recipes = dict(RECIPES)
     for c in a.cmd:
         name, secs, cmd = c.split("=", 2)
