@@ -131,6 +131,7 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
         lo.capacity = hb == "auto" ? 0 : std::atoll(hb.c_str());
         lo.lease_s = h->host->conf_f64("mapred.uda.provider.hbm.lease.s", 600);
         lo.idle_evict_s = h->host->conf_f64("mapred.uda.provider.hbm.idle.evict.s", 30);
+        lo.cached_read = h->host->conf_i64("mapred.uda.provider.hbm.cached.read", 1) != 0;
         if (lo.capacity > 0) {
           // default: stripe the store over every GPU the provider sees, so a node's reduce tasks (placed
           // over all GPUs, mapred.uda.gpu.device=auto) find their map outputs spread the same way

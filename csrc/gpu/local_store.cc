@@ -34,6 +34,7 @@ class LocalDeviceStore : public DeviceStore {
     co.odirect = true;
     co.lease_s = o.lease_s;
     co.idle_evict_s = o.idle_evict_s;
+    co.cached_read = o.cached_read;
     cache_ = std::make_unique<gpu::MofCache>(co);
     cache_->start_loaders();  // the loaders come up now, not under the first wave
   }
@@ -74,6 +75,7 @@ class LocalDeviceStore : public DeviceStore {
            ",\"open_file_max_ms\":" + std::to_string(st.open_file_max_ms) + ",\"load_gbps\":" +
            std::to_string(st.load_wall_ms > 0 ? (double)st.bytes_loaded / st.load_wall_ms / 1e6 : 0.0) +
            ",\"declined\":" + std::to_string(st.declined) + ",\"evictions\":" + std::to_string(st.evictions) +
+           ",\"cached_reads\":" + std::to_string(st.cached_reads) +
            ",\"bytes_loaded\":" + std::to_string(st.bytes_loaded) + ",\"resident_bytes\":" +
            std::to_string(st.resident_bytes) + ",\"capacity\":" + std::to_string(cache_->capacity()) +
            ",\"load_ms\":" + std::to_string(st.load_ms) + ",\"first_miss_boot_ms\":" +

@@ -57,6 +57,9 @@ class MofCache {
     int chunks = 16;                 // reads + copies in flight per loader
     int64_t read_bytes = 0;          // disk request size a chunk is read in (0: one read per chunk)
     bool odirect = true;
+    // a file whose pages are already in the page cache (map outputs written moments ago) is read through
+    // it instead of with O_DIRECT (mapred.uda.provider.hbm.cached.read)
+    bool cached_read = true;
     double lease_s = 600;            // a holder on another node idle this long is presumed dead
     // An unreferenced entry is evicted to admit another file of ITS OWN job only after this many seconds
     // without a fetch (mapred.uda.provider.hbm.idle.evict.s; 0: plain LRU). A job whose MOFs outgrow the
@@ -74,6 +77,7 @@ class MofCache {
   };
   struct Stats {
     int64_t loads = 0, hits = 0, declined = 0, evictions = 0, bytes_loaded = 0, resident_bytes = 0;
+    int64_t cached_reads = 0;  // files read through the page cache (Options::cached_read)
     int64_t holders = 0, holders_reaped = 0, releases = 0;
     double load_ms = 0;       // summed per-file load time
     double load_wall_ms = 0;  // time any load was in progress (loads overlap)

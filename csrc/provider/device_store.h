@@ -39,6 +39,7 @@ struct LocalStoreOptions {
   std::vector<int> devices{0};
   double lease_s = 600;
   double idle_evict_s = 0;  // gpu::MofCache::Options::idle_evict_s
+  bool cached_read = true;  // gpu::MofCache::Options::cached_read
 };
 // The store in this process (gpu/mof_cache.h).
 std::unique_ptr<DeviceStore> make_local_device_store(const LocalStoreOptions& o);

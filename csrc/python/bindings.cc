@@ -913,17 +913,18 @@ PYBIND11_MODULE(_uda_native, m) {
   // the provider's HBM store of MOF files on its own (gpu/mof_cache.h): loads, holders, eviction
   py::class_<gpu::MofCache>(m, "MofStore")
       .def(py::init([](int64_t capacity, std::vector<int> devices, double lease_s, int64_t chunk_bytes,
-                       double idle_evict_s) {
+                       double idle_evict_s, bool cached_read) {
              gpu::MofCache::Options o;
              o.capacity = capacity;
              o.devices = devices;
              o.lease_s = lease_s;
              o.chunk_bytes = chunk_bytes;
              o.idle_evict_s = idle_evict_s;
+             o.cached_read = cached_read;
              return new gpu::MofCache(o);
            }),
            py::arg("capacity"), py::arg("devices") = std::vector<int>{0}, py::arg("lease_s") = 600.0,
-           py::arg("chunk_bytes") = 16 << 20, py::arg("idle_evict_s") = 0.0)
+           py::arg("chunk_bytes") = 16 << 20, py::arg("idle_evict_s") = 0.0, py::arg("cached_read") = true)
       .def("acquire",
            [](gpu::MofCache& c, const std::string& job, const std::string& path, const std::string& holder) {
              gpu::MofCache::Ref r;
@@ -950,6 +951,7 @@ PYBIND11_MODULE(_uda_native, m) {
         d["holders"] = s.holders;
         d["holders_reaped"] = s.holders_reaped;
         d["releases"] = s.releases;
+        d["cached_reads"] = s.cached_reads;
         return d;
       });
   m.def("reducer_holder_id", &gpu::reducer_holder_id);

@@ -728,6 +728,7 @@ int run_node_daemon(int ctl_fd) {
       so.capacity = store_capacity(d->conf("mapred.uda.provider.hbm.bytes", "auto"), devs);
       so.lease_s = std::atof(d->conf("mapred.uda.provider.hbm.lease.s", "600").c_str());
       so.idle_evict_s = std::atof(d->conf("mapred.uda.provider.hbm.idle.evict.s", "30").c_str());
+      so.cached_read = std::atoi(d->conf("mapred.uda.provider.hbm.cached.read", "1").c_str()) != 0;
       if (so.capacity > 0) {
         std::lock_guard<std::mutex> g(d->mu);
         d->store = make_local_device_store(so);

@@ -79,6 +79,23 @@ def test_a_job_does_not_evict_its_own_recently_served_files(require_gpu, native,
     assert st["evictions"] == 2 and st["declined"] == 1, st
 
 
+@pytest.mark.parametrize("cached_read", [True, False])
+def test_files_in_the_page_cache_are_read_through_it(require_gpu, native, tmp_path, cached_read):
+    """mapred.uda.provider.hbm.cached.read: a MOF file whose pages are all in the page cache (just written)
+    is loaded with buffered reads instead of O_DIRECT (which would read it from the disk again); either way
+    every byte lands."""
+    size = 24 * MB + 4096 * 3 + 100  # a short, unaligned last read
+    f = _files(tmp_path, 2, size)
+    for p in f:
+        open(p, "rb").read()  # (surely) in the page cache
+    store = native.MofStore(capacity=4 * size, devices=[0], chunk_bytes=4 * MB, cached_read=cached_read)
+    for p in f:
+        ok, why, a, n, _ = store.acquire("job", p, "r")
+        assert ok and n == size, why
+        assert native.device_read(a, size) == open(p, "rb").read()
+    assert store.stats()["cached_reads"] == (2 if cached_read else 0)
+
+
 def test_dead_or_foreign_holders_are_dropped(require_gpu, native, tmp_path):
     size = 8 * MB
     f = _files(tmp_path, 3, size)
