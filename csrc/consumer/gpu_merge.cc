@@ -108,8 +108,7 @@ struct DeviceWorkspace {
   uint8_t* oring = nullptr;
   std::vector<hsa_signal_t> osig;
   bool sdma_out_ok = true;
-  int out_ways = 1;      // SDMA engines each delivery piece is split over
-  bool out_alt = false;  // delivery on the second engine (the job's long pole)
+  int out_ways = 1;  // SDMA engines each delivery piece is split over (the job's long pole: more)
   hsa_signal_t h2d_sig{};    // SDMA copies of this workspace: H2D of pinned spans (device_merge), LPQ spill D2H
   bool h2d_sdma_ok = true;
   double h2d_ms = 0, device_ms = 0, d2h_ms = 0, sink_ms = 0;
@@ -136,7 +135,6 @@ struct DeviceWorkspace {
   void reset_stats() {
     h2d_ms = device_ms = d2h_ms = sink_ms = 0;
     out_ways = 1;
-    out_alt = false;
   }
   // D2H stream of streamed deliveries (the merge stream is busy with the next round)
   hipStream_t copy_stream() {
@@ -756,7 +754,7 @@ void stream_out(DeviceWorkspace& ws, const DeviceMergeOut& m, hipStream_t s, Fn&
         const int64_t b = m.cuts[pb[k]], len = m.cuts[pb[k + 1]] - b;
         hsa_signal_t sg = ws.osig[k % kOutSlots];
         gpu::SdmaEngine::arm(sg, eng.parts((size_t)len, ws.out_ways));
-        eng.copy_d2h(ws.oring + (k % kOutSlots) * kOutPiece, out + b, (size_t)len, sg, ws.out_ways, ws.out_alt);
+        eng.copy_d2h(ws.oring + (k % kOutSlots) * kOutPiece, out + b, (size_t)len, sg, ws.out_ways);
       };
       size_t issued = 0, k = 0;
       // a consumer that throws (a stopped task) leaves copies in flight into the ring: they land before
@@ -2964,10 +2962,9 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     sg.s = nullptr;
     sg.s = gpu::pooled_stream(hi);
     s = sg.s;
-    // and its delivery goes over a second SDMA engine: on the first one the tasks' copy queues take turns,
-    // 1/16 of the link for this task while 15 others deliver; two engines share the link about evenly
-    // (two splitting each piece over both engines measured the same as one: 43.2 vs 42.9 GB/s)
-    ws.out_alt = true;
+    // and its delivery pieces go over two SDMA engines instead of one: the link is shared per queued copy,
+    // so while the other tasks deliver, this one's output keeps a larger share of it
+    ws.out_ways = 2;
   }
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +

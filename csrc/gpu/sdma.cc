@@ -404,11 +404,6 @@ SdmaEngine::SdmaEngine(int device) {
   }
   for (int b = 0; b < 16; ++b)
     if (use & (1u << b)) engine_ids_.push_back(1u << b);
-  {  // the second delivery engine: another of engines 0-3 (4-7 stream at half the rate)
-    uint32_t alt = mask & ~use & 0xFu;
-    alt &= (~alt + 1u);
-    alt_d2h_engine_ = alt;
-  }
   uint32_t hmask = 0;
   if (hsa_amd_memory_copy_engine_status(gpu_, cpu_, &hmask) != HSA_STATUS_SUCCESS) hmask = 0;
   uint32_t other = hmask & ~use;  // staging on a different engine than delivery
@@ -540,7 +535,7 @@ int SdmaEngine::parts(size_t bytes, int ways) const {
   return n < 1 ? 1 : n;
 }
 
-int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways, bool alt) {
+int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways) {
   const int n = parts(bytes, ways);
   if (n == 0) return 0;
   size_t per = (bytes + n - 1) / n;
@@ -552,10 +547,7 @@ int SdmaEngine::copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_
     void* d = static_cast<uint8_t*>(dst_host) + off;
     const void* s = static_cast<const uint8_t*>(src_dev) + off;
     hsa_status_t st = HSA_STATUS_ERROR;
-    if (alt && alt_d2h_engine_) {
-      st = hsa_amd_memory_async_copy_on_engine(d, cpu_, s, gpu_, len, 0, nullptr, sig,
-                                               (hsa_amd_sdma_engine_id_t)alt_d2h_engine_, false);
-    } else if (!engine_ids_.empty()) {
+    if (!engine_ids_.empty()) {
       const uint32_t eng = engine_ids_[(size_t)(next_engine_.fetch_add(1) & 0x7fffffff) % engine_ids_.size()];
       st = hsa_amd_memory_async_copy_on_engine(d, cpu_, s, gpu_, len, 0, nullptr, sig,
                                                (hsa_amd_sdma_engine_id_t)eng, false);

@@ -49,9 +49,7 @@ class SdmaEngine {
   void destroy_signal(hsa_signal_t s);
   // Device -> host copy of `bytes`, split over up to `ways` engines; `sig` must hold the number of
   // parts this call adds (use arm()): returns the number of parts issued.
-  // alt: every part on the second delivery engine (a skewed job's long-pole task: while the other tasks
-  // queue on the first engine, its copies do not wait for their turn behind all of them).
-  int copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways, bool alt = false);
+  int copy_d2h(void* dst_host, const void* src_dev, size_t bytes, hsa_signal_t sig, int ways);
   // Parts copy_d2h(bytes, ways) will issue.
   int parts(size_t bytes, int ways) const;
   // Host -> device copy (one part) on an SDMA engine other than the delivery engine when the device
@@ -76,7 +74,6 @@ class SdmaEngine {
   hsa_amd_memory_pool_t host_pool_{};
   std::vector<uint32_t> engine_ids_;  // SDMA engine bits usable for CPU <- GPU copies
   uint32_t h2d_engine_ = 0;           // SDMA engine bit for GPU <- CPU staging (0: runtime's choice)
-  uint32_t alt_d2h_engine_ = 0;       // a second CPU <- GPU engine (0: none)
   int numa_node_ = -1;
   std::atomic<int> next_engine_{0};
   bool hsa_inited_ = false;
