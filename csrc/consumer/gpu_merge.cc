@@ -2343,8 +2343,7 @@ void ReduceTask::merge_gpu() {
 // 24.0 (profiles/r6/r6j_*, r6k_nodefiles62_store20.log). Over TCP every byte is copied twice by the CPU
 // (the provider's sendfile, the reducer's receive) next to the consumers' own copies. The reference's
 // fetcher keeps its requests in flight the same way (Segment::send_request, src/Merger/StreamRW.cc).
-namespace {
-bool local_host(const std::string& spec) {
+bool mof_host_is_local(const std::string& spec) {
   std::string h = spec;
   if (const size_t c = h.rfind(':'); c != std::string::npos && h.find(':') == c) h = h.substr(0, c);
   if (h == "127.0.0.1" || h == "localhost" || h == "::1" || h.empty()) return true;
@@ -2354,8 +2353,6 @@ bool local_host(const std::string& spec) {
   return h == m || h == m.substr(0, m.find('.')) || m == h.substr(0, h.find('.'));
 }
 
-// A MOF file this process may read in place of fetching it: a regular file (no symlink) of our own user
-// holding [off, off + len). -1 if not.
 int open_local_mof(const std::string& path, int64_t off, int64_t len) {
   if (path.empty() || path[0] != '/') return -1;
   const int fd = ::open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
@@ -2367,7 +2364,6 @@ int open_local_mof(const std::string& path, int64_t off, int64_t len) {
   }
   return fd;
 }
-}  // namespace
 
 int64_t ReduceTask::fetch_declined_bytes(int device, const std::vector<DeclinedPart>& parts, gpu::DeviceBuffer& dst,
                                          std::vector<const uint8_t*>* where, int64_t* local) {
@@ -2442,7 +2438,7 @@ int64_t ReduceTask::fetch_declined_bytes(int device, const std::vector<DeclinedP
         const FetchParams& f = d.f;
         const int64_t L = d.len;
         uint8_t* dev = base + at[k];
-        fd = local_ok && local_host(f.host) ? open_local_mof(d.path, d.file_off, L) : -1;
+        fd = local_ok && mof_host_is_local(f.host) ? open_local_mof(d.path, d.file_off, L) : -1;
         if (fd >= 0) {
           for (int64_t off = 0, s = 0; off < L; s = (s + 1) % kSlots) {
             Slot& x = sl[s];

@@ -89,6 +89,12 @@ struct ReduceStats {
   std::string backend;
 };
 
+// A declined partition read in place of fetching it (device fetch, mapred.uda.gpu.fetch.local.read): the
+// provider host spec ("host[:port]") names this node, and the MOF file the provider named is a regular file
+// (not a symlink) of this process's user holding [off, off + len) -- the descriptor open for reading, or -1.
+bool mof_host_is_local(const std::string& host_spec);
+int open_local_mof(const std::string& path, int64_t off, int64_t len);
+
 // File confinement of a reduce task that runs on behalf of another local user (a merge-service session
 // whose client's uid is not the service's): what the task creates, reads back and unlinks must stay in the
 // node's own local directories, and it trusts only files this process's user owns.

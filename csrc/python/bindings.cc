@@ -20,6 +20,7 @@
 #include "device_engine.h"
 #include "device_ptr.h"
 #include "mof_cache.h"
+#include "consumer/reduce_task.h"
 #include "service/merge_service.h"
 #include "exchange.h"
 #include "api_bench.h"
@@ -1020,6 +1021,12 @@ PYBIND11_MODULE(_uda_native, m) {
   });
   // one TCP client, a fetch to an unreachable host on one thread and, while it is still trying, one to a
   // live host: returns (live fetch ms, dead host error, dead host ms, second dead fetch ms)
+  m.def("mof_host_is_local", &uda::mof_host_is_local);
+  m.def("local_mof_readable", [](const std::string& path, int64_t off, int64_t len) {
+    const int fd = uda::open_local_mof(path, off, len);
+    if (fd >= 0) ::close(fd);
+    return fd >= 0;
+  });
   // ACK string codec (transport.h): format then parse, as a TCP reducer sees the provider's answer
   m.def("ack_roundtrip", [](int status, int64_t raw_len, int64_t part_len, int64_t sent, int64_t mof_offset,
                             const std::string& path, const std::string& error) {

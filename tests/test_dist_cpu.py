@@ -291,3 +291,28 @@ def test_declined_descriptor_ack_keeps_partition_lengths(native):
     assert (ok["status"], ok["part_len"], ok["sent"], ok["path"]) == (0, 8, 8, "/a:b/file.out")
     err = native.ack_roundtrip(-2, 0, 0, 0, 0, "", "cannot resolve MOF j/m/0")
     assert err["status"] == -2 and err["error"] == "cannot resolve MOF j/m/0"
+
+
+def test_declined_partitions_are_read_locally_only_from_own_regular_files(native, tmp_path):
+    """mapred.uda.gpu.fetch.local.read: a reducer reads a declined partition from the MOF file the provider
+    named only when the provider is on this node and the file is a regular file of its own user that holds
+    the partition -- never through a symlink, never past the file's end, never a relative path."""
+    import socket
+    assert native.mof_host_is_local("127.0.0.1:9011") and native.mof_host_is_local("localhost")
+    assert native.mof_host_is_local(socket.gethostname())
+    assert not native.mof_host_is_local("10.255.255.1:9011")
+    mof = tmp_path / "file.out"
+    mof.write_bytes(b"x" * 4096)
+    assert native.local_mof_readable(str(mof), 0, 4096)
+    assert native.local_mof_readable(str(mof), 1000, 3096)
+    assert not native.local_mof_readable(str(mof), 1000, 3097)  # past the end
+    link = tmp_path / "link.out"
+    link.symlink_to(mof)
+    assert not native.local_mof_readable(str(link), 0, 10)  # a symlink planted in the path
+    assert not native.local_mof_readable("file.out", 0, 10)  # relative
+    assert not native.local_mof_readable(str(tmp_path), 0, 0)  # a directory
+    if os.geteuid() == 0:  # a file of another user
+        other = tmp_path / "other.out"
+        other.write_bytes(b"y" * 4096)
+        os.chown(other, 65534, 65534)
+        assert not native.local_mof_readable(str(other), 0, 10)
