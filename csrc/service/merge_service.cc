@@ -1,5 +1,6 @@
 // Node merge service and its client. See merge_service.h.
 #include "merge_service.h"
+#include "uda/start_trace.h"
 
 #include <fcntl.h>
 #include <poll.h>
@@ -252,6 +253,7 @@ struct MergeService::Session : std::enable_shared_from_this<MergeService::Sessio
       if (svc->opt_.session_closed) svc->opt_.session_closed(token);
       return;
     }
+    start_trace("svc_ready", token);
     send(kReady, "");
     svc->sessions_.fetch_add(1);
     run_commands();
@@ -544,6 +546,7 @@ void MergeService::handshake(int fd) {
   timeval none{0, 0};
   (void)::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
   const uint64_t token = get<uint64_t>(p, 0);
+  start_trace(t == kDataHello ? "svc_data_hello" : "svc_hello", token);
   if (t == kDataHello) {  // a task's data connection: attach it to its session (same peer process)
     // the control connection's handshake (its own thread) may not have registered the session yet
     std::shared_ptr<Session> owner;
@@ -750,6 +753,7 @@ static void check_service_peer(int fd, const std::string& path, const std::strin
 RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<std::string>& args, Host* host)
     : impl_(new Impl) {
   impl_->host = host;
+  start_trace("client_begin", 0);
   const std::string server_users = host->get_conf("mapred.uda.gpu.merge.service.server.users", "");
   impl_->sock = frame::unix_connect(path);
   if (impl_->sock < 0) throw UdaError("merge service " + path + " not reachable: " + strerror(errno));
@@ -766,6 +770,7 @@ RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<st
     hello += args[i];
   }
   if (!send_msg(impl_->sock, kHello, hello)) throw UdaError("merge service " + path + ": HELLO failed");
+  start_trace("client_hello_sent", token);
   impl_->dsock = frame::unix_connect(path);
   if (impl_->dsock >= 0) check_service_peer(impl_->dsock, path, server_users);
   std::string dh;
@@ -775,7 +780,9 @@ RemoteReduceTask::RemoteReduceTask(const std::string& path, const std::vector<st
   Impl* im = impl_.get();
   impl_->data_reader = std::thread([im] { im->data_loop(); });
   impl_->reader = std::thread([im] { im->read_loop(); });
+  start_trace("client_data_sent", token);
   const auto r = impl_->wait_result();
+  start_trace("client_ready", token);
   if (r.first != 0) {
     {
       std::lock_guard<std::mutex> g(impl_->mu);

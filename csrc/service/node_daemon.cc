@@ -30,6 +30,7 @@
 #include "uda/error.h"
 #include "uda/frame.h"
 #include "uda/log.h"
+#include "uda/start_trace.h"
 #include "uda/topology.h"
 #include "uda/transport.h"
 #include "uda/uda_bridge.h"
@@ -584,6 +585,7 @@ struct Daemon {
       int pfd;
       if (!recv_msg(ctl, &t, &p, &pfd)) break;
       if (t == kDAdopt) {  // a client connection routed to this daemon's merge service
+        start_trace("daemon_adopt", 0);
         std::lock_guard<std::mutex> g(mu);
         if (svc && pfd >= 0)
           svc->adopt(pfd);
@@ -953,7 +955,10 @@ void NodeDaemonSet::route_main() {
     (void)::poll(pf.data(), pf.size(), 200);
     if (pf[0].revents & POLLIN) {
       const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
-      if (fd >= 0) pend.push_back(Pend{fd, std::chrono::steady_clock::now() + std::chrono::seconds(10)});
+      if (fd >= 0) {
+        start_trace("router_accept", 0);
+        pend.push_back(Pend{fd, std::chrono::steady_clock::now() + std::chrono::seconds(10)});
+      }
     }
     const auto now = std::chrono::steady_clock::now();
     for (auto it = data_route.begin(); it != data_route.end();)  // data connections that never came
@@ -987,6 +992,7 @@ void NodeDaemonSet::route_main() {
           }
         }
         if (target >= 0 && d_[(size_t)target]->adopt(pend[k].fd, type == 1 ? token : 0)) {
+          start_trace(type == 1 ? "router_hello" : "router_data", token);
           routed_++;
         } else {
           refused_++;
