@@ -457,31 +457,43 @@ void MergeService::accept_main() {
     // no listener (connections come by adopt()): the loop only reaps finished sessions and handshakes
     const int pr = listen_fd_ >= 0 ? ::poll(&pf, 1, 200) : (::poll(nullptr, 0, 200), 0);
     {  // reap finished sessions and handshakes
+      // Taken out under mu_, joined and destroyed after it: the last reference to a session runs its
+      // reduce task's teardown (pooled workspaces back, pinned rings, streams), ~5-10 ms each, and under
+      // mu_ that stalled every adopt() -- and with it the daemon's control channel, descriptor fetches
+      // included -- for ~95 ms at the start of each wave of reduce tasks (UDA_START_TRACE, r7a).
+      std::vector<std::shared_ptr<Session>> done_sessions;
       std::vector<std::thread> done_shakes;
-      std::lock_guard<std::mutex> g(mu_);
-      for (auto it = live_.begin(); it != live_.end();) {
-        Session& s = **it;
-        bool done;
-        {
-          std::lock_guard<std::mutex> sg(s.mu);
-          done = s.closed && s.finished.load();  // joins below return at once
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto it = live_.begin(); it != live_.end();) {
+          Session& s = **it;
+          bool done;
+          {
+            std::lock_guard<std::mutex> sg(s.mu);
+            done = s.closed && s.finished.load();  // joins below return at once
+          }
+          if (done) {
+            done_sessions.push_back(std::move(*it));
+            it = live_.erase(it);
+          } else {
+            ++it;
+          }
         }
-        if (done) {
-          if (s.reader.joinable()) s.reader.join();
-          if (s.runner.joinable()) s.runner.join();
-          it = live_.erase(it);
-        } else {
-          ++it;
+        for (uint64_t id : shakes_done_) {
+          auto t = shakes_.find(id);
+          if (t != shakes_.end()) {
+            done_shakes.push_back(std::move(t->second));  // it has returned
+            shakes_.erase(t);
+          }
         }
+        shakes_done_.clear();
       }
-      for (uint64_t id : shakes_done_) {
-        auto t = shakes_.find(id);
-        if (t != shakes_.end()) {
-          t->second.join();  // it has returned
-          shakes_.erase(t);
-        }
+      for (auto& sp : done_sessions) {
+        if (sp->reader.joinable()) sp->reader.join();
+        if (sp->runner.joinable()) sp->runner.join();
       }
-      shakes_done_.clear();
+      done_sessions.clear();
+      for (auto& t : done_shakes) t.join();
     }
     if (pr <= 0 || !(pf.revents & POLLIN)) continue;
     const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
