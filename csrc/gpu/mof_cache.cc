@@ -534,6 +534,20 @@ void MofCache::loader_main(Loader* L) {
     try {
       const char* h2d = std::getenv("UDA_STORE_H2D");  // A/B: "blit" copies chunks with hipMemcpyAsync
       L->sdma = h2d && std::string(h2d) == "blit" ? nullptr : &SdmaEngine::for_device(L->device);
+      if (L->sdma) {
+        // the runtime creates an SDMA engine's queue at its first copy (~150 ms): take that now, not at the
+        // first chunk of the first wave -- the loader issues copies holding mu_, and every descriptor fetch
+        // of the node (the daemon's control channel) waited behind it (UDA_START_TRACE: a 173 ms stall)
+        void* scratch = nullptr;
+        HIP_CHECK(hipMalloc(&scratch, 4096));
+        try {
+          L->sdma->warm(scratch);
+        } catch (...) {
+          (void)hipFree(scratch);
+          throw;
+        }
+        HIP_CHECK(hipFree(scratch));
+      }
     } catch (const std::exception& ex) {
       UDA_LOG(kWarn, "provider HBM store: no SDMA engine on device %d (%s); hipMemcpyAsync", L->device, ex.what());
       L->sdma = nullptr;
