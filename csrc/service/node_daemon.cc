@@ -324,7 +324,9 @@ void NodeDaemonClient::reader_main(int fd, uint64_t gen) {
         done = std::move(it->second);
         pending_.erase(it);
       }
+      start_trace("fe_acquired", id);
       done(status, desc);
+      start_trace("fe_acquired_done", id);
     } else if (t == kDConfReq) {
       const uint32_t id = get<uint32_t>(p, 0);
       size_t at = 4;
@@ -594,6 +596,7 @@ struct Daemon {
         continue;
       }
       if (pfd >= 0) ::close(pfd);
+      start_trace(t == kDAcquire ? "daemon_acquire_msg" : "daemon_msg", t);
       std::shared_ptr<DeviceStore> st;
       {
         std::lock_guard<std::mutex> g(mu);
@@ -618,7 +621,9 @@ struct Daemon {
           put<uint64_t>(r, id);
           put<int32_t>(r, status);
           put_str(r, desc);
+          start_trace("daemon_reply", id);
           (void)send(kDAcquired, r);
+          start_trace("daemon_reply_sent", id);
         };
         std::string why;
         if (!st) {
@@ -626,6 +631,7 @@ struct Daemon {
         } else if (!st->acquire(job, path, holder, off, len, reply, &why)) {
           reply(kNotDeviceResident, "provider HBM store: " + why);
         }
+        start_trace("daemon_acquire_done", id);
       } else if (t == kDRelease) {
         size_t at = 0;
         const std::string path = get_str(p, &at), holder = get_str(p, &at);
