@@ -5,6 +5,7 @@
 #include <memory>
 #include <string>
 
+#include "uda/start_trace.h"
 #include "../provider/device_store.h"
 #include "device_ptr.h"
 #include "mof_cache.h"
@@ -53,7 +54,9 @@ class LocalDeviceStore : public DeviceStore {
           if (need > ref.len) return done(-4, "index beyond MOF file " + path);
           if (local || ref.ipc.handle_hex != "-")
             return done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, ref.ipc, /*leased=*/true));
+          start_trace("store_export_begin", 0);
           gpu::IpcExport x = cache->export_of(path);
+          start_trace("store_export_end", 0);
           if (x.handle_hex == "-") x.base = ref.ipc.base;  // not exportable: the descriptor says so
           done(0, gpu::make_device_descriptor(ref.device, ref.data + offset, x, /*leased=*/true));
         },

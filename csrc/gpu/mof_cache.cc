@@ -19,6 +19,7 @@
 #include "uda/fault.h"
 #include "uda/log.h"
 #include "uda/node_registry.h"
+#include "uda/start_trace.h"
 
 namespace uda {
 namespace gpu {
@@ -230,7 +231,9 @@ bool MofCache::acquire_async(const std::string& job, const std::string& path, co
     if (why) *why = "provider HBM store disabled";
     return false;
   }
+  start_trace("store_acquire_begin", 0);
   std::unique_lock<std::mutex> lk(mu_);
+  start_trace("store_acquire_locked", 0);
   const double now = now_s();
   auto it = entries_.find(path);
   if (it != entries_.end()) {
