@@ -570,66 +570,6 @@ struct StagedCount {
   ~StagedCount() { staged_merges(device).fetch_sub(1); }
 };
 
-// A skewed job's long pole (a task holding more than a round of the device's generic merges) decides the
-// job's time: while one delivers on a device, the other generic-round tasks of the device deliver `slots`
-// at a time (FIFO, mapred.uda.gpu.longpole.slots, default 1; 0 = off). All at once, 15 small tasks took
-// 15/16 of the link while the long pole's consumer waited 0.69 s per step for its D2H (config #5,
-// 60 % of 100 GB in one task); they have the slack: they finish long before it.
-class LongPoleGate {
- public:
-  static LongPoleGate& get() {
-    static LongPoleGate* g = new LongPoleGate;  // never destroyed: tasks may outlive static teardown
-    return *g;
-  }
-  void pole_begin(int device) {
-    std::lock_guard<std::mutex> g(mu_);
-    devs_[device].poles++;
-  }
-  void pole_end(int device) {
-    std::lock_guard<std::mutex> g(mu_);
-    devs_[device].poles--;
-    cv_.notify_all();
-  }
-  // A small task's delivery: true once it may deliver (call small_end), at once when no long pole
-  // delivers on the device; false if `stopped` became true while waiting.
-  template <class Stop>
-  bool small_begin(int device, int slots, Stop&& stopped) {
-    std::unique_lock<std::mutex> lk(mu_);
-    Dev& d = devs_[device];
-    const uint64_t me = d.next_ticket++;
-    d.waiting.push_back(me);
-    for (;;) {
-      if (d.waiting.front() == me && (d.poles == 0 || d.active < slots)) {
-        d.waiting.pop_front();
-        ++d.active;
-        cv_.notify_all();
-        return true;
-      }
-      if (stopped()) {
-        d.waiting.erase(std::find(d.waiting.begin(), d.waiting.end(), me));
-        cv_.notify_all();
-        return false;
-      }
-      cv_.wait_for(lk, std::chrono::milliseconds(20));
-    }
-  }
-  void small_end(int device) {
-    std::lock_guard<std::mutex> g(mu_);
-    devs_[device].active--;
-    cv_.notify_all();
-  }
-
- private:
-  struct Dev {
-    int poles = 0, active = 0;
-    uint64_t next_ticket = 0;
-    std::deque<uint64_t> waiting;
-  };
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::map<int, Dev> devs_;
-};
-
 struct GateLease {
   int device = -1;
   int which = 0;
@@ -3022,25 +2962,6 @@ bool ReduceTask::merge_gpu_device(bool probe) {
     // so while the other tasks deliver, this one's output keeps a larger share of it
     ws.out_ways = 2;
   }
-  const int pole_slots = (int)host_->conf_i64("mapred.uda.gpu.longpole.slots", 1);
-  const bool long_pole = total > round_bytes && pole_slots > 0;
-  struct PoleGuard {
-    int device;
-    bool on;
-    ~PoleGuard() {
-      if (on) LongPoleGate::get().pole_end(device);
-    }
-  } pole_guard{device, long_pole};
-  if (long_pole) LongPoleGate::get().pole_begin(device);
-  // a small task takes its delivery turn at its first delivered round (a long pole may have come meanwhile)
-  struct SmallGuard {
-    int device = 0;
-    bool on = false;
-    ~SmallGuard() {
-      if (on) LongPoleGate::get().small_end(device);
-    }
-  } small_guard;
-  small_guard.device = device;
   const gpu::GenericRoundsPlan rplan = gpu::plan_generic_rounds(rptr, rlen, (int)kind_, round_bytes, ws.rounds, s);
   // Round q merges into outs[q & 1] while a delivery thread streams round q-1 out (D2H pieces +
   // dataFromUda): the consumer's work (the reduce task's bound when one task holds most of the data)
@@ -3081,11 +3002,6 @@ bool ReduceTask::merge_gpu_device(bool probe) {
         DeviceMergeOut m;
         m.cuts = std::move(j.cuts);
         const size_t nb = m.cuts.size() < 2 ? 0 : m.cuts.size() - 1;
-        if (!long_pole && pole_slots > 0 && !small_guard.on && nb > 0) {
-          if (!LongPoleGate::get().small_begin(device, pole_slots, [&] { return stop_.load(); }))
-            throw UdaError("reduce task stopped while waiting for its delivery turn");
-          small_guard.on = true;
-        }
         stream_out(ws, m, ws.copy_stream(), [&](const uint8_t* piece, size_t c0, size_t c1) {
           for (size_t x = c0; x < c1; ++x) {
             const uint8_t* p = piece + (m.cuts[x] - m.cuts[c0]);
