@@ -76,8 +76,15 @@ constexpr int64_t kPieceBytes = 64 << 20;  // D2H piece of the pinned double buf
 // and two 64 MiB pieces through hipMemcpyAsync left its consumer waiting on D2H for 815 of 2742 ms while
 // 15 other tasks shared the link. Eight pieces of 16 MiB queued on the SDMA engines keep up to 128 MiB of
 // the task's output moving ahead of its consumer, as the TeraSort delivery does (device_reduce.cc).
-constexpr int kOutSlots = 8;
-constexpr int64_t kOutPiece = 16 << 20;
+// (UDA_OUT_SLOTS / UDA_OUT_PIECE_MB: A/B of the ring's geometry)
+const int kOutSlots = [] {
+  const char* e = std::getenv("UDA_OUT_SLOTS");
+  return e ? std::max(2, std::min(64, std::atoi(e))) : 8;
+}();
+const int64_t kOutPiece = [] {
+  const char* e = std::getenv("UDA_OUT_PIECE_MB");
+  return (e ? std::max<int64_t>(1, std::min<int64_t>(256, std::atoll(e))) : 16) << 20;
+}();
 
 // One merged LPQ output, resident in host memory or in a spill file.
 struct SpillRun {
