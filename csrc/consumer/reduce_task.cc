@@ -24,6 +24,7 @@
 #include "uda/queues.h"
 #include "uda/safe_file.h"
 #include "uda/trace.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 
@@ -478,9 +479,9 @@ void ReduceTask::on_init(const InitParams& p_in) {
       pc.pinned_bytes = host_->conf_i64("mapred.uda.gpu.prewarm.pinned.mb", 1024) << 20;
     pc.round_bytes = host_->conf_i64("mapred.uda.gpu.round.bytes", 2ll << 30);
     pc.maps = p.num_maps;
-    prewarm_thr_ = std::thread([this, pc] { prewarm_gpu(pc); });
+    prewarm_thr_ = std::thread([this, pc] { name_thread("uda-task-warm"); prewarm_gpu(pc); });
   }
-  merge_thr_ = std::thread([this] { merge_main(); });
+  merge_thr_ = std::thread([this] { name_thread("uda-task-merge"); merge_main(); });
 }
 
 void ReduceTask::place_on_gpu() {

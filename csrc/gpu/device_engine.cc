@@ -22,6 +22,7 @@
 
 #include "uda/log.h"
 #include "uda/vint.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 namespace gpu {
@@ -196,7 +197,7 @@ void PinnedPool::release(Block b) {
     reap_.push_back(b);
     if (!reaper_started_) {
       reaper_started_ = true;
-      std::thread([this] { reaper_main(); }).detach();  // the pool is never destroyed
+      std::thread([this] { name_thread("uda-pin-reaper"); reaper_main(); }).detach();  // the pool is never destroyed
     }
     reap_cv_.notify_one();
     return;
@@ -1432,8 +1433,8 @@ void ShuffleJob::plan() {
     items_.assign(R_, {});
     eof_bufs_.clear();
     for (int i = 0; i < R_; ++i) eof_bufs_.emplace_back(new uint8_t[(size_t)cfg_.kv_buf_bytes + 16]);
-    copy_thr_ = std::thread([this] { copy_loop(); });
-    for (int i = 0; i < R_; ++i) consumers_.emplace_back([this, i] { consume_loop(i); });
+    copy_thr_ = std::thread([this] { name_thread("uda-copy"); copy_loop(); });
+    for (int i = 0; i < R_; ++i) consumers_.emplace_back([this, i] { name_thread("uda-consume"); consume_loop(i); });
   }
   UDA_LOG(kInfo, "rank %d planned %d reducers x %d rounds, max round %ld records, delivery %s", cfg_.rank, R_, Q_,
           (long)max_round_records_, delivery_name().c_str());

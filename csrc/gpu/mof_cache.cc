@@ -20,6 +20,7 @@
 #include "uda/log.h"
 #include "uda/node_registry.h"
 #include "uda/start_trace.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 namespace gpu {
@@ -107,10 +108,10 @@ MofCache::Loader* MofCache::loader_locked(int device) {
     L.reset(new Loader);
     L->device = device;
     Loader* lp = L.get();
-    L->thr = std::thread([this, lp] { loader_main(lp); });
+    L->thr = std::thread([this, lp] { name_thread("uda-store-load"); loader_main(lp); });
     int n = 1;  // A/B: UDA_STORE_OPENERS entries allocated + exported + opened at once
     if (const char* e = std::getenv("UDA_STORE_OPENERS")) n = std::max(1, std::min(16, std::atoi(e)));
-    for (int i = 0; i < n; ++i) L->openers.emplace_back([this, lp] { opener_main(lp); });
+    for (int i = 0; i < n; ++i) L->openers.emplace_back([this, lp] { name_thread("uda-store-open"); opener_main(lp); });
   }
   return L.get();
 }
@@ -520,6 +521,7 @@ void MofCache::loader_main(Loader* L) {
     if (const char* e = std::getenv("UDA_STORE_READERS")) nreaders = std::max(1, std::min(32, std::atoi(e)));
     for (int i = 0; i < nreaders; ++i)
       L->readers.emplace_back([L, node] {
+        name_thread("uda-store-read");
         bind_thread_to_numa(node);
         for (;;) {
           std::function<void()> job;

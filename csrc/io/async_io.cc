@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "uda/log.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 
@@ -49,7 +50,7 @@ struct Op {
 class PoolIO : public AsyncIO {
  public:
   explicit PoolIO(int threads) {
-    for (int i = 0; i < (threads > 0 ? threads : 1); ++i) thr_.emplace_back([this] { loop(); });
+    for (int i = 0; i < (threads > 0 ? threads : 1); ++i) thr_.emplace_back([this] { name_thread("uda-aio"); loop(); });
   }
   ~PoolIO() override {
     {

@@ -8,6 +8,7 @@
 #include "../gpu/device_ptr.h"
 #include "uda/log.h"
 #include "uda/trace.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 
@@ -24,7 +25,7 @@ void Supplier::start() {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = false;
   }
-  for (int i = 0; i < std::max(1, opt_.workers); ++i) workers_.emplace_back([this] { worker(); });
+  for (int i = 0; i < std::max(1, opt_.workers); ++i) workers_.emplace_back([this] { name_thread("uda-supply"); worker(); });
   if (opt_.transport == "tcp")
     server_ = make_tcp_server(net_.data_port, net_.wqes_per_conn, opt_.bind_addr);
   else

@@ -6,6 +6,7 @@
 #include <poll.h>
 #include <sys/mman.h>
 #include <sys/resource.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/time.h>
@@ -28,6 +29,7 @@
 #include "uda/frame.h"
 #include "uda/log.h"
 #include "uda/transport.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 
@@ -370,7 +372,8 @@ MergeService::MergeService(const Options& o) : opt_(o) {
   gpu::set_pinned_shareable(true);
   set_tcp_local_bypass(true);  // hosted tasks fetch from this process's provider (if any) without a socket
   if (!opt_.path.empty()) listen_fd_ = frame::unix_listen(opt_.path, 256);
-  acceptor_ = std::thread([this] { accept_main(); });
+  wake_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  acceptor_ = std::thread([this] { name_thread("uda-svc-accept"); accept_main(); });
   UDA_LOG(kInfo, "merge service listening on %s (users: %s, max sessions %d)", opt_.path.c_str(), opt_.users.c_str(),
           opt_.max_sessions);
 }
@@ -382,7 +385,17 @@ MergeService::~MergeService() {
     sess_cv_.notify_all();
   }
   if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  if (wake_fd_ >= 0) {
+    const uint64_t one = 1;
+    (void)!::write(wake_fd_, &one, sizeof(one));
+  }
   if (acceptor_.joinable()) acceptor_.join();
+  {  // adopted after the acceptor's last pass
+    std::lock_guard<std::mutex> g(aq_mu_);
+    for (int fd : adopted_) ::close(fd);
+    adopted_.clear();
+  }
+  if (wake_fd_ >= 0) ::close(wake_fd_);
   if (listen_fd_ >= 0) close(listen_fd_);
   if (!opt_.path.empty() && opt_.path[0] != '@') ::unlink(opt_.path.c_str());
   std::map<uint64_t, std::thread> shakes;
@@ -438,6 +451,15 @@ std::string MergeService::stats_json() const {
 }
 
 void MergeService::adopt(int fd) {
+  {
+    std::lock_guard<std::mutex> g(aq_mu_);
+    adopted_.push_back(fd);
+  }
+  const uint64_t one = 1;
+  if (wake_fd_ >= 0) (void)!::write(wake_fd_, &one, sizeof(one));
+}
+
+void MergeService::start_handshake(int fd) {
   std::lock_guard<std::mutex> g(mu_);
   if (stop_) {
     ::close(fd);
@@ -445,6 +467,7 @@ void MergeService::adopt(int fd) {
   }
   const uint64_t id = next_shake_++;
   shakes_[id] = std::thread([this, fd, id] {
+    name_thread("uda-svc-shake");
     handshake(fd);
     std::lock_guard<std::mutex> g2(mu_);
     shakes_done_.insert(id);
@@ -453,9 +476,19 @@ void MergeService::adopt(int fd) {
 
 void MergeService::accept_main() {
   while (!stop_) {
-    pollfd pf{listen_fd_, POLLIN, 0};
-    // no listener (connections come by adopt()): the loop only reaps finished sessions and handshakes
-    const int pr = listen_fd_ >= 0 ? ::poll(&pf, 1, 200) : (::poll(nullptr, 0, 200), 0);
+    pollfd pf[2] = {{wake_fd_, POLLIN, 0}, {listen_fd_, POLLIN, 0}};
+    // the listener (if any) and adopt()'s wake-ups; the timeout paces the reaping of finished sessions
+    const int pr = ::poll(pf, listen_fd_ >= 0 ? 2 : 1, 200);
+    if (pr > 0 && (pf[0].revents & POLLIN)) {
+      uint64_t n;
+      (void)!::read(wake_fd_, &n, sizeof(n));
+    }
+    std::vector<int> adopted;
+    {
+      std::lock_guard<std::mutex> g(aq_mu_);
+      adopted.swap(adopted_);
+    }
+    for (int fd : adopted) start_handshake(fd);
     {  // reap finished sessions and handshakes
       // Taken out under mu_, joined and destroyed after it: the last reference to a session runs its
       // reduce task's teardown (pooled workspaces back, pinned rings, streams), ~5-10 ms each, and under
@@ -495,18 +528,12 @@ void MergeService::accept_main() {
       done_sessions.clear();
       for (auto& t : done_shakes) t.join();
     }
-    if (pr <= 0 || !(pf.revents & POLLIN)) continue;
+    if (pr <= 0 || listen_fd_ < 0 || !(pf[1].revents & POLLIN)) continue;
     const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) continue;
     // the HELLO is read on a thread of the connection's own: one slow or stalled client never delays
     // another task's admission or its data connection
-    std::lock_guard<std::mutex> g(mu_);
-    const uint64_t id = next_shake_++;
-    shakes_[id] = std::thread([this, fd, id] {
-      handshake(fd);
-      std::lock_guard<std::mutex> g2(mu_);
-      shakes_done_.insert(id);
-    });
+    start_handshake(fd);
   }
 }
 
@@ -606,8 +633,8 @@ void MergeService::handshake(int fd) {
       if (e == std::string::npos) break;
       b = e + 1;
     }
-    s->reader = std::thread([s] { s->read_loop(); });
-    s->runner = std::thread([s] { s->run(); });
+    s->reader = std::thread([s] { name_thread("uda-svc-read"); s->read_loop(); });
+    s->runner = std::thread([s] { name_thread("uda-svc-run"); s->run(); });
     closed_guard.pending = false;  // the session reports its own end
     live_.push_back(s);
     sess_cv_.notify_all();

@@ -84,7 +84,9 @@ class MergeService {
   MergeService& operator=(const MergeService&) = delete;
   const std::string& path() const { return opt_.path; }
   // A client connection accepted elsewhere (a router that passed its descriptor over SCM_RIGHTS): handled
-  // as if this service had accepted it. Takes ownership of fd.
+  // as if this service had accepted it. Takes ownership of fd. Queued for the acceptor thread, which
+  // starts its handshake: the caller (the node daemon's control channel) never creates a thread or
+  // waits for mu_, and with them for the process's address-space lock that thread creation takes.
   void adopt(int fd);
   int64_t sessions() const { return sessions_.load(); }
   int64_t refused() const { return refused_.load(); }
@@ -101,8 +103,12 @@ class MergeService {
  private:
   void accept_main();
   void handshake(int fd);  // on a thread per connection: credentials, HELLO, session start
+  void start_handshake(int fd);  // on the acceptor thread
   Options opt_;
   int listen_fd_ = -1;
+  int wake_fd_ = -1;  // eventfd: adopt() wakes the acceptor
+  std::mutex aq_mu_;
+  std::vector<int> adopted_;  // descriptors adopt() queued for the acceptor
   std::atomic<bool> stop_{false};
   std::thread acceptor_;
   std::mutex mu_;

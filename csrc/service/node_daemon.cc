@@ -30,10 +30,12 @@
 #include "uda/error.h"
 #include "uda/frame.h"
 #include "uda/log.h"
+#include "uda/stall_probe.h"
 #include "uda/start_trace.h"
 #include "uda/topology.h"
 #include "uda/transport.h"
 #include "uda/uda_bridge.h"
+#include "uda/thread_name.h"
 
 extern char** environ;
 
@@ -233,8 +235,33 @@ bool NodeDaemonClient::spawn() {
   const std::string fd_arg = std::to_string(child_fd);
   std::vector<char*> argv = {const_cast<char*>(opt_.exe.c_str()), const_cast<char*>("--daemon-fd"),
                              const_cast<char*>(fd_arg.c_str()), nullptr};
+  // The daemon starts a wave of hosted tasks at once (a dozen threads each); every thread stack mmap, every
+  // new malloc arena and each of its growth steps takes the address-space lock for writing, and in that
+  // convoy the control channel's own allocations waited 100-250 ms (UDA_STALL_PROBE). So the daemon keeps
+  // exited threads' stacks (1 GiB cache, virtual), uses at most 8 arenas made writable whole at creation
+  // (64 MiB top pad), never trims them, and serves blocks under 32 MiB from them rather than from mmap.
+  // UDA_DAEMON_TUNABLES replaces the set ("" for glibc's defaults).
+  const char* tun_env = std::getenv("UDA_DAEMON_TUNABLES");
+  const std::string tun = tun_env ? tun_env
+                                  : "glibc.pthread.stack_cache_size=1073741824:glibc.malloc.arena_max=8:"
+                                    "glibc.malloc.top_pad=67108864:glibc.malloc.trim_threshold=268435456:"
+                                    "glibc.malloc.mmap_threshold=33554432";
+  std::vector<std::string> env_store;
+  bool had_tunables = false;
+  for (char** e = environ; e && *e; ++e) {
+    std::string kv = *e;
+    if (kv.rfind("GLIBC_TUNABLES=", 0) == 0) {
+      had_tunables = true;
+      if (!tun.empty()) kv += ":" + tun;  // the later setting of a tunable wins
+    }
+    env_store.push_back(std::move(kv));
+  }
+  if (!had_tunables && !tun.empty()) env_store.push_back("GLIBC_TUNABLES=" + tun);
+  std::vector<char*> envp;
+  for (auto& kv : env_store) envp.push_back(const_cast<char*>(kv.c_str()));
+  envp.push_back(nullptr);
   pid_t pid = 0;
-  const int rc = ::posix_spawn(&pid, opt_.exe.c_str(), &fa, &attr, argv.data(), environ);
+  const int rc = ::posix_spawn(&pid, opt_.exe.c_str(), &fa, &attr, argv.data(), envp.data());
   posix_spawn_file_actions_destroy(&fa);
   posix_spawnattr_destroy(&attr);
   ::close(sv[1]);
@@ -577,10 +604,17 @@ struct Daemon {
     std::snprintf(pw, sizeof(pw), "\"prewarm\":{\"tasks\":%d,\"done\":%s,\"ms\":%.1f}", prewarm_tasks.load(),
                   prewarm_done.load() ? "true" : "false", (double)prewarm_us.load() / 1e3);
     ms = ms + "," + pw;
+    // the allocator settings the front end spawned this daemon with (glibc's view, after its parsing)
+    std::string tun = std::getenv("GLIBC_TUNABLES") ? std::getenv("GLIBC_TUNABLES") : "";
+    for (char& c : tun)
+      if (!std::isalnum((unsigned char)c) && !std::strchr("._=:", c)) c = '_';  // JSON-safe
+    ms += ",\"glibc_tunables\":\"" + tun + "\"";
     return s.size() <= 2 ? "{\"merge_service\":" + ms + "}" : s.substr(0, s.size() - 1) + ",\"merge_service\":" + ms + "}";
   }
 
   void read_loop() {
+    name_thread("uda-daemon-ctl");
+    stall_probe_watch();
     for (;;) {
       uint32_t t;
       std::string p;
@@ -807,6 +841,7 @@ int run_node_daemon(int ctl_fd) {
       d->prewarm_tasks = per * (int)devs.size();
       Daemon* dp = d.get();
       d->prewarm = std::thread([dp, devs, per, rb, kvb] {
+        name_thread("uda-prewarm");
         const auto t0 = std::chrono::steady_clock::now();
         for (int dv : devs) {
           try {
@@ -924,7 +959,7 @@ NodeDaemonSet::NodeDaemonSet(const Options& o, Host* host) : opt_(o) {
   if (!opt_.service_path.empty() && (n > 1 || o.per_gpu)) {
     try {
       listen_fd_ = frame::unix_listen(opt_.service_path, 256);
-      router_ = std::thread([this] { route_main(); });
+      router_ = std::thread([this] { name_thread("uda-router"); route_main(); });
       UDA_LOG(kInfo, "merge service %s: routing client connections over %d node daemon(s)",
               opt_.service_path.c_str(), n);
     } catch (const std::exception& e) {

@@ -27,6 +27,7 @@
 
 #include "uda/log.h"
 #include "uda/transport.h"
+#include "uda/thread_name.h"
 
 namespace uda {
 
@@ -135,7 +136,7 @@ class TcpServer : public ServerTransport {
       local_servers()[local_key_] = s;
     }
     running_ = true;
-    acceptor_ = std::thread([this] { accept_loop(); });
+    acceptor_ = std::thread([this] { name_thread("uda-tcp-accept"); accept_loop(); });
   }
 
   void stop() override {
@@ -551,7 +552,7 @@ class TcpClient : public ClientTransport {
     tune(fd);
     auto c = std::make_shared<Conn>();
     c->fd = fd;
-    c->reader = std::thread([c] { reader(c); });
+    c->reader = std::thread([c] { name_thread("uda-tcp-read"); reader(c); });
     return c;
   }
 

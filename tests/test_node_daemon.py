@@ -160,6 +160,23 @@ def test_daemon_does_not_inherit_front_end_descriptors(tmp_path):
             fe.close()
 
 
+def test_daemon_starts_with_its_allocator_tunables(tmp_path, monkeypatch):
+    """The daemon is spawned with glibc tunables that keep a wave of task starts from queueing on the
+    address-space lock (cached thread stacks, few arenas made writable whole); a GLIBC_TUNABLES of the
+    front end's environment is kept, with the daemon's settings after it."""
+    mof_dir, _, _ = _job(tmp_path, "job_tun")
+    monkeypatch.setenv("GLIBC_TUNABLES", "glibc.malloc.tcache_count=5")
+    fe = FrontEnd(mof_dir, _port(), {"mapred.uda.daemon": "1"})
+    try:
+        # glibc's own view in the daemon (/proc/<pid>/environ shows the string as glibc's parse cut it)
+        tun = fe.stats()["hbm_store"]["glibc_tunables"]
+        assert tun.startswith("glibc.malloc.tcache_count=5:"), tun
+        for want in ("glibc.pthread.stack_cache_size=1073741824", "glibc.malloc.arena_max=8", "glibc.malloc.top_pad=67108864"):
+            assert want in tun, tun
+    finally:
+        fe.close()
+
+
 def _daemon_front(tmp_path, job, conf=None, **kw):
     mof_dir, data, ids = _job(tmp_path, job, **kw)
     port = _port()
