@@ -3,21 +3,24 @@
 // been out of its idle wait (asleep in recvmsg) for 6 ms, every thread of the process that is running,
 // in uninterruptible sleep, ran >= 1 ms since the last sample, or is the watched one, is printed each 5 ms
 // (name, state, CPU time and minor faults since the last sample, kernel wait channel, syscall and first
-// arguments) until the watched thread is idle again. Off: one getenv, once.
+// arguments) until the watched thread is idle again. A sampler wake-up more than 20 ms late and each
+// change of the cgroup's throttle count are printed too. The sampler allocates nothing once started (raw
+// open/read/getdents64/write on stack buffers): a thread stuck on a malloc arena's lock or on the
+// address-space lock never holds it up. Off: one getenv, once.
 #pragma once
-#include <dirent.h>
+#include <fcntl.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
 #include <thread>
-#include <unordered_map>
+#include <vector>
 
 #include "uda/thread_name.h"
 
@@ -28,33 +31,51 @@ inline std::atomic<int>& watched() {
   static std::atomic<int> t{0};
   return t;
 }
-inline std::string read_small(const std::string& path) {
-  FILE* f = std::fopen(path.c_str(), "r");
-  if (!f) return "";
-  char buf[256];
-  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
-  std::fclose(f);
-  buf[n] = 0;
-  std::string s(buf);
-  while (!s.empty() && (s.back() == '\n' || s.back() == ' ')) s.pop_back();
-  return s;
+// The file's first `cap - 1` bytes, trailing newlines and blanks cut; "" if unreadable.
+inline const char* read_small(const char* path, char* buf, size_t cap) {
+  buf[0] = 0;
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return buf;
+  const ssize_t n = ::read(fd, buf, cap - 1);
+  ::close(fd);
+  size_t k = n > 0 ? (size_t)n : 0;
+  while (k > 0 && (buf[k - 1] == '\n' || buf[k - 1] == ' ')) --k;
+  buf[k] = 0;
+  return buf;
+}
+inline const char* task_file(int tid, const char* leaf, char* buf, size_t cap) {
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/self/task/%d/%s", tid, leaf);
+  return read_small(path, buf, cap);
 }
 inline char thread_state(int tid) {  // the field after "(comm)" in /proc/self/task/<tid>/stat
-  const std::string s = read_small("/proc/self/task/" + std::to_string(tid) + "/stat");
-  const size_t p = s.rfind(')');
-  return p != std::string::npos && p + 2 < s.size() ? s[p + 2] : '?';
+  char s[512];
+  task_file(tid, "stat", s, sizeof(s));
+  const char* p = std::strrchr(s, ')');
+  return p && p[1] == ' ' && p[2] ? p[2] : '?';
 }
-inline std::string syscall_head(int tid) {  // "<nr> <arg0> <arg1>" or "running"
-  std::string s = read_small("/proc/self/task/" + std::to_string(tid) + "/syscall");
-  size_t at = 0;
-  for (int f = 0; f < 3 && at != std::string::npos; ++f) at = s.find(' ', at + 1);
-  return at == std::string::npos ? s : s.substr(0, at);
+inline const char* syscall_head(int tid, char* buf, size_t cap) {  // "<nr> <arg0> <arg1>" or "running"
+  task_file(tid, "syscall", buf, cap);
+  char* q = buf;
+  for (int f = 0; f < 3 && q; ++f) q = std::strchr(q + 1, ' ');
+  if (q) *q = 0;
+  return buf;
 }
 inline double now_ms() {
   timespec ts{};
   clock_gettime(CLOCK_BOOTTIME, &ts);
   return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec / 1e6;
 }
+template <typename... A>
+inline void say(const char* fmt, A... a) {
+  char line[640];
+  const int n = std::snprintf(line, sizeof(line), fmt, a...);
+  if (n > 0) (void)!::write(2, line, (size_t)std::min<int>(n, (int)sizeof(line) - 1));
+}
+struct Prev {  // per thread: CPU time and minor faults at the last sweep (open addressing by tid)
+  int tid;
+  unsigned long long run_ns, minflt;
+};
 }  // namespace stall_probe_detail
 
 // The calling thread becomes the watched one; the first call starts the sampler (when enabled).
@@ -69,54 +90,83 @@ inline void stall_probe_watch() {
   if (watched().exchange(self) != 0) return;
   const double dur_ms = secs * 1e3;
   std::thread([dur_ms] {
-    const double end = now_ms() + dur_ms;
-    double busy_since = -1, last_dump = -1;
-    int lines = 0;
-    std::unordered_map<int, std::pair<unsigned long long, unsigned long long>> prev;  // tid -> run ns, faults
     name_thread("uda-stall-probe");
+    constexpr size_t kSlots = 1 << 14;
+    std::vector<Prev> prev(kSlots, Prev{0, 0, 0});  // the sampler's only allocation
+    const double end = now_ms() + dur_ms;
+    double busy_since = -1, last_dump = -1, last_wake = now_ms();
+    int lines = 0;
     const int pid = (int)getpid();
+    char thr0[128] = "", cs[512], sc[128];
     while (now_ms() < end && lines < 20000) {
       std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      const double tw = now_ms();
+      {  // this sampler itself kept from running, and cgroup CPU throttling
+        read_small("/sys/fs/cgroup/cpu.stat", cs, sizeof(cs));
+        char thr[128] = "";
+        if (const char* a = std::strstr(cs, "nr_throttled")) {
+          size_t k = 0;
+          while (a[k] && a[k] != '\n' && k + 1 < sizeof(thr)) thr[k] = a[k], ++k;
+          thr[k] = 0;
+        }
+        if (tw - last_wake > 20 || std::strcmp(thr, thr0) != 0) {
+          say("[stall-probe] pid %d %.3f sampler gap %.1f ms, %s\n", pid, tw, tw - last_wake, thr);
+          ++lines;
+        }
+        std::memcpy(thr0, thr, sizeof(thr0));
+        last_wake = tw;
+      }
       const int w = watched().load();
-      const std::string sc = syscall_head(w);
+      syscall_head(w, sc, sizeof(sc));
       // waiting for the next message: in recvmsg, asleep (not blocked in it on a lock or a fault: D)
-      const bool idle = sc.rfind("47 ", 0) == 0 && thread_state(w) == 'S';
+      const bool idle = std::strncmp(sc, "47 ", 3) == 0 && thread_state(w) == 'S';
       const double t = now_ms();
       if (idle) {
-        if (busy_since >= 0 && t - busy_since >= 6)
-          std::fprintf(stderr, "[stall-probe] pid %d %.3f end busy %.1f ms\n", pid, t, t - busy_since);
+        if (busy_since >= 0 && t - busy_since >= 6) say("[stall-probe] pid %d %.3f end busy %.1f ms\n", pid, t, t - busy_since);
         busy_since = -1;
         continue;
       }
       auto sweep = [&](bool print) {  // print: the threads that are running, blocked, or ran >= 1 ms since
-        DIR* d = opendir("/proc/self/task");
-        if (!d) return;
-        while (dirent* e = readdir(d)) {
-          if (e->d_name[0] == '.') continue;
-          const int tid = std::atoi(e->d_name);
-          const std::string dir = "/proc/self/task/" + std::to_string(tid) + "/";
-          const std::string stat = read_small(dir + "stat");
-          const size_t rp = stat.rfind(')');
-          if (rp == std::string::npos || rp + 2 >= stat.size()) continue;
-          const char st = stat[rp + 2];
-          unsigned long long minflt = 0;  // the 8th field after the state
-          {
-            const char* q = stat.c_str() + rp + 2;
-            for (int f = 0; f < 7 && q; ++f) q = std::strchr(q + 1, ' ');
-            if (q) minflt = std::strtoull(q + 1, nullptr, 10);
+        const int dfd = ::open("/proc/self/task", O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+        if (dfd < 0) return;
+        alignas(8) char dents[8192];
+        for (;;) {
+          const long n = syscall(SYS_getdents64, dfd, dents, sizeof(dents));
+          if (n <= 0) break;
+          for (long off = 0; off < n;) {
+            const unsigned short reclen = *reinterpret_cast<const unsigned short*>(dents + off + 16);
+            const char* name = dents + off + 19;  // d_ino 8, d_off 8, d_reclen 2, d_type 1
+            off += reclen;
+            if (name[0] < '0' || name[0] > '9') continue;
+            const int tid = std::atoi(name);
+            char stat[512], sched[128], comm[32], wchan[64], tsc[128];
+            task_file(tid, "stat", stat, sizeof(stat));
+            const char* rp = std::strrchr(stat, ')');
+            if (!rp || rp[1] != ' ' || !rp[2]) continue;
+            const char st = rp[2];
+            unsigned long long minflt = 0;  // the 8th field after the state
+            {
+              const char* q = rp + 2;
+              for (int f = 0; f < 7 && q; ++f) q = std::strchr(q + 1, ' ');
+              if (q) minflt = std::strtoull(q + 1, nullptr, 10);
+            }
+            const unsigned long long run_ns = std::strtoull(task_file(tid, "schedstat", sched, sizeof(sched)), nullptr, 10);
+            size_t h = (size_t)tid * 2654435761u % kSlots, probes = 0;
+            while (prev[h].tid != 0 && prev[h].tid != tid && ++probes < kSlots) h = (h + 1) % kSlots;
+            if (probes >= kSlots) prev[h].tid = 0;  // full: reuse a slot
+            Prev& pv = prev[h];
+            const bool seen = pv.tid == tid;
+            const double run_ms = seen ? (double)(run_ns - pv.run_ns) / 1e6 : 0.0;
+            const unsigned long long flt = seen ? minflt - pv.minflt : 0;
+            pv = Prev{tid, run_ns, minflt};
+            if (!print || (tid != w && st != 'R' && st != 'D' && run_ms < 1.0)) continue;
+            say("[stall-probe] pid %d %.3f busy %.1f tid %d%s %s %c ran %.1f ms faults %llu wchan %s sys %s\n", pid, t,
+                t - busy_since, tid, tid == w ? "*" : "", task_file(tid, "comm", comm, sizeof(comm)), st, run_ms, flt,
+                task_file(tid, "wchan", wchan, sizeof(wchan)), syscall_head(tid, tsc, sizeof(tsc)));
+            ++lines;
           }
-          const unsigned long long run_ns = std::strtoull(read_small(dir + "schedstat").c_str(), nullptr, 10);
-          auto& pv = prev[tid];
-          const double run_ms = pv.first ? (double)(run_ns - pv.first) / 1e6 : 0.0;
-          const unsigned long long flt = pv.first ? minflt - pv.second : 0;
-          pv = {run_ns, minflt};
-          if (!print || (tid != w && st != 'R' && st != 'D' && run_ms < 1.0)) continue;
-          std::fprintf(stderr, "[stall-probe] pid %d %.3f busy %.1f tid %d%s %s %c ran %.1f ms faults %llu wchan %s sys %s\n", pid, t,
-                       t - busy_since, tid, tid == w ? "*" : "", read_small(dir + "comm").c_str(), st, run_ms, flt,
-                       read_small(dir + "wchan").c_str(), syscall_head(tid).c_str());
-          ++lines;
         }
-        closedir(d);
+        ::close(dfd);
       };
       if (busy_since < 0) {
         busy_since = t;
@@ -124,15 +174,6 @@ inline void stall_probe_watch() {
       }
       if (t - busy_since < 6 || (last_dump >= 0 && t - last_dump < 5)) continue;
       last_dump = t;
-      {  // CPU-quota throttling of the process's cgroup (all threads stop until the period ends)
-        std::string cs = read_small("/sys/fs/cgroup/cpu.stat");
-        const size_t a = cs.find("nr_throttled");
-        if (a != std::string::npos) {
-          cs = cs.substr(a);
-          for (char& c : cs) c = c == '\n' ? ' ' : c;
-          std::fprintf(stderr, "[stall-probe] pid %d %.3f busy %.1f cgroup %s\n", pid, t, t - busy_since, cs.c_str());
-        }
-      }
       sweep(true);
     }
   }).detach();
