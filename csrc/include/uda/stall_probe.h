@@ -98,6 +98,7 @@ inline void stall_probe_watch() {
     int lines = 0;
     const int pid = (int)getpid();
     char thr0[128] = "", cs[512], sc[128];
+    unsigned long long on0 = 0, wait0 = 0;
     while (now_ms() < end && lines < 20000) {
       std::this_thread::sleep_for(std::chrono::milliseconds(2));
       const double tw = now_ms();
@@ -109,10 +110,19 @@ inline void stall_probe_watch() {
           while (a[k] && a[k] != '\n' && k + 1 < sizeof(thr)) thr[k] = a[k], ++k;
           thr[k] = 0;
         }
+        // the sampler's own CPU time and run-queue wait (schedstat): a late wake-up spent runnable but
+        // off the CPU (starved) shows as run-queue wait; stopped or blocked in the kernel shows as neither
+        char ss[128];
+        read_small("/proc/thread-self/schedstat", ss, sizeof(ss));
+        char* e1 = nullptr;
+        const unsigned long long on_ns = std::strtoull(ss, &e1, 10), wait_ns = std::strtoull(e1, nullptr, 10);
         if (tw - last_wake > 20 || std::strcmp(thr, thr0) != 0) {
-          say("[stall-probe] pid %d %.3f sampler gap %.1f ms, %s\n", pid, tw, tw - last_wake, thr);
+          say("[stall-probe] pid %d %.3f sampler gap %.1f ms (on cpu %.1f ms, run-queue wait %.1f ms), %s\n", pid, tw,
+              tw - last_wake, (double)(on_ns - on0) / 1e6, (double)(wait_ns - wait0) / 1e6, thr);
           ++lines;
         }
+        on0 = on_ns;
+        wait0 = wait_ns;
         std::memcpy(thr0, thr, sizeof(thr0));
         last_wake = tw;
       }
