@@ -41,6 +41,7 @@
 #include "uda/cmd.h"
 #include "uda/ifile.h"
 #include "uda/uda_bridge.h"
+#include "uda/fd_table.h"
 
 namespace {
 std::string js(const std::string& s) {
@@ -169,9 +170,11 @@ int main(int argc, char** argv) {
   if (argc == 3 && std::string(argv[1]) == "--daemon-fd") {
     const int ctl = std::atoi(argv[2]);
     close_inherited(ctl);
+    uda::pregrow_fd_table();
     uda::install_crash_reporter("uda node daemon");
     return uda::run_node_daemon(ctl);
   }
+  uda::pregrow_fd_table();  // the front end: a socket per fetch connection, routed client connections
   uda::install_crash_reporter("uda_mof_supplier");
   uda::gpu::ApiBenchConfig c;
   c.transport = "tcp";

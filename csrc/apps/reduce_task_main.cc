@@ -33,6 +33,7 @@
 #include "j2c_sink.h"
 #include "uda/node_registry.h"
 #include "uda/uda_bridge.h"
+#include "uda/fd_table.h"
 
 namespace {
 
@@ -94,6 +95,7 @@ std::string json_escape(const std::string& s) {
 
 int main(int argc, char** argv) {
   const double t_main = boot_ms();
+  uda::pregrow_fd_table(1 << 14);  // delivery rings (memfds), fetch connections
   uda::install_crash_reporter("uda_reduce_task");
   const double t_exec = (double)uda::process_start_ticks((int)getpid()) * 1000.0 / (double)sysconf(_SC_CLK_TCK);
   Host host;

@@ -160,6 +160,25 @@ def test_daemon_does_not_inherit_front_end_descriptors(tmp_path):
             fe.close()
 
 
+def test_daemon_and_front_end_descriptor_tables_are_grown_up_front(tmp_path):
+    """A multi-threaded process's descriptor table grows by doubling, each doubling waiting for an RCU grace
+    period while every thread that opens a descriptor waits with it (the daemon's first-wave freeze,
+    profiles/r6/r7_first_wave_stall.md): the daemon and the front end grow theirs before their threads
+    start (FDSize in /proc/<pid>/status), up to the descriptor limit."""
+    import resource
+
+    mof_dir, _, _ = _job(tmp_path, "job_fdsize")
+    fe = FrontEnd(mof_dir, _port(), {"mapred.uda.daemon": "1"})
+    try:
+        want = min(resource.getrlimit(resource.RLIMIT_NOFILE)[1], 1 << 17)
+        for pid in (fe.p.pid, fe.info["provider"]["hbm_store"]["daemon"]["pid"]):
+            with open(f"/proc/{pid}/status") as f:
+                size = int(next(l for l in f if l.startswith("FDSize:")).split()[1])
+            assert size >= want, (pid, size, want)
+    finally:
+        fe.close()
+
+
 def test_daemon_starts_with_its_allocator_tunables(tmp_path, monkeypatch):
     """The daemon is spawned with glibc tunables that keep a wave of task starts from queueing on the
     address-space lock (cached thread stacks, few arenas made writable whole); a GLIBC_TUNABLES of the
