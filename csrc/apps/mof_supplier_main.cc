@@ -30,8 +30,10 @@
 #include <iostream>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "uda/log.h"
@@ -165,12 +167,41 @@ static void close_inherited(int keep) {
   for (int fd : fds) ::close(fd);
 }
 
+// The daemon's first wave starts a dozen threads per hosted task; each new thread's stack is an mmap (and
+// its exit an madvise) on the address-space lock, where the wave's late tasks queued for up to 90 ms
+// (profiles/r6/r7_first_wave_stall.md). `n` threads started together and joined at once leave their
+// stacks in glibc's stack cache (sized by the daemon's glibc.pthread.stack_cache_size tunable), from
+// which the first wave's threads then take theirs without an mmap.
+static void prewarm_thread_stacks(int n) {
+  std::mutex mu;
+  std::condition_variable cv;
+  int started = 0;
+  bool go = false;
+  std::vector<std::thread> ts;
+  for (int i = 0; i < n; ++i)
+    ts.emplace_back([&] {
+      std::unique_lock<std::mutex> lk(mu);
+      ++started;
+      cv.notify_all();
+      cv.wait(lk, [&] { return go; });
+    });
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return started == n; });  // all alive at once: n distinct stacks
+    go = true;
+    cv.notify_all();
+  }
+  for (auto& t : ts) t.join();
+}
+
 int main(int argc, char** argv) {
   // the node daemon a provider front end starts (node_daemon.h): its control socket is descriptor N
   if (argc == 3 && std::string(argv[1]) == "--daemon-fd") {
     const int ctl = std::atoi(argv[2]);
     close_inherited(ctl);
     uda::pregrow_fd_table();
+    if (const char* e = std::getenv("UDA_DAEMON_STACKS"); !e || std::atoi(e) > 0)
+      prewarm_thread_stacks(e ? std::atoi(e) : 96);
     uda::install_crash_reporter("uda node daemon");
     return uda::run_node_daemon(ctl);
   }
