@@ -17,6 +17,7 @@
 #include "uda/cmd.h"
 #include "uda/host.h"
 #include "uda/log.h"
+#include "uda/fd_table.h"
 
 #define UDA_VERSION_STRING "uda_amd-0.1.0 (MI355X-native; reference API 3.4.1)"
 
@@ -74,6 +75,9 @@ uda_handle* uda_start(int is_net_merger, int argc, const char* const* argv, int 
     UDA_LOG(uda::kError, "bad options: %s", err.c_str());
     return nullptr;
   }
+  // a JVM host: grow its descriptor table once now rather than by doublings under load, each of which
+  // stalls every thread that opens a descriptor for an RCU grace period (uda/fd_table.h)
+  uda::pregrow_fd_table(h->is_merger ? 1 << 14 : 1 << 17);
   if (log_to_file) {
     uda::log_open_file(h->opt.log_dir, h->is_merger ? "NetMerger" : "MOFSupplier");
   } else if (cb && cb->log) {
